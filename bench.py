@@ -1,0 +1,162 @@
+#!/usr/bin/env python3
+"""Headline benchmark: netflow suspicious-connects, 20-topic collapsed-Gibbs LDA on MI355X.
+
+Metric (BASELINE.json): "netflow records scored/sec (whole node) + Gibbs iters/sec, 20-topic LDA".
+One timed *step* = one full Gibbs sweep over every token of the day (2 tokens per flow) including
+the per-sweep RCCL all-reduce of Δn_wk and the q-table refresh. ``value`` = whole-node netflow
+records swept per second (= total flows × sweeps/s). Also reported: Gibbs iters/s, tokens/s and
+the post-LDA scoring pass (records scored/s: θ·φ score of every flow + top-N selection).
+
+Weak scaling: every GPU owns ``--flows-per-gpu`` synthetic flows (default 12.5M, so N=8 is the
+BASELINE config "Netflow 100M flows, 20 topics, DP=8"). Synthetic data with random-init topic
+priors (oni355.synth.flow), random-init LDA. Launch for N>1:
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+      --master-port P bench.py --gpus N --steps K --warmup W
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--flows-per-gpu", type=int, default=12_500_000)
+    ap.add_argument("--topics", type=int, default=20)
+    ap.add_argument("--chunk-len", type=int, default=256)
+    ap.add_argument("--maxresults", type=int, default=3000)
+    ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--device", default="cuda")
+    ap.add_argument("--no-graph", action="store_true")
+    a = ap.parse_args(argv)
+
+    import torch
+
+    from oni355.parallel import comm as pc
+    from oni355.pipeline import common, flow
+    from oni355.synth.flow import generate_flows
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        if a.gpus > 1:
+            print(f"bench: --gpus {a.gpus} but WORLD_SIZE={world}; launch with torch.distributed.run", file=sys.stderr)
+            return 2
+    if a.no_graph:
+        os.environ["ONI_NO_GRAPH"] = "1"
+    comm = pc.init_from_env(a.device)
+    dev = comm.device
+    rank, world = comm.rank, comm.world
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    t_setup = time.perf_counter()
+    # hosts scale with the node-wide day so N=8 is one 100M-flow day split over 8 ranks
+    n_total = a.flows_per_gpu * world
+    day = generate_flows(a.flows_per_gpu, seed=a.seed, rank=rank, n_hosts=max(64, n_total // 25))
+    d = flow.to_device(day.cols, dev)
+    cuts = flow.compute_cuts(d, comm)
+    sw, dw = flow.wordify(d, cuts)
+    doc_keys = torch.cat([common.u32_to_i64(d["sip"]), common.u32_to_i64(d["dip"])])
+    word_keys = torch.cat([common.u32_to_i64(sw), common.u32_to_i64(dw)])
+    vocab = common.global_vocab(word_keys, comm)
+    run = common.build_and_train(doc_keys, word_keys, None, vocab, a.topics, None, 0.01, 0x0D15EA5E, 0,
+                                 a.chunk_len, comm, train=False)
+    model = run.model
+    model.initialize()
+    sync()
+    setup_s = time.perf_counter() - t_setup
+
+    # ---- warmup + timed sweeps -----------------------------------------------------------------
+    model.sweep(a.warmup)
+    sync()
+    comm.barrier()
+    sync()
+    t0 = time.perf_counter()
+    model.sweep(a.steps)
+    sync()
+    comm.barrier()
+    sync()
+    dt = time.perf_counter() - t0
+    dt = comm.allreduce_scalar(dt, "max")
+
+    # ---- post-LDA scoring pass (records scored/s), timed separately --------------------------
+    dkeys, theta = common.gather_theta(run, comm)
+    phi = model.phi()
+    sdoc = common.lookup(dkeys, common.u32_to_i64(d["sip"]))
+    ddoc = common.lookup(dkeys, common.u32_to_i64(d["dip"]))
+    swid = common.lookup(vocab, common.u32_to_i64(sw))
+    dwid = common.lookup(vocab, common.u32_to_i64(dw))
+    from oni355 import ops
+
+    def score_once():
+        hist = torch.zeros(2048, dtype=torch.int32, device=dev)
+        sc, _, _ = ops.score(theta, phi, sdoc, swid, ddoc, dwid, tol=1.0, hist=hist)
+        return common.top_n(sc, 1.0, a.maxresults, comm, rank * a.flows_per_gpu, hist=hist)
+
+    score_once()
+    sync()
+    comm.barrier()
+    reps = 5
+    t1 = time.perf_counter()
+    for _ in range(reps):
+        rows, scs = score_once()
+    sync()
+    comm.barrier()
+    score_dt = comm.allreduce_scalar((time.perf_counter() - t1) / reps, "max")
+    ll = model.log_likelihood()
+
+    tokens_local = run.corpus.T
+    tokens = int(comm.allreduce_scalar(tokens_local, "sum"))
+    ms = dt / a.steps * 1e3
+    value = n_total * a.steps / dt
+    planted = day.anomaly_rows + rank * a.flows_per_gpu
+    hits = np.isin(planted, rows.cpu().numpy()[: a.maxresults])
+    hit_frac = comm.allreduce_scalar(float(hits.sum()), "sum") / max(comm.allreduce_scalar(float(planted.size), "sum"), 1)
+    out = {
+        "metric": "netflow records scored/sec (whole node) + Gibbs iters/sec, 20-topic LDA",
+        "value": round(value, 1),
+        "unit": "records/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic netflow (oni355.synth.flow: random-init topic priors, Zipf hosts, planted anomalies)",
+        "config": {"model": "oni-suspicious-connects-flow-lda", "topics": a.topics, "global_batch": n_total,
+                   "flows_per_gpu": a.flows_per_gpu, "seq_len": 2, "parallelism": f"dp{world}",
+                   "baseline_config": "Netflow 100M flows, 20 topics, DP=8 (N=8); weak-scaled 12.5M flows/GPU"},
+        "gibbs_iters_per_sec": round(a.steps / dt, 3),
+        "tokens_per_sec": round(tokens * a.steps / dt, 1),
+        "tokens": tokens,
+        "vocab": int(vocab.numel()),
+        "docs_local": run.corpus.D,
+        "score_records_per_sec": round(n_total / score_dt, 1),
+        "score_ms": round(score_dt * 1e3, 3),
+        "loglik": ll,
+        "planted_anomaly_recall_topN": round(hit_frac, 4),
+        "setup_s": round(setup_s, 2),
+        "allreduce_s_per_sweep": (model.timings["allreduce_s"] / max(model.timings["allreduce_calls"], 1)),
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    pc.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,308 @@
+// K10/K11/K12 -- collapsed-Gibbs LDA on CDNA4: init, sweep, delta-apply (+ q-table refresh).
+//
+// Replaces oni-lda-c's variational-EM `lda est` E-step/M-step loop (lda-estimate.c run_em /
+// doc_e_step, lda-inference.c, lda-model.c lda_mle; SURVEY.md §3.2, [U-H]) with collapsed Gibbs
+// sampling, as the north star requires (BASELINE.json).
+//
+// Execution model (MI355X-first, not a translation of anything):
+//  * Documents (IPs) are owned by sampler "units" of G lanes. A unit walks one chunk (≤ L tokens
+//    of one doc) sequentially, holding the doc's topic counts n_dk IN REGISTERS (KP per lane,
+//    KS = G*KP padded topics), so the doc side is exact Gibbs within a chunk.
+//  * The word side samples against the sweep-start table q[w,k] = (n_wk+β)/(n_k+Vβ)
+//    (AD-LDA staleness, one snapshot per sweep). Topic moves are accumulated as int32 deltas
+//    (dnwk, dnk); in data-parallel runs that buffer is what RCCL all-reduces over xGMI.
+//  * A wave = one SELL slice of S = 64/G chunks; tokens are step-major so per-step word/topic
+//    loads are coalesced. The q row is re-used while consecutive tokens share a word (tokens of
+//    one (doc, word) pair are adjacent).
+//  * G = 1 for K ≤ 32 (one lane owns all topics: no cross-lane traffic at all); G ∈ {4, 8, 16}
+//    for K = 50/100 with a DPP-free __shfl_up scan across the unit.
+//  * Draws are Philox4x32-10 keyed by (seed) with counter (pos/4, doc key, sweep, stream): the
+//    chain is a pure function of the data + seed — bitwise identical for any GPU count, shard
+//    plan, chunk packing or resume point (tested against the NumPy oracle, oni355/ref/spec.py).
+//  * Long documents span several chunks. Those chunks start from the sweep-start row of ndk_src
+//    and add their deltas into ndk_dst (pre-copied row), with integer atomics: still order-free.
+#include "oni_common.h"
+
+struct OniGibbs {
+  const uint32_t* tok_word;    // SELL [Σ slice_len*S]
+  uint8_t* tok_z;              // SELL
+  const int64_t* slice_off;    // [n_slices]
+  const int32_t* slice_len;    // [n_slices]
+  const int32_t* chunk_doc;    // [n_slices*S] local doc row, -1 = padding chunk
+  const int32_t* chunk_pos0;   // position of the chunk's first token inside its doc
+  const uint32_t* chunk_key;   // doc key (RNG stream id; global, shard-independent)
+  const uint8_t* chunk_multi;  // 1 if the doc is split over several chunks
+  const int32_t* ndk_src;      // [D][KS] sweep-start doc-topic counts
+  int32_t* ndk_dst;            // [D][KS] output doc-topic counts
+  const float* q;              // [V][KS] sweep-start word factor
+  int32_t* dnwk;               // [V][KS] word-topic delta (init: the n_wk table itself)
+  int32_t* dnk;                // [KS]    topic-total delta (init: n_k itself)
+  const uint32_t* sweep_ctr;   // device scalar: current sweep number (≥ 1), graph-replay safe
+  int64_t n_slices;
+  int32_t K;
+  int32_t KS;
+  float alpha;
+  uint32_t seed0, seed1;
+};
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kWavesPerBlock = kBlock / oni::kWave;
+
+template <int KP>
+__device__ __forceinline__ void load_row_i(const int32_t* __restrict__ p, int32_t (&v)[KP]) {
+#pragma unroll
+  for (int j = 0; j < KP; j += 4) {
+    const int4 t = *reinterpret_cast<const int4*>(p + j);
+    v[j] = t.x; v[j + 1] = t.y; v[j + 2] = t.z; v[j + 3] = t.w;
+  }
+}
+template <int KP>
+__device__ __forceinline__ void load_row_f(const float* __restrict__ p, float (&v)[KP]) {
+#pragma unroll
+  for (int j = 0; j < KP; j += 4) {
+    const float4 t = *reinterpret_cast<const float4*>(p + j);
+    v[j] = t.x; v[j + 1] = t.y; v[j + 2] = t.z; v[j + 3] = t.w;
+  }
+}
+
+template <int G, int KP, bool INIT>
+__global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
+  constexpr int S = oni::kWave / G;
+  constexpr int KS = G * KP;
+  __shared__ int32_t red[kWavesPerBlock][KS];
+
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int c = lane / G;
+  const int g = lane % G;
+  const int64_t slice = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  const bool valid = slice < a.n_slices;
+  const int64_t chunk = slice * S + c;
+  const int doc = valid ? a.chunk_doc[chunk] : -1;
+  const bool live = doc >= 0;
+  const int kbase = g * KP;
+
+  int32_t n[KP];
+#pragma unroll
+  for (int j = 0; j < KP; ++j) n[j] = 0;
+  if (!INIT && live) load_row_i<KP>(a.ndk_src + (int64_t)doc * KS + kbase, n);
+
+  const int len = valid ? a.slice_len[slice] : 0;
+  const int64_t off = valid ? a.slice_off[slice] : 0;
+  const uint32_t key = live ? a.chunk_key[chunk] : 0u;
+  const uint32_t pos0 = live ? (uint32_t)a.chunk_pos0[chunk] : 0u;
+  const uint32_t sweep = INIT ? 0u : *a.sweep_ctr;
+  const uint32_t stream = INIT ? 0u : 1u;
+
+  oni::U4 r{0, 0, 0, 0};
+  uint32_t wprev = oni::kPadWord;
+  float qv[KP];
+#pragma unroll
+  for (int j = 0; j < KP; ++j) qv[j] = 0.f;
+
+  for (int s = 0; s < len; ++s) {
+    const int64_t idx = off + (int64_t)s * S + c;
+    const uint32_t w = a.tok_word[idx];
+    if (w == oni::kPadWord) continue;  // uniform across the G lanes of a unit
+    const uint32_t pos = pos0 + (uint32_t)s;
+    if (s == 0 || (pos & 3u) == 0u) r = oni::philox10(oni::U4{pos >> 2, key, sweep, stream}, a.seed0, a.seed1);
+    const uint32_t rr = oni::pick4(r, pos & 3u);
+    if constexpr (INIT) {
+      const int z = (int)__umulhi(rr, (uint32_t)a.K);
+#pragma unroll
+      for (int j = 0; j < KP; ++j) n[j] += (kbase + j == z);
+      if (g == 0) {
+        a.tok_z[idx] = (uint8_t)z;
+        atomicAdd(&a.dnwk[(int64_t)w * KS + z], 1);
+      }
+    } else {
+      const int zo = a.tok_z[idx];
+#pragma unroll
+      for (int j = 0; j < KP; ++j) n[j] -= (kbase + j == zo);
+      if (w != wprev) {
+        load_row_f<KP>(a.q + (int64_t)w * KS + kbase, qv);
+        wprev = w;
+      }
+      float loc[KP];
+      float run = 0.f;
+#pragma unroll
+      for (int j = 0; j < KP; ++j) {
+        run = run + ((float)n[j] + a.alpha) * qv[j];
+        loc[j] = run;
+      }
+      float excl = 0.f, total = run;
+      if constexpr (G > 1) {
+        float incl = run;
+#pragma unroll
+        for (int d = 1; d < G; d <<= 1) {
+          const float y = __shfl_up(incl, d, G);
+          if (g >= d) incl = incl + y;
+        }
+        excl = __shfl_up(incl, 1, G);
+        if (g == 0) excl = 0.f;
+        total = __shfl(incl, G - 1, G);
+      }
+      const float thr = oni::u01(rr) * total;
+      int cnt = 0;
+#pragma unroll
+      for (int j = 0; j < KP; ++j) cnt += ((G > 1 ? excl + loc[j] : loc[j]) <= thr);
+      if constexpr (G > 1) {
+#pragma unroll
+        for (int d = 1; d < G; d <<= 1) cnt += __shfl_xor(cnt, d, G);
+      }
+      const int zn = cnt < a.K - 1 ? cnt : a.K - 1;
+#pragma unroll
+      for (int j = 0; j < KP; ++j) n[j] += (kbase + j == zn);
+      if (zn != zo && g == 0) {
+        a.tok_z[idx] = (uint8_t)zn;
+        atomicAdd(&a.dnwk[(int64_t)w * KS + zo], -1);
+        atomicAdd(&a.dnwk[(int64_t)w * KS + zn], 1);
+      }
+    }
+  }
+
+  // ---- epilogue: doc rows + per-topic totals -------------------------------------------------
+  int32_t d[KP];
+#pragma unroll
+  for (int j = 0; j < KP; ++j) d[j] = 0;
+  if (live) {
+    int32_t* dst = a.ndk_dst + (int64_t)doc * KS + kbase;
+    if (INIT) {
+#pragma unroll
+      for (int j = 0; j < KP; ++j) d[j] = n[j];
+    } else {
+      int32_t n0[KP];
+      load_row_i<KP>(a.ndk_src + (int64_t)doc * KS + kbase, n0);
+#pragma unroll
+      for (int j = 0; j < KP; ++j) d[j] = n[j] - n0[j];
+    }
+    if (a.chunk_multi[chunk]) {
+#pragma unroll
+      for (int j = 0; j < KP; ++j)
+        if (d[j]) atomicAdd(dst + j, d[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < KP; j += 4) *reinterpret_cast<int4*>(dst + j) = make_int4(n[j], n[j + 1], n[j + 2], n[j + 3]);
+    }
+  }
+  // reduce d over the S units of this wave (lanes with equal g), then over the block's waves
+#pragma unroll
+  for (int j = 0; j < KP; ++j) {
+    int v = d[j];
+#pragma unroll
+    for (int m = G; m < oni::kWave; m <<= 1) v += __shfl_xor(v, m);
+    d[j] = v;
+  }
+  if (c == 0) {
+#pragma unroll
+    for (int j = 0; j < KP; ++j) red[wave][kbase + j] = d[j];
+  }
+  __syncthreads();
+  if (threadIdx.x < KS) {
+    int v = 0;
+#pragma unroll
+    for (int w = 0; w < kWavesPerBlock; ++w) v += red[w][threadIdx.x];
+    if (v) atomicAdd(&a.dnk[threadIdx.x], v);
+  }
+}
+
+// Delta apply + q refresh: n_wk += Δ; n_k' = n_k + Δn_k; q = (n_wk+β)/(n_k'+Vβ); zero the other
+// delta buffer for the next sweep; bump the device sweep counter. nk/dnwk are ping-ponged by the
+// host so no block ever reads what another block of this launch writes.
+__global__ __launch_bounds__(256) void k_apply(int32_t* __restrict__ nwk, const int32_t* __restrict__ dcur,
+                                                int32_t* __restrict__ dother, const int32_t* __restrict__ nk_cur,
+                                                int32_t* __restrict__ nk_next, float* __restrict__ q, int64_t V,
+                                                int K, int KS, float beta, float vbeta, uint32_t* sweep_ctr,
+                                                int bump) {
+  __shared__ float den[256];
+  __shared__ int32_t nkn[256];
+  const int32_t* dnk_cur = dcur + V * KS;
+  for (int k = threadIdx.x; k < KS; k += blockDim.x) {
+    const int32_t v = nk_cur[k] + dnk_cur[k];
+    nkn[k] = v;
+    den[k] = (float)v + vbeta;
+  }
+  __syncthreads();
+  if (blockIdx.x == 0) {
+    for (int k = threadIdx.x; k < KS; k += blockDim.x) {
+      nk_next[k] = nkn[k];
+      dother[V * KS + k] = 0;
+    }
+    if (threadIdx.x == 0 && bump) *sweep_ctr += 1u;
+  }
+  const int64_t nvec = V * KS / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
+    const int4 dv = reinterpret_cast<const int4*>(dcur)[i];
+    int4 nv = reinterpret_cast<int4*>(nwk)[i];
+    nv.x += dv.x; nv.y += dv.y; nv.z += dv.z; nv.w += dv.w;
+    reinterpret_cast<int4*>(nwk)[i] = nv;
+    reinterpret_cast<int4*>(dother)[i] = make_int4(0, 0, 0, 0);
+    const int k0 = (int)((i * 4) % KS);
+    float4 qo;
+    qo.x = k0 + 0 < K ? ((float)nv.x + beta) / den[k0 + 0] : 0.f;
+    qo.y = k0 + 1 < K ? ((float)nv.y + beta) / den[k0 + 1] : 0.f;
+    qo.z = k0 + 2 < K ? ((float)nv.z + beta) / den[k0 + 2] : 0.f;
+    qo.w = k0 + 3 < K ? ((float)nv.w + beta) / den[k0 + 3] : 0.f;
+    reinterpret_cast<float4*>(q)[i] = qo;
+  }
+}
+
+__global__ void k_copy_rows(const int32_t* __restrict__ src, int32_t* __restrict__ dst,
+                            const int32_t* __restrict__ rows, int64_t n_rows, int KS) {
+  const int64_t total = n_rows * KS;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int64_t r = rows[i / KS];
+    const int k = (int)(i % KS);
+    dst[r * KS + k] = src[r * KS + k];
+  }
+}
+
+template <int G, int KP>
+int launch_gibbs(const OniGibbs& a, bool init, hipStream_t s) {
+  if (a.KS != G * KP) return (int)hipErrorInvalidValue;
+  const unsigned grid = (unsigned)((a.n_slices + kWavesPerBlock - 1) / kWavesPerBlock);
+  if (grid == 0) return 0;
+  if (init)
+    k_gibbs<G, KP, true><<<grid, kBlock, 0, s>>>(a);
+  else
+    k_gibbs<G, KP, false><<<grid, kBlock, 0, s>>>(a);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// Supported (G, KP) configurations. K ≤ 32: G = 1 (KP = K rounded up to 4).
+ONI_API int oni_gibbs_launch(const OniGibbs* a, int G, int KP, int init, hipStream_t s) {
+  if (a->K < 1 || a->K > 255 || a->K > a->KS) return (int)hipErrorInvalidValue;
+#define ONI_CASE(g_, kp_) \
+  if (G == g_ && KP == kp_) return launch_gibbs<g_, kp_>(*a, init != 0, s);
+  ONI_CASE(1, 4) ONI_CASE(1, 8) ONI_CASE(1, 12) ONI_CASE(1, 16) ONI_CASE(1, 20) ONI_CASE(1, 24) ONI_CASE(1, 28)
+  ONI_CASE(1, 32)
+  ONI_CASE(4, 8) ONI_CASE(4, 12) ONI_CASE(4, 16)
+  ONI_CASE(8, 8) ONI_CASE(8, 12) ONI_CASE(8, 16)
+  ONI_CASE(16, 8) ONI_CASE(16, 16)
+#undef ONI_CASE
+  return (int)hipErrorInvalidValue;
+}
+
+ONI_API int oni_gibbs_sizeof_args() { return (int)sizeof(OniGibbs); }
+
+ONI_API int oni_gibbs_apply(int32_t* nwk, const int32_t* dcur, int32_t* dother, const int32_t* nk_cur,
+                            int32_t* nk_next, float* q, int64_t V, int K, int KS, float beta, float vbeta,
+                            uint32_t* sweep_ctr, int bump, hipStream_t s) {
+  if (KS % 4 != 0 || KS > 256) return (int)hipErrorInvalidValue;
+  k_apply<<<oni::grid_for(V * KS / 4, 256, 2048), 256, 0, s>>>(nwk, dcur, dother, nk_cur, nk_next, q, V, K, KS, beta,
+                                                                vbeta, sweep_ctr, bump);
+  return (int)hipGetLastError();
+}
+
+ONI_API int oni_copy_rows(const int32_t* src, int32_t* dst, const int32_t* rows, int64_t n_rows, int KS,
+                          hipStream_t s) {
+  if (n_rows == 0) return 0;
+  k_copy_rows<<<oni::grid_for(n_rows * KS), 256, 0, s>>>(src, dst, rows, n_rows, KS);
+  return (int)hipGetLastError();
+}

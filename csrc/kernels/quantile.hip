@@ -1,0 +1,100 @@
+// K01 -- exact multi-quantile cut points by LSD-free radix *select* (no sort).
+//
+// Replaces the reference's Spark `sortBy` ECDF (oni-ml Quantiles.computeDeciles / computeQuintiles,
+// SURVEY.md §2.2 C15, [U-M]) with three histogram passes over u32 order keys (11+11+10 bits).
+// Every quantile q carries its own radix prefix; a pass histograms only the keys whose high bits
+// match one of the (de-duplicated) live prefixes, all of them in ONE read of the column, into
+// P×2^nbits LDS bins. Per-block bins are flushed to the global histogram with integer atomics on
+// non-zero bins only. The host picks the digit holding each target rank between passes (and, for
+// data-parallel runs, all-reduces the histograms over RCCL first: collective X03).
+#include "oni_common.h"
+
+namespace {
+
+constexpr int kMaxPrefixes = 16;
+
+template <int NBITS>
+__global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__ keys, int64_t n, int shift,
+                                                     const uint32_t* __restrict__ prefixes, int P,
+                                                     uint32_t mask, uint32_t* __restrict__ hist) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lh[];
+  constexpr int B = 1 << NBITS;
+  const int nb = P * B;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) lh[i] = 0u;
+  uint32_t pre[kMaxPrefixes];
+#pragma unroll
+  for (int p = 0; p < kMaxPrefixes; ++p) pre[p] = p < P ? prefixes[p] : 0xFFFFFFFFu;
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t k = keys[i];
+    const uint32_t hi = k & mask;
+    const uint32_t digit = (k >> shift) & (B - 1);
+#pragma unroll
+    for (int p = 0; p < kMaxPrefixes; ++p) {
+      if (p < P && hi == pre[p]) atomicAdd(&lh[p * B + digit], 1u);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) {
+    const uint32_t v = lh[i];
+    if (v) atomicAdd(&hist[i], v);
+  }
+}
+
+__global__ void k_f32_keys(const float* __restrict__ x, int64_t n, uint32_t* __restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = oni::f32_key(x[i]);
+}
+
+__global__ void k_i64_keys(const int64_t* __restrict__ x, int64_t n, uint32_t* __restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t v = x[i];
+    out[i] = v <= 0 ? 0u : (v >= 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)v);
+  }
+}
+
+// bin(x) = #{cuts c : key(x) > c}; one thread per element, cuts in scalar registers.
+__global__ void k_bin_keys(const uint32_t* __restrict__ keys, int64_t n, const uint32_t* __restrict__ cuts, int nc,
+                           uint8_t* __restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t k = keys[i];
+    int b = 0;
+    for (int c = 0; c < nc; ++c) b += k > cuts[c];
+    out[i] = (uint8_t)b;
+  }
+}
+
+}  // namespace
+
+ONI_API int oni_radix_hist(const uint32_t* keys, int64_t n, int shift, int nbits, const uint32_t* prefixes, int P,
+                           uint32_t mask, uint32_t* hist, hipStream_t s) {
+  if (P < 1 || P > kMaxPrefixes) return (int)hipErrorInvalidValue;
+  const size_t lds = (size_t)P << nbits << 2;
+  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+  const unsigned grid = oni::grid_for(n, 256, 512);
+  if (nbits == 11)
+    k_radix_hist<11><<<grid, 256, lds, s>>>(keys, n, shift, prefixes, P, mask, hist);
+  else if (nbits == 10)
+    k_radix_hist<10><<<grid, 256, lds, s>>>(keys, n, shift, prefixes, P, mask, hist);
+  else
+    return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+ONI_API int oni_f32_keys(const float* x, int64_t n, uint32_t* out, hipStream_t s) {
+  k_f32_keys<<<oni::grid_for(n), 256, 0, s>>>(x, n, out);
+  return (int)hipGetLastError();
+}
+
+ONI_API int oni_i64_keys(const int64_t* x, int64_t n, uint32_t* out, hipStream_t s) {
+  k_i64_keys<<<oni::grid_for(n), 256, 0, s>>>(x, n, out);
+  return (int)hipGetLastError();
+}
+
+ONI_API int oni_bin_keys(const uint32_t* keys, int64_t n, const uint32_t* cuts, int nc, uint8_t* out, hipStream_t s) {
+  k_bin_keys<<<oni::grid_for(n), 256, 0, s>>>(keys, n, cuts, nc, out);
+  return (int)hipGetLastError();
+}

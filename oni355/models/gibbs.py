@@ -1,0 +1,244 @@
+"""Collapsed-Gibbs LDA engine (device-resident, data-parallel over documents).
+
+The MI355X replacement of oni-lda-c ``lda est``: instead of
+variational EM over an on-disk corpus shipped to MPI ranks, the corpus (SELL layout, see
+:mod:`oni355.models.corpus`) and all count matrices live in HBM; one sweep is
+
+    copy long-doc rows → k_gibbs (sample every token) → [RCCL all-reduce of Δn_wk ‖ Δn_k] → k_apply
+
+Outputs mirror lda-c (``final.beta`` = log φ, ``final.gamma`` = n_dk + α, ``final.other``,
+``likelihood.dat``, ``word-assignments.dat``; see :mod:`oni355.io.ldac`).
+
+Determinism contract: every z is a pure function of (data, seed, sweep) — the same for 1 or N
+GPUs, any chunk packing, and across checkpoint/resume (tests/test_gibbs*.py).
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..utils import fault
+from .corpus import Corpus, canonical_tokens
+
+
+@dataclass
+class GibbsConfig:
+    K: int = 20
+    alpha: float | None = None  # default 50/K (Griffiths & Steyvers)
+    beta: float = 0.01
+    seed: int = 0x0D15EA5E
+    use_graph: bool = True
+
+    def resolved_alpha(self) -> float:
+        return float(self.alpha) if self.alpha is not None else 50.0 / self.K
+
+
+class GibbsLDA:
+    """Device state + sweep loop. ``comm`` (oni355.parallel.comm.Comm) enables data parallelism."""
+
+    def __init__(self, corpus: Corpus, cfg: GibbsConfig, comm=None, V_global: int | None = None):
+        self.c = corpus
+        self.cfg = cfg
+        self.comm = comm
+        self.K = cfg.K
+        self.G, self.KP = ops.choose_tiling(cfg.K)
+        if corpus.G != self.G:
+            raise ValueError(f"corpus built for G={corpus.G}, K={cfg.K} needs G={self.G}")
+        self.KS = self.G * self.KP
+        self.alpha = cfg.resolved_alpha()
+        self.beta = float(cfg.beta)
+        self.V = int(V_global if V_global is not None else corpus.V)
+        self.vbeta = float(np.float32(self.V * self.beta))
+        dev = corpus.tok_word.device
+        self.device = dev
+        D, V, KS = corpus.D, self.V, self.KS
+        i32 = torch.int32
+        self.tok_z = torch.zeros(corpus.sell_slots, dtype=torch.uint8, device=dev)
+        self.ndk = [torch.zeros(max(D, 1), KS, dtype=i32, device=dev) for _ in range(2)]
+        self.nwk = torch.zeros(V, KS, dtype=i32, device=dev)
+        self.nk = [torch.zeros(KS, dtype=i32, device=dev) for _ in range(2)]
+        self.dn = [torch.zeros(V * KS + KS, dtype=i32, device=dev) for _ in range(2)]
+        self.q = torch.zeros(V, KS, dtype=torch.float32, device=dev)
+        self.sweep_ctr = torch.zeros(1, dtype=i32, device=dev)
+        self.a = 0  # ndk parity
+        self.b = 0  # delta-buffer parity
+        self.cn = 0  # nk parity
+        self.sweeps_done = 0
+        self.likelihoods: list[tuple[int, float]] = []
+        self._graph = None
+        self.timings = {"allreduce_s": 0.0, "allreduce_calls": 0}
+
+    # ---------------------------------------------------------------------------------------------
+    def _state(self, init: bool) -> dict:
+        c = self.c
+        st = dict(tok_word=c.tok_word, tok_z=self.tok_z, slice_off=c.slice_off, slice_len=c.slice_len,
+                  chunk_doc=c.chunk_doc, chunk_pos0=c.chunk_pos0, chunk_key=c.chunk_key, chunk_multi=c.chunk_multi,
+                  q=self.q)
+        VK = self.V * self.KS
+        if init:
+            st.update(ndk_src=self.ndk[0], ndk_dst=self.ndk[0], dnwk=self.nwk, dnk=self.nk[0])
+        else:
+            d = self.dn[self.b]
+            st.update(ndk_src=self.ndk[self.a], ndk_dst=self.ndk[1 - self.a], dnwk=d[:VK].view(self.V, self.KS),
+                      dnk=d[VK:])
+        return st
+
+    def initialize(self) -> None:
+        """Random topic init (Philox stream 0), counts, first q table."""
+        for t in (*self.ndk, self.nwk, *self.nk, *self.dn):
+            t.zero_()
+        self.tok_z.zero_()
+        self.a = self.b = 0
+        self.cn = 0
+        ops.gibbs_pass(self._state(True), self.G, self.KP, self.K, self.alpha, self.cfg.seed, True,
+                       self.sweep_ctr, self.c.chunk_len, host_sweep=0)
+        if self.comm is not None and self.comm.world > 1:
+            self.comm.allreduce_(self.nwk)
+            self.comm.allreduce_(self.nk[0])
+        self.sweeps_done = 0
+        self._graph = None
+        self._prime()
+
+    def _prime(self) -> None:
+        # zero-delta apply: q from n_wk, nk[1] = nk[0]; leaves dn[0], dn[1] zero
+        VK = self.V * self.KS
+        self.dn[0].zero_()
+        ops.gibbs_apply(self.nwk, self.dn[0], self.dn[1], self.nk[self.cn], self.nk[1 - self.cn], self.q, self.V,
+                        self.K, self.KS, self.beta, self.vbeta, self.sweep_ctr, bump=False)
+        self.cn = 1 - self.cn
+        self.sweep_ctr.fill_(self.sweeps_done + 1)
+        _ = VK
+
+    # ---------------------------------------------------------------------------------------------
+    def _one_sweep(self) -> None:
+        c = self.c
+        ops.copy_rows(self.ndk[self.a], self.ndk[1 - self.a], c.long_rows, self.KS)
+        ops.gibbs_pass(self._state(False), self.G, self.KP, self.K, self.alpha, self.cfg.seed, False,
+                       self.sweep_ctr, c.chunk_len, host_sweep=self.sweeps_done + 1)
+        if self.comm is not None and self.comm.world > 1:
+            t0 = time.perf_counter()
+            self.comm.allreduce_(self.dn[self.b])
+            self.timings["allreduce_s"] += time.perf_counter() - t0
+            self.timings["allreduce_calls"] += 1
+        ops.gibbs_apply(self.nwk, self.dn[self.b], self.dn[1 - self.b], self.nk[self.cn], self.nk[1 - self.cn],
+                        self.q, self.V, self.K, self.KS, self.beta, self.vbeta, self.sweep_ctr, bump=True)
+        self.a, self.b, self.cn = 1 - self.a, 1 - self.b, 1 - self.cn
+        self.sweeps_done += 1
+
+    def _graphable(self) -> bool:
+        return (self.cfg.use_graph and self.device.type == "cuda" and (self.comm is None or self.comm.world == 1)
+                and os.environ.get("ONI_NO_GRAPH", "0") != "1")
+
+    def _capture(self) -> None:
+        """Capture two sweeps (parities return to their start) into one HIP graph."""
+        saved = (self.a, self.b, self.cn, self.sweeps_done)
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        g = torch.cuda.CUDAGraph()
+        # snapshot the state the capture's warm-up would disturb: none — capture does not execute.
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                self._one_sweep()
+                self._one_sweep()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        self.a, self.b, self.cn, self.sweeps_done = saved
+        self._graph = g
+        self._graph_parity = (self.a, self.b, self.cn)
+
+    def sweep(self, n: int = 1) -> None:
+        """Run ``n`` sweeps (graph-replayed in pairs on a single GPU)."""
+        fault.maybe_inject(self.sweeps_done, self.comm.rank if self.comm else 0)
+        done = 0
+        if self._graphable() and n >= 2:
+            if self._graph is not None and self._graph_parity != (self.a, self.b, self.cn):
+                self._one_sweep()
+                done += 1
+            if self._graph is None:
+                self._capture()
+            while n - done >= 2:
+                self._graph.replay()
+                self.sweeps_done += 2
+                done += 2
+        while done < n:
+            self._one_sweep()
+            done += 1
+
+    # ---------------------------------------------------------------------------------------------
+    @property
+    def ndk_cur(self) -> torch.Tensor:
+        return self.ndk[self.a]
+
+    @property
+    def nk_cur(self) -> torch.Tensor:
+        return self.nk[self.cn]
+
+    def theta(self) -> torch.Tensor:
+        """θ[d,k] = (n_dk+α)/(n_d+Kα), padded to KS with zeros (score-kernel layout)."""
+        n = self.ndk_cur.to(torch.float32)
+        nd = n[:, : self.K].sum(1, keepdim=True)
+        th = (n + self.alpha) / (nd + self.K * self.alpha)
+        th[:, self.K:] = 0
+        return th.contiguous()
+
+    def phi(self) -> torch.Tensor:
+        """φ[w,k] = (n_wk+β)/(n_k+Vβ) for the current counts (= the q table), KS-padded."""
+        return self.q
+
+    def log_likelihood(self) -> float:
+        """Collapsed joint log p(w, z) (Griffiths & Steyvers 2004), summed over ranks."""
+        K, a, b, V = self.K, self.alpha, self.beta, self.V
+        nwk = self.nwk[:, :K].to(torch.float64)
+        nk = self.nk_cur[:K].to(torch.float64)
+        word = (K * (math.lgamma(V * b) - V * math.lgamma(b)) + torch.lgamma(nwk + b).sum()
+                - torch.lgamma(nk + V * b).sum())
+        ndk = self.ndk_cur[: self.c.D, :K].to(torch.float64)
+        nd = ndk.sum(1)
+        doc = (self.c.D * (math.lgamma(K * a) - K * math.lgamma(a)) + torch.lgamma(ndk + a).sum()
+               - torch.lgamma(nd + K * a).sum())
+        doc_v = doc.reshape(1)
+        if self.comm is not None and self.comm.world > 1:
+            self.comm.allreduce_(doc_v)
+        return float(word + doc_v[0])
+
+    def record_likelihood(self) -> float:
+        ll = self.log_likelihood()
+        self.likelihoods.append((self.sweeps_done, ll))
+        return ll
+
+    # ---------------------------------------------------------------------------------------------
+    def canonical_z(self) -> torch.Tensor:
+        c = self.c
+        out = torch.zeros(max(c.T, 1), dtype=torch.uint8, device=self.device)
+        ops.sell_perm_z(c.chunk_doc, c.chunk_pos0, c.chunk_len, c.S, c.slice_off, c.doc_tok_ptr, self.tok_z, out,
+                        True)
+        return out[: c.T]
+
+    def load_canonical_z(self, z: torch.Tensor, sweeps_done: int) -> None:
+        """Resume: scatter z into SELL, recount every table from z, refresh q (bitwise resume)."""
+        c = self.c
+        zc = torch.zeros(max(c.T, 1), dtype=torch.uint8, device=self.device)
+        zc[: c.T] = z.to(self.device)
+        self.tok_z.zero_()
+        ops.sell_perm_z(c.chunk_doc, c.chunk_pos0, c.chunk_len, c.S, c.slice_off, c.doc_tok_ptr, self.tok_z, zc,
+                        False)
+        tdoc, tword = canonical_tokens(c)
+        zz = zc[: c.T].to(torch.int64)
+        for t in (*self.ndk, self.nwk, *self.nk, *self.dn):
+            t.zero_()
+        KS = self.KS
+        self.ndk[0].view(-1).index_add_(0, tdoc * KS + zz, torch.ones_like(zz, dtype=torch.int32))
+        self.nwk.view(-1).index_add_(0, tword * KS + zz, torch.ones_like(zz, dtype=torch.int32))
+        self.nk[0].index_add_(0, zz, torch.ones_like(zz, dtype=torch.int32))
+        if self.comm is not None and self.comm.world > 1:
+            self.comm.allreduce_(self.nwk)
+            self.comm.allreduce_(self.nk[0])
+        self.a = self.b = self.cn = 0
+        self.sweeps_done = sweeps_done
+        self._graph = None
+        self._prime()

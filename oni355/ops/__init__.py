@@ -1,0 +1,320 @@
+"""Device ops: torch tensors in, torch tensors out.
+
+CUDA (= HIP on ROCm) tensors run the hand-written gfx950 kernels of ``liboni_hip.so`` -- there is
+no silent fallback, a missing library raises. CPU tensors run the NumPy specification oracle
+(:mod:`oni355.ref.spec`), which is what the CPU test-suite and the ``--device cpu`` path use.
+
+All u32 quantities (IPv4 keys, packed words, order keys) travel as ``torch.int32`` tensors holding
+the same bits; kernels reinterpret them.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from ..ref import spec
+from . import _lib
+
+__all__ = [
+    "f32_keys", "i64_keys", "quantile_cuts", "bin_keys", "flow_keys", "flow_wordify", "sell_fill",
+    "sell_perm_z", "gibbs_pass", "gibbs_apply", "copy_rows", "score", "select_below", "choose_tiling",
+]
+
+
+def _is_dev(t: torch.Tensor) -> bool:
+    return t.device.type == "cuda"
+
+
+def _u32np(t: torch.Tensor) -> np.ndarray:
+    return t.detach().cpu().numpy().view(np.uint32)
+
+
+def _from_u32(a: np.ndarray, device) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint32).view(np.int32)).to(device)
+
+
+def _need(t: torch.Tensor, dtype: torch.dtype, name: str, n: int | None = None) -> None:
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if n is not None and t.numel() != n:
+        raise ValueError(f"{name}: expected {n} elements, got {t.numel()}")
+
+
+# ------------------------------------------------------------------------------------------------
+# tiling choice for the sampler: (G lanes per unit, KP topics per lane)
+# ------------------------------------------------------------------------------------------------
+def choose_tiling(K: int) -> tuple[int, int]:
+    if K < 1 or K > 255:
+        raise ValueError("K must be in [1, 255]")
+    r4 = lambda x: (x + 3) // 4 * 4  # noqa: E731
+    if K <= 32:
+        return 1, r4(K)
+    if K <= 48:
+        return 4, 12
+    if K <= 64:
+        return 4, 16
+    if K <= 96:
+        return 8, 12
+    if K <= 128:
+        return 8, 16
+    return 16, 16
+
+
+# ------------------------------------------------------------------------------------------------
+# keys / quantiles
+# ------------------------------------------------------------------------------------------------
+def f32_keys(x: torch.Tensor) -> torch.Tensor:
+    _need(x, torch.float32, "x")
+    if not _is_dev(x):
+        return _from_u32(spec.f32_key(x.numpy()), x.device)
+    out = torch.empty(x.numel(), dtype=torch.int32, device=x.device)
+    L = _lib.lib()
+    _lib.check(L.oni_f32_keys(_lib.ptr(x), x.numel(), _lib.ptr(out), _lib.stream()), "oni_f32_keys")
+    return out
+
+
+def i64_keys(x: torch.Tensor) -> torch.Tensor:
+    _need(x, torch.int64, "x")
+    if not _is_dev(x):
+        return _from_u32(spec.i64_keys(x.numpy()), x.device)
+    out = torch.empty(x.numel(), dtype=torch.int32, device=x.device)
+    L = _lib.lib()
+    _lib.check(L.oni_i64_keys(_lib.ptr(x), x.numel(), _lib.ptr(out), _lib.stream()), "oni_i64_keys")
+    return out
+
+
+_PASSES = ((21, 11), (10, 11), (0, 10))
+
+
+def quantile_cuts(keys: torch.Tensor, fracs, allreduce=None, n_global: int | None = None) -> np.ndarray:
+    """Exact cut keys at ascending ranks ceil(num*N/den)-1 (N = global count).
+
+    ``allreduce(np.ndarray[int64]) -> np.ndarray`` sums histograms over ranks (collective X03);
+    ``n_global`` is the total element count over ranks (defaults to the local count).
+    """
+    _need(keys, torch.int32, "keys")
+    n = keys.numel() if n_global is None else int(n_global)
+    if not _is_dev(keys):
+        if allreduce is not None:
+            raise NotImplementedError("distributed quantiles need device keys")
+        return spec.quantile_cuts(_u32np(keys), fracs)
+    if n == 0:
+        return np.zeros(len(fracs), dtype=np.uint32)
+    L = _lib.lib()
+    ranks = spec.quantile_ranks(n, fracs).astype(np.int64)
+    prefix = np.zeros(len(fracs), dtype=np.uint64)
+    hist_buf = torch.zeros(16 << 11, dtype=torch.int32, device=keys.device)
+    for shift, nbits in _PASSES:
+        top = shift + nbits
+        mask = 0 if top >= 32 else (0xFFFFFFFF << top) & 0xFFFFFFFF
+        uniq, inv = np.unique(prefix, return_inverse=True)
+        P = len(uniq)
+        B = 1 << nbits
+        pre_t = torch.from_numpy(uniq.astype(np.uint32).view(np.int32)).to(keys.device)
+        hist = hist_buf[: P * B]
+        hist.zero_()
+        _lib.check(L.oni_radix_hist(_lib.ptr(keys), keys.numel(), shift, nbits, _lib.ptr(pre_t), P, mask,
+                                    _lib.ptr(hist), _lib.stream()), "oni_radix_hist")
+        h = hist.cpu().numpy().view(np.uint32).astype(np.int64).reshape(P, B)
+        if allreduce is not None:
+            h = np.asarray(allreduce(h), dtype=np.int64).reshape(P, B)
+        cum = np.cumsum(h, axis=1)
+        for qi in range(len(fracs)):
+            c = cum[inv[qi]]
+            digit = int(np.searchsorted(c, ranks[qi], side="right"))
+            digit = min(digit, B - 1)
+            if digit > 0:
+                ranks[qi] -= c[digit - 1]
+            prefix[qi] |= np.uint64(digit << shift)
+    return prefix.astype(np.uint32)
+
+
+def bin_keys(keys: torch.Tensor, cuts: np.ndarray) -> torch.Tensor:
+    _need(keys, torch.int32, "keys")
+    if not _is_dev(keys):
+        return torch.from_numpy(spec.bin_keys(_u32np(keys), cuts))
+    c = _from_u32(np.asarray(cuts, dtype=np.uint32), keys.device)
+    out = torch.empty(keys.numel(), dtype=torch.uint8, device=keys.device)
+    _lib.check(_lib.lib().oni_bin_keys(_lib.ptr(keys), keys.numel(), _lib.ptr(c), len(cuts), _lib.ptr(out),
+                                       _lib.stream()), "oni_bin_keys")
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# flow featurization
+# ------------------------------------------------------------------------------------------------
+def flow_keys(hour, minute, second, ibyt, ipkt):
+    n = hour.numel()
+    for t, nm, dt in ((hour, "hour", torch.int32), (minute, "minute", torch.int32), (second, "second", torch.int32),
+                      (ibyt, "ibyt", torch.int64), (ipkt, "ipkt", torch.int64)):
+        _need(t, dt, nm, n)
+    if not _is_dev(hour):
+        tk, bk, pk = spec.flow_keys(hour.numpy(), minute.numpy(), second.numpy(), ibyt.numpy(), ipkt.numpy())
+        return tuple(_from_u32(x, hour.device) for x in (tk, bk, pk))
+    outs = [torch.empty(n, dtype=torch.int32, device=hour.device) for _ in range(3)]
+    _lib.check(_lib.lib().oni_flow_keys(*map(_lib.ptr, (hour, minute, second, ibyt, ipkt)), n,
+                                        *map(_lib.ptr, outs), _lib.stream()), "oni_flow_keys")
+    return tuple(outs)
+
+
+def flow_wordify(sport, dport, tkey, bkey, pkey, tcuts, bcuts, pcuts):
+    n = sport.numel()
+    _need(sport, torch.int32, "sport", n)
+    _need(dport, torch.int32, "dport", n)
+    for t, nm in ((tkey, "tkey"), (bkey, "bkey"), (pkey, "pkey")):
+        _need(t, torch.int32, nm, n)
+    if not _is_dev(sport):
+        sw, dw = spec.flow_wordify(sport.numpy(), dport.numpy(), _u32np(tkey), _u32np(bkey), _u32np(pkey),
+                                   tcuts, bcuts, pcuts)
+        return _from_u32(sw, sport.device), _from_u32(dw, sport.device)
+    cuts = np.concatenate([np.asarray(tcuts, np.uint32), np.asarray(bcuts, np.uint32), np.asarray(pcuts, np.uint32)])
+    c = _from_u32(cuts, sport.device)
+    sw = torch.empty(n, dtype=torch.int32, device=sport.device)
+    dw = torch.empty(n, dtype=torch.int32, device=sport.device)
+    _lib.check(_lib.lib().oni_flow_wordify(_lib.ptr(sport), _lib.ptr(dport), _lib.ptr(tkey), _lib.ptr(bkey),
+                                           _lib.ptr(pkey), n, _lib.ptr(c), len(tcuts), len(bcuts), len(pcuts),
+                                           _lib.ptr(sw), _lib.ptr(dw), _lib.stream()), "oni_flow_wordify")
+    return sw, dw
+
+
+# ------------------------------------------------------------------------------------------------
+# SELL layout
+# ------------------------------------------------------------------------------------------------
+def sell_fill(chunk_doc, chunk_pos0, chunk_len, S, slice_off, doc_pair_ptr, pair_tokoff, pair_word, pair_cnt,
+              tok_word):
+    if not _is_dev(tok_word):
+        tw = tok_word.numpy().view(np.uint32)
+        spec.sell_fill(chunk_doc.numpy(), chunk_pos0.numpy(), chunk_len.numpy(), S, slice_off.numpy(),
+                       doc_pair_ptr.numpy(), pair_tokoff.numpy(), pair_word.numpy(), pair_cnt.numpy(), tw)
+        return tok_word
+    _need(chunk_doc, torch.int32, "chunk_doc")
+    _need(slice_off, torch.int64, "slice_off")
+    _need(pair_tokoff, torch.int64, "pair_tokoff")
+    _lib.check(_lib.lib().oni_sell_fill(*map(_lib.ptr, (chunk_doc, chunk_pos0, chunk_len)), chunk_doc.numel(), S,
+                                        *map(_lib.ptr, (slice_off, doc_pair_ptr, pair_tokoff, pair_word, pair_cnt,
+                                                        tok_word)), _lib.stream()), "oni_sell_fill")
+    return tok_word
+
+
+def sell_perm_z(chunk_doc, chunk_pos0, chunk_len, S, slice_off, doc_tok_ptr, tok_z, canon_z, to_canon: bool):
+    if not _is_dev(tok_z):
+        cd, cp, cl, so, dt = (x.numpy() for x in (chunk_doc, chunk_pos0, chunk_len, slice_off, doc_tok_ptr))
+        tz, cz = tok_z.numpy(), canon_z.numpy()
+        for i in np.nonzero(cd >= 0)[0]:
+            off = int(so[i // S]) + i % S
+            sidx = off + np.arange(int(cl[i])) * S
+            base = int(dt[cd[i]]) + int(cp[i])
+            if to_canon:
+                cz[base:base + int(cl[i])] = tz[sidx]
+            else:
+                tz[sidx] = cz[base:base + int(cl[i])]
+        return
+    _lib.check(_lib.lib().oni_sell_perm_z(*map(_lib.ptr, (chunk_doc, chunk_pos0, chunk_len)), chunk_doc.numel(), S,
+                                          _lib.ptr(slice_off), _lib.ptr(doc_tok_ptr), _lib.ptr(tok_z),
+                                          _lib.ptr(canon_z), 0 if to_canon else 1, _lib.stream()),
+               "oni_sell_perm_z")
+
+
+# ------------------------------------------------------------------------------------------------
+# sampler
+# ------------------------------------------------------------------------------------------------
+def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init: bool, sweep_ctr: torch.Tensor,
+               chunk_len: torch.Tensor, host_sweep: int | None = None) -> None:
+    """Launch one init/sweep pass. ``st`` holds the OniGibbs tensors (see csrc/kernels/gibbs.hip)."""
+    s0, s1 = spec.split_seed(seed)
+    KS = G * KP
+    if not _is_dev(st["tok_word"]):
+        npst = {k: (v.numpy().view(np.uint32) if k in ("tok_word", "chunk_key") else v.numpy())
+                for k, v in st.items()}
+        spec.gibbs_pass(npst, G, KP, K, alpha, s0, s1, init,
+                        int(host_sweep if host_sweep is not None else sweep_ctr.item()), chunk_len.numpy())
+        return
+    n_slices = st["slice_len"].numel()
+    if st["q"].shape[-1] != KS or st["ndk_src"].shape[-1] != KS:
+        raise ValueError("q / ndk row width must equal G*KP")
+    if st["chunk_doc"].numel() != n_slices * (64 // G):
+        raise ValueError("chunk table must hold S chunks per slice")
+    a = _lib.OniGibbs()
+    for name in ("tok_word", "tok_z", "slice_off", "slice_len", "chunk_doc", "chunk_pos0", "chunk_key",
+                 "chunk_multi", "ndk_src", "ndk_dst", "q", "dnwk", "dnk"):
+        setattr(a, name, _lib.ptr(st[name]))
+    a.sweep_ctr = _lib.ptr(sweep_ctr)
+    a.n_slices, a.K, a.KS, a.alpha, a.seed0, a.seed1 = n_slices, K, KS, float(alpha), s0, s1
+    _lib.check(_lib.lib().oni_gibbs_launch(C.byref(a), G, KP, 1 if init else 0, _lib.stream()), "oni_gibbs_launch")
+
+
+def gibbs_apply(nwk, dcur, dother, nk_cur, nk_next, q, V, K, KS, beta, vbeta, sweep_ctr, bump=True):
+    if not _is_dev(nwk):
+        n2, nk2, q2 = spec.gibbs_apply(nwk.numpy(), dcur[: V * KS].view(V, KS).numpy(), dcur[V * KS:].numpy(),
+                                       nk_cur.numpy(), K, beta, vbeta)
+        nwk.copy_(torch.from_numpy(n2))
+        nk_next.copy_(torch.from_numpy(nk2))
+        q.copy_(torch.from_numpy(q2))
+        dother.zero_()
+        if bump:
+            sweep_ctr += 1
+        return
+    _lib.check(_lib.lib().oni_gibbs_apply(*map(_lib.ptr, (nwk, dcur, dother, nk_cur, nk_next, q)), V, K, KS,
+                                          float(beta), float(vbeta), _lib.ptr(sweep_ctr), 1 if bump else 0,
+                                          _lib.stream()), "oni_gibbs_apply")
+
+
+def copy_rows(src, dst, rows, KS):
+    if rows.numel() == 0:
+        return
+    if not _is_dev(src):
+        r = rows.long()
+        dst[r] = src[r]
+        return
+    _lib.check(_lib.lib().oni_copy_rows(_lib.ptr(src), _lib.ptr(dst), _lib.ptr(rows), rows.numel(), KS,
+                                        _lib.stream()), "oni_copy_rows")
+
+
+# ------------------------------------------------------------------------------------------------
+# scoring / selection
+# ------------------------------------------------------------------------------------------------
+def score(theta, phi, d1, w1, d2=None, w2=None, tol: float = float("inf"), want_parts=False, hist=None):
+    """Event scores (min over the two endpoints when d2/w2 given). Returns (score, s1, s2)."""
+    n = d1.numel()
+    if not _is_dev(theta):
+        sc, s1, s2 = spec.score(theta.numpy(), phi.numpy(), d1.numpy(), w1.numpy(),
+                                None if d2 is None else d2.numpy(), None if w2 is None else w2.numpy())
+        out = torch.from_numpy(sc)
+        if hist is not None:
+            sel = sc < tol
+            b = spec.f32_key(sc[sel]) >> np.uint32(21)
+            hist += torch.from_numpy(np.bincount(b, minlength=2048).astype(np.int32))
+        return out, torch.from_numpy(s1), (None if s2 is None else torch.from_numpy(s2))
+    KS = theta.shape[-1]
+    if phi.shape[-1] != KS:
+        raise ValueError("theta/phi row widths differ")
+    out = torch.empty(n, dtype=torch.float32, device=theta.device)
+    o1 = torch.empty_like(out) if want_parts else None
+    o2 = torch.empty_like(out) if (want_parts and d2 is not None) else None
+    _lib.check(_lib.lib().oni_score(_lib.ptr(theta), _lib.ptr(phi), KS, _lib.ptr(d1), _lib.ptr(w1),
+                                    _lib.ptr(d2), _lib.ptr(w2), n, float(tol), _lib.ptr(out), _lib.ptr(o1),
+                                    _lib.ptr(o2), _lib.ptr(hist), _lib.stream()), "oni_score")
+    return out, o1, o2
+
+
+def select_below(score_t: torch.Tensor, tol: float, bmax: int, cap: int):
+    """Indices + scores of events with score < tol whose top-11 order-key bucket ≤ bmax (unordered)."""
+    if not _is_dev(score_t):
+        s = score_t.numpy()
+        m = (s < tol) & ((spec.f32_key(s) >> np.uint32(21)) <= bmax)
+        idx = np.nonzero(m)[0]
+        return torch.from_numpy(idx.astype(np.int64)), torch.from_numpy(s[idx])
+    cnt = torch.zeros(1, dtype=torch.int32, device=score_t.device)
+    out_i = torch.empty(max(cap, 1), dtype=torch.int64, device=score_t.device)
+    out_s = torch.empty(max(cap, 1), dtype=torch.float32, device=score_t.device)
+    _lib.check(_lib.lib().oni_select_below(_lib.ptr(score_t), score_t.numel(), float(tol), int(bmax), _lib.ptr(cnt),
+                                           _lib.ptr(out_i), _lib.ptr(out_s), cap, _lib.stream()),
+               "oni_select_below")
+    k = int(cnt.item())
+    if k > cap:
+        raise RuntimeError(f"select_below overflow: {k} > cap {cap}")
+    return out_i[:k], out_s[:k]

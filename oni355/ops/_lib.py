@@ -1,0 +1,107 @@
+"""ctypes binding of ``oni355/_lib/liboni_hip.so`` (the hand-written gfx950 kernels).
+
+The library exposes a plain C ABI; every launcher takes raw device pointers plus the HIP stream
+(``torch.cuda.current_stream().cuda_stream``) so kernels are ordered with torch's own work and are
+captured by ``torch.cuda.graph`` like any other launch.
+
+There is no fallback: if the library is missing or was built for another architecture, every
+device op raises. (CPU tensors go to the NumPy reference oracle explicitly, see ``oni355.ops``.)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import torch  # noqa: F401  -- must be loaded first: our .so resolves libamdhip64.so.7 to torch's copy
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(os.path.dirname(_HERE), "_lib")
+HIP_LIB_PATH = os.path.join(LIB_DIR, "liboni_hip.so")
+
+_lock = threading.Lock()
+_lib = None
+
+vp, i32, i64, f32, u32 = C.c_void_p, C.c_int32, C.c_int64, C.c_float, C.c_uint32
+
+
+class OniGibbs(C.Structure):
+    """Mirror of ``struct OniGibbs`` in csrc/kernels/gibbs.hip (size checked at load)."""
+
+    _fields_ = [
+        ("tok_word", vp), ("tok_z", vp), ("slice_off", vp), ("slice_len", vp),
+        ("chunk_doc", vp), ("chunk_pos0", vp), ("chunk_key", vp), ("chunk_multi", vp),
+        ("ndk_src", vp), ("ndk_dst", vp), ("q", vp), ("dnwk", vp), ("dnk", vp), ("sweep_ctr", vp),
+        ("n_slices", i64), ("K", i32), ("KS", i32), ("alpha", f32), ("seed0", u32), ("seed1", u32),
+    ]
+
+
+_SIGS = {
+    "oni_radix_hist": [vp, i64, C.c_int, C.c_int, vp, C.c_int, u32, vp, vp],
+    "oni_f32_keys": [vp, i64, vp, vp],
+    "oni_i64_keys": [vp, i64, vp, vp],
+    "oni_bin_keys": [vp, i64, vp, C.c_int, vp, vp],
+    "oni_flow_keys": [vp, vp, vp, vp, vp, i64, vp, vp, vp, vp],
+    "oni_flow_wordify": [vp, vp, vp, vp, vp, i64, vp, C.c_int, C.c_int, C.c_int, vp, vp, vp],
+    "oni_sell_fill": [vp, vp, vp, i64, C.c_int, vp, vp, vp, vp, vp, vp, vp],
+    "oni_sell_perm_z": [vp, vp, vp, i64, C.c_int, vp, vp, vp, vp, C.c_int, vp],
+    "oni_gibbs_launch": [C.POINTER(OniGibbs), C.c_int, C.c_int, C.c_int, vp],
+    "oni_gibbs_sizeof_args": [],
+    "oni_gibbs_apply": [vp, vp, vp, vp, vp, vp, i64, C.c_int, C.c_int, f32, f32, vp, C.c_int, vp],
+    "oni_copy_rows": [vp, vp, vp, i64, C.c_int, vp],
+    "oni_score": [vp, vp, C.c_int, vp, vp, vp, vp, i64, f32, vp, vp, vp, vp, vp],
+    "oni_select_below": [vp, i64, f32, u32, vp, vp, vp, i64, vp],
+}
+# optional symbols (added by later kernel files); bound when present
+_OPTIONAL_SIGS: dict[str, list] = {}
+
+
+def register_optional(name: str, argtypes: list) -> None:
+    _OPTIONAL_SIGS[name] = argtypes
+
+
+def lib() -> C.CDLL:
+    """Load (once) and return the HIP kernel library; raise loudly if unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(HIP_LIB_PATH):
+            raise RuntimeError(
+                f"oni355 HIP kernels not built: {HIP_LIB_PATH} missing. Run `python tools/build.py`."
+            )
+        h = C.CDLL(HIP_LIB_PATH, mode=C.RTLD_GLOBAL)
+        for name, args in _SIGS.items():
+            fn = getattr(h, name)
+            fn.argtypes = args
+            fn.restype = C.c_int
+        for name, args in _OPTIONAL_SIGS.items():
+            if hasattr(h, name):
+                fn = getattr(h, name)
+                fn.argtypes = args
+                fn.restype = C.c_int
+        if h.oni_gibbs_sizeof_args() != C.sizeof(OniGibbs):
+            raise RuntimeError("OniGibbs ABI mismatch between Python and liboni_hip.so; rebuild")
+        _lib = h
+        return h
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with hipError {rc}")
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t) -> int | None:
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError("HIP op called with a CPU tensor")
+    if not t.is_contiguous():
+        raise ValueError("HIP op needs contiguous tensors")
+    return t.data_ptr()

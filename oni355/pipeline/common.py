@@ -1,0 +1,187 @@
+"""Source-independent stages of suspicious-connects: vocabulary, owner routing, corpus, LDA,
+scoring and top-N selection (the oni-ml pre-LDA / LDA / post-LDA skeleton).
+
+Data-parallel layout: every rank featurizes its own events; tokens are
+routed to the rank that owns their document (hash of the document key), so each rank's corpus is
+document-complete and the sampler needs only the per-sweep Δn_wk all-reduce. Word ids come from
+one global sorted vocabulary (all-gather of local unique keys, X02), so ids -- and therefore every
+sample -- are independent of the GPU count.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..models.corpus import Corpus, build_corpus
+from ..models.gibbs import GibbsConfig, GibbsLDA
+from ..parallel.comm import Comm
+
+U32MASK = 0xFFFFFFFF
+
+
+def u32_to_i64(t: torch.Tensor) -> torch.Tensor:
+    """int32 tensor holding u32 bits → non-negative int64."""
+    return t.to(torch.int64) & U32MASK
+
+
+def i64_to_u32bits(t: torch.Tensor) -> torch.Tensor:
+    return (t & U32MASK).to(torch.int64).to(torch.int32) if t.dtype == torch.int64 else t
+
+
+def global_vocab(keys64: torch.Tensor, comm: Comm | None) -> torch.Tensor:
+    """Sorted unique int64 word keys over all ranks (collective X02)."""
+    loc = torch.unique(keys64)
+    if comm is None or comm.world == 1:
+        return loc
+    parts = comm.allgather_var(loc)
+    return torch.unique(torch.cat([p.to(loc.device) for p in parts]))
+
+
+def doc_owner(doc_keys64: torch.Tensor, world: int) -> torch.Tensor:
+    """Owner rank of each document: multiplicative hash of the u32 key (spreads /24 subnets)."""
+    h = (doc_keys64 * 0x9E3779B1) & U32MASK
+    return ((h >> 16) % world).to(torch.int64)
+
+
+def route_to_owners(doc_keys64: torch.Tensor, word_ids: torch.Tensor, weights: torch.Tensor, comm: Comm | None):
+    """Send each token to its document's owner rank (alltoallv). Returns local (doc, word, weight)."""
+    if comm is None or comm.world == 1:
+        return doc_keys64, word_ids, weights
+    owner = doc_owner(doc_keys64, comm.world)
+    order = torch.argsort(owner, stable=True)
+    counts = torch.bincount(owner, minlength=comm.world)
+    packed = torch.stack([doc_keys64[order], word_ids[order].to(torch.int64), weights[order].to(torch.int64)], 1)
+    recv = comm.alltoallv(packed, counts)
+    return recv[:, 0].contiguous(), recv[:, 1].contiguous(), recv[:, 2].contiguous()
+
+
+@dataclass
+class LdaRun:
+    corpus: Corpus
+    model: GibbsLDA
+    doc_keys64: torch.Tensor  # sorted unique local doc keys (row i of θ)
+    vocab: torch.Tensor        # sorted global word keys (row i of φ)
+    timings: dict = field(default_factory=dict)
+
+
+def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor, weights: torch.Tensor | None,
+                    vocab: torch.Tensor, K: int, alpha: float | None, beta: float, seed: int, sweeps: int,
+                    chunk_len: int, comm: Comm | None, eval_every: int = 0, ckpt=None, log=None,
+                    train: bool = True) -> LdaRun:
+    """Token keys → owner routing → local corpus → Gibbs LDA trained for ``sweeps`` sweeps."""
+    t0 = time.perf_counter()
+    dev = doc_keys64.device
+    word_ids = torch.searchsorted(vocab, word_keys64)
+    if weights is None:
+        weights = torch.ones_like(word_ids)
+    dk, wi, wt = route_to_owners(doc_keys64, word_ids, weights, comm)
+    udoc, inv = torch.unique(dk, return_inverse=True)
+    G, _ = ops.choose_tiling(K)
+    use_w = bool((wt != 1).any()) if wt.numel() else False
+    corpus = build_corpus(inv, wi, int(udoc.numel()), int(vocab.numel()), i64_to_u32bits(udoc), G, chunk_len,
+                          weight=wt if use_w else None)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    model = GibbsLDA(corpus, GibbsConfig(K=K, alpha=alpha, beta=beta, seed=seed), comm=comm,
+                     V_global=int(vocab.numel()))
+    run = LdaRun(corpus, model, udoc, vocab, {"corpus_s": t1 - t0})
+    if not train:
+        return run
+    if ckpt is not None and ckpt.exists():
+        ckpt.restore(model)
+    else:
+        model.initialize()
+    t2 = time.perf_counter()
+    remaining = sweeps - model.sweeps_done
+    step = eval_every if eval_every > 0 else remaining
+    ck_every = ckpt.every if ckpt is not None and ckpt.every > 0 else 0
+    while remaining > 0:
+        n = min(step, remaining)
+        if ck_every:
+            n = min(n, ck_every - (model.sweeps_done % ck_every))
+        model.sweep(n)
+        remaining -= n
+        if eval_every > 0 and model.sweeps_done % eval_every == 0:
+            ll = model.record_likelihood()
+            if log:
+                log(f"sweep {model.sweeps_done} loglik {ll:.6e}")
+        if ck_every and model.sweeps_done % ck_every == 0:
+            ckpt.save(model)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    t3 = time.perf_counter()
+    if not model.likelihoods or model.likelihoods[-1][0] != model.sweeps_done:
+        model.record_likelihood()
+    run.timings.update({"init_s": t2 - t1, "train_s": t3 - t2, "sweeps": sweeps})
+    return run
+
+
+def gather_theta(run: LdaRun, comm: Comm | None) -> tuple[torch.Tensor, torch.Tensor]:
+    """Global (sorted doc keys, θ rows) on every rank (collective X05; local when world == 1)."""
+    th = run.model.theta()
+    keys = run.doc_keys64
+    if comm is None or comm.world == 1:
+        return keys, th
+    kp = comm.allgather_var(keys)
+    tp = comm.allgather_var(th)
+    keys = torch.cat(kp)
+    th = torch.cat(tp)
+    order = torch.argsort(keys)
+    return keys[order].contiguous(), th[order].contiguous()
+
+
+def lookup(sorted_keys: torch.Tensor, q: torch.Tensor) -> torch.Tensor:
+    idx = torch.searchsorted(sorted_keys, q)
+    idx = idx.clamp_(max=max(sorted_keys.numel() - 1, 0))
+    if sorted_keys.numel() and not bool((sorted_keys[idx] == q).all()):
+        raise KeyError("lookup key missing from dictionary")
+    return idx.to(torch.int32)
+
+
+def top_n(score: torch.Tensor, tol: float, maxresults: int, comm: Comm | None, row_offset: int = 0,
+          hist: torch.Tensor | None = None):
+    """Lowest ``maxresults`` scores below ``tol`` (ties by global row id), merged over ranks (X06).
+
+    ``hist`` is the 2048-bucket histogram of score order keys (top 11 bits) of events under tol,
+    as produced by the fused score kernel; computed here when absent. Returns (global row ids
+    int64, scores f32), ascending, identical on every rank.
+    """
+    if hist is None:
+        b = u32_to_i64(ops.f32_keys(score)) >> 21
+        hist = torch.bincount(b[score < tol], minlength=2048)
+    return _top_n_from_hist(score, hist, tol, maxresults, comm, row_offset)
+
+
+def _top_n_from_hist(score, hist, tol, maxresults, comm, row_offset):
+    h = hist.to(torch.int64).cpu().numpy()
+    if comm is not None and comm.world > 1:
+        h = comm.allreduce_np(h)
+    cum = np.cumsum(h)
+    if maxresults <= 0 or cum[-1] == 0:
+        bmax = 2047 if maxresults > 0 else -1
+    else:
+        bmax = int(np.searchsorted(cum, min(maxresults, int(cum[-1])), side="left"))
+    if bmax < 0:
+        e = torch.zeros(0, dtype=torch.int64, device=score.device)
+        return e, torch.zeros(0, dtype=torch.float32, device=score.device)
+    local_cnt = int(torch.count_nonzero(score < tol)) if score.numel() else 0
+    idx, sc = ops.select_below(score, tol, bmax, cap=max(local_cnt, 1))
+    gid = idx + row_offset
+    # exact order: (score, global id); keep local top-N then merge
+    o1 = torch.argsort(gid, stable=True)
+    gid, sc = gid[o1], sc[o1]
+    o2 = torch.argsort(sc, stable=True)
+    gid, sc = gid[o2][:maxresults], sc[o2][:maxresults]
+    if comm is not None and comm.world > 1:
+        gid = torch.cat(comm.allgather_var(gid))
+        sc = torch.cat(comm.allgather_var(sc))
+        o1 = torch.argsort(gid, stable=True)
+        gid, sc = gid[o1], sc[o1]
+        o2 = torch.argsort(sc, stable=True)
+        gid, sc = gid[o2][:maxresults], sc[o2][:maxresults]
+    return gid, sc

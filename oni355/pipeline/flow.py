@@ -1,0 +1,167 @@
+"""Netflow suspicious-connects (the `oni-ml YYYYMMDD flow` path).
+
+Stages (each a device op; see csrc/kernels):
+  K01  quantile cuts: deciles(time), deciles(ibyt), quintiles(ipkt)   (radix select, X03 in DP)
+  K03  flow word creation (port rule + bins, two word keys per flow)
+  K08/K09 vocabulary, owner routing, CSR + SELL corpus (+ feedback dupes ×DUPFACTOR)
+  K10-K12 collapsed-Gibbs sweeps (+ RCCL all-reduce of Δn_wk per sweep)
+  K13/K15/K16 θ/φ, per-flow score = min(θ_sip·φ_srcw, θ_dip·φ_dstw), top-N below TOL
+
+Reference call stack being replaced: ml_ops.sh → spark-submit SuspiciousConnects (FlowPreLDA,
+OniLDACWrapper/mpiexec lda est, FlowPostLDA) → getmerge flow_results.csv ([U-M]).
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..parallel.comm import Comm
+from ..ref import spec
+from . import common
+
+DEVICE_COLS = {"trhour": torch.int32, "trminute": torch.int32, "trsec": torch.int32, "ibyt": torch.int64,
+               "ipkt": torch.int64, "sport": torch.int32, "dport": torch.int32, "sip": torch.int32,
+               "dip": torch.int32}
+
+
+def to_device(cols: dict, device) -> dict:
+    out = {}
+    for name, dt in DEVICE_COLS.items():
+        a = np.asarray(cols[name])
+        if a.dtype == np.uint32:
+            a = a.view(np.int32)
+        out[name] = torch.from_numpy(np.ascontiguousarray(a)).to(dtype=dt).to(device)
+    return out
+
+
+@dataclass
+class FlowCuts:
+    time: np.ndarray
+    ibyt: np.ndarray
+    ipkt: np.ndarray
+
+    def as_dict(self) -> dict:
+        return {"time": [float(x) for x in spec.key_f32(self.time)], "ibyt": [int(x) for x in self.ibyt],
+                "ipkt": [int(x) for x in self.ipkt]}
+
+
+def compute_cuts(d: dict, comm: Comm | None) -> FlowCuts:
+    tk, bk, pk = ops.flow_keys(d["trhour"], d["trminute"], d["trsec"], d["ibyt"], d["ipkt"])
+    n = tk.numel()
+    ar = None
+    n_glob = n
+    if comm is not None and comm.world > 1:
+        ar = comm.allreduce_np
+        n_glob = int(comm.allreduce_np(np.array([n], dtype=np.int64))[0])
+    cuts = FlowCuts(ops.quantile_cuts(tk, spec.DECILES, ar, n_glob), ops.quantile_cuts(bk, spec.DECILES, ar, n_glob),
+                    ops.quantile_cuts(pk, spec.QUINTILES, ar, n_glob))
+    d["_keys"] = (tk, bk, pk)
+    return cuts
+
+
+def wordify(d: dict, cuts: FlowCuts) -> tuple[torch.Tensor, torch.Tensor]:
+    tk, bk, pk = d.get("_keys") or ops.flow_keys(d["trhour"], d["trminute"], d["trsec"], d["ibyt"], d["ipkt"])
+    return ops.flow_wordify(d["sport"], d["dport"], tk, bk, pk, cuts.time, cuts.ibyt, cuts.ipkt)
+
+
+@dataclass
+class FlowResult:
+    rows: np.ndarray           # global row ids, ascending score
+    scores: np.ndarray
+    src_scores: np.ndarray
+    dst_scores: np.ndarray
+    src_words: np.ndarray      # packed word keys of the result rows
+    dst_words: np.ndarray
+    cuts: FlowCuts
+    timings: dict = field(default_factory=dict)
+    stats: dict = field(default_factory=dict)
+    lda: object = None
+
+
+def feedback_tokens(fb_cols: dict | None, cuts: FlowCuts, device, dupfactor: int):
+    """sev==3 analyst rows → (doc keys, word keys, weights): each word duplicated DUPFACTOR times
+    on its IP document (the reference's "noise filter"), as a count bump."""
+    if not fb_cols or len(fb_cols.get("sip", [])) == 0:
+        return None
+    d = to_device(fb_cols, device)
+    sw, dw = wordify({k: v for k, v in d.items()}, cuts)
+    docs = torch.cat([common.u32_to_i64(d["sip"]), common.u32_to_i64(d["dip"])])
+    words = torch.cat([common.u32_to_i64(sw), common.u32_to_i64(dw)])
+    return docs, words, torch.full_like(words, int(dupfactor))
+
+
+def run_flow(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxresults: int = 3000,
+             alpha: float | None = None, beta: float = 0.01, seed: int = 0x0D15EA5E, chunk_len: int = 256,
+             device="cpu", comm: Comm | None = None, feedback: dict | None = None, dupfactor: int = 1000,
+             row_offset: int = 0, eval_every: int = 0, ckpt=None, log=None) -> FlowResult:
+    """Full suspicious-connects for one (rank-local shard of a) day of flows."""
+    t = {}
+    t0 = time.perf_counter()
+    d = to_device(cols, device)
+    sync = (lambda: torch.cuda.synchronize(device)) if torch.device(device).type == "cuda" else (lambda: None)
+    sync()
+    t["h2d_s"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    cuts = compute_cuts(d, comm)
+    sw, dw = wordify(d, cuts)
+    sync()
+    t["featurize_s"] = time.perf_counter() - t0
+
+    t0 = time.perf_counter()
+    doc_keys = torch.cat([common.u32_to_i64(d["sip"]), common.u32_to_i64(d["dip"])])
+    word_keys = torch.cat([common.u32_to_i64(sw), common.u32_to_i64(dw)])
+    weights = None
+    fb = feedback_tokens(feedback, cuts, device, dupfactor)
+    if fb is not None:
+        weights = torch.cat([torch.ones_like(word_keys), fb[2]])
+        doc_keys = torch.cat([doc_keys, fb[0]])
+        word_keys = torch.cat([word_keys, fb[1]])
+    vocab = common.global_vocab(word_keys, comm)
+    sync()
+    t["vocab_s"] = time.perf_counter() - t0
+    run = common.build_and_train(doc_keys, word_keys, weights, vocab, K, alpha, beta, seed, sweeps, chunk_len, comm,
+                                 eval_every=eval_every, ckpt=ckpt, log=log)
+    t.update(run.timings)
+
+    # ---- scoring --------------------------------------------------------------------------------
+    t0 = time.perf_counter()
+    dkeys, theta = common.gather_theta(run, comm)
+    phi = run.model.phi()
+    n = d["sip"].numel()
+    sdoc = common.lookup(dkeys, common.u32_to_i64(d["sip"]))
+    ddoc = common.lookup(dkeys, common.u32_to_i64(d["dip"]))
+    swid = common.lookup(vocab, common.u32_to_i64(sw))
+    dwid = common.lookup(vocab, common.u32_to_i64(dw))
+    sync()
+    t["score_prep_s"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    hist = torch.zeros(2048, dtype=torch.int32, device=theta.device)
+    score, s1, s2 = ops.score(theta, phi, sdoc, swid, ddoc, dwid, tol=tol, want_parts=True, hist=hist)
+    rows, scs = common.top_n(score, tol, maxresults, comm, row_offset, hist=hist)
+    sync()
+    t["score_s"] = time.perf_counter() - t0
+    t["records_scored"] = n
+    # per-result parts (rows are global ids; each rank contributes its own rows)
+    loc = rows - row_offset
+    mine = (loc >= 0) & (loc < n)
+    li = loc[mine]
+    parts = torch.stack([s1[li], s2[li]], 1) if s1 is not None else torch.zeros(0, 2)
+    wparts = torch.stack([sw[li], dw[li]], 1)
+    if comm is not None and comm.world > 1:
+        gid_all = torch.cat(comm.allgather_var(rows[mine]))
+        parts = torch.cat(comm.allgather_var(parts))
+        wparts = torch.cat(comm.allgather_var(wparts))
+        pos = {int(g): i for i, g in enumerate(gid_all.tolist())}
+        order = torch.tensor([pos[int(g)] for g in rows.tolist()], dtype=torch.int64)
+        parts = parts.cpu()[order]
+        wparts = wparts.cpu()[order]
+    stats = run.corpus.stats()
+    stats.update({"n_flows": n, "loglik": run.model.likelihoods[-1][1] if run.model.likelihoods else None})
+    return FlowResult(rows=rows.cpu().numpy(), scores=scs.cpu().numpy(), src_scores=parts[:, 0].cpu().numpy(),
+                      dst_scores=parts[:, 1].cpu().numpy(), src_words=wparts[:, 0].cpu().numpy().view(np.uint32),
+                      dst_words=wparts[:, 1].cpu().numpy().view(np.uint32), cuts=cuts, timings=t, stats=stats,
+                      lda=run)

@@ -1,0 +1,319 @@
+"""NumPy specification oracle for every hand-written kernel (tests + the CPU path).
+
+Each function here is the executable spec of one HIP kernel in ``csrc/kernels`` and is written so
+that, on identical inputs, it reproduces the kernel **bit-for-bit**: same f32 operation order, no
+fused multiply-add (the kernels are built with ``-ffp-contract=off``), same Philox stream.
+
+Behaviour spec sources (the reference has no readable source):
+* flow words: SURVEY.md §2.8 (oni-ml FlowWordCreation, [U-M]);
+* quantile cuts: SURVEY.md §2.2 C15 (Quantiles.computeDeciles/Quintiles, [U-M]) with the rank
+  rule pinned here as ``rank = ceil(num*N/den) - 1`` on the ascending sort;
+* scoring: SURVEY.md §2.2 C24 (FlowPostLDA, [U-H]);
+* sampler: collapsed Gibbs (replaces oni-lda-c VEM) with the chunked, snapshot
+  semantics documented in csrc/kernels/gibbs.hip.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+U32 = np.uint32
+U64 = np.uint64
+F32 = np.float32
+MASK32 = U64(0xFFFFFFFF)
+PAD_WORD = U32(0xFFFFFFFF)
+
+DECILES = [(i, 10) for i in range(1, 10)]
+QUINTILES = [(i, 5) for i in range(1, 5)]
+
+PORT_111111 = 65536
+PORT_333333 = 65537
+
+
+# ------------------------------------------------------------------------------------------------
+# Philox4x32-10
+# ------------------------------------------------------------------------------------------------
+def philox10(c0, c1, c2, c3, k0, k1):
+    c0, c1, c2, c3 = (np.asarray(x, dtype=U32) for x in (c0, c1, c2, c3))
+    c0, c1, c2, c3 = np.broadcast_arrays(c0, c1, c2, c3)
+    c0, c1, c2, c3 = (x.copy() for x in (c0, c1, c2, c3))
+    k0 = U32(k0)
+    k1 = U32(k1)
+    for _ in range(10):
+        p0 = c0.astype(U64) * U64(0xD2511F53)
+        p1 = c2.astype(U64) * U64(0xCD9E8D57)
+        hi0, lo0 = (p0 >> U64(32)).astype(U32), (p0 & MASK32).astype(U32)
+        hi1, lo1 = (p1 >> U64(32)).astype(U32), (p1 & MASK32).astype(U32)
+        c0, c1, c2, c3 = hi1 ^ c1 ^ k0, lo1, hi0 ^ c3 ^ k1, lo0
+        k0 = U32((int(k0) + 0x9E3779B9) & 0xFFFFFFFF)
+        k1 = U32((int(k1) + 0xBB67AE85) & 0xFFFFFFFF)
+    return c0, c1, c2, c3
+
+
+def token_rand(pos, key, sweep, stream, seed0, seed1):
+    """The u32 draw of token (doc key, pos) in (sweep, stream): mirrors the kernel's pick4."""
+    pos = np.asarray(pos, dtype=U32)
+    r = philox10(pos >> U32(2), key, U32(sweep), U32(stream), seed0, seed1)
+    sel = pos & U32(3)
+    return np.select([sel == 0, sel == 1, sel == 2], [r[0], r[1], r[2]], r[3]).astype(U32)
+
+
+def u01(r):
+    return (np.asarray(r, dtype=U32) >> U32(8)).astype(F32) * F32(5.9604644775390625e-08)
+
+
+def split_seed(seed: int) -> tuple[int, int]:
+    seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    return seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
+
+
+# ------------------------------------------------------------------------------------------------
+# keys / quantiles / bins (K01, K02)
+# ------------------------------------------------------------------------------------------------
+def f32_key(x):
+    u = np.asarray(x, dtype=F32).view(U32)
+    neg = (u & U32(0x80000000)) != 0
+    return np.where(neg, ~u, u | U32(0x80000000)).astype(U32)
+
+
+def key_f32(k):
+    k = np.asarray(k, dtype=U32)
+    neg = (k & U32(0x80000000)) == 0
+    return np.where(neg, ~k, k & U32(0x7FFFFFFF)).astype(U32).view(F32)
+
+
+def i64_keys(x):
+    x = np.asarray(x, dtype=np.int64)
+    return np.clip(x, 0, 0xFFFFFFFF).astype(U32)
+
+
+def quantile_ranks(n: int, fracs) -> np.ndarray:
+    """0-based ascending ranks of the cut points: ceil(num*n/den) - 1 (clamped to [0, n-1])."""
+    r = np.array([(num * n + den - 1) // den - 1 for num, den in fracs], dtype=np.int64)
+    return np.clip(r, 0, max(n - 1, 0))
+
+
+def quantile_cuts(keys, fracs) -> np.ndarray:
+    keys = np.asarray(keys, dtype=U32)
+    if keys.size == 0:
+        return np.zeros(len(fracs), dtype=U32)
+    ranks = quantile_ranks(keys.size, fracs)
+    part = np.partition(keys, np.unique(ranks))
+    return part[ranks].astype(U32)
+
+
+def bin_keys(keys, cuts):
+    keys = np.asarray(keys, dtype=U32)
+    cuts = np.asarray(cuts, dtype=U32)
+    return (keys[:, None] > cuts[None, :]).sum(axis=1).astype(np.uint8)
+
+
+# ------------------------------------------------------------------------------------------------
+# flow word creation (K03)
+# ------------------------------------------------------------------------------------------------
+def flow_time(hour, minute, second):
+    h = np.asarray(hour).astype(F32)
+    m = np.asarray(minute).astype(F32)
+    s = np.asarray(second).astype(F32)
+    return (h + m / F32(60.0)) + s / F32(3600.0)
+
+
+def flow_keys(hour, minute, second, ibyt, ipkt):
+    return f32_key(flow_time(hour, minute, second)), i64_keys(ibyt), i64_keys(ipkt)
+
+
+def flow_port_rule(sport, dport):
+    """Returns (port_code, src_dir, dst_dir) per SURVEY.md §2.8 table (first matching row wins)."""
+    sp = np.asarray(sport, dtype=np.int64)
+    dp = np.asarray(dport, dtype=np.int64)
+    conds = [
+        (sp == 0) & (dp == 0),
+        (dp == 0) & (sp > 0),
+        (sp == 0) & (dp > 0),
+        (sp <= 1024) & (dp <= 1024),
+        (sp <= 1024) & (dp > 1024),
+        (sp > 1024) & (dp <= 1024),
+    ]
+    port = np.select(conds, [0, sp, dp, PORT_111111, sp, dp], PORT_333333).astype(np.int64)
+    sdir = np.select(conds, [0, 1, 0, 0, 1, 0], 0).astype(np.int64)
+    ddir = np.select(conds, [0, 0, 1, 0, 0, 1], 0).astype(np.int64)
+    return port, sdir, ddir
+
+
+def flow_wordify(sport, dport, tkey, bkey, pkey, tcuts, bcuts, pcuts):
+    tb = bin_keys(tkey, tcuts).astype(np.int64)
+    bb = bin_keys(bkey, bcuts).astype(np.int64)
+    pb = bin_keys(pkey, pcuts).astype(np.int64)
+    port, sdir, ddir = flow_port_rule(sport, dport)
+    base = (port << 11) | (tb << 7) | (bb << 3) | pb
+    return (base | (sdir << 28)).astype(U32), (base | (ddir << 28)).astype(U32)
+
+
+def flow_word_fields(word):
+    w = np.asarray(word, dtype=np.int64)
+    return (w >> 28) & 1, (w >> 11) & 0x1FFFF, (w >> 7) & 0xF, (w >> 3) & 0xF, w & 0x7
+
+
+def flow_word_str(word: int) -> str:
+    d, port, tb, bb, pb = (int(x) for x in flow_word_fields(np.array([word]))[:])
+    p = {PORT_111111: "111111", PORT_333333: "333333"}.get(port, str(port))
+    return f"{'-1_' if d else ''}{p}_{tb}_{bb}_{pb}"
+
+
+def flow_word_from_str(s: str) -> int:
+    d = s.startswith("-1_")
+    if d:
+        s = s[3:]
+    p, tb, bb, pb = s.split("_")
+    port = {"111111": PORT_111111, "333333": PORT_333333}.get(p, None)
+    port = int(p) if port is None else port
+    return (int(d) << 28) | (port << 11) | (int(tb) << 7) | (int(bb) << 3) | int(pb)
+
+
+# ------------------------------------------------------------------------------------------------
+# SELL fill (K09 second half)
+# ------------------------------------------------------------------------------------------------
+def sell_fill(chunk_doc, chunk_pos0, chunk_len, S, slice_off, doc_pair_ptr, pair_tokoff, pair_word, pair_cnt,
+              tok_word):
+    chunk_doc = np.asarray(chunk_doc)
+    for i in np.nonzero(chunk_doc >= 0)[0]:
+        d = int(chunk_doc[i])
+        lo, hi = int(doc_pair_ptr[d]), int(doc_pair_ptr[d + 1])
+        off = int(slice_off[i // S]) + i % S
+        pos0, ln = int(chunk_pos0[i]), int(chunk_len[i])
+        # expand this doc's pairs into token words, then take [pos0, pos0+len)
+        words = np.repeat(np.asarray(pair_word[lo:hi]), np.asarray(pair_cnt[lo:hi]))
+        tok_word[off + np.arange(ln) * S] = words[pos0:pos0 + ln].astype(U32)
+    return tok_word
+
+
+# ------------------------------------------------------------------------------------------------
+# collapsed Gibbs: init / sweep / apply (K10-K12)
+# ------------------------------------------------------------------------------------------------
+def _chunk_geometry(st, S):
+    n_slices = st["slice_len"].shape[0]
+    C = n_slices * S
+    cid = np.arange(C)
+    return cid // S, cid % S
+
+
+def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed0: int, seed1: int, init: bool,
+               sweep: int, chunk_len: np.ndarray):
+    """One init (init=True) or sweep pass over numpy state arrays, in place.
+
+    st keys: tok_word u32, tok_z u8, slice_off i64, slice_len i32, chunk_doc i32, chunk_pos0 i32,
+    chunk_key u32, chunk_multi u8, ndk_src i32 [D,KS], ndk_dst i32 [D,KS], q f32 [V,KS],
+    dnwk i32 [V,KS], dnk i32 [KS].
+    """
+    S = 64 // G
+    KS = G * KP
+    slc, lane = _chunk_geometry(st, S)
+    doc = st["chunk_doc"]
+    live = doc >= 0
+    C = doc.shape[0]
+    n = np.zeros((C, KS), dtype=np.int32)
+    if not init:
+        n[live] = st["ndk_src"][doc[live]]
+    n_start = n.copy()
+    clen = np.where(live, chunk_len, 0)
+    alpha32 = F32(alpha)
+    stream = 0 if init else 1
+    sw = 0 if init else sweep
+    for s in range(int(clen.max(initial=0))):
+        act = np.nonzero(clen > s)[0]
+        idx = st["slice_off"][slc[act]] + s * S + lane[act]
+        w = st["tok_word"][idx].astype(np.int64)
+        pos = st["chunk_pos0"][act].astype(U32) + U32(s)
+        rr = token_rand(pos, st["chunk_key"][act], sw, stream, seed0, seed1)
+        if init:
+            z = ((rr.astype(U64) * U64(K)) >> U64(32)).astype(np.int64)
+            n[act, z] += 1
+            st["tok_z"][idx] = z.astype(np.uint8)
+            np.add.at(st["dnwk"], (w, z), 1)
+            continue
+        zo = st["tok_z"][idx].astype(np.int64)
+        n[act, zo] -= 1
+        qv = st["q"][w]
+        p = (n[act].astype(F32) + alpha32) * qv
+        if G == 1:
+            cum = np.cumsum(p, axis=1, dtype=F32)
+            total = cum[:, -1]
+        else:
+            pg = p.reshape(-1, G, KP)
+            loc = np.cumsum(pg, axis=2, dtype=F32)
+            incl = loc[:, :, -1].copy()
+            d = 1
+            while d < G:
+                prev = incl.copy()
+                incl[:, d:] = prev[:, d:] + prev[:, :-d]
+                d <<= 1
+            excl = np.zeros_like(incl)
+            excl[:, 1:] = incl[:, :-1]
+            cum = (excl[:, :, None] + loc).reshape(-1, KS)
+            total = incl[:, -1]
+        thr = u01(rr) * total
+        cnt = (cum <= thr[:, None]).sum(axis=1)
+        zn = np.minimum(cnt, K - 1).astype(np.int64)
+        n[act, zn] += 1
+        ch = zn != zo
+        st["tok_z"][idx[ch]] = zn[ch].astype(np.uint8)
+        np.add.at(st["dnwk"], (w[ch], zo[ch]), -1)
+        np.add.at(st["dnwk"], (w[ch], zn[ch]), 1)
+    d = n - n_start
+    multi = live & (st["chunk_multi"] != 0)
+    single = live & ~multi
+    st["ndk_dst"][doc[single]] = n[single]
+    np.add.at(st["ndk_dst"], doc[multi], d[multi])
+    st["dnk"] += d[live].sum(axis=0).astype(np.int32)
+
+
+def gibbs_apply(nwk, dcur, dnk_cur, nk_cur, K, beta, vbeta):
+    """Returns (nwk', nk', q) exactly as k_apply computes them."""
+    nwk = nwk + dcur
+    nk = nk_cur + dnk_cur
+    den = nk.astype(F32) + F32(vbeta)
+    q = (nwk.astype(F32) + F32(beta)) / den[None, :]
+    q[:, K:] = 0
+    return nwk, nk, q.astype(F32)
+
+
+# ------------------------------------------------------------------------------------------------
+# scoring (K15)
+# ------------------------------------------------------------------------------------------------
+def dot_rows(theta_rows, phi_rows):
+    s = np.zeros(theta_rows.shape[0], dtype=F32)
+    for k in range(theta_rows.shape[1]):
+        s = s + theta_rows[:, k] * phi_rows[:, k]
+    return s
+
+
+def score(theta, phi, d1, w1, d2=None, w2=None):
+    s1 = dot_rows(theta[d1], phi[w1])
+    if d2 is None:
+        return s1, s1, None
+    s2 = dot_rows(theta[d2], phi[w2])
+    return np.minimum(s1, s2).astype(F32), s1, s2
+
+
+# ------------------------------------------------------------------------------------------------
+# slow textbook collapsed Gibbs (statistical cross-check only; not bitwise)
+# ------------------------------------------------------------------------------------------------
+def textbook_cgs(docs: list[np.ndarray], V: int, K: int, alpha: float, beta: float, sweeps: int, seed: int):
+    rng = np.random.default_rng(seed)
+    z = [rng.integers(0, K, size=len(d)) for d in docs]
+    ndk = np.zeros((len(docs), K))
+    nwk = np.zeros((V, K))
+    for d, (ws, zs) in enumerate(zip(docs, z)):
+        for w, t in zip(ws, zs):
+            ndk[d, t] += 1
+            nwk[w, t] += 1
+    nk = nwk.sum(0)
+    for _ in range(sweeps):
+        for d, ws in enumerate(docs):
+            for i, w in enumerate(ws):
+                t = z[d][i]
+                ndk[d, t] -= 1; nwk[w, t] -= 1; nk[t] -= 1
+                p = (ndk[d] + alpha) * (nwk[w] + beta) / (nk + V * beta)
+                t = rng.choice(K, p=p / p.sum())
+                z[d][i] = t
+                ndk[d, t] += 1; nwk[w, t] += 1; nk[t] += 1
+    return z, ndk, nwk

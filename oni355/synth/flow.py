@@ -1,0 +1,183 @@
+"""Seeded synthetic netflow day with random-init topic priors and planted anomalies.
+
+The reference shipped no data generator (it relied on real nfcapd sensors and the oni-demo
+dataset); the north star asks for synthetic netflow "of the named shape
+with random-init topic priors" (BASELINE.json). Generative model:
+
+* ``n_profiles`` behaviour profiles (web browsing, DNS, mail, SSH admin, backups, P2P, ...), each a
+  distribution over service port, hour of day, bytes and packets;
+* every internal host (a document) has a profile mix θ* ~ Dir(alpha_true) (sparse);
+* host activity is Zipf-distributed (a few hosts own most flows: NAT gateways, resolvers);
+* each flow: profile z ~ θ*[src], server from the profile's pool, port/hour/bytes/packets from z;
+* ``n_anomalies`` planted flows with off-profile behaviour (rare service port at an odd hour with
+  outsized volume) -- ground truth for "planted anomalies rank in the top-N" tests.
+
+Columns follow the flow schema of SURVEY.md §2.7 (nfdump CSV → Hive ``flow`` table).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+# (name, service ports, port weights, server-side?, peak hour, hour sd, log-bytes mu, sd, bytes/pkt)
+_PROFILES = [
+    ("web", [80, 443, 8080], [0.3, 0.65, 0.05], 10, 3.0, 8.5, 1.2, 700),
+    ("dns", [53], [1.0], 12, 6.0, 5.0, 0.4, 90),
+    ("mail", [25, 587, 993, 143], [0.4, 0.3, 0.2, 0.1], 9, 2.5, 9.5, 1.5, 900),
+    ("ssh", [22], [1.0], 14, 3.0, 7.5, 1.8, 120),
+    ("backup", [873, 445], [0.5, 0.5], 2, 1.0, 15.0, 1.0, 1400),
+    ("p2p", [6881, 51413], [0.5, 0.5], 21, 2.0, 11.0, 2.0, 1100),
+    ("ntp", [123], [1.0], 12, 7.0, 4.4, 0.1, 76),
+    ("ldap", [389, 636, 88], [0.4, 0.3, 0.3], 8, 2.0, 7.0, 0.8, 300),
+    ("db", [3306, 5432, 1433], [0.4, 0.4, 0.2], 11, 4.0, 10.0, 1.5, 1000),
+    ("rdp", [3389], [1.0], 15, 2.5, 12.0, 1.2, 800),
+    ("snmp", [161, 162], [0.8, 0.2], 12, 7.0, 5.5, 0.3, 150),
+    ("smb", [445, 139], [0.8, 0.2], 13, 3.0, 10.5, 1.5, 1200),
+    ("https-api", [443], [1.0], 3, 2.0, 6.5, 0.6, 400),
+    ("video", [443, 1935], [0.7, 0.3], 20, 2.0, 16.0, 1.0, 1400),
+    ("syslog", [514], [1.0], 12, 7.0, 6.0, 0.5, 200),
+    ("proxy", [3128, 8080], [0.6, 0.4], 11, 3.0, 9.0, 1.3, 800),
+    ("vpn", [500, 4500], [0.5, 0.5], 7, 2.0, 11.0, 1.5, 1000),
+    ("dhcp", [67, 68], [0.5, 0.5], 8, 3.0, 5.8, 0.2, 330),
+    ("ftp", [21, 20], [0.5, 0.5], 16, 2.0, 12.5, 1.5, 1400),
+    ("monitoring", [9100, 5666], [0.5, 0.5], 12, 7.0, 7.2, 0.4, 500),
+]
+
+_ANOMALY_PORTS = [23, 69, 79, 111, 119, 135, 513]
+
+
+@dataclass
+class FlowDay:
+    cols: dict            # column name -> numpy array (flow schema)
+    theta_true: np.ndarray  # [n_hosts, n_profiles]
+    host_ips: np.ndarray  # uint32 [n_hosts]
+    anomaly_rows: np.ndarray  # int64 row ids of planted anomalies
+
+    @property
+    def n(self) -> int:
+        return int(self.cols["sip"].shape[0])
+
+
+def _ip(a, b, c, d):
+    return (np.uint32(a) << np.uint32(24)) | (np.uint32(b) << np.uint32(16)) | (np.uint32(c) << np.uint32(8)) | np.uint32(d)
+
+
+def ip_to_str(ip: int) -> str:
+    ip = int(ip) & 0xFFFFFFFF
+    return f"{ip >> 24}.{(ip >> 16) & 255}.{(ip >> 8) & 255}.{ip & 255}"
+
+
+def str_to_ip(s: str) -> int:
+    a, b, c, d = (int(x) for x in s.strip().split("."))
+    return (a << 24) | (b << 16) | (c << 8) | d
+
+
+def generate_flows(n: int, seed: int = 7, n_hosts: int | None = None, n_profiles: int = 20,
+                   alpha_true: float = 0.08, zipf_a: float = 1.15, n_anomalies: int | None = None,
+                   date=(2016, 7, 8), rank: int = 0) -> FlowDay:
+    """Generate ``n`` flows. ``rank`` offsets the RNG stream (weak-scaling shards of one day)."""
+    rng = np.random.default_rng([seed, rank])
+    n_profiles = min(n_profiles, len(_PROFILES))
+    prof = _PROFILES[:n_profiles]
+    if n_hosts is None:
+        n_hosts = max(64, n // 25)
+    if n_anomalies is None:
+        n_anomalies = max(5, min(200, n // 50_000))
+    # hosts: 10.x.y.z (shared across ranks: same hosts appear in every shard)
+    hrng = np.random.default_rng([seed, 0xABCD])
+    hid = np.arange(n_hosts, dtype=np.int64)
+    host_ips = _ip(10, (hid >> 16) & 255, (hid >> 8) & 255, hid & 255).astype(np.uint32)
+    theta = hrng.dirichlet(np.full(n_profiles, alpha_true), size=n_hosts)
+    # servers per profile: 172.16.<p>.<i>
+    n_srv = max(4, min(250, n_hosts // 20))
+    # host activity: Zipf over a random permutation of hosts
+    w = 1.0 / np.power(np.arange(1, n_hosts + 1, dtype=np.float64), zipf_a)
+    w = w[hrng.permutation(n_hosts)]
+    w /= w.sum()
+    src = rng.choice(n_hosts, size=n, p=w)
+    # profile per flow: inverse-CDF on flattened cumulative rows
+    cum = np.cumsum(theta, axis=1)
+    cum[:, -1] = 1.0
+    u = rng.random(n)
+    flat = (cum + np.arange(n_hosts)[:, None]).ravel()
+    z = np.searchsorted(flat, src + u, side="right") - src * n_profiles
+    z = np.clip(z, 0, n_profiles - 1)
+
+    port_of = np.zeros(n, dtype=np.int64)
+    hour_f = np.zeros(n)
+    lbytes = np.zeros(n)
+    bpp = np.zeros(n)
+    for k, (_, ports, pw, peak, hsd, mu, sd, bp) in enumerate(prof):
+        m = z == k
+        cnt = int(m.sum())
+        if not cnt:
+            continue
+        port_of[m] = rng.choice(ports, size=cnt, p=np.asarray(pw) / np.sum(pw))
+        hour_f[m] = rng.normal(peak, hsd, size=cnt)
+        lbytes[m] = rng.normal(mu, sd, size=cnt)
+        bpp[m] = bp * np.exp(rng.normal(0, 0.2, size=cnt))
+    srv = rng.integers(0, n_srv, size=n)
+    dip = _ip(172, 16, z & 255, srv & 255).astype(np.uint32)
+    sip = host_ips[src]
+    eph = rng.integers(1025, 65536, size=n)
+    # ~15% of flows are recorded from the server side (service port in sport)
+    flip = rng.random(n) < 0.15
+    sport = np.where(flip, port_of, eph)
+    dport = np.where(flip, eph, port_of)
+    sip2 = np.where(flip, dip, sip)
+    dip2 = np.where(flip, sip, dip)
+
+    hour = np.mod(np.floor(hour_f), 24).astype(np.int64)
+    minute = rng.integers(0, 60, size=n)
+    second = rng.integers(0, 60, size=n)
+    ibyt = np.maximum(40, np.exp(lbytes)).astype(np.int64)
+    ipkt = np.maximum(1, np.round(ibyt / np.maximum(bpp, 40))).astype(np.int64)
+
+    # planted anomalies: off-profile rare service, odd hour, huge volume, from low-activity hosts
+    anomaly_rows = np.sort(rng.choice(n, size=min(n_anomalies, n), replace=False))
+    na = anomaly_rows.size
+    if na:
+        quiet = np.argsort(w)[: max(1, n_hosts // 10)]
+        a_src = quiet[rng.integers(0, quiet.size, size=na)]
+        sip2[anomaly_rows] = host_ips[a_src]
+        dip2[anomaly_rows] = _ip(203, 0, 113, rng.integers(1, 255, size=na) & 255)
+        sport[anomaly_rows] = rng.integers(1025, 65536, size=na)
+        dport[anomaly_rows] = rng.choice(_ANOMALY_PORTS, size=na)
+        hour[anomaly_rows] = rng.choice([3, 4], size=na)
+        ibyt[anomaly_rows] = rng.integers(500_000_000, 900_000_000, size=na)
+        ipkt[anomaly_rows] = rng.integers(1, 3, size=na)
+
+    y, mo, d = date
+    unix = (np.int64(1467936000) + hour * 3600 + minute * 60 + second).astype(np.int64)
+    cols = {
+        "treceived": unix,
+        "unix_tstamp": unix,
+        "tryear": np.full(n, y, dtype=np.int32),
+        "trmonth": np.full(n, mo, dtype=np.int32),
+        "trday": np.full(n, d, dtype=np.int32),
+        "trhour": hour.astype(np.int32),
+        "trminute": minute.astype(np.int32),
+        "trsec": second.astype(np.int32),
+        "tdur": np.round(rng.exponential(2.0, size=n), 3).astype(np.float32),
+        "sip": sip2.astype(np.uint32),
+        "dip": dip2.astype(np.uint32),
+        "sport": sport.astype(np.int32),
+        "dport": dport.astype(np.int32),
+        "proto": np.where(np.isin(port_of, [53, 123, 161, 162, 67, 68, 69, 514, 500, 4500]), 17, 6).astype(np.int32),
+        "flag": np.zeros(n, dtype=np.int32),
+        "fwd": np.zeros(n, dtype=np.int32),
+        "stos": np.zeros(n, dtype=np.int32),
+        "ipkt": ipkt,
+        "ibyt": ibyt,
+        "opkt": np.zeros(n, dtype=np.int64),
+        "obyt": np.zeros(n, dtype=np.int64),
+        "input": np.zeros(n, dtype=np.int32),
+        "output": np.zeros(n, dtype=np.int32),
+        "sas": np.zeros(n, dtype=np.int32),
+        "das": np.zeros(n, dtype=np.int32),
+        "dtos": np.zeros(n, dtype=np.int32),
+        "dir": np.zeros(n, dtype=np.int32),
+        "rip": np.zeros(n, dtype=np.uint32),
+    }
+    return FlowDay(cols=cols, theta_true=theta, host_ips=host_ips, anomaly_rows=anomaly_rows)

@@ -1,0 +1,151 @@
+"""HIP kernels vs the NumPy specification oracle (bitwise where the spec is exact)."""
+import numpy as np
+import pytest
+import torch
+
+from oni355 import ops
+from oni355.models.corpus import build_corpus
+from oni355.models.gibbs import GibbsConfig, GibbsLDA
+from oni355.ref import spec
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand_flows(n, seed):
+    r = np.random.default_rng(seed)
+    return dict(
+        hour=r.integers(0, 24, n).astype(np.int32), minute=r.integers(0, 60, n).astype(np.int32),
+        second=r.integers(0, 60, n).astype(np.int32),
+        ibyt=np.where(r.random(n) < 0.3, 1500, r.integers(0, 10**10, n)).astype(np.int64),
+        ipkt=r.integers(0, 5000, n).astype(np.int64),
+        sport=np.where(r.random(n) < 0.1, 0, r.integers(0, 65536, n)).astype(np.int32),
+        dport=np.where(r.random(n) < 0.1, 0, r.integers(0, 2048, n)).astype(np.int32))
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 100_003])
+def test_flow_keys_and_words(gpu, n):
+    f = _rand_flows(n, n)
+    T = {k: torch.from_numpy(v) for k, v in f.items()}
+    G = {k: v.to(gpu) for k, v in T.items()}
+    kc = ops.flow_keys(T["hour"], T["minute"], T["second"], T["ibyt"], T["ipkt"])
+    kg = ops.flow_keys(G["hour"], G["minute"], G["second"], G["ibyt"], G["ipkt"])
+    for a, b in zip(kc, kg):
+        assert torch.equal(a, b.cpu())
+    cuts = [np.sort(np.random.default_rng(1).integers(0, 2**32, m, dtype=np.uint64).astype(np.uint32)) for m in (9, 9, 4)]
+    wc = ops.flow_wordify(T["sport"], T["dport"], *kc, *cuts)
+    wg = ops.flow_wordify(G["sport"], G["dport"], *kg, *cuts)
+    for a, b in zip(wc, wg):
+        assert torch.equal(a, b.cpu())
+
+
+@pytest.mark.parametrize("n", [1, 7, 1000, 1_000_003])
+def test_quantile_cuts_exact(gpu, n):
+    r = np.random.default_rng(n)
+    x = np.concatenate([r.normal(size=n // 2).astype(np.float32), np.full(n - n // 2, 3.25, np.float32)])
+    keys = torch.from_numpy(spec.f32_key(x).view(np.int32)).to(gpu)
+    for fr in (spec.DECILES, spec.QUINTILES):
+        got = ops.quantile_cuts(keys, fr)
+        want = spec.quantile_cuts(spec.f32_key(x), fr)
+        assert np.array_equal(got, want)
+
+
+def _toy_tokens(n_docs, V, seed, heavy=True):
+    r = np.random.default_rng(seed)
+    lens = r.zipf(1.6, n_docs).clip(1, 3000)
+    if heavy:
+        lens[0] = 5000  # forces a multi-chunk doc
+    tdoc = np.repeat(np.arange(n_docs), lens)
+    tword = (r.zipf(1.3, tdoc.size) - 1) % V
+    keys = r.permutation(2**31 - 1)[:n_docs].astype(np.int32)
+    return torch.from_numpy(tdoc), torch.from_numpy(tword), keys
+
+
+@pytest.mark.parametrize("K", [20, 7, 50, 100])
+def test_gibbs_bitwise_vs_oracle(gpu, K):
+    tdoc, tword, keys = _toy_tokens(300, 400, K)
+    G, KP = ops.choose_tiling(K)
+    cc = build_corpus(tdoc, tword, 300, 400, torch.from_numpy(keys), G, L=64)
+    cg = build_corpus(tdoc.to(gpu), tword.to(gpu), 300, 400, torch.from_numpy(keys).to(gpu), G, L=64)
+    assert torch.equal(cc.tok_word, cg.tok_word.cpu())
+    assert torch.equal(cc.chunk_doc, cg.chunk_doc.cpu())
+    cfg = GibbsConfig(K=K, seed=1234, use_graph=False)
+    mc, mg = GibbsLDA(cc, cfg), GibbsLDA(cg, cfg)
+    mc.initialize()
+    mg.initialize()
+    assert torch.equal(mc.tok_z, mg.tok_z.cpu())
+    assert torch.equal(mc.nwk, mg.nwk.cpu())
+    assert torch.equal(mc.q, mg.q.cpu())
+    for _ in range(3):
+        mc.sweep(1)
+        mg.sweep(1)
+        assert torch.equal(mc.tok_z, mg.tok_z.cpu())
+        assert torch.equal(mc.ndk_cur, mg.ndk_cur.cpu())
+        assert torch.equal(mc.nwk, mg.nwk.cpu())
+        assert torch.equal(mc.nk_cur, mg.nk_cur.cpu())
+        assert torch.equal(mc.q, mg.q.cpu())
+    # invariants
+    T = cg.T
+    assert int(mg.nwk[:, :K].sum()) == T == int(mg.ndk_cur[:, :K].sum()) == int(mg.nk_cur[:K].sum())
+    assert int(mg.nwk.min()) >= 0 and int(mg.ndk_cur.min()) >= 0
+
+
+def test_graph_replay_matches_eager(gpu):
+    tdoc, tword, keys = _toy_tokens(500, 300, 5)
+    c = build_corpus(tdoc.to(gpu), tword.to(gpu), 500, 300, torch.from_numpy(keys).to(gpu), 1, L=128)
+    a = GibbsLDA(c, GibbsConfig(K=20, seed=9, use_graph=False))
+    b = GibbsLDA(c, GibbsConfig(K=20, seed=9, use_graph=True))
+    a.initialize()
+    a.sweep(7)
+    b.initialize()
+    b.sweep(7)
+    assert b._graph is not None
+    assert torch.equal(a.tok_z, b.tok_z) and torch.equal(a.nwk, b.nwk) and torch.equal(a.ndk_cur, b.ndk_cur)
+
+
+def test_resume_bitwise(gpu):
+    tdoc, tword, keys = _toy_tokens(200, 100, 11)
+    c = build_corpus(tdoc.to(gpu), tword.to(gpu), 200, 100, torch.from_numpy(keys).to(gpu), 1, L=64)
+    a = GibbsLDA(c, GibbsConfig(K=20, seed=3))
+    a.initialize()
+    a.sweep(6)
+    b = GibbsLDA(c, GibbsConfig(K=20, seed=3))
+    b.initialize()
+    b.sweep(2)
+    z = b.canonical_z().cpu()
+    r = GibbsLDA(c, GibbsConfig(K=20, seed=3))
+    r.load_canonical_z(z, 2)
+    r.sweep(4)
+    assert torch.equal(a.canonical_z(), r.canonical_z())
+    assert torch.equal(a.nwk, r.nwk)
+
+
+@pytest.mark.parametrize("KS", [20, 64])
+def test_score_and_select(gpu, KS):
+    r = np.random.default_rng(KS)
+    D, V, n = 1000, 700, 50_001
+    th = r.random((D, KS)).astype(np.float32) / KS
+    ph = (r.random((V, KS)) ** 8).astype(np.float32)
+    d1, d2 = r.integers(0, D, n).astype(np.int32), r.integers(0, D, n).astype(np.int32)
+    w1, w2 = r.integers(0, V, n).astype(np.int32), r.integers(0, V, n).astype(np.int32)
+    want, s1, s2 = spec.score(th, ph, d1, w1, d2, w2)
+    t = lambda a: torch.from_numpy(a).to(gpu)  # noqa: E731
+    hist = torch.zeros(2048, dtype=torch.int32, device=gpu)
+    got, g1, g2 = ops.score(t(th), t(ph), t(d1), t(w1), t(d2), t(w2), tol=0.5, want_parts=True, hist=hist)
+    assert np.array_equal(got.cpu().numpy(), want)
+    assert np.array_equal(g1.cpu().numpy(), s1) and np.array_equal(g2.cpu().numpy(), s2)
+    b = spec.f32_key(want[want < 0.5]) >> np.uint32(21)
+    assert np.array_equal(hist.cpu().numpy(), np.bincount(b, minlength=2048))
+    idx, sc = ops.select_below(got, 0.5, 1000, cap=n)
+    m = (want < 0.5) & ((spec.f32_key(want) >> np.uint32(21)) <= 1000)
+    assert np.array_equal(np.sort(idx.cpu().numpy()), np.nonzero(m)[0])
+
+
+def test_flow_pipeline_gpu_matches_cpu(gpu):
+    from oni355.pipeline.flow import run_flow
+    from oni355.synth.flow import generate_flows
+    day = generate_flows(20_000, seed=5)
+    rc = run_flow(day.cols, K=20, sweeps=6, maxresults=200, device="cpu")
+    rg = run_flow(day.cols, K=20, sweeps=6, maxresults=200, device=gpu)
+    assert np.array_equal(rc.rows, rg.rows)
+    assert np.array_equal(rc.scores, rg.scores)
+    assert rc.stats["loglik"] == pytest.approx(rg.stats["loglik"], rel=1e-12)
