@@ -98,28 +98,31 @@ def quantile_cuts(keys: torch.Tensor, fracs, allreduce=None, n_global: int | Non
     """
     _need(keys, torch.int32, "keys")
     n = keys.numel() if n_global is None else int(n_global)
-    if not _is_dev(keys):
-        if allreduce is not None:
-            raise NotImplementedError("distributed quantiles need device keys")
+    dev = _is_dev(keys)
+    if not dev and allreduce is None:
         return spec.quantile_cuts(_u32np(keys), fracs)
     if n == 0:
         return np.zeros(len(fracs), dtype=np.uint32)
-    L = _lib.lib()
+    L = _lib.lib() if dev else None
+    knp = None if dev else _u32np(keys)
     ranks = spec.quantile_ranks(n, fracs).astype(np.int64)
     prefix = np.zeros(len(fracs), dtype=np.uint64)
-    hist_buf = torch.zeros(16 << 11, dtype=torch.int32, device=keys.device)
+    hist_buf = torch.zeros(16 << 11, dtype=torch.int32, device=keys.device) if dev else None
     for shift, nbits in _PASSES:
         top = shift + nbits
         mask = 0 if top >= 32 else (0xFFFFFFFF << top) & 0xFFFFFFFF
         uniq, inv = np.unique(prefix, return_inverse=True)
         P = len(uniq)
         B = 1 << nbits
-        pre_t = torch.from_numpy(uniq.astype(np.uint32).view(np.int32)).to(keys.device)
-        hist = hist_buf[: P * B]
-        hist.zero_()
-        _lib.check(L.oni_radix_hist(_lib.ptr(keys), keys.numel(), shift, nbits, _lib.ptr(pre_t), P, mask,
-                                    _lib.ptr(hist), _lib.stream()), "oni_radix_hist")
-        h = hist.cpu().numpy().view(np.uint32).astype(np.int64).reshape(P, B)
+        if dev:
+            pre_t = torch.from_numpy(uniq.astype(np.uint32).view(np.int32)).to(keys.device)
+            hist = hist_buf[: P * B]
+            hist.zero_()
+            _lib.check(L.oni_radix_hist(_lib.ptr(keys), keys.numel(), shift, nbits, _lib.ptr(pre_t), P, mask,
+                                        _lib.ptr(hist), _lib.stream()), "oni_radix_hist")
+            h = hist.cpu().numpy().view(np.uint32).astype(np.int64).reshape(P, B)
+        else:
+            h = spec.radix_hist(knp, shift, nbits, uniq.astype(np.uint32), mask)
         if allreduce is not None:
             h = np.asarray(allreduce(h), dtype=np.int64).reshape(P, B)
         cum = np.cumsum(h, axis=1)

@@ -101,6 +101,18 @@ def quantile_cuts(keys, fracs) -> np.ndarray:
     return part[ranks].astype(U32)
 
 
+def radix_hist(keys, shift: int, nbits: int, prefixes, mask: int) -> np.ndarray:
+    """k_radix_hist: per live prefix, histogram of digit (key >> shift) & (2^nbits-1)."""
+    keys = np.asarray(keys, dtype=U32)
+    B = 1 << nbits
+    hi = keys & U32(mask)
+    digit = ((keys >> U32(shift)) & U32(B - 1)).astype(np.int64)
+    out = np.zeros((len(prefixes), B), dtype=np.int64)
+    for i, p in enumerate(prefixes):
+        out[i] = np.bincount(digit[hi == U32(p)], minlength=B)
+    return out
+
+
 def bin_keys(keys, cuts):
     keys = np.asarray(keys, dtype=U32)
     cuts = np.asarray(cuts, dtype=U32)
@@ -154,7 +166,8 @@ def flow_word_fields(word):
 
 
 def flow_word_str(word: int) -> str:
-    d, port, tb, bb, pb = (int(x) for x in flow_word_fields(np.array([word]))[:])
+    w = int(word)
+    d, port, tb, bb, pb = (w >> 28) & 1, (w >> 11) & 0x1FFFF, (w >> 7) & 0xF, (w >> 3) & 0xF, w & 0x7
     p = {PORT_111111: "111111", PORT_333333: "333333"}.get(port, str(port))
     return f"{'-1_' if d else ''}{p}_{tb}_{bb}_{pb}"
 

@@ -1,0 +1,164 @@
+"""Day-partitioned columnar store (replaces the reference's HDFS + Hive/Parquet tables partitioned
+by y/m/d/h).
+
+Layout::
+
+    <root>/<source>/<YYYYMMDD>/_schema.json        {"rows": N, "columns": {name: kind}, ...}
+    <root>/<source>/<YYYYMMDD>/<col>.npy           numeric column (np.save, no pickle)
+    <root>/<source>/<YYYYMMDD>/<col>.off.npy       string column: int64 offsets [N+1]
+    <root>/<source>/<YYYYMMDD>/<col>.chars.bin     string column: UTF-8 bytes
+
+Numeric columns are memory-mapped on read, so a rank of a data-parallel job touches only its own
+row range; strings stay as offsets+bytes (the GPU string kernels' native layout). Appends
+(ingest) go to numbered parts ``part-XXXXX/`` that readers concatenate.
+"""
+from __future__ import annotations
+
+import glob
+import json
+import os
+
+import numpy as np
+
+
+class StringColumn:
+    """Offsets + bytes view of N strings."""
+
+    def __init__(self, offsets: np.ndarray, chars: np.ndarray):
+        self.offsets = np.asarray(offsets, dtype=np.int64)
+        self.chars = np.asarray(chars, dtype=np.uint8)
+
+    @classmethod
+    def from_list(cls, items) -> "StringColumn":
+        enc = [s.encode("utf-8") if isinstance(s, str) else bytes(s) for s in items]
+        off = np.zeros(len(enc) + 1, dtype=np.int64)
+        if enc:
+            off[1:] = np.cumsum([len(e) for e in enc])
+        return cls(off, np.frombuffer(b"".join(enc), dtype=np.uint8).copy())
+
+    def __len__(self) -> int:
+        return self.offsets.size - 1
+
+    def __getitem__(self, i):
+        if isinstance(i, (int, np.integer)):
+            return bytes(self.chars[self.offsets[i]:self.offsets[i + 1]]).decode("utf-8", "replace")
+        idx = np.arange(len(self))[i] if isinstance(i, slice) else np.asarray(i)
+        return StringColumn.from_list([self[int(j)] for j in idx])
+
+    def slice(self, lo: int, hi: int) -> "StringColumn":
+        o = self.offsets[lo:hi + 1]
+        return StringColumn(o - o[0], self.chars[o[0]:o[-1]])
+
+    def to_list(self) -> list[str]:
+        return [self[i] for i in range(len(self))]
+
+    @staticmethod
+    def concat(parts: list["StringColumn"]) -> "StringColumn":
+        if not parts:
+            return StringColumn(np.zeros(1, np.int64), np.zeros(0, np.uint8))
+        offs, base = [np.zeros(1, np.int64)], 0
+        for p in parts:
+            offs.append(p.offsets[1:] + base)
+            base += int(p.offsets[-1])
+        return StringColumn(np.concatenate(offs), np.concatenate([p.chars for p in parts]))
+
+
+def day_dir(root: str, source: str, date: str) -> str:
+    return os.path.join(root, source, date)
+
+
+def _write_part(d: str, cols: dict) -> int:
+    os.makedirs(d, exist_ok=True)
+    n = None
+    kinds = {}
+    for name, v in cols.items():
+        if isinstance(v, StringColumn) or (isinstance(v, (list, tuple)) and (not v or isinstance(v[0], str))):
+            sc = v if isinstance(v, StringColumn) else StringColumn.from_list(v)
+            np.save(os.path.join(d, f"{name}.off.npy"), sc.offsets, allow_pickle=False)
+            sc.chars.tofile(os.path.join(d, f"{name}.chars.bin"))
+            kinds[name] = "string"
+            m = len(sc)
+        else:
+            a = np.asarray(v)
+            np.save(os.path.join(d, f"{name}.npy"), a, allow_pickle=False)
+            kinds[name] = str(a.dtype)
+            m = a.shape[0]
+        if n is not None and m != n:
+            raise ValueError(f"column {name} has {m} rows, expected {n}")
+        n = m
+    meta = {"rows": int(n or 0), "columns": kinds}
+    with open(os.path.join(d, "_schema.json.tmp"), "w") as f:
+        json.dump(meta, f)
+    os.replace(os.path.join(d, "_schema.json.tmp"), os.path.join(d, "_schema.json"))
+    return int(n or 0)
+
+
+def write_day(root: str, source: str, date: str, cols: dict) -> str:
+    """Replace the day's table with ``cols`` (idempotent rerun, like ``hdfs dfs -rm`` + load)."""
+    d = day_dir(root, source, date)
+    if os.path.isdir(d):
+        for p in glob.glob(os.path.join(d, "**", "*"), recursive=True):
+            if os.path.isfile(p):
+                os.remove(p)
+    _write_part(d, cols)
+    return d
+
+
+def append_part(root: str, source: str, date: str, cols: dict) -> str:
+    """Append one ingested file's rows as a new part (used by the ingest workers)."""
+    d = day_dir(root, source, date)
+    os.makedirs(d, exist_ok=True)
+    existing = sorted(glob.glob(os.path.join(d, "part-*")))
+    nxt = 0 if not existing else int(os.path.basename(existing[-1])[5:]) + 1
+    p = os.path.join(d, f"part-{nxt:05d}")
+    _write_part(p + ".tmp", cols)
+    os.replace(p + ".tmp", p)
+    return p
+
+
+def _parts(d: str) -> list[str]:
+    parts = []
+    if os.path.exists(os.path.join(d, "_schema.json")):
+        parts.append(d)
+    parts += sorted(p for p in glob.glob(os.path.join(d, "part-*")) if not p.endswith(".tmp"))
+    return parts
+
+
+def rows(root: str, source: str, date: str) -> int:
+    total = 0
+    for p in _parts(day_dir(root, source, date)):
+        with open(os.path.join(p, "_schema.json")) as f:
+            total += json.load(f)["rows"]
+    return total
+
+
+def read_day(root: str, source: str, date: str, columns=None, row_range: tuple[int, int] | None = None) -> dict:
+    d = day_dir(root, source, date)
+    parts = _parts(d)
+    if not parts:
+        raise FileNotFoundError(f"no {source} data for {date} under {root}")
+    out: dict[str, list] = {}
+    base = 0
+    lo, hi = row_range if row_range else (0, None)
+    for p in parts:
+        with open(os.path.join(p, "_schema.json")) as f:
+            meta = json.load(f)
+        n = meta["rows"]
+        plo, phi_ = max(lo - base, 0), n if hi is None else min(hi - base, n)
+        base += n
+        if phi_ <= plo:
+            continue
+        for name, kind in meta["columns"].items():
+            if columns is not None and name not in columns:
+                continue
+            if kind == "string":
+                off = np.load(os.path.join(p, f"{name}.off.npy"), allow_pickle=False)
+                chars = np.fromfile(os.path.join(p, f"{name}.chars.bin"), dtype=np.uint8)
+                out.setdefault(name, []).append(StringColumn(off, chars).slice(plo, phi_))
+            else:
+                a = np.load(os.path.join(p, f"{name}.npy"), mmap_mode="r", allow_pickle=False)
+                out.setdefault(name, []).append(np.array(a[plo:phi_]))
+    res = {}
+    for k, v in out.items():
+        res[k] = StringColumn.concat(v) if isinstance(v[0], StringColumn) else np.concatenate(v)
+    return res

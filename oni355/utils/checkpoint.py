@@ -1,0 +1,115 @@
+"""Checkpoint / resume for the Gibbs sampler.
+
+A checkpoint is the topic assignment of every token (1 byte each) grouped by document key, plus
+the sweep counter and the run's identity (K, α, β, seed, V, T). Every count table is recomputed
+from z on restore, and the counter RNG makes the resumed chain bitwise identical to an
+uninterrupted one. Shards are keyed by document, so a run may resume on a different GPU count
+(documents are re-routed to their new owners).
+
+Layout: ``<dir>/ckpt_s<sweep>_r<rank>of<world>.pt`` (+ ``manifest.json`` written by rank 0 after
+all shards of a sweep are on disk; atomic renames throughout). lda-c-style ``NNN.*`` snapshots
+are emitted separately by :mod:`oni355.io.ldac`.
+"""
+from __future__ import annotations
+
+import glob
+import json
+import os
+
+import torch
+
+
+class Checkpointer:
+    def __init__(self, directory: str, every: int = 0, comm=None, keep: int = 2):
+        self.dir = directory
+        self.every = int(every)
+        self.comm = comm
+        self.keep = keep
+        os.makedirs(directory, exist_ok=True)
+
+    @property
+    def rank(self) -> int:
+        return self.comm.rank if self.comm else 0
+
+    @property
+    def world(self) -> int:
+        return self.comm.world if self.comm else 1
+
+    def _ident(self, model) -> dict:
+        return {"K": model.K, "alpha": model.alpha, "beta": model.beta, "seed": int(model.cfg.seed), "V": model.V}
+
+    def manifest(self) -> dict | None:
+        p = os.path.join(self.dir, "manifest.json")
+        if not os.path.exists(p):
+            return None
+        with open(p) as f:
+            return json.load(f)
+
+    def exists(self) -> bool:
+        return self.manifest() is not None
+
+    def save(self, model) -> str:
+        c = model.c
+        z = model.canonical_z().cpu()
+        payload = {
+            "ident": self._ident(model),
+            "sweep": int(model.sweeps_done),
+            "doc_keys": c.doc_keys.cpu(),
+            "doc_tok_ptr": c.doc_tok_ptr.cpu(),
+            "z": z,
+            "likelihoods": list(model.likelihoods),
+        }
+        name = f"ckpt_s{model.sweeps_done}_r{self.rank}of{self.world}.pt"
+        path = os.path.join(self.dir, name)
+        torch.save(payload, path + ".tmp")
+        os.replace(path + ".tmp", path)
+        if self.comm is not None:
+            self.comm.barrier()
+        if self.rank == 0:
+            man = {"sweep": int(model.sweeps_done), "world": self.world, "ident": self._ident(model)}
+            mp = os.path.join(self.dir, "manifest.json")
+            with open(mp + ".tmp", "w") as f:
+                json.dump(man, f)
+            os.replace(mp + ".tmp", mp)
+            self._gc(model.sweeps_done)
+        if self.comm is not None:
+            self.comm.barrier()
+        return path
+
+    def _gc(self, latest: int) -> None:
+        sweeps = sorted({int(os.path.basename(p).split("_")[1][1:]) for p in glob.glob(os.path.join(self.dir, "ckpt_s*"))})
+        for s in sweeps[: max(0, len(sweeps) - self.keep)]:
+            if s == latest:
+                continue
+            for p in glob.glob(os.path.join(self.dir, f"ckpt_s{s}_r*")):
+                os.remove(p)
+
+    def restore(self, model) -> int:
+        man = self.manifest()
+        if man is None:
+            raise FileNotFoundError(f"no checkpoint manifest in {self.dir}")
+        if man["ident"] != self._ident(model):
+            raise ValueError(f"checkpoint identity {man['ident']} != run {self._ident(model)}")
+        sweep = int(man["sweep"])
+        by_key: dict[int, torch.Tensor] = {}
+        for p in sorted(glob.glob(os.path.join(self.dir, f"ckpt_s{sweep}_r*of{man['world']}.pt"))):
+            d = torch.load(p, weights_only=True)
+            keys = d["doc_keys"].tolist()
+            ptr = d["doc_tok_ptr"]
+            z = d["z"]
+            for i, k in enumerate(keys):
+                by_key[k] = z[int(ptr[i]): int(ptr[i + 1])]
+            if "likelihoods" in d and not model.likelihoods:
+                model.likelihoods = [tuple(x) for x in d["likelihoods"]]
+        c = model.c
+        parts = []
+        ptr = c.doc_tok_ptr.cpu()
+        for i, k in enumerate(c.doc_keys.cpu().tolist()):
+            zz = by_key.get(k)
+            n = int(ptr[i + 1] - ptr[i])
+            if zz is None or zz.numel() != n:
+                raise ValueError(f"checkpoint does not match corpus (doc key {k & 0xFFFFFFFF})")
+            parts.append(zz)
+        z = torch.cat(parts) if parts else torch.zeros(0, dtype=torch.uint8)
+        model.load_canonical_z(z, sweep)
+        return sweep

@@ -1,0 +1,150 @@
+"""Pure-CPU tests of the behaviour spec: word rules, bins, quantiles, config, file formats."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oni355 import config, ops
+from oni355.io import ldac
+from oni355.ref import spec
+
+
+# --- flow port rule: every row of SURVEY.md §2.8 --------------------------------------------------
+@pytest.mark.parametrize("sport,dport,port,sdir,ddir", [
+    (0, 0, 0, 0, 0),
+    (0, 80, 80, 0, 1),          # sport=0, dport>0 -> dport, dst gets -1_
+    (443, 0, 443, 1, 0),        # dport=0, sport>0 -> sport, src gets -1_
+    (22, 80, spec.PORT_111111, 0, 0),
+    (1024, 1024, spec.PORT_111111, 0, 0),
+    (80, 51000, 80, 1, 0),      # sport <= 1024 < dport -> sport, src gets -1_
+    (51000, 443, 443, 0, 1),    # dport <= 1024 < sport -> dport, dst gets -1_
+    (1025, 1025, spec.PORT_333333, 0, 0),
+    (6881, 51413, spec.PORT_333333, 0, 0),
+])
+def test_port_rule_table(sport, dport, port, sdir, ddir):
+    p, s, d = spec.flow_port_rule(np.array([sport]), np.array([dport]))
+    assert (p[0], s[0], d[0]) == (port, sdir, ddir)
+
+
+def test_word_render_roundtrip():
+    words = spec.flow_wordify(np.array([80, 0, 6000, 22]), np.array([51000, 0, 7000, 25]),
+                              spec.f32_key(np.array([1.0, 2.0, 3.0, 23.9], np.float32)),
+                              np.array([10, 20, 30, 10**9], np.uint32), np.array([1, 2, 3, 4], np.uint32),
+                              spec.f32_key(np.arange(9, dtype=np.float32) * 2.5),
+                              np.array([5, 15, 25, 35, 45, 55, 65, 75, 85], np.uint32),
+                              np.array([1, 2, 3, 4], np.uint32))
+    strs = [spec.flow_word_str(int(w)) for w in np.concatenate(words)]
+    assert strs[0] == "-1_80_1_1_0"  # src of (80 -> 51000): -1_ prefix
+    assert strs[4] == "80_1_1_0"
+    assert strs[1] == "0_1_2_1" and strs[5] == "0_1_2_1"
+    assert strs[2].startswith("333333_") and strs[3].startswith("111111_")
+    for w, s in zip(np.concatenate(words), strs):
+        assert spec.flow_word_from_str(s) == int(w)
+
+
+def test_bin_semantics():
+    cuts = np.array([10, 20, 30], np.uint32)
+    assert list(spec.bin_keys(np.array([0, 10, 11, 20, 21, 30, 31], np.uint32), cuts)) == [0, 0, 1, 1, 2, 2, 3]
+
+
+@pytest.mark.parametrize("n", [1, 2, 9, 10, 11, 1001])
+def test_quantile_ranks_and_cuts(n):
+    x = np.random.default_rng(n).permutation(n).astype(np.uint32)
+    cuts = spec.quantile_cuts(x, spec.DECILES)
+    s = np.sort(x)
+    for (num, den), c in zip(spec.DECILES, cuts):
+        r = -(-num * n // den) - 1
+        assert c == s[max(r, 0)]
+    # radix-select path (used on device and for DP) agrees with the sort path
+    k = torch.from_numpy(x.view(np.int32))
+    assert np.array_equal(ops.quantile_cuts(k, spec.DECILES, allreduce=lambda h: h), cuts)
+
+
+def test_f32_key_order():
+    x = np.array([-np.inf, -3.5, -0.0, 0.0, 1e-30, 2.0, np.inf], np.float32)
+    k = spec.f32_key(x)
+    assert np.all(np.diff(k.astype(np.int64)) >= 0)
+    assert np.array_equal(spec.key_f32(k), x)
+
+
+def test_philox_known_answer():
+    # Random123 Philox4x32-10 known-answer vector (counter 0, key 0)
+    r = spec.philox10(0, 0, 0, 0, 0, 0)
+    assert [int(v) for v in r] == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+
+
+# --- config ------------------------------------------------------------------------------------------
+def test_duxbay_parsing(tmp_path):
+    p = tmp_path / "duxbay.conf"
+    p.write_text('# comment\nUSER_DOMAIN="intel"\nTOPIC_COUNT=50\nLUSER=/home/oni\nLPATH=${LUSER}/ml\n'
+                 "DUPFACTOR=500\nTOL=1e-6\nMAXRESULTS=1000\nNODES=(node1 node2)\n")
+    cfg = config.load_config(str(p), env={"ONI_SWEEPS": "33"}, MAXRESULTS=77)
+    assert cfg.USER_DOMAIN == "intel" and cfg.TOPIC_COUNT == 50 and cfg.DUPFACTOR == 500
+    assert cfg.LPATH == "/home/oni/ml" and cfg.TOL == 1e-6 and cfg.SWEEPS == 33 and cfg.MAXRESULTS == 77
+    assert cfg.extra["LUSER"] == "/home/oni"
+
+
+def test_lda_settings():
+    s = config.parse_lda_settings("var max iter 20\nvar convergence 1e-6\nem max iter 150\nem convergence 1e-4\n"
+                                  "alpha fixed\nsweeps 300\nbeta 0.05\n")
+    assert s["em_max_iter"] == 150 and not s["estimate_alpha"] and s["sweeps"] == 300 and s["beta"] == 0.05
+
+
+# --- lda-c formats -------------------------------------------------------------------------------
+def test_ldac_roundtrip(tmp_path):
+    pd = np.array([0, 0, 1, 2, 2, 2])
+    pw = np.array([3, 7, 1, 0, 5, 9])
+    pc = np.array([2, 1, 4, 1, 1, 3])
+    f = tmp_path / "model.dat"
+    ldac.write_corpus(str(f), pd, pw, pc, 4)
+    docs = ldac.read_corpus(str(f))
+    assert len(docs) == 4 and list(docs[0][0]) == [3, 7] and list(docs[2][1]) == [1, 1, 3] and docs[3][0].size == 0
+    lb = np.log(np.random.default_rng(0).dirichlet(np.ones(10), 3))
+    g = np.random.default_rng(1).random((4, 3))
+    ldac.write_model(str(tmp_path), "final", lb, g, 0.7)
+    assert np.allclose(ldac.read_matrix(str(tmp_path / "final.beta")), lb, atol=1e-9)
+    assert ldac.read_other(str(tmp_path / "final.other")) == {"num_topics": 3, "num_terms": 10, "alpha": 0.7}
+
+
+def test_vem_recovers_topics():
+    from oni355.models import vem
+    r = np.random.default_rng(0)
+    V, K = 60, 3
+    phi = np.zeros((K, V))
+    for k in range(K):
+        phi[k, k * 20:(k + 1) * 20] = 1 / 20
+    ptr, ws, cs = [0], [], []
+    for d in range(150):
+        k = d % K
+        w = r.choice(V, 40, p=phi[k])
+        u, c = np.unique(w, return_counts=True)
+        ws += list(u)
+        cs += list(c)
+        ptr.append(len(ws))
+    res = vem.estimate(np.array(ptr), np.array(ws), np.array(cs), V, K, alpha=0.5, em_max_iter=50, threads=2)
+    th = res.theta()
+    # every document is (nearly) pure in one topic and documents of one true class share it
+    top = th.argmax(1)
+    for k in range(K):
+        assert len(set(top[k::K])) == 1
+    assert th.max(1).mean() > 0.9
+    assert np.all(np.diff(res.likelihood[1:]) > -1e-6 * np.abs(res.likelihood[1:-1]).max())
+
+
+def test_lda_cli(tmp_path):
+    import subprocess
+
+    from oni355.ops import native
+    ldac.write_corpus(str(tmp_path / "model.dat"), np.repeat(np.arange(30), 2), np.tile([0, 1], 30) + np.repeat(np.arange(30) % 2 * 2, 2),
+                      np.full(60, 3), 30)
+    (tmp_path / "settings.txt").write_text("var max iter 10\nvar convergence 1e-5\nem max iter 20\nem convergence 1e-4\nalpha estimate\n")
+    out = tmp_path / "out"
+    subprocess.run([native.binary("lda"), "est", "2.5", "2", str(tmp_path / "settings.txt"), "2",
+                    str(tmp_path / "model.dat"), "seeded", str(out)], check=True, capture_output=True)
+    assert (out / "final.beta").exists() and (out / "final.gamma").exists() and (out / "word-assignments.dat").exists()
+    subprocess.run([native.binary("lda"), "inf", str(tmp_path / "settings.txt"), str(out / "final"),
+                    str(tmp_path / "model.dat"), str(tmp_path / "inf")], check=True, capture_output=True)
+    g = ldac.read_matrix(str(tmp_path / "inf-gamma.dat"))
+    assert g.shape == (30, 2)
+    assert os.path.exists(str(tmp_path / "inf-lda-lhood.dat"))
