@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of sampler count modes on one corpus (cdna guide §5.4 rule 24: one process,
+N variants × M rounds). Prints per-variant median/min ms per sweep + per-stage event timings.
+
+  python bench/gibbs_ab.py --flows 12500000 --rounds 5 --sweeps 20
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--flows", type=int, default=12_500_000)
+    ap.add_argument("--topics", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--sweeps", type=int, default=20)
+    ap.add_argument("--burn", type=int, default=30)
+    ap.add_argument("--modes", default="atomic,recount")
+    ap.add_argument("--chunk-len", type=int, default=256)
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+
+    from oni355 import ops
+    from oni355.models.gibbs import GibbsConfig, GibbsLDA
+    from oni355.pipeline import common, flow
+    from oni355.synth.flow import generate_flows
+
+    dev = torch.device("cuda:0")
+    day = generate_flows(a.flows, seed=7, n_hosts=max(64, a.flows // 25))
+    d = flow.to_device(day.cols, dev)
+    cuts = flow.compute_cuts(d, None)
+    sw, dw = flow.wordify(d, cuts)
+    dk = torch.cat([common.u32_to_i64(d["sip"]), common.u32_to_i64(d["dip"])])
+    wk = torch.cat([common.u32_to_i64(sw), common.u32_to_i64(dw)])
+    vocab = common.global_vocab(wk, None)
+    run = common.build_and_train(dk, wk, None, vocab, a.topics, None, 0.01, 0x0D15EA5E, 0, a.chunk_len, None,
+                                 train=False)
+    c = run.corpus
+    print(json.dumps({"corpus": c.stats()}), flush=True)
+    modes = a.modes.split(",")
+    models = {m: GibbsLDA(c, GibbsConfig(K=a.topics, count_mode=m)) for m in modes}
+    for m in models.values():
+        m.initialize()
+        m.sweep(a.burn)
+    torch.cuda.synchronize()
+    # change rate at this point of the chain
+    m0 = models[modes[0]]
+    z0 = m0.tok_z.clone()
+    m0.sweep(1)
+    torch.cuda.synchronize()
+    changed = float((m0.tok_z != z0).sum()) / c.T
+    res = {m: [] for m in modes}
+    for _ in range(a.rounds):
+        for name, m in models.items():
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            m.sweep(a.sweeps)
+            torch.cuda.synchronize()
+            res[name].append((time.perf_counter() - t0) / a.sweeps * 1e3)
+    out = {"changed_frac": changed, "T": c.T}
+    for name, v in res.items():
+        out[name] = {"median_ms": float(np.median(v)), "min_ms": float(np.min(v))}
+    # per-stage timing (eager, events) for each mode
+    for name, m in models.items():
+        st = {}
+        for stage in range(3):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ts = []
+            for _ in range(5):
+                atomic = m.cfg.count_mode == "atomic"
+                ev[0].record()
+                if stage == 0:
+                    ops.gibbs_pass(m._state(False), m.G, m.KP, m.K, m.alpha, m.cfg.seed, False, m.sweep_ctr,
+                                   c.chunk_len, atomic=atomic)
+                elif stage == 1 and not atomic:
+                    ops.recount(c.wsorted, c.wslot, m.tok_z, m.dn[m.b][: m.V * m.KS].view(m.V, m.KS), m.KS)
+                elif stage == 2:
+                    ops.gibbs_apply(m.nwk, m.dn[m.b], m.dn[1 - m.b], m.nk[m.cn], m.nk[1 - m.cn], m.q, m.V, m.K, m.KS,
+                                    m.beta, m.vbeta, m.sweep_ctr, bump=False, absolute=not atomic)
+                ev[1].record()
+                torch.cuda.synchronize()
+                ts.append(ev[0].elapsed_time(ev[1]))
+            st[["sample", "recount", "apply"][stage]] = float(np.median(ts))
+        out[name]["stages_ms"] = st
+    print(json.dumps(out), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

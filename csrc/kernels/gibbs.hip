@@ -67,7 +67,7 @@ __device__ __forceinline__ void load_row_f(const float* __restrict__ p, float (&
   }
 }
 
-template <int G, int KP, bool INIT>
+template <int G, int KP, bool INIT, bool ATOMIC>
 __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
   constexpr int S = oni::kWave / G;
   constexpr int KS = G * KP;
@@ -102,9 +102,18 @@ __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
 #pragma unroll
   for (int j = 0; j < KP; ++j) qv[j] = 0.f;
 
+  // software-pipelined token stream: step s+1's word/topic loads are issued before step s's
+  // sampling, so their latency hides behind the math and stores of step s
+  uint32_t w_nx = len > 0 ? a.tok_word[off + c] : oni::kPadWord;
+  int z_nx = (!INIT && len > 0) ? (int)a.tok_z[off + c] : 0;
   for (int s = 0; s < len; ++s) {
     const int64_t idx = off + (int64_t)s * S + c;
-    const uint32_t w = a.tok_word[idx];
+    const uint32_t w = w_nx;
+    const int zo = z_nx;
+    if (s + 1 < len) {
+      w_nx = a.tok_word[idx + S];
+      if (!INIT) z_nx = a.tok_z[idx + S];
+    }
     if (w == oni::kPadWord) continue;  // uniform across the G lanes of a unit
     const uint32_t pos = pos0 + (uint32_t)s;
     if (s == 0 || (pos & 3u) == 0u) r = oni::philox10(oni::U4{pos >> 2, key, sweep, stream}, a.seed0, a.seed1);
@@ -115,10 +124,9 @@ __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
       for (int j = 0; j < KP; ++j) n[j] += (kbase + j == z);
       if (g == 0) {
         a.tok_z[idx] = (uint8_t)z;
-        atomicAdd(&a.dnwk[(int64_t)w * KS + z], 1);
+        if (ATOMIC) atomicAdd(&a.dnwk[(int64_t)w * KS + z], 1);
       }
     } else {
-      const int zo = a.tok_z[idx];
 #pragma unroll
       for (int j = 0; j < KP; ++j) n[j] -= (kbase + j == zo);
       if (w != wprev) {
@@ -157,8 +165,10 @@ __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
       for (int j = 0; j < KP; ++j) n[j] += (kbase + j == zn);
       if (zn != zo && g == 0) {
         a.tok_z[idx] = (uint8_t)zn;
-        atomicAdd(&a.dnwk[(int64_t)w * KS + zo], -1);
-        atomicAdd(&a.dnwk[(int64_t)w * KS + zn], 1);
+        if (ATOMIC) {
+          atomicAdd(&a.dnwk[(int64_t)w * KS + zo], -1);
+          atomicAdd(&a.dnwk[(int64_t)w * KS + zn], 1);
+        }
       }
     }
   }
@@ -215,7 +225,7 @@ __global__ __launch_bounds__(256) void k_apply(int32_t* __restrict__ nwk, const 
                                                 int32_t* __restrict__ dother, const int32_t* __restrict__ nk_cur,
                                                 int32_t* __restrict__ nk_next, float* __restrict__ q, int64_t V,
                                                 int K, int KS, float beta, float vbeta, uint32_t* sweep_ctr,
-                                                int bump) {
+                                                int bump, int absolute) {
   __shared__ float den[256];
   __shared__ int32_t nkn[256];
   const int32_t* dnk_cur = dcur + V * KS;
@@ -236,8 +246,11 @@ __global__ __launch_bounds__(256) void k_apply(int32_t* __restrict__ nwk, const 
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
     const int4 dv = reinterpret_cast<const int4*>(dcur)[i];
-    int4 nv = reinterpret_cast<int4*>(nwk)[i];
-    nv.x += dv.x; nv.y += dv.y; nv.z += dv.z; nv.w += dv.w;
+    int4 nv = dv;
+    if (!absolute) {
+      nv = reinterpret_cast<int4*>(nwk)[i];
+      nv.x += dv.x; nv.y += dv.y; nv.z += dv.z; nv.w += dv.w;
+    }
     reinterpret_cast<int4*>(nwk)[i] = nv;
     reinterpret_cast<int4*>(dother)[i] = make_int4(0, 0, 0, 0);
     const int k0 = (int)((i * 4) % KS);
@@ -262,24 +275,59 @@ __global__ void k_copy_rows(const int32_t* __restrict__ src, int32_t* __restrict
 }
 
 template <int G, int KP>
-int launch_gibbs(const OniGibbs& a, bool init, hipStream_t s) {
+int launch_gibbs(const OniGibbs& a, bool init, bool atomic, hipStream_t s) {
   if (a.KS != G * KP) return (int)hipErrorInvalidValue;
   const unsigned grid = (unsigned)((a.n_slices + kWavesPerBlock - 1) / kWavesPerBlock);
   if (grid == 0) return 0;
-  if (init)
-    k_gibbs<G, KP, true><<<grid, kBlock, 0, s>>>(a);
-  else
-    k_gibbs<G, KP, false><<<grid, kBlock, 0, s>>>(a);
+  if (init) {
+    if (atomic) k_gibbs<G, KP, true, true><<<grid, kBlock, 0, s>>>(a);
+    else k_gibbs<G, KP, true, false><<<grid, kBlock, 0, s>>>(a);
+  } else {
+    if (atomic) k_gibbs<G, KP, false, true><<<grid, kBlock, 0, s>>>(a);
+    else k_gibbs<G, KP, false, false><<<grid, kBlock, 0, s>>>(a);
+  }
   return (int)hipGetLastError();
+}
+
+// K11 (option B of SURVEY.md §7.4.3): rebuild the local n_wk table from z with NO global
+// per-token atomics. Tokens are visited in word-sorted order (wsorted/wslot built once with the
+// corpus); each block owns a contiguous run of them, histograms (word, topic) in LDS (rows = the
+// block's word span, capped at wmax; the tail of a very wide span goes straight to global), and
+// flushes one row-contiguous atomic per non-zero (word, topic) cell. The topic gather z[wslot]
+// reads 1 byte per token from the (L2/MALL-resident) SELL topic array.
+__global__ __launch_bounds__(256) void k_recount(const int32_t* __restrict__ wsorted, const int32_t* __restrict__ wslot,
+                                                  const uint8_t* __restrict__ tok_z, int64_t T, int32_t* __restrict__ nwk,
+                                                  int KS, int tile, int wmax) {
+  extern __shared__ __attribute__((aligned(16))) int32_t hst[];
+  const int64_t lo = (int64_t)blockIdx.x * tile;
+  if (lo >= T) return;
+  const int64_t hi = lo + tile < T ? lo + tile : T;
+  const int w_lo = wsorted[lo], w_hi = wsorted[hi - 1];
+  const int rows = (w_hi - w_lo + 1) < wmax ? (w_hi - w_lo + 1) : wmax;
+  const int cells = rows * KS;
+  for (int i = threadIdx.x; i < cells; i += blockDim.x) hst[i] = 0;
+  __syncthreads();
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const int w = wsorted[i];
+    const int z = tok_z[wslot[i]];
+    const int r = w - w_lo;
+    if (r < rows) atomicAdd(&hst[r * KS + z], 1);
+    else atomicAdd(&nwk[(int64_t)w * KS + z], 1);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < cells; i += blockDim.x) {
+    const int v = hst[i];
+    if (v) atomicAdd(&nwk[(int64_t)(w_lo + i / KS) * KS + (i % KS)], v);
+  }
 }
 
 }  // namespace
 
 // Supported (G, KP) configurations. K ≤ 32: G = 1 (KP = K rounded up to 4).
-ONI_API int oni_gibbs_launch(const OniGibbs* a, int G, int KP, int init, hipStream_t s) {
+ONI_API int oni_gibbs_launch(const OniGibbs* a, int G, int KP, int init, int atomic, hipStream_t s) {
   if (a->K < 1 || a->K > 255 || a->K > a->KS) return (int)hipErrorInvalidValue;
 #define ONI_CASE(g_, kp_) \
-  if (G == g_ && KP == kp_) return launch_gibbs<g_, kp_>(*a, init != 0, s);
+  if (G == g_ && KP == kp_) return launch_gibbs<g_, kp_>(*a, init != 0, atomic != 0, s);
   ONI_CASE(1, 4) ONI_CASE(1, 8) ONI_CASE(1, 12) ONI_CASE(1, 16) ONI_CASE(1, 20) ONI_CASE(1, 24) ONI_CASE(1, 28)
   ONI_CASE(1, 32)
   ONI_CASE(4, 8) ONI_CASE(4, 12) ONI_CASE(4, 16)
@@ -293,10 +341,19 @@ ONI_API int oni_gibbs_sizeof_args() { return (int)sizeof(OniGibbs); }
 
 ONI_API int oni_gibbs_apply(int32_t* nwk, const int32_t* dcur, int32_t* dother, const int32_t* nk_cur,
                             int32_t* nk_next, float* q, int64_t V, int K, int KS, float beta, float vbeta,
-                            uint32_t* sweep_ctr, int bump, hipStream_t s) {
+                            uint32_t* sweep_ctr, int bump, int absolute, hipStream_t s) {
   if (KS % 4 != 0 || KS > 256) return (int)hipErrorInvalidValue;
   k_apply<<<oni::grid_for(V * KS / 4, 256, 2048), 256, 0, s>>>(nwk, dcur, dother, nk_cur, nk_next, q, V, K, KS, beta,
-                                                                vbeta, sweep_ctr, bump);
+                                                                vbeta, sweep_ctr, bump, absolute);
+  return (int)hipGetLastError();
+}
+
+ONI_API int oni_recount(const int32_t* wsorted, const int32_t* wslot, const uint8_t* tok_z, int64_t T, int32_t* nwk,
+                        int KS, int tile, int wmax, hipStream_t s) {
+  if (T == 0) return 0;
+  if (tile < 256 || wmax < 1 || (size_t)wmax * KS * 4 > 64 * 1024) return (int)hipErrorInvalidValue;
+  const unsigned grid = (unsigned)((T + tile - 1) / tile);
+  k_recount<<<grid, 256, (size_t)wmax * KS * 4, s>>>(wsorted, wslot, tok_z, T, nwk, KS, tile, wmax);
   return (int)hipGetLastError();
 }
 

@@ -42,6 +42,8 @@ class Corpus:
     chunk_multi: torch.Tensor   # uint8 [ns*S]
     tok_word: torch.Tensor      # int32 [Σ slice_len*S] (PAD = -1)
     long_rows: torch.Tensor     # int32 [n_long] docs split over > 1 chunk
+    wsorted: torch.Tensor | None = None  # int32 [T] word ids of all tokens, sorted (recount path)
+    wslot: torch.Tensor | None = None    # int32 [T] SELL slot of each word-sorted token
 
     @property
     def S(self) -> int:
@@ -144,11 +146,18 @@ def build_corpus(tdoc: torch.Tensor, tword: torch.Tensor, D: int, V: int, doc_ke
         ops.sell_fill(chunk_doc, chunk_pos0, chunk_len, S, slice_off, doc_pair_ptr, pair_tokoff.contiguous(),
                       pair_word, cnt.to(torch.int32), tok_word)
     long_rows = torch.nonzero(nch > 1).flatten().to(torch.int32)
+    # word-sorted token index for the atomic-free n_wk recount (K11 option B)
+    slots = torch.nonzero(tok_word != PAD).flatten()
+    if slots.numel() >= 2**31:
+        raise ValueError("SELL slot index overflows int32")
+    wsorted, worder = torch.sort(tok_word[slots], stable=True)
+    wslot = slots[worder].to(torch.int32)
     return Corpus(D=D, V=V, T=T, G=G, L=L, doc_keys=doc_keys.to(torch.int32), pair_doc=pair_doc,
                   pair_word=pair_word, pair_cnt=cnt.to(torch.int32), doc_pair_ptr=doc_pair_ptr,
                   doc_tok_ptr=doc_tok_ptr, pair_tokoff=pair_tokoff.contiguous(), slice_off=slice_off,
                   slice_len=slice_len, chunk_doc=chunk_doc, chunk_pos0=chunk_pos0, chunk_len=chunk_len,
-                  chunk_key=chunk_key, chunk_multi=chunk_multi, tok_word=tok_word, long_rows=long_rows)
+                  chunk_key=chunk_key, chunk_multi=chunk_multi, tok_word=tok_word, long_rows=long_rows,
+                  wsorted=wsorted.contiguous(), wslot=wslot.contiguous())
 
 
 def canonical_tokens(c: Corpus) -> tuple[torch.Tensor, torch.Tensor]:

@@ -34,6 +34,7 @@ class GibbsConfig:
     beta: float = 0.01
     seed: int = 0x0D15EA5E
     use_graph: bool = True
+    count_mode: str = "recount"  # "recount" (word-sorted LDS histogram) | "atomic" (per-token Δ atomics)
 
     def resolved_alpha(self) -> float:
         return float(self.alpha) if self.alpha is not None else 50.0 / self.K
@@ -119,15 +120,21 @@ class GibbsLDA:
     def _one_sweep(self) -> None:
         c = self.c
         ops.copy_rows(self.ndk[self.a], self.ndk[1 - self.a], c.long_rows, self.KS)
+        atomic = self.cfg.count_mode == "atomic"
         ops.gibbs_pass(self._state(False), self.G, self.KP, self.K, self.alpha, self.cfg.seed, False,
-                       self.sweep_ctr, c.chunk_len, host_sweep=self.sweeps_done + 1)
+                       self.sweep_ctr, c.chunk_len, host_sweep=self.sweeps_done + 1, atomic=atomic)
+        if not atomic:
+            # dn[b] head := this rank's n_wk rebuilt from z (tail keeps Δn_k)
+            ops.recount(c.wsorted, c.wslot, self.tok_z, self.dn[self.b][: self.V * self.KS].view(self.V, self.KS),
+                        self.KS)
         if self.comm is not None and self.comm.world > 1:
             t0 = time.perf_counter()
             self.comm.allreduce_(self.dn[self.b])
             self.timings["allreduce_s"] += time.perf_counter() - t0
             self.timings["allreduce_calls"] += 1
         ops.gibbs_apply(self.nwk, self.dn[self.b], self.dn[1 - self.b], self.nk[self.cn], self.nk[1 - self.cn],
-                        self.q, self.V, self.K, self.KS, self.beta, self.vbeta, self.sweep_ctr, bump=True)
+                        self.q, self.V, self.K, self.KS, self.beta, self.vbeta, self.sweep_ctr, bump=True,
+                        absolute=not atomic)
         self.a, self.b, self.cn = 1 - self.a, 1 - self.b, 1 - self.cn
         self.sweeps_done += 1
 

@@ -226,13 +226,19 @@ def sell_perm_z(chunk_doc, chunk_pos0, chunk_len, S, slice_off, doc_tok_ptr, tok
 # sampler
 # ------------------------------------------------------------------------------------------------
 def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init: bool, sweep_ctr: torch.Tensor,
-               chunk_len: torch.Tensor, host_sweep: int | None = None) -> None:
-    """Launch one init/sweep pass. ``st`` holds the OniGibbs tensors (see csrc/kernels/gibbs.hip)."""
+               chunk_len: torch.Tensor, host_sweep: int | None = None, atomic: bool = True) -> None:
+    """Launch one init/sweep pass. ``st`` holds the OniGibbs tensors (see csrc/kernels/gibbs.hip).
+
+    ``atomic``: accumulate Δn_wk with per-token atomics; otherwise the caller rebuilds n_wk with
+    :func:`recount` after the pass (no per-token global atomics).
+    """
     s0, s1 = spec.split_seed(seed)
     KS = G * KP
     if not _is_dev(st["tok_word"]):
         npst = {k: (v.numpy().view(np.uint32) if k in ("tok_word", "chunk_key") else v.numpy())
                 for k, v in st.items()}
+        if not atomic:
+            npst["dnwk"] = np.zeros_like(npst["dnwk"])  # discarded: recount rebuilds n_wk
         spec.gibbs_pass(npst, G, KP, K, alpha, s0, s1, init,
                         int(host_sweep if host_sweep is not None else sweep_ctr.item()), chunk_len.numpy())
         return
@@ -247,12 +253,31 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
         setattr(a, name, _lib.ptr(st[name]))
     a.sweep_ctr = _lib.ptr(sweep_ctr)
     a.n_slices, a.K, a.KS, a.alpha, a.seed0, a.seed1 = n_slices, K, KS, float(alpha), s0, s1
-    _lib.check(_lib.lib().oni_gibbs_launch(C.byref(a), G, KP, 1 if init else 0, _lib.stream()), "oni_gibbs_launch")
+    _lib.check(_lib.lib().oni_gibbs_launch(C.byref(a), G, KP, 1 if init else 0, 1 if atomic else 0, _lib.stream()),
+               "oni_gibbs_launch")
 
 
-def gibbs_apply(nwk, dcur, dother, nk_cur, nk_next, q, V, K, KS, beta, vbeta, sweep_ctr, bump=True):
+RECOUNT_TILE = 4096
+
+
+def recount(wsorted, wslot, tok_z, nwk_out, KS: int) -> None:
+    """Accumulate the (word, topic) histogram of all tokens into ``nwk_out`` [V, KS] (pre-zeroed)."""
+    T = wsorted.numel()
+    if T == 0:
+        return
+    if not _is_dev(tok_z):
+        z = tok_z[wslot.long()].long()
+        nwk_out.view(-1).index_add_(0, wsorted.long() * KS + z, torch.ones_like(z, dtype=torch.int32))
+        return
+    wmax = max(1, min(16384 // KS, 4096))
+    _lib.check(_lib.lib().oni_recount(_lib.ptr(wsorted), _lib.ptr(wslot), _lib.ptr(tok_z), T, _lib.ptr(nwk_out), KS,
+                                      RECOUNT_TILE, wmax, _lib.stream()), "oni_recount")
+
+
+def gibbs_apply(nwk, dcur, dother, nk_cur, nk_next, q, V, K, KS, beta, vbeta, sweep_ctr, bump=True, absolute=False):
     if not _is_dev(nwk):
-        n2, nk2, q2 = spec.gibbs_apply(nwk.numpy(), dcur[: V * KS].view(V, KS).numpy(), dcur[V * KS:].numpy(),
+        base = np.zeros_like(nwk.numpy()) if absolute else nwk.numpy()
+        n2, nk2, q2 = spec.gibbs_apply(base, dcur[: V * KS].view(V, KS).numpy(), dcur[V * KS:].numpy(),
                                        nk_cur.numpy(), K, beta, vbeta)
         nwk.copy_(torch.from_numpy(n2))
         nk_next.copy_(torch.from_numpy(nk2))
@@ -263,7 +288,7 @@ def gibbs_apply(nwk, dcur, dother, nk_cur, nk_next, q, V, K, KS, beta, vbeta, sw
         return
     _lib.check(_lib.lib().oni_gibbs_apply(*map(_lib.ptr, (nwk, dcur, dother, nk_cur, nk_next, q)), V, K, KS,
                                           float(beta), float(vbeta), _lib.ptr(sweep_ctr), 1 if bump else 0,
-                                          _lib.stream()), "oni_gibbs_apply")
+                                          1 if absolute else 0, _lib.stream()), "oni_gibbs_apply")
 
 
 def copy_rows(src, dst, rows, KS):

@@ -60,16 +60,17 @@ def _toy_tokens(n_docs, V, seed, heavy=True):
     return torch.from_numpy(tdoc), torch.from_numpy(tword), keys
 
 
-@pytest.mark.parametrize("K", [20, 7, 50, 100])
-def test_gibbs_bitwise_vs_oracle(gpu, K):
+@pytest.mark.parametrize("K,mode", [(20, "recount"), (20, "atomic"), (7, "recount"), (50, "recount"),
+                                    (100, "atomic"), (100, "recount")])
+def test_gibbs_bitwise_vs_oracle(gpu, K, mode):
     tdoc, tword, keys = _toy_tokens(300, 400, K)
     G, KP = ops.choose_tiling(K)
     cc = build_corpus(tdoc, tword, 300, 400, torch.from_numpy(keys), G, L=64)
     cg = build_corpus(tdoc.to(gpu), tword.to(gpu), 300, 400, torch.from_numpy(keys).to(gpu), G, L=64)
     assert torch.equal(cc.tok_word, cg.tok_word.cpu())
     assert torch.equal(cc.chunk_doc, cg.chunk_doc.cpu())
-    cfg = GibbsConfig(K=K, seed=1234, use_graph=False)
-    mc, mg = GibbsLDA(cc, cfg), GibbsLDA(cg, cfg)
+    mc = GibbsLDA(cc, GibbsConfig(K=K, seed=1234, use_graph=False, count_mode="atomic"))
+    mg = GibbsLDA(cg, GibbsConfig(K=K, seed=1234, use_graph=False, count_mode=mode))
     mc.initialize()
     mg.initialize()
     assert torch.equal(mc.tok_z, mg.tok_z.cpu())
