@@ -1,0 +1,432 @@
+// DNS-response decoder for pcap / pcapng captures -- replaces the reference's
+// `editcap -c <pkt_num>` split + `tshark -T fields -e frame.time -e frame.time_epoch -e frame.len
+// -e ip.src -e ip.dst -e dns.resp.name -e dns.resp.type -e dns.resp.class -e dns.flags.rcode
+// -e dns.a` pipeline (oni-ingest dns worker, SURVEY.md §2.2 C02, [U-M]).
+//
+// P4 (intra-file parallelism) without heuristics: one sequential pass hops over record headers to
+// index every packet (cheap: 16-byte reads), then packets are decoded in parallel (OpenMP over
+// index ranges) into thread-local column buffers that are concatenated in order.
+//
+// Supported: classic pcap (µs / ns, either byte order), pcapng (SHB/IDB/EPB/SPB/OPB);
+// link types Ethernet (VLAN/QinQ), raw IPv4/IPv6, Linux cooked (SLL, SLL2), NULL/loopback;
+// IPv4 (non-fragmented) and IPv6 (no extension headers) over UDP with source port 53;
+// DNS header + first question (with name-compression pointers) + A answers.
+#include <fcntl.h>
+#include <omp.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cstring>
+#include <ctime>
+#include <string>
+#include <vector>
+
+#include "../native/oni_native.h"
+
+namespace {
+
+struct Pkt {
+  size_t off;    // start of packet bytes
+  uint32_t caplen, origlen;
+  int64_t ts_ns;
+  int linktype;
+};
+
+inline uint16_t be16(const uint8_t* p) { return (uint16_t)((p[0] << 8) | p[1]); }
+inline uint32_t be32(const uint8_t* p) { return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3]; }
+inline uint32_t rd32(const uint8_t* p, bool swap) {
+  uint32_t v;
+  std::memcpy(&v, p, 4);
+  return swap ? __builtin_bswap32(v) : v;
+}
+inline uint16_t rd16(const uint8_t* p, bool swap) {
+  uint16_t v;
+  std::memcpy(&v, p, 2);
+  return swap ? __builtin_bswap16(v) : v;
+}
+
+bool index_pcap(const uint8_t* b, size_t n, std::vector<Pkt>* out, std::string* err) {
+  if (n < 24) {
+    *err = "file too short";
+    return false;
+  }
+  const uint32_t magic = *(const uint32_t*)b;
+  bool swap = false, nano = false;
+  if (magic == 0xa1b2c3d4u) {
+  } else if (magic == 0xd4c3b2a1u) {
+    swap = true;
+  } else if (magic == 0xa1b23c4du) {
+    nano = true;
+  } else if (magic == 0x4d3cb2a1u) {
+    swap = nano = true;
+  } else if (magic == 0x0a0d0d0au) {
+    // pcapng
+    std::vector<int> if_link;
+    std::vector<int64_t> if_tsres;  // ticks per second
+    size_t pos = 0;
+    bool sw = false;
+    while (pos + 12 <= n) {
+      uint32_t type = rd32(b + pos, sw);
+      if (type == 0x0a0d0d0au) {
+        const uint32_t bom = *(const uint32_t*)(b + pos + 8);
+        sw = (bom == 0x4d3c2b1au);
+        if_link.clear();
+        if_tsres.clear();
+      }
+      const uint32_t blen = rd32(b + pos + 4, sw);
+      if (blen < 12 || pos + blen > n) break;
+      if (type == 1) {  // IDB
+        if_link.push_back(rd16(b + pos + 8, sw));
+        int64_t res = 1000000;
+        size_t o = pos + 16;
+        while (o + 4 <= pos + blen - 4) {
+          const uint16_t code = rd16(b + o, sw), len = rd16(b + o + 2, sw);
+          if (code == 0) break;
+          if (code == 9 && len >= 1) {
+            const uint8_t r = b[o + 4];
+            res = 1;
+            if (r & 0x80)
+              for (int i = 0; i < (r & 0x7f); ++i) res *= 2;
+            else
+              for (int i = 0; i < r; ++i) res *= 10;
+          }
+          o += 4 + ((len + 3) & ~3u);
+        }
+        if_tsres.push_back(res);
+      } else if (type == 6 || type == 3 || type == 2) {  // EPB / SPB / OPB
+        Pkt p;
+        if (type == 3) {
+          p.origlen = rd32(b + pos + 8, sw);
+          p.caplen = blen - 16 < p.origlen ? blen - 16 : p.origlen;
+          p.off = pos + 12;
+          p.ts_ns = 0;
+          p.linktype = if_link.empty() ? 1 : if_link[0];
+        } else {
+          const uint32_t ifid = type == 6 ? rd32(b + pos + 8, sw) : rd16(b + pos + 8, sw);
+          const uint64_t ts = ((uint64_t)rd32(b + pos + 12, sw) << 32) | rd32(b + pos + 16, sw);
+          p.caplen = rd32(b + pos + 20, sw);
+          p.origlen = rd32(b + pos + 24, sw);
+          p.off = pos + 28;
+          const int64_t res = ifid < if_tsres.size() ? if_tsres[ifid] : 1000000;
+          p.ts_ns = (int64_t)((ts / (uint64_t)res) * 1000000000ull + (ts % (uint64_t)res) * (1000000000ull / (uint64_t)res));
+          p.linktype = ifid < if_link.size() ? if_link[ifid] : 1;
+        }
+        if (p.off + p.caplen <= pos + blen) out->push_back(p);
+      }
+      pos += blen;
+    }
+    return true;
+  } else {
+    *err = "not a pcap/pcapng file";
+    return false;
+  }
+  const int link = (int)(rd32(b + 20, swap) & 0x0FFFFFFF);
+  size_t pos = 24;
+  while (pos + 16 <= n) {
+    Pkt p;
+    const uint32_t sec = rd32(b + pos, swap), frac = rd32(b + pos + 4, swap);
+    p.caplen = rd32(b + pos + 8, swap);
+    p.origlen = rd32(b + pos + 12, swap);
+    p.off = pos + 16;
+    if (p.caplen > 262144 || p.off + p.caplen > n) break;  // truncated tail
+    p.ts_ns = (int64_t)sec * 1000000000ll + (nano ? frac : (int64_t)frac * 1000);
+    p.linktype = link;
+    out->push_back(p);
+    pos = p.off + p.caplen;
+  }
+  return true;
+}
+
+// read a (possibly compressed) DNS name at `o` into `name`; returns bytes consumed at o, or -1
+int read_name(const uint8_t* m, size_t mlen, size_t o, std::string* name) {
+  name->clear();
+  size_t pos = o;
+  int consumed = -1;
+  int jumps = 0;
+  while (pos < mlen) {
+    const uint8_t l = m[pos];
+    if (l == 0) {
+      if (consumed < 0) consumed = (int)(pos + 1 - o);
+      return consumed;
+    }
+    if ((l & 0xC0) == 0xC0) {
+      if (pos + 1 >= mlen || ++jumps > 32) return -1;
+      if (consumed < 0) consumed = (int)(pos + 2 - o);
+      pos = ((size_t)(l & 0x3F) << 8) | m[pos + 1];
+      continue;
+    }
+    if ((l & 0xC0) != 0 || pos + 1 + l > mlen) return -1;
+    if (!name->empty()) name->push_back('.');
+    name->append((const char*)m + pos + 1, l);
+    if (name->size() > 255) return -1;
+    pos += 1 + l;
+  }
+  return -1;
+}
+
+struct Rows {
+  std::vector<int64_t> ts_ns;
+  std::vector<int32_t> frame_len, qtype, qclass, rcode;
+  std::vector<uint32_t> ip_src, ip_dst;
+  std::vector<int64_t> name_end, a_end;  // running offsets into chars
+  std::string names, as;
+};
+
+uint32_t fold_ipv6(const uint8_t* a) {
+  uint32_t h = 2166136261u;
+  for (int i = 0; i < 16; ++i) h = (h ^ a[i]) * 16777619u;
+  return h;
+}
+
+void decode(const uint8_t* base, const Pkt& p, Rows* r) {
+  const uint8_t* d = base + p.off;
+  size_t n = p.caplen, o = 0;
+  int ethertype = 0;
+  switch (p.linktype) {
+    case 1:  // Ethernet
+      if (n < 14) return;
+      ethertype = be16(d + 12);
+      o = 14;
+      while ((ethertype == 0x8100 || ethertype == 0x88a8) && o + 4 <= n) {
+        ethertype = be16(d + o + 2);
+        o += 4;
+      }
+      break;
+    case 113:  // Linux SLL
+      if (n < 16) return;
+      ethertype = be16(d + 14);
+      o = 16;
+      break;
+    case 276:  // Linux SLL2
+      if (n < 20) return;
+      ethertype = be16(d);
+      o = 20;
+      break;
+    case 0:  // NULL / loopback (host order family)
+      if (n < 4) return;
+      ethertype = (d[0] == 2 || d[3] == 2) ? 0x0800 : 0x86DD;
+      o = 4;
+      break;
+    default:  // raw IP (101, 228, 229, 12, 14)
+      if (n < 1) return;
+      ethertype = (d[0] >> 4) == 6 ? 0x86DD : 0x0800;
+      o = 0;
+  }
+  uint32_t src, dst;
+  size_t udp;
+  if (ethertype == 0x0800) {
+    if (o + 20 > n) return;
+    const int ihl = (d[o] & 0x0F) * 4;
+    if ((d[o] >> 4) != 4 || ihl < 20 || d[o + 9] != 17) return;
+    if ((be16(d + o + 6) & 0x3FFF) != 0) return;  // fragment
+    src = be32(d + o + 12);
+    dst = be32(d + o + 16);
+    udp = o + ihl;
+  } else if (ethertype == 0x86DD) {
+    if (o + 40 > n || d[o + 6] != 17) return;
+    src = fold_ipv6(d + o + 8);
+    dst = fold_ipv6(d + o + 24);
+    udp = o + 40;
+  } else {
+    return;
+  }
+  if (udp + 8 > n || be16(d + udp) != 53) return;
+  const uint8_t* m = d + udp + 8;
+  const size_t ml = n - udp - 8;
+  if (ml < 12) return;
+  const uint16_t flags = be16(m + 2);
+  if (!(flags & 0x8000)) return;  // responses only
+  const int qd = be16(m + 4), an = be16(m + 6);
+  if (qd < 1) return;
+  std::string name;
+  int c = read_name(m, ml, 12, &name);
+  if (c < 0 || 12 + c + 4 > ml) return;
+  size_t pos = 12 + c;
+  const int qtype = be16(m + pos), qclass = be16(m + pos + 2);
+  pos += 4;
+  for (int q = 1; q < qd; ++q) {  // skip further questions
+    std::string tmp;
+    int cc = read_name(m, ml, pos, &tmp);
+    if (cc < 0) return;
+    pos += cc + 4;
+  }
+  std::string answers;
+  for (int a = 0; a < an && pos < ml; ++a) {
+    std::string tmp;
+    int cc = read_name(m, ml, pos, &tmp);
+    if (cc < 0 || pos + cc + 10 > ml) break;
+    pos += cc;
+    const int type = be16(m + pos), rdlen = be16(m + pos + 8);
+    pos += 10;
+    if (pos + rdlen > ml) break;
+    if (type == 1 && rdlen == 4) {
+      char buf[20];
+      std::snprintf(buf, sizeof buf, "%u.%u.%u.%u", m[pos], m[pos + 1], m[pos + 2], m[pos + 3]);
+      if (!answers.empty()) answers.push_back(',');
+      answers += buf;
+    }
+    pos += rdlen;
+  }
+  r->ts_ns.push_back(p.ts_ns);
+  r->frame_len.push_back((int32_t)p.origlen);
+  r->ip_src.push_back(src);
+  r->ip_dst.push_back(dst);
+  r->qtype.push_back(qtype);
+  r->qclass.push_back(qclass);
+  r->rcode.push_back(flags & 0x000F);
+  r->names += name;
+  r->name_end.push_back((int64_t)r->names.size());
+  r->as += answers;
+  r->a_end.push_back((int64_t)r->as.size());
+}
+
+struct Handle {
+  Rows all;
+  int64_t packets = 0;
+  std::string err;
+};
+
+}  // namespace
+
+ONI_NATIVE_API void* oni_pcap_dns_open(const char* path, int threads) {
+  auto* h = new Handle();
+  const int fd = ::open(path, O_RDONLY);
+  if (fd < 0) {
+    h->err = "cannot open";
+    return h;
+  }
+  struct stat st;
+  fstat(fd, &st);
+  const size_t n = (size_t)st.st_size;
+  const uint8_t* b = nullptr;
+  if (n) b = (const uint8_t*)mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
+  std::vector<Pkt> pk;
+  if (b && b != MAP_FAILED && index_pcap(b, n, &pk, &h->err)) {
+    h->packets = (int64_t)pk.size();
+    const int T = threads > 0 ? threads : omp_get_max_threads();
+    std::vector<Rows> loc(T);
+#pragma omp parallel for num_threads(T) schedule(static, 1)
+    for (int t = 0; t < T; ++t) {
+      const size_t lo = pk.size() * (size_t)t / T, hi = pk.size() * (size_t)(t + 1) / T;
+      for (size_t i = lo; i < hi; ++i) decode(b, pk[i], &loc[t]);
+    }
+    Rows& a = h->all;
+    for (auto& r : loc) {
+      const int64_t nb = (int64_t)a.names.size(), ab = (int64_t)a.as.size();
+      a.ts_ns.insert(a.ts_ns.end(), r.ts_ns.begin(), r.ts_ns.end());
+      a.frame_len.insert(a.frame_len.end(), r.frame_len.begin(), r.frame_len.end());
+      a.ip_src.insert(a.ip_src.end(), r.ip_src.begin(), r.ip_src.end());
+      a.ip_dst.insert(a.ip_dst.end(), r.ip_dst.begin(), r.ip_dst.end());
+      a.qtype.insert(a.qtype.end(), r.qtype.begin(), r.qtype.end());
+      a.qclass.insert(a.qclass.end(), r.qclass.begin(), r.qclass.end());
+      a.rcode.insert(a.rcode.end(), r.rcode.begin(), r.rcode.end());
+      for (auto e : r.name_end) a.name_end.push_back(e + nb);
+      for (auto e : r.a_end) a.a_end.push_back(e + ab);
+      a.names += r.names;
+      a.as += r.as;
+    }
+  }
+  if (b && b != MAP_FAILED) munmap((void*)b, n);
+  ::close(fd);
+  return h;
+}
+
+ONI_NATIVE_API int oni_pcap_dns_sizes(void* hp, int64_t* rows, int64_t* name_bytes, int64_t* a_bytes,
+                                      int64_t* packets) {
+  auto* h = (Handle*)hp;
+  *rows = (int64_t)h->all.ts_ns.size();
+  *name_bytes = (int64_t)h->all.names.size();
+  *a_bytes = (int64_t)h->all.as.size();
+  *packets = h->packets;
+  return h->err.empty() ? 0 : 1;
+}
+
+ONI_NATIVE_API int oni_pcap_dns_fetch(void* hp, int64_t* ts_ns, int32_t* frame_len, uint32_t* ip_src, uint32_t* ip_dst,
+                                      int32_t* qtype, int32_t* qclass, int32_t* rcode, int64_t* name_off,
+                                      uint8_t* names, int64_t* a_off, uint8_t* as) {
+  auto* h = (Handle*)hp;
+  const Rows& a = h->all;
+  const size_t n = a.ts_ns.size();
+  std::memcpy(ts_ns, a.ts_ns.data(), n * 8);
+  std::memcpy(frame_len, a.frame_len.data(), n * 4);
+  std::memcpy(ip_src, a.ip_src.data(), n * 4);
+  std::memcpy(ip_dst, a.ip_dst.data(), n * 4);
+  std::memcpy(qtype, a.qtype.data(), n * 4);
+  std::memcpy(qclass, a.qclass.data(), n * 4);
+  std::memcpy(rcode, a.rcode.data(), n * 4);
+  name_off[0] = 0;
+  a_off[0] = 0;
+  std::memcpy(name_off + 1, a.name_end.data(), n * 8);
+  std::memcpy(a_off + 1, a.a_end.data(), n * 8);
+  std::memcpy(names, a.names.data(), a.names.size());
+  std::memcpy(as, a.as.data(), a.as.size());
+  return 0;
+}
+
+ONI_NATIVE_API void oni_pcap_dns_free(void* hp) { delete (Handle*)hp; }
+
+// ------------------------------------------------------------------------------------------------
+// pcap writer (synthetic DNS days): Ethernet/IPv4/UDP/DNS responses with one question and
+// optional A answers (name compression pointer back to the question).
+// ------------------------------------------------------------------------------------------------
+ONI_NATIVE_API int64_t oni_pcap_dns_write(const char* path, int64_t n, const int64_t* ts_ns, const uint32_t* ip_server,
+                                          const uint32_t* ip_client, const int64_t* name_off, const uint8_t* names,
+                                          const int32_t* qtype, const int32_t* rcode, const int32_t* n_answers,
+                                          const uint32_t* answer_ip, int32_t pad_to) {
+  FILE* f = std::fopen(path, "wb");
+  if (!f) return -1;
+  const uint32_t hdr[6] = {0xa1b23c4du, 0x00040002u, 0, 0, 65535, 1};  // ns resolution, v2.4, Ethernet
+  std::fwrite(hdr, 4, 6, f);
+  std::vector<uint8_t> pkt;
+  for (int64_t i = 0; i < n; ++i) {
+    pkt.clear();
+    auto put16 = [&](uint16_t v) { pkt.push_back(v >> 8); pkt.push_back(v & 255); };
+    auto put32 = [&](uint32_t v) { put16(v >> 16); put16(v & 0xFFFF); };
+    // Ethernet
+    for (int k = 0; k < 12; ++k) pkt.push_back((uint8_t)(k < 6 ? 0x02 : 0x04));
+    put16(0x0800);
+    const size_t ip0 = pkt.size();
+    pkt.push_back(0x45); pkt.push_back(0); put16(0); put16((uint16_t)i); put16(0); pkt.push_back(64); pkt.push_back(17);
+    put16(0); put32(ip_server[i]); put32(ip_client[i]);
+    const size_t udp0 = pkt.size();
+    put16(53); put16((uint16_t)(1024 + (i % 60000))); put16(0); put16(0);
+    const size_t dns0 = pkt.size();
+    const int na = n_answers ? n_answers[i] : 0;
+    put16((uint16_t)i); put16((uint16_t)(0x8180 | (rcode[i] & 0xF))); put16(1); put16((uint16_t)na); put16(0); put16(0);
+    // question name
+    int64_t a = name_off[i], b = name_off[i + 1];
+    while (a < b) {
+      int64_t e = a;
+      while (e < b && names[e] != '.') ++e;
+      const int64_t l = e - a;
+      if (l > 0 && l < 64) {
+        pkt.push_back((uint8_t)l);
+        pkt.insert(pkt.end(), names + a, names + e);
+      }
+      a = e + 1;
+    }
+    pkt.push_back(0);
+    put16((uint16_t)qtype[i]); put16(1);
+    for (int k = 0; k < na; ++k) {
+      put16(0xC00C); put16(1); put16(1); put32(300); put16(4); put32(answer_ip ? answer_ip[i] + k : 0);
+    }
+    while ((int32_t)pkt.size() < pad_to) pkt.push_back(0);
+    // lengths
+    const uint16_t iplen = (uint16_t)(pkt.size() - ip0), udplen = (uint16_t)(pkt.size() - udp0);
+    pkt[ip0 + 2] = iplen >> 8; pkt[ip0 + 3] = iplen & 255;
+    pkt[udp0 + 4] = udplen >> 8; pkt[udp0 + 5] = udplen & 255;
+    uint32_t sum = 0;
+    for (int k = 0; k < 20; k += 2) sum += (pkt[ip0 + k] << 8) | pkt[ip0 + k + 1];
+    while (sum >> 16) sum = (sum & 0xFFFF) + (sum >> 16);
+    const uint16_t ck = (uint16_t)~sum;
+    pkt[ip0 + 10] = ck >> 8; pkt[ip0 + 11] = ck & 255;
+    (void)dns0;
+    const uint32_t rec[4] = {(uint32_t)(ts_ns[i] / 1000000000ll), (uint32_t)(ts_ns[i] % 1000000000ll),
+                             (uint32_t)pkt.size(), (uint32_t)pkt.size()};
+    std::fwrite(rec, 4, 4, f);
+    std::fwrite(pkt.data(), 1, pkt.size(), f);
+  }
+  std::fclose(f);
+  return n;
+}

@@ -1,0 +1,197 @@
+// K04/K06/K07 -- GPU string featurization for DNS query names, proxy hosts/URIs/user agents.
+//
+// Reference behaviour (oni-ml DNSWordCreation / DomainProcessor.extractDomainInfo / Entropy /
+// TopDomains, ProxyWordCreation; SURVEY.md §2.2 C17/C18, §2.8, [U-M]): split a name into
+// subdomain / registered domain / TLD with country-code awareness, flag user-domain and
+// top-1M membership, measure subdomain length, Shannon entropy and dot count.
+//
+// Layout: N strings as int64 offsets [N+1] + UTF-8 bytes (the columnar store's native form).
+// One lane per string; bytes are read straight from global memory (names average ~25 B, so a
+// wave's 64 names span a few KB that stay in L1/L2). Entropy uses a per-lane 64-bin character
+// histogram in LDS (u8 counts; names are ≤ 253 B) and host-built f32 tables of c·log2(c) and
+// log2(n), so the GPU and the NumPy oracle agree bit-for-bit. Set membership (top-1M registered
+// domains) is an open-addressing table of 64-bit FNV-1a hashes, built on the host once.
+#include "oni_common.h"
+
+namespace {
+
+constexpr int kBins = 64;
+constexpr uint64_t kFnvOff = 1469598103934665603ull, kFnvPrime = 1099511628211ull;
+
+__device__ __forceinline__ uint8_t lower(uint8_t c) { return (c >= 'A' && c <= 'Z') ? (uint8_t)(c + 32) : c; }
+
+// character class for the entropy histogram: a-z 0..25, 0-9 26..35, '-' 36, '_' 37, '.' 38,
+// other bytes folded into 39..63 by value
+__device__ __forceinline__ int cbin(uint8_t c) {
+  if (c >= 'a' && c <= 'z') return c - 'a';
+  if (c >= '0' && c <= '9') return 26 + (c - '0');
+  if (c == '-') return 36;
+  if (c == '_') return 37;
+  if (c == '.') return 38;
+  return 39 + (c % 25);
+}
+
+__device__ __forceinline__ uint64_t fnv_range(const uint8_t* p, int64_t a, int64_t b) {
+  uint64_t h = kFnvOff;
+  for (int64_t i = a; i < b; ++i) h = (h ^ lower(p[i])) * kFnvPrime;
+  return h;
+}
+
+__device__ __forceinline__ bool set_probe(const uint64_t* __restrict__ tab, uint64_t mask, uint64_t h) {
+  if (!tab) return false;
+  if (h == 0) h = 1;
+  uint64_t i = (h ^ (h >> 29)) & mask;
+  for (int n = 0; n <= (int)mask && n < 4096; ++n) {
+    const uint64_t v = tab[i];
+    if (v == h) return true;
+    if (v == 0) return false;
+    i = (i + 1) & mask;
+  }
+  return false;
+}
+
+// Shannon entropy (bits) of bytes [a, b) with the exact-table formulation:
+//   H = lg[n] - (Σ_bins clogc[c_bin]) / n,    clogc[c] = c·log2(c), lg[n] = log2(n)  (f32 tables)
+__device__ float entropy_range(const uint8_t* __restrict__ p, int64_t a, int64_t b, uint8_t* h,
+                               const float* __restrict__ clogc, const float* __restrict__ lg) {
+  const int n = (int)(b - a);
+  if (n <= 0) return 0.f;
+  for (int k = 0; k < kBins; ++k) h[k] = 0;
+  for (int64_t i = a; i < b; ++i) {
+    const int k = cbin(lower(p[i]));
+    h[k] = (uint8_t)(h[k] + 1);
+  }
+  float s = 0.f;
+  for (int k = 0; k < kBins; ++k) s = s + clogc[h[k]];
+  return lg[n < 255 ? n : 255] - s / (float)n;
+}
+
+struct DomainOut {
+  uint64_t* reg_hash;   // FNV-1a of the registered domain (label.suffix)
+  uint8_t* top;         // 2 user domain, 1 top-1M, 0 other
+  int32_t* sub_len;     // subdomain length in bytes
+  float* sub_ent;       // subdomain entropy (bits)
+  int32_t* periods;     // '.' count of the (trailing-dot-stripped) name
+  int32_t* sub_off;     // [N][2] subdomain / registered-domain start offsets (relative)
+};
+
+// second-level labels that make a ccTLD a two-label public suffix (co.uk, com.br, ac.jp, ...)
+__device__ __forceinline__ bool is_sld(const uint8_t* p, int64_t a, int64_t b) {
+  const int n = (int)(b - a);
+  if (n < 2 || n > 4) return false;
+  char s[4] = {0, 0, 0, 0};
+  for (int i = 0; i < n; ++i) s[i] = (char)lower(p[a + i]);
+  const uint32_t v = (uint32_t)(uint8_t)s[0] | ((uint32_t)(uint8_t)s[1] << 8) | ((uint32_t)(uint8_t)s[2] << 16) |
+                     ((uint32_t)(uint8_t)s[3] << 24);
+#define W(a, b, c, d) ((uint32_t)(a) | ((uint32_t)(b) << 8) | ((uint32_t)(c) << 16) | ((uint32_t)(d) << 24))
+  switch (v) {
+    case W('c', 'o', 0, 0): case W('a', 'c', 0, 0): case W('o', 'r', 0, 0): case W('n', 'e', 0, 0):
+    case W('g', 'o', 0, 0): case W('c', 'o', 'm', 0): case W('n', 'e', 't', 0): case W('o', 'r', 'g', 0):
+    case W('g', 'o', 'v', 0): case W('e', 'd', 'u', 0): case W('m', 'i', 'l', 0): case W('n', 'i', 'c', 0):
+    case W('l', 't', 'd', 0): case W('p', 'l', 'c', 0): case W('s', 'c', 'h', 0): case W('n', 'o', 'm', 0):
+    case W('g', 'o', 'b', 0): case W('g', 'e', 'n', 0): case W('b', 'i', 'z', 0): case W('i', 'n', 'f', 'o'):
+    case W('g', 'o', 'u', 'v'): case W('a', 's', 's', 'o'):
+      return true;
+    default:
+      return false;
+  }
+#undef W
+}
+
+__global__ __launch_bounds__(256) void k_domain_features(const int64_t* __restrict__ off, const uint8_t* __restrict__ p,
+                                                         int64_t n, const uint64_t* __restrict__ top_tab,
+                                                         uint64_t top_mask, uint64_t user_hash, int user_is_label,
+                                                         const float* __restrict__ clogc, const float* __restrict__ lg,
+                                                         DomainOut o) {
+  __shared__ uint8_t hist[256][kBins];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t a = off[i];
+    int64_t b = off[i + 1];
+    while (b > a && p[b - 1] == '.') --b;  // trailing root dot
+    // last three dot positions
+    int64_t d1 = -1, d2 = -1, d3 = -1;
+    int per = 0;
+    for (int64_t j = b - 1; j >= a; --j)
+      if (p[j] == '.') {
+        ++per;
+        if (d1 < 0) d1 = j;
+        else if (d2 < 0) d2 = j;
+        else if (d3 < 0) d3 = j;
+      }
+    // TLD = (d1, b); second label = (d2, d1); third = (d3, d2)
+    int64_t reg = a;  // start of registered domain
+    if (d1 >= 0) {
+      const bool cc = (b - d1 - 1) == 2;  // 2-letter TLD = country code
+      if (cc && d2 >= 0 && is_sld(p, d2 + 1, d1)) reg = d3 >= 0 ? d3 + 1 : a;
+      else reg = d2 >= 0 ? d2 + 1 : a;
+      if (cc && d2 < 0 && is_sld(p, a, d1)) reg = a;  // bare "co.uk"
+    }
+    const int64_t sub_end = reg > a ? reg - 1 : a;  // subdomain = [a, reg-1)
+    const uint64_t rh = fnv_range(p, reg, b);
+    // registered label only (for USER_DOMAIN given as a bare label, e.g. "intel")
+    int64_t lab_end = reg;
+    while (lab_end < b && p[lab_end] != '.') ++lab_end;
+    const uint64_t lh = fnv_range(p, reg, lab_end);
+    uint8_t top = 0;
+    if (user_hash != 0 && (user_is_label ? lh == user_hash : rh == user_hash)) top = 2;
+    else if (set_probe(top_tab, top_mask, rh)) top = 1;
+    o.reg_hash[i] = rh;
+    o.top[i] = top;
+    o.sub_len[i] = (int32_t)(sub_end - a);
+    o.periods[i] = per;
+    o.sub_ent[i] = entropy_range(p, a, sub_end, hist[threadIdx.x], clogc, lg);
+    if (o.sub_off) {
+      o.sub_off[2 * i] = 0;
+      o.sub_off[2 * i + 1] = (int32_t)(reg - a);
+    }
+  }
+}
+
+// Generic per-string features: FNV-1a hash (lowercased), length, entropy.
+__global__ __launch_bounds__(256) void k_string_features(const int64_t* __restrict__ off, const uint8_t* __restrict__ p,
+                                                         int64_t n, const float* __restrict__ clogc,
+                                                         const float* __restrict__ lg, uint64_t* __restrict__ hash,
+                                                         int32_t* __restrict__ len, float* __restrict__ ent) {
+  __shared__ uint8_t hist[256][kBins];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t a = off[i], b = off[i + 1];
+    if (hash) hash[i] = fnv_range(p, a, b);
+    if (len) len[i] = (int32_t)(b - a);
+    if (ent) {
+      // long URIs: entropy over the first 255 bytes keeps u8 counts exact
+      ent[i] = entropy_range(p, a, (b - a) > 255 ? a + 255 : b, hist[threadIdx.x], clogc, lg);
+    }
+  }
+}
+
+__global__ void k_set_probe(const uint64_t* __restrict__ h, int64_t n, const uint64_t* __restrict__ tab, uint64_t mask,
+                            uint8_t* __restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = set_probe(tab, mask, h[i]);
+}
+
+}  // namespace
+
+ONI_API int oni_domain_features(const int64_t* off, const uint8_t* chars, int64_t n, const uint64_t* top_tab,
+                                uint64_t top_mask, uint64_t user_hash, int user_is_label, const float* clogc,
+                                const float* lg, uint64_t* reg_hash, uint8_t* top, int32_t* sub_len, float* sub_ent,
+                                int32_t* periods, hipStream_t s) {
+  DomainOut o{reg_hash, top, sub_len, sub_ent, periods, nullptr};
+  k_domain_features<<<oni::grid_for(n, 256, 2048), 256, 0, s>>>(off, chars, n, top_tab, top_mask, user_hash,
+                                                                 user_is_label, clogc, lg, o);
+  return (int)hipGetLastError();
+}
+
+ONI_API int oni_string_features(const int64_t* off, const uint8_t* chars, int64_t n, const float* clogc,
+                                const float* lg, uint64_t* hash, int32_t* len, float* ent, hipStream_t s) {
+  k_string_features<<<oni::grid_for(n, 256, 2048), 256, 0, s>>>(off, chars, n, clogc, lg, hash, len, ent);
+  return (int)hipGetLastError();
+}
+
+ONI_API int oni_set_probe(const uint64_t* h, int64_t n, const uint64_t* tab, uint64_t mask, uint8_t* out,
+                          hipStream_t s) {
+  k_set_probe<<<oni::grid_for(n), 256, 0, s>>>(h, n, tab, mask, out);
+  return (int)hipGetLastError();
+}

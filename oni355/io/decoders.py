@@ -1,0 +1,275 @@
+"""Telemetry decoders (Python side of ``liboni_native``): nfdump/ONI flow CSV, pcap DNS, proxy logs.
+
+* :func:`read_flow_csv`  -- oni-nfdump CSV (27 ONI fields) or stock ``nfdump -o csv`` (header-driven)
+* :func:`read_pcap_dns`  -- DNS responses from pcap/pcapng (the tshark fields of SURVEY.md §2.2 C02)
+* :func:`write_pcap_dns` -- our own pcap writer (synthetic DNS days)
+* :func:`read_proxy_log` -- Bluecoat-style access logs (C03)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import datetime as _dt
+
+import numpy as np
+
+from .. import schema
+from ..ops import native
+from ..store.columnar import StringColumn
+
+vp, i64, i32 = C.c_void_p, C.c_int64, C.c_int
+
+native.register("oni_csv_count_rows", [C.c_char_p, i32, i32], i64)
+native.register("oni_csv_parse", [C.c_char_p, i32, i32, vp, vp, i64, vp, C.c_char, i32], i64)
+native.register("oni_pcap_dns_open", [C.c_char_p, i32], vp)
+native.register("oni_pcap_dns_sizes", [vp, vp, vp, vp, vp], i32)
+native.register("oni_pcap_dns_fetch", [vp] + [vp] * 11, i32)
+native.register("oni_pcap_dns_free", [vp], None)
+native.register("oni_pcap_dns_write", [C.c_char_p, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32], i64)
+
+SKIP, I64, F64, IPV4, PROTO, FLAGS, TIME, STR = range(8)
+
+# ONI flow CSV (oni-nfdump output order == Hive flow schema minus unix_tstamp)
+_ONI_FLOW_FIELDS = [
+    ("treceived", TIME), ("tryear", I64), ("trmonth", I64), ("trday", I64), ("trhour", I64), ("trminute", I64),
+    ("trsec", I64), ("tdur", F64), ("sip", IPV4), ("dip", IPV4), ("sport", I64), ("dport", I64), ("proto", PROTO),
+    ("flag", FLAGS), ("fwd", I64), ("stos", I64), ("ipkt", I64), ("ibyt", I64), ("opkt", I64), ("obyt", I64),
+    ("input", I64), ("output", I64), ("sas", I64), ("das", I64), ("dtos", I64), ("dir", I64), ("rip", IPV4),
+]
+# stock nfdump -o csv header names -> (our column, kind)
+_NFDUMP_MAP = {
+    "ts": ("treceived", TIME), "td": ("tdur", F64), "sa": ("sip", IPV4), "da": ("dip", IPV4), "sp": ("sport", I64),
+    "dp": ("dport", I64), "pr": ("proto", PROTO), "flg": ("flag", FLAGS), "fwd": ("fwd", I64), "stos": ("stos", I64),
+    "ipkt": ("ipkt", I64), "ibyt": ("ibyt", I64), "opkt": ("opkt", I64), "obyt": ("obyt", I64), "in": ("input", I64),
+    "out": ("output", I64), "sas": ("sas", I64), "das": ("das", I64), "dtos": ("dtos", I64), "dir": ("dir", I64),
+    "ra": ("rip", IPV4),
+}
+_INT32_COLS = {"tryear", "trmonth", "trday", "trhour", "trminute", "trsec", "sport", "dport", "proto", "flag", "fwd",
+               "stos", "input", "output", "sas", "das", "dtos", "dir"}
+
+
+def _parse(path: str, fields: list[tuple[str | None, int]], skip_header: bool, sep: str = ",", threads: int = 0):
+    L = native.lib()
+    bpath = path.encode()
+    n = L.oni_csv_count_rows(bpath, int(skip_header), threads)
+    if n < 0:
+        raise OSError(f"cannot read {path}")
+    outs, arrs = [], {}
+    kinds = np.array([k for _, k in fields], dtype=np.int32)
+    for name, k in fields:
+        if name is None or k == SKIP:
+            outs.append(None)
+            continue
+        dt = {I64: np.int64, F64: np.float64, IPV4: np.uint32, PROTO: np.int32, FLAGS: np.int32, TIME: np.int64,
+              STR: np.int64}.get(k)
+        a = np.zeros(n * 2 if k == STR else n, dtype=np.int64 if k == STR else dt)
+        arrs[name] = a
+        outs.append(a.ctypes.data)
+    optr = (C.c_void_p * len(outs))(*outs)
+    valid = np.zeros(n, dtype=np.uint8)
+    got = L.oni_csv_parse(bpath, int(skip_header), len(fields), kinds.ctypes.data, optr, n, valid.ctypes.data,
+                          sep.encode(), threads)
+    if got < 0:
+        raise OSError(f"parse failed for {path} ({got})")
+    m = valid.astype(bool)
+    return {k: v[m] if v.size == n else v.reshape(n, 2)[m] for k, v in arrs.items()}, int((~m).sum())
+
+
+def read_flow_csv(path: str, threads: int = 0) -> tuple[dict, int]:
+    """Decode a flow CSV into flow-schema columns. Returns (cols, n_bad_rows)."""
+    with open(path, "rb") as f:
+        first = f.readline().decode("utf-8", "replace").strip()
+    heads = [h.strip().lower() for h in first.split(",")]
+    has_header = not any(ch.isdigit() for ch in heads[0][:4]) if heads else False
+    if has_header and heads[0] in ("ts", "te"):
+        fields = [(_NFDUMP_MAP.get(h, (None, SKIP))) for h in heads]
+    elif has_header and heads[0] in ("treceived", "tr"):
+        fields = list(_ONI_FLOW_FIELDS)
+    else:
+        fields = list(_ONI_FLOW_FIELDS)
+    cols, bad = _parse(path, fields, has_header, threads=threads)
+    return finish_flow_cols(cols), bad
+
+
+def finish_flow_cols(cols: dict) -> dict:
+    n = len(next(iter(cols.values()))) if cols else 0
+    t = cols.get("treceived", np.zeros(n, np.int64))
+    cols["unix_tstamp"] = t.copy()
+    if "trhour" not in cols:
+        dt = t.astype("datetime64[s]")
+        days = dt.astype("datetime64[D]")
+        secs = (dt - days).astype(np.int64)
+        ymd = days.astype(object)
+        cols["tryear"] = np.array([d.year for d in ymd], np.int32) if n else np.zeros(0, np.int32)
+        cols["trmonth"] = np.array([d.month for d in ymd], np.int32) if n else np.zeros(0, np.int32)
+        cols["trday"] = np.array([d.day for d in ymd], np.int32) if n else np.zeros(0, np.int32)
+        cols["trhour"] = (secs // 3600).astype(np.int32)
+        cols["trminute"] = (secs // 60 % 60).astype(np.int32)
+        cols["trsec"] = (secs % 60).astype(np.int32)
+    out = {}
+    for c in schema.FLOW_COLUMNS:
+        if c in cols:
+            v = cols[c]
+        elif c in schema.FLOW_IP_COLUMNS:
+            v = np.zeros(n, np.uint32)
+        else:
+            v = np.zeros(n, np.int64)
+        if c in _INT32_COLS:
+            v = v.astype(np.int32)
+        elif c == "tdur":
+            v = v.astype(np.float32)
+        out[c] = v
+    return out
+
+
+def write_flow_csv(path: str, cols: dict, header: bool = True) -> None:
+    """ONI flow CSV (inverse of :func:`read_flow_csv`), used by tests and the demo."""
+    from .results import ip_str
+    n = len(cols["sip"])
+    with open(path, "w") as f:
+        if header:
+            f.write(",".join(c for c, _ in _ONI_FLOW_FIELDS) + "\n")
+        for i in range(n):
+            row = []
+            for c, k in _ONI_FLOW_FIELDS:
+                v = cols[c][i]
+                if k == TIME:
+                    row.append(_dt.datetime.fromtimestamp(int(v), tz=_dt.timezone.utc).strftime("%Y-%m-%d %H:%M:%S"))
+                elif k == IPV4:
+                    row.append(ip_str(v))
+                elif k == F64:
+                    row.append(f"{float(v):.3f}")
+                else:
+                    row.append(str(int(v)))
+            f.write(",".join(row) + "\n")
+
+
+# ------------------------------------------------------------------------------------------------
+# Bluecoat proxy logs (C03)
+# ------------------------------------------------------------------------------------------------
+_BLUECOAT = {  # Bluecoat field name -> (schema column, kind)
+    "date": ("p_date", STR), "time": ("p_time", STR), "time-taken": ("duration", I64), "c-ip": ("clientip", IPV4),
+    "cs-username": ("username", STR), "cs-auth-group": ("authgroup", STR), "x-exception-id": ("exceptionid", STR),
+    "sc-filter-result": ("filterresult", STR), "cs-categories": ("webcat", STR), "cs(referer)": ("referer", STR),
+    "sc-status": ("respcode", I64), "s-action": ("action", STR), "cs-method": ("reqmethod", STR),
+    "rs(content-type)": ("resconttype", STR), "cs-uri-scheme": ("urischeme", STR), "cs-host": ("host", STR),
+    "cs-uri-port": ("uriport", I64), "cs-uri-path": ("uripath", STR), "cs-uri-query": ("uriquery", STR),
+    "cs-uri-extension": ("uriextension", STR), "cs(user-agent)": ("useragent", STR), "s-ip": ("serverip", IPV4),
+    "sc-bytes": ("scbytes", I64), "cs-bytes": ("csbytes", I64), "x-virus-id": ("virusid", STR),
+    "x-bluecoat-application-name": ("bcappname", STR), "x-bluecoat-application-operation": ("bcappoperation", STR),
+}
+
+
+def _gather_strings(buf: np.ndarray, spans: np.ndarray) -> StringColumn:
+    b, e = spans[:, 0], spans[:, 1]
+    ln = np.maximum(e - b, 0)
+    off = np.zeros(len(ln) + 1, np.int64)
+    np.cumsum(ln, out=off[1:])
+    if off[-1] == 0:
+        return StringColumn(off, np.zeros(0, np.uint8))
+    idx = np.repeat(b - off[:-1], ln) + np.arange(off[-1])
+    return StringColumn(off, buf[idx])
+
+
+def read_proxy_log(path: str, threads: int = 0) -> dict:
+    """Bluecoat access log (``#Fields:`` header defines the order) → proxy-schema columns."""
+    from .. import schema
+    fields_hdr = None
+    with open(path, "rb") as f:
+        for raw in f:
+            line = raw.decode("utf-8", "replace").strip()
+            if line.startswith("#Fields:"):
+                fields_hdr = line[len("#Fields:"):].split()
+                break
+            if line and not line.startswith("#"):
+                break
+    if fields_hdr is None:
+        from ..synth.proxy import PROXY_FIELDS
+        fields_hdr = PROXY_FIELDS
+    fields = [_BLUECOAT.get(h.lower(), (None, SKIP)) for h in fields_hdr]
+    cols, bad = _parse(path, fields, False, sep=" ", threads=threads)
+    buf = np.memmap(path, dtype=np.uint8, mode="r") if os.path.getsize(path) else np.zeros(0, np.uint8)
+    out = {}
+    n = len(next(iter(cols.values()))) if cols else 0
+    for c in schema.PROXY_COLUMNS:
+        if c in cols:
+            v = cols[c]
+            out[c] = _gather_strings(np.asarray(buf), v) if v.ndim == 2 else v
+        elif c == "fulluri":
+            continue
+        elif c in ("clientip", "serverip"):
+            out[c] = np.zeros(n, np.uint32)
+        elif c in ("duration", "respcode", "uriport", "scbytes", "csbytes"):
+            out[c] = np.zeros(n, np.int64)
+        else:
+            out[c] = StringColumn.from_list(["-"] * n)
+    for c in ("respcode", "uriport"):
+        out[c] = np.asarray(out[c]).astype(np.int32)
+    sch, host, port, pth, qry = (out[k].to_list() if hasattr(out[k], "to_list") else out[k]
+                                 for k in ("urischeme", "host", "uriport", "uripath", "uriquery"))
+    full = []
+    for s, h, p, pa, q in zip(sch, host, port, pth, qry):
+        u = f"{s}://{h}" + (f":{p}" if p not in (0, 80, 443) else "") + (pa if pa != "-" else "")
+        full.append(u + (q if q not in ("-", "") else ""))
+    out["fulluri"] = StringColumn.from_list(full)
+    out["_bad_rows"] = bad
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# pcap DNS
+# ------------------------------------------------------------------------------------------------
+def read_pcap_dns(path: str, threads: int = 0) -> dict:
+    L = native.lib()
+    h = L.oni_pcap_dns_open(path.encode(), threads)
+    try:
+        rows, nb, ab, pk = (C.c_int64() for _ in range(4))
+        rc = L.oni_pcap_dns_sizes(h, C.byref(rows), C.byref(nb), C.byref(ab), C.byref(pk))
+        if rc != 0:
+            raise OSError(f"cannot decode {path}")
+        n = rows.value
+        ts = np.zeros(n, np.int64)
+        flen = np.zeros(n, np.int32)
+        src = np.zeros(n, np.uint32)
+        dst = np.zeros(n, np.uint32)
+        qt = np.zeros(n, np.int32)
+        qc = np.zeros(n, np.int32)
+        rc_ = np.zeros(n, np.int32)
+        noff = np.zeros(n + 1, np.int64)
+        names = np.zeros(max(nb.value, 1), np.uint8)
+        aoff = np.zeros(n + 1, np.int64)
+        aa = np.zeros(max(ab.value, 1), np.uint8)
+        L.oni_pcap_dns_fetch(h, *(x.ctypes.data for x in (ts, flen, src, dst, qt, qc, rc_, noff, names, aoff, aa)))
+    finally:
+        L.oni_pcap_dns_free(h)
+    unix = ts // 1_000_000_000
+    return {
+        "frame_time": StringColumn.from_list([_dt.datetime.fromtimestamp(t / 1e9, tz=_dt.timezone.utc)
+                                              .strftime("%b %d, %Y %H:%M:%S.%f UTC") for t in ts.tolist()]),
+        "unix_tstamp": unix,
+        "frame_len": flen,
+        "ip_src": src,
+        "ip_dst": dst,
+        "dns_qry_name": StringColumn(noff, names[: nb.value]),
+        "dns_qry_type": qt,
+        "dns_qry_class": qc,
+        "dns_qry_rcode": rc_,
+        "dns_a": StringColumn(aoff, aa[: ab.value]),
+        "_packets": pk.value,
+    }
+
+
+def write_pcap_dns(path: str, ts_ns, ip_server, ip_client, names: StringColumn, qtype, rcode, n_answers=None,
+                   answer_ip=None, pad_to: int = 0) -> int:
+    n = len(names)
+    arrs = [np.ascontiguousarray(a, dt) for a, dt in ((ts_ns, np.int64), (ip_server, np.uint32),
+                                                       (ip_client, np.uint32), (names.offsets, np.int64),
+                                                       (names.chars, np.uint8), (qtype, np.int32),
+                                                       (rcode, np.int32))]
+    na = np.ascontiguousarray(n_answers if n_answers is not None else np.zeros(n), np.int32)
+    ai = np.ascontiguousarray(answer_ip if answer_ip is not None else np.zeros(n), np.uint32)
+    r = native.lib().oni_pcap_dns_write(path.encode(), n, *(a.ctypes.data for a in arrs), na.ctypes.data,
+                                        ai.ctypes.data, pad_to)
+    if r != n:
+        raise OSError(f"pcap write failed: {path}")
+    return r

@@ -47,6 +47,31 @@ def flow_rows(cols: dict, local_rows: np.ndarray, src_words, dst_words, src_scor
     return out
 
 
+_EVENT_IP_COLUMNS = {"ip_src", "ip_dst", "clientip", "serverip"}
+
+
+def event_rows(source: str, cols: dict, local_rows, words: list[str], scores) -> list[list]:
+    """DNS / proxy result rows: raw columns in schema order + word + score."""
+    names = schema.raw_columns(source)
+    out = []
+    for i, r in enumerate(np.asarray(local_rows, dtype=np.int64)):
+        row = []
+        for c in names:
+            v = cols.get(c)
+            if v is None:
+                row.append("")
+            elif hasattr(v, "offsets"):
+                row.append(v[int(r)])
+            elif c in _EVENT_IP_COLUMNS:
+                row.append(ip_str(v[r]))
+            else:
+                row.append(str(v[r]))
+        if source == "dns" and not row[0]:
+            row[0] = _fmt_time(cols["unix_tstamp"][r])
+        out.append(row + [words[i], f"{float(scores[i]):.9g}"])
+    return out
+
+
 def write_csv(path: str, header: list[str], rows: list[list], with_header: bool = True) -> str:
     os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
     tmp = path + ".tmp"

@@ -157,6 +157,62 @@ def top_n(score: torch.Tensor, tol: float, maxresults: int, comm: Comm | None, r
     return _top_n_from_hist(score, hist, tol, maxresults, comm, row_offset)
 
 
+@dataclass
+class SingleResult:
+    rows: np.ndarray      # global row ids, ascending score
+    scores: np.ndarray
+    words: np.ndarray     # packed word keys (u64) of the result rows
+    timings: dict
+    stats: dict
+    lda: object = None
+
+
+def run_single_doc_events(doc_keys64: torch.Tensor, word_keys64: torch.Tensor, K: int, sweeps: int, tol: float,
+                          maxresults: int, alpha, beta: float, seed: int, chunk_len: int, comm: Comm | None,
+                          feedback=None, row_offset: int = 0, eval_every: int = 0, ckpt=None, log=None,
+                          timings: dict | None = None) -> SingleResult:
+    """Shared DNS/proxy path: one (doc, word) token per event; score = θ_doc·φ_word (C24)."""
+    t = dict(timings or {})
+    dev = doc_keys64.device
+    sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
+    t0 = time.perf_counter()
+    dk, wk, wts = doc_keys64, word_keys64, None
+    if feedback is not None:
+        wts = torch.cat([torch.ones_like(wk), feedback[2]])
+        dk = torch.cat([dk, feedback[0]])
+        wk = torch.cat([wk, feedback[1]])
+    vocab = global_vocab(wk, comm)
+    sync()
+    t["vocab_s"] = time.perf_counter() - t0
+    run = build_and_train(dk, wk, wts, vocab, K, alpha, beta, seed, sweeps, chunk_len, comm, eval_every=eval_every,
+                          ckpt=ckpt, log=log)
+    t.update(run.timings)
+    t0 = time.perf_counter()
+    dkeys, theta = gather_theta(run, comm)
+    d1 = lookup(dkeys, doc_keys64)
+    w1 = lookup(vocab, word_keys64)
+    hist = torch.zeros(2048, dtype=torch.int32, device=dev)
+    from .. import ops as _ops
+    score, _, _ = _ops.score(theta, run.model.phi(), d1, w1, tol=tol, hist=hist)
+    rows, scs = top_n(score, tol, maxresults, comm, row_offset, hist=hist)
+    sync()
+    t["score_s"] = time.perf_counter() - t0
+    t["records_scored"] = int(doc_keys64.numel())
+    loc = rows - row_offset
+    mine = (loc >= 0) & (loc < doc_keys64.numel())
+    words = word_keys64[loc[mine]]
+    if comm is not None and comm.world > 1:
+        gid_all = torch.cat(comm.allgather_var(rows[mine]))
+        words = torch.cat(comm.allgather_var(words))
+        pos = {int(g): i for i, g in enumerate(gid_all.tolist())}
+        words = words.cpu()[torch.tensor([pos[int(g)] for g in rows.tolist()], dtype=torch.int64)]
+    stats = run.corpus.stats()
+    stats.update({"events": int(doc_keys64.numel()),
+                  "loglik": run.model.likelihoods[-1][1] if run.model.likelihoods else None})
+    return SingleResult(rows=rows.cpu().numpy(), scores=scs.cpu().numpy(),
+                        words=words.cpu().numpy().view(np.uint64), timings=t, stats=stats, lda=run)
+
+
 def _top_n_from_hist(score, hist, tol, maxresults, comm, row_offset):
     h = hist.to(torch.int64).cpu().numpy()
     if comm is not None and comm.world > 1:

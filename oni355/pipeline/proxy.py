@@ -1,0 +1,150 @@
+"""Proxy suspicious-connects (the `oni-ml YYYYMMDD proxy` path; SURVEY.md §2.2 C18, §2.8 "Proxy").
+
+Bluecoat log → (C++ tokenizer) → columns → [GPU] host registered-domain/top-1M flag (K04),
+user-agent frequency (K07: FNV hash → unique counts → per-event count), URI length + entropy (K06),
+quantile cuts (K01) → word packing → corpus/LDA → score θ_client·φ_word → top-N.
+
+Word (bit-packed u64, rendered ``top_tb_method_uab_ctype_eb_lb_respcode``):
+  top(2b) @31 | time decile(4b) @27 | method code(4b) @23 | UA-frequency quintile(3b) @20 |
+  content-type class(4b) @16 | URI-entropy quintile(3b) @13 | URI-length quintile(3b) @10 |
+  response code(10b) @0
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..ops import strings as sops
+from ..parallel.comm import Comm
+from ..ref import spec
+from ..store.columnar import StringColumn
+from . import common
+from .dns import top_set
+
+METHODS = ["OTHER", "GET", "POST", "PUT", "HEAD", "CONNECT", "OPTIONS", "DELETE", "TRACE", "PATCH"]
+CTYPE_CLASSES = [("", 0), ("-", 0), ("text/html", 1), ("text/", 2), ("image/", 3), ("application/javascript", 4),
+                 ("application/json", 4), ("application/octet-stream", 5), ("application/", 6), ("video/", 7),
+                 ("audio/", 8), ("multipart/", 9)]
+BINNED = [("time", spec.DECILES, 27), ("ua_freq", spec.QUINTILES, 20), ("uri_ent", spec.QUINTILES, 13),
+          ("uri_len", spec.QUINTILES, 10)]
+RAW = [("method", 0xF, 23), ("ctype", 0xF, 16), ("respcode", 0x3FF, 0)]
+TOP_SHIFT = 31
+
+
+def ctype_class(s: str) -> int:
+    s = s.strip().lower()
+    best, blen = 10, -1
+    for prefix, code in CTYPE_CLASSES:
+        if (s == prefix if prefix in ("", "-") else s.startswith(prefix)) and len(prefix) > blen:
+            best, blen = code, len(prefix)
+    return best
+
+
+def word_str(w: int) -> str:
+    w = int(w)
+    vals = {"top": (w >> TOP_SHIFT) & 3}
+    for name, fr, s in BINNED:
+        vals[name] = (w >> s) & (15 if fr is spec.DECILES else 7)
+    for name, m, s in RAW:
+        vals[name] = (w >> s) & m
+    return "_".join(str(vals[k]) for k in ("top", "time", "method", "ua_freq", "ctype", "uri_ent", "uri_len", "respcode"))
+
+
+def _codes_by_hash(col: StringColumn, dev, fn) -> torch.Tensor:
+    """Categorical code per row via the distinct values only (few distinct methods / types)."""
+    off = torch.from_numpy(col.offsets).to(dev)
+    ch = torch.from_numpy(col.chars if col.chars.size else np.zeros(1, np.uint8)).to(dev)
+    h, _, _ = sops.string_features(off, ch)
+    uniq, first_idx, inv = _unique_first(h)
+    labels = [fn(col[int(i)]) for i in first_idx.tolist()]
+    table = torch.tensor(labels, dtype=torch.int32, device=dev)
+    return table[inv].contiguous() if len(labels) else torch.zeros(0, dtype=torch.int32, device=dev)
+
+
+def _unique_first(h: torch.Tensor):
+    uniq, inv = torch.unique(h, return_inverse=True)
+    first = torch.full((uniq.numel(),), h.numel(), dtype=torch.int64, device=h.device)
+    first.scatter_reduce_(0, inv, torch.arange(h.numel(), device=h.device), reduce="amin")
+    return uniq, first.cpu(), inv
+
+
+def method_code(s: str) -> int:
+    s = s.strip().upper()
+    return METHODS.index(s) if s in METHODS else 0
+
+
+def featurize(cols: dict, device, comm: Comm | None, topset, allreduce_counts: bool = True):
+    dev = torch.device(device)
+    n = len(cols["clientip"])
+
+    def strcol(name):
+        c: StringColumn = cols[name]
+        return (torch.from_numpy(c.offsets).to(dev),
+                torch.from_numpy(c.chars if c.chars.size else np.zeros(1, np.uint8)).to(dev))
+
+    ho, hc = strcol("host")
+    _, top, _, _, _ = sops.domain_features(ho, hc, topset, "")
+    # time of day from p_time "HH:MM:SS"
+    pt = cols["p_time"]
+    ptb = np.frombuffer(pt.chars.tobytes(), dtype=np.uint8) if pt.chars.size else np.zeros(0, np.uint8)
+    o = pt.offsets[:-1]
+    def dig(k):
+        return (ptb[o + k].astype(np.int64) - 48) if n else np.zeros(0, np.int64)
+    hh, mm, ss = dig(0) * 10 + dig(1), dig(3) * 10 + dig(4), dig(6) * 10 + dig(7)
+    t = (torch.from_numpy(hh.astype(np.float32)) + torch.from_numpy(mm.astype(np.float32)) / 60.0) \
+        + torch.from_numpy(ss.astype(np.float32)) / 3600.0
+    tkey = ops.f32_keys(t.to(dev).contiguous())
+    # user-agent frequency over the day (global across ranks)
+    uo, uc = strcol("useragent")
+    uh, _, _ = sops.string_features(uo, uc)
+    uq, inv = torch.unique(uh, return_inverse=True)
+    cnt = torch.bincount(inv, minlength=uq.numel())
+    if comm is not None and comm.world > 1:
+        keys = torch.cat(comm.allgather_var(uq))
+        cnts = torch.cat(comm.allgather_var(cnt))
+        gk, ginv = torch.unique(keys, return_inverse=True)
+        gc = torch.zeros(gk.numel(), dtype=torch.int64, device=gk.device).index_add_(0, ginv, cnts.to(torch.int64))
+        cnt = gc[torch.searchsorted(gk, uq.to(gk.device))].to(dev)
+    ua_freq = cnt[inv].clamp(max=2**31 - 1).to(torch.int32).contiguous()
+    fo, fc = strcol("fulluri")
+    _, ulen, uent = sops.string_features(fo, fc)
+    keys = {"time": tkey, "ua_freq": ua_freq, "uri_ent": ops.f32_keys(uent), "uri_len": ulen}
+    ar, n_glob = None, n
+    if comm is not None and comm.world > 1:
+        ar = comm.allreduce_np
+        n_glob = int(comm.allreduce_np(np.array([n], np.int64))[0])
+    cuts = {name: ops.quantile_cuts(keys[name], fr, ar, n_glob) for name, fr, _ in BINNED}
+    raws = {"method": _codes_by_hash(cols["reqmethod"], dev, method_code),
+            "ctype": _codes_by_hash(cols["resconttype"], dev, ctype_class),
+            "respcode": torch.from_numpy(np.asarray(cols["respcode"]).astype(np.int32)).to(dev)}
+    words = sops.pack_words([keys[nm] for nm, _, _ in BINNED], [cuts[nm] for nm, _, _ in BINNED],
+                            [s for _, _, s in BINNED], [raws[nm] for nm, _, _ in RAW], [m for _, m, _ in RAW],
+                            [s for _, _, s in RAW], raw8=top, r8mask=3, r8shift=TOP_SHIFT)
+    return words, cuts
+
+
+def run_proxy(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxresults: int = 3000,
+              alpha: float | None = None, beta: float = 0.01, seed: int = 0x0D15EA5E, chunk_len: int = 256,
+              device="cpu", comm: Comm | None = None, top_domains=None, feedback: dict | None = None,
+              dupfactor: int = 1000, row_offset: int = 0, eval_every: int = 0, ckpt=None,
+              log=None) -> common.SingleResult:
+    t = {}
+    t0 = time.perf_counter()
+    topset = top_set(top_domains)
+    words, cuts = featurize(cols, device, comm, topset)
+    dev = words.device
+    docs = torch.from_numpy(np.asarray(cols["clientip"], np.uint32).astype(np.int64)).to(dev)
+    t["featurize_s"] = time.perf_counter() - t0
+    fb = None
+    if feedback and len(feedback.get("clientip", [])):
+        fw, _ = featurize(feedback, device, None, topset)
+        fdoc = torch.from_numpy(np.asarray(feedback["clientip"], np.uint32).astype(np.int64)).to(dev)
+        fb = (fdoc, fw, torch.full_like(fw, int(dupfactor)))
+    res = common.run_single_doc_events(docs, words, K, sweeps, tol, maxresults, alpha, beta, seed, chunk_len, comm,
+                                       feedback=fb, row_offset=row_offset, eval_every=eval_every, ckpt=ckpt, log=log,
+                                       timings=t)
+    res.stats["cuts"] = {k: [int(x) for x in v] for k, v in cuts.items()}
+    return res

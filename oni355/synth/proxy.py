@@ -1,0 +1,141 @@
+"""Seeded synthetic web-proxy day (Bluecoat access-log fields) with planted anomalies.
+
+Documents are client IPs; profiles differ in hosts, methods, content types, user agents, URI
+shapes and time of day. Planted anomalies: rare user agent + POST of long high-entropy URIs to a
+non-top host at night (C2 beaconing / exfiltration shape). :func:`write_log` renders the day as a
+Bluecoat ``#Fields:`` access log so the C++ log tokenizer is exercised end to end.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from ..store.columnar import StringColumn
+
+_UAS = ["Mozilla/5.0 (Windows NT 10.0; Win64; x64) AppleWebKit/537.36 Chrome/51.0 Safari/537.36",
+        "Mozilla/5.0 (Macintosh; Intel Mac OS X 10_11_5) AppleWebKit/601.6.17 Safari/601.6.17",
+        "Mozilla/5.0 (Windows NT 6.1; Trident/7.0; rv:11.0) like Gecko",
+        "Microsoft-CryptoAPI/6.1", "Windows-Update-Agent/7.9", "curl/7.47.0", "okhttp/3.2.0",
+        "Mozilla/5.0 (iPhone; CPU iPhone OS 9_3 like Mac OS X) Mobile/13E238"]
+_HOSTS = {"web": ["www.google.com", "www.bbc.co.uk", "en.wikipedia.org", "www.amazon.com", "news.yahoo.com"],
+          "cdn": ["d1.cloudfront.net", "a248.e.akamai.net", "static.xx.fbcdn.net"],
+          "update": ["download.windowsupdate.com", "ctldl.windowsupdate.com", "swcdn.apple.com"],
+          "api": ["api.github.com", "graph.facebook.com", "api.twitter.com"],
+          "video": ["r3---sn.googlevideo.com", "video.twimg.com"]}
+_CTYPES = {"web": ["text/html", "text/css", "application/javascript", "image/png"],
+           "cdn": ["image/jpeg", "image/gif", "application/javascript"],
+           "update": ["application/octet-stream", "application/x-cab-compressed"],
+           "api": ["application/json"], "video": ["video/mp4"]}
+_PROFILES = [  # (hosts, methods, method weights, ua indices, peak hour, hour sd)
+    ("web", ["GET", "POST"], [0.9, 0.1], [0, 1, 2, 7], 13, 3.5),
+    ("cdn", ["GET"], [1.0], [0, 1, 2, 7], 14, 4.0),
+    ("update", ["GET", "HEAD"], [0.8, 0.2], [3, 4], 3, 2.0),
+    ("api", ["GET", "POST", "PUT"], [0.6, 0.3, 0.1], [5, 6], 11, 4.0),
+    ("video", ["GET"], [1.0], [0, 1, 7], 20, 2.0),
+]
+
+PROXY_FIELDS = ["date", "time", "time-taken", "c-ip", "cs-username", "cs-auth-group", "x-exception-id",
+                "sc-filter-result", "cs-categories", "cs(Referer)", "sc-status", "s-action", "cs-method",
+                "rs(Content-Type)", "cs-uri-scheme", "cs-host", "cs-uri-port", "cs-uri-path", "cs-uri-query",
+                "cs-uri-extension", "cs(User-Agent)", "s-ip", "sc-bytes", "cs-bytes", "x-virus-id"]
+
+
+@dataclass
+class ProxyDay:
+    cols: dict
+    anomaly_rows: np.ndarray
+
+    @property
+    def n(self) -> int:
+        return int(len(self.cols["clientip"]))
+
+
+def generate_proxy(n: int, seed: int = 9, n_clients: int | None = None, alpha_true: float = 0.15,
+                   n_anomalies: int | None = None, rank: int = 0, date: str = "2016-07-08") -> ProxyDay:
+    rng = np.random.default_rng([seed, rank])
+    hrng = np.random.default_rng([seed, 0xB1])
+    P = len(_PROFILES)
+    if n_clients is None:
+        n_clients = max(32, n // 50)
+    if n_anomalies is None:
+        n_anomalies = max(5, min(200, n // 20000))
+    theta = hrng.dirichlet(np.full(P, alpha_true), size=n_clients)
+    w = 1.0 / np.power(np.arange(1, n_clients + 1), 1.1)
+    w = w[hrng.permutation(n_clients)]
+    w /= w.sum()
+    cli = rng.choice(n_clients, size=n, p=w)
+    cum = np.cumsum(theta, axis=1)
+    cum[:, -1] = 1
+    z = np.clip(np.searchsorted((cum + np.arange(n_clients)[:, None]).ravel(), cli + rng.random(n), side="right")
+                - cli * P, 0, P - 1)
+    host, method, ua, ctype, path = [""] * n, [""] * n, [""] * n, [""] * n, [""] * n
+    hour_f = np.zeros(n)
+    for k, (key, meths, mw, uas, peak, hsd) in enumerate(_PROFILES):
+        idx = np.nonzero(z == k)[0]
+        m = idx.size
+        if not m:
+            continue
+        hs, cts = _HOSTS[key], _CTYPES[key]
+        hsel = rng.integers(0, len(hs), m)
+        csel = rng.integers(0, len(cts), m)
+        msel = rng.choice(len(meths), size=m, p=np.asarray(mw) / np.sum(mw))
+        usel = rng.choice(uas, size=m)
+        depth = rng.integers(1, 4, m)
+        hour_f[idx] = rng.normal(peak, hsd, m)
+        for j, i in enumerate(idx):
+            host[i], ctype[i], method[i], ua[i] = hs[hsel[j]], cts[csel[j]], meths[msel[j]], _UAS[usel[j]]
+            path[i] = "/" + "/".join(f"p{rng.integers(0, 50)}" for _ in range(depth[j])) + ".html"
+    status = np.where(rng.random(n) < 0.92, 200, rng.choice([304, 404, 302, 500], size=n))
+    hour = np.mod(np.floor(hour_f), 24).astype(int)
+    anomaly_rows = np.sort(rng.choice(n, size=min(n_anomalies, n), replace=False))
+    quiet = np.argsort(w)[: max(1, n_clients // 10)]
+    for i in anomaly_rows:
+        cli[i] = quiet[rng.integers(0, quiet.size)]
+        host[i] = f"x{rng.integers(1000, 9999)}.badcdn-sync.biz"
+        method[i] = "POST"
+        ua[i] = f"Mozilla/4.0 (compatible; agent-{rng.integers(10**6, 10**7)})"
+        ctype[i] = "application/x-www-form-urlencoded"
+        path[i] = "/" + "".join(chr(c) for c in rng.choice(np.frombuffer(b"abcdefABCDEF0123456789+/=", np.uint8), 120))
+        hour[i] = 3
+        status[i] = 200
+    minute = rng.integers(0, 60, n)
+    sec = rng.integers(0, 60, n)
+    ptime = [f"{h:02d}:{m:02d}:{s:02d}" for h, m, s in zip(hour, minute, sec)]
+    client = ((10 << 24) | (2 << 16) | cli).astype(np.uint32)
+    fulluri = [f"http://{h}{p}" for h, p in zip(host, path)]
+    cols = {
+        "p_date": StringColumn.from_list([date] * n), "p_time": StringColumn.from_list(ptime),
+        "clientip": client, "host": StringColumn.from_list(host), "reqmethod": StringColumn.from_list(method),
+        "useragent": StringColumn.from_list(ua), "resconttype": StringColumn.from_list(ctype),
+        "duration": rng.integers(1, 5000, n).astype(np.int64), "username": StringColumn.from_list(["-"] * n),
+        "authgroup": StringColumn.from_list(["-"] * n), "exceptionid": StringColumn.from_list(["-"] * n),
+        "filterresult": StringColumn.from_list(["OBSERVED"] * n), "webcat": StringColumn.from_list(["-"] * n),
+        "referer": StringColumn.from_list(["-"] * n), "respcode": status.astype(np.int32),
+        "action": StringColumn.from_list(["TCP_NC_MISS"] * n), "urischeme": StringColumn.from_list(["http"] * n),
+        "uriport": np.full(n, 80, np.int32), "uripath": StringColumn.from_list(path),
+        "uriquery": StringColumn.from_list(["-"] * n), "uriextension": StringColumn.from_list(["html"] * n),
+        "serverip": np.full(n, (93 << 24) | 1, np.uint32), "scbytes": rng.integers(200, 200000, n).astype(np.int64),
+        "csbytes": rng.integers(100, 2000, n).astype(np.int64), "virusid": StringColumn.from_list(["-"] * n),
+        "bcappname": StringColumn.from_list(["-"] * n), "bcappoperation": StringColumn.from_list(["-"] * n),
+        "fulluri": StringColumn.from_list(fulluri),
+    }
+    return ProxyDay(cols=cols, anomaly_rows=anomaly_rows)
+
+
+def write_log(day: ProxyDay, path: str) -> None:
+    """Bluecoat main-format access log with a #Fields header."""
+    from ..io.results import ip_str
+    c = day.cols
+    order = ["p_date", "p_time", "duration", "clientip", "username", "authgroup", "exceptionid", "filterresult",
+             "webcat", "referer", "respcode", "action", "reqmethod", "resconttype", "urischeme", "host", "uriport",
+             "uripath", "uriquery", "uriextension", "useragent", "serverip", "scbytes", "csbytes", "virusid"]
+    with open(path, "w") as f:
+        f.write("#Software: SGOS 6.5\n#Fields: " + " ".join(PROXY_FIELDS) + "\n")
+        for i in range(day.n):
+            vals = []
+            for name in order:
+                v = c[name]
+                s = v[i] if hasattr(v, "offsets") else (ip_str(v[i]) if name in ("clientip", "serverip") else str(v[i]))
+                vals.append(f'"{s}"' if (" " in s or s == "") else s)
+            f.write(" ".join(vals) + "\n")

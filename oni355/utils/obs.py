@@ -1,0 +1,104 @@
+"""Observability: stage timers (HIP-event backed on device), roctx ranges, JSON-lines metrics
+(SURVEY.md §5.1 / §5.5). The reference wrapped ml_ops.sh steps in ``time`` and relied on Spark UI
+and lda-c's printed likelihoods; here every run appends one structured record to metrics.jsonl.
+"""
+from __future__ import annotations
+
+import contextlib
+import ctypes
+import json
+import os
+import threading
+import time
+
+_roctx = None
+_roctx_lock = threading.Lock()
+
+
+def _load_roctx():
+    global _roctx
+    with _roctx_lock:
+        if _roctx is None:
+            for name in ("libroctx64.so", "/opt/rocm/lib/libroctx64.so"):
+                try:
+                    lib = ctypes.CDLL(name)
+                    lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
+                    lib.roctxRangePop.argtypes = []
+                    _roctx = lib
+                    break
+                except OSError:
+                    continue
+            if _roctx is None:
+                _roctx = False
+    return _roctx
+
+
+@contextlib.contextmanager
+def range_(name: str):
+    """roctx range (visible in rocprofv3 --marker-trace); no-op if roctx is unavailable."""
+    lib = _load_roctx() if os.environ.get("ONI_ROCTX", "1") == "1" else False
+    if lib:
+        lib.roctxRangePushA(name.encode())
+    try:
+        yield
+    finally:
+        if lib:
+            lib.roctxRangePop()
+
+
+class StageTimer:
+    """Wall-clock stage timer; with ``device`` set, brackets stages with HIP events."""
+
+    def __init__(self, device=None):
+        self.device = device
+        self.wall: dict[str, float] = {}
+        self._events: list = []
+
+    @contextlib.contextmanager
+    def stage(self, name: str):
+        import torch
+        use_ev = self.device is not None and getattr(self.device, "type", "") == "cuda"
+        if use_ev:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        t0 = time.perf_counter()
+        with range_(name):
+            yield
+        if use_ev:
+            e1.record()
+            self._events.append((name, e0, e1))
+        self.wall[name] = self.wall.get(name, 0.0) + time.perf_counter() - t0
+
+    def device_ms(self) -> dict[str, float]:
+        import torch
+        if self._events:
+            torch.cuda.synchronize(self.device)
+        out: dict[str, float] = {}
+        for name, e0, e1 in self._events:
+            out[name] = out.get(name, 0.0) + e0.elapsed_time(e1)
+        return out
+
+
+class MetricsLog:
+    """Append-only JSON-lines sink."""
+
+    def __init__(self, path: str):
+        self.path = path
+        os.makedirs(os.path.dirname(os.path.abspath(path)) or ".", exist_ok=True)
+
+    def write(self, rec: dict) -> None:
+        rec = {"ts": time.time(), **rec}
+        with open(self.path, "a") as f:
+            f.write(json.dumps(rec, default=_default) + "\n")
+
+
+def _default(o):
+    try:
+        import numpy as np
+        if isinstance(o, np.generic):
+            return o.item()
+        if isinstance(o, np.ndarray):
+            return o.tolist()
+    except ImportError:  # pragma: no cover
+        pass
+    return str(o)
