@@ -1,0 +1,132 @@
+"""Parallel ingest (oni-ingest master_collector.py + worker.py).
+
+Reference: a watchdog Observer publishes each new file path to a Kafka topic; N worker processes
+consume partitions, decode (nfdump / tshark), ``hadoop fs -put`` and load Hive parquet partitions.
+
+Here (single node, no Kafka/HDFS): a collector polls ``collector_path`` for files matching
+``supported_files``, waits until a file's size is stable, and hands it to a thread pool; each
+worker decodes with the native C++ decoders (which release the GIL) and appends the rows to the
+day-partitioned columnar store, split by the UTC day of each row's timestamp. Processed files are
+recorded in ``<collector_path>/.oni_ingested`` (idempotent restarts) and optionally moved away.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import datetime as _dt
+import fnmatch
+import json
+import os
+import shutil
+import threading
+import time
+
+import numpy as np
+
+from ..store import columnar
+
+DEFAULT_PATTERNS = {"flow": ["nfcapd.*", "*.csv"], "dns": ["*.pcap", "*.pcapng"], "proxy": ["*.log"]}
+
+
+def decode_file(source: str, path: str) -> dict:
+    from ..io import decoders
+    if source == "flow":
+        if path.endswith(".csv") or path.endswith(".txt"):
+            return decoders.read_flow_csv(path)[0]
+        from ..io import nfcapd
+        return nfcapd.read_nfcapd(path)
+    if source == "dns":
+        return {k: v for k, v in decoders.read_pcap_dns(path).items() if not k.startswith("_")}
+    return {k: v for k, v in decoders.read_proxy_log(path).items() if not k.startswith("_")}
+
+
+def _row_days(source: str, cols: dict) -> np.ndarray:
+    if source in ("flow", "dns"):
+        t = np.asarray(cols["unix_tstamp"], np.int64)
+        return (t // 86400).astype(np.int64)
+    d = cols["p_date"].to_list()
+    return np.array([(_dt.date.fromisoformat(x) - _dt.date(1970, 1, 1)).days if x else 0 for x in d], np.int64)
+
+
+def store_rows(root: str, source: str, cols: dict) -> dict[str, int]:
+    """Append decoded rows to their day partitions; returns {YYYYMMDD: rows}."""
+    days = _row_days(source, cols)
+    out = {}
+    for day in np.unique(days):
+        idx = np.nonzero(days == day)[0]
+        part = {k: (v[idx] if not hasattr(v, "offsets") else v[idx]) for k, v in cols.items()}
+        date = (_dt.date(1970, 1, 1) + _dt.timedelta(days=int(day))).strftime("%Y%m%d")
+        columnar.append_part(root, source, date, part)
+        out[date] = int(idx.size)
+    return out
+
+
+class Collector:
+    def __init__(self, source: str, collector_path: str, data_root: str, patterns=None, workers: int = 4,
+                 move_to: str | None = None, log=print):
+        self.source = source
+        self.path = collector_path
+        self.root = data_root
+        self.patterns = patterns or DEFAULT_PATTERNS[source]
+        self.pool = cf.ThreadPoolExecutor(max_workers=workers)
+        self.move_to = move_to
+        self.log = log
+        self.state_file = os.path.join(collector_path, ".oni_ingested")
+        self.done = set()
+        if os.path.exists(self.state_file):
+            with open(self.state_file) as f:
+                self.done = {ln.strip() for ln in f if ln.strip()}
+        self.lock = threading.Lock()
+        self.sizes: dict[str, int] = {}
+        self.stats = {"files": 0, "rows": 0, "errors": 0}
+
+    def _candidates(self) -> list[str]:
+        out = []
+        for name in sorted(os.listdir(self.path)):
+            p = os.path.join(self.path, name)
+            if name.startswith(".") or not os.path.isfile(p) or name in self.done:
+                continue
+            if any(fnmatch.fnmatch(name, pat) for pat in self.patterns):
+                out.append(p)
+        return out
+
+    def _stable(self, p: str) -> bool:
+        s = os.path.getsize(p)
+        prev = self.sizes.get(p)
+        self.sizes[p] = s
+        return prev == s
+
+    def _work(self, p: str) -> dict:
+        t0 = time.perf_counter()
+        cols = decode_file(self.source, p)  # parallel: the C++ decoders release the GIL
+        with self.lock:  # part numbering is per day directory: serialise the appends
+            per_day = store_rows(self.root, self.source, cols)
+            name = os.path.basename(p)
+            self.done.add(name)
+            with open(self.state_file, "a") as f:
+                f.write(name + "\n")
+            self.stats["files"] += 1
+            self.stats["rows"] += sum(per_day.values())
+        if self.move_to:
+            os.makedirs(self.move_to, exist_ok=True)
+            shutil.move(p, os.path.join(self.move_to, os.path.basename(p)))
+        rec = {"file": p, "days": per_day, "seconds": time.perf_counter() - t0}
+        self.log(json.dumps(rec))
+        return rec
+
+    def run_once(self, wait_stable: bool = False) -> list[dict]:
+        files = [p for p in self._candidates() if (not wait_stable or self._stable(p))]
+        futs = [self.pool.submit(self._work, p) for p in files]
+        out = []
+        for f in futs:
+            try:
+                out.append(f.result())
+            except Exception as e:  # noqa: BLE001 - keep the collector alive, report the file
+                self.stats["errors"] += 1
+                self.log(json.dumps({"error": str(e)}))
+        return out
+
+    def watch(self, interval: float = 5.0, stop: threading.Event | None = None) -> None:
+        stop = stop or threading.Event()
+        while not stop.is_set():
+            self.run_once(wait_stable=True)
+            stop.wait(interval)
