@@ -22,7 +22,7 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--sweeps", type=int, default=20)
     ap.add_argument("--burn", type=int, default=30)
-    ap.add_argument("--modes", default="atomic,recount")
+    ap.add_argument("--modes", default="atomic,recount,recount+qpf")
     ap.add_argument("--chunk-len", type=int, default=256)
     a = ap.parse_args()
     import numpy as np
@@ -46,7 +46,8 @@ def main() -> int:
     c = run.corpus
     print(json.dumps({"corpus": c.stats()}), flush=True)
     modes = a.modes.split(",")
-    models = {m: GibbsLDA(c, GibbsConfig(K=a.topics, count_mode=m)) for m in modes}
+    models = {m: GibbsLDA(c, GibbsConfig(K=a.topics, count_mode=m.split("+")[0], prefetch_q="qpf" in m))
+              for m in modes}
     for m in models.values():
         m.initialize()
         m.sweep(a.burn)
@@ -79,7 +80,7 @@ def main() -> int:
                 ev[0].record()
                 if stage == 0:
                     ops.gibbs_pass(m._state(False), m.G, m.KP, m.K, m.alpha, m.cfg.seed, False, m.sweep_ctr,
-                                   c.chunk_len, atomic=atomic)
+                                   c.chunk_len, atomic=atomic, prefetch_q=m.cfg.prefetch_q)
                 elif stage == 1 and not atomic:
                     ops.recount(c.wsorted, c.wslot, m.tok_z, m.dn[m.b][: m.V * m.KS].view(m.V, m.KS), m.KS)
                 elif stage == 2:

@@ -67,7 +67,7 @@ __device__ __forceinline__ void load_row_f(const float* __restrict__ p, float (&
   }
 }
 
-template <int G, int KP, bool INIT, bool ATOMIC>
+template <int G, int KP, bool INIT, bool ATOMIC, bool QPF>
 __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
   constexpr int S = oni::kWave / G;
   constexpr int KS = G * KP;
@@ -106,6 +106,11 @@ __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
   // sampling, so their latency hides behind the math and stores of step s
   uint32_t w_nx = len > 0 ? a.tok_word[off + c] : oni::kPadWord;
   int z_nx = (!INIT && len > 0) ? (int)a.tok_z[off + c] : 0;
+  // QPF: the next token's q row is also fetched one step ahead (needs only its word id)
+  float qn[KP];
+#pragma unroll
+  for (int j = 0; j < KP; ++j) qn[j] = 0.f;
+  if (QPF && !INIT && w_nx != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)w_nx * KS + kbase, qn);
   for (int s = 0; s < len; ++s) {
     const int64_t idx = off + (int64_t)s * S + c;
     const uint32_t w = w_nx;
@@ -130,7 +135,12 @@ __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
 #pragma unroll
       for (int j = 0; j < KP; ++j) n[j] -= (kbase + j == zo);
       if (w != wprev) {
-        load_row_f<KP>(a.q + (int64_t)w * KS + kbase, qv);
+        if (QPF) {
+#pragma unroll
+          for (int j = 0; j < KP; ++j) qv[j] = qn[j];
+        } else {
+          load_row_f<KP>(a.q + (int64_t)w * KS + kbase, qv);
+        }
         wprev = w;
       }
       float loc[KP];
@@ -170,6 +180,8 @@ __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
           atomicAdd(&a.dnwk[(int64_t)w * KS + zn], 1);
         }
       }
+      if (QPF && s + 1 < len && w_nx != w && w_nx != oni::kPadWord)
+        load_row_f<KP>(a.q + (int64_t)w_nx * KS + kbase, qn);
     }
   }
 
@@ -275,16 +287,18 @@ __global__ void k_copy_rows(const int32_t* __restrict__ src, int32_t* __restrict
 }
 
 template <int G, int KP>
-int launch_gibbs(const OniGibbs& a, bool init, bool atomic, hipStream_t s) {
+int launch_gibbs(const OniGibbs& a, bool init, bool atomic, bool qpf, hipStream_t s) {
   if (a.KS != G * KP) return (int)hipErrorInvalidValue;
   const unsigned grid = (unsigned)((a.n_slices + kWavesPerBlock - 1) / kWavesPerBlock);
   if (grid == 0) return 0;
   if (init) {
-    if (atomic) k_gibbs<G, KP, true, true><<<grid, kBlock, 0, s>>>(a);
-    else k_gibbs<G, KP, true, false><<<grid, kBlock, 0, s>>>(a);
+    k_gibbs<G, KP, true, true, false><<<grid, kBlock, 0, s>>>(a);  // init always builds n_wk by atomics
+  } else if (atomic) {
+    k_gibbs<G, KP, false, true, false><<<grid, kBlock, 0, s>>>(a);
+  } else if (qpf && G == 1) {
+    k_gibbs<G, KP, false, false, (G == 1)><<<grid, kBlock, 0, s>>>(a);
   } else {
-    if (atomic) k_gibbs<G, KP, false, true><<<grid, kBlock, 0, s>>>(a);
-    else k_gibbs<G, KP, false, false><<<grid, kBlock, 0, s>>>(a);
+    k_gibbs<G, KP, false, false, false><<<grid, kBlock, 0, s>>>(a);
   }
   return (int)hipGetLastError();
 }
@@ -324,10 +338,10 @@ __global__ __launch_bounds__(256) void k_recount(const int32_t* __restrict__ wso
 }  // namespace
 
 // Supported (G, KP) configurations. K ≤ 32: G = 1 (KP = K rounded up to 4).
-ONI_API int oni_gibbs_launch(const OniGibbs* a, int G, int KP, int init, int atomic, hipStream_t s) {
+ONI_API int oni_gibbs_launch(const OniGibbs* a, int G, int KP, int init, int atomic, int qpf, hipStream_t s) {
   if (a->K < 1 || a->K > 255 || a->K > a->KS) return (int)hipErrorInvalidValue;
 #define ONI_CASE(g_, kp_) \
-  if (G == g_ && KP == kp_) return launch_gibbs<g_, kp_>(*a, init != 0, atomic != 0, s);
+  if (G == g_ && KP == kp_) return launch_gibbs<g_, kp_>(*a, init != 0, atomic != 0, qpf != 0, s);
   ONI_CASE(1, 4) ONI_CASE(1, 8) ONI_CASE(1, 12) ONI_CASE(1, 16) ONI_CASE(1, 20) ONI_CASE(1, 24) ONI_CASE(1, 28)
   ONI_CASE(1, 32)
   ONI_CASE(4, 8) ONI_CASE(4, 12) ONI_CASE(4, 16)

@@ -35,6 +35,7 @@ class GibbsConfig:
     seed: int = 0x0D15EA5E
     use_graph: bool = True
     count_mode: str = "recount"  # "recount" (word-sorted LDS histogram) | "atomic" (per-token Δ atomics)
+    prefetch_q: bool = True      # K<=32: fetch the next token's q row one step ahead
 
     def resolved_alpha(self) -> float:
         return float(self.alpha) if self.alpha is not None else 50.0 / self.K
@@ -122,7 +123,8 @@ class GibbsLDA:
         ops.copy_rows(self.ndk[self.a], self.ndk[1 - self.a], c.long_rows, self.KS)
         atomic = self.cfg.count_mode == "atomic"
         ops.gibbs_pass(self._state(False), self.G, self.KP, self.K, self.alpha, self.cfg.seed, False,
-                       self.sweep_ctr, c.chunk_len, host_sweep=self.sweeps_done + 1, atomic=atomic)
+                       self.sweep_ctr, c.chunk_len, host_sweep=self.sweeps_done + 1, atomic=atomic,
+                       prefetch_q=self.cfg.prefetch_q)
         if not atomic:
             # dn[b] head := this rank's n_wk rebuilt from z (tail keeps Δn_k)
             ops.recount(c.wsorted, c.wslot, self.tok_z, self.dn[self.b][: self.V * self.KS].view(self.V, self.KS),

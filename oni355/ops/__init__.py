@@ -226,7 +226,8 @@ def sell_perm_z(chunk_doc, chunk_pos0, chunk_len, S, slice_off, doc_tok_ptr, tok
 # sampler
 # ------------------------------------------------------------------------------------------------
 def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init: bool, sweep_ctr: torch.Tensor,
-               chunk_len: torch.Tensor, host_sweep: int | None = None, atomic: bool = True) -> None:
+               chunk_len: torch.Tensor, host_sweep: int | None = None, atomic: bool = True,
+               prefetch_q: bool = False) -> None:
     """Launch one init/sweep pass. ``st`` holds the OniGibbs tensors (see csrc/kernels/gibbs.hip).
 
     ``atomic``: accumulate Δn_wk with per-token atomics; otherwise the caller rebuilds n_wk with
@@ -253,7 +254,8 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
         setattr(a, name, _lib.ptr(st[name]))
     a.sweep_ctr = _lib.ptr(sweep_ctr)
     a.n_slices, a.K, a.KS, a.alpha, a.seed0, a.seed1 = n_slices, K, KS, float(alpha), s0, s1
-    _lib.check(_lib.lib().oni_gibbs_launch(C.byref(a), G, KP, 1 if init else 0, 1 if atomic else 0, _lib.stream()),
+    _lib.check(_lib.lib().oni_gibbs_launch(C.byref(a), G, KP, 1 if init else 0, 1 if atomic else 0,
+                                           1 if prefetch_q else 0, _lib.stream()),
                "oni_gibbs_launch")
 
 

@@ -56,12 +56,12 @@ def _toy_tokens(n_docs, V, seed, heavy=True):
         lens[0] = 5000  # forces a multi-chunk doc
     tdoc = np.repeat(np.arange(n_docs), lens)
     tword = (r.zipf(1.3, tdoc.size) - 1) % V
-    keys = r.permutation(2**31 - 1)[:n_docs].astype(np.int32)
+    keys = ((np.arange(n_docs, dtype=np.int64) * 2654435761 + seed) % (2**31 - 1)).astype(np.int32)  # distinct
     return torch.from_numpy(tdoc), torch.from_numpy(tword), keys
 
 
-@pytest.mark.parametrize("K,mode", [(20, "recount"), (20, "atomic"), (7, "recount"), (50, "recount"),
-                                    (100, "atomic"), (100, "recount")])
+@pytest.mark.parametrize("K,mode", [(20, "recount"), (20, "recount+noqpf"), (20, "atomic"), (7, "recount"),
+                                    (50, "recount"), (100, "atomic"), (100, "recount")])
 def test_gibbs_bitwise_vs_oracle(gpu, K, mode):
     tdoc, tword, keys = _toy_tokens(300, 400, K)
     G, KP = ops.choose_tiling(K)
@@ -70,7 +70,8 @@ def test_gibbs_bitwise_vs_oracle(gpu, K, mode):
     assert torch.equal(cc.tok_word, cg.tok_word.cpu())
     assert torch.equal(cc.chunk_doc, cg.chunk_doc.cpu())
     mc = GibbsLDA(cc, GibbsConfig(K=K, seed=1234, use_graph=False, count_mode="atomic"))
-    mg = GibbsLDA(cg, GibbsConfig(K=K, seed=1234, use_graph=False, count_mode=mode))
+    mg = GibbsLDA(cg, GibbsConfig(K=K, seed=1234, use_graph=False, count_mode=mode.split("+")[0],
+                                  prefetch_q="noqpf" not in mode))
     mc.initialize()
     mg.initialize()
     assert torch.equal(mc.tok_z, mg.tok_z.cpu())
