@@ -22,8 +22,9 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--sweeps", type=int, default=20)
     ap.add_argument("--burn", type=int, default=30)
-    ap.add_argument("--modes", default="atomic,recount,recount+qpf")
+    ap.add_argument("--modes", default="recount+qpf,delta+qpf,delta")
     ap.add_argument("--chunk-len", type=int, default=256)
+    ap.add_argument("--chunk-lens", default="", help="extra A/B: comma list of L values (delta+qpf)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -76,22 +77,46 @@ def main() -> int:
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
             ts = []
             for _ in range(5):
-                atomic = m.cfg.count_mode == "atomic"
                 ev[0].record()
+                head = m.dn[m.b][: m.V * m.KS].view(m.V, m.KS)
                 if stage == 0:
                     ops.gibbs_pass(m._state(False), m.G, m.KP, m.K, m.alpha, m.cfg.seed, False, m.sweep_ctr,
-                                   c.chunk_len, atomic=atomic, prefetch_q=m.cfg.prefetch_q)
-                elif stage == 1 and not atomic:
-                    ops.recount(c.wsorted, c.wslot, m.tok_z, m.dn[m.b][: m.V * m.KS].view(m.V, m.KS), m.KS)
+                                   c.chunk_len, mode=m.mode, prefetch_q=m.cfg.prefetch_q,
+                                   chg_mask=getattr(m, "chg_mask", None))
+                elif stage == 1 and m.mode == 0:
+                    ops.recount(c.wsorted, c.wslot, m.tok_z, head, m.KS)
+                elif stage == 1 and m.mode == 2:
+                    ops.delta_recount(c.wslot, c.tile_wlo, c.tile_whi, m.chg_mask, c.tok_word, m.tok_z, m.tok_zprev,
+                                      head, m.KS, m.G)
                 elif stage == 2:
                     ops.gibbs_apply(m.nwk, m.dn[m.b], m.dn[1 - m.b], m.nk[m.cn], m.nk[1 - m.cn], m.q, m.V, m.K, m.KS,
-                                    m.beta, m.vbeta, m.sweep_ctr, bump=False, absolute=not atomic)
+                                    m.beta, m.vbeta, m.sweep_ctr, bump=False, absolute=m.mode == 0)
                 ev[1].record()
                 torch.cuda.synchronize()
                 ts.append(ev[0].elapsed_time(ev[1]))
             st[["sample", "recount", "apply"][stage]] = float(np.median(ts))
         out[name]["stages_ms"] = st
     print(json.dumps(out), flush=True)
+    # chunk-length sweep (the sampler's serial critical path is L steps per lane)
+    for L in [int(x) for x in a.chunk_lens.split(",") if x]:
+        del models
+        torch.cuda.empty_cache()
+        rl = common.build_and_train(dk, wk, None, vocab, a.topics, None, 0.01, 0x0D15EA5E, 0, L, None, train=False)
+        m = GibbsLDA(rl.corpus, GibbsConfig(K=a.topics, count_mode="delta", prefetch_q=True))
+        m.initialize()
+        m.sweep(a.burn)
+        ts = []
+        for _ in range(a.rounds):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            m.sweep(a.sweeps)
+            torch.cuda.synchronize()
+            ts.append((time.perf_counter() - t0) / a.sweeps * 1e3)
+        models = {}
+        print(json.dumps({"chunk_len": L, "median_ms": float(np.median(ts)), "min_ms": float(np.min(ts)),
+                          "slices": rl.corpus.n_slices, "long_docs": int(rl.corpus.long_rows.numel()),
+                          "loglik": m.log_likelihood()}), flush=True)
+        del m, rl
     return 0
 
 

@@ -38,6 +38,7 @@ struct OniGibbs {
   int32_t* dnwk;               // [V][KS] word-topic delta (init: the n_wk table itself)
   int32_t* dnk;                // [KS]    topic-total delta (init: n_k itself)
   const uint32_t* sweep_ctr;   // device scalar: current sweep number (≥ 1), graph-replay safe
+  uint64_t* chg_mask;          // MODE 2: one u64 per SELL step, bit c*G set if slot c's topic changed
   int64_t n_slices;
   int32_t K;
   int32_t KS;
@@ -67,8 +68,11 @@ __device__ __forceinline__ void load_row_f(const float* __restrict__ p, float (&
   }
 }
 
-template <int G, int KP, bool INIT, bool ATOMIC, bool QPF>
+// MODE: 0 = no n_wk bookkeeping (full recount afterwards), 1 = per-token Δ atomics,
+//       2 = changed-slot ballot mask per step (delta recount afterwards)
+template <int G, int KP, bool INIT, int MODE, bool QPF>
 __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
+  constexpr bool ATOMIC = MODE == 1;
   constexpr int S = oni::kWave / G;
   constexpr int KS = G * KP;
   __shared__ int32_t red[kWavesPerBlock][KS];
@@ -180,6 +184,11 @@ __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
           atomicAdd(&a.dnwk[(int64_t)w * KS + zn], 1);
         }
       }
+      if constexpr (MODE == 2) {
+        // lane 0 (c = 0) owns the slice's longest chunk, so it is active at every step
+        const uint64_t m = __ballot(zn != zo && g == 0);
+        if (lane == 0) a.chg_mask[(off + (int64_t)s * S) / S] = m;
+      }
       if (QPF && s + 1 < len && w_nx != w && w_nx != oni::kPadWord)
         load_row_f<KP>(a.q + (int64_t)w_nx * KS + kbase, qn);
     }
@@ -287,20 +296,75 @@ __global__ void k_copy_rows(const int32_t* __restrict__ src, int32_t* __restrict
 }
 
 template <int G, int KP>
-int launch_gibbs(const OniGibbs& a, bool init, bool atomic, bool qpf, hipStream_t s) {
+int launch_gibbs(const OniGibbs& a, bool init, int mode, bool qpf, hipStream_t s) {
   if (a.KS != G * KP) return (int)hipErrorInvalidValue;
   const unsigned grid = (unsigned)((a.n_slices + kWavesPerBlock - 1) / kWavesPerBlock);
   if (grid == 0) return 0;
+  constexpr bool Q = G == 1;  // the q-row prefetch variant exists for one-lane units only
   if (init) {
-    k_gibbs<G, KP, true, true, false><<<grid, kBlock, 0, s>>>(a);  // init always builds n_wk by atomics
-  } else if (atomic) {
-    k_gibbs<G, KP, false, true, false><<<grid, kBlock, 0, s>>>(a);
-  } else if (qpf && G == 1) {
-    k_gibbs<G, KP, false, false, (G == 1)><<<grid, kBlock, 0, s>>>(a);
+    k_gibbs<G, KP, true, 1, false><<<grid, kBlock, 0, s>>>(a);  // init always builds n_wk by atomics
+  } else if (mode == 1) {
+    k_gibbs<G, KP, false, 1, false><<<grid, kBlock, 0, s>>>(a);
+  } else if (mode == 2) {
+    if (qpf && Q) k_gibbs<G, KP, false, 2, Q><<<grid, kBlock, 0, s>>>(a);
+    else k_gibbs<G, KP, false, 2, false><<<grid, kBlock, 0, s>>>(a);
+  } else if (qpf && Q) {
+    k_gibbs<G, KP, false, 0, Q><<<grid, kBlock, 0, s>>>(a);
   } else {
-    k_gibbs<G, KP, false, false, false><<<grid, kBlock, 0, s>>>(a);
+    k_gibbs<G, KP, false, 0, false><<<grid, kBlock, 0, s>>>(a);
   }
   return (int)hipGetLastError();
+}
+
+// Delta recount (MODE 2): only tokens whose topic changed this sweep (per-step ballot masks,
+// an L2-resident bitmap: 1 bit per SELL slot) touch the z arrays. Tokens are visited in
+// word-sorted order; a changed token adds -1 at (w, z_prev) and +1 at (w, z) to the block's LDS
+// table and refreshes z_prev; non-zero cells are flushed as row-contiguous atomics into Δn_wk.
+// The word id of a changed token is re-read from the SELL word array (only ~5% of tokens), so
+// the per-token stream is the 4-byte slot index alone.
+__global__ __launch_bounds__(256) void k_delta_recount(const int32_t* __restrict__ wslot,
+                                                        const int32_t* __restrict__ tile_wlo,
+                                                        const int32_t* __restrict__ tile_whi,
+                                                        const uint64_t* __restrict__ mask,
+                                                        const uint32_t* __restrict__ tok_word,
+                                                        const uint8_t* __restrict__ tok_z,
+                                                        uint8_t* __restrict__ tok_zprev, int64_t T,
+                                                        int32_t* __restrict__ dnwk, int KS, int log2S, int G,
+                                                        int tile, int wmax) {
+  extern __shared__ __attribute__((aligned(16))) int32_t hst[];
+  const int64_t lo = (int64_t)blockIdx.x * tile;
+  if (lo >= T) return;
+  const int64_t hi = lo + tile < T ? lo + tile : T;
+  const int w_lo = tile_wlo[blockIdx.x], w_hi = tile_whi[blockIdx.x];
+  const int rows = (w_hi - w_lo + 1) < wmax ? (w_hi - w_lo + 1) : wmax;
+  const int cells = rows * KS;
+  for (int i = threadIdx.x; i < cells; i += blockDim.x) hst[i] = 0;
+  __syncthreads();
+  const int64_t Smask = (1ll << log2S) - 1;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const int64_t slot = __builtin_nontemporal_load(&wslot[i]);
+    const uint64_t m = mask[slot >> log2S];
+    const int bit = (int)(slot & Smask) * G;
+    if ((m >> bit) & 1ull) {
+      const int w = (int)tok_word[slot];
+      const int zn = tok_z[slot];
+      const int zo = tok_zprev[slot];
+      tok_zprev[slot] = (uint8_t)zn;
+      const int r = w - w_lo;
+      if (r < rows) {
+        atomicAdd(&hst[r * KS + zn], 1);
+        atomicAdd(&hst[r * KS + zo], -1);
+      } else {
+        atomicAdd(&dnwk[(int64_t)w * KS + zn], 1);
+        atomicAdd(&dnwk[(int64_t)w * KS + zo], -1);
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < cells; i += blockDim.x) {
+    const int v = hst[i];
+    if (v) atomicAdd(&dnwk[(int64_t)(w_lo + i / KS) * KS + (i % KS)], v);
+  }
 }
 
 // K11 (option B of SURVEY.md §7.4.3): rebuild the local n_wk table from z with NO global
@@ -338,10 +402,11 @@ __global__ __launch_bounds__(256) void k_recount(const int32_t* __restrict__ wso
 }  // namespace
 
 // Supported (G, KP) configurations. K ≤ 32: G = 1 (KP = K rounded up to 4).
-ONI_API int oni_gibbs_launch(const OniGibbs* a, int G, int KP, int init, int atomic, int qpf, hipStream_t s) {
-  if (a->K < 1 || a->K > 255 || a->K > a->KS) return (int)hipErrorInvalidValue;
+ONI_API int oni_gibbs_launch(const OniGibbs* a, int G, int KP, int init, int mode, int qpf, hipStream_t s) {
+  if (a->K < 1 || a->K > 255 || a->K > a->KS || mode < 0 || mode > 2) return (int)hipErrorInvalidValue;
+  if (mode == 2 && !a->chg_mask) return (int)hipErrorInvalidValue;
 #define ONI_CASE(g_, kp_) \
-  if (G == g_ && KP == kp_) return launch_gibbs<g_, kp_>(*a, init != 0, atomic != 0, qpf != 0, s);
+  if (G == g_ && KP == kp_) return launch_gibbs<g_, kp_>(*a, init != 0, mode, qpf != 0, s);
   ONI_CASE(1, 4) ONI_CASE(1, 8) ONI_CASE(1, 12) ONI_CASE(1, 16) ONI_CASE(1, 20) ONI_CASE(1, 24) ONI_CASE(1, 28)
   ONI_CASE(1, 32)
   ONI_CASE(4, 8) ONI_CASE(4, 12) ONI_CASE(4, 16)
@@ -368,6 +433,17 @@ ONI_API int oni_recount(const int32_t* wsorted, const int32_t* wslot, const uint
   if (tile < 256 || wmax < 1 || (size_t)wmax * KS * 4 > 64 * 1024) return (int)hipErrorInvalidValue;
   const unsigned grid = (unsigned)((T + tile - 1) / tile);
   k_recount<<<grid, 256, (size_t)wmax * KS * 4, s>>>(wsorted, wslot, tok_z, T, nwk, KS, tile, wmax);
+  return (int)hipGetLastError();
+}
+
+ONI_API int oni_delta_recount(const int32_t* wslot, const int32_t* tile_wlo, const int32_t* tile_whi,
+                              const uint64_t* mask, const uint32_t* tok_word, const uint8_t* tok_z, uint8_t* tok_zprev,
+                              int64_t T, int32_t* dnwk, int KS, int log2S, int G, int tile, int wmax, hipStream_t s) {
+  if (T == 0) return 0;
+  if (tile < 256 || wmax < 1 || (size_t)wmax * KS * 4 > 64 * 1024) return (int)hipErrorInvalidValue;
+  const unsigned grid = (unsigned)((T + tile - 1) / tile);
+  k_delta_recount<<<grid, 256, (size_t)wmax * KS * 4, s>>>(wslot, tile_wlo, tile_whi, mask, tok_word, tok_z, tok_zprev,
+                                                            T, dnwk, KS, log2S, G, tile, wmax);
   return (int)hipGetLastError();
 }
 

@@ -44,6 +44,8 @@ class Corpus:
     long_rows: torch.Tensor     # int32 [n_long] docs split over > 1 chunk
     wsorted: torch.Tensor | None = None  # int32 [T] word ids of all tokens, sorted (recount path)
     wslot: torch.Tensor | None = None    # int32 [T] SELL slot of each word-sorted token
+    tile_wlo: torch.Tensor | None = None  # int32 [n_tiles] first word of each recount tile
+    tile_whi: torch.Tensor | None = None  # int32 [n_tiles] last word of each recount tile
 
     @property
     def S(self) -> int:
@@ -152,12 +154,18 @@ def build_corpus(tdoc: torch.Tensor, tword: torch.Tensor, D: int, V: int, doc_ke
         raise ValueError("SELL slot index overflows int32")
     wsorted, worder = torch.sort(tok_word[slots], stable=True)
     wslot = slots[worder].to(torch.int32)
+    tile = ops.RECOUNT_TILE
+    starts = torch.arange(0, wsorted.numel(), tile, device=dev)
+    tile_wlo = wsorted[starts].to(torch.int32) if starts.numel() else torch.zeros(0, dtype=torch.int32, device=dev)
+    ends = torch.clamp(starts + tile - 1, max=max(wsorted.numel() - 1, 0))
+    tile_whi = wsorted[ends].to(torch.int32) if starts.numel() else torch.zeros(0, dtype=torch.int32, device=dev)
     return Corpus(D=D, V=V, T=T, G=G, L=L, doc_keys=doc_keys.to(torch.int32), pair_doc=pair_doc,
                   pair_word=pair_word, pair_cnt=cnt.to(torch.int32), doc_pair_ptr=doc_pair_ptr,
                   doc_tok_ptr=doc_tok_ptr, pair_tokoff=pair_tokoff.contiguous(), slice_off=slice_off,
                   slice_len=slice_len, chunk_doc=chunk_doc, chunk_pos0=chunk_pos0, chunk_len=chunk_len,
                   chunk_key=chunk_key, chunk_multi=chunk_multi, tok_word=tok_word, long_rows=long_rows,
-                  wsorted=wsorted.contiguous(), wslot=wslot.contiguous())
+                  wsorted=wsorted.contiguous(), wslot=wslot.contiguous(), tile_wlo=tile_wlo.contiguous(),
+                  tile_whi=tile_whi.contiguous())
 
 
 def canonical_tokens(c: Corpus) -> tuple[torch.Tensor, torch.Tensor]:

@@ -34,7 +34,9 @@ class GibbsConfig:
     beta: float = 0.01
     seed: int = 0x0D15EA5E
     use_graph: bool = True
-    count_mode: str = "recount"  # "recount" (word-sorted LDS histogram) | "atomic" (per-token Δ atomics)
+    # n_wk bookkeeping: "delta" (changed-slot masks + word-sorted delta recount; default),
+    # "recount" (full word-sorted LDS histogram every sweep) | "atomic" (per-token Δ atomics)
+    count_mode: str = "delta"
     prefetch_q: bool = True      # K<=32: fetch the next token's q row one step ahead
 
     def resolved_alpha(self) -> float:
@@ -68,6 +70,12 @@ class GibbsLDA:
         self.dn = [torch.zeros(V * KS + KS, dtype=i32, device=dev) for _ in range(2)]
         self.q = torch.zeros(V, KS, dtype=torch.float32, device=dev)
         self.sweep_ctr = torch.zeros(1, dtype=i32, device=dev)
+        if cfg.count_mode not in ("delta", "recount", "atomic"):
+            raise ValueError(f"unknown count_mode {cfg.count_mode}")
+        self.mode = {"recount": 0, "atomic": 1, "delta": 2}[cfg.count_mode]
+        if self.mode == 2:
+            self.tok_zprev = torch.zeros_like(self.tok_z)
+            self.chg_mask = torch.zeros(max(corpus.sell_slots // corpus.S, 1), dtype=torch.int64, device=dev)
         self.a = 0  # ndk parity
         self.b = 0  # delta-buffer parity
         self.cn = 0  # nk parity
@@ -103,6 +111,8 @@ class GibbsLDA:
         if self.comm is not None and self.comm.world > 1:
             self.comm.allreduce_(self.nwk)
             self.comm.allreduce_(self.nk[0])
+        if self.mode == 2:
+            self.tok_zprev.copy_(self.tok_z)
         self.sweeps_done = 0
         self._graph = None
         self._prime()
@@ -121,14 +131,17 @@ class GibbsLDA:
     def _one_sweep(self) -> None:
         c = self.c
         ops.copy_rows(self.ndk[self.a], self.ndk[1 - self.a], c.long_rows, self.KS)
-        atomic = self.cfg.count_mode == "atomic"
         ops.gibbs_pass(self._state(False), self.G, self.KP, self.K, self.alpha, self.cfg.seed, False,
-                       self.sweep_ctr, c.chunk_len, host_sweep=self.sweeps_done + 1, atomic=atomic,
-                       prefetch_q=self.cfg.prefetch_q)
-        if not atomic:
+                       self.sweep_ctr, c.chunk_len, host_sweep=self.sweeps_done + 1, mode=self.mode,
+                       prefetch_q=self.cfg.prefetch_q, chg_mask=getattr(self, "chg_mask", None))
+        head = self.dn[self.b][: self.V * self.KS].view(self.V, self.KS)
+        if self.mode == 0:
             # dn[b] head := this rank's n_wk rebuilt from z (tail keeps Δn_k)
-            ops.recount(c.wsorted, c.wslot, self.tok_z, self.dn[self.b][: self.V * self.KS].view(self.V, self.KS),
-                        self.KS)
+            ops.recount(c.wsorted, c.wslot, self.tok_z, head, self.KS)
+        elif self.mode == 2:
+            # dn[b] head := Δn_wk of the tokens that changed topic this sweep
+            ops.delta_recount(c.wslot, c.tile_wlo, c.tile_whi, self.chg_mask, c.tok_word, self.tok_z, self.tok_zprev,
+                              head, self.KS, self.G)
         if self.comm is not None and self.comm.world > 1:
             t0 = time.perf_counter()
             self.comm.allreduce_(self.dn[self.b])
@@ -136,7 +149,7 @@ class GibbsLDA:
             self.timings["allreduce_calls"] += 1
         ops.gibbs_apply(self.nwk, self.dn[self.b], self.dn[1 - self.b], self.nk[self.cn], self.nk[1 - self.cn],
                         self.q, self.V, self.K, self.KS, self.beta, self.vbeta, self.sweep_ctr, bump=True,
-                        absolute=not atomic)
+                        absolute=self.mode == 0)
         self.a, self.b, self.cn = 1 - self.a, 1 - self.b, 1 - self.cn
         self.sweeps_done += 1
 
@@ -247,6 +260,8 @@ class GibbsLDA:
         if self.comm is not None and self.comm.world > 1:
             self.comm.allreduce_(self.nwk)
             self.comm.allreduce_(self.nk[0])
+        if self.mode == 2:
+            self.tok_zprev.copy_(self.tok_z)
         self.a = self.b = self.cn = 0
         self.sweeps_done = sweeps_done
         self._graph = None

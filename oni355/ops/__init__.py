@@ -226,13 +226,14 @@ def sell_perm_z(chunk_doc, chunk_pos0, chunk_len, S, slice_off, doc_tok_ptr, tok
 # sampler
 # ------------------------------------------------------------------------------------------------
 def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init: bool, sweep_ctr: torch.Tensor,
-               chunk_len: torch.Tensor, host_sweep: int | None = None, atomic: bool = True,
-               prefetch_q: bool = False) -> None:
+               chunk_len: torch.Tensor, host_sweep: int | None = None, mode: int = 1,
+               prefetch_q: bool = False, chg_mask: torch.Tensor | None = None) -> None:
     """Launch one init/sweep pass. ``st`` holds the OniGibbs tensors (see csrc/kernels/gibbs.hip).
 
-    ``atomic``: accumulate Δn_wk with per-token atomics; otherwise the caller rebuilds n_wk with
-    :func:`recount` after the pass (no per-token global atomics).
+    ``mode`` 1: accumulate Δn_wk with per-token atomics; 0: the caller rebuilds n_wk with
+    :func:`recount`; 2: record changed slots in ``chg_mask`` for :func:`delta_recount`.
     """
+    atomic = mode == 1
     s0, s1 = spec.split_seed(seed)
     KS = G * KP
     if not _is_dev(st["tok_word"]):
@@ -253,10 +254,37 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
                  "chunk_multi", "ndk_src", "ndk_dst", "q", "dnwk", "dnk"):
         setattr(a, name, _lib.ptr(st[name]))
     a.sweep_ctr = _lib.ptr(sweep_ctr)
+    if mode == 2:
+        if chg_mask is None or chg_mask.numel() * (64 // G) < st["tok_word"].numel():
+            raise ValueError("delta mode needs a change mask with one word per SELL step")
+        a.chg_mask = _lib.ptr(chg_mask)
     a.n_slices, a.K, a.KS, a.alpha, a.seed0, a.seed1 = n_slices, K, KS, float(alpha), s0, s1
-    _lib.check(_lib.lib().oni_gibbs_launch(C.byref(a), G, KP, 1 if init else 0, 1 if atomic else 0,
+    _lib.check(_lib.lib().oni_gibbs_launch(C.byref(a), G, KP, 1 if init else 0, int(mode),
                                            1 if prefetch_q else 0, _lib.stream()),
                "oni_gibbs_launch")
+
+
+def delta_recount(wslot, tile_wlo, tile_whi, chg_mask, tok_word, tok_z, tok_zprev, dnwk_out, KS: int, G: int) -> None:
+    """Δn_wk of the tokens whose topic changed this sweep (+1 new, -1 previous); refreshes z_prev."""
+    T = wslot.numel()
+    if T == 0:
+        return
+    if not _is_dev(tok_z):
+        sl = wslot.long()
+        zn, zo = tok_z[sl].long(), tok_zprev[sl].long()
+        ch = zn != zo
+        w = tok_word[sl][ch].long()
+        one = torch.ones(int(ch.sum()), dtype=torch.int32)
+        dnwk_out.view(-1).index_add_(0, w * KS + zn[ch], one)
+        dnwk_out.view(-1).index_add_(0, w * KS + zo[ch], -one)
+        tok_zprev[sl[ch]] = tok_z[sl[ch]]
+        return
+    S = 64 // G
+    wmax = max(1, min(16384 // KS, 4096))
+    _lib.check(_lib.lib().oni_delta_recount(*map(_lib.ptr, (wslot, tile_wlo, tile_whi, chg_mask, tok_word, tok_z,
+                                                            tok_zprev)), T, _lib.ptr(dnwk_out), KS,
+                                            S.bit_length() - 1, G, RECOUNT_TILE, wmax, _lib.stream()),
+               "oni_delta_recount")
 
 
 RECOUNT_TILE = 4096

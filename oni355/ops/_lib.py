@@ -31,7 +31,7 @@ class OniGibbs(C.Structure):
     _fields_ = [
         ("tok_word", vp), ("tok_z", vp), ("slice_off", vp), ("slice_len", vp),
         ("chunk_doc", vp), ("chunk_pos0", vp), ("chunk_key", vp), ("chunk_multi", vp),
-        ("ndk_src", vp), ("ndk_dst", vp), ("q", vp), ("dnwk", vp), ("dnk", vp), ("sweep_ctr", vp),
+        ("ndk_src", vp), ("ndk_dst", vp), ("q", vp), ("dnwk", vp), ("dnk", vp), ("sweep_ctr", vp), ("chg_mask", vp),
         ("n_slices", i64), ("K", i32), ("KS", i32), ("alpha", f32), ("seed0", u32), ("seed1", u32),
     ]
 
@@ -49,6 +49,7 @@ _SIGS = {
     "oni_gibbs_sizeof_args": [],
     "oni_gibbs_apply": [vp, vp, vp, vp, vp, vp, i64, C.c_int, C.c_int, f32, f32, vp, C.c_int, C.c_int, vp],
     "oni_recount": [vp, vp, vp, i64, vp, C.c_int, C.c_int, C.c_int, vp],
+    "oni_delta_recount": [vp, vp, vp, vp, vp, vp, vp, i64, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp],
     "oni_copy_rows": [vp, vp, vp, i64, C.c_int, vp],
     "oni_score": [vp, vp, C.c_int, vp, vp, vp, vp, i64, f32, vp, vp, vp, vp, vp],
     "oni_select_below": [vp, i64, f32, u32, vp, vp, vp, i64, vp],

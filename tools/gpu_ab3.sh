@@ -1,0 +1,12 @@
+#!/bin/bash
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp PYTHONUNBUFFERED=1
+mkdir -p gpurun_out
+echo "start $(date)" > gpurun_out/progress.log
+timeout -k 10 600 python -m pytest tests/test_gpu_kernels.py tests/test_gpu_strings.py -x -v -m gpu --timeout 200 --durations=5 > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed" >> gpurun_out/progress.log; exit 1; }
+echo "pytest ok $(date)" >> gpurun_out/progress.log
+timeout -k 10 600 python bench/gibbs_ab.py --rounds 5 --sweeps 20 --chunk-lens 32,64,128,256 > gpurun_out/gibbs_ab.json 2> gpurun_out/gibbs_ab.err || { echo "ab failed" >> gpurun_out/progress.log; exit 1; }
+echo "ab ok $(date)" >> gpurun_out/progress.log
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_ab -o ab -- python bench/gibbs_ab.py --rounds 2 --sweeps 10 --modes delta+qpf > gpurun_out/prof_ab.log 2>&1 || { echo "prof failed" >> gpurun_out/progress.log; exit 1; }
+echo "prof ok $(date)" >> gpurun_out/progress.log
