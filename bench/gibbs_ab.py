@@ -22,8 +22,8 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--sweeps", type=int, default=20)
     ap.add_argument("--burn", type=int, default=30)
-    ap.add_argument("--modes", default="recount+qpf,delta+qpf,delta")
-    ap.add_argument("--chunk-len", type=int, default=256)
+    ap.add_argument("--modes", default="dual+qpf,delta+qpf,recount+qpf")
+    ap.add_argument("--chunk-len", type=int, default=128)
     ap.add_argument("--chunk-lens", default="", help="extra A/B: comma list of L values (delta+qpf)")
     a = ap.parse_args()
     import numpy as np
@@ -82,15 +82,17 @@ def main() -> int:
                 if stage == 0:
                     ops.gibbs_pass(m._state(False), m.G, m.KP, m.K, m.alpha, m.cfg.seed, False, m.sweep_ctr,
                                    c.chunk_len, mode=m.mode, prefetch_q=m.cfg.prefetch_q,
-                                   chg_mask=getattr(m, "chg_mask", None))
+                                   chg_mask=getattr(m, "chg_mask", None), wpos=c.wpos, z_w=getattr(m, "z_w", None))
                 elif stage == 1 and m.mode == 0:
                     ops.recount(c.wsorted, c.wslot, m.tok_z, head, m.KS)
+                elif stage == 1 and m.mode == 3:
+                    ops.recount(c.wsorted, None, m.z_w, head, m.KS)
                 elif stage == 1 and m.mode == 2:
                     ops.delta_recount(c.wslot, c.tile_wlo, c.tile_whi, m.chg_mask, c.tok_word, m.tok_z, m.tok_zprev,
                                       head, m.KS, m.G)
                 elif stage == 2:
                     ops.gibbs_apply(m.nwk, m.dn[m.b], m.dn[1 - m.b], m.nk[m.cn], m.nk[1 - m.cn], m.q, m.V, m.K, m.KS,
-                                    m.beta, m.vbeta, m.sweep_ctr, bump=False, absolute=m.mode == 0)
+                                    m.beta, m.vbeta, m.sweep_ctr, bump=False, absolute=m.mode in (0, 3))
                 ev[1].record()
                 torch.cuda.synchronize()
                 ts.append(ev[0].elapsed_time(ev[1]))
@@ -102,7 +104,7 @@ def main() -> int:
         del models
         torch.cuda.empty_cache()
         rl = common.build_and_train(dk, wk, None, vocab, a.topics, None, 0.01, 0x0D15EA5E, 0, L, None, train=False)
-        m = GibbsLDA(rl.corpus, GibbsConfig(K=a.topics, count_mode="delta", prefetch_q=True))
+        m = GibbsLDA(rl.corpus, GibbsConfig(K=a.topics, count_mode="dual", prefetch_q=True))
         m.initialize()
         m.sweep(a.burn)
         ts = []

@@ -39,6 +39,8 @@ struct OniGibbs {
   int32_t* dnk;                // [KS]    topic-total delta (init: n_k itself)
   const uint32_t* sweep_ctr;   // device scalar: current sweep number (≥ 1), graph-replay safe
   uint64_t* chg_mask;          // MODE 2: one u64 per SELL step, bit c*G set if slot c's topic changed
+  const int32_t* wpos;         // MODE 3: word-sorted position of every SELL slot
+  uint8_t* z_w;                // MODE 3: topic array in word-sorted order (kept in sync for changed tokens)
   int64_t n_slices;
   int32_t K;
   int32_t KS;
@@ -69,7 +71,8 @@ __device__ __forceinline__ void load_row_f(const float* __restrict__ p, float (&
 }
 
 // MODE: 0 = no n_wk bookkeeping (full recount afterwards), 1 = per-token Δ atomics,
-//       2 = changed-slot ballot mask per step (delta recount afterwards)
+//       2 = changed-slot ballot mask per step (delta recount afterwards),
+//       3 = changed topics also scattered into the word-sorted copy z_w (streaming recount afterwards)
 template <int G, int KP, bool INIT, int MODE, bool QPF>
 __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
   constexpr bool ATOMIC = MODE == 1;
@@ -179,6 +182,7 @@ __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
       for (int j = 0; j < KP; ++j) n[j] += (kbase + j == zn);
       if (zn != zo && g == 0) {
         a.tok_z[idx] = (uint8_t)zn;
+        if constexpr (MODE == 3) a.z_w[a.wpos[idx]] = (uint8_t)zn;
         if (ATOMIC) {
           atomicAdd(&a.dnwk[(int64_t)w * KS + zo], -1);
           atomicAdd(&a.dnwk[(int64_t)w * KS + zn], 1);
@@ -308,6 +312,9 @@ int launch_gibbs(const OniGibbs& a, bool init, int mode, bool qpf, hipStream_t s
   } else if (mode == 2) {
     if (qpf && Q) k_gibbs<G, KP, false, 2, Q><<<grid, kBlock, 0, s>>>(a);
     else k_gibbs<G, KP, false, 2, false><<<grid, kBlock, 0, s>>>(a);
+  } else if (mode == 3) {
+    if (qpf && Q) k_gibbs<G, KP, false, 3, Q><<<grid, kBlock, 0, s>>>(a);
+    else k_gibbs<G, KP, false, 3, false><<<grid, kBlock, 0, s>>>(a);
   } else if (qpf && Q) {
     k_gibbs<G, KP, false, 0, Q><<<grid, kBlock, 0, s>>>(a);
   } else {
@@ -387,7 +394,7 @@ __global__ __launch_bounds__(256) void k_recount(const int32_t* __restrict__ wso
   __syncthreads();
   for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
     const int w = wsorted[i];
-    const int z = tok_z[wslot[i]];
+    const int z = wslot ? tok_z[wslot[i]] : tok_z[i];  // wslot == nullptr: tok_z is already word-sorted
     const int r = w - w_lo;
     if (r < rows) atomicAdd(&hst[r * KS + z], 1);
     else atomicAdd(&nwk[(int64_t)w * KS + z], 1);
@@ -403,8 +410,9 @@ __global__ __launch_bounds__(256) void k_recount(const int32_t* __restrict__ wso
 
 // Supported (G, KP) configurations. K ≤ 32: G = 1 (KP = K rounded up to 4).
 ONI_API int oni_gibbs_launch(const OniGibbs* a, int G, int KP, int init, int mode, int qpf, hipStream_t s) {
-  if (a->K < 1 || a->K > 255 || a->K > a->KS || mode < 0 || mode > 2) return (int)hipErrorInvalidValue;
+  if (a->K < 1 || a->K > 255 || a->K > a->KS || mode < 0 || mode > 3) return (int)hipErrorInvalidValue;
   if (mode == 2 && !a->chg_mask) return (int)hipErrorInvalidValue;
+  if (mode == 3 && (!a->wpos || !a->z_w)) return (int)hipErrorInvalidValue;
 #define ONI_CASE(g_, kp_) \
   if (G == g_ && KP == kp_) return launch_gibbs<g_, kp_>(*a, init != 0, mode, qpf != 0, s);
   ONI_CASE(1, 4) ONI_CASE(1, 8) ONI_CASE(1, 12) ONI_CASE(1, 16) ONI_CASE(1, 20) ONI_CASE(1, 24) ONI_CASE(1, 28)

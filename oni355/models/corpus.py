@@ -46,6 +46,7 @@ class Corpus:
     wslot: torch.Tensor | None = None    # int32 [T] SELL slot of each word-sorted token
     tile_wlo: torch.Tensor | None = None  # int32 [n_tiles] first word of each recount tile
     tile_whi: torch.Tensor | None = None  # int32 [n_tiles] last word of each recount tile
+    wpos: torch.Tensor | None = None      # int32 [SELL slots] word-sorted position of each slot (-1: pad)
 
     @property
     def S(self) -> int:
@@ -159,13 +160,15 @@ def build_corpus(tdoc: torch.Tensor, tword: torch.Tensor, D: int, V: int, doc_ke
     tile_wlo = wsorted[starts].to(torch.int32) if starts.numel() else torch.zeros(0, dtype=torch.int32, device=dev)
     ends = torch.clamp(starts + tile - 1, max=max(wsorted.numel() - 1, 0))
     tile_whi = wsorted[ends].to(torch.int32) if starts.numel() else torch.zeros(0, dtype=torch.int32, device=dev)
+    wpos = torch.full((tok_word.numel(),), -1, dtype=torch.int32, device=dev)
+    wpos[wslot.long()] = torch.arange(wslot.numel(), dtype=torch.int32, device=dev)
     return Corpus(D=D, V=V, T=T, G=G, L=L, doc_keys=doc_keys.to(torch.int32), pair_doc=pair_doc,
                   pair_word=pair_word, pair_cnt=cnt.to(torch.int32), doc_pair_ptr=doc_pair_ptr,
                   doc_tok_ptr=doc_tok_ptr, pair_tokoff=pair_tokoff.contiguous(), slice_off=slice_off,
                   slice_len=slice_len, chunk_doc=chunk_doc, chunk_pos0=chunk_pos0, chunk_len=chunk_len,
                   chunk_key=chunk_key, chunk_multi=chunk_multi, tok_word=tok_word, long_rows=long_rows,
                   wsorted=wsorted.contiguous(), wslot=wslot.contiguous(), tile_wlo=tile_wlo.contiguous(),
-                  tile_whi=tile_whi.contiguous())
+                  tile_whi=tile_whi.contiguous(), wpos=wpos)
 
 
 def canonical_tokens(c: Corpus) -> tuple[torch.Tensor, torch.Tensor]:

@@ -34,9 +34,10 @@ class GibbsConfig:
     beta: float = 0.01
     seed: int = 0x0D15EA5E
     use_graph: bool = True
-    # n_wk bookkeeping: "delta" (changed-slot masks + word-sorted delta recount; default),
-    # "recount" (full word-sorted LDS histogram every sweep) | "atomic" (per-token Δ atomics)
-    count_mode: str = "delta"
+    # n_wk bookkeeping: "dual" (changed topics mirrored into a word-sorted z copy, streaming
+    # recount; default), "delta" (changed-slot masks + word-sorted delta recount), "recount"
+    # (full gathered recount) | "atomic" (per-token Δ atomics)
+    count_mode: str = "dual"
     prefetch_q: bool = True      # K<=32: fetch the next token's q row one step ahead
 
     def resolved_alpha(self) -> float:
@@ -70,9 +71,11 @@ class GibbsLDA:
         self.dn = [torch.zeros(V * KS + KS, dtype=i32, device=dev) for _ in range(2)]
         self.q = torch.zeros(V, KS, dtype=torch.float32, device=dev)
         self.sweep_ctr = torch.zeros(1, dtype=i32, device=dev)
-        if cfg.count_mode not in ("delta", "recount", "atomic"):
+        if cfg.count_mode not in ("dual", "delta", "recount", "atomic"):
             raise ValueError(f"unknown count_mode {cfg.count_mode}")
-        self.mode = {"recount": 0, "atomic": 1, "delta": 2}[cfg.count_mode]
+        self.mode = {"recount": 0, "atomic": 1, "delta": 2, "dual": 3}[cfg.count_mode]
+        if self.mode == 3:
+            self.z_w = torch.zeros(max(corpus.T, 1), dtype=torch.uint8, device=dev)
         if self.mode == 2:
             self.tok_zprev = torch.zeros_like(self.tok_z)
             self.chg_mask = torch.zeros(max(corpus.sell_slots // corpus.S, 1), dtype=torch.int64, device=dev)
@@ -111,11 +114,17 @@ class GibbsLDA:
         if self.comm is not None and self.comm.world > 1:
             self.comm.allreduce_(self.nwk)
             self.comm.allreduce_(self.nk[0])
-        if self.mode == 2:
-            self.tok_zprev.copy_(self.tok_z)
+        self._sync_aux_z()
         self.sweeps_done = 0
         self._graph = None
         self._prime()
+
+    def _sync_aux_z(self) -> None:
+        """Bring the auxiliary topic copies (z_prev / word-sorted z) in line with tok_z."""
+        if self.mode == 2:
+            self.tok_zprev.copy_(self.tok_z)
+        elif self.mode == 3 and self.c.T:
+            self.z_w[: self.c.T] = self.tok_z[self.c.wslot.long()]
 
     def _prime(self) -> None:
         # zero-delta apply: q from n_wk, nk[1] = nk[0]; leaves dn[0], dn[1] zero
@@ -133,11 +142,15 @@ class GibbsLDA:
         ops.copy_rows(self.ndk[self.a], self.ndk[1 - self.a], c.long_rows, self.KS)
         ops.gibbs_pass(self._state(False), self.G, self.KP, self.K, self.alpha, self.cfg.seed, False,
                        self.sweep_ctr, c.chunk_len, host_sweep=self.sweeps_done + 1, mode=self.mode,
-                       prefetch_q=self.cfg.prefetch_q, chg_mask=getattr(self, "chg_mask", None))
+                       prefetch_q=self.cfg.prefetch_q, chg_mask=getattr(self, "chg_mask", None), wpos=c.wpos,
+                       z_w=getattr(self, "z_w", None))
         head = self.dn[self.b][: self.V * self.KS].view(self.V, self.KS)
         if self.mode == 0:
             # dn[b] head := this rank's n_wk rebuilt from z (tail keeps Δn_k)
             ops.recount(c.wsorted, c.wslot, self.tok_z, head, self.KS)
+        elif self.mode == 3:
+            # dn[b] head := this rank's n_wk, streamed from the word-sorted topic copy
+            ops.recount(c.wsorted, None, self.z_w, head, self.KS)
         elif self.mode == 2:
             # dn[b] head := Δn_wk of the tokens that changed topic this sweep
             ops.delta_recount(c.wslot, c.tile_wlo, c.tile_whi, self.chg_mask, c.tok_word, self.tok_z, self.tok_zprev,
@@ -149,7 +162,7 @@ class GibbsLDA:
             self.timings["allreduce_calls"] += 1
         ops.gibbs_apply(self.nwk, self.dn[self.b], self.dn[1 - self.b], self.nk[self.cn], self.nk[1 - self.cn],
                         self.q, self.V, self.K, self.KS, self.beta, self.vbeta, self.sweep_ctr, bump=True,
-                        absolute=self.mode == 0)
+                        absolute=self.mode in (0, 3))
         self.a, self.b, self.cn = 1 - self.a, 1 - self.b, 1 - self.cn
         self.sweeps_done += 1
 
@@ -260,8 +273,7 @@ class GibbsLDA:
         if self.comm is not None and self.comm.world > 1:
             self.comm.allreduce_(self.nwk)
             self.comm.allreduce_(self.nk[0])
-        if self.mode == 2:
-            self.tok_zprev.copy_(self.tok_z)
+        self._sync_aux_z()
         self.a = self.b = self.cn = 0
         self.sweeps_done = sweeps_done
         self._graph = None

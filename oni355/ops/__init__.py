@@ -227,11 +227,13 @@ def sell_perm_z(chunk_doc, chunk_pos0, chunk_len, S, slice_off, doc_tok_ptr, tok
 # ------------------------------------------------------------------------------------------------
 def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init: bool, sweep_ctr: torch.Tensor,
                chunk_len: torch.Tensor, host_sweep: int | None = None, mode: int = 1,
-               prefetch_q: bool = False, chg_mask: torch.Tensor | None = None) -> None:
+               prefetch_q: bool = False, chg_mask: torch.Tensor | None = None, wpos: torch.Tensor | None = None,
+               z_w: torch.Tensor | None = None) -> None:
     """Launch one init/sweep pass. ``st`` holds the OniGibbs tensors (see csrc/kernels/gibbs.hip).
 
     ``mode`` 1: accumulate Δn_wk with per-token atomics; 0: the caller rebuilds n_wk with
-    :func:`recount`; 2: record changed slots in ``chg_mask`` for :func:`delta_recount`.
+    :func:`recount`; 2: record changed slots in ``chg_mask`` for :func:`delta_recount`; 3: also
+    write changed topics into the word-sorted copy ``z_w`` (via ``wpos``) for a streaming recount.
     """
     atomic = mode == 1
     s0, s1 = spec.split_seed(seed)
@@ -243,6 +245,9 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
             npst["dnwk"] = np.zeros_like(npst["dnwk"])  # discarded: recount rebuilds n_wk
         spec.gibbs_pass(npst, G, KP, K, alpha, s0, s1, init,
                         int(host_sweep if host_sweep is not None else sweep_ctr.item()), chunk_len.numpy())
+        if mode == 3:
+            valid = wpos >= 0
+            z_w[wpos[valid].long()] = st["tok_z"][valid]
         return
     n_slices = st["slice_len"].numel()
     if st["q"].shape[-1] != KS or st["ndk_src"].shape[-1] != KS:
@@ -258,6 +263,10 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
         if chg_mask is None or chg_mask.numel() * (64 // G) < st["tok_word"].numel():
             raise ValueError("delta mode needs a change mask with one word per SELL step")
         a.chg_mask = _lib.ptr(chg_mask)
+    if mode == 3:
+        if wpos is None or z_w is None or wpos.numel() != st["tok_word"].numel():
+            raise ValueError("dual mode needs wpos [SELL slots] and z_w [T]")
+        a.wpos, a.z_w = _lib.ptr(wpos), _lib.ptr(z_w)
     a.n_slices, a.K, a.KS, a.alpha, a.seed0, a.seed1 = n_slices, K, KS, float(alpha), s0, s1
     _lib.check(_lib.lib().oni_gibbs_launch(C.byref(a), G, KP, 1 if init else 0, int(mode),
                                            1 if prefetch_q else 0, _lib.stream()),
@@ -291,12 +300,16 @@ RECOUNT_TILE = 4096
 
 
 def recount(wsorted, wslot, tok_z, nwk_out, KS: int) -> None:
-    """Accumulate the (word, topic) histogram of all tokens into ``nwk_out`` [V, KS] (pre-zeroed)."""
+    """Accumulate the (word, topic) histogram of all tokens into ``nwk_out`` [V, KS] (pre-zeroed).
+
+    ``wslot`` maps word-sorted tokens to SELL slots of ``tok_z``; ``wslot=None`` means ``tok_z``
+    is already in word-sorted order (the streaming recount of the dual-z mode).
+    """
     T = wsorted.numel()
     if T == 0:
         return
     if not _is_dev(tok_z):
-        z = tok_z[wslot.long()].long()
+        z = (tok_z[wslot.long()] if wslot is not None else tok_z[:T]).long()
         nwk_out.view(-1).index_add_(0, wsorted.long() * KS + z, torch.ones_like(z, dtype=torch.int32))
         return
     wmax = max(1, min(16384 // KS, 4096))

@@ -60,8 +60,8 @@ def _toy_tokens(n_docs, V, seed, heavy=True):
     return torch.from_numpy(tdoc), torch.from_numpy(tword), keys
 
 
-@pytest.mark.parametrize("K,mode", [(20, "recount"), (20, "recount+noqpf"), (20, "atomic"), (7, "recount"),
-                                    (50, "recount"), (100, "atomic"), (100, "recount")])
+@pytest.mark.parametrize("K,mode", [(20, "dual"), (20, "dual+noqpf"), (20, "delta"), (20, "recount"), (20, "atomic"),
+                                    (7, "dual"), (50, "dual"), (50, "delta"), (100, "atomic"), (100, "dual")])
 def test_gibbs_bitwise_vs_oracle(gpu, K, mode):
     tdoc, tword, keys = _toy_tokens(300, 400, K)
     G, KP = ops.choose_tiling(K)
