@@ -33,7 +33,7 @@ def main(argv=None) -> int:
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--flows-per-gpu", type=int, default=12_500_000)
     ap.add_argument("--topics", type=int, default=20)
-    ap.add_argument("--chunk-len", type=int, default=256)
+    ap.add_argument("--chunk-len", type=int, default=128)
     ap.add_argument("--maxresults", type=int, default=3000)
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--device", default="cuda")

@@ -406,7 +406,97 @@ __global__ __launch_bounds__(256) void k_recount(const int32_t* __restrict__ wso
   }
 }
 
+// Streaming recount for KS ≤ 32 (dual-z mode): z_w is word-sorted, so each thread takes 16
+// CONTIGUOUS tokens (one 64-B word-id load + one 16-B topic load), counts them in a register
+// histogram while the word stays the same (frequent words dominate by tokens), and only flushes
+// non-zero bins to the block's LDS table when the word changes. This removes the LDS-atomic
+// hot spots of one-atomic-per-token (tokens of a frequent word share a handful of topics).
+template <int KS>
+__global__ __launch_bounds__(256) void k_recount_reg(const int32_t* __restrict__ wsorted, const uint8_t* __restrict__ z_w,
+                                                      int64_t T, int32_t* __restrict__ nwk, int tile, int wmax) {
+  extern __shared__ __attribute__((aligned(16))) int32_t hst[];
+  constexpr int E = 16;
+  const int64_t lo = (int64_t)blockIdx.x * tile;
+  if (lo >= T) return;
+  const int64_t hi = lo + tile < T ? lo + tile : T;
+  const int w_lo = wsorted[lo], w_hi = wsorted[hi - 1];
+  const int rows = (w_hi - w_lo + 1) < wmax ? (w_hi - w_lo + 1) : wmax;
+  const int cells = rows * KS;
+  for (int i = threadIdx.x; i < cells; i += blockDim.x) hst[i] = 0;
+  __syncthreads();
+  int cnt[KS];
+#pragma unroll
+  for (int k = 0; k < KS; ++k) cnt[k] = 0;
+  int cur = -1;
+  auto flush = [&](int w) {
+    if (w < 0) return;
+    const int r = w - w_lo;
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      if (cnt[k]) {
+        if (r < rows) atomicAdd(&hst[r * KS + k], cnt[k]);
+        else atomicAdd(&nwk[(int64_t)w * KS + k], cnt[k]);
+        cnt[k] = 0;
+      }
+    }
+  };
+  for (int64_t t0 = lo + (int64_t)threadIdx.x * E; t0 < hi; t0 += (int64_t)blockDim.x * E) {
+    int wv[E];
+    uint8_t zv[E];
+    const int n = (int)(hi - t0 < E ? hi - t0 : E);
+    if (n == E) {
+#pragma unroll
+      for (int q = 0; q < E; q += 4) {
+        const int4 v = *reinterpret_cast<const int4*>(wsorted + t0 + q);
+        wv[q] = v.x; wv[q + 1] = v.y; wv[q + 2] = v.z; wv[q + 3] = v.w;
+      }
+      const uint4 zz = *reinterpret_cast<const uint4*>(z_w + t0);
+      const uint32_t zw[4] = {zz.x, zz.y, zz.z, zz.w};
+#pragma unroll
+      for (int q = 0; q < E; ++q) zv[q] = (uint8_t)(zw[q >> 2] >> (8 * (q & 3)));
+    } else {
+#pragma unroll
+      for (int q = 0; q < E; ++q) {
+        wv[q] = q < n ? wsorted[t0 + q] : -1;
+        zv[q] = q < n ? z_w[t0 + q] : 0;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < E; ++q) {
+      if (q >= n) break;
+      if (wv[q] != cur) {
+        flush(cur);
+        cur = wv[q];
+      }
+#pragma unroll
+      for (int k = 0; k < KS; ++k) cnt[k] += (k == (int)zv[q]);
+    }
+  }
+  flush(cur);
+  __syncthreads();
+  for (int i = threadIdx.x; i < cells; i += blockDim.x) {
+    const int v = hst[i];
+    if (v) atomicAdd(&nwk[(int64_t)(w_lo + i / KS) * KS + (i % KS)], v);
+  }
+}
+
 }  // namespace
+
+ONI_API int oni_recount_stream(const int32_t* wsorted, const uint8_t* z_w, int64_t T, int32_t* nwk, int KS, int tile,
+                               int wmax, hipStream_t s) {
+  if (T == 0) return 0;
+  if (tile % (256 * 16) != 0 || wmax < 1 || (size_t)wmax * KS * 4 > 64 * 1024) return (int)hipErrorInvalidValue;
+  const unsigned grid = (unsigned)((T + tile - 1) / tile);
+  const size_t lds = (size_t)wmax * KS * 4;
+#define ONI_RC(ks_)                                                                       \
+  if (KS == ks_) {                                                                        \
+    k_recount_reg<ks_><<<grid, 256, lds, s>>>(wsorted, z_w, T, nwk, tile, wmax);          \
+    return (int)hipGetLastError();                                                        \
+  }
+  ONI_RC(4) ONI_RC(8) ONI_RC(12) ONI_RC(16) ONI_RC(20) ONI_RC(24) ONI_RC(28) ONI_RC(32)
+#undef ONI_RC
+  return (int)hipErrorInvalidValue;
+}
 
 // Supported (G, KP) configurations. K ≤ 32: G = 1 (KP = K rounded up to 4).
 ONI_API int oni_gibbs_launch(const OniGibbs* a, int G, int KP, int init, int mode, int qpf, hipStream_t s) {

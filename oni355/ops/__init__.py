@@ -313,8 +313,16 @@ def recount(wsorted, wslot, tok_z, nwk_out, KS: int) -> None:
         nwk_out.view(-1).index_add_(0, wsorted.long() * KS + z, torch.ones_like(z, dtype=torch.int32))
         return
     wmax = max(1, min(16384 // KS, 4096))
+    if wslot is None and KS <= 32 and STREAM_RECOUNT:
+        # word-sorted topics: contiguous per-thread runs counted in registers (k_recount_reg)
+        _lib.check(_lib.lib().oni_recount_stream(_lib.ptr(wsorted), _lib.ptr(tok_z), T, _lib.ptr(nwk_out), KS,
+                                                 RECOUNT_TILE, wmax, _lib.stream()), "oni_recount_stream")
+        return
     _lib.check(_lib.lib().oni_recount(_lib.ptr(wsorted), _lib.ptr(wslot), _lib.ptr(tok_z), T, _lib.ptr(nwk_out), KS,
                                       RECOUNT_TILE, wmax, _lib.stream()), "oni_recount")
+
+
+STREAM_RECOUNT = True
 
 
 def gibbs_apply(nwk, dcur, dother, nk_cur, nk_next, q, V, K, KS, beta, vbeta, sweep_ctr, bump=True, absolute=False):

@@ -10,3 +10,5 @@ timeout -k 10 600 python bench/gibbs_ab.py --rounds 5 --sweeps 20 --chunk-lens 3
 echo "ab ok $(date)" >> gpurun_out/progress.log
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_ab -o ab -- python bench/gibbs_ab.py --rounds 2 --sweeps 10 --modes delta+qpf > gpurun_out/prof_ab.log 2>&1 || { echo "prof failed" >> gpurun_out/progress.log; exit 1; }
 echo "prof ok $(date)" >> gpurun_out/progress.log
+timeout -k 10 400 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed" >> gpurun_out/progress.log; exit 1; }
+echo "bench ok $(date)" >> gpurun_out/progress.log
