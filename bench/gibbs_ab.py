@@ -24,7 +24,8 @@ def main() -> int:
     ap.add_argument("--burn", type=int, default=30)
     ap.add_argument("--modes", default="dual+qpf,delta+qpf,recount+qpf")
     ap.add_argument("--chunk-len", type=int, default=128)
-    ap.add_argument("--chunk-lens", default="", help="extra A/B: comma list of L values (delta+qpf)")
+    ap.add_argument("--chunk-lens", default="", help="extra A/B: comma list of L values (dual+qpf)")
+    ap.add_argument("--lds", action="store_true", help="chunk-length A/B with the LDS-count sampler")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -47,7 +48,8 @@ def main() -> int:
     c = run.corpus
     print(json.dumps({"corpus": c.stats()}), flush=True)
     modes = a.modes.split(",")
-    models = {m: GibbsLDA(c, GibbsConfig(K=a.topics, count_mode=m.split("+")[0], prefetch_q="qpf" in m))
+    models = {m: GibbsLDA(c, GibbsConfig(K=a.topics, count_mode=m.split("+")[0], prefetch_q="qpf" in m,
+                                         lds_counts="lds" in m))
               for m in modes}
     for m in models.values():
         m.initialize()
@@ -73,7 +75,9 @@ def main() -> int:
     # per-stage timing (eager, events) for each mode
     for name, m in models.items():
         st = {}
-        for stage in range(3):
+        for stage in range(4):
+            if stage == 3 and m.mode != 3:
+                continue
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
             ts = []
             for _ in range(5):
@@ -81,7 +85,7 @@ def main() -> int:
                 head = m.dn[m.b][: m.V * m.KS].view(m.V, m.KS)
                 if stage == 0:
                     ops.gibbs_pass(m._state(False), m.G, m.KP, m.K, m.alpha, m.cfg.seed, False, m.sweep_ctr,
-                                   c.chunk_len, mode=m.mode, prefetch_q=m.cfg.prefetch_q,
+                                   c.chunk_len, mode=m.mode, prefetch_q=m.qpf,
                                    chg_mask=getattr(m, "chg_mask", None), wpos=c.wpos, z_w=getattr(m, "z_w", None))
                 elif stage == 1 and m.mode == 0:
                     ops.recount(c.wsorted, c.wslot, m.tok_z, head, m.KS)
@@ -90,13 +94,17 @@ def main() -> int:
                 elif stage == 1 and m.mode == 2:
                     ops.delta_recount(c.wslot, c.tile_wlo, c.tile_whi, m.chg_mask, c.tok_word, m.tok_z, m.tok_zprev,
                                       head, m.KS, m.G)
+                elif stage == 3:
+                    ops.STREAM_RECOUNT = False
+                    ops.recount(c.wsorted, None, m.z_w, head, m.KS)
+                    ops.STREAM_RECOUNT = True
                 elif stage == 2:
                     ops.gibbs_apply(m.nwk, m.dn[m.b], m.dn[1 - m.b], m.nk[m.cn], m.nk[1 - m.cn], m.q, m.V, m.K, m.KS,
                                     m.beta, m.vbeta, m.sweep_ctr, bump=False, absolute=m.mode in (0, 3))
                 ev[1].record()
                 torch.cuda.synchronize()
                 ts.append(ev[0].elapsed_time(ev[1]))
-            st[["sample", "recount", "apply"][stage]] = float(np.median(ts))
+            st[["sample", "recount", "apply", "recount_lds"][stage]] = float(np.median(ts))
         out[name]["stages_ms"] = st
     print(json.dumps(out), flush=True)
     # chunk-length sweep (the sampler's serial critical path is L steps per lane)
@@ -104,7 +112,7 @@ def main() -> int:
         del models
         torch.cuda.empty_cache()
         rl = common.build_and_train(dk, wk, None, vocab, a.topics, None, 0.01, 0x0D15EA5E, 0, L, None, train=False)
-        m = GibbsLDA(rl.corpus, GibbsConfig(K=a.topics, count_mode="dual", prefetch_q=True))
+        m = GibbsLDA(rl.corpus, GibbsConfig(K=a.topics, count_mode="dual", prefetch_q=True, lds_counts=a.lds))
         m.initialize()
         m.sweep(a.burn)
         ts = []

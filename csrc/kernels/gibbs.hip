@@ -299,12 +299,168 @@ __global__ void k_copy_rows(const int32_t* __restrict__ src, int32_t* __restrict
   }
 }
 
+// K ≤ 32 sweep with the doc-topic counts staged in LDS (one lane = one unit, G = 1).
+//
+// Each lane owns an LDS row a[0..KS) = (float)n_dk (exact integers while counts < 2^24, checked
+// by the host; the weight is formed as (a + α)·q exactly like k_gibbs), so the per-token count update is two single-address LDS read-modify-writes instead
+// of 2·KS compare/select VALU ops, and the row costs no VGPRs. The categorical draw takes two
+// passes over (a, q): pass 1 sums the total, pass 2 recomputes the same running sum (identical
+// f32 ops → identical values) and counts cut points ≤ thr, so no KS-long cumulative array is
+// held in registers either. Row stride is an odd number of 16-B slots → conflict-free b128 reads.
+// Bit-identical to k_gibbs (and the NumPy oracle).
+template <int KP, int MODE>
+__global__ __launch_bounds__(kBlock) void k_gibbs_lds(const OniGibbs a) {
+  constexpr int KS = KP;
+  constexpr int STRIDE = ((KS / 4) % 2 == 0) ? KS + 4 : KS;
+  __shared__ __attribute__((aligned(16))) float sa[kBlock * STRIDE];
+  __shared__ int32_t red[kWavesPerBlock][KS];
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int64_t slice = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  const bool valid = slice < a.n_slices;
+  const int64_t chunk = slice * 64 + lane;
+  const int doc = valid ? a.chunk_doc[chunk] : -1;
+  const bool live = doc >= 0;
+  float* my = sa + threadIdx.x * STRIDE;
+  {
+    int32_t n0[KP];
+#pragma unroll
+    for (int j = 0; j < KP; ++j) n0[j] = 0;
+    if (live) load_row_i<KP>(a.ndk_src + (int64_t)doc * KS, n0);
+#pragma unroll
+    for (int j = 0; j < KP; j += 4)
+      *reinterpret_cast<float4*>(my + j) =
+          make_float4((float)n0[j], (float)n0[j + 1], (float)n0[j + 2], (float)n0[j + 3]);
+  }
+  const int len = valid ? a.slice_len[slice] : 0;
+  const int64_t off = valid ? a.slice_off[slice] : 0;
+  const uint32_t key = live ? a.chunk_key[chunk] : 0u;
+  const uint32_t pos0 = live ? (uint32_t)a.chunk_pos0[chunk] : 0u;
+  const uint32_t sweep = *a.sweep_ctr;
+  oni::U4 r{0, 0, 0, 0};
+  uint32_t wprev = oni::kPadWord;
+  float qv[KP], qn[KP];
+#pragma unroll
+  for (int j = 0; j < KP; ++j) qv[j] = qn[j] = 0.f;
+  uint32_t w_nx = len > 0 ? a.tok_word[off + lane] : oni::kPadWord;
+  int z_nx = len > 0 ? (int)a.tok_z[off + lane] : 0;
+  if (w_nx != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)w_nx * KS, qn);
+  for (int s = 0; s < len; ++s) {
+    const int64_t idx = off + (int64_t)s * 64 + lane;
+    const uint32_t w = w_nx;
+    const int zo = z_nx;
+    if (s + 1 < len) {
+      w_nx = a.tok_word[idx + 64];
+      z_nx = a.tok_z[idx + 64];
+    }
+    if (w == oni::kPadWord) continue;
+    const uint32_t pos = pos0 + (uint32_t)s;
+    if (s == 0 || (pos & 3u) == 0u) r = oni::philox10(oni::U4{pos >> 2, key, sweep, 1u}, a.seed0, a.seed1);
+    const uint32_t rr = oni::pick4(r, pos & 3u);
+    my[zo] = my[zo] - 1.0f;
+    if (w != wprev) {
+#pragma unroll
+      for (int j = 0; j < KP; ++j) qv[j] = qn[j];
+      wprev = w;
+    }
+    float run = 0.f;
+#pragma unroll
+    for (int j = 0; j < KP; j += 4) {
+      const float4 av = *reinterpret_cast<const float4*>(my + j);
+      run = run + (av.x + a.alpha) * qv[j];
+      run = run + (av.y + a.alpha) * qv[j + 1];
+      run = run + (av.z + a.alpha) * qv[j + 2];
+      run = run + (av.w + a.alpha) * qv[j + 3];
+    }
+    const float thr = oni::u01(rr) * run;
+    float run2 = 0.f;
+    int cnt = 0;
+#pragma unroll
+    for (int j = 0; j < KP; j += 4) {
+      const float4 av = *reinterpret_cast<const float4*>(my + j);
+      run2 = run2 + (av.x + a.alpha) * qv[j];
+      cnt += run2 <= thr;
+      run2 = run2 + (av.y + a.alpha) * qv[j + 1];
+      cnt += run2 <= thr;
+      run2 = run2 + (av.z + a.alpha) * qv[j + 2];
+      cnt += run2 <= thr;
+      run2 = run2 + (av.w + a.alpha) * qv[j + 3];
+      cnt += run2 <= thr;
+    }
+    const int zn = cnt < a.K - 1 ? cnt : a.K - 1;
+    my[zn] = my[zn] + 1.0f;
+    if (zn != zo) {
+      a.tok_z[idx] = (uint8_t)zn;
+      if constexpr (MODE == 3) a.z_w[a.wpos[idx]] = (uint8_t)zn;
+      if constexpr (MODE == 1) {
+        atomicAdd(&a.dnwk[(int64_t)w * KS + zo], -1);
+        atomicAdd(&a.dnwk[(int64_t)w * KS + zn], 1);
+      }
+    }
+    if constexpr (MODE == 2) {
+      const uint64_t m = __ballot(zn != zo);
+      if (lane == 0) a.chg_mask[(off + (int64_t)s * 64) / 64] = m;
+    }
+    if (s + 1 < len && w_nx != w && w_nx != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)w_nx * KS, qn);
+  }
+  // epilogue: counts back to ints, doc rows, per-topic totals
+  int32_t d[KP], n[KP];
+#pragma unroll
+  for (int j = 0; j < KP; ++j) {
+    n[j] = (int32_t)my[j];
+    d[j] = 0;
+  }
+  if (live) {
+    int32_t* dst = a.ndk_dst + (int64_t)doc * KS;
+    int32_t n0[KP];
+    load_row_i<KP>(a.ndk_src + (int64_t)doc * KS, n0);
+#pragma unroll
+    for (int j = 0; j < KP; ++j) d[j] = n[j] - n0[j];
+    if (a.chunk_multi[chunk]) {
+#pragma unroll
+      for (int j = 0; j < KP; ++j)
+        if (d[j]) atomicAdd(dst + j, d[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < KP; j += 4) *reinterpret_cast<int4*>(dst + j) = make_int4(n[j], n[j + 1], n[j + 2], n[j + 3]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < KP; ++j) {
+    int v = d[j];
+#pragma unroll
+    for (int m = 1; m < oni::kWave; m <<= 1) v += __shfl_xor(v, m);
+    d[j] = v;
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < KP; ++j) red[wave][j] = d[j];
+  }
+  __syncthreads();
+  if (threadIdx.x < KS) {
+    int v = 0;
+#pragma unroll
+    for (int w = 0; w < kWavesPerBlock; ++w) v += red[w][threadIdx.x];
+    if (v) atomicAdd(&a.dnk[threadIdx.x], v);
+  }
+}
+
 template <int G, int KP>
-int launch_gibbs(const OniGibbs& a, bool init, int mode, bool qpf, hipStream_t s) {
+int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s) {
   if (a.KS != G * KP) return (int)hipErrorInvalidValue;
   const unsigned grid = (unsigned)((a.n_slices + kWavesPerBlock - 1) / kWavesPerBlock);
   if (grid == 0) return 0;
   constexpr bool Q = G == 1;  // the q-row prefetch variant exists for one-lane units only
+  if constexpr (G == 1) {
+    // lds-staged doc counts: selected by the host with qpf == 2 (counts proven < 2^22)
+    if (!init && qpf == 2) {
+      if (mode == 0) k_gibbs_lds<KP, 0><<<grid, kBlock, 0, s>>>(a);
+      else if (mode == 1) k_gibbs_lds<KP, 1><<<grid, kBlock, 0, s>>>(a);
+      else if (mode == 2) k_gibbs_lds<KP, 2><<<grid, kBlock, 0, s>>>(a);
+      else k_gibbs_lds<KP, 3><<<grid, kBlock, 0, s>>>(a);
+      return (int)hipGetLastError();
+    }
+  }
   if (init) {
     k_gibbs<G, KP, true, 1, false><<<grid, kBlock, 0, s>>>(a);  // init always builds n_wk by atomics
   } else if (mode == 1) {
@@ -504,7 +660,7 @@ ONI_API int oni_gibbs_launch(const OniGibbs* a, int G, int KP, int init, int mod
   if (mode == 2 && !a->chg_mask) return (int)hipErrorInvalidValue;
   if (mode == 3 && (!a->wpos || !a->z_w)) return (int)hipErrorInvalidValue;
 #define ONI_CASE(g_, kp_) \
-  if (G == g_ && KP == kp_) return launch_gibbs<g_, kp_>(*a, init != 0, mode, qpf != 0, s);
+  if (G == g_ && KP == kp_) return launch_gibbs<g_, kp_>(*a, init != 0, mode, qpf, s);
   ONI_CASE(1, 4) ONI_CASE(1, 8) ONI_CASE(1, 12) ONI_CASE(1, 16) ONI_CASE(1, 20) ONI_CASE(1, 24) ONI_CASE(1, 28)
   ONI_CASE(1, 32)
   ONI_CASE(4, 8) ONI_CASE(4, 12) ONI_CASE(4, 16)

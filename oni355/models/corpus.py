@@ -67,6 +67,9 @@ class Corpus:
     def doc_lengths(self) -> torch.Tensor:
         return self.doc_tok_ptr[1:] - self.doc_tok_ptr[:-1]
 
+    def max_doc_len(self) -> int:
+        return int(self.doc_lengths().max()) if self.D else 0
+
     def stats(self) -> dict:
         return {"D": self.D, "V": self.V, "T": self.T, "nnz": self.nnz, "slices": self.n_slices,
                 "sell_slots": self.sell_slots, "sell_fill": (self.T / max(self.sell_slots, 1)),

@@ -39,6 +39,7 @@ class GibbsConfig:
     # (full gathered recount) | "atomic" (per-token Δ atomics)
     count_mode: str = "dual"
     prefetch_q: bool = True      # K<=32: fetch the next token's q row one step ahead
+    lds_counts: bool = False     # K<=32: doc-topic counts staged in LDS (k_gibbs_lds) instead of VGPRs
 
     def resolved_alpha(self) -> float:
         return float(self.alpha) if self.alpha is not None else 50.0 / self.K
@@ -79,6 +80,10 @@ class GibbsLDA:
         if self.mode == 2:
             self.tok_zprev = torch.zeros_like(self.tok_z)
             self.chg_mask = torch.zeros(max(corpus.sell_slots // corpus.S, 1), dtype=torch.int64, device=dev)
+        # the LDS sampler keeps counts as f32 integers: exact below 2^24 tokens per document
+        self.qpf = 1 if cfg.prefetch_q else 0
+        if cfg.lds_counts and self.G == 1 and corpus.max_doc_len() < (1 << 24):
+            self.qpf = 2
         self.a = 0  # ndk parity
         self.b = 0  # delta-buffer parity
         self.cn = 0  # nk parity
@@ -142,7 +147,7 @@ class GibbsLDA:
         ops.copy_rows(self.ndk[self.a], self.ndk[1 - self.a], c.long_rows, self.KS)
         ops.gibbs_pass(self._state(False), self.G, self.KP, self.K, self.alpha, self.cfg.seed, False,
                        self.sweep_ctr, c.chunk_len, host_sweep=self.sweeps_done + 1, mode=self.mode,
-                       prefetch_q=self.cfg.prefetch_q, chg_mask=getattr(self, "chg_mask", None), wpos=c.wpos,
+                       prefetch_q=self.qpf, chg_mask=getattr(self, "chg_mask", None), wpos=c.wpos,
                        z_w=getattr(self, "z_w", None))
         head = self.dn[self.b][: self.V * self.KS].view(self.V, self.KS)
         if self.mode == 0:

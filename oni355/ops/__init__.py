@@ -227,13 +227,14 @@ def sell_perm_z(chunk_doc, chunk_pos0, chunk_len, S, slice_off, doc_tok_ptr, tok
 # ------------------------------------------------------------------------------------------------
 def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init: bool, sweep_ctr: torch.Tensor,
                chunk_len: torch.Tensor, host_sweep: int | None = None, mode: int = 1,
-               prefetch_q: bool = False, chg_mask: torch.Tensor | None = None, wpos: torch.Tensor | None = None,
+               prefetch_q: bool | int = False, chg_mask: torch.Tensor | None = None, wpos: torch.Tensor | None = None,
                z_w: torch.Tensor | None = None) -> None:
     """Launch one init/sweep pass. ``st`` holds the OniGibbs tensors (see csrc/kernels/gibbs.hip).
 
     ``mode`` 1: accumulate Δn_wk with per-token atomics; 0: the caller rebuilds n_wk with
     :func:`recount`; 2: record changed slots in ``chg_mask`` for :func:`delta_recount`; 3: also
     write changed topics into the word-sorted copy ``z_w`` (via ``wpos``) for a streaming recount.
+    ``prefetch_q`` 1: register sampler with next-q-row prefetch; 2: LDS-staged doc counts (G=1).
     """
     atomic = mode == 1
     s0, s1 = spec.split_seed(seed)
@@ -269,7 +270,7 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
         a.wpos, a.z_w = _lib.ptr(wpos), _lib.ptr(z_w)
     a.n_slices, a.K, a.KS, a.alpha, a.seed0, a.seed1 = n_slices, K, KS, float(alpha), s0, s1
     _lib.check(_lib.lib().oni_gibbs_launch(C.byref(a), G, KP, 1 if init else 0, int(mode),
-                                           1 if prefetch_q else 0, _lib.stream()),
+                                           int(prefetch_q), _lib.stream()),
                "oni_gibbs_launch")
 
 

@@ -61,7 +61,9 @@ def _toy_tokens(n_docs, V, seed, heavy=True):
 
 
 @pytest.mark.parametrize("K,mode", [(20, "dual"), (20, "dual+noqpf"), (20, "delta"), (20, "recount"), (20, "atomic"),
-                                    (7, "dual"), (50, "dual"), (50, "delta"), (100, "atomic"), (100, "dual")])
+                                    (20, "dual+lds"), (20, "delta+lds"), (20, "atomic+lds"), (7, "dual+lds"),
+                                    (32, "dual+lds"), (7, "dual"), (50, "dual"), (50, "delta"), (100, "atomic"),
+                                    (100, "dual")])
 def test_gibbs_bitwise_vs_oracle(gpu, K, mode):
     tdoc, tword, keys = _toy_tokens(300, 400, K)
     G, KP = ops.choose_tiling(K)
@@ -71,7 +73,8 @@ def test_gibbs_bitwise_vs_oracle(gpu, K, mode):
     assert torch.equal(cc.chunk_doc, cg.chunk_doc.cpu())
     mc = GibbsLDA(cc, GibbsConfig(K=K, seed=1234, use_graph=False, count_mode="atomic"))
     mg = GibbsLDA(cg, GibbsConfig(K=K, seed=1234, use_graph=False, count_mode=mode.split("+")[0],
-                                  prefetch_q="noqpf" not in mode))
+                                  prefetch_q="noqpf" not in mode, lds_counts="lds" in mode))
+    assert (mg.qpf == 2) == ("lds" in mode)
     mc.initialize()
     mg.initialize()
     assert torch.equal(mc.tok_z, mg.tok_z.cpu())
