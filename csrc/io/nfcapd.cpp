@@ -11,10 +11,13 @@
 //   common record: flags, ext_map, msec_first/last, first/last, fwd_status, tcp_flags, prot, tos,
 //                  srcport, dstport, exporter_sysid, biFlowDir, flowEndReason  (32 B) then
 //                  src/dst address (v4 or v6), packets (4/8 B), bytes (4/8 B), map extensions.
-//   block compression: none, LZO1X (own decompressor), LZ4 block (own decompressor).
+//   block compression: none, LZO1X (own decompressor), LZ4 block (own decompressor), bzip2
+//   (the system libbz2, resolved with dlopen: the image ships the library but not its header).
 //
 // Not verifiable against the reference's submodule (empty gitlink): the format
 // is pinned by tests against our own writer (oni_nfcapd_write) and hand-built LZO/LZ4 streams.
+#include <dlfcn.h>
+
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -31,6 +34,45 @@ constexpr uint32_t kFlagLZO = 0x1, kFlagBZ2 = 0x8, kFlagLZ4 = 0x10;
 int ext_size(int id) {
   static const int sz[] = {0, 0, 0, 0, 4, 8, 4, 8, 4, 4, 16, 4, 16, 4, 4, 8, 4, 8, 4, 8, 16, 16, 40, 4, 16, 4, 8, 8};
   return (id >= 0 && id < (int)(sizeof(sz) / sizeof(sz[0]))) ? sz[id] : 0;
+}
+
+// ---- bzip2 (system libbz2.so.1, BZ2_bzBuffToBuff* one-shot API) --------------------------------
+using BzDecFn = int (*)(char*, unsigned*, char*, unsigned, int, int);
+using BzEncFn = int (*)(char*, unsigned*, char*, unsigned, int, int, int);
+constexpr int kBzOk = 0, kBzOutbuffFull = -8;
+
+void* bz2_handle() {
+  static void* h = dlopen("libbz2.so.1", RTLD_NOW | RTLD_LOCAL);
+  return h;
+}
+
+bool bz2_decompress(const uint8_t* in, size_t in_len, std::vector<uint8_t>* out) {
+  void* h = bz2_handle();
+  auto fn = h ? (BzDecFn)dlsym(h, "BZ2_bzBuffToBuffDecompress") : nullptr;
+  if (!fn || in_len > 0xFFFFFFFFu) return false;
+  size_t cap = in_len * 8 < (1u << 20) ? (1u << 20) : in_len * 8;
+  for (int tries = 0; tries < 8 && cap <= 0xFFFFFFFFu; ++tries, cap *= 4) {
+    out->resize(cap);
+    unsigned dl = (unsigned)cap;
+    const int rc = fn((char*)out->data(), &dl, (char*)in, (unsigned)in_len, 0, 0);
+    if (rc == kBzOk) {
+      out->resize(dl);
+      return true;
+    }
+    if (rc != kBzOutbuffFull) return false;
+  }
+  return false;
+}
+
+bool bz2_compress(const std::vector<uint8_t>& in, std::vector<uint8_t>* out) {
+  void* h = bz2_handle();
+  auto fn = h ? (BzEncFn)dlsym(h, "BZ2_bzBuffToBuffCompress") : nullptr;
+  if (!fn) return false;
+  unsigned dl = (unsigned)(in.size() + in.size() / 100 + 601);
+  out->resize(dl);
+  if (fn((char*)out->data(), &dl, (char*)in.data(), (unsigned)in.size(), 9, 0, 0) != kBzOk) return false;
+  out->resize(dl);
+  return true;
 }
 
 // ---- LZO1X decompressor (safe: bounds-checked) -------------------------------------------------
@@ -345,8 +387,8 @@ ONI_NATIVE_API void* oni_nfcapd_open(const char* path) {
     h->err = "not an nfcapd LAYOUT_VERSION_1 file";
     return h;
   }
-  if (flags & kFlagBZ2) {
-    h->err = "bz2-compressed nfcapd blocks are not supported";
+  if ((flags & kFlagBZ2) && !bz2_handle()) {
+    h->err = "bz2-compressed nfcapd file but libbz2.so.1 is not loadable";
     return h;
   }
   size_t pos = 140 + 160;  // header + stat record
@@ -376,6 +418,13 @@ ONI_NATIVE_API void* oni_nfcapd_open(const char* path) {
       } else if (flags & kFlagLZ4) {
         if (!lz4_decompress(data, size, &dec)) {
           h->err = "lz4 decompression failed";
+          break;
+        }
+        data = dec.data();
+        dlen = dec.size();
+      } else if (flags & kFlagBZ2) {
+        if (!bz2_decompress(data, size, &dec)) {
+          h->err = "bz2 decompression failed";
           break;
         }
         data = dec.data();
@@ -438,7 +487,8 @@ ONI_NATIVE_API int oni_lz4_decompress(const uint8_t* in, int64_t n, uint8_t* out
 }
 
 // ---- writer: LAYOUT_VERSION_1, one ext map {4 (io16), 6 (as16), 8 (multiple), 14, 16, 23, 27} ----
-// compression: 0 none, 1 LZO1X (literal-run encoding: valid stream, no matches), 2 LZ4 (literals only)
+// compression: 0 none, 1 LZO1X (literal-run encoding: valid stream, no matches), 2 LZ4 (literals only),
+// 3 bzip2 (libbz2)
 ONI_NATIVE_API int64_t oni_nfcapd_write(const char* path, int64_t n, const int64_t* first_ms, const int64_t* last_ms,
                                         const int64_t* received_ms, const uint32_t* sip, const uint32_t* dip,
                                         const int32_t* sport, const int32_t* dport, const int32_t* proto,
@@ -450,7 +500,12 @@ ONI_NATIVE_API int64_t oni_nfcapd_write(const char* path, int64_t n, const int64
   if (!f) return -1;
   std::vector<uint8_t> hdr(140 + 160, 0);
   const uint16_t magic = kMagic, version = 1;
-  const uint32_t flags = compression == 1 ? kFlagLZO : (compression == 2 ? kFlagLZ4 : 0);
+  const uint32_t flags =
+      compression == 1 ? kFlagLZO : (compression == 2 ? kFlagLZ4 : (compression == 3 ? kFlagBZ2 : 0));
+  if (compression == 3 && !bz2_handle()) {
+    std::fclose(f);
+    return -2;
+  }
   const uint32_t nblocks = (uint32_t)((n + per_block - 1) / per_block) + 1;
   std::memcpy(hdr.data(), &magic, 2);
   std::memcpy(hdr.data() + 2, &version, 2);
@@ -500,6 +555,8 @@ ONI_NATIVE_API int64_t oni_nfcapd_write(const char* path, int64_t n, const int64
         payload.push_back((uint8_t)(lit << 4));
       }
       payload.insert(payload.end(), raw.begin(), raw.end());
+    } else if (compression == 3) {
+      if (!bz2_compress(raw, &payload)) payload.clear();
     } else {
       payload = raw;
     }

@@ -58,7 +58,7 @@ def write_nfcapd(path: str, cols: dict, compression: str = "none", per_block: in
             np.asarray(cols.get("sas", z32), np.int32), np.asarray(cols.get("das", z32), np.int32),
             np.asarray(cols.get("rip", np.zeros(n)), np.uint32)]
     arrs = [np.ascontiguousarray(a) for a in arrs]
-    comp = {"none": 0, "lzo": 1, "lz4": 2}[compression]
+    comp = {"none": 0, "lzo": 1, "lz4": 2, "bz2": 3}[compression]
     r = native.lib().oni_nfcapd_write(path.encode(), n, *(a.ctypes.data for a in arrs), comp, per_block)
     if r != n:
         raise OSError(f"nfcapd write failed: {path}")

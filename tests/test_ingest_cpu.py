@@ -1,4 +1,4 @@
-"""Decoders + ingest on CPU: nfcapd (none/LZO/LZ4), LZO/LZ4 stream decoding, columnar store,
+"""Decoders + ingest on CPU: nfcapd (none/LZO/LZ4/bzip2), LZO/LZ4 stream decoding, columnar store,
 collector → day partitions → oni-ml from the store."""
 import os
 
@@ -12,11 +12,14 @@ from oni355.synth.flow import generate_flows
 KEYS = ["sip", "dip", "sport", "dport", "ibyt", "ipkt", "trhour", "trminute", "trsec", "proto", "unix_tstamp"]
 
 
-@pytest.mark.parametrize("comp", ["none", "lzo", "lz4"])
+@pytest.mark.parametrize("comp", ["none", "lzo", "lz4", "bz2"])
 def test_nfcapd_roundtrip(tmp_path, comp):
     day = generate_flows(5000, seed=2)
     p = str(tmp_path / "nfcapd.201607080000")
     nfcapd.write_nfcapd(p, day.cols, comp, per_block=1234)
+    if comp == "bz2":
+        raw = open(p, "rb").read()
+        assert raw.count(b"BZh9") >= 2  # every data block is a real bzip2 stream
     c = nfcapd.read_nfcapd(p)
     for k in KEYS:
         assert np.array_equal(np.asarray(c[k]), np.asarray(day.cols[k])), k

@@ -122,7 +122,7 @@ def build_native(n_jobs: int, verbose: bool, sanitize: bool) -> list[str]:
     lib = os.path.join(LIBDIR, f"liboni_native{suffix}.so")
     if objs:
         _run([CXX, "-shared", "-fopenmp", *([f for f in flags if f.startswith("-fsanitize")]), *objs,
-              "-o", lib + ".tmp"], verbose)
+              "-ldl", "-o", lib + ".tmp"], verbose)
         os.replace(lib + ".tmp", lib)
         outs.append(lib)
     for m in mains:
@@ -130,7 +130,7 @@ def build_native(n_jobs: int, verbose: bool, sanitize: bool) -> list[str]:
         o = os.path.join(OBJ, "native", f"{os.path.basename(m)}.{tag}.o")
         exe = os.path.join(BINDIR, name + suffix)
         _run([CXX, "-fopenmp", *([f for f in flags if f.startswith("-fsanitize")]), o, *objs,
-              "-o", exe + ".tmp"], verbose)
+              "-ldl", "-o", exe + ".tmp"], verbose)
         os.replace(exe + ".tmp", exe)
         outs.append(exe)
     return outs
