@@ -95,16 +95,16 @@ def main() -> int:
                     ops.delta_recount(c.wslot, c.tile_wlo, c.tile_whi, m.chg_mask, c.tok_word, m.tok_z, m.tok_zprev,
                                       head, m.KS, m.G)
                 elif stage == 3:
-                    ops.STREAM_RECOUNT = False
+                    ops.STREAM_RECOUNT = not ops.STREAM_RECOUNT
                     ops.recount(c.wsorted, None, m.z_w, head, m.KS)
-                    ops.STREAM_RECOUNT = True
+                    ops.STREAM_RECOUNT = not ops.STREAM_RECOUNT
                 elif stage == 2:
                     ops.gibbs_apply(m.nwk, m.dn[m.b], m.dn[1 - m.b], m.nk[m.cn], m.nk[1 - m.cn], m.q, m.V, m.K, m.KS,
                                     m.beta, m.vbeta, m.sweep_ctr, bump=False, absolute=m.mode in (0, 3))
                 ev[1].record()
                 torch.cuda.synchronize()
                 ts.append(ev[0].elapsed_time(ev[1]))
-            st[["sample", "recount", "apply", "recount_lds"][stage]] = float(np.median(ts))
+            st[["sample", "recount", "apply", "recount_alt"][stage]] = float(np.median(ts))
         out[name]["stages_ms"] = st
     print(json.dumps(out), flush=True)
     # chunk-length sweep (the sampler's serial critical path is L steps per lane)

@@ -301,18 +301,83 @@ __global__ void k_copy_rows(const int32_t* __restrict__ src, int32_t* __restrict
 
 // K ≤ 32 sweep with the doc-topic counts staged in LDS (one lane = one unit, G = 1).
 //
-// Each lane owns an LDS row a[0..KS) = (float)n_dk (exact integers while counts < 2^24, checked
-// by the host; the weight is formed as (a + α)·q exactly like k_gibbs), so the per-token count update is two single-address LDS read-modify-writes instead
-// of 2·KS compare/select VALU ops, and the row costs no VGPRs. The categorical draw takes two
-// passes over (a, q): pass 1 sums the total, pass 2 recomputes the same running sum (identical
-// f32 ops → identical values) and counts cut points ≤ thr, so no KS-long cumulative array is
-// held in registers either. Row stride is an odd number of 16-B slots → conflict-free b128 reads.
-// Bit-identical to k_gibbs (and the NumPy oracle).
+// Why: k_gibbs<1,KP> is VALU-issue bound (≈280 vector instructions per token at K = 20, 80 of
+// them the compare/select updates n[zo]-- / n[zn]++ of a register row with a per-lane index,
+// 20 the int→float converts and 20 the q-row copy on a word change). Here
+//  * each lane owns an LDS row a[0..KS) = (float)n_dk (exact integers below 2^24, checked by the
+//    host), so the count updates are two single-address LDS read-modify-writes;
+//  * the weights form a single fma chain P_j = fma(a_j + α, q_j, P_{j-1}) (the "fma" numerics of
+//    the spec, oni355/ref/spec.py gibbs_pass(fma=True)), P kept in registers for the count pass;
+//  * the q row of the next token is always prefetched into the other half of a register
+//    ping-pong (the loop is unrolled by two), so no per-token row copy is needed.
+// Row stride is an odd number of 16-B slots → conflict-free ds_read_b128.
+template <int KP>
+struct LdsRow {
+  static constexpr int kSlots = ((KP / 4) % 2 == 0) ? KP / 4 + 1 : KP / 4;
+};
+
+template <int KP, int MODE>
+__device__ __forceinline__ void lds_step(const OniGibbs& a, int s, int len, int64_t off, int lane, uint32_t key,
+                                         uint32_t pos0, uint32_t sweep, float4* __restrict__ row, oni::U4& r,
+                                         uint32_t& w_nx, int& z_nx, const float (&qc)[KP], float (&qn)[KP],
+                                         uint64_t* chg_word) {
+  constexpr int KS = KP;
+  float* rowf = reinterpret_cast<float*>(row);
+  const int64_t idx = off + (int64_t)s * 64 + lane;
+  const uint32_t w = w_nx;
+  const int zo = z_nx;
+  if (s + 1 < len) {
+    w_nx = a.tok_word[idx + 64];
+    z_nx = a.tok_z[idx + 64];
+    if (w_nx != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)w_nx * KS, qn);
+  }
+  const uint32_t pos = pos0 + (uint32_t)s;
+  if (s == 0 || (pos & 3u) == 0u) r = oni::philox10(oni::U4{pos >> 2, key, sweep, 1u}, a.seed0, a.seed1);
+  bool changed = false;
+  if (w != oni::kPadWord) {
+    const uint32_t rr = oni::pick4(r, pos & 3u);
+    rowf[zo] = rowf[zo] - 1.0f;
+    float P[KP];
+    float run = 0.f;
+#pragma unroll
+    for (int j = 0; j < KP / 4; ++j) {
+      const float4 av = row[j];
+      run = fmaf(av.x + a.alpha, qc[4 * j + 0], run);
+      P[4 * j + 0] = run;
+      run = fmaf(av.y + a.alpha, qc[4 * j + 1], run);
+      P[4 * j + 1] = run;
+      run = fmaf(av.z + a.alpha, qc[4 * j + 2], run);
+      P[4 * j + 2] = run;
+      run = fmaf(av.w + a.alpha, qc[4 * j + 3], run);
+      P[4 * j + 3] = run;
+    }
+    const float thr = oni::u01(rr) * run;
+    int cnt = 0;
+#pragma unroll
+    for (int j = 0; j < KP; ++j) cnt += P[j] <= thr;
+    const int zn = cnt < a.K - 1 ? cnt : a.K - 1;
+    rowf[zn] = rowf[zn] + 1.0f;
+    changed = zn != zo;
+    if (changed) {
+      a.tok_z[idx] = (uint8_t)zn;
+      if constexpr (MODE == 3) a.z_w[a.wpos[idx]] = (uint8_t)zn;
+      if constexpr (MODE == 1) {
+        atomicAdd(&a.dnwk[(int64_t)w * KS + zo], -1);
+        atomicAdd(&a.dnwk[(int64_t)w * KS + zn], 1);
+      }
+    }
+  }
+  if constexpr (MODE == 2) {
+    const uint64_t m = __ballot(changed);
+    if (lane == 0) chg_word[s] = m;
+  }
+}
+
 template <int KP, int MODE>
 __global__ __launch_bounds__(kBlock) void k_gibbs_lds(const OniGibbs a) {
   constexpr int KS = KP;
-  constexpr int STRIDE = ((KS / 4) % 2 == 0) ? KS + 4 : KS;
-  __shared__ __attribute__((aligned(16))) float sa[kBlock * STRIDE];
+  constexpr int kSlots = LdsRow<KP>::kSlots;
+  __shared__ float4 sa[kBlock * kSlots];
   __shared__ int32_t red[kWavesPerBlock][KS];
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
@@ -321,101 +386,42 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_lds(const OniGibbs a) {
   const int64_t chunk = slice * 64 + lane;
   const int doc = valid ? a.chunk_doc[chunk] : -1;
   const bool live = doc >= 0;
-  float* my = sa + threadIdx.x * STRIDE;
-  {
-    int32_t n0[KP];
+  float4* row = sa + threadIdx.x * kSlots;
+  int32_t n0[KP];
 #pragma unroll
-    for (int j = 0; j < KP; ++j) n0[j] = 0;
-    if (live) load_row_i<KP>(a.ndk_src + (int64_t)doc * KS, n0);
+  for (int j = 0; j < KP; ++j) n0[j] = 0;
+  if (live) load_row_i<KP>(a.ndk_src + (int64_t)doc * KS, n0);
 #pragma unroll
-    for (int j = 0; j < KP; j += 4)
-      *reinterpret_cast<float4*>(my + j) =
-          make_float4((float)n0[j], (float)n0[j + 1], (float)n0[j + 2], (float)n0[j + 3]);
-  }
+  for (int j = 0; j < KP / 4; ++j)
+    row[j] = make_float4((float)n0[4 * j], (float)n0[4 * j + 1], (float)n0[4 * j + 2], (float)n0[4 * j + 3]);
   const int len = valid ? a.slice_len[slice] : 0;
   const int64_t off = valid ? a.slice_off[slice] : 0;
   const uint32_t key = live ? a.chunk_key[chunk] : 0u;
   const uint32_t pos0 = live ? (uint32_t)a.chunk_pos0[chunk] : 0u;
   const uint32_t sweep = *a.sweep_ctr;
+  uint64_t* chg_word = MODE == 2 ? a.chg_mask + off / 64 : nullptr;
   oni::U4 r{0, 0, 0, 0};
-  uint32_t wprev = oni::kPadWord;
-  float qv[KP], qn[KP];
+  float qa[KP], qb[KP];
 #pragma unroll
-  for (int j = 0; j < KP; ++j) qv[j] = qn[j] = 0.f;
+  for (int j = 0; j < KP; ++j) qa[j] = qb[j] = 0.f;
   uint32_t w_nx = len > 0 ? a.tok_word[off + lane] : oni::kPadWord;
   int z_nx = len > 0 ? (int)a.tok_z[off + lane] : 0;
-  if (w_nx != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)w_nx * KS, qn);
-  for (int s = 0; s < len; ++s) {
-    const int64_t idx = off + (int64_t)s * 64 + lane;
-    const uint32_t w = w_nx;
-    const int zo = z_nx;
-    if (s + 1 < len) {
-      w_nx = a.tok_word[idx + 64];
-      z_nx = a.tok_z[idx + 64];
-    }
-    if (w == oni::kPadWord) continue;
-    const uint32_t pos = pos0 + (uint32_t)s;
-    if (s == 0 || (pos & 3u) == 0u) r = oni::philox10(oni::U4{pos >> 2, key, sweep, 1u}, a.seed0, a.seed1);
-    const uint32_t rr = oni::pick4(r, pos & 3u);
-    my[zo] = my[zo] - 1.0f;
-    if (w != wprev) {
-#pragma unroll
-      for (int j = 0; j < KP; ++j) qv[j] = qn[j];
-      wprev = w;
-    }
-    float run = 0.f;
-#pragma unroll
-    for (int j = 0; j < KP; j += 4) {
-      const float4 av = *reinterpret_cast<const float4*>(my + j);
-      run = run + (av.x + a.alpha) * qv[j];
-      run = run + (av.y + a.alpha) * qv[j + 1];
-      run = run + (av.z + a.alpha) * qv[j + 2];
-      run = run + (av.w + a.alpha) * qv[j + 3];
-    }
-    const float thr = oni::u01(rr) * run;
-    float run2 = 0.f;
-    int cnt = 0;
-#pragma unroll
-    for (int j = 0; j < KP; j += 4) {
-      const float4 av = *reinterpret_cast<const float4*>(my + j);
-      run2 = run2 + (av.x + a.alpha) * qv[j];
-      cnt += run2 <= thr;
-      run2 = run2 + (av.y + a.alpha) * qv[j + 1];
-      cnt += run2 <= thr;
-      run2 = run2 + (av.z + a.alpha) * qv[j + 2];
-      cnt += run2 <= thr;
-      run2 = run2 + (av.w + a.alpha) * qv[j + 3];
-      cnt += run2 <= thr;
-    }
-    const int zn = cnt < a.K - 1 ? cnt : a.K - 1;
-    my[zn] = my[zn] + 1.0f;
-    if (zn != zo) {
-      a.tok_z[idx] = (uint8_t)zn;
-      if constexpr (MODE == 3) a.z_w[a.wpos[idx]] = (uint8_t)zn;
-      if constexpr (MODE == 1) {
-        atomicAdd(&a.dnwk[(int64_t)w * KS + zo], -1);
-        atomicAdd(&a.dnwk[(int64_t)w * KS + zn], 1);
-      }
-    }
-    if constexpr (MODE == 2) {
-      const uint64_t m = __ballot(zn != zo);
-      if (lane == 0) a.chg_mask[(off + (int64_t)s * 64) / 64] = m;
-    }
-    if (s + 1 < len && w_nx != w && w_nx != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)w_nx * KS, qn);
+  if (w_nx != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)w_nx * KS, qa);
+  for (int s = 0; s < len; s += 2) {
+    lds_step<KP, MODE>(a, s, len, off, lane, key, pos0, sweep, row, r, w_nx, z_nx, qa, qb, chg_word);
+    if (s + 1 < len)
+      lds_step<KP, MODE>(a, s + 1, len, off, lane, key, pos0, sweep, row, r, w_nx, z_nx, qb, qa, chg_word);
   }
   // epilogue: counts back to ints, doc rows, per-topic totals
+  const float* rowf = reinterpret_cast<const float*>(row);
   int32_t d[KP], n[KP];
 #pragma unroll
   for (int j = 0; j < KP; ++j) {
-    n[j] = (int32_t)my[j];
-    d[j] = 0;
+    n[j] = (int32_t)rowf[j];
+    d[j] = n[j] - n0[j];
   }
   if (live) {
     int32_t* dst = a.ndk_dst + (int64_t)doc * KS;
-    int32_t n0[KP];
-    load_row_i<KP>(a.ndk_src + (int64_t)doc * KS, n0);
-#pragma unroll
-    for (int j = 0; j < KP; ++j) d[j] = n[j] - n0[j];
     if (a.chunk_multi[chunk]) {
 #pragma unroll
       for (int j = 0; j < KP; ++j)

@@ -17,7 +17,7 @@ from __future__ import annotations
 import math
 import os
 import time
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import numpy as np
 import torch
@@ -39,7 +39,9 @@ class GibbsConfig:
     # (full gathered recount) | "atomic" (per-token Δ atomics)
     count_mode: str = "dual"
     prefetch_q: bool = True      # K<=32: fetch the next token's q row one step ahead
-    lds_counts: bool = False     # K<=32: doc-topic counts staged in LDS (k_gibbs_lds) instead of VGPRs
+    # K<=32: doc-topic counts staged in LDS (k_gibbs_lds, fma numerics) instead of VGPRs;
+    # ONI_SAMPLER=lds|reg overrides the default
+    lds_counts: bool = field(default_factory=lambda: os.environ.get("ONI_SAMPLER", "reg") == "lds")
 
     def resolved_alpha(self) -> float:
         return float(self.alpha) if self.alpha is not None else 50.0 / self.K

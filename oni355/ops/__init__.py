@@ -245,7 +245,8 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
         if not atomic:
             npst["dnwk"] = np.zeros_like(npst["dnwk"])  # discarded: recount rebuilds n_wk
         spec.gibbs_pass(npst, G, KP, K, alpha, s0, s1, init,
-                        int(host_sweep if host_sweep is not None else sweep_ctr.item()), chunk_len.numpy())
+                        int(host_sweep if host_sweep is not None else sweep_ctr.item()), chunk_len.numpy(),
+                        fma=(int(prefetch_q) == 2 and not init))
         if mode == 3:
             valid = wpos >= 0
             z_w[wpos[valid].long()] = st["tok_z"][valid]
@@ -323,7 +324,7 @@ def recount(wsorted, wslot, tok_z, nwk_out, KS: int) -> None:
                                       RECOUNT_TILE, wmax, _lib.stream()), "oni_recount")
 
 
-STREAM_RECOUNT = True
+STREAM_RECOUNT = False  # k_recount (LDS histogram) measured faster: 0.105 vs 0.112 ms
 
 
 def gibbs_apply(nwk, dcur, dother, nk_cur, nk_next, q, V, K, KS, beta, vbeta, sweep_ctr, bump=True, absolute=False):

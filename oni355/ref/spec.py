@@ -209,9 +209,36 @@ def _chunk_geometry(st, S):
     return cid // S, cid % S
 
 
+def fma_f32(a: np.ndarray, b: np.ndarray, c: np.ndarray) -> np.ndarray:
+    """Correctly rounded f32 fma(a, b, c) (= v_fma_f32), emulated exactly in float64.
+
+    a·b is exact in f64 (24+24 bits); s = a·b + c is rounded once, its error e is recovered with
+    TwoSum. round_f32(s) is then the right answer unless s sits exactly on a midpoint between two
+    f32 values with e ≠ 0, in which case e decides the direction.
+    """
+    p = a.astype(np.float64) * b.astype(np.float64)
+    c64 = c.astype(np.float64)
+    s = p + c64
+    bb = s - p
+    e = (p - (s - bb)) + (c64 - bb)
+    r = s.astype(F32)
+    r64 = r.astype(np.float64)
+    other = np.nextafter(r, np.where(s > r64, np.inf, -np.inf).astype(F32))
+    mid = (s != r64) & ((r64 + other.astype(np.float64)) * 0.5 == s) & (e != 0)
+    if mid.any():
+        # exact value = s + e: above the midpoint -> the larger neighbour of s, else the smaller
+        hi = np.where(r64 > s, r, other)
+        lo = np.where(r64 > s, other, r)
+        r = np.where(mid, np.where(e > 0, hi, lo), r)
+    return r.astype(F32)
+
+
 def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed0: int, seed1: int, init: bool,
-               sweep: int, chunk_len: np.ndarray):
+               sweep: int, chunk_len: np.ndarray, fma: bool = False):
     """One init (init=True) or sweep pass over numpy state arrays, in place.
+
+    ``fma`` selects the numerics of the LDS-count sampler (k_gibbs_lds, G = 1): the running
+    weight sum is P_j = fma(n_j + α, q_j, P_{j-1}) instead of P_j = P_{j-1} + (n_j + α)·q_j.
 
     st keys: tok_word u32, tok_z u8, slice_off i64, slice_len i32, chunk_doc i32, chunk_pos0 i32,
     chunk_key u32, chunk_multi u8, ndk_src i32 [D,KS], ndk_dst i32 [D,KS], q f32 [V,KS],
@@ -246,8 +273,20 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed0: int, seed
         zo = st["tok_z"][idx].astype(np.int64)
         n[act, zo] -= 1
         qv = st["q"][w]
-        p = (n[act].astype(F32) + alpha32) * qv
-        if G == 1:
+        if fma:
+            assert G == 1
+            av = n[act].astype(F32) + alpha32
+            cum = np.empty_like(av)
+            run = np.zeros(av.shape[0], dtype=F32)
+            for j in range(KS):
+                run = fma_f32(av[:, j], qv[:, j], run)
+                cum[:, j] = run
+            total = run
+        else:
+            p = (n[act].astype(F32) + alpha32) * qv
+        if fma:
+            pass  # cum/total built above
+        elif G == 1:
             cum = np.cumsum(p, axis=1, dtype=F32)
             total = cum[:, -1]
         else:

@@ -71,7 +71,7 @@ def test_gibbs_bitwise_vs_oracle(gpu, K, mode):
     cg = build_corpus(tdoc.to(gpu), tword.to(gpu), 300, 400, torch.from_numpy(keys).to(gpu), G, L=64)
     assert torch.equal(cc.tok_word, cg.tok_word.cpu())
     assert torch.equal(cc.chunk_doc, cg.chunk_doc.cpu())
-    mc = GibbsLDA(cc, GibbsConfig(K=K, seed=1234, use_graph=False, count_mode="atomic"))
+    mc = GibbsLDA(cc, GibbsConfig(K=K, seed=1234, use_graph=False, count_mode="atomic", lds_counts="lds" in mode))
     mg = GibbsLDA(cg, GibbsConfig(K=K, seed=1234, use_graph=False, count_mode=mode.split("+")[0],
                                   prefetch_q="noqpf" not in mode, lds_counts="lds" in mode))
     assert (mg.qpf == 2) == ("lds" in mode)

@@ -148,3 +148,42 @@ def test_lda_cli(tmp_path):
     g = ldac.read_matrix(str(tmp_path / "inf-gamma.dat"))
     assert g.shape == (30, 2)
     assert os.path.exists(str(tmp_path / "inf-lda-lhood.dat"))
+
+
+def test_fma_f32_matches_exact_rounding():
+    from fractions import Fraction
+    r = np.random.default_rng(3)
+    n = 3000
+    a = (r.random(n) * 100).astype(np.float32)
+    b = (r.random(n) * 1e-3).astype(np.float32)
+    c = r.random(n).astype(np.float32)
+    # midpoint cases: c + a*b lands exactly on / next to a half-ulp of c
+    a[:1000] = np.float32(1.0) + np.float32(2.0 ** -23) * r.integers(0, 4, 1000).astype(np.float32)
+    b[:1000] = np.float32(2.0 ** -24)
+    c[:1000] = np.float32(1.0)
+    got = spec.fma_f32(a, b, c)
+    for i in range(n):
+        v = Fraction(float(a[i])) * Fraction(float(b[i])) + Fraction(float(c[i]))
+        f = np.float32(float(v))
+        cands = [np.nextafter(f, np.float32(-np.inf)), f, np.nextafter(f, np.float32(np.inf))]
+        best = min(cands, key=lambda x: (abs(Fraction(float(x)) - v), int(np.float32(x).view(np.uint32)) & 1))
+        assert got[i] == best, i
+
+
+def test_lds_sampler_oracle_keeps_counts_consistent():
+    import torch
+
+    from oni355.models.corpus import build_corpus
+    from oni355.models.gibbs import GibbsConfig, GibbsLDA
+    r = np.random.default_rng(4)
+    lens = r.integers(1, 300, 80)
+    tdoc = torch.from_numpy(np.repeat(np.arange(80), lens))
+    tword = torch.from_numpy(r.integers(0, 50, int(lens.sum())))
+    keys = torch.arange(80, dtype=torch.int32) * 7 + 1
+    c = build_corpus(tdoc, tword, 80, 50, keys, 1, L=64)
+    m = GibbsLDA(c, GibbsConfig(K=20, seed=5, lds_counts=True))
+    assert m.qpf == 2
+    m.initialize()
+    m.sweep(3)
+    T = c.T
+    assert int(m.nwk[:, :20].sum()) == T == int(m.ndk_cur[:, :20].sum()) == int(m.nk_cur[:20].sum())
