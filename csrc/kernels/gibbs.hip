@@ -316,51 +316,56 @@ struct LdsRow {
   static constexpr int kSlots = ((KP / 4) % 2 == 0) ? KP / 4 + 1 : KP / 4;
 };
 
-template <int KP, int MODE>
+// One token step of k_gibbs_lds. Token words/topics (and MODE-3 word-sorted slots) are
+// streamed two steps ahead in a parity-indexed register pair (P is the compile-time parity of s),
+// the q row one step ahead into the other half of the q ping-pong.
+template <int KP, int MODE, int P>
 __device__ __forceinline__ void lds_step(const OniGibbs& a, int s, int len, int64_t off, int lane, uint32_t key,
                                          uint32_t pos0, uint32_t sweep, float4* __restrict__ row, oni::U4& r,
-                                         uint32_t& w_nx, int& z_nx, const float (&qc)[KP], float (&qn)[KP],
-                                         uint64_t* chg_word) {
+                                         uint32_t (&wq)[2], int (&zq)[2], int32_t (&pq)[2], const float (&qc)[KP],
+                                         float (&qn)[KP], uint64_t* chg_word) {
   constexpr int KS = KP;
   float* rowf = reinterpret_cast<float*>(row);
   const int64_t idx = off + (int64_t)s * 64 + lane;
-  const uint32_t w = w_nx;
-  const int zo = z_nx;
-  if (s + 1 < len) {
-    w_nx = a.tok_word[idx + 64];
-    z_nx = a.tok_z[idx + 64];
-    if (w_nx != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)w_nx * KS, qn);
+  const uint32_t w = wq[P];
+  const int zo = zq[P];
+  const int32_t wp = pq[P];
+  if (s + 2 < len) {
+    wq[P] = a.tok_word[idx + 128];
+    zq[P] = a.tok_z[idx + 128];
+    if constexpr (MODE == 3) pq[P] = a.wpos[idx + 128];
   }
+  if (s + 1 < len && wq[1 - P] != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)wq[1 - P] * KS, qn);
   const uint32_t pos = pos0 + (uint32_t)s;
   if (s == 0 || (pos & 3u) == 0u) r = oni::philox10(oni::U4{pos >> 2, key, sweep, 1u}, a.seed0, a.seed1);
   bool changed = false;
   if (w != oni::kPadWord) {
     const uint32_t rr = oni::pick4(r, pos & 3u);
     rowf[zo] = rowf[zo] - 1.0f;
-    float P[KP];
+    float Pc[KP];
     float run = 0.f;
 #pragma unroll
     for (int j = 0; j < KP / 4; ++j) {
       const float4 av = row[j];
       run = fmaf(av.x + a.alpha, qc[4 * j + 0], run);
-      P[4 * j + 0] = run;
+      Pc[4 * j + 0] = run;
       run = fmaf(av.y + a.alpha, qc[4 * j + 1], run);
-      P[4 * j + 1] = run;
+      Pc[4 * j + 1] = run;
       run = fmaf(av.z + a.alpha, qc[4 * j + 2], run);
-      P[4 * j + 2] = run;
+      Pc[4 * j + 2] = run;
       run = fmaf(av.w + a.alpha, qc[4 * j + 3], run);
-      P[4 * j + 3] = run;
+      Pc[4 * j + 3] = run;
     }
     const float thr = oni::u01(rr) * run;
     int cnt = 0;
 #pragma unroll
-    for (int j = 0; j < KP; ++j) cnt += P[j] <= thr;
+    for (int j = 0; j < KP; ++j) cnt += Pc[j] <= thr;
     const int zn = cnt < a.K - 1 ? cnt : a.K - 1;
     rowf[zn] = rowf[zn] + 1.0f;
     changed = zn != zo;
     if (changed) {
       a.tok_z[idx] = (uint8_t)zn;
-      if constexpr (MODE == 3) a.z_w[a.wpos[idx]] = (uint8_t)zn;
+      if constexpr (MODE == 3) a.z_w[wp] = (uint8_t)zn;
       if constexpr (MODE == 1) {
         atomicAdd(&a.dnwk[(int64_t)w * KS + zo], -1);
         atomicAdd(&a.dnwk[(int64_t)w * KS + zn], 1);
@@ -387,13 +392,15 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_lds(const OniGibbs a) {
   const int doc = valid ? a.chunk_doc[chunk] : -1;
   const bool live = doc >= 0;
   float4* row = sa + threadIdx.x * kSlots;
-  int32_t n0[KP];
+  {
+    int32_t n0[KP];
 #pragma unroll
-  for (int j = 0; j < KP; ++j) n0[j] = 0;
-  if (live) load_row_i<KP>(a.ndk_src + (int64_t)doc * KS, n0);
+    for (int j = 0; j < KP; ++j) n0[j] = 0;
+    if (live) load_row_i<KP>(a.ndk_src + (int64_t)doc * KS, n0);
 #pragma unroll
-  for (int j = 0; j < KP / 4; ++j)
-    row[j] = make_float4((float)n0[4 * j], (float)n0[4 * j + 1], (float)n0[4 * j + 2], (float)n0[4 * j + 3]);
+    for (int j = 0; j < KP / 4; ++j)
+      row[j] = make_float4((float)n0[4 * j], (float)n0[4 * j + 1], (float)n0[4 * j + 2], (float)n0[4 * j + 3]);
+  }
   const int len = valid ? a.slice_len[slice] : 0;
   const int64_t off = valid ? a.slice_off[slice] : 0;
   const uint32_t key = live ? a.chunk_key[chunk] : 0u;
@@ -404,17 +411,28 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_lds(const OniGibbs a) {
   float qa[KP], qb[KP];
 #pragma unroll
   for (int j = 0; j < KP; ++j) qa[j] = qb[j] = 0.f;
-  uint32_t w_nx = len > 0 ? a.tok_word[off + lane] : oni::kPadWord;
-  int z_nx = len > 0 ? (int)a.tok_z[off + lane] : 0;
-  if (w_nx != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)w_nx * KS, qa);
-  for (int s = 0; s < len; s += 2) {
-    lds_step<KP, MODE>(a, s, len, off, lane, key, pos0, sweep, row, r, w_nx, z_nx, qa, qb, chg_word);
-    if (s + 1 < len)
-      lds_step<KP, MODE>(a, s + 1, len, off, lane, key, pos0, sweep, row, r, w_nx, z_nx, qb, qa, chg_word);
+  uint32_t wq[2] = {oni::kPadWord, oni::kPadWord};
+  int zq[2] = {0, 0};
+  int32_t pq[2] = {0, 0};
+  for (int t = 0; t < 2; ++t) {
+    if (t < len) {
+      wq[t] = a.tok_word[off + t * 64 + lane];
+      zq[t] = a.tok_z[off + t * 64 + lane];
+      if constexpr (MODE == 3) pq[t] = a.wpos[off + t * 64 + lane];
+    }
   }
-  // epilogue: counts back to ints, doc rows, per-topic totals
+  if (wq[0] != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)wq[0] * KS, qa);
+  for (int s = 0; s < len; s += 2) {
+    lds_step<KP, MODE, 0>(a, s, len, off, lane, key, pos0, sweep, row, r, wq, zq, pq, qa, qb, chg_word);
+    if (s + 1 < len)
+      lds_step<KP, MODE, 1>(a, s + 1, len, off, lane, key, pos0, sweep, row, r, wq, zq, pq, qb, qa, chg_word);
+  }
+  // epilogue: counts back to ints, doc rows, per-topic totals (n0 re-read: keeps it out of VGPRs)
   const float* rowf = reinterpret_cast<const float*>(row);
-  int32_t d[KP], n[KP];
+  int32_t d[KP], n[KP], n0[KP];
+#pragma unroll
+  for (int j = 0; j < KP; ++j) n0[j] = 0;
+  if (live) load_row_i<KP>(a.ndk_src + (int64_t)doc * KS, n0);
 #pragma unroll
   for (int j = 0; j < KP; ++j) {
     n[j] = (int32_t)rowf[j];
