@@ -36,7 +36,7 @@ struct OniGibbs {
   int32_t* ndk_dst;            // [D][KS] output doc-topic counts
   const float* q;              // [V][KS] sweep-start word factor
   int32_t* dnwk;               // [V][KS] word-topic delta (init: the n_wk table itself)
-  int32_t* dnk;                // [KS]    topic-total delta (init: n_k itself)
+  int32_t* dnk;                // [nk_rep][KS] topic-total delta replicas (init: n_k itself, nk_rep = 1)
   const uint32_t* sweep_ctr;   // device scalar: current sweep number (≥ 1), graph-replay safe
   uint64_t* chg_mask;          // MODE 2: one u64 per SELL step, bit c*G set if slot c's topic changed
   const int32_t* wpos;         // MODE 3: word-sorted position of every SELL slot
@@ -46,6 +46,8 @@ struct OniGibbs {
   int32_t KS;
   float alpha;
   uint32_t seed0, seed1;
+  int32_t nk_rep;              // dnk holds nk_rep replicas of [KS] (power of 2): block b adds into b % nk_rep
+  int32_t pad_;
 };
 
 namespace {
@@ -67,6 +69,43 @@ __device__ __forceinline__ void load_row_f(const float* __restrict__ p, float (&
   for (int j = 0; j < KP; j += 4) {
     const float4 t = *reinterpret_cast<const float4*>(p + j);
     v[j] = t.x; v[j + 1] = t.y; v[j + 2] = t.z; v[j + 3] = t.w;
+  }
+}
+
+// Long documents: all full-length chunks of a doc are adjacent in the chunk order (stable sort by
+// length), so consecutive units of a wave often belong to the same doc. Their count deltas are
+// summed over each such run inside the wave first (segmented suffix sum over units, shuffles at
+// unit stride G) and only the run's first unit issues the atomics: same-address atomics execute
+// serially at the memory side, so one heavy IP spread over thousands of chunks would otherwise
+// queue KS × chunks adds on a single row (measured: ~2 ms/sweep in the high-change early sweeps).
+template <int G, int KP>
+__device__ __forceinline__ void flush_multi_rows(int32_t* __restrict__ ndk_dst, int KS, int doc, bool multi,
+                                                 int kbase, const int32_t (&delta)[KP]) {
+  constexpr int S = oni::kWave / G;
+  const int lane = threadIdx.x & (oni::kWave - 1);
+  const int c = lane / G;
+  const int prev_doc = __shfl_up(doc, G);
+  const bool head = (c == 0) || prev_doc != doc;
+  const uint64_t heads = __ballot(head && (lane % G) == 0);
+  const int first_lane_of_next = c * G + G;
+  const uint64_t above = first_lane_of_next < oni::kWave ? heads & (~0ull << first_lane_of_next) : 0ull;
+  const int next = above ? (__ffsll((unsigned long long)above) - 1) / G : S;
+  int32_t d[KP];
+#pragma unroll
+  for (int j = 0; j < KP; ++j) d[j] = delta[j];
+#pragma unroll
+  for (int off = 1; off < S; off <<= 1) {
+#pragma unroll
+    for (int j = 0; j < KP; ++j) {
+      const int o = __shfl_down(d[j], off * G);
+      if (c + off < next) d[j] += o;
+    }
+  }
+  if (multi && head) {
+    int32_t* dst = ndk_dst + (int64_t)doc * KS + kbase;
+#pragma unroll
+    for (int j = 0; j < KP; ++j)
+      if (d[j]) atomicAdd(dst + j, d[j]);
   }
 }
 
@@ -213,14 +252,14 @@ __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
 #pragma unroll
       for (int j = 0; j < KP; ++j) d[j] = n[j] - n0[j];
     }
-    if (a.chunk_multi[chunk]) {
-#pragma unroll
-      for (int j = 0; j < KP; ++j)
-        if (d[j]) atomicAdd(dst + j, d[j]);
-    } else {
+    if (!a.chunk_multi[chunk]) {
 #pragma unroll
       for (int j = 0; j < KP; j += 4) *reinterpret_cast<int4*>(dst + j) = make_int4(n[j], n[j + 1], n[j + 2], n[j + 3]);
     }
+  }
+  {
+    const bool multi = live && a.chunk_multi[chunk];
+    if (__ballot(multi)) flush_multi_rows<G, KP>(a.ndk_dst, KS, doc, multi, kbase, d);
   }
   // reduce d over the S units of this wave (lanes with equal g), then over the block's waves
 #pragma unroll
@@ -239,7 +278,7 @@ __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
     int v = 0;
 #pragma unroll
     for (int w = 0; w < kWavesPerBlock; ++w) v += red[w][threadIdx.x];
-    if (v) atomicAdd(&a.dnk[threadIdx.x], v);
+    if (v) atomicAdd(&a.dnk[(int)(blockIdx.x & (unsigned)(a.nk_rep - 1)) * KS + threadIdx.x], v);
   }
 }
 
@@ -250,21 +289,20 @@ __global__ __launch_bounds__(256) void k_apply(int32_t* __restrict__ nwk, const 
                                                 int32_t* __restrict__ dother, const int32_t* __restrict__ nk_cur,
                                                 int32_t* __restrict__ nk_next, float* __restrict__ q, int64_t V,
                                                 int K, int KS, float beta, float vbeta, uint32_t* sweep_ctr,
-                                                int bump, int absolute) {
+                                                int bump, int absolute, int nk_rep) {
   __shared__ float den[256];
   __shared__ int32_t nkn[256];
   const int32_t* dnk_cur = dcur + V * KS;
   for (int k = threadIdx.x; k < KS; k += blockDim.x) {
-    const int32_t v = nk_cur[k] + dnk_cur[k];
+    int32_t v = nk_cur[k];
+    for (int r = 0; r < nk_rep; ++r) v += dnk_cur[r * KS + k];
     nkn[k] = v;
     den[k] = (float)v + vbeta;
   }
   __syncthreads();
   if (blockIdx.x == 0) {
-    for (int k = threadIdx.x; k < KS; k += blockDim.x) {
-      nk_next[k] = nkn[k];
-      dother[V * KS + k] = 0;
-    }
+    for (int k = threadIdx.x; k < KS; k += blockDim.x) nk_next[k] = nkn[k];
+    for (int k = threadIdx.x; k < nk_rep * KS; k += blockDim.x) dother[V * KS + k] = 0;
     if (threadIdx.x == 0 && bump) *sweep_ctr += 1u;
   }
   const int64_t nvec = V * KS / 4;
@@ -438,17 +476,13 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_lds(const OniGibbs a) {
     n[j] = (int32_t)rowf[j];
     d[j] = n[j] - n0[j];
   }
-  if (live) {
+  const bool multi = live && a.chunk_multi[chunk];
+  if (live && !multi) {
     int32_t* dst = a.ndk_dst + (int64_t)doc * KS;
-    if (a.chunk_multi[chunk]) {
 #pragma unroll
-      for (int j = 0; j < KP; ++j)
-        if (d[j]) atomicAdd(dst + j, d[j]);
-    } else {
-#pragma unroll
-      for (int j = 0; j < KP; j += 4) *reinterpret_cast<int4*>(dst + j) = make_int4(n[j], n[j + 1], n[j + 2], n[j + 3]);
-    }
+    for (int j = 0; j < KP; j += 4) *reinterpret_cast<int4*>(dst + j) = make_int4(n[j], n[j + 1], n[j + 2], n[j + 3]);
   }
+  if (__ballot(multi)) flush_multi_rows<1, KP>(a.ndk_dst, KS, doc, multi, 0, d);
 #pragma unroll
   for (int j = 0; j < KP; ++j) {
     int v = d[j];
@@ -465,7 +499,7 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_lds(const OniGibbs a) {
     int v = 0;
 #pragma unroll
     for (int w = 0; w < kWavesPerBlock; ++w) v += red[w][threadIdx.x];
-    if (v) atomicAdd(&a.dnk[threadIdx.x], v);
+    if (v) atomicAdd(&a.dnk[(int)(blockIdx.x & (unsigned)(a.nk_rep - 1)) * KS + threadIdx.x], v);
   }
 }
 
@@ -680,6 +714,7 @@ ONI_API int oni_recount_stream(const int32_t* wsorted, const uint8_t* z_w, int64
 
 // Supported (G, KP) configurations. K ≤ 32: G = 1 (KP = K rounded up to 4).
 ONI_API int oni_gibbs_launch(const OniGibbs* a, int G, int KP, int init, int mode, int qpf, hipStream_t s) {
+  if (a->nk_rep < 1 || (a->nk_rep & (a->nk_rep - 1))) return (int)hipErrorInvalidValue;
   if (a->K < 1 || a->K > 255 || a->K > a->KS || mode < 0 || mode > 3) return (int)hipErrorInvalidValue;
   if (mode == 2 && !a->chg_mask) return (int)hipErrorInvalidValue;
   if (mode == 3 && (!a->wpos || !a->z_w)) return (int)hipErrorInvalidValue;
@@ -698,10 +733,10 @@ ONI_API int oni_gibbs_sizeof_args() { return (int)sizeof(OniGibbs); }
 
 ONI_API int oni_gibbs_apply(int32_t* nwk, const int32_t* dcur, int32_t* dother, const int32_t* nk_cur,
                             int32_t* nk_next, float* q, int64_t V, int K, int KS, float beta, float vbeta,
-                            uint32_t* sweep_ctr, int bump, int absolute, hipStream_t s) {
-  if (KS % 4 != 0 || KS > 256) return (int)hipErrorInvalidValue;
+                            uint32_t* sweep_ctr, int bump, int absolute, int nk_rep, hipStream_t s) {
+  if (KS % 4 != 0 || KS > 256 || nk_rep < 1 || (nk_rep & (nk_rep - 1))) return (int)hipErrorInvalidValue;
   k_apply<<<oni::grid_for(V * KS / 4, 256, 2048), 256, 0, s>>>(nwk, dcur, dother, nk_cur, nk_next, q, V, K, KS, beta,
-                                                                vbeta, sweep_ctr, bump, absolute);
+                                                                vbeta, sweep_ctr, bump, absolute, nk_rep);
   return (int)hipGetLastError();
 }
 

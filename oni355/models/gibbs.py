@@ -27,6 +27,9 @@ from ..utils import fault
 from .corpus import Corpus, canonical_tokens
 
 
+NK_REP = 32
+
+
 @dataclass
 class GibbsConfig:
     K: int = 20
@@ -71,7 +74,9 @@ class GibbsLDA:
         self.ndk = [torch.zeros(max(D, 1), KS, dtype=i32, device=dev) for _ in range(2)]
         self.nwk = torch.zeros(V, KS, dtype=i32, device=dev)
         self.nk = [torch.zeros(KS, dtype=i32, device=dev) for _ in range(2)]
-        self.dn = [torch.zeros(V * KS + KS, dtype=i32, device=dev) for _ in range(2)]
+        # Δn_k in NK_REP replicas (block b adds into b % NK_REP): the per-block topic totals
+        # would otherwise queue thousands of same-address atomics on KS words
+        self.dn = [torch.zeros(V * KS + NK_REP * KS, dtype=i32, device=dev) for _ in range(2)]
         self.q = torch.zeros(V, KS, dtype=torch.float32, device=dev)
         self.sweep_ctr = torch.zeros(1, dtype=i32, device=dev)
         if cfg.count_mode not in ("dual", "delta", "recount", "atomic"):

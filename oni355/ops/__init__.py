@@ -239,9 +239,13 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
     atomic = mode == 1
     s0, s1 = spec.split_seed(seed)
     KS = G * KP
+    nk_rep = st["dnk"].numel() // KS
+    if nk_rep < 1 or nk_rep * KS != st["dnk"].numel() or nk_rep & (nk_rep - 1):
+        raise ValueError("dnk must hold a power-of-two number of [KS] replicas")
     if not _is_dev(st["tok_word"]):
         npst = {k: (v.numpy().view(np.uint32) if k in ("tok_word", "chunk_key") else v.numpy())
                 for k, v in st.items()}
+        npst["dnk"] = npst["dnk"][:KS]  # replica 0 (the sum over replicas is what counts)
         if not atomic:
             npst["dnwk"] = np.zeros_like(npst["dnwk"])  # discarded: recount rebuilds n_wk
         spec.gibbs_pass(npst, G, KP, K, alpha, s0, s1, init,
@@ -270,6 +274,7 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
             raise ValueError("dual mode needs wpos [SELL slots] and z_w [T]")
         a.wpos, a.z_w = _lib.ptr(wpos), _lib.ptr(z_w)
     a.n_slices, a.K, a.KS, a.alpha, a.seed0, a.seed1 = n_slices, K, KS, float(alpha), s0, s1
+    a.nk_rep = nk_rep
     _lib.check(_lib.lib().oni_gibbs_launch(C.byref(a), G, KP, 1 if init else 0, int(mode),
                                            int(prefetch_q), _lib.stream()),
                "oni_gibbs_launch")
@@ -328,9 +333,14 @@ STREAM_RECOUNT = False  # k_recount (LDS histogram) measured faster: 0.105 vs 0.
 
 
 def gibbs_apply(nwk, dcur, dother, nk_cur, nk_next, q, V, K, KS, beta, vbeta, sweep_ctr, bump=True, absolute=False):
+    """n_wk ← Δ (or absolute), n_k ← n_k + Σ_replicas Δn_k, q refresh; zeroes ``dother``.
+
+    ``dcur``/``dother`` are [V·KS + R·KS]: the Δn_wk table then R replicas of Δn_k."""
+    nk_rep = (dcur.numel() - V * KS) // KS
     if not _is_dev(nwk):
         base = np.zeros_like(nwk.numpy()) if absolute else nwk.numpy()
-        n2, nk2, q2 = spec.gibbs_apply(base, dcur[: V * KS].view(V, KS).numpy(), dcur[V * KS:].numpy(),
+        n2, nk2, q2 = spec.gibbs_apply(base, dcur[: V * KS].view(V, KS).numpy(),
+                                       dcur[V * KS:].view(-1, KS).sum(0, dtype=torch.int32).numpy(),
                                        nk_cur.numpy(), K, beta, vbeta)
         nwk.copy_(torch.from_numpy(n2))
         nk_next.copy_(torch.from_numpy(nk2))
@@ -341,7 +351,7 @@ def gibbs_apply(nwk, dcur, dother, nk_cur, nk_next, q, V, K, KS, beta, vbeta, sw
         return
     _lib.check(_lib.lib().oni_gibbs_apply(*map(_lib.ptr, (nwk, dcur, dother, nk_cur, nk_next, q)), V, K, KS,
                                           float(beta), float(vbeta), _lib.ptr(sweep_ctr), 1 if bump else 0,
-                                          1 if absolute else 0, _lib.stream()), "oni_gibbs_apply")
+                                          1 if absolute else 0, nk_rep, _lib.stream()), "oni_gibbs_apply")
 
 
 def copy_rows(src, dst, rows, KS):

@@ -34,6 +34,7 @@ class OniGibbs(C.Structure):
         ("ndk_src", vp), ("ndk_dst", vp), ("q", vp), ("dnwk", vp), ("dnk", vp), ("sweep_ctr", vp), ("chg_mask", vp),
         ("wpos", vp), ("z_w", vp),
         ("n_slices", i64), ("K", i32), ("KS", i32), ("alpha", f32), ("seed0", u32), ("seed1", u32),
+        ("nk_rep", i32), ("pad_", i32),
     ]
 
 
@@ -48,7 +49,7 @@ _SIGS = {
     "oni_sell_perm_z": [vp, vp, vp, i64, C.c_int, vp, vp, vp, vp, C.c_int, vp],
     "oni_gibbs_launch": [C.POINTER(OniGibbs), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp],
     "oni_gibbs_sizeof_args": [],
-    "oni_gibbs_apply": [vp, vp, vp, vp, vp, vp, i64, C.c_int, C.c_int, f32, f32, vp, C.c_int, C.c_int, vp],
+    "oni_gibbs_apply": [vp, vp, vp, vp, vp, vp, i64, C.c_int, C.c_int, f32, f32, vp, C.c_int, C.c_int, C.c_int, vp],
     "oni_recount": [vp, vp, vp, i64, vp, C.c_int, C.c_int, C.c_int, vp],
     "oni_recount_stream": [vp, vp, i64, vp, C.c_int, C.c_int, C.c_int, vp],
     "oni_delta_recount": [vp, vp, vp, vp, vp, vp, vp, i64, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp],
