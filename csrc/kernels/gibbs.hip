@@ -594,24 +594,69 @@ __global__ __launch_bounds__(256) void k_delta_recount(const int32_t* __restrict
 // block's word span, capped at wmax; the tail of a very wide span goes straight to global), and
 // flushes one row-contiguous atomic per non-zero (word, topic) cell. The topic gather z[wslot]
 // reads 1 byte per token from the (L2/MALL-resident) SELL topic array.
+// Word-sorted recount tile: 4096 tokens, 256 threads × 16 CONTIGUOUS tokens each, loaded with
+// 16-B vector loads up front (one memory round trip per thread instead of a dependent
+// load→atomic chain per token), counted into an LDS histogram of the tile's word rows, flushed
+// with one global atomic per non-zero cell. The LDS histogram is capped at kRecountCells cells
+// (8 KB) so ≥ 8 blocks fit per CU — a 64 KB cap left 2 waves per SIMD and made the kernel
+// latency-bound; rows beyond the cap (tail tiles of rare words) go straight to global atomics.
+constexpr int kRecountTile = 4096;
+constexpr int kRecountCells = 2048;
+
 __global__ __launch_bounds__(256) void k_recount(const int32_t* __restrict__ wsorted, const int32_t* __restrict__ wslot,
                                                   const uint8_t* __restrict__ tok_z, int64_t T, int32_t* __restrict__ nwk,
-                                                  int KS, int tile, int wmax) {
-  extern __shared__ __attribute__((aligned(16))) int32_t hst[];
-  const int64_t lo = (int64_t)blockIdx.x * tile;
+                                                  int KS) {
+  __shared__ int32_t hst[kRecountCells];
+  const int64_t lo = (int64_t)blockIdx.x * kRecountTile;
   if (lo >= T) return;
-  const int64_t hi = lo + tile < T ? lo + tile : T;
+  const int64_t hi = lo + kRecountTile < T ? lo + kRecountTile : T;
   const int w_lo = wsorted[lo], w_hi = wsorted[hi - 1];
-  const int rows = (w_hi - w_lo + 1) < wmax ? (w_hi - w_lo + 1) : wmax;
+  const int cap_rows = kRecountCells / KS;
+  const int rows = (w_hi - w_lo + 1) < cap_rows ? (w_hi - w_lo + 1) : cap_rows;
   const int cells = rows * KS;
   for (int i = threadIdx.x; i < cells; i += blockDim.x) hst[i] = 0;
+  const int64_t base = lo + (int64_t)threadIdx.x * 16;
+  int w[16], z[16];
+  int nt = 0;
+  if (base + 16 <= hi) {
+    nt = 16;
+    const int4* wp = reinterpret_cast<const int4*>(wsorted + base);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int4 v = wp[q];
+      w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+    }
+    if (wslot) {
+      const int4* sp = reinterpret_cast<const int4*>(wslot + base);
+      int sl[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int4 v = sp[q];
+        sl[4 * q] = v.x; sl[4 * q + 1] = v.y; sl[4 * q + 2] = v.z; sl[4 * q + 3] = v.w;
+      }
+#pragma unroll
+      for (int t = 0; t < 16; ++t) z[t] = tok_z[sl[t]];
+    } else {
+      const uint4 zb = *reinterpret_cast<const uint4*>(tok_z + base);
+      const uint32_t zz[4] = {zb.x, zb.y, zb.z, zb.w};
+#pragma unroll
+      for (int t = 0; t < 16; ++t) z[t] = (int)((zz[t >> 2] >> (8 * (t & 3))) & 0xFFu);
+    }
+  } else if (base < hi) {
+    nt = (int)(hi - base);
+    for (int t = 0; t < nt; ++t) {
+      w[t] = wsorted[base + t];
+      z[t] = wslot ? tok_z[wslot[base + t]] : tok_z[base + t];
+    }
+  }
   __syncthreads();
-  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-    const int w = wsorted[i];
-    const int z = wslot ? tok_z[wslot[i]] : tok_z[i];  // wslot == nullptr: tok_z is already word-sorted
-    const int r = w - w_lo;
-    if (r < rows) atomicAdd(&hst[r * KS + z], 1);
-    else atomicAdd(&nwk[(int64_t)w * KS + z], 1);
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    if (t < nt) {
+      const int r = w[t] - w_lo;
+      if (r < rows) atomicAdd(&hst[r * KS + z[t]], 1);
+      else atomicAdd(&nwk[(int64_t)w[t] * KS + z[t]], 1);
+    }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < cells; i += blockDim.x) {
@@ -743,9 +788,11 @@ ONI_API int oni_gibbs_apply(int32_t* nwk, const int32_t* dcur, int32_t* dother, 
 ONI_API int oni_recount(const int32_t* wsorted, const int32_t* wslot, const uint8_t* tok_z, int64_t T, int32_t* nwk,
                         int KS, int tile, int wmax, hipStream_t s) {
   if (T == 0) return 0;
-  if (tile < 256 || wmax < 1 || (size_t)wmax * KS * 4 > 64 * 1024) return (int)hipErrorInvalidValue;
-  const unsigned grid = (unsigned)((T + tile - 1) / tile);
-  k_recount<<<grid, 256, (size_t)wmax * KS * 4, s>>>(wsorted, wslot, tok_z, T, nwk, KS, tile, wmax);
+  if (KS < 1 || KS > kRecountCells) return (int)hipErrorInvalidValue;
+  (void)tile;
+  (void)wmax;
+  const unsigned grid = (unsigned)((T + kRecountTile - 1) / kRecountTile);
+  k_recount<<<grid, 256, 0, s>>>(wsorted, wslot, tok_z, T, nwk, KS);
   return (int)hipGetLastError();
 }
 

@@ -296,7 +296,7 @@ def delta_recount(wslot, tile_wlo, tile_whi, chg_mask, tok_word, tok_z, tok_zpre
         tok_zprev[sl[ch]] = tok_z[sl[ch]]
         return
     S = 64 // G
-    wmax = max(1, min(16384 // KS, 4096))
+    wmax = max(1, RECOUNT_CELLS // KS)  # small LDS histograms: occupancy, not capacity, bounds these kernels
     _lib.check(_lib.lib().oni_delta_recount(*map(_lib.ptr, (wslot, tile_wlo, tile_whi, chg_mask, tok_word, tok_z,
                                                             tok_zprev)), T, _lib.ptr(dnwk_out), KS,
                                             S.bit_length() - 1, G, RECOUNT_TILE, wmax, _lib.stream()),
@@ -304,6 +304,7 @@ def delta_recount(wslot, tile_wlo, tile_whi, chg_mask, tok_word, tok_z, tok_zpre
 
 
 RECOUNT_TILE = 4096
+RECOUNT_CELLS = 2048  # LDS histogram cells per recount block (8 KB; matches kRecountCells)
 
 
 def recount(wsorted, wslot, tok_z, nwk_out, KS: int) -> None:
@@ -319,7 +320,7 @@ def recount(wsorted, wslot, tok_z, nwk_out, KS: int) -> None:
         z = (tok_z[wslot.long()] if wslot is not None else tok_z[:T]).long()
         nwk_out.view(-1).index_add_(0, wsorted.long() * KS + z, torch.ones_like(z, dtype=torch.int32))
         return
-    wmax = max(1, min(16384 // KS, 4096))
+    wmax = max(1, RECOUNT_CELLS // KS)  # small LDS histograms: occupancy, not capacity, bounds these kernels
     if wslot is None and KS <= 32 and STREAM_RECOUNT:
         # word-sorted topics: contiguous per-thread runs counted in registers (k_recount_reg)
         _lib.check(_lib.lib().oni_recount_stream(_lib.ptr(wsorted), _lib.ptr(tok_z), T, _lib.ptr(nwk_out), KS,
