@@ -37,10 +37,12 @@ class GibbsConfig:
     beta: float = 0.01
     seed: int = 0x0D15EA5E
     use_graph: bool = True
-    # n_wk bookkeeping: "dual" (changed topics mirrored into a word-sorted z copy, streaming
-    # recount; default), "delta" (changed-slot masks + word-sorted delta recount), "recount"
-    # (full gathered recount) | "atomic" (per-token Δ atomics)
-    count_mode: str = "dual"
+    # n_wk bookkeeping: "auto" (default: "recount" while most topics still move, then "delta"),
+    # "dual" (changed topics mirrored into a word-sorted z copy, streaming recount), "delta"
+    # (changed-slot masks + word-sorted delta recount: cost ∝ changed tokens), "recount" (full
+    # gathered recount: constant cost) | "atomic" (per-token Δ atomics)
+    count_mode: str = "auto"
+    auto_switch: int = 15        # "auto": first sweep (1-based) that uses the delta recount
     prefetch_q: bool = True      # K<=32: fetch the next token's q row one step ahead
     # K<=32: doc-topic counts staged in LDS (k_gibbs_lds, fma numerics) instead of VGPRs;
     # ONI_SAMPLER=lds|reg overrides the default
@@ -79,9 +81,11 @@ class GibbsLDA:
         self.dn = [torch.zeros(V * KS + NK_REP * KS, dtype=i32, device=dev) for _ in range(2)]
         self.q = torch.zeros(V, KS, dtype=torch.float32, device=dev)
         self.sweep_ctr = torch.zeros(1, dtype=i32, device=dev)
-        if cfg.count_mode not in ("dual", "delta", "recount", "atomic"):
+        if cfg.count_mode not in ("auto", "dual", "delta", "recount", "atomic"):
             raise ValueError(f"unknown count_mode {cfg.count_mode}")
-        self.mode = {"recount": 0, "atomic": 1, "delta": 2, "dual": 3}[cfg.count_mode]
+        self.auto = cfg.count_mode == "auto"
+        self.mode = {"recount": 0, "atomic": 1, "delta": 2, "dual": 3, "auto": 2}[cfg.count_mode]
+        self._zprev_synced = False
         if self.mode == 3:
             self.z_w = torch.zeros(max(corpus.T, 1), dtype=torch.uint8, device=dev)
         if self.mode == 2:
@@ -97,6 +101,7 @@ class GibbsLDA:
         self.sweeps_done = 0
         self.likelihoods: list[tuple[int, float]] = []
         self._graph = None
+        self._graphs: dict = {}
         self.timings = {"allreduce_s": 0.0, "allreduce_calls": 0}
 
     # ---------------------------------------------------------------------------------------------
@@ -131,10 +136,17 @@ class GibbsLDA:
         self._graph = None
         self._prime()
 
+    def _sweep_mode(self, sweep: int) -> int:
+        """Count mode used by (1-based) sweep ``sweep``."""
+        if self.auto:
+            return 0 if sweep < self.cfg.auto_switch else 2
+        return self.mode
+
     def _sync_aux_z(self) -> None:
         """Bring the auxiliary topic copies (z_prev / word-sorted z) in line with tok_z."""
         if self.mode == 2:
             self.tok_zprev.copy_(self.tok_z)
+            self._zprev_synced = True
         elif self.mode == 3 and self.c.T:
             self.z_w[: self.c.T] = self.tok_z[self.c.wslot.long()]
 
@@ -151,19 +163,23 @@ class GibbsLDA:
     # ---------------------------------------------------------------------------------------------
     def _one_sweep(self) -> None:
         c = self.c
+        mode = self._sweep_mode(self.sweeps_done + 1)
+        if mode == 2 and not self._zprev_synced:
+            self.tok_zprev.copy_(self.tok_z)  # entering delta mode: z_prev := z (eager, outside graphs)
+        self._zprev_synced = mode == 2
         ops.copy_rows(self.ndk[self.a], self.ndk[1 - self.a], c.long_rows, self.KS)
         ops.gibbs_pass(self._state(False), self.G, self.KP, self.K, self.alpha, self.cfg.seed, False,
-                       self.sweep_ctr, c.chunk_len, host_sweep=self.sweeps_done + 1, mode=self.mode,
+                       self.sweep_ctr, c.chunk_len, host_sweep=self.sweeps_done + 1, mode=mode,
                        prefetch_q=self.qpf, chg_mask=getattr(self, "chg_mask", None), wpos=c.wpos,
                        z_w=getattr(self, "z_w", None))
         head = self.dn[self.b][: self.V * self.KS].view(self.V, self.KS)
-        if self.mode == 0:
+        if mode == 0:
             # dn[b] head := this rank's n_wk rebuilt from z (tail keeps Δn_k)
             ops.recount(c.wsorted, c.wslot, self.tok_z, head, self.KS)
-        elif self.mode == 3:
+        elif mode == 3:
             # dn[b] head := this rank's n_wk, streamed from the word-sorted topic copy
             ops.recount(c.wsorted, None, self.z_w, head, self.KS)
-        elif self.mode == 2:
+        elif mode == 2:
             # dn[b] head := Δn_wk of the tokens that changed topic this sweep
             ops.delta_recount(c.wslot, c.tile_wlo, c.tile_whi, self.chg_mask, c.tok_word, self.tok_z, self.tok_zprev,
                               head, self.KS, self.G)
@@ -174,7 +190,7 @@ class GibbsLDA:
             self.timings["allreduce_calls"] += 1
         ops.gibbs_apply(self.nwk, self.dn[self.b], self.dn[1 - self.b], self.nk[self.cn], self.nk[1 - self.cn],
                         self.q, self.V, self.K, self.KS, self.beta, self.vbeta, self.sweep_ctr, bump=True,
-                        absolute=self.mode in (0, 3))
+                        absolute=mode in (0, 3))
         self.a, self.b, self.cn = 1 - self.a, 1 - self.b, 1 - self.cn
         self.sweeps_done += 1
 
@@ -182,39 +198,51 @@ class GibbsLDA:
         return (self.cfg.use_graph and self.device.type == "cuda" and (self.comm is None or self.comm.world == 1)
                 and os.environ.get("ONI_NO_GRAPH", "0") != "1")
 
-    def _capture(self) -> None:
-        """Capture two sweeps (parities return to their start) into one HIP graph."""
-        saved = (self.a, self.b, self.cn, self.sweeps_done)
+    def _capture(self, mode: int):
+        """Capture two sweeps of count mode ``mode`` (parities return to their start) into one HIP graph."""
+        saved = (self.a, self.b, self.cn, self.sweeps_done, self._zprev_synced)
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         g = torch.cuda.CUDAGraph()
-        # snapshot the state the capture's warm-up would disturb: none — capture does not execute.
+        # capture does not execute: the host-side parities are rewound afterwards
         with torch.cuda.stream(s):
             with torch.cuda.graph(g, stream=s):
                 self._one_sweep()
                 self._one_sweep()
         torch.cuda.current_stream(self.device).wait_stream(s)
-        self.a, self.b, self.cn, self.sweeps_done = saved
-        self._graph = g
-        self._graph_parity = (self.a, self.b, self.cn)
+        self.a, self.b, self.cn, self.sweeps_done, self._zprev_synced = saved
+        entry = (g, (self.a, self.b, self.cn))
+        self._graphs[mode] = entry
+        return entry
 
     def sweep(self, n: int = 1) -> None:
-        """Run ``n`` sweeps (graph-replayed in pairs on a single GPU)."""
+        """Run ``n`` sweeps (graph-replayed in same-mode pairs on a single GPU)."""
         fault.maybe_inject(self.sweeps_done, self.comm.rank if self.comm else 0)
+        if self._graph is None:
+            self._graphs = {}
         done = 0
-        if self._graphable() and n >= 2:
-            if self._graph is not None and self._graph_parity != (self.a, self.b, self.cn):
+        while done < n:
+            m1 = self._sweep_mode(self.sweeps_done + 1)
+            m2 = self._sweep_mode(self.sweeps_done + 2)
+            if not (self._graphable() and n - done >= 2 and m1 == m2):
                 self._one_sweep()
                 done += 1
-            if self._graph is None:
-                self._capture()
-            while n - done >= 2:
-                self._graph.replay()
-                self.sweeps_done += 2
-                done += 2
-        while done < n:
-            self._one_sweep()
-            done += 1
+                continue
+            if m1 == 2 and not self._zprev_synced:
+                self.tok_zprev.copy_(self.tok_z)
+                self._zprev_synced = True
+            entry = self._graphs.get(m1)
+            if entry is not None and entry[1] != (self.a, self.b, self.cn):
+                self._one_sweep()  # realign parities with the captured pair
+                done += 1
+                continue
+            if entry is None:
+                entry = self._capture(m1)
+            self._graph = entry[0]
+            entry[0].replay()
+            self.sweeps_done += 2
+            self._zprev_synced = m1 == 2
+            done += 2
 
     # ---------------------------------------------------------------------------------------------
     @property

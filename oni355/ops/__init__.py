@@ -330,7 +330,7 @@ def recount(wsorted, wslot, tok_z, nwk_out, KS: int) -> None:
                                       RECOUNT_TILE, wmax, _lib.stream()), "oni_recount")
 
 
-STREAM_RECOUNT = False  # k_recount (LDS histogram) measured faster: 0.105 vs 0.112 ms
+STREAM_RECOUNT = True  # k_recount_reg (register runs) 0.065 ms vs k_recount (LDS) 0.093 ms, both at 8 KB LDS
 
 
 def gibbs_apply(nwk, dcur, dother, nk_cur, nk_next, q, V, K, KS, beta, vbeta, sweep_ctr, bump=True, absolute=False):

@@ -187,3 +187,22 @@ def test_lds_sampler_oracle_keeps_counts_consistent():
     m.sweep(3)
     T = c.T
     assert int(m.nwk[:, :20].sum()) == T == int(m.ndk_cur[:, :20].sum()) == int(m.nk_cur[:20].sum())
+
+
+def test_auto_count_mode_matches_recount():
+    import torch
+
+    from oni355.models.corpus import build_corpus
+    from oni355.models.gibbs import GibbsConfig, GibbsLDA
+    r = np.random.default_rng(8)
+    lens = r.integers(1, 200, 60)
+    tdoc = torch.from_numpy(np.repeat(np.arange(60), lens))
+    tword = torch.from_numpy(r.integers(0, 40, int(lens.sum())))
+    keys = torch.arange(60, dtype=torch.int32) * 11 + 3
+    c = build_corpus(tdoc, tword, 60, 40, keys, 1, L=64)
+    a = GibbsLDA(c, GibbsConfig(K=20, seed=2, count_mode="auto", auto_switch=3))
+    b = GibbsLDA(c, GibbsConfig(K=20, seed=2, count_mode="recount"))
+    for m in (a, b):
+        m.initialize()
+        m.sweep(6)
+    assert torch.equal(a.tok_z, b.tok_z) and torch.equal(a.nwk, b.nwk) and torch.equal(a.ndk_cur, b.ndk_cur)

@@ -11,3 +11,7 @@ timeout -k 10 600 python bench/gibbs_traj.py --sweeps 60 --modes ${TRAJ_MODES:-r
 echo "traj ok $(date)" >> gpurun_out/progress.log
 timeout -k 10 600 python bench/gibbs_ab.py --rounds 5 --sweeps 20 --modes ${AB_MODES:-dual+qpf,dual+lds,recount+lds} > gpurun_out/gibbs_ab.json 2> gpurun_out/gibbs_ab.err || { echo "ab failed" >> gpurun_out/progress.log; exit 1; }
 echo "ab ok $(date)" >> gpurun_out/progress.log
+if [ -n "$BENCH" ]; then
+  timeout -k 10 400 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed" >> gpurun_out/progress.log; exit 1; }
+  echo "bench ok $(date)" >> gpurun_out/progress.log
+fi
