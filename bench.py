@@ -25,6 +25,11 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+# Reference-equivalent CPU path (C++ variational-EM lda est on this host's 8 cores, same synthetic
+# 12.5M-flow day): flows × EM iterations / s. BASELINE.md "Measured baselines";
+# profiles/r1_cpu_baseline_12.5M.json; reproduce with bench/cpu_baseline.py.
+BASELINE_RECORDS_PER_SEC = 889_887.5
+
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
@@ -134,7 +139,7 @@ def main(argv=None) -> int:
         "ms_per_step": round(ms, 4),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": None,
+        "vs_baseline": round(value / BASELINE_RECORDS_PER_SEC, 1),
         "dtype": "fp32",
         "data": "synthetic netflow (oni355.synth.flow: random-init topic priors, Zipf hosts, planted anomalies)",
         "config": {"model": "oni-suspicious-connects-flow-lda", "topics": a.topics, "global_batch": n_total,
