@@ -62,3 +62,28 @@ def test_dp_matches_single_process(world):
     assert np.array_equal(one[1], many[1])
     assert np.array_equal(one[2], many[2]) and np.array_equal(one[3], many[3])
     assert one[4] == pytest.approx(many[4], rel=1e-9)
+
+
+def test_balanced_owner_evens_out_power_law_docs():
+    import numpy as np
+    import torch
+
+    from oni355.pipeline import common
+
+    class _Comm:
+        world = 8
+
+        def allgather_var(self, t):
+            return [t]
+
+    r = np.random.default_rng(0)
+    keys = torch.from_numpy(r.zipf(1.1, 400_000).astype(np.int64) * 7919 % (2**32))  # top doc ~9 % < 1/8
+    w = torch.ones_like(keys)
+    own = common.balanced_owner(keys, w, _Comm())
+    load = torch.bincount(own, minlength=8).double()
+    hashed = torch.bincount(common.doc_owner(keys, 8), minlength=8).double()
+    assert float(load.max() / load.mean()) < 1.05 < float(hashed.max() / hashed.mean())
+    # same doc -> same owner
+    u, inv = torch.unique(keys, return_inverse=True)
+    first = torch.zeros(u.numel(), dtype=torch.int64).scatter_(0, inv, own)
+    assert torch.equal(first[inv], own)
