@@ -43,6 +43,8 @@ class GibbsConfig:
     # gathered recount: constant cost) | "atomic" (per-token Δ atomics)
     count_mode: str = "auto"
     auto_switch: int = 15        # "auto": first sweep (1-based) that uses the delta recount
+    # debug: verify count invariants after every sweep() call (ONI_CHECK_INVARIANTS=1)
+    check_invariants: bool = field(default_factory=lambda: os.environ.get("ONI_CHECK_INVARIANTS", "0") == "1")
     prefetch_q: bool = True      # K<=32: fetch the next token's q row one step ahead
     # K<=32: doc-topic counts staged in LDS (k_gibbs_lds, fma numerics) instead of VGPRs;
     # ONI_SAMPLER=lds|reg overrides the default
@@ -102,6 +104,7 @@ class GibbsLDA:
         self.likelihoods: list[tuple[int, float]] = []
         self._graph = None
         self._graphs: dict = {}
+        self._watchdog = fault.Watchdog.from_env()
         self.timings = {"allreduce_s": 0.0, "allreduce_calls": 0}
 
     # ---------------------------------------------------------------------------------------------
@@ -220,6 +223,33 @@ class GibbsLDA:
         fault.maybe_inject(self.sweeps_done, self.comm.rank if self.comm else 0)
         if self._graph is None:
             self._graphs = {}
+        if self._watchdog is not None:
+            self._watchdog.kick()
+        self._sweep_n(n)
+        if self._watchdog is not None:
+            self._watchdog.kick()
+        if self.cfg.check_invariants:
+            self.check_invariants()
+
+    def check_invariants(self) -> None:
+        """Debug-mode count invariants: Σn_wk = Σn_k = global tokens, Σn_dk = local
+        tokens, no negative count, n_k = column sums of n_wk. Raises AssertionError."""
+        K = self.K
+        T_loc = torch.tensor([float(self.c.T)], dtype=torch.float64, device=self.device)
+        T_glob = T_loc.clone()
+        if self.comm is not None and self.comm.world > 1:
+            self.comm.allreduce_(T_glob)
+        nwk = self.nwk[:, :K].to(torch.int64)
+        nk = self.nk_cur[:K].to(torch.int64)
+        ndk = self.ndk_cur[: self.c.D, :K].to(torch.int64)
+        tg, tl = int(T_glob.item()), int(T_loc.item())
+        assert int(nwk.min()) >= 0 and int(ndk.min()) >= 0 and int(nk.min()) >= 0, "negative count"
+        assert int(nwk.sum()) == tg, f"sum n_wk {int(nwk.sum())} != tokens {tg}"
+        assert torch.equal(nwk.sum(0), nk), "n_k != column sums of n_wk"
+        assert int(ndk.sum()) == tl, f"sum n_dk {int(ndk.sum())} != local tokens {tl}"
+        assert not bool(self.nwk[:, K:].any()) and not bool(self.ndk_cur[:, K:].any()), "padding topics used"
+
+    def _sweep_n(self, n: int) -> None:
         done = 0
         while done < n:
             m1 = self._sweep_mode(self.sweeps_done + 1)

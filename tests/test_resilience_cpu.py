@@ -85,3 +85,37 @@ def test_resume_on_different_rank_count(tmp_path):
     resumed = run_flow(_day().cols, K=20, sweeps=6, maxresults=50, device="cpu", ckpt=Checkpointer(ck, every=2))
     full = run_flow(_day().cols, K=20, sweeps=6, maxresults=50, device="cpu")
     assert np.array_equal(full.rows, resumed.rows) and np.array_equal(full.scores, resumed.scores)
+
+
+def test_watchdog_fires_and_kick_defers():
+    import time
+
+    from oni355.utils.fault import Watchdog
+    fired = []
+    w = Watchdog(0.2, on_timeout=lambda: fired.append(time.monotonic()))
+    for _ in range(5):
+        time.sleep(0.08)
+        w.kick()
+    assert not fired
+    time.sleep(0.6)
+    assert fired
+    w.close()
+
+
+def test_invariant_checks_run_and_catch_corruption():
+    import numpy as np
+    import pytest
+    import torch
+
+    from oni355.models.corpus import build_corpus
+    from oni355.models.gibbs import GibbsConfig, GibbsLDA
+    r = np.random.default_rng(1)
+    lens = r.integers(1, 100, 30)
+    c = build_corpus(torch.from_numpy(np.repeat(np.arange(30), lens)), torch.from_numpy(r.integers(0, 25, int(lens.sum()))),
+                     30, 25, torch.arange(30, dtype=torch.int32), 1, L=64)
+    m = GibbsLDA(c, GibbsConfig(K=20, seed=1, check_invariants=True))
+    m.initialize()
+    m.sweep(3)
+    m.nwk[0, 0] -= 1
+    with pytest.raises(AssertionError):
+        m.check_invariants()
