@@ -37,13 +37,18 @@ def main(argv=None) -> int:
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--flows-per-gpu", type=int, default=12_500_000)
-    ap.add_argument("--topics", type=int, default=20)
+    ap.add_argument("--topics", type=int, default=None)
+    ap.add_argument("--source", choices=["flow", "dns", "proxy"], default="flow")
+    ap.add_argument("--events-per-gpu", type=int, default=2_000_000, help="dns/proxy events per GPU")
     ap.add_argument("--chunk-len", type=int, default=128)
     ap.add_argument("--maxresults", type=int, default=3000)
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--no-graph", action="store_true")
     a = ap.parse_args(argv)
+    a.topics_set = a.topics is not None
+    if a.topics is None:
+        a.topics = 20
 
     import torch
 
@@ -67,16 +72,42 @@ def main(argv=None) -> int:
             torch.cuda.synchronize(dev)
 
     t_setup = time.perf_counter()
-    # hosts scale with the node-wide day so N=8 is one 100M-flow day split over 8 ranks
-    n_total = a.flows_per_gpu * world
-    day = generate_flows(a.flows_per_gpu, seed=a.seed, rank=rank, n_hosts=max(64, n_total // 25))
-    d = flow.to_device(day.cols, dev)
-    cuts = flow.compute_cuts(d, comm)
-    sw, dw = flow.wordify(d, cuts)
-    doc_keys = torch.cat([common.u32_to_i64(d["sip"]), common.u32_to_i64(d["dip"])])
-    word_keys = torch.cat([common.u32_to_i64(sw), common.u32_to_i64(dw)])
+    from oni355 import ops
+    if a.source == "flow":
+        # hosts scale with the node-wide day so N=8 is one 100M-flow day split over 8 ranks
+        per = a.flows_per_gpu
+        n_total = per * world
+        day = generate_flows(per, seed=a.seed, rank=rank, n_hosts=max(64, n_total // 25))
+        d = flow.to_device(day.cols, dev)
+        cuts = flow.compute_cuts(d, comm)
+        sw, dw = flow.wordify(d, cuts)
+        doc_keys = torch.cat([common.u32_to_i64(d["sip"]), common.u32_to_i64(d["dip"])])
+        word_keys = torch.cat([common.u32_to_i64(sw), common.u32_to_i64(dw)])
+        sides = [(common.u32_to_i64(d["sip"]), common.u32_to_i64(sw)), (common.u32_to_i64(d["dip"]), common.u32_to_i64(dw))]
+        K = a.topics
+    else:
+        per = a.events_per_gpu
+        n_total = per * world
+        if a.source == "dns":
+            from oni355.pipeline import dns as src
+            from oni355.synth.dns import generate_dns
+            day = generate_dns(per, seed=a.seed, rank=rank, n_clients=max(32, n_total // 40))
+            d = src.to_device(day.cols, dev)
+            words, _, _ = src.featurize(d, comm, src.top_set(day.top_domains), "intel")
+            doc_keys = common.u32_to_i64(d["ip_dst"])
+        else:
+            from oni355.pipeline import proxy as src
+            from oni355.synth.proxy import generate_proxy
+            day = generate_proxy(per, seed=a.seed, rank=rank, n_clients=max(32, n_total // 40))
+            from oni355.pipeline.dns import top_set
+            from oni355.synth.dns import top_domain_list
+            words, _ = src.featurize(day.cols, dev, comm, top_set(top_domain_list()))
+            doc_keys = torch.from_numpy(np.asarray(day.cols["clientip"], np.uint32).astype(np.int64)).to(dev)
+        word_keys = words.to(torch.int64)
+        sides = [(doc_keys, word_keys)]
+        K = a.topics if a.topics_set else 50
     vocab = common.global_vocab(word_keys, comm)
-    run = common.build_and_train(doc_keys, word_keys, None, vocab, a.topics, None, 0.01, 0x0D15EA5E, 0,
+    run = common.build_and_train(doc_keys, word_keys, None, vocab, K, None, 0.01, 0x0D15EA5E, 0,
                                  a.chunk_len, comm, train=False)
     model = run.model
     model.initialize()
@@ -99,16 +130,15 @@ def main(argv=None) -> int:
     # ---- post-LDA scoring pass (records scored/s), timed separately --------------------------
     dkeys, theta = common.gather_theta(run, comm)
     phi = model.phi()
-    sdoc = common.lookup(dkeys, common.u32_to_i64(d["sip"]))
-    ddoc = common.lookup(dkeys, common.u32_to_i64(d["dip"]))
-    swid = common.lookup(vocab, common.u32_to_i64(sw))
-    dwid = common.lookup(vocab, common.u32_to_i64(dw))
-    from oni355 import ops
+    lk = [(common.lookup(dkeys, dk_), common.lookup(vocab, wk_)) for dk_, wk_ in sides]
 
     def score_once():
         hist = torch.zeros(2048, dtype=torch.int32, device=dev)
-        sc, _, _ = ops.score(theta, phi, sdoc, swid, ddoc, dwid, tol=1.0, hist=hist)
-        return common.top_n(sc, 1.0, a.maxresults, comm, rank * a.flows_per_gpu, hist=hist)
+        if len(lk) == 2:
+            sc, _, _ = ops.score(theta, phi, lk[0][0], lk[0][1], lk[1][0], lk[1][1], tol=1.0, hist=hist)
+        else:
+            sc, _, _ = ops.score(theta, phi, lk[0][0], lk[0][1], tol=1.0, hist=hist)
+        return common.top_n(sc, 1.0, a.maxresults, comm, rank * per, hist=hist)
 
     score_once()
     sync()
@@ -126,11 +156,14 @@ def main(argv=None) -> int:
     tokens = int(comm.allreduce_scalar(tokens_local, "sum"))
     ms = dt / a.steps * 1e3
     value = n_total * a.steps / dt
-    planted = day.anomaly_rows + rank * a.flows_per_gpu
+    planted = day.anomaly_rows + rank * per
     hits = np.isin(planted, rows.cpu().numpy()[: a.maxresults])
     hit_frac = comm.allreduce_scalar(float(hits.sum()), "sum") / max(comm.allreduce_scalar(float(planted.size), "sum"), 1)
+    metric = "netflow records scored/sec (whole node) + Gibbs iters/sec, 20-topic LDA"
+    if a.source != "flow":
+        metric = f"{a.source} records scored/sec (whole node) + Gibbs iters/sec, {K}-topic LDA"
     out = {
-        "metric": "netflow records scored/sec (whole node) + Gibbs iters/sec, 20-topic LDA",
+        "metric": metric,
         "value": round(value, 1),
         "unit": "records/s",
         "n_gpus": world,
@@ -139,12 +172,15 @@ def main(argv=None) -> int:
         "ms_per_step": round(ms, 4),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": round(value / BASELINE_RECORDS_PER_SEC, 1),
+        "vs_baseline": round(value / BASELINE_RECORDS_PER_SEC, 1) if a.source == "flow" else None,
         "dtype": "fp32",
-        "data": "synthetic netflow (oni355.synth.flow: random-init topic priors, Zipf hosts, planted anomalies)",
-        "config": {"model": "oni-suspicious-connects-flow-lda", "topics": a.topics, "global_batch": n_total,
-                   "flows_per_gpu": a.flows_per_gpu, "seq_len": 2, "parallelism": f"dp{world}",
-                   "baseline_config": "Netflow 100M flows, 20 topics, DP=8 (N=8); weak-scaled 12.5M flows/GPU"},
+        "data": f"synthetic {a.source} (oni355.synth.{a.source}: random-init topic priors, Zipf hosts, planted anomalies)",
+        "config": {"model": f"oni-suspicious-connects-{a.source}-lda", "topics": K, "global_batch": n_total,
+                   "events_per_gpu": per, "seq_len": 2 if a.source == "flow" else 1, "parallelism": f"dp{world}",
+                   "baseline_config": ("Netflow 100M flows, 20 topics, DP=8 (N=8); weak-scaled 12.5M flows/GPU"
+                                       if a.source == "flow" else
+                                       "DNS suspicious-connects (pcap->word pipeline), 50 topics"
+                                       if a.source == "dns" else "proxy suspicious-connects")},
         "gibbs_iters_per_sec": round(a.steps / dt, 3),
         "tokens_per_sec": round(tokens * a.steps / dt, 1),
         "tokens": tokens,

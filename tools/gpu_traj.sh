@@ -15,3 +15,9 @@ if [ -n "$BENCH" ]; then
   timeout -k 10 400 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed" >> gpurun_out/progress.log; exit 1; }
   echo "bench ok $(date)" >> gpurun_out/progress.log
 fi
+if [ -n "$BENCH_SRC" ]; then
+  for src in $BENCH_SRC; do
+    timeout -k 10 500 python bench.py --source $src --steps 30 --warmup 10 > gpurun_out/bench_$src.json 2> gpurun_out/bench_$src.err || { echo "bench $src failed" >> gpurun_out/progress.log; exit 1; }
+    echo "bench $src ok $(date)" >> gpurun_out/progress.log
+  done
+fi
