@@ -39,6 +39,8 @@ def main(argv=None) -> int:
     ap.add_argument("--flows-per-gpu", type=int, default=12_500_000)
     ap.add_argument("--topics", type=int, default=None)
     ap.add_argument("--source", choices=["flow", "dns", "proxy"], default="flow")
+    ap.add_argument("--score-path", choices=["pairs", "gather"], default="pairs",
+                    help="pairs: distinct-pair SDDMM + 4-B gathers; gather: per-event θ/φ row gathers")
     ap.add_argument("--events-per-gpu", type=int, default=2_000_000, help="dns/proxy events per GPU")
     ap.add_argument("--chunk-len", type=int, default=128)
     ap.add_argument("--maxresults", type=int, default=3000)
@@ -130,11 +132,15 @@ def main(argv=None) -> int:
     # ---- post-LDA scoring pass (records scored/s), timed separately --------------------------
     dkeys, theta = common.gather_theta(run, comm)
     phi = model.phi()
+    # distinct (doc, word) pairs + per-endpoint pair index: built once per day (corpus dictionaries)
+    plan = common.score_plan(dkeys, vocab, sides)
     lk = [(common.lookup(dkeys, dk_), common.lookup(vocab, wk_)) for dk_, wk_ in sides]
 
     def score_once():
         hist = torch.zeros(2048, dtype=torch.int32, device=dev)
-        if len(lk) == 2:
+        if a.score_path == "pairs":
+            sc, _, _ = common.plan_score(theta, phi, plan, 1.0, hist=hist)
+        elif len(lk) == 2:
             sc, _, _ = ops.score(theta, phi, lk[0][0], lk[0][1], lk[1][0], lk[1][1], tol=1.0, hist=hist)
         else:
             sc, _, _ = ops.score(theta, phi, lk[0][0], lk[0][1], tol=1.0, hist=hist)
@@ -188,6 +194,8 @@ def main(argv=None) -> int:
         "docs_local": run.corpus.D,
         "score_records_per_sec": round(n_total / score_dt, 1),
         "score_ms": round(score_dt * 1e3, 3),
+        "score_path": a.score_path,
+        "score_pairs": plan.n_pairs,
         "loglik": ll,
         "planted_anomaly_recall_topN": round(hit_frac, 4),
         "setup_s": round(setup_s, 2),

@@ -393,6 +393,38 @@ def score(theta, phi, d1, w1, d2=None, w2=None, tol: float = float("inf"), want_
     return out, o1, o2
 
 
+def pair_score(theta, phi, pdoc, pword) -> torch.Tensor:
+    """Score of every distinct (doc, word) pair: θ[pdoc]·φ[pword] (K15 SDDMM, k_score dot order)."""
+    P = pdoc.numel()
+    if not _is_dev(theta):
+        return torch.from_numpy(spec.dot_rows(theta.numpy()[pdoc.numpy()], phi.numpy()[pword.numpy()]))
+    KS = theta.shape[-1]
+    out = torch.empty(P, dtype=torch.float32, device=theta.device)
+    _lib.check(_lib.lib().oni_pair_score(_lib.ptr(theta), _lib.ptr(phi), KS, _lib.ptr(pdoc), _lib.ptr(pword), P,
+                                         _lib.ptr(out), _lib.stream()), "oni_pair_score")
+    return out
+
+
+def event_min(ps, p1, p2=None, tol: float = float("inf"), want_parts=False, hist=None):
+    """Per-event score from pair scores: ps[p1] or min(ps[p1], ps[p2]); optional order-key histogram."""
+    n = p1.numel()
+    if not _is_dev(ps):
+        s1 = ps[p1.long()]
+        s2 = ps[p2.long()] if p2 is not None else None
+        sc = torch.where(s2 < s1, s2, s1) if s2 is not None else s1.clone()
+        if hist is not None:
+            a = sc.numpy()
+            b = spec.f32_key(a[a < tol]) >> np.uint32(21)
+            hist += torch.from_numpy(np.bincount(b, minlength=2048).astype(np.int32))
+        return sc, (s1 if want_parts else None), (s2 if want_parts else None)
+    out = torch.empty(n, dtype=torch.float32, device=ps.device)
+    o1 = torch.empty_like(out) if want_parts else None
+    o2 = torch.empty_like(out) if (want_parts and p2 is not None) else None
+    _lib.check(_lib.lib().oni_event_min(_lib.ptr(ps), _lib.ptr(p1), _lib.ptr(p2), n, float(tol), _lib.ptr(out),
+                                        _lib.ptr(o1), _lib.ptr(o2), _lib.ptr(hist), _lib.stream()), "oni_event_min")
+    return out, o1, o2
+
+
 def select_below(score_t: torch.Tensor, tol: float, bmax: int, cap: int):
     """Indices + scores of events with score < tol whose top-11 order-key bucket ≤ bmax (unordered)."""
     if not _is_dev(score_t):

@@ -56,6 +56,8 @@ _SIGS = {
     "oni_copy_rows": [vp, vp, vp, i64, C.c_int, vp],
     "oni_score": [vp, vp, C.c_int, vp, vp, vp, vp, i64, f32, vp, vp, vp, vp, vp],
     "oni_select_below": [vp, i64, f32, u32, vp, vp, vp, i64, vp],
+    "oni_pair_score": [vp, vp, C.c_int, vp, vp, i64, vp, vp],
+    "oni_event_min": [vp, vp, vp, i64, f32, vp, vp, vp, vp, vp],
 }
 # optional symbols (added by later kernel files); bound when present
 _OPTIONAL_SIGS: dict[str, list] = {}

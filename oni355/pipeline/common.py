@@ -180,6 +180,38 @@ def lookup(sorted_keys: torch.Tensor, q: torch.Tensor) -> torch.Tensor:
     return idx.to(torch.int32)
 
 
+@dataclass
+class ScorePlan:
+    """Distinct (doc, word) pairs of a set of events + each event endpoint's pair index (K09/K15).
+
+    Built once per day after training (the dictionaries are final); scoring is then one SDDMM
+    over the distinct pairs and a 4-B gather per endpoint (ops.pair_score / ops.event_min)."""
+    pdoc: torch.Tensor
+    pword: torch.Tensor
+    inv: list
+
+    @property
+    def n_pairs(self) -> int:
+        return int(self.pdoc.numel())
+
+
+def score_plan(dkeys: torch.Tensor, vocab: torch.Tensor, sides) -> ScorePlan:
+    """``sides``: [(doc_keys64, word_keys64)] per event endpoint (1 for DNS/proxy, 2 for flows)."""
+    V = int(vocab.numel())
+    ids = [lookup(dkeys, dk).to(torch.int64) * V + lookup(vocab, wk).to(torch.int64) for dk, wk in sides]
+    uniq, inv = torch.unique(torch.cat(ids), return_inverse=True)
+    if uniq.numel() >= 2**31:
+        raise ValueError("too many distinct pairs for int32 indices")
+    invs = [x.to(torch.int32).contiguous() for x in inv.split([t.numel() for t in ids])]
+    return ScorePlan((uniq // V).to(torch.int32).contiguous(), (uniq % V).to(torch.int32).contiguous(), invs)
+
+
+def plan_score(theta: torch.Tensor, phi: torch.Tensor, plan: ScorePlan, tol: float, hist=None, want_parts=False):
+    ps = ops.pair_score(theta, phi, plan.pdoc, plan.pword)
+    return ops.event_min(ps, plan.inv[0], plan.inv[1] if len(plan.inv) > 1 else None, tol=tol,
+                          want_parts=want_parts, hist=hist)
+
+
 def top_n(score: torch.Tensor, tol: float, maxresults: int, comm: Comm | None, row_offset: int = 0,
           hist: torch.Tensor | None = None):
     """Lowest ``maxresults`` scores below ``tol`` (ties by global row id), merged over ranks (X06).
@@ -226,11 +258,12 @@ def run_single_doc_events(doc_keys64: torch.Tensor, word_keys64: torch.Tensor, K
     t.update(run.timings)
     t0 = time.perf_counter()
     dkeys, theta = gather_theta(run, comm)
-    d1 = lookup(dkeys, doc_keys64)
-    w1 = lookup(vocab, word_keys64)
+    plan = score_plan(dkeys, vocab, [(doc_keys64, word_keys64)])
+    sync()
+    t["score_prep_s"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
     hist = torch.zeros(2048, dtype=torch.int32, device=dev)
-    from .. import ops as _ops
-    score, _, _ = _ops.score(theta, run.model.phi(), d1, w1, tol=tol, hist=hist)
+    score, _, _ = plan_score(theta, run.model.phi(), plan, tol, hist=hist)
     rows, scs = top_n(score, tol, maxresults, comm, row_offset, hist=hist)
     sync()
     t["score_s"] = time.perf_counter() - t0

@@ -132,15 +132,13 @@ def run_flow(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxre
     dkeys, theta = common.gather_theta(run, comm)
     phi = run.model.phi()
     n = d["sip"].numel()
-    sdoc = common.lookup(dkeys, common.u32_to_i64(d["sip"]))
-    ddoc = common.lookup(dkeys, common.u32_to_i64(d["dip"]))
-    swid = common.lookup(vocab, common.u32_to_i64(sw))
-    dwid = common.lookup(vocab, common.u32_to_i64(dw))
+    plan = common.score_plan(dkeys, vocab, [(common.u32_to_i64(d["sip"]), common.u32_to_i64(sw)),
+                                            (common.u32_to_i64(d["dip"]), common.u32_to_i64(dw))])
     sync()
     t["score_prep_s"] = time.perf_counter() - t0
     t0 = time.perf_counter()
     hist = torch.zeros(2048, dtype=torch.int32, device=theta.device)
-    score, s1, s2 = ops.score(theta, phi, sdoc, swid, ddoc, dwid, tol=tol, want_parts=True, hist=hist)
+    score, s1, s2 = common.plan_score(theta, phi, plan, tol, hist=hist, want_parts=True)
     rows, scs = common.top_n(score, tol, maxresults, comm, row_offset, hist=hist)
     sync()
     t["score_s"] = time.perf_counter() - t0

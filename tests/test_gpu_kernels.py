@@ -156,3 +156,27 @@ def test_flow_pipeline_gpu_matches_cpu(gpu):
     assert np.array_equal(rc.rows, rg.rows)
     assert np.array_equal(rc.scores, rg.scores)
     assert rc.stats["loglik"] == pytest.approx(rg.stats["loglik"], rel=1e-12)
+
+
+@pytest.mark.parametrize("two", [True, False])
+def test_pair_plan_score_matches_gather(gpu, two):
+    from oni355.pipeline import common
+    r = np.random.default_rng(3)
+    D, V, n, KS = 900, 600, 200_003, 20
+    th = torch.from_numpy((r.random((D, KS)) / KS).astype(np.float32)).to(gpu)
+    ph = torch.from_numpy((r.random((V, KS)) ** 6).astype(np.float32)).to(gpu)
+    dkeys = torch.arange(D, dtype=torch.int64, device=gpu) * 3 + 1
+    vocab = torch.arange(V, dtype=torch.int64, device=gpu) * 5 + 2
+    sides = [(dkeys[torch.from_numpy(r.integers(0, D, n)).to(gpu)], vocab[torch.from_numpy(r.integers(0, V, n)).to(gpu)])
+             for _ in range(2 if two else 1)]
+    plan = common.score_plan(dkeys, vocab, sides)
+    h1 = torch.zeros(2048, dtype=torch.int32, device=gpu)
+    h2 = torch.zeros(2048, dtype=torch.int32, device=gpu)
+    got, g1, g2 = common.plan_score(th, ph, plan, 0.3, hist=h1, want_parts=True)
+    lk = [(common.lookup(dkeys, a), common.lookup(vocab, b)) for a, b in sides]
+    args = [x for p in lk for x in p]
+    want, w1, w2 = ops.score(th, ph, *args, tol=0.3, want_parts=True, hist=h2)
+    assert torch.equal(got, want) and torch.equal(g1, w1)
+    if two:
+        assert torch.equal(g2, w2)
+    assert torch.equal(h1, h2)
