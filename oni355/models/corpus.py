@@ -15,6 +15,7 @@ from dataclasses import dataclass
 import torch
 
 from .. import ops
+from ..utils.obs import traced
 
 PAD = -1  # 0xFFFFFFFF as int32
 
@@ -83,6 +84,7 @@ def _excl_cumsum(x: torch.Tensor) -> torch.Tensor:
     return out
 
 
+@traced("oni:build_corpus")
 def build_corpus(tdoc: torch.Tensor, tword: torch.Tensor, D: int, V: int, doc_keys: torch.Tensor, G: int,
                  L: int = 256, weight: torch.Tensor | None = None) -> Corpus:
     """Build pairs/CSR/SELL from token (doc id, word id[, weight]) arrays (any device)."""

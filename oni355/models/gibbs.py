@@ -23,6 +23,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from ..utils.obs import traced
 from ..utils import fault
 from .corpus import Corpus, canonical_tokens
 
@@ -122,6 +123,7 @@ class GibbsLDA:
                       dnk=d[VK:])
         return st
 
+    @traced("oni:lda.initialize")
     def initialize(self) -> None:
         """Random topic init (Philox stream 0), counts, first q table."""
         for t in (*self.ndk, self.nwk, *self.nk, *self.dn):
@@ -218,6 +220,7 @@ class GibbsLDA:
         self._graphs[mode] = entry
         return entry
 
+    @traced("oni:lda.sweeps")
     def sweep(self, n: int = 1) -> None:
         """Run ``n`` sweeps (graph-replayed in same-mode pairs on a single GPU)."""
         fault.maybe_inject(self.sweeps_done, self.comm.rank if self.comm else 0)
@@ -295,6 +298,7 @@ class GibbsLDA:
         """φ[w,k] = (n_wk+β)/(n_k+Vβ) for the current counts (= the q table), KS-padded."""
         return self.q
 
+    @traced("oni:lda.loglik")
     def log_likelihood(self) -> float:
         """Collapsed joint log p(w, z) (Griffiths & Steyvers 2004), summed over ranks."""
         K, a, b, V = self.K, self.alpha, self.beta, self.V

@@ -16,6 +16,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from ..utils.obs import traced
 from ..models.corpus import Corpus, build_corpus
 from ..models.gibbs import GibbsConfig, GibbsLDA
 from ..parallel.comm import Comm
@@ -32,6 +33,7 @@ def i64_to_u32bits(t: torch.Tensor) -> torch.Tensor:
     return (t & U32MASK).to(torch.int64).to(torch.int32) if t.dtype == torch.int64 else t
 
 
+@traced("oni:vocab")
 def global_vocab(keys64: torch.Tensor, comm: Comm | None) -> torch.Tensor:
     """Sorted unique int64 word keys over all ranks (collective X02)."""
     loc = torch.unique(keys64)
@@ -84,6 +86,7 @@ def balanced_owner(doc_keys64: torch.Tensor, weights: torch.Tensor, comm: Comm) 
     return gown.to(doc_keys64.device)[torch.searchsorted(gkeys.to(doc_keys64.device), doc_keys64)]
 
 
+@traced("oni:route_to_owners")
 def route_to_owners(doc_keys64: torch.Tensor, word_ids: torch.Tensor, weights: torch.Tensor, comm: Comm | None):
     """Send each token to its document's owner rank (alltoallv). Returns local (doc, word, weight)."""
     if comm is None or comm.world == 1:
@@ -105,6 +108,7 @@ class LdaRun:
     timings: dict = field(default_factory=dict)
 
 
+@traced("oni:build_and_train")
 def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor, weights: torch.Tensor | None,
                     vocab: torch.Tensor, K: int, alpha: float | None, beta: float, seed: int, sweeps: int,
                     chunk_len: int, comm: Comm | None, eval_every: int = 0, ckpt=None, log=None,
@@ -158,6 +162,7 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor, weights
     return run
 
 
+@traced("oni:gather_theta")
 def gather_theta(run: LdaRun, comm: Comm | None) -> tuple[torch.Tensor, torch.Tensor]:
     """Global (sorted doc keys, θ rows) on every rank (collective X05; local when world == 1)."""
     th = run.model.theta()
@@ -195,6 +200,7 @@ class ScorePlan:
         return int(self.pdoc.numel())
 
 
+@traced("oni:score_plan")
 def score_plan(dkeys: torch.Tensor, vocab: torch.Tensor, sides) -> ScorePlan:
     """``sides``: [(doc_keys64, word_keys64)] per event endpoint (1 for DNS/proxy, 2 for flows)."""
     V = int(vocab.numel())
@@ -206,12 +212,14 @@ def score_plan(dkeys: torch.Tensor, vocab: torch.Tensor, sides) -> ScorePlan:
     return ScorePlan((uniq // V).to(torch.int32).contiguous(), (uniq % V).to(torch.int32).contiguous(), invs)
 
 
+@traced("oni:score")
 def plan_score(theta: torch.Tensor, phi: torch.Tensor, plan: ScorePlan, tol: float, hist=None, want_parts=False):
     ps = ops.pair_score(theta, phi, plan.pdoc, plan.pword)
     return ops.event_min(ps, plan.inv[0], plan.inv[1] if len(plan.inv) > 1 else None, tol=tol,
                           want_parts=want_parts, hist=hist)
 
 
+@traced("oni:top_n")
 def top_n(score: torch.Tensor, tol: float, maxresults: int, comm: Comm | None, row_offset: int = 0,
           hist: torch.Tensor | None = None):
     """Lowest ``maxresults`` scores below ``tol`` (ties by global row id), merged over ranks (X06).

@@ -17,6 +17,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from ..utils.obs import traced
 from ..ops import strings as sops
 from ..parallel.comm import Comm
 from ..ref import spec
@@ -78,6 +79,7 @@ def time_keys(unix: torch.Tensor) -> torch.Tensor:
     return ops.f32_keys(t.contiguous())
 
 
+@traced("oni:dns.featurize")
 def featurize(d: dict, comm: Comm | None, topset: HashSet | None, user_domain: str):
     rh, top, sub_len, sub_ent, per = sops.domain_features(d["name_off"], d["name_chars"], topset, user_domain)
     keys = {"frame_len": d["frame_len"], "time": time_keys(d["unix_tstamp"]), "sub_len": sub_len,
@@ -95,6 +97,7 @@ def featurize(d: dict, comm: Comm | None, topset: HashSet | None, user_domain: s
     return words, cuts, feats
 
 
+@traced("oni:dns.run")
 def run_dns(cols: dict, K: int = 50, sweeps: int = 200, tol: float = 1.0, maxresults: int = 3000,
             alpha: float | None = None, beta: float = 0.01, seed: int = 0x0D15EA5E, chunk_len: int = 128,
             device="cpu", comm: Comm | None = None, top_domains=None, user_domain: str = "",

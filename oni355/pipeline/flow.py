@@ -19,6 +19,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from ..utils.obs import traced
 from ..parallel.comm import Comm
 from ..ref import spec
 from . import common
@@ -49,6 +50,7 @@ class FlowCuts:
                 "ipkt": [int(x) for x in self.ipkt]}
 
 
+@traced("oni:flow.quantile_cuts")
 def compute_cuts(d: dict, comm: Comm | None) -> FlowCuts:
     tk, bk, pk = ops.flow_keys(d["trhour"], d["trminute"], d["trsec"], d["ibyt"], d["ipkt"])
     n = tk.numel()
@@ -63,6 +65,7 @@ def compute_cuts(d: dict, comm: Comm | None) -> FlowCuts:
     return cuts
 
 
+@traced("oni:flow.wordify")
 def wordify(d: dict, cuts: FlowCuts) -> tuple[torch.Tensor, torch.Tensor]:
     tk, bk, pk = d.get("_keys") or ops.flow_keys(d["trhour"], d["trminute"], d["trsec"], d["ibyt"], d["ipkt"])
     return ops.flow_wordify(d["sport"], d["dport"], tk, bk, pk, cuts.time, cuts.ibyt, cuts.ipkt)
@@ -94,6 +97,7 @@ def feedback_tokens(fb_cols: dict | None, cuts: FlowCuts, device, dupfactor: int
     return docs, words, torch.full_like(words, int(dupfactor))
 
 
+@traced("oni:flow.run")
 def run_flow(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxresults: int = 3000,
              alpha: float | None = None, beta: float = 0.01, seed: int = 0x0D15EA5E, chunk_len: int = 128,
              device="cpu", comm: Comm | None = None, feedback: dict | None = None, dupfactor: int = 1000,

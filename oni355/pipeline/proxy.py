@@ -17,6 +17,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from ..utils.obs import traced
 from ..ops import strings as sops
 from ..parallel.comm import Comm
 from ..ref import spec
@@ -76,6 +77,7 @@ def method_code(s: str) -> int:
     return METHODS.index(s) if s in METHODS else 0
 
 
+@traced("oni:proxy.featurize")
 def featurize(cols: dict, device, comm: Comm | None, topset, allreduce_counts: bool = True):
     dev = torch.device(device)
     n = len(cols["clientip"])
@@ -126,6 +128,7 @@ def featurize(cols: dict, device, comm: Comm | None, topset, allreduce_counts: b
     return words, cuts
 
 
+@traced("oni:proxy.run")
 def run_proxy(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxresults: int = 3000,
               alpha: float | None = None, beta: float = 0.01, seed: int = 0x0D15EA5E, chunk_len: int = 128,
               device="cpu", comm: Comm | None = None, top_domains=None, feedback: dict | None = None,

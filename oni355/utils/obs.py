@@ -102,3 +102,16 @@ def _default(o):
     except ImportError:  # pragma: no cover
         pass
     return str(o)
+
+
+def traced(name: str):
+    """Decorator: run the function inside a roctx range ``name`` (rocprofv3 --marker-trace)."""
+    import functools
+
+    def deco(fn):
+        @functools.wraps(fn)
+        def wrapper(*a, **kw):
+            with range_(name):
+                return fn(*a, **kw)
+        return wrapper
+    return deco
