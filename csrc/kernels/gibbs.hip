@@ -41,6 +41,7 @@ struct OniGibbs {
   uint64_t* chg_mask;          // MODE 2: one u64 per SELL step, bit c*G set if slot c's topic changed
   const int32_t* wpos;         // MODE 3: word-sorted position of every SELL slot
   uint8_t* z_w;                // MODE 3: topic array in word-sorted order (kept in sync for changed tokens)
+  int32_t* chg_count;          // optional: += number of tokens whose topic changed (drives the auto mode)
   int64_t n_slices;
   int32_t K;
   int32_t KS;
@@ -53,6 +54,9 @@ struct OniGibbs {
 namespace {
 
 constexpr int kBlock = 256;
+// Δ buffers are [V·KS | nk_rep·KS | kDnAux]: the aux words ride along in the all-reduce
+// ([0] = number of changed tokens this sweep); k_apply zeroes all of it in the other buffer.
+constexpr int kDnAux = 4;
 constexpr int kWavesPerBlock = kBlock / oni::kWave;
 
 template <int KP>
@@ -70,6 +74,13 @@ __device__ __forceinline__ void load_row_f(const float* __restrict__ p, float (&
     const float4 t = *reinterpret_cast<const float4*>(p + j);
     v[j] = t.x; v[j + 1] = t.y; v[j + 2] = t.z; v[j + 3] = t.w;
   }
+}
+
+// Sum a per-lane count over the wave; lane 0 adds it to *dst (one atomic per wave).
+__device__ __forceinline__ void add_wave_count(int32_t* dst, int v) {
+#pragma unroll
+  for (int m = 1; m < oni::kWave; m <<= 1) v += __shfl_xor(v, m);
+  if ((threadIdx.x & (oni::kWave - 1)) == 0 && v) atomicAdd(dst, v);
 }
 
 // Long documents: all full-length chunks of a doc are adjacent in the chunk order (stable sort by
@@ -148,6 +159,7 @@ __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
 #pragma unroll
   for (int j = 0; j < KP; ++j) qv[j] = 0.f;
 
+  int nchg = 0;
   // software-pipelined token stream: step s+1's word/topic loads are issued before step s's
   // sampling, so their latency hides behind the math and stores of step s
   uint32_t w_nx = len > 0 ? a.tok_word[off + c] : oni::kPadWord;
@@ -220,6 +232,7 @@ __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
 #pragma unroll
       for (int j = 0; j < KP; ++j) n[j] += (kbase + j == zn);
       if (zn != zo && g == 0) {
+        ++nchg;
         a.tok_z[idx] = (uint8_t)zn;
         if constexpr (MODE == 3) a.z_w[a.wpos[idx]] = (uint8_t)zn;
         if (ATOMIC) {
@@ -238,6 +251,7 @@ __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
   }
 
   // ---- epilogue: doc rows + per-topic totals -------------------------------------------------
+  if (!INIT && a.chg_count) add_wave_count(a.chg_count, nchg);
   int32_t d[KP];
 #pragma unroll
   for (int j = 0; j < KP; ++j) d[j] = 0;
@@ -302,7 +316,7 @@ __global__ __launch_bounds__(256) void k_apply(int32_t* __restrict__ nwk, const 
   __syncthreads();
   if (blockIdx.x == 0) {
     for (int k = threadIdx.x; k < KS; k += blockDim.x) nk_next[k] = nkn[k];
-    for (int k = threadIdx.x; k < nk_rep * KS; k += blockDim.x) dother[V * KS + k] = 0;
+    for (int k = threadIdx.x; k < nk_rep * KS + kDnAux; k += blockDim.x) dother[V * KS + k] = 0;
     if (threadIdx.x == 0 && bump) *sweep_ctr += 1u;
   }
   const int64_t nvec = V * KS / 4;
@@ -361,7 +375,7 @@ template <int KP, int MODE, int P>
 __device__ __forceinline__ void lds_step(const OniGibbs& a, int s, int len, int64_t off, int lane, uint32_t key,
                                          uint32_t pos0, uint32_t sweep, float4* __restrict__ row, oni::U4& r,
                                          uint32_t (&wq)[2], int (&zq)[2], int32_t (&pq)[2], const float (&qc)[KP],
-                                         float (&qn)[KP], uint64_t* chg_word) {
+                                         float (&qn)[KP], uint64_t* chg_word, int& nchg) {
   constexpr int KS = KP;
   float* rowf = reinterpret_cast<float*>(row);
   const int64_t idx = off + (int64_t)s * 64 + lane;
@@ -401,6 +415,7 @@ __device__ __forceinline__ void lds_step(const OniGibbs& a, int s, int len, int6
     const int zn = cnt < a.K - 1 ? cnt : a.K - 1;
     rowf[zn] = rowf[zn] + 1.0f;
     changed = zn != zo;
+    nchg += changed;
     if (changed) {
       a.tok_z[idx] = (uint8_t)zn;
       if constexpr (MODE == 3) a.z_w[wp] = (uint8_t)zn;
@@ -449,6 +464,7 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_lds(const OniGibbs a) {
   float qa[KP], qb[KP];
 #pragma unroll
   for (int j = 0; j < KP; ++j) qa[j] = qb[j] = 0.f;
+  int nchg = 0;
   uint32_t wq[2] = {oni::kPadWord, oni::kPadWord};
   int zq[2] = {0, 0};
   int32_t pq[2] = {0, 0};
@@ -461,10 +477,11 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_lds(const OniGibbs a) {
   }
   if (wq[0] != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)wq[0] * KS, qa);
   for (int s = 0; s < len; s += 2) {
-    lds_step<KP, MODE, 0>(a, s, len, off, lane, key, pos0, sweep, row, r, wq, zq, pq, qa, qb, chg_word);
+    lds_step<KP, MODE, 0>(a, s, len, off, lane, key, pos0, sweep, row, r, wq, zq, pq, qa, qb, chg_word, nchg);
     if (s + 1 < len)
-      lds_step<KP, MODE, 1>(a, s + 1, len, off, lane, key, pos0, sweep, row, r, wq, zq, pq, qb, qa, chg_word);
+      lds_step<KP, MODE, 1>(a, s + 1, len, off, lane, key, pos0, sweep, row, r, wq, zq, pq, qb, qa, chg_word, nchg);
   }
+  if (a.chg_count) add_wave_count(a.chg_count, nchg);
   // epilogue: counts back to ints, doc rows, per-topic totals (n0 re-read: keeps it out of VGPRs)
   const float* rowf = reinterpret_cast<const float*>(row);
   int32_t d[KP], n[KP], n0[KP];

@@ -43,7 +43,11 @@ class GibbsConfig:
     # (changed-slot masks + word-sorted delta recount: cost ∝ changed tokens), "recount" (full
     # gathered recount: constant cost) | "atomic" (per-token Δ atomics)
     count_mode: str = "auto"
-    auto_switch: int = 15        # "auto": first sweep (1-based) that uses the delta recount
+    # "auto": switch to the delta recount once the all-reduced fraction of tokens that changed
+    # topic in a sweep falls below auto_threshold (measured on device, read two sweeps late so the
+    # host never stalls the stream); auto_switch > 0 instead fixes the first delta sweep (tests)
+    auto_switch: int = 0
+    auto_threshold: float = 0.08
     # debug: verify count invariants after every sweep() call (ONI_CHECK_INVARIANTS=1)
     check_invariants: bool = field(default_factory=lambda: os.environ.get("ONI_CHECK_INVARIANTS", "0") == "1")
     prefetch_q: bool = True      # K<=32: fetch the next token's q row one step ahead
@@ -81,7 +85,8 @@ class GibbsLDA:
         self.nk = [torch.zeros(KS, dtype=i32, device=dev) for _ in range(2)]
         # Δn_k in NK_REP replicas (block b adds into b % NK_REP): the per-block topic totals
         # would otherwise queue thousands of same-address atomics on KS words
-        self.dn = [torch.zeros(V * KS + NK_REP * KS, dtype=i32, device=dev) for _ in range(2)]
+        self._aux_off = V * KS + NK_REP * KS
+        self.dn = [torch.zeros(self._aux_off + ops.DN_AUX, dtype=i32, device=dev) for _ in range(2)]
         self.q = torch.zeros(V, KS, dtype=torch.float32, device=dev)
         self.sweep_ctr = torch.zeros(1, dtype=i32, device=dev)
         if cfg.count_mode not in ("auto", "dual", "delta", "recount", "atomic"):
@@ -89,6 +94,11 @@ class GibbsLDA:
         self.auto = cfg.count_mode == "auto"
         self.mode = {"recount": 0, "atomic": 1, "delta": 2, "dual": 3, "auto": 2}[cfg.count_mode]
         self._zprev_synced = False
+        self._delta_on = False
+        self._force_mode = None
+        self._chg_q: list = []    # (sweep index, host buffer, event) of pending change-count copies
+        self.T_global = corpus.T
+        self.change_log: list[tuple[int, float]] = []
         if self.mode == 3:
             self.z_w = torch.zeros(max(corpus.T, 1), dtype=torch.uint8, device=dev)
         if self.mode == 2:
@@ -120,7 +130,7 @@ class GibbsLDA:
         else:
             d = self.dn[self.b]
             st.update(ndk_src=self.ndk[self.a], ndk_dst=self.ndk[1 - self.a], dnwk=d[:VK].view(self.V, self.KS),
-                      dnk=d[VK:])
+                      dnk=d[VK:self._aux_off], chg_count=d[self._aux_off:self._aux_off + 1])
         return st
 
     @traced("oni:lda.initialize")
@@ -136,6 +146,9 @@ class GibbsLDA:
         if self.comm is not None and self.comm.world > 1:
             self.comm.allreduce_(self.nwk)
             self.comm.allreduce_(self.nk[0])
+        self.T_global = int(self.nk[0][: self.K].sum())
+        self._delta_on = False
+        self._chg_q = []
         self._sync_aux_z()
         self.sweeps_done = 0
         self._graph = None
@@ -143,9 +156,43 @@ class GibbsLDA:
 
     def _sweep_mode(self, sweep: int) -> int:
         """Count mode used by (1-based) sweep ``sweep``."""
+        if self._force_mode is not None:
+            return self._force_mode
         if self.auto:
-            return 0 if sweep < self.cfg.auto_switch else 2
+            if self.cfg.auto_switch > 0:
+                return 0 if sweep < self.cfg.auto_switch else 2
+            return 2 if self._delta_on else 0
         return self.mode
+
+    def _note_changes(self) -> None:
+        """Queue an async copy of the last completed sweep's (all-reduced) changed-token count."""
+        if not self.auto or self.cfg.auto_switch > 0 or self._delta_on:
+            return
+        src = self.dn[1 - self.b][self._aux_off:self._aux_off + 1]
+        if self.device.type == "cuda":
+            buf = torch.empty(1, dtype=torch.int32, pin_memory=True)
+            buf.copy_(src, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            buf, ev = src.clone(), None
+        self._chg_q.append((self.sweeps_done, buf, ev))
+
+    def _decide_mode(self) -> None:
+        """At even sweep counts, consume counts of sweeps ≤ now-2 (deterministic on every rank)."""
+        if not self._chg_q or self.sweeps_done % 2:
+            return
+        latest = None
+        while self._chg_q and self._chg_q[0][0] <= self.sweeps_done - 2:
+            sw, buf, ev = self._chg_q.pop(0)
+            if ev is not None:
+                ev.synchronize()
+            latest = (sw, int(buf[0]) / max(self.T_global, 1))
+        if latest is not None:
+            self.change_log.append(latest)
+            if latest[1] < self.cfg.auto_threshold:
+                self._delta_on = True
+                self._chg_q.clear()
 
     def _sync_aux_z(self) -> None:
         """Bring the auxiliary topic copies (z_prev / word-sorted z) in line with tok_z."""
@@ -206,6 +253,9 @@ class GibbsLDA:
     def _capture(self, mode: int):
         """Capture two sweeps of count mode ``mode`` (parities return to their start) into one HIP graph."""
         saved = (self.a, self.b, self.cn, self.sweeps_done, self._zprev_synced)
+        self._force_mode = mode
+        if mode == 2:
+            self._zprev_synced = True  # the eager z_prev sync happens before the first replay
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         g = torch.cuda.CUDAGraph()
@@ -216,6 +266,7 @@ class GibbsLDA:
                 self._one_sweep()
         torch.cuda.current_stream(self.device).wait_stream(s)
         self.a, self.b, self.cn, self.sweeps_done, self._zprev_synced = saved
+        self._force_mode = None
         entry = (g, (self.a, self.b, self.cn))
         self._graphs[mode] = entry
         return entry
@@ -255,10 +306,12 @@ class GibbsLDA:
     def _sweep_n(self, n: int) -> None:
         done = 0
         while done < n:
+            self._decide_mode()
             m1 = self._sweep_mode(self.sweeps_done + 1)
             m2 = self._sweep_mode(self.sweeps_done + 2)
             if not (self._graphable() and n - done >= 2 and m1 == m2):
                 self._one_sweep()
+                self._note_changes()
                 done += 1
                 continue
             if m1 == 2 and not self._zprev_synced:
@@ -267,14 +320,18 @@ class GibbsLDA:
             entry = self._graphs.get(m1)
             if entry is not None and entry[1] != (self.a, self.b, self.cn):
                 self._one_sweep()  # realign parities with the captured pair
+                self._note_changes()
                 done += 1
                 continue
             if entry is None:
                 entry = self._capture(m1)
+                if self.auto and self.cfg.auto_switch == 0 and m1 == 0 and 2 not in self._graphs:
+                    self._capture(2)  # capture the delta pair now: no capture stall at the switch
             self._graph = entry[0]
             entry[0].replay()
             self.sweeps_done += 2
             self._zprev_synced = m1 == 2
+            self._note_changes()
             done += 2
 
     # ---------------------------------------------------------------------------------------------
@@ -350,5 +407,8 @@ class GibbsLDA:
         self._sync_aux_z()
         self.a = self.b = self.cn = 0
         self.sweeps_done = sweeps_done
+        self.T_global = int(self.nk[0][: self.K].sum())
+        self._delta_on = False
+        self._chg_q = []
         self._graph = None
         self._prime()

@@ -243,8 +243,10 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
     if nk_rep < 1 or nk_rep * KS != st["dnk"].numel() or nk_rep & (nk_rep - 1):
         raise ValueError("dnk must hold a power-of-two number of [KS] replicas")
     if not _is_dev(st["tok_word"]):
+        chg = st.get("chg_count")
+        z_before = st["tok_z"].clone() if chg is not None else None
         npst = {k: (v.numpy().view(np.uint32) if k in ("tok_word", "chunk_key") else v.numpy())
-                for k, v in st.items()}
+                for k, v in st.items() if v is not None}
         npst["dnk"] = npst["dnk"][:KS]  # replica 0 (the sum over replicas is what counts)
         if not atomic:
             npst["dnwk"] = np.zeros_like(npst["dnwk"])  # discarded: recount rebuilds n_wk
@@ -254,6 +256,8 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
         if mode == 3:
             valid = wpos >= 0
             z_w[wpos[valid].long()] = st["tok_z"][valid]
+        if chg is not None:
+            chg += int((st["tok_z"] != z_before).sum())
         return
     n_slices = st["slice_len"].numel()
     if st["q"].shape[-1] != KS or st["ndk_src"].shape[-1] != KS:
@@ -273,6 +277,8 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
         if wpos is None or z_w is None or wpos.numel() != st["tok_word"].numel():
             raise ValueError("dual mode needs wpos [SELL slots] and z_w [T]")
         a.wpos, a.z_w = _lib.ptr(wpos), _lib.ptr(z_w)
+    if st.get("chg_count") is not None:
+        a.chg_count = _lib.ptr(st["chg_count"])
     a.n_slices, a.K, a.KS, a.alpha, a.seed0, a.seed1 = n_slices, K, KS, float(alpha), s0, s1
     a.nk_rep = nk_rep
     _lib.check(_lib.lib().oni_gibbs_launch(C.byref(a), G, KP, 1 if init else 0, int(mode),
@@ -304,6 +310,7 @@ def delta_recount(wslot, tile_wlo, tile_whi, chg_mask, tok_word, tok_z, tok_zpre
 
 
 RECOUNT_TILE = 4096
+DN_AUX = 4  # auxiliary int32 words at the end of a Δ buffer (matches kDnAux)
 RECOUNT_CELLS = 2048  # LDS histogram cells per recount block (8 KB; matches kRecountCells)
 
 
@@ -336,12 +343,15 @@ STREAM_RECOUNT = True  # k_recount_reg (register runs) 0.065 ms vs k_recount (LD
 def gibbs_apply(nwk, dcur, dother, nk_cur, nk_next, q, V, K, KS, beta, vbeta, sweep_ctr, bump=True, absolute=False):
     """n_wk ← Δ (or absolute), n_k ← n_k + Σ_replicas Δn_k, q refresh; zeroes ``dother``.
 
-    ``dcur``/``dother`` are [V·KS + R·KS]: the Δn_wk table then R replicas of Δn_k."""
-    nk_rep = (dcur.numel() - V * KS) // KS
+    ``dcur``/``dother`` are [V·KS + R·KS + DN_AUX]: the Δn_wk table, R replicas of Δn_k, then
+    DN_AUX auxiliary words ([0] = tokens that changed topic; all-reduced with the rest)."""
+    nk_rep = (dcur.numel() - V * KS - DN_AUX) // KS
+    if nk_rep < 1 or V * KS + nk_rep * KS + DN_AUX != dcur.numel():
+        raise ValueError("Δ buffer must be [V*KS + nk_rep*KS + DN_AUX]")
     if not _is_dev(nwk):
         base = np.zeros_like(nwk.numpy()) if absolute else nwk.numpy()
         n2, nk2, q2 = spec.gibbs_apply(base, dcur[: V * KS].view(V, KS).numpy(),
-                                       dcur[V * KS:].view(-1, KS).sum(0, dtype=torch.int32).numpy(),
+                                       dcur[V * KS: V * KS + nk_rep * KS].view(-1, KS).sum(0, dtype=torch.int32).numpy(),
                                        nk_cur.numpy(), K, beta, vbeta)
         nwk.copy_(torch.from_numpy(n2))
         nk_next.copy_(torch.from_numpy(nk2))

@@ -94,18 +94,22 @@ def test_gibbs_bitwise_vs_oracle(gpu, K, mode):
     assert int(mg.nwk.min()) >= 0 and int(mg.ndk_cur.min()) >= 0
 
 
-@pytest.mark.parametrize("mode", ["auto", "dual", "delta"])
-def test_graph_replay_matches_eager(gpu, mode):
+@pytest.mark.parametrize("mode,switch", [("auto", 4), ("auto", 0), ("dual", 0), ("delta", 0)])
+def test_graph_replay_matches_eager(gpu, mode, switch):
     tdoc, tword, keys = _toy_tokens(500, 300, 5)
     c = build_corpus(tdoc.to(gpu), tword.to(gpu), 500, 300, torch.from_numpy(keys).to(gpu), 1, L=128)
-    a = GibbsLDA(c, GibbsConfig(K=20, seed=9, use_graph=False, count_mode=mode, auto_switch=4))
-    b = GibbsLDA(c, GibbsConfig(K=20, seed=9, use_graph=True, count_mode=mode, auto_switch=4))
+    a = GibbsLDA(c, GibbsConfig(K=20, seed=9, use_graph=False, count_mode=mode, auto_switch=switch,
+                                auto_threshold=0.5))
+    b = GibbsLDA(c, GibbsConfig(K=20, seed=9, use_graph=True, count_mode=mode, auto_switch=switch,
+                                auto_threshold=0.5))
     a.initialize()
     a.sweep(9)
     b.initialize()
     b.sweep(2)
     b.sweep(7)
     assert b._graph is not None
+    if mode == "auto" and switch == 0:
+        assert b._delta_on and a._delta_on
     assert torch.equal(a.tok_z, b.tok_z) and torch.equal(a.nwk, b.nwk) and torch.equal(a.ndk_cur, b.ndk_cur)
 
 

@@ -206,3 +206,22 @@ def test_auto_count_mode_matches_recount():
         m.initialize()
         m.sweep(6)
     assert torch.equal(a.tok_z, b.tok_z) and torch.equal(a.nwk, b.nwk) and torch.equal(a.ndk_cur, b.ndk_cur)
+
+
+def test_adaptive_auto_mode_switches_and_matches_recount():
+    import torch
+
+    from oni355.models.corpus import build_corpus
+    from oni355.models.gibbs import GibbsConfig, GibbsLDA
+    r = np.random.default_rng(9)
+    lens = r.integers(1, 200, 60)
+    tdoc = torch.from_numpy(np.repeat(np.arange(60), lens))
+    tword = torch.from_numpy(r.integers(0, 40, int(lens.sum())))
+    c = build_corpus(tdoc, tword, 60, 40, torch.arange(60, dtype=torch.int32) * 5 + 1, 1, L=64)
+    a = GibbsLDA(c, GibbsConfig(K=20, seed=4, count_mode="auto", auto_threshold=0.99))
+    b = GibbsLDA(c, GibbsConfig(K=20, seed=4, count_mode="recount"))
+    for m in (a, b):
+        m.initialize()
+        m.sweep(8)
+    assert a._delta_on and a.change_log and 0 < a.change_log[0][1] < 1
+    assert torch.equal(a.tok_z, b.tok_z) and torch.equal(a.nwk, b.nwk) and torch.equal(a.nk_cur, b.nk_cur)
