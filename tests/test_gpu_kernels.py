@@ -99,9 +99,9 @@ def test_graph_replay_matches_eager(gpu, mode, switch):
     tdoc, tword, keys = _toy_tokens(500, 300, 5)
     c = build_corpus(tdoc.to(gpu), tword.to(gpu), 500, 300, torch.from_numpy(keys).to(gpu), 1, L=128)
     a = GibbsLDA(c, GibbsConfig(K=20, seed=9, use_graph=False, count_mode=mode, auto_switch=switch,
-                                auto_threshold=0.5))
+                                auto_threshold=0.99))
     b = GibbsLDA(c, GibbsConfig(K=20, seed=9, use_graph=True, count_mode=mode, auto_switch=switch,
-                                auto_threshold=0.5))
+                                auto_threshold=0.99))
     a.initialize()
     a.sweep(9)
     b.initialize()
