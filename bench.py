@@ -42,7 +42,7 @@ def main(argv=None) -> int:
     ap.add_argument("--score-path", choices=["pairs", "gather"], default="pairs",
                     help="pairs: distinct-pair SDDMM + 4-B gathers; gather: per-event θ/φ row gathers")
     ap.add_argument("--events-per-gpu", type=int, default=2_000_000, help="dns/proxy events per GPU")
-    ap.add_argument("--chunk-len", type=int, default=128)
+    ap.add_argument("--chunk-len", type=int, default=0, help="0 = auto (global token count)")
     ap.add_argument("--maxresults", type=int, default=3000)
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--device", default="cuda")

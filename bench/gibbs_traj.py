@@ -20,7 +20,7 @@ def main() -> int:
     ap.add_argument("--topics", type=int, default=20)
     ap.add_argument("--sweeps", type=int, default=60)
     ap.add_argument("--modes", default="recount,dual,recount+lds,dual+lds")
-    ap.add_argument("--chunk-len", type=int, default=128)
+    ap.add_argument("--chunk-len", type=int, default=0, help="0 = auto (global token count)")
     a = ap.parse_args()
     import torch
 

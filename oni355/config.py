@@ -31,7 +31,7 @@ class OniConfig:
     ALPHA: float = -1.0             # <= 0: 50/K
     BETA: float = 0.01
     SEED: int = 0x0D15EA5E
-    CHUNK_LEN: int = 128            # max tokens per sampler chunk (long-document split; 128 measured best)
+    CHUNK_LEN: int = 0              # tokens per sampler chunk; 0 = auto from the global token count (32..128)
     EVAL_EVERY: int = 0             # log-likelihood every N sweeps (0 = only at the end)
     CKPT_EVERY: int = 0             # checkpoint every N sweeps (0 = never)
     # paths

@@ -10,6 +10,8 @@ times. A token's position in that order (plus the document key) is its RNG ident
 """
 from __future__ import annotations
 
+import math
+
 from dataclasses import dataclass
 
 import torch
@@ -82,6 +84,17 @@ def _excl_cumsum(x: torch.Tensor) -> torch.Tensor:
     if x.numel():
         torch.cumsum(x.to(torch.int64), 0, out=out[1:])
     return out
+
+
+def auto_chunk_len(T_global: int, G: int, lo: int = 32, hi: int = 128) -> int:
+    """Chunk length from the GLOBAL token count (so every GPU count picks the same L and the
+    chain stays world-size invariant): aim at ~4096 slices of S = 64/G chunks, power of two in
+    [lo, hi]. Measured on MI355X: 25M flow tokens → 128 (best of 32..256); 2M DNS tokens at
+    K = 50 → 32 (the wave count, not per-token work, bounds small corpora)."""
+    S = 64 // G
+    want = max(T_global, 1) / (S * 4096.0)
+    L = 1 << int(round(math.log2(max(want, 1.0))))
+    return int(min(max(L, lo), hi))
 
 
 @traced("oni:build_corpus")

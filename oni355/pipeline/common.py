@@ -17,7 +17,7 @@ import torch
 
 from .. import ops
 from ..utils.obs import traced
-from ..models.corpus import Corpus, build_corpus
+from ..models.corpus import Corpus, auto_chunk_len, build_corpus
 from ..models.gibbs import GibbsConfig, GibbsLDA
 from ..parallel.comm import Comm
 
@@ -122,6 +122,11 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor, weights
     dk, wi, wt = route_to_owners(doc_keys64, word_ids, weights, comm)
     udoc, inv = torch.unique(dk, return_inverse=True)
     G, _ = ops.choose_tiling(K)
+    if chunk_len <= 0:
+        T_glob = float(wt.sum()) if wt.numel() else 0.0
+        if comm is not None and comm.world > 1:
+            T_glob = comm.allreduce_scalar(T_glob, "sum")
+        chunk_len = auto_chunk_len(int(T_glob), G)
     use_w = bool((wt != 1).any()) if wt.numel() else False
     corpus = build_corpus(inv, wi, int(udoc.numel()), int(vocab.numel()), i64_to_u32bits(udoc), G, chunk_len,
                           weight=wt if use_w else None)

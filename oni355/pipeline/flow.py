@@ -99,7 +99,7 @@ def feedback_tokens(fb_cols: dict | None, cuts: FlowCuts, device, dupfactor: int
 
 @traced("oni:flow.run")
 def run_flow(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxresults: int = 3000,
-             alpha: float | None = None, beta: float = 0.01, seed: int = 0x0D15EA5E, chunk_len: int = 128,
+             alpha: float | None = None, beta: float = 0.01, seed: int = 0x0D15EA5E, chunk_len: int = 0,
              device="cpu", comm: Comm | None = None, feedback: dict | None = None, dupfactor: int = 1000,
              row_offset: int = 0, eval_every: int = 0, ckpt=None, log=None) -> FlowResult:
     """Full suspicious-connects for one (rank-local shard of a) day of flows."""

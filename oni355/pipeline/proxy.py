@@ -130,7 +130,7 @@ def featurize(cols: dict, device, comm: Comm | None, topset, allreduce_counts: b
 
 @traced("oni:proxy.run")
 def run_proxy(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxresults: int = 3000,
-              alpha: float | None = None, beta: float = 0.01, seed: int = 0x0D15EA5E, chunk_len: int = 128,
+              alpha: float | None = None, beta: float = 0.01, seed: int = 0x0D15EA5E, chunk_len: int = 0,
               device="cpu", comm: Comm | None = None, top_domains=None, feedback: dict | None = None,
               dupfactor: int = 1000, row_offset: int = 0, eval_every: int = 0, ckpt=None,
               log=None) -> common.SingleResult:
