@@ -22,7 +22,7 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--sweeps", type=int, default=20)
     ap.add_argument("--burn", type=int, default=30)
-    ap.add_argument("--modes", default="dual+qpf,delta+qpf,recount+qpf")
+    ap.add_argument("--modes", default="delta,delta+qpf,recount,dual", help="count_mode[+sampler]")
     ap.add_argument("--chunk-len", type=int, default=128)
     ap.add_argument("--chunk-lens", default="", help="extra A/B: comma list of L values (dual+qpf)")
     ap.add_argument("--lds", action="store_true", help="chunk-length A/B with the LDS-count sampler")
@@ -48,8 +48,8 @@ def main() -> int:
     c = run.corpus
     print(json.dumps({"corpus": c.stats()}), flush=True)
     modes = a.modes.split(",")
-    models = {m: GibbsLDA(c, GibbsConfig(K=a.topics, count_mode=m.split("+")[0], prefetch_q="qpf" in m,
-                                         lds_counts="lds" in m))
+    models = {m: GibbsLDA(c, GibbsConfig(K=a.topics, count_mode=m.split("+")[0],
+                                         sampler=m.split("+")[1] if "+" in m else "pp"))
               for m in modes}
     for m in models.values():
         m.initialize()
@@ -69,14 +69,15 @@ def main() -> int:
             m.sweep(a.sweeps)
             torch.cuda.synchronize()
             res[name].append((time.perf_counter() - t0) / a.sweeps * 1e3)
-    out = {"changed_frac": changed, "T": c.T}
+    out = {"changed_frac": changed, "T": c.T, "modes_at_stage_timing": {k: v._sweep_mode(v.sweeps_done + 1) for k, v in models.items()}}
     for name, v in res.items():
         out[name] = {"median_ms": float(np.median(v)), "min_ms": float(np.min(v))}
     # per-stage timing (eager, events) for each mode
     for name, m in models.items():
         st = {}
+        md = m._sweep_mode(m.sweeps_done + 1)
         for stage in range(4):
-            if stage == 3 and m.mode != 3:
+            if stage == 3 and md != 3:
                 continue
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
             ts = []
@@ -85,13 +86,13 @@ def main() -> int:
                 head = m.dn[m.b][: m.V * m.KS].view(m.V, m.KS)
                 if stage == 0:
                     ops.gibbs_pass(m._state(False), m.G, m.KP, m.K, m.alpha, m.cfg.seed, False, m.sweep_ctr,
-                                   c.chunk_len, mode=m.mode, prefetch_q=m.qpf,
+                                   c.chunk_len, mode=md, prefetch_q=m.qpf,
                                    chg_mask=getattr(m, "chg_mask", None), wpos=c.wpos, z_w=getattr(m, "z_w", None))
-                elif stage == 1 and m.mode == 0:
+                elif stage == 1 and md == 0:
                     ops.recount(c.wsorted, c.wslot, m.tok_z, head, m.KS)
-                elif stage == 1 and m.mode == 3:
+                elif stage == 1 and md == 3:
                     ops.recount(c.wsorted, None, m.z_w, head, m.KS)
-                elif stage == 1 and m.mode == 2:
+                elif stage == 1 and md == 2:
                     ops.delta_recount(c.wslot, c.tile_wlo, c.tile_whi, m.chg_mask, c.tok_word, m.tok_z, m.tok_zprev,
                                       head, m.KS, m.G)
                 elif stage == 3:
@@ -100,7 +101,7 @@ def main() -> int:
                     ops.STREAM_RECOUNT = not ops.STREAM_RECOUNT
                 elif stage == 2:
                     ops.gibbs_apply(m.nwk, m.dn[m.b], m.dn[1 - m.b], m.nk[m.cn], m.nk[1 - m.cn], m.q, m.V, m.K, m.KS,
-                                    m.beta, m.vbeta, m.sweep_ctr, bump=False, absolute=m.mode in (0, 3))
+                                    m.beta, m.vbeta, m.sweep_ctr, bump=False, absolute=md in (0, 3))
                 ev[1].record()
                 torch.cuda.synchronize()
                 ts.append(ev[0].elapsed_time(ev[1]))
@@ -112,7 +113,7 @@ def main() -> int:
         del models
         torch.cuda.empty_cache()
         rl = common.build_and_train(dk, wk, None, vocab, a.topics, None, 0.01, 0x0D15EA5E, 0, L, None, train=False)
-        m = GibbsLDA(rl.corpus, GibbsConfig(K=a.topics, count_mode="dual", prefetch_q=True, lds_counts=a.lds))
+        m = GibbsLDA(rl.corpus, GibbsConfig(K=a.topics, count_mode="auto", sampler="lds" if a.lds else "pp"))
         m.initialize()
         m.sweep(a.burn)
         ts = []

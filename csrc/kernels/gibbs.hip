@@ -296,6 +296,168 @@ __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
   }
 }
 
+// ---- ping-pong register sampler (the default sweep kernel) ------------------------------------
+// Same numerics as k_gibbs (mul + add weight chain, bitwise identical), restructured for issue
+// rate: the loop is unrolled by two so the q row of the next token always lands in the other half
+// of a register ping-pong (no per-token 20-wide row copy on a word change, which k_gibbs pays as
+// v_cndmask because the change is lane-divergent), and token words/topics (plus MODE-3 word-sorted
+// slots) stream two steps ahead so their HBM latency hides behind two steps of math.
+template <int G, int KP, int MODE, int P>
+__device__ __forceinline__ void pp_step(const OniGibbs& a, int s, int len, int64_t off, int c, int g, int lane,
+                                        uint32_t key, uint32_t pos0, uint32_t sweep, int32_t (&n)[KP], oni::U4& r,
+                                        uint32_t (&wq)[2], int (&zq)[2], int32_t (&pq)[2], const float (&qc)[KP],
+                                        float (&qn)[KP], int& nchg) {
+  constexpr int S = oni::kWave / G;
+  constexpr int KS = G * KP;
+  const int kbase = g * KP;
+  const int64_t idx = off + (int64_t)s * S + c;
+  const uint32_t w = wq[P];
+  const int zo = zq[P];
+  const int32_t wp = pq[P];
+  if (s + 2 < len) {
+    wq[P] = a.tok_word[idx + 2 * S];
+    zq[P] = a.tok_z[idx + 2 * S];
+    if constexpr (MODE == 3) pq[P] = a.wpos[idx + 2 * S];
+  }
+  if (s + 1 < len && wq[1 - P] != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)wq[1 - P] * KS + kbase, qn);
+  if (w == oni::kPadWord) return;  // uniform across the G lanes of a unit
+  const uint32_t pos = pos0 + (uint32_t)s;
+  if (s == 0 || (pos & 3u) == 0u) r = oni::philox10(oni::U4{pos >> 2, key, sweep, 1u}, a.seed0, a.seed1);
+  const uint32_t rr = oni::pick4(r, pos & 3u);
+#pragma unroll
+  for (int j = 0; j < KP; ++j) n[j] -= (kbase + j == zo);
+  float loc[KP];
+  float run = 0.f;
+#pragma unroll
+  for (int j = 0; j < KP; ++j) {
+    run = run + ((float)n[j] + a.alpha) * qc[j];
+    loc[j] = run;
+  }
+  float excl = 0.f, total = run;
+  if constexpr (G > 1) {
+    float incl = run;
+#pragma unroll
+    for (int d = 1; d < G; d <<= 1) {
+      const float y = __shfl_up(incl, d, G);
+      if (g >= d) incl = incl + y;
+    }
+    excl = __shfl_up(incl, 1, G);
+    if (g == 0) excl = 0.f;
+    total = __shfl(incl, G - 1, G);
+  }
+  const float thr = oni::u01(rr) * total;
+  int cnt = 0;
+#pragma unroll
+  for (int j = 0; j < KP; ++j) cnt += ((G > 1 ? excl + loc[j] : loc[j]) <= thr);
+  if constexpr (G > 1) {
+#pragma unroll
+    for (int d = 1; d < G; d <<= 1) cnt += __shfl_xor(cnt, d, G);
+  }
+  const int zn = cnt < a.K - 1 ? cnt : a.K - 1;
+#pragma unroll
+  for (int j = 0; j < KP; ++j) n[j] += (kbase + j == zn);
+  const bool changed = zn != zo && g == 0;
+  if (changed) {
+    ++nchg;
+    a.tok_z[idx] = (uint8_t)zn;
+    if constexpr (MODE == 3) a.z_w[wp] = (uint8_t)zn;
+    if constexpr (MODE == 1) {
+      atomicAdd(&a.dnwk[(int64_t)w * KS + zo], -1);
+      atomicAdd(&a.dnwk[(int64_t)w * KS + zn], 1);
+    }
+  }
+  if constexpr (MODE == 2) {
+    // lane 0 (c = 0) owns the slice's longest chunk, so it is active at every step
+    const uint64_t m = __ballot(changed);
+    if (lane == 0) a.chg_mask[(off + (int64_t)s * S) / S] = m;
+  }
+}
+
+template <int G, int KP, int MODE>
+__global__ __launch_bounds__(kBlock) void k_gibbs_pp(const OniGibbs a) {
+  constexpr int S = oni::kWave / G;
+  constexpr int KS = G * KP;
+  __shared__ int32_t red[kWavesPerBlock][KS];
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int c = lane / G;
+  const int g = lane % G;
+  const int64_t slice = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  const bool valid = slice < a.n_slices;
+  const int64_t chunk = slice * S + c;
+  const int doc = valid ? a.chunk_doc[chunk] : -1;
+  const bool live = doc >= 0;
+  const int kbase = g * KP;
+  int32_t n[KP];
+#pragma unroll
+  for (int j = 0; j < KP; ++j) n[j] = 0;
+  if (live) load_row_i<KP>(a.ndk_src + (int64_t)doc * KS + kbase, n);
+  const int len = valid ? a.slice_len[slice] : 0;
+  const int64_t off = valid ? a.slice_off[slice] : 0;
+  const uint32_t key = live ? a.chunk_key[chunk] : 0u;
+  const uint32_t pos0 = live ? (uint32_t)a.chunk_pos0[chunk] : 0u;
+  const uint32_t sweep = *a.sweep_ctr;
+  oni::U4 r{0, 0, 0, 0};
+  int nchg = 0;
+  float qa[KP], qb[KP];
+#pragma unroll
+  for (int j = 0; j < KP; ++j) qa[j] = qb[j] = 0.f;
+  uint32_t wq[2] = {oni::kPadWord, oni::kPadWord};
+  int zq[2] = {0, 0};
+  int32_t pq[2] = {0, 0};
+  for (int t = 0; t < 2; ++t) {
+    if (t < len) {
+      wq[t] = a.tok_word[off + t * S + c];
+      zq[t] = a.tok_z[off + t * S + c];
+      if constexpr (MODE == 3) pq[t] = a.wpos[off + t * S + c];
+    }
+  }
+  if (wq[0] != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)wq[0] * KS + kbase, qa);
+  for (int s = 0; s < len; s += 2) {
+    pp_step<G, KP, MODE, 0>(a, s, len, off, c, g, lane, key, pos0, sweep, n, r, wq, zq, pq, qa, qb, nchg);
+    if (s + 1 < len)
+      pp_step<G, KP, MODE, 1>(a, s + 1, len, off, c, g, lane, key, pos0, sweep, n, r, wq, zq, pq, qb, qa, nchg);
+  }
+  if (a.chg_count) add_wave_count(a.chg_count, nchg);
+  // ---- epilogue (as k_gibbs): doc rows + per-topic totals --------------------------------------
+  int32_t d[KP];
+#pragma unroll
+  for (int j = 0; j < KP; ++j) d[j] = 0;
+  if (live) {
+    int32_t* dst = a.ndk_dst + (int64_t)doc * KS + kbase;
+    int32_t n0[KP];
+    load_row_i<KP>(a.ndk_src + (int64_t)doc * KS + kbase, n0);
+#pragma unroll
+    for (int j = 0; j < KP; ++j) d[j] = n[j] - n0[j];
+    if (!a.chunk_multi[chunk]) {
+#pragma unroll
+      for (int j = 0; j < KP; j += 4) *reinterpret_cast<int4*>(dst + j) = make_int4(n[j], n[j + 1], n[j + 2], n[j + 3]);
+    }
+  }
+  {
+    const bool multi = live && a.chunk_multi[chunk];
+    if (__ballot(multi)) flush_multi_rows<G, KP>(a.ndk_dst, KS, doc, multi, kbase, d);
+  }
+#pragma unroll
+  for (int j = 0; j < KP; ++j) {
+    int v = d[j];
+#pragma unroll
+    for (int m = G; m < oni::kWave; m <<= 1) v += __shfl_xor(v, m);
+    d[j] = v;
+  }
+  if (c == 0) {
+#pragma unroll
+    for (int j = 0; j < KP; ++j) red[wave][kbase + j] = d[j];
+  }
+  __syncthreads();
+  if (threadIdx.x < KS) {
+    int v = 0;
+#pragma unroll
+    for (int w = 0; w < kWavesPerBlock; ++w) v += red[w][threadIdx.x];
+    if (v) atomicAdd(&a.dnk[(int)(blockIdx.x & (unsigned)(a.nk_rep - 1)) * KS + threadIdx.x], v);
+  }
+}
+
 // Delta apply + q refresh: n_wk += Δ; n_k' = n_k + Δn_k; q = (n_wk+β)/(n_k'+Vβ); zero the other
 // delta buffer for the next sweep; bump the device sweep counter. nk/dnwk are ping-ponged by the
 // host so no block ever reads what another block of this launch writes.
@@ -522,35 +684,43 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_lds(const OniGibbs a) {
 
 template <int G, int KP>
 int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s) {
-  if (a.KS != G * KP) return (int)hipErrorInvalidValue;
+  // qpf (sampler variant): 1 = k_gibbs_pp (ping-pong register sampler, default), 0 = k_gibbs with
+  // a q-row load on each word change, 4 = k_gibbs with one-step q prefetch + row copy (G = 1),
+  // 2 = k_gibbs_lds (LDS-staged counts, fma numerics, G = 1)
+  if (a.KS != G * KP || mode < 0 || mode > 3) return (int)hipErrorInvalidValue;
   const unsigned grid = (unsigned)((a.n_slices + kWavesPerBlock - 1) / kWavesPerBlock);
   if (grid == 0) return 0;
-  constexpr bool Q = G == 1;  // the q-row prefetch variant exists for one-lane units only
+  if (init) {
+    k_gibbs<G, KP, true, 1, false><<<grid, kBlock, 0, s>>>(a);  // init always builds n_wk by atomics
+    return (int)hipGetLastError();
+  }
   if constexpr (G == 1) {
-    // lds-staged doc counts: selected by the host with qpf == 2 (counts proven < 2^22)
-    if (!init && qpf == 2) {
+    if (qpf == 2) {
       if (mode == 0) k_gibbs_lds<KP, 0><<<grid, kBlock, 0, s>>>(a);
       else if (mode == 1) k_gibbs_lds<KP, 1><<<grid, kBlock, 0, s>>>(a);
       else if (mode == 2) k_gibbs_lds<KP, 2><<<grid, kBlock, 0, s>>>(a);
       else k_gibbs_lds<KP, 3><<<grid, kBlock, 0, s>>>(a);
       return (int)hipGetLastError();
     }
+    if (qpf == 4) {
+      if (mode == 0) k_gibbs<1, KP, false, 0, true><<<grid, kBlock, 0, s>>>(a);
+      else if (mode == 1) k_gibbs<1, KP, false, 1, true><<<grid, kBlock, 0, s>>>(a);
+      else if (mode == 2) k_gibbs<1, KP, false, 2, true><<<grid, kBlock, 0, s>>>(a);
+      else k_gibbs<1, KP, false, 3, true><<<grid, kBlock, 0, s>>>(a);
+      return (int)hipGetLastError();
+    }
   }
-  if (init) {
-    k_gibbs<G, KP, true, 1, false><<<grid, kBlock, 0, s>>>(a);  // init always builds n_wk by atomics
-  } else if (mode == 1) {
-    k_gibbs<G, KP, false, 1, false><<<grid, kBlock, 0, s>>>(a);
-  } else if (mode == 2) {
-    if (qpf && Q) k_gibbs<G, KP, false, 2, Q><<<grid, kBlock, 0, s>>>(a);
-    else k_gibbs<G, KP, false, 2, false><<<grid, kBlock, 0, s>>>(a);
-  } else if (mode == 3) {
-    if (qpf && Q) k_gibbs<G, KP, false, 3, Q><<<grid, kBlock, 0, s>>>(a);
-    else k_gibbs<G, KP, false, 3, false><<<grid, kBlock, 0, s>>>(a);
-  } else if (qpf && Q) {
-    k_gibbs<G, KP, false, 0, Q><<<grid, kBlock, 0, s>>>(a);
-  } else {
-    k_gibbs<G, KP, false, 0, false><<<grid, kBlock, 0, s>>>(a);
+  if (qpf == 1) {
+    if (mode == 0) k_gibbs_pp<G, KP, 0><<<grid, kBlock, 0, s>>>(a);
+    else if (mode == 1) k_gibbs_pp<G, KP, 1><<<grid, kBlock, 0, s>>>(a);
+    else if (mode == 2) k_gibbs_pp<G, KP, 2><<<grid, kBlock, 0, s>>>(a);
+    else k_gibbs_pp<G, KP, 3><<<grid, kBlock, 0, s>>>(a);
+    return (int)hipGetLastError();
   }
+  if (mode == 0) k_gibbs<G, KP, false, 0, false><<<grid, kBlock, 0, s>>>(a);
+  else if (mode == 1) k_gibbs<G, KP, false, 1, false><<<grid, kBlock, 0, s>>>(a);
+  else if (mode == 2) k_gibbs<G, KP, false, 2, false><<<grid, kBlock, 0, s>>>(a);
+  else k_gibbs<G, KP, false, 3, false><<<grid, kBlock, 0, s>>>(a);
   return (int)hipGetLastError();
 }
 

@@ -29,6 +29,7 @@ from .corpus import Corpus, canonical_tokens
 
 
 NK_REP = 32
+SAMPLERS = {"pp": 1, "plain": 0, "lds": 2, "qpf": 4}  # -> oni_gibbs_launch qpf argument
 
 
 @dataclass
@@ -50,10 +51,10 @@ class GibbsConfig:
     auto_threshold: float = 0.08
     # debug: verify count invariants after every sweep() call (ONI_CHECK_INVARIANTS=1)
     check_invariants: bool = field(default_factory=lambda: os.environ.get("ONI_CHECK_INVARIANTS", "0") == "1")
-    prefetch_q: bool = True      # K<=32: fetch the next token's q row one step ahead
-    # K<=32: doc-topic counts staged in LDS (k_gibbs_lds, fma numerics) instead of VGPRs;
-    # ONI_SAMPLER=lds|reg overrides the default
-    lds_counts: bool = field(default_factory=lambda: os.environ.get("ONI_SAMPLER", "reg") == "lds")
+    # sweep kernel: "pp" ping-pong register sampler (default), "qpf" one-step q prefetch with a row
+    # copy, "plain" q-row load on each word change, "lds" LDS-staged doc counts (K ≤ 32, fma
+    # numerics); ONI_SAMPLER overrides the default
+    sampler: str = field(default_factory=lambda: os.environ.get("ONI_SAMPLER", "pp"))
 
     def resolved_alpha(self) -> float:
         return float(self.alpha) if self.alpha is not None else 50.0 / self.K
@@ -105,9 +106,13 @@ class GibbsLDA:
             self.tok_zprev = torch.zeros_like(self.tok_z)
             self.chg_mask = torch.zeros(max(corpus.sell_slots // corpus.S, 1), dtype=torch.int64, device=dev)
         # the LDS sampler keeps counts as f32 integers: exact below 2^24 tokens per document
-        self.qpf = 1 if cfg.prefetch_q else 0
-        if cfg.lds_counts and self.G == 1 and corpus.max_doc_len() < (1 << 24):
-            self.qpf = 2
+        if cfg.sampler not in SAMPLERS:
+            raise ValueError(f"unknown sampler {cfg.sampler}")
+        self.qpf = SAMPLERS[cfg.sampler]
+        if self.qpf in (2, 4) and self.G != 1:
+            self.qpf = 1  # lds / qpf variants exist for one-lane units (K ≤ 32) only
+        if self.qpf == 2 and corpus.max_doc_len() >= (1 << 24):
+            self.qpf = 1  # LDS rows hold counts as f32: exact below 2^24
         self.a = 0  # ndk parity
         self.b = 0  # delta-buffer parity
         self.cn = 0  # nk parity

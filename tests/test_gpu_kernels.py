@@ -60,7 +60,8 @@ def _toy_tokens(n_docs, V, seed, heavy=True):
     return torch.from_numpy(tdoc), torch.from_numpy(tword), keys
 
 
-@pytest.mark.parametrize("K,mode", [(20, "dual"), (20, "dual+noqpf"), (20, "delta"), (20, "recount"), (20, "atomic"),
+@pytest.mark.parametrize("K,mode", [(20, "dual"), (20, "dual+plain"), (20, "dual+qpf"), (20, "delta+qpf"),
+                                    (20, "delta"), (20, "recount"), (20, "atomic"), (50, "recount+plain"),
                                     (20, "dual+lds"), (20, "delta+lds"), (20, "atomic+lds"), (7, "dual+lds"),
                                     (32, "dual+lds"), (7, "dual"), (50, "dual"), (50, "delta"), (100, "atomic"),
                                     (100, "dual")])
@@ -71,10 +72,11 @@ def test_gibbs_bitwise_vs_oracle(gpu, K, mode):
     cg = build_corpus(tdoc.to(gpu), tword.to(gpu), 300, 400, torch.from_numpy(keys).to(gpu), G, L=64)
     assert torch.equal(cc.tok_word, cg.tok_word.cpu())
     assert torch.equal(cc.chunk_doc, cg.chunk_doc.cpu())
-    mc = GibbsLDA(cc, GibbsConfig(K=K, seed=1234, use_graph=False, count_mode="atomic", lds_counts="lds" in mode))
-    mg = GibbsLDA(cg, GibbsConfig(K=K, seed=1234, use_graph=False, count_mode=mode.split("+")[0],
-                                  prefetch_q="noqpf" not in mode, lds_counts="lds" in mode))
-    assert (mg.qpf == 2) == ("lds" in mode)
+    sampler = mode.split("+")[1] if "+" in mode else "pp"
+    mc = GibbsLDA(cc, GibbsConfig(K=K, seed=1234, use_graph=False, count_mode="atomic",
+                                  sampler="lds" if sampler == "lds" else "pp"))
+    mg = GibbsLDA(cg, GibbsConfig(K=K, seed=1234, use_graph=False, count_mode=mode.split("+")[0], sampler=sampler))
+    assert (mg.qpf == 2) == (sampler == "lds")
     mc.initialize()
     mg.initialize()
     assert torch.equal(mc.tok_z, mg.tok_z.cpu())
