@@ -374,7 +374,7 @@ __device__ __forceinline__ void pp_step(const OniGibbs& a, int s, int len, int64
 }
 
 template <int G, int KP, int MODE>
-__global__ __launch_bounds__(kBlock) void k_gibbs_pp(const OniGibbs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_gibbs_pp(const OniGibbs a) {
   constexpr int S = oni::kWave / G;
   constexpr int KS = G * KP;
   __shared__ int32_t red[kWavesPerBlock][KS];
