@@ -49,7 +49,7 @@ def main() -> int:
     print(json.dumps({"corpus": c.stats()}), flush=True)
     modes = a.modes.split(",")
     models = {m: GibbsLDA(c, GibbsConfig(K=a.topics, count_mode=m.split("+")[0],
-                                         sampler=m.split("+")[1] if "+" in m else "pp"))
+                                         sampler=m.split("+")[1] if "+" in m else "auto"))
               for m in modes}
     for m in models.values():
         m.initialize()
@@ -113,7 +113,7 @@ def main() -> int:
         del models
         torch.cuda.empty_cache()
         rl = common.build_and_train(dk, wk, None, vocab, a.topics, None, 0.01, 0x0D15EA5E, 0, L, None, train=False)
-        m = GibbsLDA(rl.corpus, GibbsConfig(K=a.topics, count_mode="auto", sampler="lds" if a.lds else "pp"))
+        m = GibbsLDA(rl.corpus, GibbsConfig(K=a.topics, count_mode="auto", sampler="lds" if a.lds else "auto"))
         m.initialize()
         m.sweep(a.burn)
         ts = []

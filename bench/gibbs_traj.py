@@ -41,7 +41,7 @@ def main() -> int:
     c = run.corpus
     for mname in a.modes.split(","):
         m = GibbsLDA(c, GibbsConfig(K=a.topics, count_mode=mname.split("+")[0], use_graph=False,
-                                    sampler=mname.split("+")[1] if "+" in mname else "pp"))
+                                    sampler=mname.split("+")[1] if "+" in mname else "auto"))
         m.initialize()
         torch.cuda.synchronize()
         ms, chg = [], []

@@ -51,10 +51,11 @@ class GibbsConfig:
     auto_threshold: float = 0.08
     # debug: verify count invariants after every sweep() call (ONI_CHECK_INVARIANTS=1)
     check_invariants: bool = field(default_factory=lambda: os.environ.get("ONI_CHECK_INVARIANTS", "0") == "1")
-    # sweep kernel: "pp" ping-pong register sampler (default), "qpf" one-step q prefetch with a row
-    # copy, "plain" q-row load on each word change, "lds" LDS-staged doc counts (K ≤ 32, fma
-    # numerics); ONI_SAMPLER overrides the default
-    sampler: str = field(default_factory=lambda: os.environ.get("ONI_SAMPLER", "pp"))
+    # sweep kernel: "auto" (default: "qpf" for K ≤ 32, "plain" above — the measured winners),
+    # "qpf" one-step q-row prefetch, "plain" q-row load on each word change, "pp" ping-pong
+    # registers + 2-step token prefetch, "lds" LDS-staged doc counts (K ≤ 32, fma numerics).
+    # ONI_SAMPLER overrides the default. All but "lds" are bitwise identical.
+    sampler: str = field(default_factory=lambda: os.environ.get("ONI_SAMPLER", "auto"))
 
     def resolved_alpha(self) -> float:
         return float(self.alpha) if self.alpha is not None else 50.0 / self.K
@@ -106,9 +107,9 @@ class GibbsLDA:
             self.tok_zprev = torch.zeros_like(self.tok_z)
             self.chg_mask = torch.zeros(max(corpus.sell_slots // corpus.S, 1), dtype=torch.int64, device=dev)
         # the LDS sampler keeps counts as f32 integers: exact below 2^24 tokens per document
-        if cfg.sampler not in SAMPLERS:
+        if cfg.sampler not in SAMPLERS and cfg.sampler != "auto":
             raise ValueError(f"unknown sampler {cfg.sampler}")
-        self.qpf = SAMPLERS[cfg.sampler]
+        self.qpf = SAMPLERS[cfg.sampler] if cfg.sampler != "auto" else (SAMPLERS["qpf"] if self.G == 1 else 0)
         if self.qpf in (2, 4) and self.G != 1:
             self.qpf = 1  # lds / qpf variants exist for one-lane units (K ≤ 32) only
         if self.qpf == 2 and corpus.max_doc_len() >= (1 << 24):

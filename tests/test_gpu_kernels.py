@@ -60,8 +60,8 @@ def _toy_tokens(n_docs, V, seed, heavy=True):
     return torch.from_numpy(tdoc), torch.from_numpy(tword), keys
 
 
-@pytest.mark.parametrize("K,mode", [(20, "dual"), (20, "dual+plain"), (20, "dual+qpf"), (20, "delta+qpf"),
-                                    (20, "delta"), (20, "recount"), (20, "atomic"), (50, "recount+plain"),
+@pytest.mark.parametrize("K,mode", [(20, "dual"), (20, "dual+plain"), (20, "dual+pp"), (20, "delta+pp"),
+                                    (20, "delta"), (20, "recount"), (20, "atomic"), (50, "recount+pp"),
                                     (20, "dual+lds"), (20, "delta+lds"), (20, "atomic+lds"), (7, "dual+lds"),
                                     (32, "dual+lds"), (7, "dual"), (50, "dual"), (50, "delta"), (100, "atomic"),
                                     (100, "dual")])
@@ -72,9 +72,9 @@ def test_gibbs_bitwise_vs_oracle(gpu, K, mode):
     cg = build_corpus(tdoc.to(gpu), tword.to(gpu), 300, 400, torch.from_numpy(keys).to(gpu), G, L=64)
     assert torch.equal(cc.tok_word, cg.tok_word.cpu())
     assert torch.equal(cc.chunk_doc, cg.chunk_doc.cpu())
-    sampler = mode.split("+")[1] if "+" in mode else "pp"
+    sampler = mode.split("+")[1] if "+" in mode else "auto"
     mc = GibbsLDA(cc, GibbsConfig(K=K, seed=1234, use_graph=False, count_mode="atomic",
-                                  sampler="lds" if sampler == "lds" else "pp"))
+                                  sampler="lds" if sampler == "lds" else "auto"))
     mg = GibbsLDA(cg, GibbsConfig(K=K, seed=1234, use_graph=False, count_mode=mode.split("+")[0], sampler=sampler))
     assert (mg.qpf == 2) == (sampler == "lds")
     mc.initialize()
