@@ -759,7 +759,7 @@ __global__ __launch_bounds__(256) void k_delta_recount(const int32_t* __restrict
     const int4* sp = reinterpret_cast<const int4*>(wslot + base);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int4 v = sp[q];
+      const int4 v = __builtin_nontemporal_load(sp + q);
       sl[4 * q] = v.x; sl[4 * q + 1] = v.y; sl[4 * q + 2] = v.z; sl[4 * q + 3] = v.w;
     }
   } else if (base < hi) {
