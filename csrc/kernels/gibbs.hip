@@ -749,52 +749,22 @@ __global__ __launch_bounds__(256) void k_delta_recount(const int32_t* __restrict
   for (int i = threadIdx.x; i < cells; i += blockDim.x) hst[i] = 0;
   __syncthreads();
   const int64_t Smask = (1ll << log2S) - 1;
-  // 16 CONTIGUOUS word-sorted tokens per thread: all slot / mask loads issued before any is
-  // consumed (memory-level parallelism instead of a dependent load chain per token)
-  const int64_t base = lo + (int64_t)threadIdx.x * 16;
-  int32_t sl[16];
-  int nt = 0;
-  if (base + 16 <= hi && tile % 16 == 0) {
-    nt = 16;
-    const int4* sp = reinterpret_cast<const int4*>(wslot + base);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int4 v = __builtin_nontemporal_load(sp + q);
-      sl[4 * q] = v.x; sl[4 * q + 1] = v.y; sl[4 * q + 2] = v.z; sl[4 * q + 3] = v.w;
-    }
-  } else if (base < hi) {
-    nt = (int)(hi - base < 16 ? hi - base : 16);
-    for (int t = 0; t < nt; ++t) sl[t] = wslot[base + t];
-  }
-  uint32_t hit = 0;
-#pragma unroll
-  for (int t = 0; t < 16; ++t) {
-    if (t < nt) {
-      const uint64_t m = mask[(int64_t)sl[t] >> log2S];
-      const int bit = (int)((int64_t)sl[t] & Smask) * G;
-      hit |= (uint32_t)((m >> bit) & 1ull) << t;
-    }
-  }
-  int wv[16], zn[16], zo[16];
-#pragma unroll
-  for (int t = 0; t < 16; ++t) {
-    if (hit & (1u << t)) {
-      wv[t] = (int)tok_word[sl[t]];
-      zn[t] = tok_z[sl[t]];
-      zo[t] = tok_zprev[sl[t]];
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < 16; ++t) {
-    if (hit & (1u << t)) {
-      tok_zprev[sl[t]] = (uint8_t)zn[t];
-      const int r = wv[t] - w_lo;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const int64_t slot = __builtin_nontemporal_load(&wslot[i]);
+    const uint64_t m = mask[slot >> log2S];
+    const int bit = (int)(slot & Smask) * G;
+    if ((m >> bit) & 1ull) {
+      const int w = (int)tok_word[slot];
+      const int zn = tok_z[slot];
+      const int zo = tok_zprev[slot];
+      tok_zprev[slot] = (uint8_t)zn;
+      const int r = w - w_lo;
       if (r < rows) {
-        atomicAdd(&hst[r * KS + zn[t]], 1);
-        atomicAdd(&hst[r * KS + zo[t]], -1);
+        atomicAdd(&hst[r * KS + zn], 1);
+        atomicAdd(&hst[r * KS + zo], -1);
       } else {
-        atomicAdd(&dnwk[(int64_t)wv[t] * KS + zn[t]], 1);
-        atomicAdd(&dnwk[(int64_t)wv[t] * KS + zo[t]], -1);
+        atomicAdd(&dnwk[(int64_t)w * KS + zn], 1);
+        atomicAdd(&dnwk[(int64_t)w * KS + zo], -1);
       }
     }
   }
@@ -1017,7 +987,7 @@ ONI_API int oni_delta_recount(const int32_t* wslot, const int32_t* tile_wlo, con
                               const uint64_t* mask, const uint32_t* tok_word, const uint8_t* tok_z, uint8_t* tok_zprev,
                               int64_t T, int32_t* dnwk, int KS, int log2S, int G, int tile, int wmax, hipStream_t s) {
   if (T == 0) return 0;
-  if (tile != 256 * 16 || wmax < 1 || (size_t)wmax * KS * 4 > 64 * 1024) return (int)hipErrorInvalidValue;
+  if (tile < 256 || wmax < 1 || (size_t)wmax * KS * 4 > 64 * 1024) return (int)hipErrorInvalidValue;
   const unsigned grid = (unsigned)((T + tile - 1) / tile);
   k_delta_recount<<<grid, 256, (size_t)wmax * KS * 4, s>>>(wslot, tile_wlo, tile_whi, mask, tok_word, tok_z, tok_zprev,
                                                             T, dnwk, KS, log2S, G, tile, wmax);
