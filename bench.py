@@ -39,8 +39,9 @@ def main(argv=None) -> int:
     ap.add_argument("--flows-per-gpu", type=int, default=12_500_000)
     ap.add_argument("--topics", type=int, default=None)
     ap.add_argument("--source", choices=["flow", "dns", "proxy"], default="flow")
-    ap.add_argument("--score-path", choices=["pairs", "gather"], default="pairs",
-                    help="pairs: distinct-pair SDDMM + 4-B gathers; gather: per-event θ/φ row gathers")
+    ap.add_argument("--score-path", choices=["tiles", "pairs", "gather"], default="tiles",
+                    help="tiles: distinct pairs as 16x16 MFMA blocks; pairs: per-pair VALU dots; "
+                         "gather: per-event θ/φ row gathers (tiles/pairs + 4-B per-event pair gathers)")
     ap.add_argument("--events-per-gpu", type=int, default=2_000_000, help="dns/proxy events per GPU")
     ap.add_argument("--chunk-len", type=int, default=0, help="0 = auto (global token count)")
     ap.add_argument("--maxresults", type=int, default=3000)
@@ -133,29 +134,34 @@ def main(argv=None) -> int:
     dkeys, theta = common.gather_theta(run, comm)
     phi = model.phi()
     # distinct (doc, word) pairs + per-endpoint pair index: built once per day (corpus dictionaries)
-    plan = common.score_plan(dkeys, vocab, sides)
+    plans = {"tiles": common.score_plan(dkeys, vocab, sides, tiles=True),
+             "pairs": common.score_plan(dkeys, vocab, sides, tiles=False)}
     lk = [(common.lookup(dkeys, dk_), common.lookup(vocab, wk_)) for dk_, wk_ in sides]
 
-    def score_once():
+    def score_once(path):
         hist = torch.zeros(2048, dtype=torch.int32, device=dev)
-        if a.score_path == "pairs":
-            sc, _, _ = common.plan_score(theta, phi, plan, 1.0, hist=hist)
+        if path in plans:
+            sc, _, _ = common.plan_score(theta, phi, plans[path], 1.0, hist=hist)
         elif len(lk) == 2:
             sc, _, _ = ops.score(theta, phi, lk[0][0], lk[0][1], lk[1][0], lk[1][1], tol=1.0, hist=hist)
         else:
             sc, _, _ = ops.score(theta, phi, lk[0][0], lk[0][1], tol=1.0, hist=hist)
         return common.top_n(sc, 1.0, a.maxresults, comm, rank * per, hist=hist)
 
-    score_once()
-    sync()
-    comm.barrier()
-    reps = 5
-    t1 = time.perf_counter()
-    for _ in range(reps):
-        rows, scs = score_once()
-    sync()
-    comm.barrier()
-    score_dt = comm.allreduce_scalar((time.perf_counter() - t1) / reps, "max")
+    def time_path(path, reps=5):
+        score_once(path)
+        sync()
+        comm.barrier()
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            res = score_once(path)
+        sync()
+        comm.barrier()
+        return comm.allreduce_scalar((time.perf_counter() - t1) / reps, "max"), res
+
+    score_ab = {p: round(time_path(p)[0] * 1e3, 3) for p in ("tiles", "pairs", "gather") if p != a.score_path}
+    score_dt, (rows, scs) = time_path(a.score_path)
+    plan = plans["tiles"]
     ll = model.log_likelihood()
 
     tokens_local = run.corpus.T
@@ -195,7 +201,10 @@ def main(argv=None) -> int:
         "score_records_per_sec": round(n_total / score_dt, 1),
         "score_ms": round(score_dt * 1e3, 3),
         "score_path": a.score_path,
+        "score_ms_other_paths": score_ab,
         "score_pairs": plan.n_pairs,
+        "score_mfma_items": plan.tiles.n_items,
+        "score_mfma_block_density": round(plan.tiles.density(), 4),
         "loglik": ll,
         "planted_anomaly_recall_topN": round(hit_frac, 4),
         "setup_s": round(setup_s, 2),

@@ -40,7 +40,9 @@ struct OniGibbs {
   const uint32_t* sweep_ctr;   // device scalar: current sweep number (≥ 1), graph-replay safe
   uint64_t* chg_mask;          // MODE 2: one u64 per SELL step, bit c*G set if slot c's topic changed
   const int32_t* wpos;         // MODE 3: word-sorted position of every SELL slot
-  uint8_t* z_w;                // MODE 3: topic array in word-sorted order (kept in sync for changed tokens)
+  uint8_t* z_w;                // MODE 3/4: topic array in word-sorted order (kept in sync for changed tokens)
+  uint8_t* zo_w;               // MODE 4: previous topic of each changed token, word-sorted order
+                               // (MODE 4 reuses chg_mask as a u32 bitmap over word-sorted positions)
   int32_t* chg_count;          // optional: += number of tokens whose topic changed (drives the auto mode)
   int64_t n_slices;
   int32_t K;
@@ -120,9 +122,19 @@ __device__ __forceinline__ void flush_multi_rows(int32_t* __restrict__ ndk_dst, 
   }
 }
 
+// MODE 4: a changed token records (old, new) topic at its word-sorted position p and sets bit p
+// of a word-sorted bitmap; k_wdelta_recount then visits only set bits, reading contiguous
+// word ids and topic pairs (no per-token slot indirection, no z_prev array).
+__device__ __forceinline__ void mark_changed_w(const OniGibbs& a, int32_t p, int zo, int zn) {
+  a.z_w[p] = (uint8_t)zn;
+  a.zo_w[p] = (uint8_t)zo;
+  atomicOr(reinterpret_cast<uint32_t*>(a.chg_mask) + (p >> 5), 1u << (p & 31));
+}
+
 // MODE: 0 = no n_wk bookkeeping (full recount afterwards), 1 = per-token Δ atomics,
 //       2 = changed-slot ballot mask per step (delta recount afterwards),
 //       3 = changed topics also scattered into the word-sorted copy z_w (streaming recount afterwards)
+//       4 = changed tokens marked in a word-sorted bitmap + (old, new) topic copies (k_wdelta_recount)
 template <int G, int KP, bool INIT, int MODE, bool QPF>
 __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
   constexpr bool ATOMIC = MODE == 1;
@@ -235,6 +247,7 @@ __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
         ++nchg;
         a.tok_z[idx] = (uint8_t)zn;
         if constexpr (MODE == 3) a.z_w[a.wpos[idx]] = (uint8_t)zn;
+        if constexpr (MODE == 4) mark_changed_w(a, a.wpos[idx], zo, zn);
         if (ATOMIC) {
           atomicAdd(&a.dnwk[(int64_t)w * KS + zo], -1);
           atomicAdd(&a.dnwk[(int64_t)w * KS + zn], 1);
@@ -317,7 +330,7 @@ __device__ __forceinline__ void pp_step(const OniGibbs& a, int s, int len, int64
   if (s + 2 < len) {
     wq[P] = a.tok_word[idx + 2 * S];
     zq[P] = a.tok_z[idx + 2 * S];
-    if constexpr (MODE == 3) pq[P] = a.wpos[idx + 2 * S];
+    if constexpr (MODE == 3 || MODE == 4) pq[P] = a.wpos[idx + 2 * S];
   }
   if (s + 1 < len && wq[1 - P] != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)wq[1 - P] * KS + kbase, qn);
   if (w == oni::kPadWord) return;  // uniform across the G lanes of a unit
@@ -361,6 +374,7 @@ __device__ __forceinline__ void pp_step(const OniGibbs& a, int s, int len, int64
     ++nchg;
     a.tok_z[idx] = (uint8_t)zn;
     if constexpr (MODE == 3) a.z_w[wp] = (uint8_t)zn;
+    if constexpr (MODE == 4) mark_changed_w(a, wp, zo, zn);
     if constexpr (MODE == 1) {
       atomicAdd(&a.dnwk[(int64_t)w * KS + zo], -1);
       atomicAdd(&a.dnwk[(int64_t)w * KS + zn], 1);
@@ -409,7 +423,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     if (t < len) {
       wq[t] = a.tok_word[off + t * S + c];
       zq[t] = a.tok_z[off + t * S + c];
-      if constexpr (MODE == 3) pq[t] = a.wpos[off + t * S + c];
+      if constexpr (MODE == 3 || MODE == 4) pq[t] = a.wpos[off + t * S + c];
     }
   }
   if (wq[0] != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)wq[0] * KS + kbase, qa);
@@ -468,12 +482,25 @@ __global__ __launch_bounds__(256) void k_apply(int32_t* __restrict__ nwk, const 
                                                 int bump, int absolute, int nk_rep) {
   __shared__ float den[256];
   __shared__ int32_t nkn[256];
+  __shared__ int32_t part[256];
   const int32_t* dnk_cur = dcur + V * KS;
-  for (int k = threadIdx.x; k < KS; k += blockDim.x) {
-    int32_t v = nk_cur[k];
-    for (int r = 0; r < nk_rep; ++r) v += dnk_cur[r * KS + k];
-    nkn[k] = v;
-    den[k] = (float)v + vbeta;
+  // Σ over the nk_rep Δn_k replicas, spread over the whole block (256/KS replica groups, ≤ 3
+  // loads per thread at K = 20) instead of one serial 32-load chain per topic: integer sums, so
+  // the result is order-independent
+  {
+    const int groups = (int)blockDim.x / KS;
+    const int k = (int)threadIdx.x % KS, gi = (int)threadIdx.x / KS;
+    int32_t v = 0;
+    if (gi < groups)
+      for (int r = gi; r < nk_rep; r += groups) v += dnk_cur[r * KS + k];
+    part[threadIdx.x] = v;
+    __syncthreads();
+    if ((int)threadIdx.x < KS) {
+      int32_t t = nk_cur[threadIdx.x];
+      for (int g2 = 0; g2 < groups; ++g2) t += part[g2 * KS + threadIdx.x];
+      nkn[threadIdx.x] = t;
+      den[threadIdx.x] = (float)t + vbeta;
+    }
   }
   __syncthreads();
   if (blockIdx.x == 0) {
@@ -687,11 +714,23 @@ int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s)
   // qpf (sampler variant): 1 = k_gibbs_pp (ping-pong register sampler, default), 0 = k_gibbs with
   // a q-row load on each word change, 4 = k_gibbs with one-step q prefetch + row copy (G = 1),
   // 2 = k_gibbs_lds (LDS-staged counts, fma numerics, G = 1)
-  if (a.KS != G * KP || mode < 0 || mode > 3) return (int)hipErrorInvalidValue;
+  if (a.KS != G * KP || mode < 0 || mode > 4) return (int)hipErrorInvalidValue;
   const unsigned grid = (unsigned)((a.n_slices + kWavesPerBlock - 1) / kWavesPerBlock);
   if (grid == 0) return 0;
   if (init) {
     k_gibbs<G, KP, true, 1, false><<<grid, kBlock, 0, s>>>(a);  // init always builds n_wk by atomics
+    return (int)hipGetLastError();
+  }
+  if (mode == 4) {  // word-sorted change bitmap: register samplers only
+    if constexpr (G == 1) {
+      if (qpf == 4) {
+        k_gibbs<1, KP, false, 4, true><<<grid, kBlock, 0, s>>>(a);
+        return (int)hipGetLastError();
+      }
+    }
+    if (qpf == 1) k_gibbs_pp<G, KP, 4><<<grid, kBlock, 0, s>>>(a);
+    else if (qpf == 0) k_gibbs<G, KP, false, 4, false><<<grid, kBlock, 0, s>>>(a);
+    else return (int)hipErrorInvalidValue;
     return (int)hipGetLastError();
   }
   if constexpr (G == 1) {
@@ -926,7 +965,67 @@ __global__ __launch_bounds__(256) void k_recount_reg(const int32_t* __restrict__
   }
 }
 
+// Word-bitmap delta recount (MODE 4). A block owns 256 bitmap words = 8192 word-sorted token
+// positions; each thread reads one 32-bit word (coalesced 1 KB per block), clears it, and for
+// each set bit reads the position's word id (wsorted) and its (old, new) topics (zo_w, z_w) --
+// all contiguous arrays in word-sorted order, touched only where a token changed. Deltas go to
+// an LDS table over the block's word span (rows capped at wmax; wider spans go straight to
+// global atomics) and are flushed one row-contiguous atomic per non-zero cell. Cost ∝ changed
+// tokens + T/8 bytes of bitmap, vs the slot-indexed delta recount's 4 B/token scan.
+constexpr int kWBitsPerBlock = 256 * 32;
+
+__global__ __launch_bounds__(256) void k_wdelta_recount(uint32_t* __restrict__ wbits,
+                                                         const int32_t* __restrict__ wsorted,
+                                                         const uint8_t* __restrict__ z_w,
+                                                         const uint8_t* __restrict__ zo_w, int64_t T,
+                                                         int32_t* __restrict__ dnwk, int KS, int wmax) {
+  extern __shared__ __attribute__((aligned(16))) int32_t hst[];
+  const int64_t lo = (int64_t)blockIdx.x * kWBitsPerBlock;
+  if (lo >= T) return;
+  const int64_t hi = lo + kWBitsPerBlock < T ? lo + kWBitsPerBlock : T;
+  const int w_lo = wsorted[lo], w_hi = wsorted[hi - 1];
+  const int rows = (w_hi - w_lo + 1) < wmax ? (w_hi - w_lo + 1) : wmax;
+  const int cells = rows * KS;
+  for (int i = threadIdx.x; i < cells; i += blockDim.x) hst[i] = 0;
+  __syncthreads();
+  const int64_t word = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  uint32_t m = 0;
+  if (word * 32 < T) {
+    m = wbits[word];
+    if (m) wbits[word] = 0u;
+  }
+  while (m) {
+    const int b = __ffs(m) - 1;
+    m &= m - 1u;
+    const int64_t i = word * 32 + b;
+    const int w = wsorted[i];
+    const int zn = z_w[i], zo = zo_w[i];
+    const int r = w - w_lo;
+    if (r < rows) {
+      atomicAdd(&hst[r * KS + zn], 1);
+      atomicAdd(&hst[r * KS + zo], -1);
+    } else {
+      atomicAdd(&dnwk[(int64_t)w * KS + zn], 1);
+      atomicAdd(&dnwk[(int64_t)w * KS + zo], -1);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < cells; i += blockDim.x) {
+    const int v = hst[i];
+    if (v) atomicAdd(&dnwk[(int64_t)(w_lo + i / KS) * KS + (i % KS)], v);
+  }
+}
+
 }  // namespace
+
+ONI_API int oni_wdelta_recount(uint32_t* wbits, const int32_t* wsorted, const uint8_t* z_w, const uint8_t* zo_w,
+                               int64_t T, int32_t* dnwk, int KS, int wmax, hipStream_t s) {
+  if (T == 0) return 0;
+  if (wmax < 1 || KS < 1 || (size_t)wmax * KS * 4 > 64 * 1024) return (int)hipErrorInvalidValue;
+  const unsigned grid = (unsigned)((T + kWBitsPerBlock - 1) / kWBitsPerBlock);
+  k_wdelta_recount<<<grid, 256, (size_t)wmax * KS * 4, s>>>(wbits, wsorted, z_w, zo_w, T, dnwk, KS, wmax);
+  return (int)hipGetLastError();
+}
 
 ONI_API int oni_recount_stream(const int32_t* wsorted, const uint8_t* z_w, int64_t T, int32_t* nwk, int KS, int tile,
                                int wmax, hipStream_t s) {
@@ -947,9 +1046,10 @@ ONI_API int oni_recount_stream(const int32_t* wsorted, const uint8_t* z_w, int64
 // Supported (G, KP) configurations. K ≤ 32: G = 1 (KP = K rounded up to 4).
 ONI_API int oni_gibbs_launch(const OniGibbs* a, int G, int KP, int init, int mode, int qpf, hipStream_t s) {
   if (a->nk_rep < 1 || (a->nk_rep & (a->nk_rep - 1))) return (int)hipErrorInvalidValue;
-  if (a->K < 1 || a->K > 255 || a->K > a->KS || mode < 0 || mode > 3) return (int)hipErrorInvalidValue;
+  if (a->K < 1 || a->K > 255 || a->K > a->KS || mode < 0 || mode > 4) return (int)hipErrorInvalidValue;
   if (mode == 2 && !a->chg_mask) return (int)hipErrorInvalidValue;
   if (mode == 3 && (!a->wpos || !a->z_w)) return (int)hipErrorInvalidValue;
+  if (mode == 4 && (!a->wpos || !a->z_w || !a->zo_w || !a->chg_mask)) return (int)hipErrorInvalidValue;
 #define ONI_CASE(g_, kp_) \
   if (G == g_ && KP == kp_) return launch_gibbs<g_, kp_>(*a, init != 0, mode, qpf, s);
   ONI_CASE(1, 4) ONI_CASE(1, 8) ONI_CASE(1, 12) ONI_CASE(1, 16) ONI_CASE(1, 20) ONI_CASE(1, 24) ONI_CASE(1, 28)

@@ -43,7 +43,10 @@ class GibbsConfig:
     # "dual" (changed topics mirrored into a word-sorted z copy, streaming recount), "delta"
     # (changed-slot masks + word-sorted delta recount: cost ∝ changed tokens), "recount" (full
     # gathered recount: constant cost) | "atomic" (per-token Δ atomics)
-    count_mode: str = "auto"
+    # "wdelta" (changed tokens set a bit in a word-sorted bitmap + keep (old, new) topics in
+    # word-sorted order: the recount touches only changed tokens, no slot indirection).
+    # ONI_COUNT_MODE overrides the default.
+    count_mode: str = field(default_factory=lambda: os.environ.get("ONI_COUNT_MODE", "auto"))
     # "auto": switch to the delta recount once the all-reduced fraction of tokens that changed
     # topic in a sweep falls below auto_threshold (measured on device, read two sweeps late so the
     # host never stalls the stream); auto_switch > 0 instead fixes the first delta sweep (tests)
@@ -91,18 +94,22 @@ class GibbsLDA:
         self.dn = [torch.zeros(self._aux_off + ops.DN_AUX, dtype=i32, device=dev) for _ in range(2)]
         self.q = torch.zeros(V, KS, dtype=torch.float32, device=dev)
         self.sweep_ctr = torch.zeros(1, dtype=i32, device=dev)
-        if cfg.count_mode not in ("auto", "dual", "delta", "recount", "atomic"):
+        if cfg.count_mode not in ("auto", "dual", "delta", "recount", "atomic", "wdelta"):
             raise ValueError(f"unknown count_mode {cfg.count_mode}")
         self.auto = cfg.count_mode == "auto"
-        self.mode = {"recount": 0, "atomic": 1, "delta": 2, "dual": 3, "auto": 2}[cfg.count_mode]
+        self.mode = {"recount": 0, "atomic": 1, "delta": 2, "dual": 3, "wdelta": 4, "auto": 2}[cfg.count_mode]
         self._zprev_synced = False
         self._delta_on = False
         self._force_mode = None
         self._chg_q: list = []    # (sweep index, host buffer, event) of pending change-count copies
         self.T_global = corpus.T
         self.change_log: list[tuple[int, float]] = []
-        if self.mode == 3:
+        if self.mode in (3, 4):
             self.z_w = torch.zeros(max(corpus.T, 1), dtype=torch.uint8, device=dev)
+        if self.mode == 4:
+            # word-sorted change bitmap (+ slack word) and the previous topic of each changed token
+            self.wbits = torch.zeros((corpus.T + 31) // 32 + 1, dtype=torch.int32, device=dev)
+            self.zo_w = torch.zeros(max(corpus.T, 1), dtype=torch.uint8, device=dev)
         if self.mode == 2:
             self.tok_zprev = torch.zeros_like(self.tok_z)
             self.chg_mask = torch.zeros(max(corpus.sell_slots // corpus.S, 1), dtype=torch.int64, device=dev)
@@ -112,6 +119,8 @@ class GibbsLDA:
         self.qpf = SAMPLERS[cfg.sampler] if cfg.sampler != "auto" else (SAMPLERS["qpf"] if self.G == 1 else 0)
         if self.qpf in (2, 4) and self.G != 1:
             self.qpf = 1  # lds / qpf variants exist for one-lane units (K ≤ 32) only
+        if self.qpf == 2 and self.mode == 4:
+            self.qpf = 4  # the word-bitmap delta mode is implemented by the register samplers
         if self.qpf == 2 and corpus.max_doc_len() >= (1 << 24):
             self.qpf = 1  # LDS rows hold counts as f32: exact below 2^24
         self.a = 0  # ndk parity
@@ -205,8 +214,10 @@ class GibbsLDA:
         if self.mode == 2:
             self.tok_zprev.copy_(self.tok_z)
             self._zprev_synced = True
-        elif self.mode == 3 and self.c.T:
+        elif self.mode in (3, 4) and self.c.T:
             self.z_w[: self.c.T] = self.tok_z[self.c.wslot.long()]
+            if self.mode == 4:
+                self.wbits.zero_()
 
     def _prime(self) -> None:
         # zero-delta apply: q from n_wk, nk[1] = nk[0]; leaves dn[0], dn[1] zero
@@ -228,10 +239,14 @@ class GibbsLDA:
         ops.copy_rows(self.ndk[self.a], self.ndk[1 - self.a], c.long_rows, self.KS)
         ops.gibbs_pass(self._state(False), self.G, self.KP, self.K, self.alpha, self.cfg.seed, False,
                        self.sweep_ctr, c.chunk_len, host_sweep=self.sweeps_done + 1, mode=mode,
-                       prefetch_q=self.qpf, chg_mask=getattr(self, "chg_mask", None), wpos=c.wpos,
-                       z_w=getattr(self, "z_w", None))
+                       prefetch_q=self.qpf,
+                       chg_mask=self.wbits if mode == 4 else getattr(self, "chg_mask", None), wpos=c.wpos,
+                       z_w=getattr(self, "z_w", None), zo_w=getattr(self, "zo_w", None))
         head = self.dn[self.b][: self.V * self.KS].view(self.V, self.KS)
-        if mode == 0:
+        if mode == 4:
+            # dn[b] head := Δn_wk of the tokens marked in the word-sorted change bitmap
+            ops.wdelta_recount(self.wbits, c.wsorted, self.z_w, self.zo_w, head, self.KS)
+        elif mode == 0:
             # dn[b] head := this rank's n_wk rebuilt from z (tail keeps Δn_k)
             ops.recount(c.wsorted, c.wslot, self.tok_z, head, self.KS)
         elif mode == 3:

@@ -228,12 +228,14 @@ def sell_perm_z(chunk_doc, chunk_pos0, chunk_len, S, slice_off, doc_tok_ptr, tok
 def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init: bool, sweep_ctr: torch.Tensor,
                chunk_len: torch.Tensor, host_sweep: int | None = None, mode: int = 1,
                prefetch_q: bool | int = False, chg_mask: torch.Tensor | None = None, wpos: torch.Tensor | None = None,
-               z_w: torch.Tensor | None = None) -> None:
+               z_w: torch.Tensor | None = None, zo_w: torch.Tensor | None = None) -> None:
     """Launch one init/sweep pass. ``st`` holds the OniGibbs tensors (see csrc/kernels/gibbs.hip).
 
     ``mode`` 1: accumulate Δn_wk with per-token atomics; 0: the caller rebuilds n_wk with
     :func:`recount`; 2: record changed slots in ``chg_mask`` for :func:`delta_recount`; 3: also
-    write changed topics into the word-sorted copy ``z_w`` (via ``wpos``) for a streaming recount.
+    write changed topics into the word-sorted copy ``z_w`` (via ``wpos``) for a streaming recount;
+    4: changed tokens set their word-sorted bit in ``chg_mask`` (int32 bitmap) and record
+    (old, new) topics in ``zo_w`` / ``z_w`` for :func:`wdelta_recount`.
     ``prefetch_q`` 1: register sampler with next-q-row prefetch; 2: LDS-staged doc counts (G=1).
     """
     atomic = mode == 1
@@ -242,9 +244,14 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
     nk_rep = st["dnk"].numel() // KS
     if nk_rep < 1 or nk_rep * KS != st["dnk"].numel() or nk_rep & (nk_rep - 1):
         raise ValueError("dnk must hold a power-of-two number of [KS] replicas")
+    if mode == 4:
+        T = int(z_w.numel()) if z_w is not None else 0
+        if (wpos is None or z_w is None or zo_w is None or chg_mask is None or wpos.numel() != st["tok_word"].numel()
+                or zo_w.numel() < T or chg_mask.dtype != torch.int32 or chg_mask.numel() * 32 < T):
+            raise ValueError("wdelta mode needs wpos [SELL slots], z_w/zo_w [T] and an int32 bitmap of T bits")
     if not _is_dev(st["tok_word"]):
         chg = st.get("chg_count")
-        z_before = st["tok_z"].clone() if chg is not None else None
+        z_before = st["tok_z"].clone() if (chg is not None or mode == 4) else None
         npst = {k: (v.numpy().view(np.uint32) if k in ("tok_word", "chunk_key") else v.numpy())
                 for k, v in st.items() if v is not None}
         npst["dnk"] = npst["dnk"][:KS]  # replica 0 (the sum over replicas is what counts)
@@ -256,6 +263,14 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
         if mode == 3:
             valid = wpos >= 0
             z_w[wpos[valid].long()] = st["tok_z"][valid]
+        if mode == 4:
+            ch = st["tok_z"] != z_before
+            p = wpos[ch].long()
+            z_w[p] = st["tok_z"][ch]
+            zo_w[p] = z_before[ch]
+            upd = np.zeros(chg_mask.numel(), dtype=np.uint32)
+            np.bitwise_or.at(upd, (p >> 5).numpy(), (np.uint32(1) << (p & 31).numpy().astype(np.uint32)))
+            chg_mask |= torch.from_numpy(upd.view(np.int32))
         if chg is not None:
             chg += int((st["tok_z"] != z_before).sum())
         return
@@ -277,6 +292,8 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
         if wpos is None or z_w is None or wpos.numel() != st["tok_word"].numel():
             raise ValueError("dual mode needs wpos [SELL slots] and z_w [T]")
         a.wpos, a.z_w = _lib.ptr(wpos), _lib.ptr(z_w)
+    if mode == 4:
+        a.wpos, a.z_w, a.zo_w, a.chg_mask = _lib.ptr(wpos), _lib.ptr(z_w), _lib.ptr(zo_w), _lib.ptr(chg_mask)
     if st.get("chg_count") is not None:
         a.chg_count = _lib.ptr(st["chg_count"])
     a.n_slices, a.K, a.KS, a.alpha, a.seed0, a.seed1 = n_slices, K, KS, float(alpha), s0, s1
@@ -307,6 +324,27 @@ def delta_recount(wslot, tile_wlo, tile_whi, chg_mask, tok_word, tok_z, tok_zpre
                                                             tok_zprev)), T, _lib.ptr(dnwk_out), KS,
                                             S.bit_length() - 1, G, RECOUNT_TILE, wmax, _lib.stream()),
                "oni_delta_recount")
+
+
+def wdelta_recount(wbits, wsorted, z_w, zo_w, dnwk_out, KS: int) -> None:
+    """Δn_wk of the tokens marked in the word-sorted bitmap ``wbits`` (+1 at (w, z_w), -1 at
+    (w, zo_w)); clears the bitmap (k_wdelta_recount)."""
+    T = wsorted.numel()
+    if T == 0:
+        return
+    if not _is_dev(wsorted):
+        b = wbits.numpy().view(np.uint32)
+        pos = np.nonzero(np.unpackbits(b.view(np.uint8), bitorder="little")[:T])[0]
+        pt = torch.from_numpy(pos)
+        w = wsorted[pt].long()
+        one = torch.ones(pos.size, dtype=torch.int32)
+        dnwk_out.view(-1).index_add_(0, w * KS + z_w[pt].long(), one)
+        dnwk_out.view(-1).index_add_(0, w * KS + zo_w[pt].long(), -one)
+        wbits.zero_()
+        return
+    wmax = max(1, RECOUNT_CELLS // KS)
+    _lib.check(_lib.lib().oni_wdelta_recount(*map(_lib.ptr, (wbits, wsorted, z_w, zo_w)), T, _lib.ptr(dnwk_out), KS,
+                                             wmax, _lib.stream()), "oni_wdelta_recount")
 
 
 RECOUNT_TILE = 4096
@@ -412,6 +450,30 @@ def pair_score(theta, phi, pdoc, pword) -> torch.Tensor:
     out = torch.empty(P, dtype=torch.float32, device=theta.device)
     _lib.check(_lib.lib().oni_pair_score(_lib.ptr(theta), _lib.ptr(phi), KS, _lib.ptr(pdoc), _lib.ptr(pword), P,
                                          _lib.ptr(out), _lib.stream()), "oni_pair_score")
+    return out
+
+
+def tile_score(theta, phi, item_docs, item_words, item_p0, pair_rc, pdoc, pword) -> torch.Tensor:
+    """Pair scores by 16×16 MFMA blocks (K15 MFMA variant, k_tile_score), item-major pair order.
+
+    ``pdoc``/``pword`` (the pairs in the same item-major order) are what the CPU oracle dots; the
+    device kernel reads only the item tables. Numerics: k-ordered fmaf chain (spec.dot_rows_fma).
+    """
+    P = pair_rc.numel()
+    if not _is_dev(theta):
+        return torch.from_numpy(spec.dot_rows_fma(theta.numpy()[pdoc.numpy()], phi.numpy()[pword.numpy()]))
+    KS = theta.shape[-1]
+    if phi.shape[-1] != KS:
+        raise ValueError("theta/phi row widths differ")
+    n_items = item_p0.numel() - 1
+    _need(item_docs, torch.int32, "item_docs", n_items * 16)
+    _need(item_words, torch.int32, "item_words", n_items * 16)
+    _need(item_p0, torch.int64, "item_p0")
+    _need(pair_rc, torch.uint8, "pair_rc")
+    out = torch.empty(P, dtype=torch.float32, device=theta.device)
+    _lib.check(_lib.lib().oni_tile_score(_lib.ptr(theta), _lib.ptr(phi), KS, _lib.ptr(item_docs),
+                                         _lib.ptr(item_words), _lib.ptr(item_p0), _lib.ptr(pair_rc), n_items,
+                                         _lib.ptr(out), _lib.stream()), "oni_tile_score")
     return out
 
 

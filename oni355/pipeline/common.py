@@ -191,35 +191,126 @@ def lookup(sorted_keys: torch.Tensor, q: torch.Tensor) -> torch.Tensor:
 
 
 @dataclass
+class TilePlan:
+    """16-doc × 16-word MFMA blocks covering every distinct pair (k_tile_score items)."""
+    item_docs: torch.Tensor   # int32 [n_items*16] θ row of each tile row (-1: none)
+    item_words: torch.Tensor  # int32 [n_items*16] φ row of each block column (-1: none)
+    item_p0: torch.Tensor     # int64 [n_items+1] pair range of each item (pairs are item-major)
+    pair_rc: torch.Tensor     # uint8 [P] (row << 4) | col of each pair inside its item
+
+    @property
+    def n_items(self) -> int:
+        return int(self.item_p0.numel()) - 1
+
+    def density(self) -> float:
+        """Fraction of the computed 16×16 outputs that are real pairs."""
+        return float(self.pair_rc.numel()) / max(256 * self.n_items, 1)
+
+
+@dataclass
 class ScorePlan:
     """Distinct (doc, word) pairs of a set of events + each event endpoint's pair index (K09/K15).
 
     Built once per day after training (the dictionaries are final); scoring is then one SDDMM
-    over the distinct pairs and a 4-B gather per endpoint (ops.pair_score / ops.event_min)."""
+    over the distinct pairs (ops.pair_score on the VALU, or ops.tile_score on MFMA blocks when
+    ``tiles`` is set; pairs are then stored item-major) and a 4-B gather per endpoint
+    (ops.event_min)."""
     pdoc: torch.Tensor
     pword: torch.Tensor
     inv: list
+    tiles: TilePlan | None = None
 
     @property
     def n_pairs(self) -> int:
         return int(self.pdoc.numel())
 
 
+def tile_plan(pdoc: torch.Tensor, pword: torch.Tensor, D: int, V: int) -> tuple[TilePlan, torch.Tensor]:
+    """Group distinct pairs into MFMA items; returns (plan, perm) with pairs[perm] item-major.
+
+    Documents are ordered heaviest first (then by their smallest word), so the dense rows of
+    heavy IPs share tiles and single-pair documents with the same word share a block column.
+    A tile is 16 consecutive documents of that order; its words (the union over its documents)
+    are cut into blocks of 16; an item is one (tile, block).
+    """
+    dev = pdoc.device
+    i64 = torch.int64
+    P = pdoc.numel()
+    pd, pw = pdoc.to(i64), pword.to(i64)
+    npairs = torch.bincount(pd, minlength=D)
+    first = torch.full((D,), V, dtype=i64, device=dev).scatter_reduce_(0, pd, pw, reduce="amin")
+    _, o1 = torch.sort(first, stable=True)
+    _, o2 = torch.sort(npairs[o1], descending=True, stable=True)
+    dorder = o1[o2]
+    rank = torch.empty(D, dtype=i64, device=dev)
+    rank[dorder] = torch.arange(D, dtype=i64, device=dev)
+    prank = rank[pd]
+    tile, row = prank // 16, prank % 16
+    n_tiles = (D + 15) // 16
+    tile_docs = torch.full((n_tiles * 16,), -1, dtype=torch.int32, device=dev)
+    tile_docs[:D] = dorder.to(torch.int32)
+    u, inv = torch.unique(tile * V + pw, return_inverse=True)
+    utile = u // V
+    tcount = torch.bincount(utile, minlength=n_tiles)
+    tstart = _excl_cumsum(tcount)
+    col = torch.arange(u.numel(), dtype=i64, device=dev) - tstart[utile]
+    nblk = (tcount + 15) // 16
+    istart = _excl_cumsum(nblk)
+    n_items = int(istart[-1])
+    uitem = istart[utile] + col // 16
+    item_words = torch.full((n_items * 16,), -1, dtype=torch.int32, device=dev)
+    item_words[uitem * 16 + col % 16] = (u % V).to(torch.int32)
+    item_tile = torch.repeat_interleave(torch.arange(n_tiles, dtype=i64, device=dev), nblk)
+    item_docs = tile_docs.view(n_tiles, 16)[item_tile].reshape(-1).contiguous()
+    p_item = uitem[inv]
+    rc = row * 16 + (col % 16)[inv]
+    perm = torch.argsort(p_item * 256 + rc)
+    item_p0 = _excl_cumsum(torch.bincount(p_item, minlength=n_items))
+    plan = TilePlan(item_docs, item_words, item_p0.contiguous(), rc[perm].to(torch.uint8).contiguous())
+    if P != int(item_p0[-1]):
+        raise AssertionError("tile plan lost pairs")
+    return plan, perm
+
+
+def _excl_cumsum(x: torch.Tensor) -> torch.Tensor:
+    out = torch.zeros(x.numel() + 1, dtype=torch.int64, device=x.device)
+    if x.numel():
+        torch.cumsum(x.to(torch.int64), 0, out=out[1:])
+    return out
+
+
+SCORE_TILES = True  # MFMA block scoring by default (see bench.py --score-path; profiles/ A/B)
+
+
 @traced("oni:score_plan")
-def score_plan(dkeys: torch.Tensor, vocab: torch.Tensor, sides) -> ScorePlan:
-    """``sides``: [(doc_keys64, word_keys64)] per event endpoint (1 for DNS/proxy, 2 for flows)."""
+def score_plan(dkeys: torch.Tensor, vocab: torch.Tensor, sides, tiles: bool | None = None) -> ScorePlan:
+    """``sides``: [(doc_keys64, word_keys64)] per event endpoint (1 for DNS/proxy, 2 for flows).
+
+    ``tiles`` (default :data:`SCORE_TILES`) also builds the MFMA item plan and stores the pairs
+    item-major."""
     V = int(vocab.numel())
     ids = [lookup(dkeys, dk).to(torch.int64) * V + lookup(vocab, wk).to(torch.int64) for dk, wk in sides]
     uniq, inv = torch.unique(torch.cat(ids), return_inverse=True)
     if uniq.numel() >= 2**31:
         raise ValueError("too many distinct pairs for int32 indices")
+    pdoc, pword = uniq // V, uniq % V
+    tp = None
+    if SCORE_TILES if tiles is None else tiles:
+        tp, perm = tile_plan(pdoc, pword, int(dkeys.numel()), V)
+        newpos = torch.empty_like(perm)
+        newpos[perm] = torch.arange(perm.numel(), dtype=perm.dtype, device=perm.device)
+        pdoc, pword, inv = pdoc[perm], pword[perm], newpos[inv]
     invs = [x.to(torch.int32).contiguous() for x in inv.split([t.numel() for t in ids])]
-    return ScorePlan((uniq // V).to(torch.int32).contiguous(), (uniq % V).to(torch.int32).contiguous(), invs)
+    return ScorePlan(pdoc.to(torch.int32).contiguous(), pword.to(torch.int32).contiguous(), invs, tp)
 
 
 @traced("oni:score")
 def plan_score(theta: torch.Tensor, phi: torch.Tensor, plan: ScorePlan, tol: float, hist=None, want_parts=False):
-    ps = ops.pair_score(theta, phi, plan.pdoc, plan.pword)
+    if plan.tiles is not None:
+        t = plan.tiles
+        ps = ops.tile_score(theta, phi, t.item_docs, t.item_words, t.item_p0, t.pair_rc, plan.pdoc, plan.pword)
+    else:
+        ps = ops.pair_score(theta, phi, plan.pdoc, plan.pword)
     return ops.event_min(ps, plan.inv[0], plan.inv[1] if len(plan.inv) > 1 else None, tol=tol,
                           want_parts=want_parts, hist=hist)
 

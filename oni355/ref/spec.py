@@ -338,6 +338,14 @@ def dot_rows(theta_rows, phi_rows):
     return s
 
 
+def dot_rows_fma(theta_rows, phi_rows):
+    """k-ordered fmaf chain from 0: the numerics of v_mfma_f32_16x16x4_f32 (k_tile_score)."""
+    s = np.zeros(theta_rows.shape[0], dtype=F32)
+    for k in range(theta_rows.shape[1]):
+        s = fma_f32(theta_rows[:, k], phi_rows[:, k], s)
+    return s
+
+
 def score(theta, phi, d1, w1, d2=None, w2=None):
     s1 = dot_rows(theta[d1], phi[w1])
     if d2 is None:

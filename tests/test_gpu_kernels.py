@@ -64,7 +64,8 @@ def _toy_tokens(n_docs, V, seed, heavy=True):
                                     (20, "delta"), (20, "recount"), (20, "atomic"), (50, "recount+pp"),
                                     (20, "dual+lds"), (20, "delta+lds"), (20, "atomic+lds"), (7, "dual+lds"),
                                     (32, "dual+lds"), (7, "dual"), (50, "dual"), (50, "delta"), (100, "atomic"),
-                                    (100, "dual")])
+                                    (100, "dual"), (20, "wdelta"), (20, "wdelta+pp"), (20, "wdelta+plain"),
+                                    (50, "wdelta"), (100, "wdelta")])
 def test_gibbs_bitwise_vs_oracle(gpu, K, mode):
     tdoc, tword, keys = _toy_tokens(300, 400, K)
     G, KP = ops.choose_tiling(K)
@@ -77,6 +78,8 @@ def test_gibbs_bitwise_vs_oracle(gpu, K, mode):
                                   sampler="lds" if sampler == "lds" else "auto"))
     mg = GibbsLDA(cg, GibbsConfig(K=K, seed=1234, use_graph=False, count_mode=mode.split("+")[0], sampler=sampler))
     assert (mg.qpf == 2) == (sampler == "lds")
+    if mode.startswith("wdelta"):
+        assert mg.mode == 4
     mc.initialize()
     mg.initialize()
     assert torch.equal(mc.tok_z, mg.tok_z.cpu())
@@ -96,7 +99,7 @@ def test_gibbs_bitwise_vs_oracle(gpu, K, mode):
     assert int(mg.nwk.min()) >= 0 and int(mg.ndk_cur.min()) >= 0
 
 
-@pytest.mark.parametrize("mode,switch", [("auto", 4), ("auto", 0), ("dual", 0), ("delta", 0)])
+@pytest.mark.parametrize("mode,switch", [("auto", 4), ("auto", 0), ("dual", 0), ("delta", 0), ("wdelta", 0)])
 def test_graph_replay_matches_eager(gpu, mode, switch):
     tdoc, tword, keys = _toy_tokens(500, 300, 5)
     c = build_corpus(tdoc.to(gpu), tword.to(gpu), 500, 300, torch.from_numpy(keys).to(gpu), 1, L=128)
@@ -175,7 +178,7 @@ def test_pair_plan_score_matches_gather(gpu, two):
     vocab = torch.arange(V, dtype=torch.int64, device=gpu) * 5 + 2
     sides = [(dkeys[torch.from_numpy(r.integers(0, D, n)).to(gpu)], vocab[torch.from_numpy(r.integers(0, V, n)).to(gpu)])
              for _ in range(2 if two else 1)]
-    plan = common.score_plan(dkeys, vocab, sides)
+    plan = common.score_plan(dkeys, vocab, sides, tiles=False)
     h1 = torch.zeros(2048, dtype=torch.int32, device=gpu)
     h2 = torch.zeros(2048, dtype=torch.int32, device=gpu)
     got, g1, g2 = common.plan_score(th, ph, plan, 0.3, hist=h1, want_parts=True)
@@ -186,3 +189,31 @@ def test_pair_plan_score_matches_gather(gpu, two):
     if two:
         assert torch.equal(g2, w2)
     assert torch.equal(h1, h2)
+
+
+@pytest.mark.parametrize("KS", [20, 52])
+def test_tile_score_mfma_bitwise_vs_fma_oracle(gpu, KS):
+    """k_tile_score (v_mfma_f32_16x16x4_f32 blocks) == the k-ordered fmaf-chain oracle, bit for bit."""
+    from oni355.pipeline import common
+    r = np.random.default_rng(KS)
+    D, V, n = 700, 500, 60_001
+    th = (r.random((D, KS)) / KS).astype(np.float32)
+    ph = (r.random((V, KS)) ** 6).astype(np.float32)
+    th[:, KS - 2:] = 0  # zero padding columns as theta()/phi() produce
+    ph[:, KS - 2:] = 0
+    dkeys = torch.arange(D, dtype=torch.int64) * 3 + 1
+    vocab = torch.arange(V, dtype=torch.int64) * 5 + 2
+    # power-law docs so tiles mix dense heavy rows with single-pair rows
+    dsel = torch.from_numpy(np.minimum(r.zipf(1.3, n) - 1, D - 1))
+    sides = [(dkeys[dsel], vocab[torch.from_numpy(r.integers(0, V, n))])]
+    plan_c = common.score_plan(dkeys, vocab, sides, tiles=True)
+    want = common.plan_score(torch.from_numpy(th), torch.from_numpy(ph), plan_c, 0.3)[0]
+    g = lambda x: x.to(gpu)  # noqa: E731
+    plan_g = common.score_plan(g(dkeys), g(vocab), [(g(a), g(b)) for a, b in sides], tiles=True)
+    t = plan_g.tiles
+    ps = ops.tile_score(g(torch.from_numpy(th)), g(torch.from_numpy(ph)), t.item_docs, t.item_words, t.item_p0,
+                        t.pair_rc, plan_g.pdoc, plan_g.pword)
+    ref = spec.dot_rows_fma(th[plan_g.pdoc.cpu().numpy()], ph[plan_g.pword.cpu().numpy()])
+    assert np.array_equal(ps.cpu().numpy(), ref)
+    got = common.plan_score(g(torch.from_numpy(th)), g(torch.from_numpy(ph)), plan_g, 0.3)[0]
+    assert torch.equal(got.cpu(), want)

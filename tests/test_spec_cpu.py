@@ -225,3 +225,25 @@ def test_adaptive_auto_mode_switches_and_matches_recount():
         m.sweep(8)
     assert a._delta_on and a.change_log and 0 < a.change_log[0][1] < 1
     assert torch.equal(a.tok_z, b.tok_z) and torch.equal(a.nwk, b.nwk) and torch.equal(a.nk_cur, b.nk_cur)
+
+
+def test_wdelta_count_mode_matches_recount():
+    """Word-bitmap delta bookkeeping (MODE 4) reproduces the full recount's chain exactly."""
+    import torch
+
+    from oni355.models.corpus import build_corpus
+    from oni355.models.gibbs import GibbsConfig, GibbsLDA
+    r = np.random.default_rng(10)
+    lens = r.integers(1, 300, 50)
+    tdoc = torch.from_numpy(np.repeat(np.arange(50), lens))
+    tword = torch.from_numpy(r.integers(0, 60, int(lens.sum())))
+    c = build_corpus(tdoc, tword, 50, 60, torch.arange(50, dtype=torch.int32) * 7 + 2, 1, L=64)
+    a = GibbsLDA(c, GibbsConfig(K=20, seed=6, count_mode="wdelta"))
+    b = GibbsLDA(c, GibbsConfig(K=20, seed=6, count_mode="recount"))
+    for m in (a, b):
+        m.initialize()
+        m.sweep(5)
+    assert torch.equal(a.tok_z, b.tok_z) and torch.equal(a.nwk, b.nwk) and torch.equal(a.nk_cur, b.nk_cur)
+    assert not bool(a.wbits.any())  # the recount clears every bit it consumed
+    # z_w stays the word-sorted image of tok_z
+    assert torch.equal(a.z_w[: c.T], a.tok_z[c.wslot.long()])
