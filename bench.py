@@ -39,7 +39,7 @@ def main(argv=None) -> int:
     ap.add_argument("--flows-per-gpu", type=int, default=12_500_000)
     ap.add_argument("--topics", type=int, default=None)
     ap.add_argument("--source", choices=["flow", "dns", "proxy"], default="flow")
-    ap.add_argument("--score-path", choices=["tiles", "pairs", "gather"], default="tiles",
+    ap.add_argument("--score-path", choices=["tiles", "pairs", "gather"], default="pairs",
                     help="tiles: distinct pairs as 16x16 MFMA blocks; pairs: per-pair VALU dots; "
                          "gather: per-event θ/φ row gathers (tiles/pairs + 4-B per-event pair gathers)")
     ap.add_argument("--events-per-gpu", type=int, default=2_000_000, help="dns/proxy events per GPU")

@@ -87,11 +87,14 @@ def main() -> int:
                 if stage == 0:
                     ops.gibbs_pass(m._state(False), m.G, m.KP, m.K, m.alpha, m.cfg.seed, False, m.sweep_ctr,
                                    c.chunk_len, mode=md, prefetch_q=m.qpf,
-                                   chg_mask=getattr(m, "chg_mask", None), wpos=c.wpos, z_w=getattr(m, "z_w", None))
+                                   chg_mask=m.wbits if md == 4 else getattr(m, "chg_mask", None), wpos=c.wpos,
+                                   z_w=getattr(m, "z_w", None), zz_w=getattr(m, "zz_w", None))
                 elif stage == 1 and md == 0:
                     ops.recount(c.wsorted, c.wslot, m.tok_z, head, m.KS)
                 elif stage == 1 and md == 3:
                     ops.recount(c.wsorted, None, m.z_w, head, m.KS)
+                elif stage == 1 and md == 4:
+                    ops.wdelta_recount(m.wbits, c.wsorted, m.zz_w, head, m.KS)
                 elif stage == 1 and md == 2:
                     ops.delta_recount(c.wslot, c.tile_wlo, c.tile_whi, m.chg_mask, c.tok_word, m.tok_z, m.tok_zprev,
                                       head, m.KS, m.G)

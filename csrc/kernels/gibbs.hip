@@ -40,8 +40,8 @@ struct OniGibbs {
   const uint32_t* sweep_ctr;   // device scalar: current sweep number (≥ 1), graph-replay safe
   uint64_t* chg_mask;          // MODE 2: one u64 per SELL step, bit c*G set if slot c's topic changed
   const int32_t* wpos;         // MODE 3: word-sorted position of every SELL slot
-  uint8_t* z_w;                // MODE 3/4: topic array in word-sorted order (kept in sync for changed tokens)
-  uint8_t* zo_w;               // MODE 4: previous topic of each changed token, word-sorted order
+  uint8_t* z_w;                // MODE 3: topic array in word-sorted order (kept in sync for changed tokens)
+  uint16_t* zz_w;              // MODE 4: (old | new << 8) topics of each changed token, word-sorted order
                                // (MODE 4 reuses chg_mask as a u32 bitmap over word-sorted positions)
   int32_t* chg_count;          // optional: += number of tokens whose topic changed (drives the auto mode)
   int64_t n_slices;
@@ -126,8 +126,7 @@ __device__ __forceinline__ void flush_multi_rows(int32_t* __restrict__ ndk_dst, 
 // of a word-sorted bitmap; k_wdelta_recount then visits only set bits, reading contiguous
 // word ids and topic pairs (no per-token slot indirection, no z_prev array).
 __device__ __forceinline__ void mark_changed_w(const OniGibbs& a, int32_t p, int zo, int zn) {
-  a.z_w[p] = (uint8_t)zn;
-  a.zo_w[p] = (uint8_t)zo;
+  a.zz_w[p] = (uint16_t)(zo | (zn << 8));  // one 2-B store: only read where the bit below is set
   atomicOr(reinterpret_cast<uint32_t*>(a.chg_mask) + (p >> 5), 1u << (p & 31));
 }
 
@@ -967,7 +966,7 @@ __global__ __launch_bounds__(256) void k_recount_reg(const int32_t* __restrict__
 
 // Word-bitmap delta recount (MODE 4). A block owns 256 bitmap words = 8192 word-sorted token
 // positions; each thread reads one 32-bit word (coalesced 1 KB per block), clears it, and for
-// each set bit reads the position's word id (wsorted) and its (old, new) topics (zo_w, z_w) --
+// each set bit reads the position's word id (wsorted) and its (old, new) topic pair (zz_w) --
 // all contiguous arrays in word-sorted order, touched only where a token changed. Deltas go to
 // an LDS table over the block's word span (rows capped at wmax; wider spans go straight to
 // global atomics) and are flushed one row-contiguous atomic per non-zero cell. Cost ∝ changed
@@ -976,8 +975,7 @@ constexpr int kWBitsPerBlock = 256 * 32;
 
 __global__ __launch_bounds__(256) void k_wdelta_recount(uint32_t* __restrict__ wbits,
                                                          const int32_t* __restrict__ wsorted,
-                                                         const uint8_t* __restrict__ z_w,
-                                                         const uint8_t* __restrict__ zo_w, int64_t T,
+                                                         const uint16_t* __restrict__ zz_w, int64_t T,
                                                          int32_t* __restrict__ dnwk, int KS, int wmax) {
   extern __shared__ __attribute__((aligned(16))) int32_t hst[];
   const int64_t lo = (int64_t)blockIdx.x * kWBitsPerBlock;
@@ -999,7 +997,8 @@ __global__ __launch_bounds__(256) void k_wdelta_recount(uint32_t* __restrict__ w
     m &= m - 1u;
     const int64_t i = word * 32 + b;
     const int w = wsorted[i];
-    const int zn = z_w[i], zo = zo_w[i];
+    const uint32_t zz = zz_w[i];
+    const int zo = (int)(zz & 0xFFu), zn = (int)(zz >> 8);
     const int r = w - w_lo;
     if (r < rows) {
       atomicAdd(&hst[r * KS + zn], 1);
@@ -1018,12 +1017,12 @@ __global__ __launch_bounds__(256) void k_wdelta_recount(uint32_t* __restrict__ w
 
 }  // namespace
 
-ONI_API int oni_wdelta_recount(uint32_t* wbits, const int32_t* wsorted, const uint8_t* z_w, const uint8_t* zo_w,
-                               int64_t T, int32_t* dnwk, int KS, int wmax, hipStream_t s) {
+ONI_API int oni_wdelta_recount(uint32_t* wbits, const int32_t* wsorted, const uint16_t* zz_w, int64_t T,
+                               int32_t* dnwk, int KS, int wmax, hipStream_t s) {
   if (T == 0) return 0;
   if (wmax < 1 || KS < 1 || (size_t)wmax * KS * 4 > 64 * 1024) return (int)hipErrorInvalidValue;
   const unsigned grid = (unsigned)((T + kWBitsPerBlock - 1) / kWBitsPerBlock);
-  k_wdelta_recount<<<grid, 256, (size_t)wmax * KS * 4, s>>>(wbits, wsorted, z_w, zo_w, T, dnwk, KS, wmax);
+  k_wdelta_recount<<<grid, 256, (size_t)wmax * KS * 4, s>>>(wbits, wsorted, zz_w, T, dnwk, KS, wmax);
   return (int)hipGetLastError();
 }
 
@@ -1049,7 +1048,7 @@ ONI_API int oni_gibbs_launch(const OniGibbs* a, int G, int KP, int init, int mod
   if (a->K < 1 || a->K > 255 || a->K > a->KS || mode < 0 || mode > 4) return (int)hipErrorInvalidValue;
   if (mode == 2 && !a->chg_mask) return (int)hipErrorInvalidValue;
   if (mode == 3 && (!a->wpos || !a->z_w)) return (int)hipErrorInvalidValue;
-  if (mode == 4 && (!a->wpos || !a->z_w || !a->zo_w || !a->chg_mask)) return (int)hipErrorInvalidValue;
+  if (mode == 4 && (!a->wpos || !a->zz_w || !a->chg_mask)) return (int)hipErrorInvalidValue;
 #define ONI_CASE(g_, kp_) \
   if (G == g_ && KP == kp_) return launch_gibbs<g_, kp_>(*a, init != 0, mode, qpf, s);
   ONI_CASE(1, 4) ONI_CASE(1, 8) ONI_CASE(1, 12) ONI_CASE(1, 16) ONI_CASE(1, 20) ONI_CASE(1, 24) ONI_CASE(1, 28)

@@ -43,9 +43,26 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void k_tile_score(
   const int kq = lane >> 4;  // k offset inside a 4-deep step
   const int64_t wave_global = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   const int64_t n_waves = (int64_t)gridDim.x * kWavesPerBlock;
+  // the next item's row indices and pair range are fetched one item ahead, so each item waits on
+  // one memory round trip (its θ/φ rows) instead of three (indices → rows, range → pair bytes)
+  int32_t d_nx = -1, w_nx = -1;
+  int64_t p_nx0 = 0, p_nx1 = 0;
+  if (wave_global < n_items) {
+    d_nx = item_docs[wave_global * kItemRows + r];
+    w_nx = item_words[wave_global * kItemRows + r];
+    p_nx0 = item_p0[wave_global];
+    p_nx1 = item_p0[wave_global + 1];
+  }
   for (int64_t it = wave_global; it < n_items; it += n_waves) {
-    const int32_t d = item_docs[it * kItemRows + r];
-    const int32_t w = item_words[it * kItemRows + r];
+    const int32_t d = d_nx, w = w_nx;
+    const int64_t p0 = p_nx0, np = p_nx1 - p_nx0;
+    const int64_t nx = it + n_waves;
+    if (nx < n_items) {
+      d_nx = item_docs[nx * kItemRows + r];
+      w_nx = item_words[nx * kItemRows + r];
+      p_nx0 = item_p0[nx];
+      p_nx1 = item_p0[nx + 1];
+    }
     // empty rows/columns read row 0 and multiply by a zero operand: keeps loads unconditional
     const float* ta = theta + (int64_t)(d < 0 ? 0 : d) * ks + kq;
     const float* pb = phi + (int64_t)(w < 0 ? 0 : w) * ks + kq;
@@ -66,8 +83,6 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void k_tile_score(
         acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ta[4 * s] * ma, pb[4 * s] * mb, acc, 0, 0, 0);
     }
     // C[row][col] lives in lane (row >> 2) * 16 + col, register row & 3
-    const int64_t p0 = item_p0[it];
-    const int64_t np = item_p0[it + 1] - p0;
     for (int64_t base = 0; base < np; base += 64) {
       const bool ok = base + lane < np;
       const uint32_t rc = ok ? pair_rc[p0 + base + lane] : 0u;

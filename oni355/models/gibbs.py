@@ -51,7 +51,11 @@ class GibbsConfig:
     # topic in a sweep falls below auto_threshold (measured on device, read two sweeps late so the
     # host never stalls the stream); auto_switch > 0 instead fixes the first delta sweep (tests)
     auto_switch: int = 0
-    auto_threshold: float = 0.08
+    # 0.12: the wdelta sweep beats the full recount below ~12-15 % changed tokens (bench A/B on the
+    # 12.5M-flow day: 0.08 → 0.309, 0.12 → 0.304, 0.16 → 0.307 ms/sweep over sweeps 11-60)
+    auto_threshold: float = field(default_factory=lambda: float(os.environ.get("ONI_AUTO_THRESHOLD", "0.12")))
+    # the delta bookkeeping auto mode switches to: "wdelta" (word-sorted change bitmap) | "delta"
+    auto_delta: str = field(default_factory=lambda: os.environ.get("ONI_AUTO_DELTA", "wdelta"))
     # debug: verify count invariants after every sweep() call (ONI_CHECK_INVARIANTS=1)
     check_invariants: bool = field(default_factory=lambda: os.environ.get("ONI_CHECK_INVARIANTS", "0") == "1")
     # sweep kernel: "auto" (default: "qpf" for K ≤ 32, "plain" above — the measured winners),
@@ -97,19 +101,25 @@ class GibbsLDA:
         if cfg.count_mode not in ("auto", "dual", "delta", "recount", "atomic", "wdelta"):
             raise ValueError(f"unknown count_mode {cfg.count_mode}")
         self.auto = cfg.count_mode == "auto"
-        self.mode = {"recount": 0, "atomic": 1, "delta": 2, "dual": 3, "wdelta": 4, "auto": 2}[cfg.count_mode]
-        self._zprev_synced = False
+        # auto: full recount while most topics still move, then the delta mode named by auto_delta
+        auto_delta = {"wdelta": 4, "delta": 2}[cfg.auto_delta]
+        if cfg.sampler == "lds":
+            auto_delta = 2  # the LDS-count sampler implements the slot-mask delta bookkeeping only
+        self.mode = {"recount": 0, "atomic": 1, "delta": 2, "dual": 3, "wdelta": 4, "auto": auto_delta}[cfg.count_mode]
+        # the auxiliary topic state of self.mode (z_prev for 2, word-sorted z_w for 4) matches tok_z
+        self._aux_synced = False
         self._delta_on = False
         self._force_mode = None
         self._chg_q: list = []    # (sweep index, host buffer, event) of pending change-count copies
         self.T_global = corpus.T
         self.change_log: list[tuple[int, float]] = []
-        if self.mode in (3, 4):
+        if self.mode == 3:
             self.z_w = torch.zeros(max(corpus.T, 1), dtype=torch.uint8, device=dev)
         if self.mode == 4:
-            # word-sorted change bitmap (+ slack word) and the previous topic of each changed token
+            # word-sorted change bitmap (+ slack word) and (old | new << 8) of each changed token;
+            # zz_w is only read where a bit is set, so it never needs a sync with tok_z
             self.wbits = torch.zeros((corpus.T + 31) // 32 + 1, dtype=torch.int32, device=dev)
-            self.zo_w = torch.zeros(max(corpus.T, 1), dtype=torch.uint8, device=dev)
+            self.zz_w = torch.zeros(max(corpus.T, 1), dtype=torch.int16, device=dev)
         if self.mode == 2:
             self.tok_zprev = torch.zeros_like(self.tok_z)
             self.chg_mask = torch.zeros(max(corpus.sell_slots // corpus.S, 1), dtype=torch.int64, device=dev)
@@ -175,8 +185,8 @@ class GibbsLDA:
             return self._force_mode
         if self.auto:
             if self.cfg.auto_switch > 0:
-                return 0 if sweep < self.cfg.auto_switch else 2
-            return 2 if self._delta_on else 0
+                return 0 if sweep < self.cfg.auto_switch else self.mode
+            return self.mode if self._delta_on else 0
         return self.mode
 
     def _note_changes(self) -> None:
@@ -213,11 +223,15 @@ class GibbsLDA:
         """Bring the auxiliary topic copies (z_prev / word-sorted z) in line with tok_z."""
         if self.mode == 2:
             self.tok_zprev.copy_(self.tok_z)
-            self._zprev_synced = True
-        elif self.mode in (3, 4) and self.c.T:
+        elif self.mode == 3 and self.c.T:
             self.z_w[: self.c.T] = self.tok_z[self.c.wslot.long()]
-            if self.mode == 4:
-                self.wbits.zero_()
+        elif self.mode == 4:
+            self.wbits.zero_()
+        self._aux_synced = True
+
+    def _keeps_aux(self, mode: int) -> bool:
+        """Does a sweep in count mode ``mode`` leave self.mode's auxiliary topic state in sync?"""
+        return mode == self.mode or self.mode == 4  # MODE 4's bitmap is empty between sweeps
 
     def _prime(self) -> None:
         # zero-delta apply: q from n_wk, nk[1] = nk[0]; leaves dn[0], dn[1] zero
@@ -233,19 +247,19 @@ class GibbsLDA:
     def _one_sweep(self) -> None:
         c = self.c
         mode = self._sweep_mode(self.sweeps_done + 1)
-        if mode == 2 and not self._zprev_synced:
-            self.tok_zprev.copy_(self.tok_z)  # entering delta mode: z_prev := z (eager, outside graphs)
-        self._zprev_synced = mode == 2
+        if mode == self.mode and mode in (2, 4) and not self._aux_synced:
+            self._sync_aux_z()  # entering a delta mode: z_prev / z_w := z (eager, outside graphs)
+        self._aux_synced = self._keeps_aux(mode)
         ops.copy_rows(self.ndk[self.a], self.ndk[1 - self.a], c.long_rows, self.KS)
         ops.gibbs_pass(self._state(False), self.G, self.KP, self.K, self.alpha, self.cfg.seed, False,
                        self.sweep_ctr, c.chunk_len, host_sweep=self.sweeps_done + 1, mode=mode,
                        prefetch_q=self.qpf,
                        chg_mask=self.wbits if mode == 4 else getattr(self, "chg_mask", None), wpos=c.wpos,
-                       z_w=getattr(self, "z_w", None), zo_w=getattr(self, "zo_w", None))
+                       z_w=getattr(self, "z_w", None), zz_w=getattr(self, "zz_w", None))
         head = self.dn[self.b][: self.V * self.KS].view(self.V, self.KS)
         if mode == 4:
             # dn[b] head := Δn_wk of the tokens marked in the word-sorted change bitmap
-            ops.wdelta_recount(self.wbits, c.wsorted, self.z_w, self.zo_w, head, self.KS)
+            ops.wdelta_recount(self.wbits, c.wsorted, self.zz_w, head, self.KS)
         elif mode == 0:
             # dn[b] head := this rank's n_wk rebuilt from z (tail keeps Δn_k)
             ops.recount(c.wsorted, c.wslot, self.tok_z, head, self.KS)
@@ -273,10 +287,10 @@ class GibbsLDA:
 
     def _capture(self, mode: int):
         """Capture two sweeps of count mode ``mode`` (parities return to their start) into one HIP graph."""
-        saved = (self.a, self.b, self.cn, self.sweeps_done, self._zprev_synced)
+        saved = (self.a, self.b, self.cn, self.sweeps_done, self._aux_synced)
         self._force_mode = mode
-        if mode == 2:
-            self._zprev_synced = True  # the eager z_prev sync happens before the first replay
+        if mode == self.mode:
+            self._aux_synced = True  # the eager aux sync happens before the first replay
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         g = torch.cuda.CUDAGraph()
@@ -286,7 +300,7 @@ class GibbsLDA:
                 self._one_sweep()
                 self._one_sweep()
         torch.cuda.current_stream(self.device).wait_stream(s)
-        self.a, self.b, self.cn, self.sweeps_done, self._zprev_synced = saved
+        self.a, self.b, self.cn, self.sweeps_done, self._aux_synced = saved
         self._force_mode = None
         entry = (g, (self.a, self.b, self.cn))
         self._graphs[mode] = entry
@@ -335,9 +349,8 @@ class GibbsLDA:
                 self._note_changes()
                 done += 1
                 continue
-            if m1 == 2 and not self._zprev_synced:
-                self.tok_zprev.copy_(self.tok_z)
-                self._zprev_synced = True
+            if m1 == self.mode and m1 in (2, 4) and not self._aux_synced:
+                self._sync_aux_z()
             entry = self._graphs.get(m1)
             if entry is not None and entry[1] != (self.a, self.b, self.cn):
                 self._one_sweep()  # realign parities with the captured pair
@@ -346,12 +359,12 @@ class GibbsLDA:
                 continue
             if entry is None:
                 entry = self._capture(m1)
-                if self.auto and self.cfg.auto_switch == 0 and m1 == 0 and 2 not in self._graphs:
-                    self._capture(2)  # capture the delta pair now: no capture stall at the switch
+                if self.auto and self.cfg.auto_switch == 0 and m1 == 0 and self.mode not in self._graphs:
+                    self._capture(self.mode)  # capture the delta pair now: no capture stall at the switch
             self._graph = entry[0]
             entry[0].replay()
             self.sweeps_done += 2
-            self._zprev_synced = m1 == 2
+            self._aux_synced = self._keeps_aux(m1)
             self._note_changes()
             done += 2
 

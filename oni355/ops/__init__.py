@@ -228,14 +228,14 @@ def sell_perm_z(chunk_doc, chunk_pos0, chunk_len, S, slice_off, doc_tok_ptr, tok
 def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init: bool, sweep_ctr: torch.Tensor,
                chunk_len: torch.Tensor, host_sweep: int | None = None, mode: int = 1,
                prefetch_q: bool | int = False, chg_mask: torch.Tensor | None = None, wpos: torch.Tensor | None = None,
-               z_w: torch.Tensor | None = None, zo_w: torch.Tensor | None = None) -> None:
+               z_w: torch.Tensor | None = None, zz_w: torch.Tensor | None = None) -> None:
     """Launch one init/sweep pass. ``st`` holds the OniGibbs tensors (see csrc/kernels/gibbs.hip).
 
     ``mode`` 1: accumulate Δn_wk with per-token atomics; 0: the caller rebuilds n_wk with
     :func:`recount`; 2: record changed slots in ``chg_mask`` for :func:`delta_recount`; 3: also
     write changed topics into the word-sorted copy ``z_w`` (via ``wpos``) for a streaming recount;
     4: changed tokens set their word-sorted bit in ``chg_mask`` (int32 bitmap) and record
-    (old, new) topics in ``zo_w`` / ``z_w`` for :func:`wdelta_recount`.
+    old | new << 8 in ``zz_w`` (int16, word-sorted) for :func:`wdelta_recount`.
     ``prefetch_q`` 1: register sampler with next-q-row prefetch; 2: LDS-staged doc counts (G=1).
     """
     atomic = mode == 1
@@ -245,10 +245,10 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
     if nk_rep < 1 or nk_rep * KS != st["dnk"].numel() or nk_rep & (nk_rep - 1):
         raise ValueError("dnk must hold a power-of-two number of [KS] replicas")
     if mode == 4:
-        T = int(z_w.numel()) if z_w is not None else 0
-        if (wpos is None or z_w is None or zo_w is None or chg_mask is None or wpos.numel() != st["tok_word"].numel()
-                or zo_w.numel() < T or chg_mask.dtype != torch.int32 or chg_mask.numel() * 32 < T):
-            raise ValueError("wdelta mode needs wpos [SELL slots], z_w/zo_w [T] and an int32 bitmap of T bits")
+        T = int(zz_w.numel()) if zz_w is not None else 0
+        if (wpos is None or zz_w is None or chg_mask is None or wpos.numel() != st["tok_word"].numel()
+                or zz_w.dtype != torch.int16 or chg_mask.dtype != torch.int32 or chg_mask.numel() * 32 < T):
+            raise ValueError("wdelta mode needs wpos [SELL slots], int16 zz_w [T] and an int32 bitmap of T bits")
     if not _is_dev(st["tok_word"]):
         chg = st.get("chg_count")
         z_before = st["tok_z"].clone() if (chg is not None or mode == 4) else None
@@ -266,8 +266,7 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
         if mode == 4:
             ch = st["tok_z"] != z_before
             p = wpos[ch].long()
-            z_w[p] = st["tok_z"][ch]
-            zo_w[p] = z_before[ch]
+            zz_w[p] = (z_before[ch].to(torch.int32) | (st["tok_z"][ch].to(torch.int32) << 8)).to(torch.int16)
             upd = np.zeros(chg_mask.numel(), dtype=np.uint32)
             np.bitwise_or.at(upd, (p >> 5).numpy(), (np.uint32(1) << (p & 31).numpy().astype(np.uint32)))
             chg_mask |= torch.from_numpy(upd.view(np.int32))
@@ -293,7 +292,7 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
             raise ValueError("dual mode needs wpos [SELL slots] and z_w [T]")
         a.wpos, a.z_w = _lib.ptr(wpos), _lib.ptr(z_w)
     if mode == 4:
-        a.wpos, a.z_w, a.zo_w, a.chg_mask = _lib.ptr(wpos), _lib.ptr(z_w), _lib.ptr(zo_w), _lib.ptr(chg_mask)
+        a.wpos, a.zz_w, a.chg_mask = _lib.ptr(wpos), _lib.ptr(zz_w), _lib.ptr(chg_mask)
     if st.get("chg_count") is not None:
         a.chg_count = _lib.ptr(st["chg_count"])
     a.n_slices, a.K, a.KS, a.alpha, a.seed0, a.seed1 = n_slices, K, KS, float(alpha), s0, s1
@@ -326,9 +325,9 @@ def delta_recount(wslot, tile_wlo, tile_whi, chg_mask, tok_word, tok_z, tok_zpre
                "oni_delta_recount")
 
 
-def wdelta_recount(wbits, wsorted, z_w, zo_w, dnwk_out, KS: int) -> None:
-    """Δn_wk of the tokens marked in the word-sorted bitmap ``wbits`` (+1 at (w, z_w), -1 at
-    (w, zo_w)); clears the bitmap (k_wdelta_recount)."""
+def wdelta_recount(wbits, wsorted, zz_w, dnwk_out, KS: int) -> None:
+    """Δn_wk of the tokens marked in the word-sorted bitmap ``wbits`` (+1 at (w, new), -1 at
+    (w, old) with zz_w = old | new << 8); clears the bitmap (k_wdelta_recount)."""
     T = wsorted.numel()
     if T == 0:
         return
@@ -338,12 +337,13 @@ def wdelta_recount(wbits, wsorted, z_w, zo_w, dnwk_out, KS: int) -> None:
         pt = torch.from_numpy(pos)
         w = wsorted[pt].long()
         one = torch.ones(pos.size, dtype=torch.int32)
-        dnwk_out.view(-1).index_add_(0, w * KS + z_w[pt].long(), one)
-        dnwk_out.view(-1).index_add_(0, w * KS + zo_w[pt].long(), -one)
+        zz = zz_w[pt].to(torch.int64) & 0xFFFF
+        dnwk_out.view(-1).index_add_(0, w * KS + (zz >> 8), one)
+        dnwk_out.view(-1).index_add_(0, w * KS + (zz & 0xFF), -one)
         wbits.zero_()
         return
     wmax = max(1, RECOUNT_CELLS // KS)
-    _lib.check(_lib.lib().oni_wdelta_recount(*map(_lib.ptr, (wbits, wsorted, z_w, zo_w)), T, _lib.ptr(dnwk_out), KS,
+    _lib.check(_lib.lib().oni_wdelta_recount(*map(_lib.ptr, (wbits, wsorted, zz_w)), T, _lib.ptr(dnwk_out), KS,
                                              wmax, _lib.stream()), "oni_wdelta_recount")
 
 

@@ -32,7 +32,7 @@ class OniGibbs(C.Structure):
         ("tok_word", vp), ("tok_z", vp), ("slice_off", vp), ("slice_len", vp),
         ("chunk_doc", vp), ("chunk_pos0", vp), ("chunk_key", vp), ("chunk_multi", vp),
         ("ndk_src", vp), ("ndk_dst", vp), ("q", vp), ("dnwk", vp), ("dnk", vp), ("sweep_ctr", vp), ("chg_mask", vp),
-        ("wpos", vp), ("z_w", vp), ("zo_w", vp), ("chg_count", vp),
+        ("wpos", vp), ("z_w", vp), ("zz_w", vp), ("chg_count", vp),
         ("n_slices", i64), ("K", i32), ("KS", i32), ("alpha", f32), ("seed0", u32), ("seed1", u32),
         ("nk_rep", i32), ("pad_", i32),
     ]
@@ -59,7 +59,7 @@ _SIGS = {
     "oni_pair_score": [vp, vp, C.c_int, vp, vp, i64, vp, vp],
     "oni_event_min": [vp, vp, vp, i64, f32, vp, vp, vp, vp, vp],
     "oni_tile_score": [vp, vp, C.c_int, vp, vp, vp, vp, i64, vp, vp],
-    "oni_wdelta_recount": [vp, vp, vp, vp, i64, vp, C.c_int, C.c_int, vp],
+    "oni_wdelta_recount": [vp, vp, vp, i64, vp, C.c_int, C.c_int, vp],
 }
 # optional symbols (added by later kernel files); bound when present
 _OPTIONAL_SIGS: dict[str, list] = {}

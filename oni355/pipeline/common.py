@@ -279,7 +279,9 @@ def _excl_cumsum(x: torch.Tensor) -> torch.Tensor:
     return out
 
 
-SCORE_TILES = True  # MFMA block scoring by default (see bench.py --score-path; profiles/ A/B)
+# MFMA block scoring is kept as an option: at K = 20 and the flow day's 12 % block density the
+# VALU pair dot measured 39 µs vs 74 µs for k_tile_score (profiles/r1_pmc_score_mfma_vs_valu.json)
+SCORE_TILES = False
 
 
 @traced("oni:score_plan")

@@ -1,0 +1,61 @@
+"""bench.py contract on CPU (gloo): one JSON line from rank 0 with the BASELINE metric/config keys,
+for world size 1 and for a 2-rank torch.distributed.run launch (the driver's N>1 command shape)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = ["--steps", "2", "--warmup", "1", "--flows-per-gpu", "3000", "--device", "cpu"]
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(cmd):
+    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONUNBUFFERED="1")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def _check(out, n):
+    with open(os.path.join(ROOT, "BASELINE.json")) as f:
+        base = json.load(f)
+    assert out["metric"] == base["metric"]
+    assert out["n_gpus"] == n and out["steps"] == 2 and out["warmup"] == 1
+    assert out["value"] > 0 and out["ms_per_step"] > 0 and out["higher_is_better"] is True
+    assert out["scaling"] == "weak" and out["config"]["parallelism"] == f"dp{n}"
+    assert out["config"]["global_batch"] == 3000 * n
+    assert out["score_path"] == "pairs" and out["score_mfma_items"] > 0 and "tiles" in out["score_ms_other_paths"]
+
+
+def test_bench_single_process():
+    _check(_run([sys.executable, "bench.py", *ARGS]), 1)
+
+
+@pytest.mark.slow
+def test_bench_two_ranks_torchrun():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", "bench.py", "--gpus", "2", *ARGS]
+    _check(_run(cmd), 2)
+
+
+def test_allreduce_bench_gloo_two_ranks():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", "bench/allreduce.py", "--device", "cpu",
+           "--min-kb", "64", "--max-mb", "1", "--iters", "2", "--warmup", "1"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rows = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert [x["bytes"] for x in rows] == [65536, 262144, 1048576]
+    assert all(x["ok"] and x["ranks"] == 2 and x["busbw_GBps"] > 0 for x in rows)
