@@ -8,7 +8,7 @@ DATE=20160708
 DEV="${ONI_DEVICE:-$(python -c 'import torch;print("cuda" if torch.cuda.is_available() else "cpu")')}"
 rm -rf "$WORK"; mkdir -p "$WORK/collector/flow" "$WORK/collector/dns" "$WORK/collector/proxy"
 cd "$ROOT"
-python tools/build.py >/dev/null
+[ -f oni355/_lib/liboni_hip.so ] && [ -f oni355/_lib/liboni_native.so ] || python tools/build.py >/dev/null
 python - "$WORK" <<'PY'
 import sys
 from oni355.synth.flow import generate_flows
