@@ -79,3 +79,25 @@ def test_collector_to_store_to_ml(tmp_path):
     assert ml.main(["20160708", "flow", "1.0", "20", "--data-root", root, "--device", "cpu", "--sweeps", "3",
                     "--lpath", lp, "--quiet"]) == 0
     assert os.path.exists(os.path.join(lp, "flow", "20160708", "flow_results.csv"))
+
+
+@pytest.mark.parametrize("fmt", ["oni", "nfdump"])
+def test_oni_nfdump_cli_csv_matches_reader(tmp_path, fmt):
+    """oni-nfdump (C++ nfcapd → CSV formatter) output parses back to the same flow columns."""
+    import subprocess
+
+    from oni355.io.decoders import read_flow_csv
+    exe = os.path.join(os.path.dirname(nfcapd.__file__), "..", "_lib", "bin", "oni-nfdump")
+    day = generate_flows(3000, seed=6)
+    p1, p2 = str(tmp_path / "nfcapd.a"), str(tmp_path / "nfcapd.b")
+    nfcapd.write_nfcapd(p1, {k: v[:1700] for k, v in day.cols.items()}, "lzo", per_block=500)
+    nfcapd.write_nfcapd(p2, {k: v[1700:] for k, v in day.cols.items()}, "lz4")
+    out = str(tmp_path / "flows.csv")
+    r = subprocess.run([exe, "-r", p1, "-r", p2, "-o", fmt, "-w", out], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    cols, bad = read_flow_csv(out)
+    assert bad == 0
+    for k in KEYS:
+        assert np.array_equal(np.asarray(cols[k]), np.asarray(day.cols[k])), k
+    bad_r = subprocess.run([exe, "-r", str(tmp_path / "missing")], capture_output=True, text=True)
+    assert bad_r.returncode == 1 and "cannot open" in bad_r.stderr
