@@ -56,8 +56,7 @@ def main(argv=None) -> int:
     import torch
 
     from oni355.parallel import comm as pc
-    from oni355.pipeline import common, flow
-    from oni355.synth.flow import generate_flows
+    from oni355.pipeline import common
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus:
@@ -76,42 +75,12 @@ def main(argv=None) -> int:
 
     t_setup = time.perf_counter()
     from oni355 import ops
-    if a.source == "flow":
-        # hosts scale with the node-wide day so N=8 is one 100M-flow day split over 8 ranks
-        per = a.flows_per_gpu
-        n_total = per * world
-        day = generate_flows(per, seed=a.seed, rank=rank, n_hosts=max(64, n_total // 25))
-        d = flow.to_device(day.cols, dev)
-        cuts = flow.compute_cuts(d, comm)
-        sw, dw = flow.wordify(d, cuts)
-        doc_keys = torch.cat([common.u32_to_i64(d["sip"]), common.u32_to_i64(d["dip"])])
-        word_keys = torch.cat([common.u32_to_i64(sw), common.u32_to_i64(dw)])
-        sides = [(common.u32_to_i64(d["sip"]), common.u32_to_i64(sw)), (common.u32_to_i64(d["dip"]), common.u32_to_i64(dw))]
-        K = a.topics
-    else:
-        per = a.events_per_gpu
-        n_total = per * world
-        if a.source == "dns":
-            from oni355.pipeline import dns as src
-            from oni355.synth.dns import generate_dns
-            day = generate_dns(per, seed=a.seed, rank=rank, n_clients=max(32, n_total // 40))
-            d = src.to_device(day.cols, dev)
-            words, _, _ = src.featurize(d, comm, src.top_set(day.top_domains), "intel")
-            doc_keys = common.u32_to_i64(d["ip_dst"])
-        else:
-            from oni355.pipeline import proxy as src
-            from oni355.synth.proxy import generate_proxy
-            day = generate_proxy(per, seed=a.seed, rank=rank, n_clients=max(32, n_total // 40))
-            from oni355.pipeline.dns import top_set
-            from oni355.synth.dns import top_domain_list
-            words, _ = src.featurize(day.cols, dev, comm, top_set(top_domain_list()))
-            doc_keys = torch.from_numpy(np.asarray(day.cols["clientip"], np.uint32).astype(np.int64)).to(dev)
-        word_keys = words.to(torch.int64)
-        sides = [(doc_keys, word_keys)]
-        K = a.topics if a.topics_set else 50
-    vocab = common.global_vocab(word_keys, comm)
-    run = common.build_and_train(doc_keys, word_keys, None, vocab, K, None, 0.01, 0x0D15EA5E, 0,
-                                 a.chunk_len, comm, train=False)
+    from oni355.pipeline.synthetic import build_source
+    # flows: hosts scale with the node-wide day so N=8 is one 100M-flow day split over 8 ranks
+    per = a.flows_per_gpu if a.source == "flow" else a.events_per_gpu
+    K = a.topics if (a.source == "flow" or a.topics_set) else 50
+    su = build_source(a.source, per, K, comm, seed=a.seed, chunk_len=a.chunk_len)
+    n_total, day, sides, vocab, run = su.n_total, su.day, su.sides, su.vocab, su.run
     model = run.model
     model.initialize()
     sync()

@@ -1,0 +1,123 @@
+#!/usr/bin/env python3
+"""Config 5 of BASELINE.json: combined flow + DNS + proxy day, one LDA model per source
+(as ml_ops.sh runs one model per data source), K = 100 by default, data parallel over the node.
+
+One timed *step* = one full Gibbs sweep of each of the three models (all three resident in HBM);
+``value`` = all events of the node-wide day × steps / s. Also reports per-model ms/sweep, the
+measured HBM peak next to the sizing model (oni355.utils.sizing) and that model's projection for
+the named 1B-event / 8-GPU configuration.
+
+  python bench/combined.py                                   # 1 GPU, 12.5M flows + 6.25M DNS + 6.25M proxy
+  python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 bench/combined.py \
+      --flows-per-gpu 62500000 --dns-per-gpu 31250000 --proxy-per-gpu 31250000   # the 1B-event day
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--flows-per-gpu", type=int, default=12_500_000)
+    ap.add_argument("--dns-per-gpu", type=int, default=6_250_000)
+    ap.add_argument("--proxy-per-gpu", type=int, default=6_250_000)
+    ap.add_argument("--topics", type=int, default=100)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--device", default="cuda")
+    a = ap.parse_args(argv)
+    import torch
+
+    from oni355.parallel import comm as pc
+    from oni355.pipeline.synthetic import build_source
+    from oni355.utils import sizing
+
+    comm = pc.init_from_env(a.device)
+    dev = comm.device
+    cuda = dev.type == "cuda"
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize(dev)
+
+    t0 = time.perf_counter()
+    # heartbeat on stderr: generating a 100M-event shard takes minutes with no other output
+    import threading
+    done = threading.Event()
+
+    def beat():
+        while not done.wait(30.0):
+            print(f"[combined] rank {comm.rank}: {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+    threading.Thread(target=beat, daemon=True).start()
+    sources = []
+    for src, per in (("flow", a.flows_per_gpu), ("dns", a.dns_per_gpu), ("proxy", a.proxy_per_gpu)):
+        if per <= 0:
+            continue
+        su = build_source(src, per, a.topics, comm, seed=a.seed)
+        su.model.initialize()
+        sources.append(su)
+        su.day = None  # host columns are no longer needed
+        print(f"[combined] {src}: {per} events/rank ready at {time.perf_counter() - t0:.1f} s", file=sys.stderr,
+              flush=True)
+    sync()
+    setup_s = time.perf_counter() - t0
+    done.set()
+    for su in sources:
+        su.model.sweep(a.warmup)
+    sync()
+    comm.barrier()
+    per_model = {}
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        for su in sources:
+            su.model.sweep(1)
+    sync()
+    comm.barrier()
+    dt = comm.allreduce_scalar(time.perf_counter() - t0, "max")
+    # per-model sweep time, measured separately after the combined loop
+    for su in sources:
+        sync()
+        t1 = time.perf_counter()
+        su.model.sweep(4)
+        sync()
+        per_model[su.source] = round(comm.allreduce_scalar(time.perf_counter() - t1, "max") / 4 * 1e3, 4)
+    events = sum(su.n_total for su in sources)
+    plans = [sizing.plan(su.source, su.per_rank, su.K, su.run.corpus.D, int(su.vocab.numel()),
+                         0 if su.source == "flow" else 48) for su in sources]
+    peak = torch.cuda.max_memory_allocated(dev) if cuda else 0
+    projection = sizing.plan_combined(1_000_000_000, 8, a.topics)
+    out = {
+        "metric": f"combined flow+dns+proxy records/sec (whole node) + Gibbs iters/sec, {a.topics}-topic LDA x3",
+        "value": round(events * a.steps / dt, 1), "unit": "records/s", "n_gpus": comm.world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "dtype": "fp32", "data": "synthetic flow/dns/proxy (oni355.synth)",
+        "config": {"model": "oni-suspicious-connects-combined-lda", "topics": a.topics, "global_batch": events,
+                   "events_per_gpu": {su.source: su.per_rank for su in sources},
+                   "parallelism": f"dp{comm.world}",
+                   "baseline_config": "Combined flow+DNS+proxy 1B events, 100 topics, 8xMI355X (weak-scaled)"},
+        "ms_per_sweep_by_model": per_model,
+        "tokens": {su.source: int(comm.allreduce_scalar(su.run.corpus.T, "sum")) for su in sources},
+        "vocab": {su.source: int(su.vocab.numel()) for su in sources},
+        "hbm_peak_GB_measured": round(peak / 1e9, 3),
+        "hbm_plan_GB": [p.as_dict() for p in plans],
+        "projection_1B_events_8gpu": {"per_gpu_peak_GB": round(sum(p.steady_bytes for p in projection) / 1e9
+                                                               + max(p.peak_bytes - p.steady_bytes
+                                                                     for p in projection) / 1e9, 2),
+                                      "fits_288GB": all(p.fits() for p in projection)},
+        "setup_s": round(setup_s, 2),
+    }
+    if comm.rank == 0:
+        print(json.dumps(out), flush=True)
+    pc.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

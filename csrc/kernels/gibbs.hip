@@ -711,7 +711,7 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_lds(const OniGibbs a) {
 template <int G, int KP>
 int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s) {
   // qpf (sampler variant): 1 = k_gibbs_pp (ping-pong register sampler, default), 0 = k_gibbs with
-  // a q-row load on each word change, 4 = k_gibbs with one-step q prefetch + row copy (G = 1),
+  // a q-row load on each word change, 4 = k_gibbs with one-step q prefetch + row copy,
   // 2 = k_gibbs_lds (LDS-staged counts, fma numerics, G = 1)
   if (a.KS != G * KP || mode < 0 || mode > 4) return (int)hipErrorInvalidValue;
   const unsigned grid = (unsigned)((a.n_slices + kWavesPerBlock - 1) / kWavesPerBlock);
@@ -721,13 +721,8 @@ int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s)
     return (int)hipGetLastError();
   }
   if (mode == 4) {  // word-sorted change bitmap: register samplers only
-    if constexpr (G == 1) {
-      if (qpf == 4) {
-        k_gibbs<1, KP, false, 4, true><<<grid, kBlock, 0, s>>>(a);
-        return (int)hipGetLastError();
-      }
-    }
-    if (qpf == 1) k_gibbs_pp<G, KP, 4><<<grid, kBlock, 0, s>>>(a);
+    if (qpf == 4) k_gibbs<G, KP, false, 4, true><<<grid, kBlock, 0, s>>>(a);
+    else if (qpf == 1) k_gibbs_pp<G, KP, 4><<<grid, kBlock, 0, s>>>(a);
     else if (qpf == 0) k_gibbs<G, KP, false, 4, false><<<grid, kBlock, 0, s>>>(a);
     else return (int)hipErrorInvalidValue;
     return (int)hipGetLastError();
@@ -740,13 +735,13 @@ int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s)
       else k_gibbs_lds<KP, 3><<<grid, kBlock, 0, s>>>(a);
       return (int)hipGetLastError();
     }
-    if (qpf == 4) {
-      if (mode == 0) k_gibbs<1, KP, false, 0, true><<<grid, kBlock, 0, s>>>(a);
-      else if (mode == 1) k_gibbs<1, KP, false, 1, true><<<grid, kBlock, 0, s>>>(a);
-      else if (mode == 2) k_gibbs<1, KP, false, 2, true><<<grid, kBlock, 0, s>>>(a);
-      else k_gibbs<1, KP, false, 3, true><<<grid, kBlock, 0, s>>>(a);
-      return (int)hipGetLastError();
-    }
+  }
+  if (qpf == 4) {  // one-step q-row prefetch (any unit width)
+    if (mode == 0) k_gibbs<G, KP, false, 0, true><<<grid, kBlock, 0, s>>>(a);
+    else if (mode == 1) k_gibbs<G, KP, false, 1, true><<<grid, kBlock, 0, s>>>(a);
+    else if (mode == 2) k_gibbs<G, KP, false, 2, true><<<grid, kBlock, 0, s>>>(a);
+    else k_gibbs<G, KP, false, 3, true><<<grid, kBlock, 0, s>>>(a);
+    return (int)hipGetLastError();
   }
   if (qpf == 1) {
     if (mode == 0) k_gibbs_pp<G, KP, 0><<<grid, kBlock, 0, s>>>(a);

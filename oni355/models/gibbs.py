@@ -127,8 +127,8 @@ class GibbsLDA:
         if cfg.sampler not in SAMPLERS and cfg.sampler != "auto":
             raise ValueError(f"unknown sampler {cfg.sampler}")
         self.qpf = SAMPLERS[cfg.sampler] if cfg.sampler != "auto" else (SAMPLERS["qpf"] if self.G == 1 else 0)
-        if self.qpf in (2, 4) and self.G != 1:
-            self.qpf = 1  # lds / qpf variants exist for one-lane units (K ≤ 32) only
+        if self.qpf == 2 and self.G != 1:
+            self.qpf = 1  # the LDS-count variant exists for one-lane units (K ≤ 32) only
         if self.qpf == 2 and self.mode == 4:
             self.qpf = 4  # the word-bitmap delta mode is implemented by the register samplers
         if self.qpf == 2 and corpus.max_doc_len() >= (1 << 24):

@@ -59,3 +59,17 @@ def test_allreduce_bench_gloo_two_ranks():
     rows = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert [x["bytes"] for x in rows] == [65536, 262144, 1048576]
     assert all(x["ok"] and x["ranks"] == 2 and x["busbw_GBps"] > 0 for x in rows)
+
+
+def test_combined_bench_cpu_and_sizing():
+    from oni355.utils import sizing
+    out = _run([sys.executable, "bench/combined.py", "--device", "cpu", "--flows-per-gpu", "2000", "--dns-per-gpu",
+                "1000", "--proxy-per-gpu", "1000", "--steps", "1", "--warmup", "1", "--topics", "50"])
+    assert out["value"] > 0 and set(out["ms_per_sweep_by_model"]) == {"flow", "dns", "proxy"}
+    assert out["tokens"] == {"flow": 4000, "dns": 1000, "proxy": 1000}
+    assert out["projection_1B_events_8gpu"]["fits_288GB"] is True
+    # the planner grows with every input and flags what cannot fit
+    a = sizing.plan("flow", 10**6, 20, 10**4, 10**4)
+    b = sizing.plan("flow", 2 * 10**6, 20, 10**4, 10**4)
+    assert b.steady_bytes > a.steady_bytes and b.peak_bytes > b.steady_bytes
+    assert not sizing.plan("flow", 20 * 10**9, 100, 10**6, 10**6).fits()

@@ -65,7 +65,8 @@ def _toy_tokens(n_docs, V, seed, heavy=True):
                                     (20, "dual+lds"), (20, "delta+lds"), (20, "atomic+lds"), (7, "dual+lds"),
                                     (32, "dual+lds"), (7, "dual"), (50, "dual"), (50, "delta"), (100, "atomic"),
                                     (100, "dual"), (20, "wdelta"), (20, "wdelta+pp"), (20, "wdelta+plain"),
-                                    (50, "wdelta"), (100, "wdelta")])
+                                    (50, "wdelta"), (100, "wdelta"), (50, "recount+qpf"), (50, "wdelta+qpf"),
+                                    (100, "dual+qpf"), (64, "delta+qpf")])
 def test_gibbs_bitwise_vs_oracle(gpu, K, mode):
     tdoc, tword, keys = _toy_tokens(300, 400, K)
     G, KP = ops.choose_tiling(K)
