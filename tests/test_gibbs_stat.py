@@ -1,0 +1,94 @@
+"""Statistical check of the collapsed-Gibbs engine (SURVEY.md §4.3 "sampler (c)"): on a corpus drawn
+from known topics φ* and doc mixes θ* (random-init Dirichlet priors), the sampler must recover φ*
+(Hungarian matching of topics, mean Jensen-Shannon divergence) and its log-likelihood must rise
+then plateau. The CPU run goes through the NumPy oracle (the kernels' specification); the GPU run
+through the HIP sampler with the production count modes."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+from scipy.optimize import linear_sum_assignment
+
+from oni355 import ops
+from oni355.models.corpus import build_corpus
+from oni355.models.gibbs import GibbsConfig, GibbsLDA
+
+
+def _planted(D=240, V=120, K=6, mean_len=90, seed=0):
+    r = np.random.default_rng(seed)
+    # well-separated sparse topics: each topic concentrates on its own band of words
+    phi = r.dirichlet(np.full(V, 0.05), K)
+    band = V // K
+    for k in range(K):
+        phi[k, k * band:(k + 1) * band] += 4.0 / band
+    phi /= phi.sum(1, keepdims=True)
+    theta = r.dirichlet(np.full(K, 0.2), D)
+    lens = r.integers(mean_len // 2, mean_len * 3 // 2, D)
+    tdoc, tword = [], []
+    for d in range(D):
+        z = r.choice(K, lens[d], p=theta[d])
+        w = np.array([r.choice(V, p=phi[k]) for k in z])
+        tdoc.append(np.full(lens[d], d))
+        tword.append(w)
+    tdoc = np.concatenate(tdoc)
+    tword = np.concatenate(tword)
+    o = np.lexsort((tword, tdoc))  # doc-major, words grouped (the corpus build order)
+    return tdoc[o], tword[o], phi
+
+
+def _js(p, q):
+    m = 0.5 * (p + q)
+
+    def kl(a, b):
+        a = np.clip(a, 1e-12, None)
+        return float((a * np.log(a / np.clip(b, 1e-12, None))).sum())
+    return 0.5 * kl(p, m) + 0.5 * kl(q, m)
+
+
+def _recovery(model, phi_true, K):
+    phi = model.phi().cpu().numpy()[:, :K].T.astype(np.float64)  # (K, V)
+    phi /= phi.sum(1, keepdims=True)
+    cost = np.array([[_js(phi_true[i], phi[j]) for j in range(K)] for i in range(K)])
+    ri, ci = linear_sum_assignment(cost)
+    return float(cost[ri, ci].mean())
+
+
+def _run(device, count_mode, sweeps=60):
+    K = 6
+    tdoc, tword, phi_true = _planted(K=K)
+    D, V = int(tdoc.max()) + 1, 120
+    G, _ = ops.choose_tiling(K)
+    keys = torch.arange(D, dtype=torch.int32) * 13 + 5
+    c = build_corpus(torch.from_numpy(tdoc).to(device), torch.from_numpy(tword).to(device), D, V, keys.to(device),
+                     G, L=64)
+    m = GibbsLDA(c, GibbsConfig(K=K, alpha=0.2, beta=0.05, seed=77, count_mode=count_mode))
+    m.initialize()
+    ll = [m.log_likelihood()]
+    for _ in range(sweeps // 10):
+        m.sweep(10)
+        ll.append(m.log_likelihood())
+    # random-init baseline divergence for scale
+    rnd = np.random.default_rng(1).dirichlet(np.ones(V), K)
+    base = float(np.mean([_js(phi_true[k], rnd[k]) for k in range(K)]))
+    return _recovery(m, phi_true, K), base, ll
+
+
+def _check(js, base, ll):
+    assert js < 0.1 * base, (js, base)
+    assert js < 0.05, js
+    assert ll[-1] > ll[0] + 0.05 * abs(ll[0]), ll           # likelihood rises substantially
+    late = np.abs(np.diff(ll[-3:])).max()
+    assert late < 0.02 * abs(ll[-1]), ll                    # ...then plateaus
+
+
+def test_gibbs_recovers_planted_topics_cpu():
+    js, base, ll = _run(torch.device("cpu"), "atomic")
+    _check(js, base, ll)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("count_mode", ["auto", "recount", "wdelta"])
+def test_gibbs_recovers_planted_topics_gpu(gpu, count_mode):
+    js, base, ll = _run(gpu, count_mode)
+    _check(js, base, ll)
