@@ -55,6 +55,9 @@ def main(argv=None) -> int:
 
     import torch
 
+    from oni355.utils.obs import stack_dumps_from_env
+    stack_dumps_from_env()
+
     from oni355.parallel import comm as pc
     from oni355.pipeline import common
 

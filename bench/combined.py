@@ -35,6 +35,9 @@ def main(argv=None) -> int:
     a = ap.parse_args(argv)
     import torch
 
+    from oni355.utils.obs import stack_dumps_from_env
+    stack_dumps_from_env()
+
     from oni355.parallel import comm as pc
     from oni355.pipeline.synthetic import build_source
     from oni355.utils import sizing
@@ -48,27 +51,20 @@ def main(argv=None) -> int:
             torch.cuda.synchronize(dev)
 
     t0 = time.perf_counter()
-    # heartbeat on stderr: generating a 100M-event shard takes minutes with no other output
-    import threading
-    done = threading.Event()
-
-    def beat():
-        while not done.wait(30.0):
-            print(f"[combined] rank {comm.rank}: {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
-    threading.Thread(target=beat, daemon=True).start()
     sources = []
     for src, per in (("flow", a.flows_per_gpu), ("dns", a.dns_per_gpu), ("proxy", a.proxy_per_gpu)):
         if per <= 0:
             continue
         su = build_source(src, per, a.topics, comm, seed=a.seed)
+        sync()
         su.model.initialize()
+        sync()
         sources.append(su)
         su.day = None  # host columns are no longer needed
         print(f"[combined] {src}: {per} events/rank ready at {time.perf_counter() - t0:.1f} s", file=sys.stderr,
               flush=True)
     sync()
     setup_s = time.perf_counter() - t0
-    done.set()
     for su in sources:
         su.model.sweep(a.warmup)
     sync()

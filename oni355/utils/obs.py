@@ -115,3 +115,17 @@ def traced(name: str):
                 return fn(*a, **kw)
         return wrapper
     return deco
+
+
+def stack_dumps_from_env(var: str = "ONI_STACK_DUMP_S") -> bool:
+    """Hang diagnosis: with ``$ONI_STACK_DUMP_S`` = N, dump every thread's Python stack to stderr
+    every N seconds (faulthandler), so a stalled run names the call it is stuck in."""
+    try:
+        every = float(os.environ.get(var, "0") or 0)
+    except ValueError:
+        every = 0.0
+    if every <= 0:
+        return False
+    import faulthandler
+    faulthandler.dump_traceback_later(every, repeat=True)
+    return True
