@@ -65,8 +65,20 @@ _SIGS = {
 _OPTIONAL_SIGS: dict[str, list] = {}
 
 
+def _bind(h: C.CDLL, name: str, argtypes: list) -> None:
+    fn = getattr(h, name)
+    fn.argtypes = argtypes
+    fn.restype = C.c_int
+
+
 def register_optional(name: str, argtypes: list) -> None:
-    _OPTIONAL_SIGS[name] = argtypes
+    """Declare a launcher's C signature. Binds at once if the library is already loaded: an
+    unbound ctypes function would pass 64-bit device pointers as 32-bit C ints (silently
+    truncated), so a module imported after the first kernel launch must not stay unbound."""
+    with _lock:
+        _OPTIONAL_SIGS[name] = argtypes
+        if _lib is not None and hasattr(_lib, name):
+            _bind(_lib, name, argtypes)
 
 
 def lib() -> C.CDLL:
@@ -83,14 +95,10 @@ def lib() -> C.CDLL:
             )
         h = C.CDLL(HIP_LIB_PATH, mode=C.RTLD_GLOBAL)
         for name, args in _SIGS.items():
-            fn = getattr(h, name)
-            fn.argtypes = args
-            fn.restype = C.c_int
+            _bind(h, name, args)
         for name, args in _OPTIONAL_SIGS.items():
             if hasattr(h, name):
-                fn = getattr(h, name)
-                fn.argtypes = args
-                fn.restype = C.c_int
+                _bind(h, name, args)
         if h.oni_gibbs_sizeof_args() != C.sizeof(OniGibbs):
             raise RuntimeError("OniGibbs ABI mismatch between Python and liboni_hip.so; rebuild")
         _lib = h
