@@ -141,7 +141,9 @@ def generate_dns(n: int, seed: int = 5, n_clients: int | None = None, user_domai
         v = int(v) & 0xFFFFFFFF
         return f"{v >> 24}.{(v >> 16) & 255}.{(v >> 8) & 255}.{v & 255}"
 
-    a_str = [",".join(_ip(int(a) + k) for k in range(c)) for a, c in zip(answer, n_ans)]
+    a_str = [""] * n
+    for i in np.nonzero(n_ans)[0].tolist():
+        a_str[i] = ",".join(_ip(int(answer[i]) + k) for k in range(int(n_ans[i])))
     cols = {
         "frame_time": StringColumn.from_list([""] * n),
         "unix_tstamp": unix.astype(np.int64),

@@ -119,7 +119,10 @@ def traced(name: str):
 
 def stack_dumps_from_env(var: str = "ONI_STACK_DUMP_S") -> bool:
     """Hang diagnosis: with ``$ONI_STACK_DUMP_S`` = N, dump every thread's Python stack to stderr
-    every N seconds (faulthandler), so a stalled run names the call it is stuck in."""
+    every N seconds (faulthandler), so a stalled run names the call it is stuck in.
+
+    Diagnostic runs only: the dump walks the other threads' frames without holding the GIL and
+    can crash a busy interpreter (seen once, mid list-comprehension, after ~6 dumps)."""
     try:
         every = float(os.environ.get(var, "0") or 0)
     except ValueError:

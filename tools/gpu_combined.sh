@@ -2,7 +2,7 @@
 # config 5: combined flow+dns+proxy, K=100 — default shard, then one GPU's share of the 1B-event day
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-export PYTHONUNBUFFERED=1 ONI_STACK_DUMP_S=60
+export PYTHONUNBUFFERED=1
 mkdir -p gpurun_out
 P="gpurun_out/progress.log"
 echo "start $(date)" > "$P"
