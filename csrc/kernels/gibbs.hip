@@ -708,11 +708,222 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_lds(const OniGibbs a) {
   }
 }
 
+// ---- multi-lane units (K > 32) with LDS-staged counts ------------------------------------------
+// k_gibbs<G>1> is VALU-issue bound (measured at K = 100: ≈1250 SIMD cycles per wave step, i.e.
+// ≈250 vector instructions for the 8 tokens a wave samples per step). Per lane and per topic slot
+// it spends ≈11 instructions: a compare/select pair for each of n[zo]-- and n[zn]++ (register
+// rows can only be indexed by select chains), convert + add + mul + add for the weight, and
+// add + compare + select to count the prefix entries below the threshold. Here
+//  * lane (unit c, g) keeps its KP counts as f32 in a private LDS row, so each count update is one
+//    ds_add_f32 by the owning lane (exact integers below 2^24, checked by the host);
+//  * the weights form an fma chain P_j = fma(n_j + α, q_j, P_{j-1}) inside the lane (the spec's
+//    "fma" numerics, oni355/ref/spec.py gibbs_pass(fma=True), extended to G > 1) followed by the
+//    same cross-lane Hillis-Steele scan as k_gibbs;
+//  * the count #{j : excl + P_j ≤ thr} is a branch-free binary search over the lane's monotone
+//    prefix (5 compares + 11 selects for KP = 16 instead of 16 compare/add pairs) — exact because
+//    fl(excl + x) is monotone in x.
+// ≈2× fewer VALU instructions per token; bitwise equal to the fma oracle.
+template <int KP>
+__device__ __forceinline__ int count_le(const float (&P)[KP], float excl, float thr) {
+  if constexpr (KP == 16) {
+    if (excl + P[15] <= thr) return 16;
+    const bool b3 = excl + P[7] <= thr;
+    const bool b2 = excl + (b3 ? P[11] : P[3]) <= thr;
+    const float a1 = b2 ? P[5] : P[1], a2 = b2 ? P[13] : P[9];
+    const bool b1 = excl + (b3 ? a2 : a1) <= thr;
+    const float c0 = b1 ? P[2] : P[0], c1 = b1 ? P[6] : P[4], c2 = b1 ? P[10] : P[8], c3 = b1 ? P[14] : P[12];
+    const float d0 = b2 ? c1 : c0, d1 = b2 ? c3 : c2;
+    const bool b0 = excl + (b3 ? d1 : d0) <= thr;
+    return (b3 ? 8 : 0) + (b2 ? 4 : 0) + (b1 ? 2 : 0) + (b0 ? 1 : 0);
+  } else if constexpr (KP == 8) {
+    if (excl + P[7] <= thr) return 8;
+    const bool b2 = excl + P[3] <= thr;
+    const bool b1 = excl + (b2 ? P[5] : P[1]) <= thr;
+    const float c0 = b1 ? P[2] : P[0], c1 = b1 ? P[6] : P[4];
+    const bool b0 = excl + (b2 ? c1 : c0) <= thr;
+    return (b2 ? 4 : 0) + (b1 ? 2 : 0) + (b0 ? 1 : 0);
+  } else {
+    int cnt = 0;
+#pragma unroll
+    for (int j = 0; j < KP; ++j) cnt += (excl + P[j] <= thr);
+    return cnt;
+  }
+}
+
+// Sum of an int over each aligned group of G ∈ {4, 8, 16} lanes with DPP butterflies (no LDS
+// crossbar round trip): quad_perm swaps for 1 and 2, half-row / row mirrors for 4 and 8 (after the
+// lower levels every lane of a sub-group holds the sub-group sum, so any cross pairing works).
+template <int G>
+__device__ __forceinline__ int group_sum_dpp(int v) {
+  static_assert(G == 4 || G == 8 || G == 16, "DPP group sums need G in {4, 8, 16}");
+  v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, true);   // quad_perm [1,0,3,2]
+  v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, true);   // quad_perm [2,3,0,1]
+  if constexpr (G >= 8) v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, true);  // row_half_mirror
+  if constexpr (G >= 16) v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, true);  // row_mirror
+  return v;
+}
+
+template <int G, int KP, int MODE>
+__global__ __launch_bounds__(kBlock) void k_gibbs_ldsg(const OniGibbs a) {
+  static_assert(G > 1, "G = 1 uses k_gibbs_lds");
+  constexpr int S = oni::kWave / G;
+  constexpr int KS = G * KP;
+  constexpr int kSlots = LdsRow<KP>::kSlots;
+  __shared__ float4 sa[kBlock * kSlots];
+  __shared__ int32_t red[kWavesPerBlock][KS];
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int c = lane / G;
+  const int g = lane % G;
+  const int64_t slice = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  const bool valid = slice < a.n_slices;
+  const int64_t chunk = slice * S + c;
+  const int doc = valid ? a.chunk_doc[chunk] : -1;
+  const bool live = doc >= 0;
+  const int kbase = g * KP;
+  float4* row = sa + threadIdx.x * kSlots;
+  float* rowf = reinterpret_cast<float*>(row);
+  {
+    int32_t n0[KP];
+#pragma unroll
+    for (int j = 0; j < KP; ++j) n0[j] = 0;
+    if (live) load_row_i<KP>(a.ndk_src + (int64_t)doc * KS + kbase, n0);
+#pragma unroll
+    for (int j = 0; j < KP / 4; ++j)
+      row[j] = make_float4((float)n0[4 * j], (float)n0[4 * j + 1], (float)n0[4 * j + 2], (float)n0[4 * j + 3]);
+  }
+  const int len = valid ? a.slice_len[slice] : 0;
+  const int64_t off = valid ? a.slice_off[slice] : 0;
+  const uint32_t key = live ? a.chunk_key[chunk] : 0u;
+  const uint32_t pos0 = live ? (uint32_t)a.chunk_pos0[chunk] : 0u;
+  const uint32_t sweep = *a.sweep_ctr;
+  // Philox blocks are shared by the unit: lane g holds the block of 4-token group gbase + g, so
+  // the unit computes one block per G·4 tokens instead of every lane computing one per 4 tokens
+  // (the 36 quarter-rate integer multiplies of a block were ≈30 % of the sampler's issue slots)
+  uint32_t gbase = pos0 >> 2;
+  oni::U4 r = oni::philox10(oni::U4{gbase + (uint32_t)g, key, sweep, 1u}, a.seed0, a.seed1);
+  uint32_t wprev = oni::kPadWord;
+  float qv[KP];
+#pragma unroll
+  for (int j = 0; j < KP; ++j) qv[j] = 0.f;
+  int nchg = 0;
+  uint32_t w_nx = len > 0 ? a.tok_word[off + c] : oni::kPadWord;
+  int z_nx = len > 0 ? (int)a.tok_z[off + c] : 0;
+  for (int s = 0; s < len; ++s) {
+    const int64_t idx = off + (int64_t)s * S + c;
+    const uint32_t w = w_nx;
+    const int zo = z_nx;
+    if (s + 1 < len) {
+      w_nx = a.tok_word[idx + S];
+      z_nx = a.tok_z[idx + S];
+    }
+    if (w == oni::kPadWord) continue;  // uniform across the G lanes of a unit
+    const uint32_t pos = pos0 + (uint32_t)s;
+    const uint32_t gi = pos >> 2;
+    if (gi - gbase >= (uint32_t)G) {  // uniform within the unit
+      gbase = gi;
+      r = oni::philox10(oni::U4{gbase + (uint32_t)g, key, sweep, 1u}, a.seed0, a.seed1);
+    }
+    const uint32_t rr = (uint32_t)__shfl((int)oni::pick4(r, pos & 3u), (int)(gi - gbase), G);
+    const unsigned zlo = (unsigned)(zo - kbase);
+    if (zlo < (unsigned)KP) rowf[zlo] -= 1.0f;
+    if (w != wprev) {
+      load_row_f<KP>(a.q + (int64_t)w * KS + kbase, qv);
+      wprev = w;
+    }
+    float P[KP];
+    float run = 0.f;
+#pragma unroll
+    for (int j = 0; j < KP / 4; ++j) {
+      const float4 av = row[j];
+      run = fmaf(av.x + a.alpha, qv[4 * j + 0], run);
+      P[4 * j + 0] = run;
+      run = fmaf(av.y + a.alpha, qv[4 * j + 1], run);
+      P[4 * j + 1] = run;
+      run = fmaf(av.z + a.alpha, qv[4 * j + 2], run);
+      P[4 * j + 2] = run;
+      run = fmaf(av.w + a.alpha, qv[4 * j + 3], run);
+      P[4 * j + 3] = run;
+    }
+    float incl = run;
+#pragma unroll
+    for (int d = 1; d < G; d <<= 1) {
+      const float y = __shfl_up(incl, d, G);
+      if (g >= d) incl = incl + y;
+    }
+    float excl = __shfl_up(incl, 1, G);
+    if (g == 0) excl = 0.f;
+    const float total = __shfl(incl, G - 1, G);
+    const float thr = oni::u01(rr) * total;
+    const int cnt = group_sum_dpp<G>(count_le<KP>(P, excl, thr));
+    const int zn = cnt < a.K - 1 ? cnt : a.K - 1;
+    const unsigned znl = (unsigned)(zn - kbase);
+    if (znl < (unsigned)KP) rowf[znl] += 1.0f;
+    const bool changed = zn != zo && g == 0;
+    if (changed) {
+      ++nchg;
+      a.tok_z[idx] = (uint8_t)zn;
+      if constexpr (MODE == 3) a.z_w[a.wpos[idx]] = (uint8_t)zn;
+      if constexpr (MODE == 4) mark_changed_w(a, a.wpos[idx], zo, zn);
+      if constexpr (MODE == 1) {
+        atomicAdd(&a.dnwk[(int64_t)w * KS + zo], -1);
+        atomicAdd(&a.dnwk[(int64_t)w * KS + zn], 1);
+      }
+    }
+    if constexpr (MODE == 2) {
+      // lane 0 (c = 0) owns the slice's longest chunk, so it is active at every step
+      const uint64_t m = __ballot(changed);
+      if (lane == 0) a.chg_mask[(off + (int64_t)s * S) / S] = m;
+    }
+  }
+  if (a.chg_count) add_wave_count(a.chg_count, nchg);
+  // ---- epilogue (as k_gibbs): doc rows + per-topic totals ----------------------------------------
+  int32_t d[KP], n[KP];
+#pragma unroll
+  for (int j = 0; j < KP; ++j) {
+    n[j] = (int32_t)rowf[j];
+    d[j] = 0;
+  }
+  if (live) {
+    int32_t* dst = a.ndk_dst + (int64_t)doc * KS + kbase;
+    int32_t n0[KP];
+    load_row_i<KP>(a.ndk_src + (int64_t)doc * KS + kbase, n0);
+#pragma unroll
+    for (int j = 0; j < KP; ++j) d[j] = n[j] - n0[j];
+    if (!a.chunk_multi[chunk]) {
+#pragma unroll
+      for (int j = 0; j < KP; j += 4) *reinterpret_cast<int4*>(dst + j) = make_int4(n[j], n[j + 1], n[j + 2], n[j + 3]);
+    }
+  }
+  {
+    const bool multi = live && a.chunk_multi[chunk];
+    if (__ballot(multi)) flush_multi_rows<G, KP>(a.ndk_dst, KS, doc, multi, kbase, d);
+  }
+#pragma unroll
+  for (int j = 0; j < KP; ++j) {
+    int v = d[j];
+#pragma unroll
+    for (int m = G; m < oni::kWave; m <<= 1) v += __shfl_xor(v, m);
+    d[j] = v;
+  }
+  if (c == 0) {
+#pragma unroll
+    for (int j = 0; j < KP; ++j) red[wave][kbase + j] = d[j];
+  }
+  __syncthreads();
+  if (threadIdx.x < KS) {
+    int v = 0;
+#pragma unroll
+    for (int w = 0; w < kWavesPerBlock; ++w) v += red[w][threadIdx.x];
+    if (v) atomicAdd(&a.dnk[(int)(blockIdx.x & (unsigned)(a.nk_rep - 1)) * KS + threadIdx.x], v);
+  }
+}
+
 template <int G, int KP>
 int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s) {
   // qpf (sampler variant): 1 = k_gibbs_pp (ping-pong register sampler, default), 0 = k_gibbs with
   // a q-row load on each word change, 4 = k_gibbs with one-step q prefetch + row copy,
-  // 2 = k_gibbs_lds (LDS-staged counts, fma numerics, G = 1)
+  // 2 = k_gibbs_lds (G = 1) / k_gibbs_ldsg (G > 1): LDS-staged counts, fma numerics
   if (a.KS != G * KP || mode < 0 || mode > 4) return (int)hipErrorInvalidValue;
   const unsigned grid = (unsigned)((a.n_slices + kWavesPerBlock - 1) / kWavesPerBlock);
   if (grid == 0) return 0;
@@ -720,7 +931,13 @@ int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s)
     k_gibbs<G, KP, true, 1, false><<<grid, kBlock, 0, s>>>(a);  // init always builds n_wk by atomics
     return (int)hipGetLastError();
   }
-  if (mode == 4) {  // word-sorted change bitmap: register samplers only
+  if (mode == 4) {  // word-sorted change bitmap: register samplers + the multi-lane LDS sampler
+    if constexpr (G > 1) {
+      if (qpf == 2) {
+        k_gibbs_ldsg<G, KP, 4><<<grid, kBlock, 0, s>>>(a);
+        return (int)hipGetLastError();
+      }
+    }
     if (qpf == 4) k_gibbs<G, KP, false, 4, true><<<grid, kBlock, 0, s>>>(a);
     else if (qpf == 1) k_gibbs_pp<G, KP, 4><<<grid, kBlock, 0, s>>>(a);
     else if (qpf == 0) k_gibbs<G, KP, false, 4, false><<<grid, kBlock, 0, s>>>(a);
@@ -733,6 +950,14 @@ int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s)
       else if (mode == 1) k_gibbs_lds<KP, 1><<<grid, kBlock, 0, s>>>(a);
       else if (mode == 2) k_gibbs_lds<KP, 2><<<grid, kBlock, 0, s>>>(a);
       else k_gibbs_lds<KP, 3><<<grid, kBlock, 0, s>>>(a);
+      return (int)hipGetLastError();
+    }
+  } else {
+    if (qpf == 2) {
+      if (mode == 0) k_gibbs_ldsg<G, KP, 0><<<grid, kBlock, 0, s>>>(a);
+      else if (mode == 1) k_gibbs_ldsg<G, KP, 1><<<grid, kBlock, 0, s>>>(a);
+      else if (mode == 2) k_gibbs_ldsg<G, KP, 2><<<grid, kBlock, 0, s>>>(a);
+      else k_gibbs_ldsg<G, KP, 3><<<grid, kBlock, 0, s>>>(a);
       return (int)hipGetLastError();
     }
   }

@@ -58,10 +58,12 @@ class GibbsConfig:
     auto_delta: str = field(default_factory=lambda: os.environ.get("ONI_AUTO_DELTA", "wdelta"))
     # debug: verify count invariants after every sweep() call (ONI_CHECK_INVARIANTS=1)
     check_invariants: bool = field(default_factory=lambda: os.environ.get("ONI_CHECK_INVARIANTS", "0") == "1")
-    # sweep kernel: "auto" (default: "qpf" for K ≤ 32, "plain" above — the measured winners),
+    # sweep kernel: "auto" (default: "qpf" for K ≤ 32, "lds" above — the measured winners),
     # "qpf" one-step q-row prefetch, "plain" q-row load on each word change, "pp" ping-pong
-    # registers + 2-step token prefetch, "lds" LDS-staged doc counts (K ≤ 32, fma numerics).
-    # ONI_SAMPLER overrides the default. All but "lds" are bitwise identical.
+    # registers + 2-step token prefetch, "lds" LDS-staged doc counts (fma numerics; for K > 32 the
+    # multi-lane k_gibbs_ldsg: 1.59 → 1.06 ms per 25M-token sweep at K = 100, 0.80 → 0.57 at K = 50).
+    # ONI_SAMPLER overrides the default. All but "lds" are bitwise identical to each other; "lds"
+    # is bitwise identical to the oracle's fma numerics.
     sampler: str = field(default_factory=lambda: os.environ.get("ONI_SAMPLER", "auto"))
 
     def resolved_alpha(self) -> float:
@@ -103,8 +105,8 @@ class GibbsLDA:
         self.auto = cfg.count_mode == "auto"
         # auto: full recount while most topics still move, then the delta mode named by auto_delta
         auto_delta = {"wdelta": 4, "delta": 2}[cfg.auto_delta]
-        if cfg.sampler == "lds":
-            auto_delta = 2  # the LDS-count sampler implements the slot-mask delta bookkeeping only
+        if cfg.sampler == "lds" and self.G == 1:
+            auto_delta = 2  # the one-lane LDS sampler implements the slot-mask delta bookkeeping only
         self.mode = {"recount": 0, "atomic": 1, "delta": 2, "dual": 3, "wdelta": 4, "auto": auto_delta}[cfg.count_mode]
         # the auxiliary topic state of self.mode (z_prev for 2, word-sorted z_w for 4) matches tok_z
         self._aux_synced = False
@@ -126,11 +128,10 @@ class GibbsLDA:
         # the LDS sampler keeps counts as f32 integers: exact below 2^24 tokens per document
         if cfg.sampler not in SAMPLERS and cfg.sampler != "auto":
             raise ValueError(f"unknown sampler {cfg.sampler}")
-        self.qpf = SAMPLERS[cfg.sampler] if cfg.sampler != "auto" else (SAMPLERS["qpf"] if self.G == 1 else 0)
-        if self.qpf == 2 and self.G != 1:
-            self.qpf = 1  # the LDS-count variant exists for one-lane units (K ≤ 32) only
-        if self.qpf == 2 and self.mode == 4:
-            self.qpf = 4  # the word-bitmap delta mode is implemented by the register samplers
+        self.qpf = SAMPLERS[cfg.sampler] if cfg.sampler != "auto" else (SAMPLERS["qpf"] if self.G == 1 else
+                                                                         SAMPLERS["lds"])
+        if self.qpf == 2 and self.mode == 4 and self.G == 1:
+            self.qpf = 4  # one-lane units: the word-bitmap delta mode is in the register samplers
         if self.qpf == 2 and corpus.max_doc_len() >= (1 << 24):
             self.qpf = 1  # LDS rows hold counts as f32: exact below 2^24
         self.a = 0  # ndk parity

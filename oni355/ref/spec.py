@@ -237,8 +237,10 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed0: int, seed
                sweep: int, chunk_len: np.ndarray, fma: bool = False):
     """One init (init=True) or sweep pass over numpy state arrays, in place.
 
-    ``fma`` selects the numerics of the LDS-count sampler (k_gibbs_lds, G = 1): the running
-    weight sum is P_j = fma(n_j + α, q_j, P_{j-1}) instead of P_j = P_{j-1} + (n_j + α)·q_j.
+    ``fma`` selects the numerics of the LDS-count samplers (k_gibbs_lds for G = 1, k_gibbs_ldsg
+    for G > 1): inside each lane's KP topics the running weight sum is
+    P_j = fma(n_j + α, q_j, P_{j-1}) instead of P_j = P_{j-1} + (n_j + α)·q_j; lanes are then
+    combined by the same Hillis-Steele scan.
 
     st keys: tok_word u32, tok_z u8, slice_off i64, slice_len i32, chunk_doc i32, chunk_pos0 i32,
     chunk_key u32, chunk_multi u8, ndk_src i32 [D,KS], ndk_dst i32 [D,KS], q f32 [V,KS],
@@ -274,24 +276,22 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed0: int, seed
         n[act, zo] -= 1
         qv = st["q"][w]
         if fma:
-            assert G == 1
-            av = n[act].astype(F32) + alpha32
-            cum = np.empty_like(av)
-            run = np.zeros(av.shape[0], dtype=F32)
-            for j in range(KS):
-                run = fma_f32(av[:, j], qv[:, j], run)
-                cum[:, j] = run
-            total = run
+            # per-lane fma chains over each lane's KP topics (k_gibbs_lds / k_gibbs_ldsg)
+            av = (n[act].astype(F32) + alpha32).reshape(-1, G, KP)
+            qg = qv.reshape(-1, G, KP)
+            loc = np.empty_like(av)
+            run = np.zeros(av.shape[:2], dtype=F32)
+            for j in range(KP):
+                run = fma_f32(av[:, :, j], qg[:, :, j], run)
+                loc[:, :, j] = run
         else:
             p = (n[act].astype(F32) + alpha32) * qv
-        if fma:
-            pass  # cum/total built above
-        elif G == 1:
-            cum = np.cumsum(p, axis=1, dtype=F32)
+        if G == 1:
+            cum = loc.reshape(-1, KS) if fma else np.cumsum(p, axis=1, dtype=F32)
             total = cum[:, -1]
         else:
-            pg = p.reshape(-1, G, KP)
-            loc = np.cumsum(pg, axis=2, dtype=F32)
+            if not fma:
+                loc = np.cumsum(p.reshape(-1, G, KP), axis=2, dtype=F32)
             incl = loc[:, :, -1].copy()
             d = 1
             while d < G:

@@ -66,7 +66,9 @@ def _toy_tokens(n_docs, V, seed, heavy=True):
                                     (32, "dual+lds"), (7, "dual"), (50, "dual"), (50, "delta"), (100, "atomic"),
                                     (100, "dual"), (20, "wdelta"), (20, "wdelta+pp"), (20, "wdelta+plain"),
                                     (50, "wdelta"), (100, "wdelta"), (50, "recount+qpf"), (50, "wdelta+qpf"),
-                                    (100, "dual+qpf"), (64, "delta+qpf")])
+                                    (100, "dual+qpf"), (64, "delta+qpf"), (50, "recount+lds"), (100, "recount+lds"),
+                                    (50, "wdelta+lds"), (100, "wdelta+lds"), (100, "atomic+lds"), (64, "delta+lds"),
+                                    (40, "dual+lds"), (80, "wdelta+lds"), (128, "recount+lds"), (200, "atomic+lds")])
 def test_gibbs_bitwise_vs_oracle(gpu, K, mode):
     tdoc, tword, keys = _toy_tokens(300, 400, K)
     G, KP = ops.choose_tiling(K)
