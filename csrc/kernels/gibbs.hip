@@ -763,7 +763,36 @@ __device__ __forceinline__ int group_sum_dpp(int v) {
   return v;
 }
 
-template <int G, int KP, int MODE>
+// Float Hillis-Steele inclusive scan over aligned groups of G ≤ 16 lanes with DPP row shifts:
+// the same additions in the same order as the __shfl_up scan (bitwise identical), without LDS
+// crossbar round trips. Groups never straddle a 16-lane DPP row.
+template <int D>
+__device__ __forceinline__ float dpp_row_shr(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x110 + D, 0xF, 0xF, true));
+}
+
+template <int G>
+__device__ __forceinline__ float group_scan_dpp(float x, int g) {
+  static_assert(G == 4 || G == 8 || G == 16, "DPP group scans need G in {4, 8, 16}");
+  float y = dpp_row_shr<1>(x);
+  if (g >= 1) x = x + y;
+  y = dpp_row_shr<2>(x);
+  if (g >= 2) x = x + y;
+  if constexpr (G >= 8) {
+    y = dpp_row_shr<4>(x);
+    if (g >= 4) x = x + y;
+  }
+  if constexpr (G >= 16) {
+    y = dpp_row_shr<8>(x);
+    if (g >= 8) x = x + y;
+  }
+  return x;
+}
+
+// QP = 1: the q row of the next token is prefetched one step ahead (token words stream two steps
+// ahead so the prefetch address is known early) and copied in on a word change; QP = 0 loads the
+// row when the word changes.
+template <int G, int KP, int MODE, int QP>
 __global__ __launch_bounds__(kBlock) void k_gibbs_ldsg(const OniGibbs a) {
   static_assert(G > 1, "G = 1 uses k_gibbs_lds");
   constexpr int S = oni::kWave / G;
@@ -803,17 +832,29 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_ldsg(const OniGibbs a) {
   uint32_t gbase = pos0 >> 2;
   oni::U4 r = oni::philox10(oni::U4{gbase + (uint32_t)g, key, sweep, 1u}, a.seed0, a.seed1);
   uint32_t wprev = oni::kPadWord;
-  float qv[KP];
+  float qv[KP], qn[KP];
 #pragma unroll
-  for (int j = 0; j < KP; ++j) qv[j] = 0.f;
+  for (int j = 0; j < KP; ++j) qv[j] = qn[j] = 0.f;
   int nchg = 0;
   uint32_t w_nx = len > 0 ? a.tok_word[off + c] : oni::kPadWord;
   int z_nx = len > 0 ? (int)a.tok_z[off + c] : 0;
+  uint32_t w_nx2 = (QP && len > 1) ? a.tok_word[off + S + c] : oni::kPadWord;
+  if (QP && w_nx != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)w_nx * KS + kbase, qn);
   for (int s = 0; s < len; ++s) {
     const int64_t idx = off + (int64_t)s * S + c;
     const uint32_t w = w_nx;
     const int zo = z_nx;
-    if (s + 1 < len) {
+    if constexpr (QP) {
+      w_nx = w_nx2;
+      if (s + 1 < len) z_nx = a.tok_z[idx + S];
+      if (s + 2 < len) w_nx2 = a.tok_word[idx + 2 * S];
+      if (w != wprev) {
+#pragma unroll
+        for (int j = 0; j < KP; ++j) qv[j] = qn[j];
+        wprev = w;
+      }
+      if (s + 1 < len && w_nx != w && w_nx != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)w_nx * KS + kbase, qn);
+    } else if (s + 1 < len) {
       w_nx = a.tok_word[idx + S];
       z_nx = a.tok_z[idx + S];
     }
@@ -827,7 +868,7 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_ldsg(const OniGibbs a) {
     const uint32_t rr = (uint32_t)__shfl((int)oni::pick4(r, pos & 3u), (int)(gi - gbase), G);
     const unsigned zlo = (unsigned)(zo - kbase);
     if (zlo < (unsigned)KP) rowf[zlo] -= 1.0f;
-    if (w != wprev) {
+    if (!QP && w != wprev) {
       load_row_f<KP>(a.q + (int64_t)w * KS + kbase, qv);
       wprev = w;
     }
@@ -845,13 +886,8 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_ldsg(const OniGibbs a) {
       run = fmaf(av.w + a.alpha, qv[4 * j + 3], run);
       P[4 * j + 3] = run;
     }
-    float incl = run;
-#pragma unroll
-    for (int d = 1; d < G; d <<= 1) {
-      const float y = __shfl_up(incl, d, G);
-      if (g >= d) incl = incl + y;
-    }
-    float excl = __shfl_up(incl, 1, G);
+    const float incl = group_scan_dpp<G>(run, g);
+    float excl = dpp_row_shr<1>(incl);
     if (g == 0) excl = 0.f;
     const float total = __shfl(incl, G - 1, G);
     const float thr = oni::u01(rr) * total;
@@ -925,6 +961,7 @@ int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s)
   // a q-row load on each word change, 4 = k_gibbs with one-step q prefetch + row copy,
   // 2 = k_gibbs_lds (G = 1) / k_gibbs_ldsg (G > 1): LDS-staged counts, fma numerics
   if (a.KS != G * KP || mode < 0 || mode > 4) return (int)hipErrorInvalidValue;
+  if (G == 1 && qpf == 5) qpf = 2;  // q-prefetching LDS sampler is the multi-lane variant
   const unsigned grid = (unsigned)((a.n_slices + kWavesPerBlock - 1) / kWavesPerBlock);
   if (grid == 0) return 0;
   if (init) {
@@ -933,8 +970,9 @@ int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s)
   }
   if (mode == 4) {  // word-sorted change bitmap: register samplers + the multi-lane LDS sampler
     if constexpr (G > 1) {
-      if (qpf == 2) {
-        k_gibbs_ldsg<G, KP, 4><<<grid, kBlock, 0, s>>>(a);
+      if (qpf == 2 || qpf == 5) {
+        if (qpf == 5) k_gibbs_ldsg<G, KP, 4, 1><<<grid, kBlock, 0, s>>>(a);
+        else k_gibbs_ldsg<G, KP, 4, 0><<<grid, kBlock, 0, s>>>(a);
         return (int)hipGetLastError();
       }
     }
@@ -954,10 +992,17 @@ int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s)
     }
   } else {
     if (qpf == 2) {
-      if (mode == 0) k_gibbs_ldsg<G, KP, 0><<<grid, kBlock, 0, s>>>(a);
-      else if (mode == 1) k_gibbs_ldsg<G, KP, 1><<<grid, kBlock, 0, s>>>(a);
-      else if (mode == 2) k_gibbs_ldsg<G, KP, 2><<<grid, kBlock, 0, s>>>(a);
-      else k_gibbs_ldsg<G, KP, 3><<<grid, kBlock, 0, s>>>(a);
+      if (mode == 0) k_gibbs_ldsg<G, KP, 0, 0><<<grid, kBlock, 0, s>>>(a);
+      else if (mode == 1) k_gibbs_ldsg<G, KP, 1, 0><<<grid, kBlock, 0, s>>>(a);
+      else if (mode == 2) k_gibbs_ldsg<G, KP, 2, 0><<<grid, kBlock, 0, s>>>(a);
+      else k_gibbs_ldsg<G, KP, 3, 0><<<grid, kBlock, 0, s>>>(a);
+      return (int)hipGetLastError();
+    }
+    if (qpf == 5) {
+      if (mode == 0) k_gibbs_ldsg<G, KP, 0, 1><<<grid, kBlock, 0, s>>>(a);
+      else if (mode == 1) k_gibbs_ldsg<G, KP, 1, 1><<<grid, kBlock, 0, s>>>(a);
+      else if (mode == 2) k_gibbs_ldsg<G, KP, 2, 1><<<grid, kBlock, 0, s>>>(a);
+      else k_gibbs_ldsg<G, KP, 3, 1><<<grid, kBlock, 0, s>>>(a);
       return (int)hipGetLastError();
     }
   }

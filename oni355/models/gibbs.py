@@ -29,7 +29,7 @@ from .corpus import Corpus, canonical_tokens
 
 
 NK_REP = 32
-SAMPLERS = {"pp": 1, "plain": 0, "lds": 2, "qpf": 4}  # -> oni_gibbs_launch qpf argument
+SAMPLERS = {"pp": 1, "plain": 0, "lds": 2, "qpf": 4, "ldsq": 5}  # -> oni_gibbs_launch qpf argument
 
 
 @dataclass
@@ -130,9 +130,11 @@ class GibbsLDA:
             raise ValueError(f"unknown sampler {cfg.sampler}")
         self.qpf = SAMPLERS[cfg.sampler] if cfg.sampler != "auto" else (SAMPLERS["qpf"] if self.G == 1 else
                                                                          SAMPLERS["lds"])
+        if self.qpf == 5 and self.G == 1:
+            self.qpf = 2  # "ldsq" (LDS counts + q-row prefetch) is the multi-lane variant; G = 1 has "lds"
         if self.qpf == 2 and self.mode == 4 and self.G == 1:
             self.qpf = 4  # one-lane units: the word-bitmap delta mode is in the register samplers
-        if self.qpf == 2 and corpus.max_doc_len() >= (1 << 24):
+        if self.qpf in (2, 5) and corpus.max_doc_len() >= (1 << 24):
             self.qpf = 1  # LDS rows hold counts as f32: exact below 2^24
         self.a = 0  # ndk parity
         self.b = 0  # delta-buffer parity

@@ -12,7 +12,7 @@ timeout -k 10 300 python -u -m pytest tests/test_gibbs_stat.py -x -q --timeout 1
 tail -2 gpurun_out/ldsg_stat.log
 for K in 100 50; do
   timeout -k 10 300 python bench/gibbs_ab.py --topics $K --rounds 3 --sweeps 10 --burn 10 \
-    --modes recount,recount+lds,wdelta,wdelta+lds > gpurun_out/ldsg_ab_k$K.json 2> gpurun_out/ldsg_ab_k$K.err \
+    --modes ${MODES:-recount,recount+lds,recount+ldsq,wdelta+lds,wdelta+ldsq} > gpurun_out/ldsg_ab_k$K.json 2> gpurun_out/ldsg_ab_k$K.err \
     || { echo "ab K=$K failed"; tail -20 gpurun_out/ldsg_ab_k$K.err; exit 1; }
   echo "ab K=$K ok"
 done
