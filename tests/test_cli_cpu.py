@@ -87,3 +87,33 @@ def test_dns_proxy_cli(tmp_path, source):
     assert fb is not None and len(next(iter(fb.values()))) == 2
     assert ml.main(["20160708", source, "1.0", "40", *inp, "--device", "cpu", "--sweeps", "4", "--lpath", lp,
                     "--quiet"]) == 0
+
+
+def test_setup_layout_templates_and_ingest_config(tmp_path):
+    """oni-setup (the oni-setup module's role): folders, table definitions, duxbay.conf and
+    ingest_conf.json templates that the other entry points consume; idempotent unless --force."""
+    import json
+
+    from oni355 import schema
+    from oni355.cli import ingest as ingest_cli
+    from oni355.cli import setup as setup_cli
+    from oni355.config import OniConfig, load_config
+    root, lp, st, conf = (str(tmp_path / x) for x in ("store", "data", "stage", "conf"))
+    assert setup_cli.main(["--data-root", root, "--lpath", lp, "--stage", st, "--conf-dir", conf]) == 0
+    for src in schema.SOURCES:
+        t = json.load(open(os.path.join(root, src, "_table.json")))
+        assert [c["name"] for c in t["columns"]] == schema.raw_columns(src)
+        assert t["results_columns"] == schema.result_columns(src)
+        assert os.path.isdir(os.path.join(lp, src)) and os.path.isdir(os.path.join(st, src))
+    kinds = {c["name"]: c["kind"] for c in json.load(open(os.path.join(root, "dns", "_table.json")))["columns"]}
+    assert kinds["dns_qry_name"] == "string" and kinds["ip_dst"] == "uint32" and kinds["unix_tstamp"] == "int64"
+    cfg = load_config(os.path.join(conf, "duxbay.conf"), env={})
+    d = OniConfig()
+    assert cfg.TOPIC_COUNT == d.TOPIC_COUNT and cfg.DUPFACTOR == d.DUPFACTOR and cfg.SEED == d.SEED
+    assert cfg.DATA_ROOT == os.path.abspath(root) and cfg.LPATH == os.path.abspath(lp) and not cfg.extra
+    # second run: nothing rewritten; --force rewrites
+    r = setup_cli.setup(root, lp, st, conf)
+    assert r == {"created_dirs": [], "written": []}
+    assert len(setup_cli.setup(root, lp, st, conf, force=True)["written"]) == 5
+    # the ingest template drives oni-ingest (empty collector dir → nothing to do, no errors)
+    assert ingest_cli.main(["-t", "flow", "--config", os.path.join(conf, "ingest_conf.json"), "--once"]) == 0
