@@ -573,7 +573,7 @@ __device__ __forceinline__ void lds_step(const OniGibbs& a, int s, int len, int6
   if (s + 2 < len) {
     wq[P] = a.tok_word[idx + 128];
     zq[P] = a.tok_z[idx + 128];
-    if constexpr (MODE == 3) pq[P] = a.wpos[idx + 128];
+    if constexpr (MODE == 3 || MODE == 4) pq[P] = a.wpos[idx + 128];
   }
   if (s + 1 < len && wq[1 - P] != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)wq[1 - P] * KS, qn);
   const uint32_t pos = pos0 + (uint32_t)s;
@@ -607,6 +607,7 @@ __device__ __forceinline__ void lds_step(const OniGibbs& a, int s, int len, int6
     if (changed) {
       a.tok_z[idx] = (uint8_t)zn;
       if constexpr (MODE == 3) a.z_w[wp] = (uint8_t)zn;
+      if constexpr (MODE == 4) mark_changed_w(a, wp, zo, zn);
       if constexpr (MODE == 1) {
         atomicAdd(&a.dnwk[(int64_t)w * KS + zo], -1);
         atomicAdd(&a.dnwk[(int64_t)w * KS + zn], 1);
@@ -660,7 +661,7 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_lds(const OniGibbs a) {
     if (t < len) {
       wq[t] = a.tok_word[off + t * 64 + lane];
       zq[t] = a.tok_z[off + t * 64 + lane];
-      if constexpr (MODE == 3) pq[t] = a.wpos[off + t * 64 + lane];
+      if constexpr (MODE == 3 || MODE == 4) pq[t] = a.wpos[off + t * 64 + lane];
     }
   }
   if (wq[0] != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)wq[0] * KS, qa);
@@ -968,11 +969,16 @@ int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s)
     k_gibbs<G, KP, true, 1, false><<<grid, kBlock, 0, s>>>(a);  // init always builds n_wk by atomics
     return (int)hipGetLastError();
   }
-  if (mode == 4) {  // word-sorted change bitmap: register samplers + the multi-lane LDS sampler
+  if (mode == 4) {  // word-sorted change bitmap
     if constexpr (G > 1) {
       if (qpf == 2 || qpf == 5) {
         if (qpf == 5) k_gibbs_ldsg<G, KP, 4, 1><<<grid, kBlock, 0, s>>>(a);
         else k_gibbs_ldsg<G, KP, 4, 0><<<grid, kBlock, 0, s>>>(a);
+        return (int)hipGetLastError();
+      }
+    } else {
+      if (qpf == 2) {
+        k_gibbs_lds<KP, 4><<<grid, kBlock, 0, s>>>(a);
         return (int)hipGetLastError();
       }
     }

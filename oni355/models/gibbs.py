@@ -105,8 +105,6 @@ class GibbsLDA:
         self.auto = cfg.count_mode == "auto"
         # auto: full recount while most topics still move, then the delta mode named by auto_delta
         auto_delta = {"wdelta": 4, "delta": 2}[cfg.auto_delta]
-        if cfg.sampler == "lds" and self.G == 1:
-            auto_delta = 2  # the one-lane LDS sampler implements the slot-mask delta bookkeeping only
         self.mode = {"recount": 0, "atomic": 1, "delta": 2, "dual": 3, "wdelta": 4, "auto": auto_delta}[cfg.count_mode]
         # the auxiliary topic state of self.mode (z_prev for 2, word-sorted z_w for 4) matches tok_z
         self._aux_synced = False
@@ -132,8 +130,6 @@ class GibbsLDA:
                                                                          SAMPLERS["lds"])
         if self.qpf == 5 and self.G == 1:
             self.qpf = 2  # "ldsq" (LDS counts + q-row prefetch) is the multi-lane variant; G = 1 has "lds"
-        if self.qpf == 2 and self.mode == 4 and self.G == 1:
-            self.qpf = 4  # one-lane units: the word-bitmap delta mode is in the register samplers
         if self.qpf in (2, 5) and corpus.max_doc_len() >= (1 << 24):
             self.qpf = 1  # LDS rows hold counts as f32: exact below 2^24
         self.a = 0  # ndk parity

@@ -71,7 +71,8 @@ def _toy_tokens(n_docs, V, seed, heavy=True):
                                     (40, "dual+lds"), (80, "wdelta+lds"), (128, "recount+lds"), (200, "atomic+lds"),
                                     (50, "recount+ldsq"), (100, "wdelta+ldsq"), (64, "delta+ldsq"), (100, "dual+ldsq"),
                                     (200, "atomic+ldsq"), (50, "dual+plain"), (100, "wdelta+plain"),
-                                    (100, "atomic+plain"), (64, "delta+pp")])
+                                    (100, "atomic+plain"), (64, "delta+pp"), (20, "wdelta+lds"), (7, "wdelta+lds"),
+                                    (32, "wdelta+lds"), (20, "recount+lds")])
 def test_gibbs_bitwise_vs_oracle(gpu, K, mode):
     tdoc, tword, keys = _toy_tokens(300, 400, K)
     G, KP = ops.choose_tiling(K)
