@@ -39,7 +39,7 @@ def main(argv=None) -> int:
     ap.add_argument("--flows-per-gpu", type=int, default=12_500_000)
     ap.add_argument("--topics", type=int, default=None)
     ap.add_argument("--source", choices=["flow", "dns", "proxy"], default="flow")
-    ap.add_argument("--score-path", choices=["tiles", "pairs", "gather"], default="pairs",
+    ap.add_argument("--score-path", choices=["tiles", "pairs", "pairs_unsorted", "gather"], default="pairs",
                     help="tiles: distinct pairs as 16x16 MFMA blocks; pairs: per-pair VALU dots; "
                          "gather: per-event θ/φ row gathers (tiles/pairs + 4-B per-event pair gathers)")
     ap.add_argument("--events-per-gpu", type=int, default=2_000_000, help="dns/proxy events per GPU")
@@ -107,7 +107,8 @@ def main(argv=None) -> int:
     phi = model.phi()
     # distinct (doc, word) pairs + per-endpoint pair index: built once per day (corpus dictionaries)
     plans = {"tiles": common.score_plan(dkeys, vocab, sides, tiles=True),
-             "pairs": common.score_plan(dkeys, vocab, sides, tiles=False)}
+             "pairs": common.score_plan(dkeys, vocab, sides, tiles=False),
+             "pairs_unsorted": common.score_plan(dkeys, vocab, sides, tiles=False, sort_events=False)}
     lk = [(common.lookup(dkeys, dk_), common.lookup(vocab, wk_)) for dk_, wk_ in sides]
 
     def score_once(path):
@@ -118,7 +119,8 @@ def main(argv=None) -> int:
             sc, _, _ = ops.score(theta, phi, lk[0][0], lk[0][1], lk[1][0], lk[1][1], tol=1.0, hist=hist)
         else:
             sc, _, _ = ops.score(theta, phi, lk[0][0], lk[0][1], tol=1.0, hist=hist)
-        return common.top_n(sc, 1.0, a.maxresults, comm, rank * per, hist=hist)
+        order = plans[path].order if path in plans else None
+        return common.top_n(sc, 1.0, a.maxresults, comm, rank * per, hist=hist, order=order)
 
     def time_path(path, reps=5):
         score_once(path)
@@ -131,7 +133,8 @@ def main(argv=None) -> int:
         comm.barrier()
         return comm.allreduce_scalar((time.perf_counter() - t1) / reps, "max"), res
 
-    score_ab = {p: round(time_path(p)[0] * 1e3, 3) for p in ("tiles", "pairs", "gather") if p != a.score_path}
+    score_ab = {p: round(time_path(p)[0] * 1e3, 3) for p in ("tiles", "pairs", "pairs_unsorted", "gather")
+                if p != a.score_path}
     score_dt, (rows, scs) = time_path(a.score_path)
     plan = plans["tiles"]
     ll = model.log_likelihood()

@@ -219,6 +219,12 @@ class ScorePlan:
     pword: torch.Tensor
     inv: list
     tiles: TilePlan | None = None
+    # events regrouped by their first endpoint's pair (SCORE_SORT_EVENTS): the gather of that
+    # endpoint's pair score becomes a monotone stream instead of a random 4-B read per event;
+    # ``order`` maps plan position → event, ``rank`` event → plan position
+    order: torch.Tensor | None = None
+    rank: torch.Tensor | None = None
+    inv_sorted: list | None = None
 
     @property
     def n_pairs(self) -> int:
@@ -282,10 +288,14 @@ def _excl_cumsum(x: torch.Tensor) -> torch.Tensor:
 # MFMA block scoring is kept as an option: at K = 20 and the flow day's 12 % block density the
 # VALU pair dot measured 39 µs vs 74 µs for k_tile_score (profiles/r1_pmc_score_mfma_vs_valu.json)
 SCORE_TILES = False
+# score events in first-endpoint pair order (one monotone + one random gather per flow instead of
+# two random ones; DNS/proxy events become a pure stream); results map back through plan.order
+SCORE_SORT_EVENTS = True
 
 
 @traced("oni:score_plan")
-def score_plan(dkeys: torch.Tensor, vocab: torch.Tensor, sides, tiles: bool | None = None) -> ScorePlan:
+def score_plan(dkeys: torch.Tensor, vocab: torch.Tensor, sides, tiles: bool | None = None,
+               sort_events: bool | None = None) -> ScorePlan:
     """``sides``: [(doc_keys64, word_keys64)] per event endpoint (1 for DNS/proxy, 2 for flows).
 
     ``tiles`` (default :data:`SCORE_TILES`) also builds the MFMA item plan and stores the pairs
@@ -303,33 +313,50 @@ def score_plan(dkeys: torch.Tensor, vocab: torch.Tensor, sides, tiles: bool | No
         newpos[perm] = torch.arange(perm.numel(), dtype=perm.dtype, device=perm.device)
         pdoc, pword, inv = pdoc[perm], pword[perm], newpos[inv]
     invs = [x.to(torch.int32).contiguous() for x in inv.split([t.numel() for t in ids])]
-    return ScorePlan(pdoc.to(torch.int32).contiguous(), pword.to(torch.int32).contiguous(), invs, tp)
+    plan = ScorePlan(pdoc.to(torch.int32).contiguous(), pword.to(torch.int32).contiguous(), invs, tp)
+    if SCORE_SORT_EVENTS if sort_events is None else sort_events:
+        order = torch.argsort(invs[0], stable=True)
+        rank = torch.empty_like(order)
+        rank[order] = torch.arange(order.numel(), dtype=order.dtype, device=order.device)
+        plan.order, plan.rank = order, rank
+        plan.inv_sorted = [x[order].contiguous() for x in invs]
+    return plan
 
 
 @traced("oni:score")
 def plan_score(theta: torch.Tensor, phi: torch.Tensor, plan: ScorePlan, tol: float, hist=None, want_parts=False):
+    """(score, s1, s2) per event in PLAN order (event order unless plan.order is set; map plan
+    positions back with plan.order / event indices forward with plan.rank)."""
     if plan.tiles is not None:
         t = plan.tiles
         ps = ops.tile_score(theta, phi, t.item_docs, t.item_words, t.item_p0, t.pair_rc, plan.pdoc, plan.pword)
     else:
         ps = ops.pair_score(theta, phi, plan.pdoc, plan.pword)
-    return ops.event_min(ps, plan.inv[0], plan.inv[1] if len(plan.inv) > 1 else None, tol=tol,
-                          want_parts=want_parts, hist=hist)
+    inv = plan.inv_sorted if plan.inv_sorted is not None else plan.inv
+    return ops.event_min(ps, inv[0], inv[1] if len(inv) > 1 else None, tol=tol, want_parts=want_parts, hist=hist)
+
+
+def to_event_order(plan: ScorePlan, x: torch.Tensor | None) -> torch.Tensor | None:
+    """Per-event values produced in plan order (plan_score) → event order."""
+    if x is None or plan.rank is None:
+        return x
+    return x[plan.rank]
 
 
 @traced("oni:top_n")
 def top_n(score: torch.Tensor, tol: float, maxresults: int, comm: Comm | None, row_offset: int = 0,
-          hist: torch.Tensor | None = None):
+          hist: torch.Tensor | None = None, order: torch.Tensor | None = None):
     """Lowest ``maxresults`` scores below ``tol`` (ties by global row id), merged over ranks (X06).
 
     ``hist`` is the 2048-bucket histogram of score order keys (top 11 bits) of events under tol,
     as produced by the fused score kernel; computed here when absent. Returns (global row ids
-    int64, scores f32), ascending, identical on every rank.
+    int64, scores f32), ascending, identical on every rank. ``order`` (a score plan's event order)
+    maps positions of ``score`` to local event ids.
     """
     if hist is None:
         b = u32_to_i64(ops.f32_keys(score)) >> 21
         hist = torch.bincount(b[score < tol], minlength=2048)
-    return _top_n_from_hist(score, hist, tol, maxresults, comm, row_offset)
+    return _top_n_from_hist(score, hist, tol, maxresults, comm, row_offset, order)
 
 
 @dataclass
@@ -370,7 +397,7 @@ def run_single_doc_events(doc_keys64: torch.Tensor, word_keys64: torch.Tensor, K
     t0 = time.perf_counter()
     hist = torch.zeros(2048, dtype=torch.int32, device=dev)
     score, _, _ = plan_score(theta, run.model.phi(), plan, tol, hist=hist)
-    rows, scs = top_n(score, tol, maxresults, comm, row_offset, hist=hist)
+    rows, scs = top_n(score, tol, maxresults, comm, row_offset, hist=hist, order=plan.order)
     sync()
     t["score_s"] = time.perf_counter() - t0
     t["records_scored"] = int(doc_keys64.numel())
@@ -389,10 +416,9 @@ def run_single_doc_events(doc_keys64: torch.Tensor, word_keys64: torch.Tensor, K
                         words=words.cpu().numpy().view(np.uint64), timings=t, stats=stats, lda=run)
 
 
-def _top_n_from_hist(score, hist, tol, maxresults, comm, row_offset):
-    h = hist.to(torch.int64).cpu().numpy()
-    if comm is not None and comm.world > 1:
-        h = comm.allreduce_np(h)
+def _top_n_from_hist(score, hist, tol, maxresults, comm, row_offset, order=None):
+    h_loc = hist.to(torch.int64).cpu().numpy()
+    h = comm.allreduce_np(h_loc) if comm is not None and comm.world > 1 else h_loc
     cum = np.cumsum(h)
     if maxresults <= 0 or cum[-1] == 0:
         bmax = 2047 if maxresults > 0 else -1
@@ -401,8 +427,11 @@ def _top_n_from_hist(score, hist, tol, maxresults, comm, row_offset):
     if bmax < 0:
         e = torch.zeros(0, dtype=torch.int64, device=score.device)
         return e, torch.zeros(0, dtype=torch.float32, device=score.device)
-    local_cnt = int(torch.count_nonzero(score < tol)) if score.numel() else 0
-    idx, sc = ops.select_below(score, tol, bmax, cap=max(local_cnt, 1))
+    # the local histogram already counts this rank's candidates: no extra pass over the scores
+    cap = int(np.cumsum(h_loc)[bmax])
+    idx, sc = ops.select_below(score, tol, bmax, cap=max(cap, 1))
+    if order is not None:
+        idx = order[idx]
     gid = idx + row_offset
     # exact order: (score, global id); keep local top-N then merge
     o1 = torch.argsort(gid, stable=True)

@@ -143,7 +143,7 @@ def run_flow(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxre
     t0 = time.perf_counter()
     hist = torch.zeros(2048, dtype=torch.int32, device=theta.device)
     score, s1, s2 = common.plan_score(theta, phi, plan, tol, hist=hist, want_parts=True)
-    rows, scs = common.top_n(score, tol, maxresults, comm, row_offset, hist=hist)
+    rows, scs = common.top_n(score, tol, maxresults, comm, row_offset, hist=hist, order=plan.order)
     sync()
     t["score_s"] = time.perf_counter() - t0
     t["records_scored"] = n
@@ -151,7 +151,8 @@ def run_flow(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxre
     loc = rows - row_offset
     mine = (loc >= 0) & (loc < n)
     li = loc[mine]
-    parts = torch.stack([s1[li], s2[li]], 1) if s1 is not None else torch.zeros(0, 2)
+    pi = plan.rank[li] if plan.rank is not None else li  # plan positions of the result events
+    parts = torch.stack([s1[pi], s2[pi]], 1) if s1 is not None else torch.zeros(0, 2)
     wparts = torch.stack([sw[li], dw[li]], 1)
     if comm is not None and comm.world > 1:
         gid_all = torch.cat(comm.allgather_var(rows[mine]))

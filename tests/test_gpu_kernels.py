@@ -190,7 +190,8 @@ def test_pair_plan_score_matches_gather(gpu, two):
     plan = common.score_plan(dkeys, vocab, sides, tiles=False)
     h1 = torch.zeros(2048, dtype=torch.int32, device=gpu)
     h2 = torch.zeros(2048, dtype=torch.int32, device=gpu)
-    got, g1, g2 = common.plan_score(th, ph, plan, 0.3, hist=h1, want_parts=True)
+    got, g1, g2 = (common.to_event_order(plan, x) for x in common.plan_score(th, ph, plan, 0.3, hist=h1,
+                                                                             want_parts=True))
     lk = [(common.lookup(dkeys, a), common.lookup(vocab, b)) for a, b in sides]
     args = [x for p in lk for x in p]
     want, w1, w2 = ops.score(th, ph, *args, tol=0.3, want_parts=True, hist=h2)
@@ -216,7 +217,7 @@ def test_tile_score_mfma_bitwise_vs_fma_oracle(gpu, KS):
     dsel = torch.from_numpy(np.minimum(r.zipf(1.3, n) - 1, D - 1))
     sides = [(dkeys[dsel], vocab[torch.from_numpy(r.integers(0, V, n))])]
     plan_c = common.score_plan(dkeys, vocab, sides, tiles=True)
-    want = common.plan_score(torch.from_numpy(th), torch.from_numpy(ph), plan_c, 0.3)[0]
+    want = common.to_event_order(plan_c, common.plan_score(torch.from_numpy(th), torch.from_numpy(ph), plan_c, 0.3)[0])
     g = lambda x: x.to(gpu)  # noqa: E731
     plan_g = common.score_plan(g(dkeys), g(vocab), [(g(a), g(b)) for a, b in sides], tiles=True)
     t = plan_g.tiles
@@ -224,5 +225,6 @@ def test_tile_score_mfma_bitwise_vs_fma_oracle(gpu, KS):
                         t.pair_rc, plan_g.pdoc, plan_g.pword)
     ref = spec.dot_rows_fma(th[plan_g.pdoc.cpu().numpy()], ph[plan_g.pword.cpu().numpy()])
     assert np.array_equal(ps.cpu().numpy(), ref)
-    got = common.plan_score(g(torch.from_numpy(th)), g(torch.from_numpy(ph)), plan_g, 0.3)[0]
+    got = common.to_event_order(plan_g, common.plan_score(g(torch.from_numpy(th)), g(torch.from_numpy(ph)), plan_g,
+                                                          0.3)[0])
     assert torch.equal(got.cpu(), want)

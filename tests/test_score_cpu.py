@@ -1,6 +1,7 @@
 """Scoring plans on CPU: the MFMA tile plan covers every distinct pair exactly once, and the
 tile path (fma-chain numerics) agrees with the VALU pair path to within f32 rounding."""
 import numpy as np
+import pytest
 import torch
 
 from oni355.pipeline import common
@@ -44,9 +45,35 @@ def test_tile_path_close_to_pair_path():
     r = np.random.default_rng(0)
     th = torch.from_numpy((r.random((300, 20)) / 20).astype(np.float32))
     ph = torch.from_numpy((r.random((200, 20)) ** 4).astype(np.float32))
-    a = common.plan_score(th, ph, common.score_plan(dkeys, vocab, sides, tiles=True), 1.0)[0].numpy()
-    b = common.plan_score(th, ph, common.score_plan(dkeys, vocab, sides, tiles=False), 1.0)[0].numpy()
+    pa, pb = common.score_plan(dkeys, vocab, sides, tiles=True), common.score_plan(dkeys, vocab, sides, tiles=False)
+    a = common.to_event_order(pa, common.plan_score(th, ph, pa, 1.0)[0]).numpy()
+    b = common.to_event_order(pb, common.plan_score(th, ph, pb, 1.0)[0]).numpy()
     assert np.allclose(a, b, rtol=2e-6, atol=0)
+
+
+@pytest.mark.parametrize("two", [False, True])
+def test_event_sorted_plan_matches_event_order(two):
+    """Scoring in first-endpoint pair order (SCORE_SORT_EVENTS) is a pure permutation: same
+    per-event scores, same top-N rows and scores (ties by global row id) as event order."""
+    dkeys, vocab, sides = _sides(3, two=two)
+    r = np.random.default_rng(1)
+    th = torch.from_numpy((r.random((dkeys.numel(), 20)) / 20).astype(np.float32))
+    ph = torch.from_numpy((r.random((vocab.numel(), 20)) ** 4).astype(np.float32))
+    ps_ = common.score_plan(dkeys, vocab, sides, tiles=False, sort_events=True)
+    pu = common.score_plan(dkeys, vocab, sides, tiles=False, sort_events=False)
+    assert ps_.order is not None and pu.order is None
+    assert torch.equal(ps_.order[ps_.rank], torch.arange(ps_.order.numel()))
+    sa, s1a, s2a = common.plan_score(th, ph, ps_, 1.0, want_parts=True)
+    sb, s1b, s2b = common.plan_score(th, ph, pu, 1.0, want_parts=True)
+    assert torch.equal(common.to_event_order(ps_, sa), sb)
+    assert torch.equal(common.to_event_order(ps_, s1a), s1b)
+    if two:
+        assert torch.equal(common.to_event_order(ps_, s2a), s2b)
+        assert bool((ps_.inv_sorted[0][1:] >= ps_.inv_sorted[0][:-1]).all())  # first endpoint streams
+    for mr in (1, 17, 10_000):
+        ra, ca = common.top_n(sa, 0.5, mr, None, row_offset=1000, order=ps_.order)
+        rb, cb = common.top_n(sb, 0.5, mr, None, row_offset=1000)
+        assert torch.equal(ra, rb) and torch.equal(ca, cb)
 
 
 def test_fma_oracle_matches_float64_rounding():
