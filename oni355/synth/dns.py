@@ -122,12 +122,20 @@ def generate_dns(n: int, seed: int = 5, n_clients: int | None = None, user_domai
     if anomaly_rows.size:
         quiet = np.argsort(w)[: max(1, n_clients // 10)]
         cli[anomaly_rows] = quiet[rng.integers(0, quiet.size, size=anomaly_rows.size)]
-        hx = _hex(rng, anomaly_rows.size, 40, 60)
+        # each anomaly is an individually rare behaviour (tunnel/DGA-like name of varying shape, odd
+        # record type, odd hour): a hundred copies of ONE pattern would form a topic of their own
+        # and stop being rare for the model at large day sizes
+        na = anomaly_rows.size
+        hx = _hex(rng, na, 20, 72)
+        nlab = rng.integers(1, 4, size=na)
         for j, i in enumerate(anomaly_rows):
-            names[i] = f"{hx[j][:30]}.{hx[j][30:]}.x{rng.integers(100, 999)}tunnel.biz"
-        qtype[anomaly_rows] = rng.choice([16, 10], size=anomaly_rows.size)
-        rcode[anomaly_rows] = 0
-        hour[anomaly_rows] = 3
+            h, k = hx[j], int(nlab[j])
+            cut = np.linspace(0, len(h), k + 1).astype(int)
+            sub = ".".join(h[cut[t]:cut[t + 1]] for t in range(k))
+            names[i] = f"{sub}.x{rng.integers(100, 999)}tunnel.biz"
+        qtype[anomaly_rows] = rng.choice([16, 10, 13, 17, 29, 99, 252, 255], size=na)
+        rcode[anomaly_rows] = rng.choice([0, 2, 5], size=na)
+        hour[anomaly_rows] = rng.integers(1, 6, size=na)
     minute = rng.integers(0, 60, size=n)
     sec = rng.integers(0, 60, size=n)
     unix = date_unix + hour * 3600 + minute * 60 + sec

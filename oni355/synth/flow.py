@@ -44,7 +44,10 @@ _PROFILES = [
     ("monitoring", [9100, 5666], [0.5, 0.5], 12, 7.0, 7.2, 0.4, 500),
 ]
 
-_ANOMALY_PORTS = [23, 69, 79, 111, 119, 135, 513]
+# rarely-used service ports (none is in a profile): planted anomalies draw from all of them so
+# that each anomaly is an individually rare word, not one more frequent pattern
+_ANOMALY_PORTS = [7, 9, 13, 19, 23, 37, 42, 69, 70, 79, 102, 111, 113, 119, 135, 137, 177, 179, 194, 201, 264,
+                  318, 383, 427, 464, 497, 512, 513, 515, 520, 540, 554, 631, 646, 666, 749, 750, 902, 992, 1011]
 
 
 @dataclass
@@ -144,9 +147,11 @@ def generate_flows(n: int, seed: int = 7, n_hosts: int | None = None, n_profiles
         dip2[anomaly_rows] = _ip(203, 0, 113, rng.integers(1, 255, size=na) & 255)
         sport[anomaly_rows] = rng.integers(1025, 65536, size=na)
         dport[anomaly_rows] = rng.choice(_ANOMALY_PORTS, size=na)
-        hour[anomaly_rows] = rng.choice([3, 4], size=na)
+        hour[anomaly_rows] = rng.integers(1, 6, size=na)
         ibyt[anomaly_rows] = rng.integers(500_000_000, 900_000_000, size=na)
-        ipkt[anomaly_rows] = rng.integers(1, 3, size=na)
+        # volume shape: a few giant packets, or a flood of them
+        flood = rng.random(na) < 0.5
+        ipkt[anomaly_rows] = np.where(flood, rng.integers(400_000, 600_000, size=na), rng.integers(1, 3, size=na))
 
     y, mo, d = date
     unix = (np.int64(1467936000) + hour * 3600 + minute * 60 + second).astype(np.int64)

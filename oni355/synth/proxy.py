@@ -90,14 +90,19 @@ def generate_proxy(n: int, seed: int = 9, n_clients: int | None = None, alpha_tr
     hour = np.mod(np.floor(hour_f), 24).astype(int)
     anomaly_rows = np.sort(rng.choice(n, size=min(n_anomalies, n), replace=False))
     quiet = np.argsort(w)[: max(1, n_clients // 10)]
+    # individually rare behaviours (see synth.dns): varying method, content type, URI shape, hour
+    a_methods = ["POST", "PUT", "CONNECT", "DELETE", "PROPFIND", "OPTIONS"]
+    a_ctypes = ["application/x-www-form-urlencoded", "application/octet-stream", "application/x-msdownload",
+                "application/x-sh", "text/x-python"]
     for i in anomaly_rows:
         cli[i] = quiet[rng.integers(0, quiet.size)]
         host[i] = f"x{rng.integers(1000, 9999)}.badcdn-sync.biz"
-        method[i] = "POST"
+        method[i] = a_methods[rng.integers(0, len(a_methods))]
         ua[i] = f"Mozilla/4.0 (compatible; agent-{rng.integers(10**6, 10**7)})"
-        ctype[i] = "application/x-www-form-urlencoded"
-        path[i] = "/" + "".join(chr(c) for c in rng.choice(np.frombuffer(b"abcdefABCDEF0123456789+/=", np.uint8), 120))
-        hour[i] = 3
+        ctype[i] = a_ctypes[rng.integers(0, len(a_ctypes))]
+        plen = int(rng.integers(40, 200))
+        path[i] = "/" + "".join(chr(c) for c in rng.choice(np.frombuffer(b"abcdefABCDEF0123456789+/=", np.uint8), plen))
+        hour[i] = int(rng.integers(1, 6))
         status[i] = 200
     minute = rng.integers(0, 60, n)
     sec = rng.integers(0, 60, n)
