@@ -167,7 +167,7 @@ class GibbsLDA:
         self.cn = 0
         ops.gibbs_pass(self._state(True), self.G, self.KP, self.K, self.alpha, self.cfg.seed, True,
                        self.sweep_ctr, self.c.chunk_len, host_sweep=0)
-        if self.comm is not None and self.comm.world > 1:
+        if self.comm is not None and self.comm.dist:
             self.comm.allreduce_(self.nwk)
             self.comm.allreduce_(self.nk[0])
         self.T_global = int(self.nk[0][: self.K].sum())
@@ -269,7 +269,7 @@ class GibbsLDA:
             # dn[b] head := Δn_wk of the tokens that changed topic this sweep
             ops.delta_recount(c.wslot, c.tile_wlo, c.tile_whi, self.chg_mask, c.tok_word, self.tok_z, self.tok_zprev,
                               head, self.KS, self.G)
-        if self.comm is not None and self.comm.world > 1:
+        if self.comm is not None and self.comm.dist:
             t0 = time.perf_counter()
             self.comm.allreduce_(self.dn[self.b])
             self.timings["allreduce_s"] += time.perf_counter() - t0
@@ -281,7 +281,7 @@ class GibbsLDA:
         self.sweeps_done += 1
 
     def _graphable(self) -> bool:
-        return (self.cfg.use_graph and self.device.type == "cuda" and (self.comm is None or self.comm.world == 1)
+        return (self.cfg.use_graph and self.device.type == "cuda" and (self.comm is None or not self.comm.dist)
                 and os.environ.get("ONI_NO_GRAPH", "0") != "1")
 
     def _capture(self, mode: int):
@@ -325,7 +325,7 @@ class GibbsLDA:
         K = self.K
         T_loc = torch.tensor([float(self.c.T)], dtype=torch.float64, device=self.device)
         T_glob = T_loc.clone()
-        if self.comm is not None and self.comm.world > 1:
+        if self.comm is not None and self.comm.dist:
             self.comm.allreduce_(T_glob)
         nwk = self.nwk[:, :K].to(torch.int64)
         nk = self.nk_cur[:K].to(torch.int64)
@@ -401,7 +401,7 @@ class GibbsLDA:
         doc = (self.c.D * (math.lgamma(K * a) - K * math.lgamma(a)) + torch.lgamma(ndk + a).sum()
                - torch.lgamma(nd + K * a).sum())
         doc_v = doc.reshape(1)
-        if self.comm is not None and self.comm.world > 1:
+        if self.comm is not None and self.comm.dist:
             self.comm.allreduce_(doc_v)
         return float(word + doc_v[0])
 
@@ -434,7 +434,7 @@ class GibbsLDA:
         self.ndk[0].view(-1).index_add_(0, tdoc * KS + zz, torch.ones_like(zz, dtype=torch.int32))
         self.nwk.view(-1).index_add_(0, tword * KS + zz, torch.ones_like(zz, dtype=torch.int32))
         self.nk[0].index_add_(0, zz, torch.ones_like(zz, dtype=torch.int32))
-        if self.comm is not None and self.comm.world > 1:
+        if self.comm is not None and self.comm.dist:
             self.comm.allreduce_(self.nwk)
             self.comm.allreduce_(self.nk[0])
         self._sync_aux_z()

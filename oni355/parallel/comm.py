@@ -24,28 +24,32 @@ import torch.distributed as dist
 
 
 class Comm:
-    def __init__(self, rank: int = 0, world: int = 1, device: torch.device | None = None, group=None):
+    def __init__(self, rank: int = 0, world: int = 1, device: torch.device | None = None, group=None,
+                 forced: bool = False):
         self.rank = rank
         self.world = world
         self.device = device or torch.device("cpu")
         self.group = group
+        # collectives run whenever a process group exists: world > 1, or a forced 1-rank group
+        # (ONI_FORCE_DIST=1) that drives the real RCCL / gloo code paths on a single device
+        self.dist = world > 1 or forced
 
     # -- basic ------------------------------------------------------------------------------------
     def allreduce_(self, t: torch.Tensor) -> torch.Tensor:
-        if self.world > 1:
+        if self.dist:
             dist.all_reduce(t, group=self.group)
         return t
 
     def allreduce_np(self, a) -> np.ndarray:
         a = np.asarray(a)
-        if self.world == 1:
+        if not self.dist:
             return a
         t = torch.from_numpy(np.ascontiguousarray(a)).to(self.device)
         dist.all_reduce(t, group=self.group)
         return t.cpu().numpy()
 
     def allreduce_scalar(self, x: float, op: str = "sum") -> float:
-        if self.world == 1:
+        if not self.dist:
             return float(x)
         t = torch.tensor([float(x)], dtype=torch.float64, device=self.device)
         dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
@@ -53,21 +57,21 @@ class Comm:
         return float(t.item())
 
     def barrier(self) -> None:
-        if self.world > 1:
+        if self.dist:
             if self.device.type == "cuda":
                 dist.barrier(group=self.group, device_ids=[self.device.index or 0])
             else:
                 dist.barrier(group=self.group)
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
-        if self.world > 1:
+        if self.dist:
             dist.broadcast(t, src=src, group=self.group)
         return t
 
     # -- variable-size gathers / exchanges ------------------------------------------------------
     def allgather_var(self, t: torch.Tensor) -> list[torch.Tensor]:
         """All-gather tensors whose first dim differs per rank."""
-        if self.world == 1:
+        if not self.dist:
             return [t]
         n = torch.tensor([t.shape[0]], dtype=torch.int64, device=self.device)
         ns = [torch.zeros_like(n) for _ in range(self.world)]
@@ -82,7 +86,7 @@ class Comm:
 
     def alltoallv(self, t: torch.Tensor, send_counts: torch.Tensor) -> torch.Tensor:
         """Exchange rows: rows [off_r, off_r + send_counts[r]) of ``t`` go to rank r."""
-        if self.world == 1:
+        if not self.dist:
             return t
         sc = send_counts.to(torch.int64).to(self.device)
         rc = torch.empty_like(sc)
@@ -103,8 +107,12 @@ def init_from_env(device_type: str | None = None, timeout_s: float = 600.0) -> C
     device = torch.device(device_type, local) if device_type == "cuda" else torch.device("cpu")
     if device_type == "cuda":
         torch.cuda.set_device(device)
-    if world == 1:
+    forced = os.environ.get("ONI_FORCE_DIST", "0") == "1"
+    if world == 1 and not forced:
         return Comm(0, 1, device)
+    if world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29531")
     os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     if not dist.is_initialized():
         backend = "nccl" if device_type == "cuda" else "gloo"
@@ -113,7 +121,7 @@ def init_from_env(device_type: str | None = None, timeout_s: float = 600.0) -> C
             kw["device_id"] = device
         dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
-    return Comm(rank, world, device)
+    return Comm(rank, world, device, forced=forced)
 
 
 def shutdown() -> None:

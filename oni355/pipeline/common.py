@@ -37,7 +37,7 @@ def i64_to_u32bits(t: torch.Tensor) -> torch.Tensor:
 def global_vocab(keys64: torch.Tensor, comm: Comm | None) -> torch.Tensor:
     """Sorted unique int64 word keys over all ranks (collective X02)."""
     loc = torch.unique(keys64)
-    if comm is None or comm.world == 1:
+    if comm is None or not comm.dist:
         return loc
     parts = comm.allgather_var(loc)
     return torch.unique(torch.cat([p.to(loc.device) for p in parts]))
@@ -89,7 +89,7 @@ def balanced_owner(doc_keys64: torch.Tensor, weights: torch.Tensor, comm: Comm) 
 @traced("oni:route_to_owners")
 def route_to_owners(doc_keys64: torch.Tensor, word_ids: torch.Tensor, weights: torch.Tensor, comm: Comm | None):
     """Send each token to its document's owner rank (alltoallv). Returns local (doc, word, weight)."""
-    if comm is None or comm.world == 1:
+    if comm is None or not comm.dist:
         return doc_keys64, word_ids, weights
     owner = balanced_owner(doc_keys64, weights, comm)
     order = torch.argsort(owner, stable=True)
@@ -124,7 +124,7 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor, weights
     G, _ = ops.choose_tiling(K)
     if chunk_len <= 0:
         T_glob = float(wt.sum()) if wt.numel() else 0.0
-        if comm is not None and comm.world > 1:
+        if comm is not None and comm.dist:
             T_glob = comm.allreduce_scalar(T_glob, "sum")
         chunk_len = auto_chunk_len(int(T_glob), G)
     use_w = bool((wt != 1).any()) if wt.numel() else False
@@ -172,7 +172,7 @@ def gather_theta(run: LdaRun, comm: Comm | None) -> tuple[torch.Tensor, torch.Te
     """Global (sorted doc keys, θ rows) on every rank (collective X05; local when world == 1)."""
     th = run.model.theta()
     keys = run.doc_keys64
-    if comm is None or comm.world == 1:
+    if comm is None or not comm.dist:
         return keys, th
     kp = comm.allgather_var(keys)
     tp = comm.allgather_var(th)
@@ -404,7 +404,7 @@ def run_single_doc_events(doc_keys64: torch.Tensor, word_keys64: torch.Tensor, K
     loc = rows - row_offset
     mine = (loc >= 0) & (loc < doc_keys64.numel())
     words = word_keys64[loc[mine]]
-    if comm is not None and comm.world > 1:
+    if comm is not None and comm.dist:
         gid_all = torch.cat(comm.allgather_var(rows[mine]))
         words = torch.cat(comm.allgather_var(words))
         pos = {int(g): i for i, g in enumerate(gid_all.tolist())}
@@ -418,7 +418,7 @@ def run_single_doc_events(doc_keys64: torch.Tensor, word_keys64: torch.Tensor, K
 
 def _top_n_from_hist(score, hist, tol, maxresults, comm, row_offset, order=None):
     h_loc = hist.to(torch.int64).cpu().numpy()
-    h = comm.allreduce_np(h_loc) if comm is not None and comm.world > 1 else h_loc
+    h = comm.allreduce_np(h_loc) if comm is not None and comm.dist else h_loc
     cum = np.cumsum(h)
     if maxresults <= 0 or cum[-1] == 0:
         bmax = 2047 if maxresults > 0 else -1
@@ -438,7 +438,7 @@ def _top_n_from_hist(score, hist, tol, maxresults, comm, row_offset, order=None)
     gid, sc = gid[o1], sc[o1]
     o2 = torch.argsort(sc, stable=True)
     gid, sc = gid[o2][:maxresults], sc[o2][:maxresults]
-    if comm is not None and comm.world > 1:
+    if comm is not None and comm.dist:
         gid = torch.cat(comm.allgather_var(gid))
         sc = torch.cat(comm.allgather_var(sc))
         o1 = torch.argsort(gid, stable=True)

@@ -86,7 +86,7 @@ def featurize(d: dict, comm: Comm | None, topset: HashSet | None, user_domain: s
             "sub_ent": ops.f32_keys(sub_ent), "periods": per}
     n = d["frame_len"].numel()
     ar, n_glob = None, n
-    if comm is not None and comm.world > 1:
+    if comm is not None and comm.dist:
         ar = comm.allreduce_np
         n_glob = int(comm.allreduce_np(np.array([n], np.int64))[0])
     cuts = {name: ops.quantile_cuts(keys[name].contiguous(), fr, ar, n_glob) for name, fr, _ in BINNED}

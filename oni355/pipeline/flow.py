@@ -56,7 +56,7 @@ def compute_cuts(d: dict, comm: Comm | None) -> FlowCuts:
     n = tk.numel()
     ar = None
     n_glob = n
-    if comm is not None and comm.world > 1:
+    if comm is not None and comm.dist:
         ar = comm.allreduce_np
         n_glob = int(comm.allreduce_np(np.array([n], dtype=np.int64))[0])
     cuts = FlowCuts(ops.quantile_cuts(tk, spec.DECILES, ar, n_glob), ops.quantile_cuts(bk, spec.DECILES, ar, n_glob),
@@ -154,7 +154,7 @@ def run_flow(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxre
     pi = plan.rank[li] if plan.rank is not None else li  # plan positions of the result events
     parts = torch.stack([s1[pi], s2[pi]], 1) if s1 is not None else torch.zeros(0, 2)
     wparts = torch.stack([sw[li], dw[li]], 1)
-    if comm is not None and comm.world > 1:
+    if comm is not None and comm.dist:
         gid_all = torch.cat(comm.allgather_var(rows[mine]))
         parts = torch.cat(comm.allgather_var(parts))
         wparts = torch.cat(comm.allgather_var(wparts))

@@ -104,7 +104,7 @@ def featurize(cols: dict, device, comm: Comm | None, topset, allreduce_counts: b
     uh, _, _ = sops.string_features(uo, uc)
     uq, inv = torch.unique(uh, return_inverse=True)
     cnt = torch.bincount(inv, minlength=uq.numel())
-    if comm is not None and comm.world > 1:
+    if comm is not None and comm.dist:
         keys = torch.cat(comm.allgather_var(uq))
         cnts = torch.cat(comm.allgather_var(cnt))
         gk, ginv = torch.unique(keys, return_inverse=True)
@@ -115,7 +115,7 @@ def featurize(cols: dict, device, comm: Comm | None, topset, allreduce_counts: b
     _, ulen, uent = sops.string_features(fo, fc)
     keys = {"time": tkey, "ua_freq": ua_freq, "uri_ent": ops.f32_keys(uent), "uri_len": ulen}
     ar, n_glob = None, n
-    if comm is not None and comm.world > 1:
+    if comm is not None and comm.dist:
         ar = comm.allreduce_np
         n_glob = int(comm.allreduce_np(np.array([n], np.int64))[0])
     cuts = {name: ops.quantile_cuts(keys[name], fr, ar, n_glob) for name, fr, _ in BINNED}

@@ -73,3 +73,19 @@ def test_combined_bench_cpu_and_sizing():
     b = sizing.plan("flow", 2 * 10**6, 20, 10**4, 10**4)
     assert b.steady_bytes > a.steady_bytes and b.peak_bytes > b.steady_bytes
     assert not sizing.plan("flow", 20 * 10**9, 100, 10**6, 10**6).fits()
+
+
+def test_bench_forced_one_rank_process_group_matches_plain():
+    """ONI_FORCE_DIST=1 drives every collective through a real 1-rank process group (the RCCL code
+    path on a single GPU box; gloo here): same model and results as the collective-free run."""
+    plain = _run([sys.executable, "bench.py", *ARGS])
+    env_cmd = [sys.executable, "bench.py", *ARGS]
+    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONUNBUFFERED="1", ONI_FORCE_DIST="1",
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
+    r = subprocess.run(env_cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    forced = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    _check(forced, 1)
+    for k in ("loglik", "tokens", "vocab", "docs_local", "planted_anomaly_recall_topN", "score_pairs"):
+        assert forced[k] == plain[k], k
+    assert forced["allreduce_s_per_sweep"] > 0 and plain["allreduce_s_per_sweep"] == 0
