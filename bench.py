@@ -53,6 +53,12 @@ def main(argv=None) -> int:
     if a.topics is None:
         a.topics = 20
 
+    # the contract is ONE JSON line on stdout: keep the real stdout for it and send everything else
+    # written to fd 1 (RCCL's version banner at communicator creation, library chatter) to stderr
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
+
     import torch
 
     from oni355.utils.obs import stack_dumps_from_env
@@ -186,7 +192,7 @@ def main(argv=None) -> int:
         "allreduce_s_per_sweep": (model.timings["allreduce_s"] / max(model.timings["allreduce_calls"], 1)),
     }
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     pc.shutdown()
     return 0
 

@@ -33,6 +33,12 @@ def main(argv=None) -> int:
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--device", default="cuda")
     a = ap.parse_args(argv)
+    # the contract is ONE JSON line on stdout: keep the real stdout for it and send everything else
+    # written to fd 1 (RCCL's version banner at communicator creation, library chatter) to stderr
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
+
     import torch
 
     from oni355.utils.obs import stack_dumps_from_env
@@ -110,7 +116,7 @@ def main(argv=None) -> int:
         "setup_s": round(setup_s, 2),
     }
     if comm.rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     pc.shutdown()
     return 0
 

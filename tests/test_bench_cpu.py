@@ -22,8 +22,8 @@ def _run(cmd):
     env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONUNBUFFERED="1")
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stderr[-3000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout  # stdout is exactly the JSON line
     return json.loads(lines[0])
 
 
