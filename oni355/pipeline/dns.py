@@ -17,6 +17,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from ..io import staging
 from ..utils.obs import traced
 from ..ops import strings as sops
 from ..parallel.comm import Comm
@@ -57,15 +58,16 @@ def load_top_domains(path: str) -> list[str]:
 
 
 def to_device(cols: dict, device) -> dict:
+    up = staging.upload
     d = {}
     for k in ("unix_tstamp",):
-        d[k] = torch.from_numpy(np.asarray(cols[k], np.int64)).to(device)
+        d[k] = up(np.asarray(cols[k], np.int64), device)
     for k in ("frame_len", "dns_qry_type", "dns_qry_rcode"):
-        d[k] = torch.from_numpy(np.asarray(cols[k]).astype(np.int32)).to(device)
-    d["ip_dst"] = torch.from_numpy(np.asarray(cols["ip_dst"], np.uint32).view(np.int32)).to(device)
+        d[k] = up(np.asarray(cols[k]).astype(np.int32), device)
+    d["ip_dst"] = up(np.asarray(cols["ip_dst"], np.uint32).view(np.int32), device)
     nm: StringColumn = cols["dns_qry_name"]
-    d["name_off"] = torch.from_numpy(nm.offsets).to(device)
-    d["name_chars"] = torch.from_numpy(nm.chars if nm.chars.size else np.zeros(1, np.uint8)).to(device)
+    d["name_off"] = up(nm.offsets, device)
+    d["name_chars"] = up(nm.chars if nm.chars.size else np.zeros(1, np.uint8), device)
     return d
 
 

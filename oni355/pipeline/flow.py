@@ -19,6 +19,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from ..io import staging
 from ..utils.obs import traced
 from ..parallel.comm import Comm
 from ..ref import spec
@@ -30,12 +31,14 @@ DEVICE_COLS = {"trhour": torch.int32, "trminute": torch.int32, "trsec": torch.in
 
 
 def to_device(cols: dict, device) -> dict:
+    """Host columns → device through the pinned staging ring (io/staging.py): the host-side
+    dtype conversion of column j+1 overlaps the DMA of column j."""
     out = {}
     for name, dt in DEVICE_COLS.items():
         a = np.asarray(cols[name])
         if a.dtype == np.uint32:
             a = a.view(np.int32)
-        out[name] = torch.from_numpy(np.ascontiguousarray(a)).to(dtype=dt).to(device)
+        out[name] = staging.upload(a, device, dt)
     return out
 
 

@@ -17,6 +17,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from ..io import staging
 from ..utils.obs import traced
 from ..ops import strings as sops
 from ..parallel.comm import Comm
@@ -56,8 +57,8 @@ def word_str(w: int) -> str:
 
 def _codes_by_hash(col: StringColumn, dev, fn) -> torch.Tensor:
     """Categorical code per row via the distinct values only (few distinct methods / types)."""
-    off = torch.from_numpy(col.offsets).to(dev)
-    ch = torch.from_numpy(col.chars if col.chars.size else np.zeros(1, np.uint8)).to(dev)
+    off = staging.upload(col.offsets, dev)
+    ch = staging.upload(col.chars if col.chars.size else np.zeros(1, np.uint8), dev)
     h, _, _ = sops.string_features(off, ch)
     uniq, first_idx, inv = _unique_first(h)
     labels = [fn(col[int(i)]) for i in first_idx.tolist()]
@@ -84,8 +85,8 @@ def featurize(cols: dict, device, comm: Comm | None, topset, allreduce_counts: b
 
     def strcol(name):
         c: StringColumn = cols[name]
-        return (torch.from_numpy(c.offsets).to(dev),
-                torch.from_numpy(c.chars if c.chars.size else np.zeros(1, np.uint8)).to(dev))
+        return (staging.upload(c.offsets, dev),
+                staging.upload(c.chars if c.chars.size else np.zeros(1, np.uint8), dev))
 
     ho, hc = strcol("host")
     _, top, _, _, _ = sops.domain_features(ho, hc, topset, "")
@@ -121,7 +122,7 @@ def featurize(cols: dict, device, comm: Comm | None, topset, allreduce_counts: b
     cuts = {name: ops.quantile_cuts(keys[name], fr, ar, n_glob) for name, fr, _ in BINNED}
     raws = {"method": _codes_by_hash(cols["reqmethod"], dev, method_code),
             "ctype": _codes_by_hash(cols["resconttype"], dev, ctype_class),
-            "respcode": torch.from_numpy(np.asarray(cols["respcode"]).astype(np.int32)).to(dev)}
+            "respcode": staging.upload(np.asarray(cols["respcode"]).astype(np.int32), dev)}
     words = sops.pack_words([keys[nm] for nm, _, _ in BINNED], [cuts[nm] for nm, _, _ in BINNED],
                             [s for _, _, s in BINNED], [raws[nm] for nm, _, _ in RAW], [m for _, m, _ in RAW],
                             [s for _, _, s in RAW], raw8=top, r8mask=3, r8shift=TOP_SHIFT)
@@ -139,7 +140,7 @@ def run_proxy(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxr
     topset = top_set(top_domains)
     words, cuts = featurize(cols, device, comm, topset)
     dev = words.device
-    docs = torch.from_numpy(np.asarray(cols["clientip"], np.uint32).astype(np.int64)).to(dev)
+    docs = staging.upload(np.asarray(cols["clientip"], np.uint32).astype(np.int64), dev)
     t["featurize_s"] = time.perf_counter() - t0
     fb = None
     if feedback and len(feedback.get("clientip", [])):

@@ -1,0 +1,49 @@
+"""Pinned staging ring (csrc/kernels/stage.hip, oni355/io/staging.py): host → HBM uploads."""
+import numpy as np
+import pytest
+import torch
+
+from oni355.io import staging
+
+
+def test_cpu_target_returns_host_values():
+    a = np.arange(1000, dtype=np.uint32)
+    t = staging.upload(a, "cpu", torch.int64)
+    assert t.dtype == torch.int64 and torch.equal(t, torch.arange(1000, dtype=torch.int64))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m", ["1", "reg"])
+def test_staged_upload_bitwise_many_sizes(gpu, monkeypatch, m):
+    monkeypatch.setenv("ONI_STAGED_H2D", m)
+    rng = np.random.default_rng(3)
+    # sizes around the chunk boundary, empty, odd byte counts; > N_BUF chunks so the ring wraps
+    cb = staging.CHUNK_BYTES
+    for nbytes in (0, 1, 7, 4096, cb - 1, cb, cb + 3, 5 * cb + 11):
+        a = rng.integers(0, 256, nbytes, dtype=np.uint8)
+        t = staging.upload(a, gpu)
+        assert t.device.type == "cuda" and t.dtype == torch.uint8 and t.numel() == nbytes
+        assert np.array_equal(t.cpu().numpy(), a)
+    before = staging.stats()
+    x = rng.standard_normal(3_000_001).astype(np.float32)
+    tx = staging.upload(x, gpu)
+    # kernels on the same stream are ordered after the queued copies
+    s = float(tx.double().sum().item())
+    assert s == pytest.approx(float(x.astype(np.float64).sum()), rel=1e-12)
+    if m == "1":
+        assert staging.stats()["bytes"] - before["bytes"] == x.nbytes
+    staging.sync()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m", ["1", "reg"])
+def test_flow_to_device_staged_matches_plain(gpu, monkeypatch, m):
+    from oni355.pipeline import flow
+    from oni355.synth.flow import generate_flows
+    day = generate_flows(200_000, seed=5)
+    monkeypatch.setenv("ONI_STAGED_H2D", m)
+    got = flow.to_device(day.cols, gpu)
+    monkeypatch.setenv("ONI_STAGED_H2D", "0")
+    want = flow.to_device(day.cols, gpu)
+    for k in want:
+        assert got[k].dtype == want[k].dtype and torch.equal(got[k], want[k]), k
