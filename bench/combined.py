@@ -41,8 +41,9 @@ def main(argv=None) -> int:
 
     import torch
 
-    from oni355.utils.obs import stack_dumps_from_env
+    from oni355.utils.obs import heartbeat_from_env, stack_dumps_from_env
     stack_dumps_from_env()
+    heartbeat_from_env()
 
     from oni355.parallel import comm as pc
     from oni355.pipeline.synthetic import build_source

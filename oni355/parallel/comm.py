@@ -25,11 +25,15 @@ import torch.distributed as dist
 
 class Comm:
     def __init__(self, rank: int = 0, world: int = 1, device: torch.device | None = None, group=None,
-                 forced: bool = False):
+                 forced: bool = False, backend: str | None = None):
         self.rank = rank
         self.world = world
         self.device = device or torch.device("cpu")
         self.group = group
+        self.backend = backend or ("nccl" if self.device.type == "cuda" else "gloo")
+        # gloo over device tensors (ONI_DIST_BACKEND=gloo: several ranks sharing one GPU, the
+        # SURVEY §4.3 shard emulation): collectives go through host copies
+        self._via_host = self.device.type == "cuda" and self.backend == "gloo"
         # collectives run whenever a process group exists: world > 1, or a forced 1-rank group
         # (ONI_FORCE_DIST=1) that drives the real RCCL / gloo code paths on a single device
         self.dist = world > 1 or forced
@@ -37,42 +41,58 @@ class Comm:
     # -- basic ------------------------------------------------------------------------------------
     def allreduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.dist:
-            dist.all_reduce(t, group=self.group)
+            if self._via_host and t.is_cuda:
+                h = t.cpu()
+                dist.all_reduce(h, group=self.group)
+                t.copy_(h)
+            else:
+                dist.all_reduce(t, group=self.group)
         return t
 
     def allreduce_np(self, a) -> np.ndarray:
         a = np.asarray(a)
         if not self.dist:
             return a
-        t = torch.from_numpy(np.ascontiguousarray(a)).to(self.device)
+        t = torch.from_numpy(np.ascontiguousarray(a)).to(self._coll_device)
         dist.all_reduce(t, group=self.group)
         return t.cpu().numpy()
 
     def allreduce_scalar(self, x: float, op: str = "sum") -> float:
         if not self.dist:
             return float(x)
-        t = torch.tensor([float(x)], dtype=torch.float64, device=self.device)
+        t = torch.tensor([float(x)], dtype=torch.float64, device=self._coll_device)
         dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
                                "min": dist.ReduceOp.MIN}[op], group=self.group)
         return float(t.item())
 
     def barrier(self) -> None:
         if self.dist:
-            if self.device.type == "cuda":
+            if self.device.type == "cuda" and self.backend == "nccl":
                 dist.barrier(group=self.group, device_ids=[self.device.index or 0])
             else:
                 dist.barrier(group=self.group)
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.dist:
-            dist.broadcast(t, src=src, group=self.group)
+            if self._via_host and t.is_cuda:
+                h = t.cpu()
+                dist.broadcast(h, src=src, group=self.group)
+                t.copy_(h)
+            else:
+                dist.broadcast(t, src=src, group=self.group)
         return t
+
+    @property
+    def _coll_device(self) -> torch.device:
+        return torch.device("cpu") if self._via_host else self.device
 
     # -- variable-size gathers / exchanges ------------------------------------------------------
     def allgather_var(self, t: torch.Tensor) -> list[torch.Tensor]:
         """All-gather tensors whose first dim differs per rank."""
         if not self.dist:
             return [t]
+        if self._via_host and t.is_cuda:
+            return [o.to(self.device) for o in self._host_view().allgather_var(t.cpu())]
         n = torch.tensor([t.shape[0]], dtype=torch.int64, device=self.device)
         ns = [torch.zeros_like(n) for _ in range(self.world)]
         dist.all_gather(ns, n, group=self.group)
@@ -88,6 +108,8 @@ class Comm:
         """Exchange rows: rows [off_r, off_r + send_counts[r]) of ``t`` go to rank r."""
         if not self.dist:
             return t
+        if self._via_host and t.is_cuda:
+            return self._host_view().alltoallv(t.cpu(), send_counts.cpu()).to(self.device)
         sc = send_counts.to(torch.int64).to(self.device)
         rc = torch.empty_like(sc)
         dist.all_to_all_single(rc, sc, group=self.group)
@@ -95,6 +117,9 @@ class Comm:
         dist.all_to_all_single(out, t.to(self.device).contiguous(), output_split_sizes=rc.tolist(),
                                input_split_sizes=sc.tolist(), group=self.group)
         return out
+
+    def _host_view(self) -> "Comm":
+        return Comm(self.rank, self.world, torch.device("cpu"), self.group, forced=self.dist, backend="gloo")
 
 
 def init_from_env(device_type: str | None = None, timeout_s: float = 600.0) -> Comm:
@@ -114,14 +139,16 @@ def init_from_env(device_type: str | None = None, timeout_s: float = 600.0) -> C
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29531")
     os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    # ONI_DIST_BACKEND=gloo with device tensors: several ranks may share one GPU (shard emulation,
+    # SURVEY §4.3); RCCL needs one GPU per rank
+    backend = os.environ.get("ONI_DIST_BACKEND") or ("nccl" if device_type == "cuda" else "gloo")
     if not dist.is_initialized():
-        backend = "nccl" if device_type == "cuda" else "gloo"
         kw = {}
-        if device_type == "cuda":
+        if device_type == "cuda" and backend == "nccl":
             kw["device_id"] = device
         dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
-    return Comm(rank, world, device, forced=forced)
+    return Comm(rank, world, device, forced=forced, backend=backend)
 
 
 def shutdown() -> None:

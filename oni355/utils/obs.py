@@ -117,6 +117,29 @@ def traced(name: str):
     return deco
 
 
+def heartbeat_from_env(var: str = "ONI_HEARTBEAT_S", tag: str = "heartbeat") -> bool:
+    """With ``$ONI_HEARTBEAT_S`` = N, a daemon thread prints one elapsed-time line to stderr every N
+    seconds: long host-side setups (1B-event synthetic days) show progress to a hang watchdog
+    without the frame walking of :func:`stack_dumps_from_env`."""
+    try:
+        every = float(os.environ.get(var, "0") or 0)
+    except ValueError:
+        every = 0.0
+    if every <= 0:
+        return False
+    import sys
+    import threading
+    t0 = time.perf_counter()
+
+    def beat():
+        while True:
+            time.sleep(every)
+            print(f"[{tag}] {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=beat, daemon=True, name="oni-heartbeat").start()
+    return True
+
+
 def stack_dumps_from_env(var: str = "ONI_STACK_DUMP_S") -> bool:
     """Hang diagnosis: with ``$ONI_STACK_DUMP_S`` = N, dump every thread's Python stack to stderr
     every N seconds (faulthandler), so a stalled run names the call it is stuck in.
