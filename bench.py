@@ -1,48 +1,58 @@
 #!/usr/bin/env python3
-"""Headline benchmark: netflow suspicious-connects, 20-topic collapsed-Gibbs LDA on MI355X.
+"""Headline benchmark: netflow suspicious-connects with 20-topic collapsed-Gibbs LDA on MI355X.
 
 Metric (BASELINE.json): "netflow records scored/sec (whole node) + Gibbs iters/sec, 20-topic LDA".
-One timed *step* = one full Gibbs sweep over every token of the day (2 tokens per flow) including
-the per-sweep RCCL all-reduce of Δn_wk and the q-table refresh. ``value`` = whole-node netflow
-records swept per second (= total flows × sweeps/s). Also reported: Gibbs iters/s, tokens/s and
-the post-LDA scoring pass (records scored/s: θ·φ score of every flow + top-N selection).
+
+One timed *step* (default ``--mode pipeline``) is one complete ``oni-ml YYYYMMDD flow`` day run on
+every rank's shard — exactly what the CLI executes (oni355.pipeline.flow.run_flow), from the
+day's raw columns in host memory to the rendered, globally ordered top-N result rows (CSV written
+by rank 0):
+
+    H2D → quantile cuts (K01, X03) → flow words (K03) → vocabulary (K08, X02) → owner routing →
+    corpus CSR + SELL (K09) → LDA init + ``--sweeps`` Gibbs sweeps (K10-K12, X01 per sweep) →
+    θ/φ (K13, X05) → score plan + scores (K15) → top-N (K16, X06) → CSV rows.
+
+``value`` = whole-node flows fully processed (scored) per second = global flows × steps / time.
+``gibbs_iters_per_sec`` = sweeps of the in-step training / its device time (median over steps).
+``--mode sweep`` times bare sweeps of an already built model instead (the round-1 measurement,
+reported as flow-sweeps/s under a different metric name; for sampler A/B work).
 
 Weak scaling: every GPU owns ``--flows-per-gpu`` synthetic flows (default 12.5M, so N=8 is the
 BASELINE config "Netflow 100M flows, 20 topics, DP=8"). Synthetic data with random-init topic
-priors (oni355.synth.flow), random-init LDA. Launch for N>1:
-  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
-      --master-port P bench.py --gpus N --steps K --warmup W
+priors (oni355.synth.flow), random-init LDA. ``--gpus N`` outside torchrun re-launches itself
+under ``torch.distributed.run`` (a child process, started before anything touches the GPU).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import statistics
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-# Reference-equivalent CPU path (C++ variational-EM lda est on this host's 8 cores, same synthetic
-# 12.5M-flow day): flows × EM iterations / s. BASELINE.md "Measured baselines";
-# profiles/r1_cpu_baseline_12.5M.json; reproduce with bench/cpu_baseline.py.
-BASELINE_RECORDS_PER_SEC = 889_887.5
+METRIC = "netflow records scored/sec (whole node) + Gibbs iters/sec, 20-topic LDA"
 
 
-def main(argv=None) -> int:
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--mode", choices=["pipeline", "sweep"], default="pipeline")
+    ap.add_argument("--sweeps", type=int, default=200, help="Gibbs sweeps per pipeline step (oni-ml default)")
     ap.add_argument("--flows-per-gpu", type=int, default=12_500_000)
+    ap.add_argument("--events-per-gpu", type=int, default=2_000_000, help="dns/proxy events per GPU")
     ap.add_argument("--topics", type=int, default=None)
     ap.add_argument("--source", choices=["flow", "dns", "proxy"], default="flow")
-    ap.add_argument("--score-path", choices=["tiles", "pairs", "pairs_unsorted", "gather"], default="pairs",
-                    help="tiles: distinct pairs as 16x16 MFMA blocks; pairs: per-pair VALU dots; "
-                         "gather: per-event θ/φ row gathers (tiles/pairs + 4-B per-event pair gathers)")
-    ap.add_argument("--events-per-gpu", type=int, default=2_000_000, help="dns/proxy events per GPU")
+    ap.add_argument("--from-pcap", action="store_true",
+                    help="dns: every step decodes the shard's pcap file (config 3 'pcap→word pipeline')")
     ap.add_argument("--chunk-len", type=int, default=0, help="0 = auto (global token count)")
     ap.add_argument("--maxresults", type=int, default=3000)
     ap.add_argument("--seed", type=int, default=7)
@@ -51,7 +61,28 @@ def main(argv=None) -> int:
     a = ap.parse_args(argv)
     a.topics_set = a.topics is not None
     if a.topics is None:
-        a.topics = 20
+        a.topics = 20 if a.source != "dns" else 50
+    return a
+
+
+def relaunch(n: int, argv: list[str]) -> int:
+    """Start N ranks under torch.distributed.run as a CHILD process (never an exec)."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    a = parse(argv)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return relaunch(a.gpus, argv)
 
     # the contract is ONE JSON line on stdout: keep the real stdout for it and send everything else
     # written to fd 1 (RCCL's version banner at communicator creation, library chatter) to stderr
@@ -61,140 +92,223 @@ def main(argv=None) -> int:
 
     import torch
 
-    from oni355.utils.obs import stack_dumps_from_env
+    from oni355.utils.obs import stack_dumps_from_env, heartbeat_from_env
     stack_dumps_from_env()
+    heartbeat_from_env()
 
     from oni355.parallel import comm as pc
-    from oni355.pipeline import common
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus:
-        if a.gpus > 1:
-            print(f"bench: --gpus {a.gpus} but WORLD_SIZE={world}; launch with torch.distributed.run", file=sys.stderr)
-            return 2
+        print(f"bench: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
     if a.no_graph:
         os.environ["ONI_NO_GRAPH"] = "1"
     comm = pc.init_from_env(a.device)
+    try:
+        out = run_sweep_mode(a, comm) if a.mode == "sweep" else run_pipeline_mode(a, comm)
+    finally:
+        pass
+    if comm.rank == 0:
+        print(json.dumps(out), file=json_out, flush=True)
+    pc.shutdown()
+    return 0
+
+
+def _sync(dev):
+    import torch
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def _median_timings(per_step: list[dict]) -> dict:
+    keys = [k for k in per_step[0] if k.endswith("_s")]
+    return {k: round(statistics.median(t[k] for t in per_step), 5) for k in keys}
+
+
+# -------------------------------------------------------------------------------------------------
+def make_shard(a, comm):
+    """This rank's shard of the synthetic day (host columns) + its global row offset."""
+    rank, world = comm.rank, comm.world
+    per = a.flows_per_gpu if a.source == "flow" else a.events_per_gpu
+    n_total = per * world
+    if a.source == "flow":
+        from oni355.synth.flow import generate_flows
+        day = generate_flows(per, seed=a.seed, rank=rank, n_hosts=max(64, n_total // 25))
+    elif a.source == "dns":
+        from oni355.synth.dns import generate_dns
+        day = generate_dns(per, seed=a.seed, rank=rank, n_clients=max(32, n_total // 40))
+    else:
+        from oni355.synth.proxy import generate_proxy
+        day = generate_proxy(per, seed=a.seed, rank=rank, n_clients=max(32, n_total // 40))
+    return day, per, n_total
+
+
+def run_pipeline_mode(a, comm) -> dict:
+    import torch
+
+    from oni355 import schema
+    from oni355.io import results as rio
+
     dev = comm.device
     rank, world = comm.rank, comm.world
-
-    def sync():
-        if dev.type == "cuda":
-            torch.cuda.synchronize(dev)
-
     t_setup = time.perf_counter()
-    from oni355 import ops
-    from oni355.pipeline.synthetic import build_source
-    # flows: hosts scale with the node-wide day so N=8 is one 100M-flow day split over 8 ranks
-    per = a.flows_per_gpu if a.source == "flow" else a.events_per_gpu
-    K = a.topics if (a.source == "flow" or a.topics_set) else 50
-    su = build_source(a.source, per, K, comm, seed=a.seed, chunk_len=a.chunk_len)
-    n_total, day, sides, vocab, run = su.n_total, su.day, su.sides, su.vocab, su.run
-    model = run.model
-    model.initialize()
-    sync()
+    day, per, n_total = make_shard(a, comm)
+    row_off = rank * per
+    tmp = tempfile.mkdtemp(prefix="oni_bench_")
+    pcap = None
+    if a.source == "dns" and a.from_pcap:
+        from oni355.synth.dns import write_pcap
+        pcap = os.path.join(tmp, f"dns_rank{rank}.pcap")
+        write_pcap(day, pcap)
+    top = day.top_domains if a.source == "dns" else None
     setup_s = time.perf_counter() - t_setup
 
-    # ---- warmup + timed sweeps -----------------------------------------------------------------
-    model.sweep(a.warmup)
-    sync()
-    comm.barrier()
-    sync()
-    t0 = time.perf_counter()
-    model.sweep(a.steps)
-    sync()
-    comm.barrier()
-    sync()
-    dt = time.perf_counter() - t0
-    dt = comm.allreduce_scalar(dt, "max")
+    kw = dict(K=a.topics, sweeps=a.sweeps, tol=1.0, maxresults=a.maxresults, chunk_len=a.chunk_len, device=dev,
+              comm=comm, row_offset=row_off)
 
-    # ---- post-LDA scoring pass (records scored/s), timed separately --------------------------
-    dkeys, theta = common.gather_theta(run, comm)
-    phi = model.phi()
-    # distinct (doc, word) pairs + per-endpoint pair index: built once per day (corpus dictionaries)
-    plans = {"tiles": common.score_plan(dkeys, vocab, sides, tiles=True),
-             "pairs": common.score_plan(dkeys, vocab, sides, tiles=False),
-             "pairs_unsorted": common.score_plan(dkeys, vocab, sides, tiles=False, sort_events=False)}
-    lk = [(common.lookup(dkeys, dk_), common.lookup(vocab, wk_)) for dk_, wk_ in sides]
-
-    def score_once(path):
-        hist = torch.zeros(2048, dtype=torch.int32, device=dev)
-        if path in plans:
-            sc, _, _ = common.plan_score(theta, phi, plans[path], 1.0, hist=hist)
-        elif len(lk) == 2:
-            sc, _, _ = ops.score(theta, phi, lk[0][0], lk[0][1], lk[1][0], lk[1][1], tol=1.0, hist=hist)
+    def step():
+        t0 = time.perf_counter()
+        if a.source == "flow":
+            from oni355.pipeline.flow import run_flow
+            cols = day.cols
+            res = run_flow(cols, **kw)
+        elif a.source == "dns":
+            from oni355.pipeline.dns import run_dns
+            if pcap is not None:
+                from oni355.io.decoders import read_pcap_dns
+                cols = read_pcap_dns(pcap)
+            else:
+                cols = day.cols
+            t_dec = time.perf_counter() - t0
+            res = run_dns(cols, top_domains=top, user_domain="intel", **kw)
+            res.timings["decode_s"] = t_dec
         else:
-            sc, _, _ = ops.score(theta, phi, lk[0][0], lk[0][1], tol=1.0, hist=hist)
-        order = plans[path].order if path in plans else None
-        return common.top_n(sc, 1.0, a.maxresults, comm, rank * per, hist=hist, order=order)
-
-    def time_path(path, reps=5):
-        score_once(path)
-        sync()
-        comm.barrier()
+            from oni355.pipeline.proxy import run_proxy
+            cols = day.cols
+            res = run_proxy(cols, **kw)
         t1 = time.perf_counter()
-        for _ in range(reps):
-            res = score_once(path)
-        sync()
-        comm.barrier()
-        return comm.allreduce_scalar((time.perf_counter() - t1) / reps, "max"), res
+        rendered = rio.render_result(a.source, cols, res, row_off, comm)
+        if rank == 0:
+            rio.write_csv(os.path.join(tmp, f"{a.source}_results.csv"), schema.result_columns(a.source), rendered)
+        res.timings["results_s"] = time.perf_counter() - t1
+        return res
 
-    score_ab = {p: round(time_path(p)[0] * 1e3, 3) for p in ("tiles", "pairs", "pairs_unsorted", "gather")
-                if p != a.score_path}
-    score_dt, (rows, scs) = time_path(a.score_path)
-    plan = plans["tiles"]
-    ll = model.log_likelihood()
+    for _ in range(a.warmup):
+        step()
+    _sync(dev)
+    comm.barrier()
+    _sync(dev)
+    per_step, res = [], None
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        ts = time.perf_counter()
+        res = step()
+        res.timings["step_s"] = time.perf_counter() - ts
+        per_step.append(res.timings)
+    _sync(dev)
+    comm.barrier()
+    _sync(dev)
+    dt = comm.allreduce_scalar(time.perf_counter() - t0, "max")
 
-    tokens_local = run.corpus.T
-    tokens = int(comm.allreduce_scalar(tokens_local, "sum"))
-    ms = dt / a.steps * 1e3
-    value = n_total * a.steps / dt
-    planted = day.anomaly_rows + rank * per
-    hits = np.isin(planted, rows.cpu().numpy()[: a.maxresults])
+    med = _median_timings(per_step)
+    # device time of the in-step training on a GPU (HIP events), host wall time on the CPU path
+    train_s = comm.allreduce_scalar(med.get("train_dev_s", med.get("train_s", 0.0)), "max")
+    model = res.lda.model
+    tokens = int(comm.allreduce_scalar(res.lda.corpus.T, "sum"))
+    planted = day.anomaly_rows + row_off
+    hits = np.isin(planted, res.rows[: a.maxresults])
     hit_frac = comm.allreduce_scalar(float(hits.sum()), "sum") / max(comm.allreduce_scalar(float(planted.size), "sum"), 1)
-    metric = "netflow records scored/sec (whole node) + Gibbs iters/sec, 20-topic LDA"
-    if a.source != "flow":
-        metric = f"{a.source} records scored/sec (whole node) + Gibbs iters/sec, {K}-topic LDA"
-    out = {
+    value = n_total * a.steps / dt
+    K = a.topics
+    metric = METRIC if a.source == "flow" else f"{a.source} records scored/sec (whole node) + Gibbs iters/sec, {K}-topic LDA"
+    baseline_cfg = {"flow": "Netflow 100M flows, 20 topics, DP=8 (N=8); weak-scaled 12.5M flows/GPU",
+                    "dns": "DNS suspicious-connects (pcap->word pipeline), 50 topics",
+                    "proxy": "proxy suspicious-connects"}[a.source]
+    return {
         "metric": metric,
         "value": round(value, 1),
         "unit": "records/s",
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
-        "ms_per_step": round(ms, 4),
+        "ms_per_step": round(dt / a.steps * 1e3, 3),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": round(value / BASELINE_RECORDS_PER_SEC, 1) if a.source == "flow" else None,
+        # the reference publishes no number (BASELINE.md); the CPU reference-equivalent
+        # measurement lives in BASELINE.md and is not comparable work per iteration
+        "vs_baseline": None,
         "dtype": "fp32",
-        "data": f"synthetic {a.source} (oni355.synth.{a.source}: random-init topic priors, Zipf hosts, planted anomalies)",
+        "data": f"synthetic {a.source} (oni355.synth.{a.source}: random-init topic priors, Zipf hosts, planted anomalies)"
+                + (", decoded from pcap every step" if pcap else ""),
         "config": {"model": f"oni-suspicious-connects-{a.source}-lda", "topics": K, "global_batch": n_total,
                    "events_per_gpu": per, "seq_len": 2 if a.source == "flow" else 1, "parallelism": f"dp{world}",
-                   "baseline_config": ("Netflow 100M flows, 20 topics, DP=8 (N=8); weak-scaled 12.5M flows/GPU"
-                                       if a.source == "flow" else
-                                       "DNS suspicious-connects (pcap->word pipeline), 50 topics"
-                                       if a.source == "dns" else "proxy suspicious-connects")},
+                   "sweeps_per_step": a.sweeps, "maxresults": a.maxresults, "baseline_config": baseline_cfg},
+        "step": "one full oni-ml day run per step: host columns -> H2D -> featurize -> corpus -> "
+                f"{a.sweeps} Gibbs sweeps -> score -> top-{a.maxresults} -> CSV rows",
+        "gibbs_iters_per_sec": round(a.sweeps / train_s, 2) if train_s > 0 else None,
+        "ms_per_sweep_in_training": round(train_s / a.sweeps * 1e3, 4) if train_s > 0 else None,
+        "tokens_per_sec_training": round(tokens * a.sweeps / train_s, 1) if train_s > 0 else None,
+        "stage_median_s": med,
+        "tokens": tokens,
+        "vocab": int(res.lda.vocab.numel()),
+        "docs_local": res.lda.corpus.D,
+        "loglik": model.likelihoods[-1][1] if model.likelihoods else None,
+        "planted_anomaly_recall_topN": round(hit_frac, 4),
+        "setup_s": round(setup_s, 2),
+        "allreduce_ms_per_sweep": model.allreduce_ms_per_sweep(),
+        "allreduce_bytes_per_sweep": model.allreduce_bytes_per_sweep(),
+    }
+
+
+# -------------------------------------------------------------------------------------------------
+def run_sweep_mode(a, comm) -> dict:
+    """Bare sweeps of an already built model (round-1 measurement): flows × sweeps / s."""
+    from oni355.pipeline.synthetic import build_source
+    dev = comm.device
+    world = comm.world
+    t_setup = time.perf_counter()
+    per = a.flows_per_gpu if a.source == "flow" else a.events_per_gpu
+    su = build_source(a.source, per, a.topics, comm, seed=a.seed, chunk_len=a.chunk_len)
+    model = su.run.model
+    model.initialize()
+    _sync(dev)
+    setup_s = time.perf_counter() - t_setup
+    model.sweep(a.warmup)
+    _sync(dev)
+    comm.barrier()
+    _sync(dev)
+    t0 = time.perf_counter()
+    model.sweep(a.steps)
+    _sync(dev)
+    comm.barrier()
+    _sync(dev)
+    dt = comm.allreduce_scalar(time.perf_counter() - t0, "max")
+    tokens = int(comm.allreduce_scalar(su.run.corpus.T, "sum"))
+    return {
+        "metric": f"{a.source} record-sweeps/sec (whole node), {a.topics}-topic collapsed-Gibbs LDA",
+        "value": round(su.n_total * a.steps / dt, 1),
+        "unit": "records*sweeps/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(dt / a.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": f"synthetic {a.source}",
+        "config": {"model": f"oni-suspicious-connects-{a.source}-lda", "topics": a.topics, "global_batch": su.n_total,
+                   "seq_len": 2 if a.source == "flow" else 1, "parallelism": f"dp{world}"},
+        "step": f"one Gibbs sweep (sweeps {a.warmup + 1}..{a.warmup + a.steps} after init)",
         "gibbs_iters_per_sec": round(a.steps / dt, 3),
         "tokens_per_sec": round(tokens * a.steps / dt, 1),
         "tokens": tokens,
-        "vocab": int(vocab.numel()),
-        "docs_local": run.corpus.D,
-        "score_records_per_sec": round(n_total / score_dt, 1),
-        "score_ms": round(score_dt * 1e3, 3),
-        "score_path": a.score_path,
-        "score_ms_other_paths": score_ab,
-        "score_pairs": plan.n_pairs,
-        "score_mfma_items": plan.tiles.n_items,
-        "score_mfma_block_density": round(plan.tiles.density(), 4),
-        "loglik": ll,
-        "planted_anomaly_recall_topN": round(hit_frac, 4),
+        "vocab": int(su.vocab.numel()),
         "setup_s": round(setup_s, 2),
-        "allreduce_s_per_sweep": (model.timings["allreduce_s"] / max(model.timings["allreduce_calls"], 1)),
+        "allreduce_ms_per_sweep": model.allreduce_ms_per_sweep(),
+        "allreduce_bytes_per_sweep": model.allreduce_bytes_per_sweep(),
     }
-    if rank == 0:
-        print(json.dumps(out), file=json_out, flush=True)
-    pc.shutdown()
-    return 0
 
 
 if __name__ == "__main__":

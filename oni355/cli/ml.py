@@ -186,29 +186,13 @@ def main(argv=None) -> int:
     if a.source == "flow":
         from ..pipeline.flow import run_flow
         res = run_flow(cols, **common_kw)
-        rows_local = res.rows - row_off
-        mine = (rows_local >= 0) & (rows_local < len(cols["sip"]))
-        rendered = rio.flow_rows(cols, rows_local[mine], res.src_words[mine], res.dst_words[mine],
-                                 res.src_scores[mine], res.dst_scores[mine], res.scores[mine])
+    elif a.source == "dns":
+        from ..pipeline.dns import run_dns
+        res = run_dns(cols, top_domains=top, user_domain=cfg.USER_DOMAIN, **common_kw)
     else:
-        if a.source == "dns":
-            from ..pipeline.dns import run_dns, word_str
-            res = run_dns(cols, top_domains=top, user_domain=cfg.USER_DOMAIN, **common_kw)
-        else:
-            from ..pipeline.proxy import run_proxy, word_str
-            res = run_proxy(cols, top_domains=top, **common_kw)
-        ncol = len(cols["ip_dst" if a.source == "dns" else "clientip"])
-        rows_local = res.rows - row_off
-        mine = (rows_local >= 0) & (rows_local < ncol)
-        rendered = rio.event_rows(a.source, cols, rows_local[mine], [word_str(w) for w in res.words[mine]],
-                                  res.scores[mine])
-    gids = res.rows[mine].tolist()
-    if world > 1:
-        import torch.distributed as dist
-        allp = [None] * world
-        dist.all_gather_object(allp, (gids, rendered))
-        by_gid = {g: r for gl, rl in allp for g, r in zip(gl, rl)}
-        rendered = [by_gid[int(g)] for g in res.rows.tolist()]
+        from ..pipeline.proxy import run_proxy
+        res = run_proxy(cols, top_domains=top, **common_kw)
+    rendered = rio.render_result(a.source, cols, res, row_off, comm)
     out = None
     if rank == 0:
         from .. import schema

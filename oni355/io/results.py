@@ -72,6 +72,36 @@ def event_rows(source: str, cols: dict, local_rows, words: list[str], scores) ->
     return out
 
 
+def render_result(source: str, cols: dict, res, row_off: int, comm=None) -> list[list]:
+    """Result rows of a pipeline run (FlowResult / SingleResult) as CSV fields, ascending score.
+
+    Each rank renders the result rows it holds (``cols`` is its shard, starting at global row
+    ``row_off``); with a process group the rendered rows are gathered (collective X06's payload)
+    and every rank returns the full, globally ordered list."""
+    rows_local = res.rows - row_off
+    if source == "flow":
+        mine = (rows_local >= 0) & (rows_local < len(cols["sip"]))
+        rendered = flow_rows(cols, rows_local[mine], res.src_words[mine], res.dst_words[mine],
+                             res.src_scores[mine], res.dst_scores[mine], res.scores[mine])
+    else:
+        if source == "dns":
+            from ..pipeline.dns import word_str
+        else:
+            from ..pipeline.proxy import word_str
+        ncol = len(cols["ip_dst" if source == "dns" else "clientip"])
+        mine = (rows_local >= 0) & (rows_local < ncol)
+        rendered = event_rows(source, cols, rows_local[mine], [word_str(w) for w in res.words[mine]],
+                              res.scores[mine])
+    if comm is None or not comm.dist:
+        return rendered
+    import torch.distributed as dist
+    gids = res.rows[mine].tolist()
+    allp = [None] * comm.world
+    dist.all_gather_object(allp, (gids, rendered), group=comm.group)
+    by_gid = {g: r for gl, rl in allp for g, r in zip(gl, rl)}
+    return [by_gid[int(g)] for g in res.rows.tolist()]
+
+
 def write_csv(path: str, header: list[str], rows: list[list], with_header: bool = True) -> str:
     os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
     tmp = path + ".tmp"

@@ -16,7 +16,6 @@ from __future__ import annotations
 
 import math
 import os
-import time
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -140,7 +139,10 @@ class GibbsLDA:
         self._graph = None
         self._graphs: dict = {}
         self._watchdog = fault.Watchdog.from_env()
-        self.timings = {"allreduce_s": 0.0, "allreduce_calls": 0}
+        self.timings = {"allreduce_calls": 0}
+        self._ar_events: list = []
+        self._capturing = False
+        self._corrupted = False
 
     # ---------------------------------------------------------------------------------------------
     def _state(self, init: bool) -> dict:
@@ -270,19 +272,67 @@ class GibbsLDA:
             ops.delta_recount(c.wslot, c.tile_wlo, c.tile_whi, self.chg_mask, c.tok_word, self.tok_z, self.tok_zprev,
                               head, self.KS, self.G)
         if self.comm is not None and self.comm.dist:
-            t0 = time.perf_counter()
-            self.comm.allreduce_(self.dn[self.b])
-            self.timings["allreduce_s"] += time.perf_counter() - t0
-            self.timings["allreduce_calls"] += 1
+            self._allreduce_dn(self.dn[self.b])
         ops.gibbs_apply(self.nwk, self.dn[self.b], self.dn[1 - self.b], self.nk[self.cn], self.nk[1 - self.cn],
                         self.q, self.V, self.K, self.KS, self.beta, self.vbeta, self.sweep_ctr, bump=True,
                         absolute=mode in (0, 3))
         self.a, self.b, self.cn = 1 - self.a, 1 - self.b, 1 - self.cn
         self.sweeps_done += 1
 
+    def _allreduce_dn(self, buf: torch.Tensor) -> None:
+        """X01: all-reduce of the sweep's Δ buffer (Δn_wk ‖ Δn_k replicas ‖ aux words).
+
+        Eager calls are bracketed by HIP events on the compute stream (the RCCL kernel runs on
+        the process group's stream, which the compute stream waits on), so the recorded time is
+        the device-side time the sweep spends in the collective. Graph-captured sweeps cannot
+        carry timing events; :meth:`allreduce_ms_per_sweep` then probes the same payload."""
+        timed = (self.device.type == "cuda" and not self._capturing and len(self._ar_events) < 64)
+        if timed:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+        self.comm.allreduce_(buf)
+        if timed:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self._ar_events.append((e0, e1))
+        self.timings["allreduce_calls"] += 1
+
+    def allreduce_bytes_per_sweep(self) -> int:
+        """Bytes each rank contributes to X01 per sweep (0 without a process group)."""
+        if self.comm is None or not self.comm.dist:
+            return 0
+        return int(self.dn[0].numel() * self.dn[0].element_size())
+
+    def allreduce_ms_per_sweep(self, probe_reps: int = 20) -> float | None:
+        """Median device time of the per-sweep Δ all-reduce (ms). Uses the events of eager sweeps;
+        when every sweep ran inside a HIP graph, probes ``probe_reps`` all-reduces of a scratch
+        buffer of the same size. None without a process group or off-GPU."""
+        if self.comm is None or not self.comm.dist or self.device.type != "cuda":
+            return None
+        times = []
+        if self._ar_events:
+            self._ar_events[-1][1].synchronize()
+            times = [a.elapsed_time(b) for a, b in self._ar_events]
+        if not times:
+            scratch = torch.zeros_like(self.dn[0])
+            for _ in range(probe_reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                self.comm.allreduce_(scratch)
+                e1.record()
+                times.append((e0, e1))
+            times[-1][1].synchronize()
+            times = [a.elapsed_time(b) for a, b in times]
+        return round(float(np.median(times)), 4)
+
     def _graphable(self) -> bool:
-        return (self.cfg.use_graph and self.device.type == "cuda" and (self.comm is None or not self.comm.dist)
-                and os.environ.get("ONI_NO_GRAPH", "0") != "1")
+        if not (self.cfg.use_graph and self.device.type == "cuda" and os.environ.get("ONI_NO_GRAPH", "0") != "1"):
+            return False
+        if self.comm is None or not self.comm.dist:
+            return True
+        # RCCL collectives are captured into the sweep graph (the communicator exists: initialize()
+        # already all-reduced n_wk); gloo routes through host copies and cannot be captured
+        return self.comm.graph_capturable() and os.environ.get("ONI_DIST_GRAPH", "1") != "0"
 
     def _capture(self, mode: int):
         """Capture two sweeps of count mode ``mode`` (parities return to their start) into one HIP graph."""
@@ -294,10 +344,16 @@ class GibbsLDA:
         s.wait_stream(torch.cuda.current_stream(self.device))
         g = torch.cuda.CUDAGraph()
         # capture does not execute: the host-side parities are rewound afterwards
-        with torch.cuda.stream(s):
-            with torch.cuda.graph(g, stream=s):
-                self._one_sweep()
-                self._one_sweep()
+        calls = self.timings["allreduce_calls"]
+        self._capturing = True
+        try:
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s):
+                    self._one_sweep()
+                    self._one_sweep()
+        finally:
+            self._capturing = False
+            self.timings["allreduce_calls"] = calls
         torch.cuda.current_stream(self.device).wait_stream(s)
         self.a, self.b, self.cn, self.sweeps_done, self._aux_synced = saved
         self._force_mode = None
@@ -308,16 +364,41 @@ class GibbsLDA:
     @traced("oni:lda.sweeps")
     def sweep(self, n: int = 1) -> None:
         """Run ``n`` sweeps (graph-replayed in same-mode pairs on a single GPU)."""
-        fault.maybe_inject(self.sweeps_done, self.comm.rank if self.comm else 0)
+        fault.maybe_inject(self.sweeps_done, self.comm.rank if self.comm else 0, corrupt=self._corrupt)
         if self._graph is None:
             self._graphs = {}
         if self._watchdog is not None:
-            self._watchdog.kick()
-        self._sweep_n(n)
-        if self._watchdog is not None:
-            self._watchdog.kick()
+            self._watchdog.arm()
+        try:
+            self._sweep_n(n)
+        finally:
+            if self._watchdog is not None:
+                self._watchdog.disarm()
         if self.cfg.check_invariants:
             self.check_invariants()
+        if self._corrupted:
+            self.check_health()
+
+    def _corrupt(self) -> None:
+        """ONI_FAULT kind:nan -- poison the state the way a bad DMA / bit flip would."""
+        self.nwk[0, 0] = -1 - self.nwk[0, 0].abs()
+        self.q[0, 0] = float("nan")
+        self._corrupted = True
+
+    def check_health(self) -> None:
+        """Cheap numerical health check: finite q table, no negative topic totals. Raises
+        fault.NumericalFault (the supervisor then restarts from the last good checkpoint)."""
+        bad_q = not bool(torch.isfinite(self.q[:, : self.K]).all())
+        bad_n = bool((self.nk_cur[: self.K] < 0).any()) or bool((self.nwk[:, : self.K] < 0).any())
+        if bad_q or bad_n:
+            raise fault.NumericalFault(f"corrupt model state after sweep {self.sweeps_done}: "
+                                       f"non-finite q={bad_q}, negative counts={bad_n}")
+
+    def close(self) -> None:
+        """Stop the watchdog thread (training finished)."""
+        if self._watchdog is not None:
+            self._watchdog.close()
+            self._watchdog = None
 
     def check_invariants(self) -> None:
         """Debug-mode count invariants: Σn_wk = Σn_k = global tokens, Σn_dk = local
@@ -366,6 +447,8 @@ class GibbsLDA:
             self._aux_synced = self._keeps_aux(m1)
             self._note_changes()
             done += 2
+            if self._watchdog is not None:
+                self._watchdog.kick()
 
     # ---------------------------------------------------------------------------------------------
     @property
@@ -407,6 +490,8 @@ class GibbsLDA:
 
     def record_likelihood(self) -> float:
         ll = self.log_likelihood()
+        if not math.isfinite(ll):
+            raise fault.NumericalFault(f"non-finite log-likelihood {ll} after sweep {self.sweeps_done}")
         self.likelihoods.append((self.sweeps_done, ll))
         return ll
 

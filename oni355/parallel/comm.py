@@ -53,7 +53,8 @@ class Comm:
         a = np.asarray(a)
         if not self.dist:
             return a
-        t = torch.from_numpy(np.ascontiguousarray(a)).to(self._coll_device)
+        # a private copy: on CPU collectives torch.from_numpy would alias (and reduce into) ``a``
+        t = torch.from_numpy(np.array(a, copy=True)).to(self._coll_device)
         dist.all_reduce(t, group=self.group)
         return t.cpu().numpy()
 
@@ -81,6 +82,11 @@ class Comm:
             else:
                 dist.broadcast(t, src=src, group=self.group)
         return t
+
+    def graph_capturable(self) -> bool:
+        """Can this communicator's device collectives be captured into a HIP graph? (RCCL on
+        device tensors: yes; gloo, including gloo-through-host-copies: no.)"""
+        return self.device.type == "cuda" and self.backend == "nccl" and not self._via_host
 
     @property
     def _coll_device(self) -> torch.device:
@@ -129,6 +135,11 @@ def init_from_env(device_type: str | None = None, timeout_s: float = 600.0) -> C
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if device_type is None:
         device_type = "cuda" if torch.cuda.is_available() else "cpu"
+    # ONI_DIST_BACKEND=gloo with device tensors: several ranks may share one GPU (shard emulation,
+    # SURVEY §4.3) -- ranks map onto the visible devices round-robin; RCCL needs one GPU per rank
+    backend = os.environ.get("ONI_DIST_BACKEND") or ("nccl" if device_type == "cuda" else "gloo")
+    if device_type == "cuda" and backend == "gloo":
+        local %= max(torch.cuda.device_count(), 1)
     device = torch.device(device_type, local) if device_type == "cuda" else torch.device("cpu")
     if device_type == "cuda":
         torch.cuda.set_device(device)
@@ -139,9 +150,6 @@ def init_from_env(device_type: str | None = None, timeout_s: float = 600.0) -> C
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29531")
     os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
-    # ONI_DIST_BACKEND=gloo with device tensors: several ranks may share one GPU (shard emulation,
-    # SURVEY §4.3); RCCL needs one GPU per rank
-    backend = os.environ.get("ONI_DIST_BACKEND") or ("nccl" if device_type == "cuda" else "gloo")
     if not dist.is_initialized():
         kw = {}
         if device_type == "cuda" and backend == "nccl":

@@ -9,14 +9,13 @@ sample -- are independent of the GPU count.
 """
 from __future__ import annotations
 
-import time
 from dataclasses import dataclass, field
 
 import numpy as np
 import torch
 
 from .. import ops
-from ..utils.obs import traced
+from ..utils.obs import StageTimer, traced
 from ..models.corpus import Corpus, auto_chunk_len, build_corpus
 from ..models.gibbs import GibbsConfig, GibbsLDA
 from ..parallel.comm import Comm
@@ -112,58 +111,65 @@ class LdaRun:
 def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor, weights: torch.Tensor | None,
                     vocab: torch.Tensor, K: int, alpha: float | None, beta: float, seed: int, sweeps: int,
                     chunk_len: int, comm: Comm | None, eval_every: int = 0, ckpt=None, log=None,
-                    train: bool = True) -> LdaRun:
-    """Token keys → owner routing → local corpus → Gibbs LDA trained for ``sweeps`` sweeps."""
-    t0 = time.perf_counter()
+                    train: bool = True, timer: StageTimer | None = None, ldac_dir: str | None = None,
+                    ldac_lag: int = 0) -> LdaRun:
+    """Token keys → owner routing → local corpus → Gibbs LDA trained for ``sweeps`` sweeps.
+
+    ``ldac_dir`` + ``ldac_lag`` > 0 emit lda-c ``NNN.{beta,gamma,other}`` snapshots every
+    ``ldac_lag`` sweeps (oni-lda-c's LAG); ``final.*`` is written by the caller."""
     dev = doc_keys64.device
-    word_ids = torch.searchsorted(vocab, word_keys64)
-    if weights is None:
-        weights = torch.ones_like(word_ids)
-    dk, wi, wt = route_to_owners(doc_keys64, word_ids, weights, comm)
-    udoc, inv = torch.unique(dk, return_inverse=True)
-    G, _ = ops.choose_tiling(K)
-    if chunk_len <= 0:
-        T_glob = float(wt.sum()) if wt.numel() else 0.0
-        if comm is not None and comm.dist:
-            T_glob = comm.allreduce_scalar(T_glob, "sum")
-        chunk_len = auto_chunk_len(int(T_glob), G)
-    use_w = bool((wt != 1).any()) if wt.numel() else False
-    corpus = build_corpus(inv, wi, int(udoc.numel()), int(vocab.numel()), i64_to_u32bits(udoc), G, chunk_len,
-                          weight=wt if use_w else None)
-    if dev.type == "cuda":
-        torch.cuda.synchronize(dev)
-    t1 = time.perf_counter()
-    model = GibbsLDA(corpus, GibbsConfig(K=K, alpha=alpha, beta=beta, seed=seed), comm=comm,
-                     V_global=int(vocab.numel()))
-    run = LdaRun(corpus, model, udoc, vocab, {"corpus_s": t1 - t0})
-    if not train:
-        return run
-    if ckpt is not None and ckpt.exists():
-        ckpt.restore(model)
-    else:
-        model.initialize()
-    t2 = time.perf_counter()
-    remaining = sweeps - model.sweeps_done
-    step = eval_every if eval_every > 0 else remaining
-    ck_every = ckpt.every if ckpt is not None and ckpt.every > 0 else 0
-    while remaining > 0:
-        n = min(step, remaining)
-        if ck_every:
-            n = min(n, ck_every - (model.sweeps_done % ck_every))
-        model.sweep(n)
-        remaining -= n
-        if eval_every > 0 and model.sweeps_done % eval_every == 0:
-            ll = model.record_likelihood()
-            if log:
-                log(f"sweep {model.sweeps_done} loglik {ll:.6e}")
-        if ck_every and model.sweeps_done % ck_every == 0:
-            ckpt.save(model)
-    if dev.type == "cuda":
-        torch.cuda.synchronize(dev)
-    t3 = time.perf_counter()
+    timer = timer or StageTimer(dev)
+    with timer.stage("corpus"):
+        word_ids = torch.searchsorted(vocab, word_keys64)
+        if weights is None:
+            weights = torch.ones_like(word_ids)
+        dk, wi, wt = route_to_owners(doc_keys64, word_ids, weights, comm)
+        udoc, inv = torch.unique(dk, return_inverse=True)
+        G, _ = ops.choose_tiling(K)
+        if chunk_len <= 0:
+            T_glob = float(wt.sum()) if wt.numel() else 0.0
+            if comm is not None and comm.dist:
+                T_glob = comm.allreduce_scalar(T_glob, "sum")
+            chunk_len = auto_chunk_len(int(T_glob), G)
+        use_w = bool((wt != 1).any()) if wt.numel() else False
+        corpus = build_corpus(inv, wi, int(udoc.numel()), int(vocab.numel()), i64_to_u32bits(udoc), G, chunk_len,
+                              weight=wt if use_w else None)
+    with timer.stage("init"):
+        model = GibbsLDA(corpus, GibbsConfig(K=K, alpha=alpha, beta=beta, seed=seed), comm=comm,
+                         V_global=int(vocab.numel()))
+        run = LdaRun(corpus, model, udoc, vocab, {})
+        if not train:
+            return run
+        if ckpt is not None and ckpt.exists():
+            ckpt.restore(model)
+        else:
+            model.initialize()
+    with timer.stage("train"):
+        remaining = sweeps - model.sweeps_done
+        step = eval_every if eval_every > 0 else remaining
+        ck_every = ckpt.every if ckpt is not None and ckpt.every > 0 else 0
+        lag = int(ldac_lag) if ldac_dir else 0
+        while remaining > 0:
+            n = min(step, remaining)
+            if ck_every:
+                n = min(n, ck_every - (model.sweeps_done % ck_every))
+            if lag:
+                n = min(n, lag - (model.sweeps_done % lag))
+            model.sweep(n)
+            remaining -= n
+            if eval_every > 0 and model.sweeps_done % eval_every == 0:
+                ll = model.record_likelihood()
+                if log:
+                    log(f"sweep {model.sweeps_done} loglik {ll:.6e}")
+            if ck_every and model.sweeps_done % ck_every == 0:
+                ckpt.save(model)
+            if lag and model.sweeps_done % lag == 0 and remaining > 0:
+                from ..io import ldac
+                ldac.export_gibbs(ldac_dir, model, prefix=f"{model.sweeps_done:03d}")
+    model.close()
     if not model.likelihoods or model.likelihoods[-1][0] != model.sweeps_done:
         model.record_likelihood()
-    run.timings.update({"init_s": t2 - t1, "train_s": t3 - t2, "sweeps": sweeps})
+    run.timings.update({"sweeps": sweeps})
     return run
 
 
@@ -372,34 +378,29 @@ class SingleResult:
 def run_single_doc_events(doc_keys64: torch.Tensor, word_keys64: torch.Tensor, K: int, sweeps: int, tol: float,
                           maxresults: int, alpha, beta: float, seed: int, chunk_len: int, comm: Comm | None,
                           feedback=None, row_offset: int = 0, eval_every: int = 0, ckpt=None, log=None,
-                          timings: dict | None = None) -> SingleResult:
+                          timer: StageTimer | None = None, ldac_dir: str | None = None,
+                          ldac_lag: int = 0) -> SingleResult:
     """Shared DNS/proxy path: one (doc, word) token per event; score = θ_doc·φ_word (C24)."""
-    t = dict(timings or {})
     dev = doc_keys64.device
-    sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
-    t0 = time.perf_counter()
-    dk, wk, wts = doc_keys64, word_keys64, None
-    if feedback is not None:
-        wts = torch.cat([torch.ones_like(wk), feedback[2]])
-        dk = torch.cat([dk, feedback[0]])
-        wk = torch.cat([wk, feedback[1]])
-    vocab = global_vocab(wk, comm)
-    sync()
-    t["vocab_s"] = time.perf_counter() - t0
+    timer = timer or StageTimer(dev)
+    with timer.stage("vocab"):
+        dk, wk, wts = doc_keys64, word_keys64, None
+        if feedback is not None:
+            wts = torch.cat([torch.ones_like(wk), feedback[2]])
+            dk = torch.cat([dk, feedback[0]])
+            wk = torch.cat([wk, feedback[1]])
+        vocab = global_vocab(wk, comm)
     run = build_and_train(dk, wk, wts, vocab, K, alpha, beta, seed, sweeps, chunk_len, comm, eval_every=eval_every,
-                          ckpt=ckpt, log=log)
+                          ckpt=ckpt, log=log, timer=timer, ldac_dir=ldac_dir, ldac_lag=ldac_lag)
+    with timer.stage("score_prep"):
+        dkeys, theta = gather_theta(run, comm)
+        plan = score_plan(dkeys, vocab, [(doc_keys64, word_keys64)])
+    with timer.stage("score"):
+        hist = torch.zeros(2048, dtype=torch.int32, device=dev)
+        score, _, _ = plan_score(theta, run.model.phi(), plan, tol, hist=hist)
+        rows, scs = top_n(score, tol, maxresults, comm, row_offset, hist=hist, order=plan.order)
+    t = timer.summary()
     t.update(run.timings)
-    t0 = time.perf_counter()
-    dkeys, theta = gather_theta(run, comm)
-    plan = score_plan(dkeys, vocab, [(doc_keys64, word_keys64)])
-    sync()
-    t["score_prep_s"] = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    hist = torch.zeros(2048, dtype=torch.int32, device=dev)
-    score, _, _ = plan_score(theta, run.model.phi(), plan, tol, hist=hist)
-    rows, scs = top_n(score, tol, maxresults, comm, row_offset, hist=hist, order=plan.order)
-    sync()
-    t["score_s"] = time.perf_counter() - t0
     t["records_scored"] = int(doc_keys64.numel())
     loc = rows - row_offset
     mine = (loc >= 0) & (loc < doc_keys64.numel())

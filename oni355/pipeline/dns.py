@@ -11,14 +11,13 @@ Document = ``ip_dst`` (the client receiving the response).
 """
 from __future__ import annotations
 
-import time
 
 import numpy as np
 import torch
 
 from .. import ops
 from ..io import staging
-from ..utils.obs import traced
+from ..utils.obs import StageTimer, traced
 from ..ops import strings as sops
 from ..parallel.comm import Comm
 from ..ref import spec
@@ -104,13 +103,13 @@ def run_dns(cols: dict, K: int = 50, sweeps: int = 200, tol: float = 1.0, maxres
             alpha: float | None = None, beta: float = 0.01, seed: int = 0x0D15EA5E, chunk_len: int = 0,
             device="cpu", comm: Comm | None = None, top_domains=None, user_domain: str = "",
             feedback: dict | None = None, dupfactor: int = 1000, row_offset: int = 0, eval_every: int = 0,
-            ckpt=None, log=None) -> common.SingleResult:
-    t = {}
-    t0 = time.perf_counter()
-    d = to_device(cols, device)
-    topset = top_set(top_domains)
-    words, cuts, feats = featurize(d, comm, topset, user_domain)
-    t["featurize_s"] = time.perf_counter() - t0
+            ckpt=None, log=None, ldac_dir: str | None = None, ldac_lag: int = 0) -> common.SingleResult:
+    timer = StageTimer(device)
+    with timer.stage("h2d"):
+        d = to_device(cols, device)
+    with timer.stage("featurize"):
+        topset = top_set(top_domains)
+        words, cuts, feats = featurize(d, comm, topset, user_domain)
     docs = common.u32_to_i64(d["ip_dst"])
     fb = None
     if feedback and len(feedback.get("ip_dst", [])):
@@ -126,7 +125,7 @@ def run_dns(cols: dict, K: int = 50, sweeps: int = 200, tol: float = 1.0, maxres
         fb = (fdoc, fw, torch.full_like(fw, int(dupfactor)))
     res = common.run_single_doc_events(docs, words, K, sweeps, tol, maxresults, alpha, beta, seed, chunk_len, comm,
                                        feedback=fb, row_offset=row_offset, eval_every=eval_every, ckpt=ckpt, log=log,
-                                       timings=t)
+                                       timer=timer, ldac_dir=ldac_dir, ldac_lag=ldac_lag)
     res.stats["cuts"] = {k: [int(x) for x in v] for k, v in cuts.items()}
     res.stats["features"] = feats
     return res

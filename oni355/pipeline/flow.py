@@ -12,7 +12,6 @@ OniLDACWrapper/mpiexec lda est, FlowPostLDA) → getmerge flow_results.csv ([U-M
 """
 from __future__ import annotations
 
-import time
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -20,7 +19,7 @@ import torch
 
 from .. import ops
 from ..io import staging
-from ..utils.obs import traced
+from ..utils.obs import StageTimer, traced
 from ..parallel.comm import Comm
 from ..ref import spec
 from . import common
@@ -104,51 +103,42 @@ def feedback_tokens(fb_cols: dict | None, cuts: FlowCuts, device, dupfactor: int
 def run_flow(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxresults: int = 3000,
              alpha: float | None = None, beta: float = 0.01, seed: int = 0x0D15EA5E, chunk_len: int = 0,
              device="cpu", comm: Comm | None = None, feedback: dict | None = None, dupfactor: int = 1000,
-             row_offset: int = 0, eval_every: int = 0, ckpt=None, log=None) -> FlowResult:
+             row_offset: int = 0, eval_every: int = 0, ckpt=None, log=None, ldac_dir: str | None = None,
+             ldac_lag: int = 0) -> FlowResult:
     """Full suspicious-connects for one (rank-local shard of a) day of flows."""
-    t = {}
-    t0 = time.perf_counter()
-    d = to_device(cols, device)
-    sync = (lambda: torch.cuda.synchronize(device)) if torch.device(device).type == "cuda" else (lambda: None)
-    sync()
-    t["h2d_s"] = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    cuts = compute_cuts(d, comm)
-    sw, dw = wordify(d, cuts)
-    sync()
-    t["featurize_s"] = time.perf_counter() - t0
-
-    t0 = time.perf_counter()
-    doc_keys = torch.cat([common.u32_to_i64(d["sip"]), common.u32_to_i64(d["dip"])])
-    word_keys = torch.cat([common.u32_to_i64(sw), common.u32_to_i64(dw)])
-    weights = None
-    fb = feedback_tokens(feedback, cuts, device, dupfactor)
-    if fb is not None:
-        weights = torch.cat([torch.ones_like(word_keys), fb[2]])
-        doc_keys = torch.cat([doc_keys, fb[0]])
-        word_keys = torch.cat([word_keys, fb[1]])
-    vocab = common.global_vocab(word_keys, comm)
-    sync()
-    t["vocab_s"] = time.perf_counter() - t0
+    timer = StageTimer(device)
+    with timer.stage("h2d"):
+        d = to_device(cols, device)
+    with timer.stage("featurize"):
+        cuts = compute_cuts(d, comm)
+        sw, dw = wordify(d, cuts)
+    with timer.stage("vocab"):
+        doc_keys = torch.cat([common.u32_to_i64(d["sip"]), common.u32_to_i64(d["dip"])])
+        word_keys = torch.cat([common.u32_to_i64(sw), common.u32_to_i64(dw)])
+        weights = None
+        fb = feedback_tokens(feedback, cuts, device, dupfactor)
+        if fb is not None:
+            weights = torch.cat([torch.ones_like(word_keys), fb[2]])
+            doc_keys = torch.cat([doc_keys, fb[0]])
+            word_keys = torch.cat([word_keys, fb[1]])
+        vocab = common.global_vocab(word_keys, comm)
     run = common.build_and_train(doc_keys, word_keys, weights, vocab, K, alpha, beta, seed, sweeps, chunk_len, comm,
-                                 eval_every=eval_every, ckpt=ckpt, log=log)
-    t.update(run.timings)
+                                 eval_every=eval_every, ckpt=ckpt, log=log, timer=timer, ldac_dir=ldac_dir,
+                                 ldac_lag=ldac_lag)
 
     # ---- scoring --------------------------------------------------------------------------------
-    t0 = time.perf_counter()
-    dkeys, theta = common.gather_theta(run, comm)
-    phi = run.model.phi()
-    n = d["sip"].numel()
-    plan = common.score_plan(dkeys, vocab, [(common.u32_to_i64(d["sip"]), common.u32_to_i64(sw)),
-                                            (common.u32_to_i64(d["dip"]), common.u32_to_i64(dw))])
-    sync()
-    t["score_prep_s"] = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    hist = torch.zeros(2048, dtype=torch.int32, device=theta.device)
-    score, s1, s2 = common.plan_score(theta, phi, plan, tol, hist=hist, want_parts=True)
-    rows, scs = common.top_n(score, tol, maxresults, comm, row_offset, hist=hist, order=plan.order)
-    sync()
-    t["score_s"] = time.perf_counter() - t0
+    with timer.stage("score_prep"):
+        dkeys, theta = common.gather_theta(run, comm)
+        phi = run.model.phi()
+        n = d["sip"].numel()
+        plan = common.score_plan(dkeys, vocab, [(common.u32_to_i64(d["sip"]), common.u32_to_i64(sw)),
+                                                (common.u32_to_i64(d["dip"]), common.u32_to_i64(dw))])
+    with timer.stage("score"):
+        hist = torch.zeros(2048, dtype=torch.int32, device=theta.device)
+        score, s1, s2 = common.plan_score(theta, phi, plan, tol, hist=hist, want_parts=True)
+        rows, scs = common.top_n(score, tol, maxresults, comm, row_offset, hist=hist, order=plan.order)
+    t = timer.summary()
+    t.update(run.timings)
     t["records_scored"] = n
     # per-result parts (rows are global ids; each rank contributes its own rows)
     loc = rows - row_offset

@@ -11,14 +11,13 @@ Word (bit-packed u64, rendered ``top_tb_method_uab_ctype_eb_lb_respcode``):
 """
 from __future__ import annotations
 
-import time
 
 import numpy as np
 import torch
 
 from .. import ops
 from ..io import staging
-from ..utils.obs import traced
+from ..utils.obs import StageTimer, traced
 from ..ops import strings as sops
 from ..parallel.comm import Comm
 from ..ref import spec
@@ -134,14 +133,13 @@ def run_proxy(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxr
               alpha: float | None = None, beta: float = 0.01, seed: int = 0x0D15EA5E, chunk_len: int = 0,
               device="cpu", comm: Comm | None = None, top_domains=None, feedback: dict | None = None,
               dupfactor: int = 1000, row_offset: int = 0, eval_every: int = 0, ckpt=None,
-              log=None) -> common.SingleResult:
-    t = {}
-    t0 = time.perf_counter()
-    topset = top_set(top_domains)
-    words, cuts = featurize(cols, device, comm, topset)
-    dev = words.device
-    docs = staging.upload(np.asarray(cols["clientip"], np.uint32).astype(np.int64), dev)
-    t["featurize_s"] = time.perf_counter() - t0
+              log=None, ldac_dir: str | None = None, ldac_lag: int = 0) -> common.SingleResult:
+    timer = StageTimer(device)
+    with timer.stage("featurize"):
+        topset = top_set(top_domains)
+        words, cuts = featurize(cols, device, comm, topset)
+        dev = words.device
+        docs = staging.upload(np.asarray(cols["clientip"], np.uint32).astype(np.int64), dev)
     fb = None
     if feedback and len(feedback.get("clientip", [])):
         fw, _ = featurize(feedback, device, None, topset)
@@ -149,6 +147,6 @@ def run_proxy(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxr
         fb = (fdoc, fw, torch.full_like(fw, int(dupfactor)))
     res = common.run_single_doc_events(docs, words, K, sweeps, tol, maxresults, alpha, beta, seed, chunk_len, comm,
                                        feedback=fb, row_offset=row_offset, eval_every=eval_every, ckpt=ckpt, log=log,
-                                       timings=t)
+                                       timer=timer, ldac_dir=ldac_dir, ldac_lag=ldac_lag)
     res.stats["cuts"] = {k: [int(x) for x in v] for k, v in cuts.items()}
     return res

@@ -91,25 +91,42 @@ class Checkpointer:
         if man["ident"] != self._ident(model):
             raise ValueError(f"checkpoint identity {man['ident']} != run {self._ident(model)}")
         sweep = int(man["sweep"])
-        by_key: dict[int, torch.Tensor] = {}
+        c = model.c
+        mask = 0xFFFFFFFF
+        my_keys = c.doc_keys.cpu().to(torch.int64) & mask
+        my_ptr = c.doc_tok_ptr.cpu().to(torch.int64)
+        my_len = my_ptr[1:] - my_ptr[:-1]
+        z = torch.zeros(int(my_ptr[-1]) if my_ptr.numel() else 0, dtype=torch.uint8)
+        found = torch.zeros(my_keys.numel(), dtype=torch.bool)
+        # vectorised: every shard's documents are matched to this rank's by key (searchsorted) and
+        # their token ranges copied with one index gather; shards holding none of them are skipped
         for p in sorted(glob.glob(os.path.join(self.dir, f"ckpt_s{sweep}_r*of{man['world']}.pt"))):
             d = torch.load(p, weights_only=True)
-            keys = d["doc_keys"].tolist()
-            ptr = d["doc_tok_ptr"]
-            z = d["z"]
-            for i, k in enumerate(keys):
-                by_key[k] = z[int(ptr[i]): int(ptr[i + 1])]
             if "likelihoods" in d and not model.likelihoods:
                 model.likelihoods = [tuple(x) for x in d["likelihoods"]]
-        c = model.c
-        parts = []
-        ptr = c.doc_tok_ptr.cpu()
-        for i, k in enumerate(c.doc_keys.cpu().tolist()):
-            zz = by_key.get(k)
-            n = int(ptr[i + 1] - ptr[i])
-            if zz is None or zz.numel() != n:
-                raise ValueError(f"checkpoint does not match corpus (doc key {k & 0xFFFFFFFF})")
-            parts.append(zz)
-        z = torch.cat(parts) if parts else torch.zeros(0, dtype=torch.uint8)
+            keys = d["doc_keys"].to(torch.int64) & mask
+            if keys.numel() == 0 or my_keys.numel() == 0:
+                continue
+            ptr = d["doc_tok_ptr"].to(torch.int64)
+            order = torch.argsort(keys)
+            sk = keys[order]
+            pos = torch.searchsorted(sk, my_keys).clamp_(max=sk.numel() - 1)
+            hit = sk[pos] == my_keys
+            if not bool(hit.any()):
+                continue
+            dst = torch.nonzero(hit).flatten()
+            src = order[pos[dst]]
+            lens = ptr[src + 1] - ptr[src]
+            if not torch.equal(lens, my_len[dst]):
+                bad = dst[torch.nonzero(lens != my_len[dst]).flatten()[0]]
+                raise ValueError(f"checkpoint does not match corpus (doc key {int(my_keys[bad])})")
+            n = int(lens.sum())
+            rep = torch.repeat_interleave(torch.arange(dst.numel()), lens)
+            within = torch.arange(n) - torch.repeat_interleave(torch.cumsum(lens, 0) - lens, lens)
+            z[my_ptr[dst][rep] + within] = d["z"][ptr[src][rep] + within]
+            found[dst] = True
+        if not bool(found.all()):
+            miss = int(my_keys[torch.nonzero(~found).flatten()[0]])
+            raise ValueError(f"checkpoint does not match corpus (doc key {miss} missing)")
         model.load_canonical_z(z, sweep)
         return sweep

@@ -47,17 +47,21 @@ def range_(name: str):
 
 
 class StageTimer:
-    """Wall-clock stage timer; with ``device`` set, brackets stages with HIP events."""
+    """Per-stage timer used by every pipeline (oni355.pipeline.*): host wall time of each stage
+    plus, on a GPU, its device time from HIP events recorded on the current stream -- so stages
+    need no host synchronisation between them. :meth:`summary` gives ``<stage>_s`` (host wall)
+    and ``<stage>_dev_s`` (device) entries; each stage is also a roctx range."""
 
     def __init__(self, device=None):
-        self.device = device
+        import torch
+        self.device = torch.device(device) if device is not None else None
         self.wall: dict[str, float] = {}
         self._events: list = []
 
     @contextlib.contextmanager
     def stage(self, name: str):
         import torch
-        use_ev = self.device is not None and getattr(self.device, "type", "") == "cuda"
+        use_ev = self.device is not None and self.device.type == "cuda"
         if use_ev:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -76,6 +80,13 @@ class StageTimer:
         out: dict[str, float] = {}
         for name, e0, e1 in self._events:
             out[name] = out.get(name, 0.0) + e0.elapsed_time(e1)
+        return out
+
+    def summary(self) -> dict[str, float]:
+        """``<stage>_s`` host wall seconds and ``<stage>_dev_s`` device seconds (synchronises)."""
+        out = {f"{k}_s": v for k, v in self.wall.items()}
+        for k, ms in self.device_ms().items():
+            out[f"{k}_dev_s"] = ms / 1e3
         return out
 
 

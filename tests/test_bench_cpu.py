@@ -9,7 +9,7 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ARGS = ["--steps", "2", "--warmup", "1", "--flows-per-gpu", "3000", "--device", "cpu"]
+ARGS = ["--steps", "2", "--warmup", "1", "--flows-per-gpu", "3000", "--sweeps", "6", "--device", "cpu"]
 
 
 def _port():
@@ -35,11 +35,21 @@ def _check(out, n):
     assert out["value"] > 0 and out["ms_per_step"] > 0 and out["higher_is_better"] is True
     assert out["scaling"] == "weak" and out["config"]["parallelism"] == f"dp{n}"
     assert out["config"]["global_batch"] == 3000 * n
-    assert out["score_path"] == "pairs" and out["score_mfma_items"] > 0 and "tiles" in out["score_ms_other_paths"]
+    # a step is a full day run: every stage is timed and the in-step training reports its sweep rate
+    for stage in ("h2d_s", "featurize_s", "vocab_s", "corpus_s", "init_s", "train_s", "score_prep_s", "score_s",
+                  "results_s", "step_s"):
+        assert stage in out["stage_median_s"], stage
+    assert out["gibbs_iters_per_sec"] > 0 and out["config"]["sweeps_per_step"] == 6
+    assert out["vs_baseline"] is None
 
 
 def test_bench_single_process():
     _check(_run([sys.executable, "bench.py", *ARGS]), 1)
+
+
+def test_bench_self_launches_ranks():
+    """``bench.py --gpus 2`` outside torchrun starts its own 2-rank torch.distributed.run child."""
+    _check(_run([sys.executable, "bench.py", "--gpus", "2", *ARGS]), 2)
 
 
 @pytest.mark.slow
@@ -86,6 +96,6 @@ def test_bench_forced_one_rank_process_group_matches_plain():
     assert r.returncode == 0, r.stderr[-3000:]
     forced = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     _check(forced, 1)
-    for k in ("loglik", "tokens", "vocab", "docs_local", "planted_anomaly_recall_topN", "score_pairs"):
+    for k in ("loglik", "tokens", "vocab", "docs_local", "planted_anomaly_recall_topN"):
         assert forced[k] == plain[k], k
-    assert forced["allreduce_s_per_sweep"] > 0 and plain["allreduce_s_per_sweep"] == 0
+    assert forced["allreduce_bytes_per_sweep"] > 0 and plain["allreduce_bytes_per_sweep"] == 0

@@ -24,7 +24,7 @@ def _free_port():
 
 def _worker(rank, world, port, n_total, out_q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK="0", ONI_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
+                      LOCAL_RANK=str(rank), ONI_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
     import torch
     torch.set_num_threads(2)
     from oni355.parallel import comm as pc
@@ -72,3 +72,46 @@ def test_dp_ranks_sharing_gpu_match_single_process(gpu, world):
     assert np.array_equal(one[1], many[1])
     assert np.array_equal(one[2], many[2]) and np.array_equal(one[3], many[3])
     assert one[4] == pytest.approx(many[4], rel=1e-9)
+
+
+def _forced_rccl_worker(port, n_total, sweeps, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ONI_FORCE_DIST="1",
+                      HSA_ENABLE_IPC_MODE_LEGACY="0")
+    os.environ.pop("WORLD_SIZE", None)
+    os.environ.pop("ONI_DIST_BACKEND", None)
+    from oni355.parallel import comm as pc
+    from oni355.pipeline.flow import run_flow
+    from oni355.synth.flow import generate_flows
+    comm = pc.init_from_env("cuda")
+    assert comm.dist and comm.backend == "nccl" and comm.graph_capturable()
+    day = generate_flows(n_total, seed=11)
+    res = run_flow(day.cols, K=20, sweeps=sweeps, maxresults=200, device="cuda:0", comm=comm)
+    m = res.lda.model
+    out_q.put((res.rows, res.scores, res.stats["loglik"], len(m._graphs), m.allreduce_ms_per_sweep(),
+               m.allreduce_bytes_per_sweep()))
+    comm.barrier()
+    pc.shutdown()
+
+
+def test_forced_rccl_sweeps_replay_from_graphs_bitwise(gpu):
+    """A 1-rank RCCL process group (ONI_FORCE_DIST=1): the per-sweep Δ all-reduce is captured into
+    the sweep HIP graphs and the run stays bitwise equal to the collective-free world=1 run."""
+    n, sweeps = 20_000, 8
+    from oni355.pipeline.flow import run_flow
+    from oni355.synth.flow import generate_flows
+    plain = run_flow(generate_flows(n, seed=11).cols, K=20, sweeps=sweeps, maxresults=200, device="cuda:0")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_forced_rccl_worker, args=(_free_port(), n, sweeps, q))
+    p.start()
+    try:
+        rows, scores, ll, n_graphs, ar_ms, ar_bytes = q.get(timeout=100)
+    finally:
+        p.join(timeout=30)
+        if p.exitcode is None:
+            p.kill()
+    assert p.exitcode == 0
+    assert n_graphs >= 1, "DP sweeps were not captured into a HIP graph"
+    assert ar_ms is not None and ar_ms > 0 and ar_bytes > 0
+    assert np.array_equal(plain.rows, rows) and np.array_equal(plain.scores, scores)
+    assert plain.stats["loglik"] == ll
