@@ -190,7 +190,7 @@ def run_pipeline_mode(a, comm) -> dict:
         t1 = time.perf_counter()
         rendered = rio.render_result(a.source, cols, res, row_off, comm)
         if rank == 0:
-            rio.write_csv(os.path.join(tmp, f"{a.source}_results.csv"), schema.result_columns(a.source), rendered)
+            rio.write_rendered(os.path.join(tmp, f"{a.source}_results.csv"), schema.result_columns(a.source), rendered)
         res.timings["results_s"] = time.perf_counter() - t1
         return res
 

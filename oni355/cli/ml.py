@@ -196,7 +196,8 @@ def main(argv=None) -> int:
     out = None
     if rank == 0:
         from .. import schema
-        out = rio.write_csv(rio.results_path(cfg.LPATH, a.source, a.date), schema.result_columns(a.source), rendered)
+        out = rio.write_rendered(rio.results_path(cfg.LPATH, a.source, a.date), schema.result_columns(a.source),
+                                 rendered)
         m = MetricsLog(os.path.join(os.path.dirname(out), "metrics.jsonl"))
         m.write({"event": "oni-ml", "source": a.source, "date": a.date, "events": n_total, "ranks": world,
                  "device": device, "load_s": t_load, **{k: v for k, v in res.timings.items()},

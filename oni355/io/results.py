@@ -8,12 +8,16 @@ from __future__ import annotations
 
 import csv
 import datetime as _dt
+import io
 import os
 
 import numpy as np
 
 from .. import schema
 from ..ref import spec
+from ..store.columnar import StringColumn
+
+_EMPTY = StringColumn.from_list([""])
 
 
 def ip_str(v) -> str:
@@ -38,6 +42,7 @@ def _fmt(col: str, v) -> str:
 
 
 def flow_rows(cols: dict, local_rows: np.ndarray, src_words, dst_words, src_scores, dst_scores, scores) -> list[list]:
+    """Pure-Python rendering of flow result rows (the specification of :func:`format_flow`)."""
     out = []
     for i, r in enumerate(np.asarray(local_rows, dtype=np.int64)):
         row = [_fmt(c, cols[c][r]) for c in schema.FLOW_COLUMNS]
@@ -51,7 +56,7 @@ _EVENT_IP_COLUMNS = {"ip_src", "ip_dst", "clientip", "serverip"}
 
 
 def event_rows(source: str, cols: dict, local_rows, words: list[str], scores) -> list[list]:
-    """DNS / proxy result rows: raw columns in schema order + word + score."""
+    """Pure-Python rendering of DNS / proxy result rows (specification of :func:`format_events`)."""
     names = schema.raw_columns(source)
     out = []
     for i, r in enumerate(np.asarray(local_rows, dtype=np.int64)):
@@ -72,17 +77,121 @@ def event_rows(source: str, cols: dict, local_rows, words: list[str], scores) ->
     return out
 
 
-def render_result(source: str, cols: dict, res, row_off: int, comm=None) -> list[list]:
-    """Result rows of a pipeline run (FlowResult / SingleResult) as CSV fields, ascending score.
+# ------------------------------------------------------------------------------------------------
+# native rendering (csrc/native/csv_format.cpp): typed result columns → CSV text in one C++ pass
+# ------------------------------------------------------------------------------------------------
+K_INT, K_IP, K_TIME, K_FLOAT, K_SCORE, K_STR, K_FLOWWORD = range(7)
 
-    Each rank renders the result rows it holds (``cols`` is its shard, starting at global row
-    ``row_off``); with a process group the rendered rows are gathered (collective X06's payload)
-    and every rank returns the full, globally ordered list."""
+
+class Rendered:
+    """CSV text of result rows: ``blob`` (bytes, rows end in '\n') and each row's end offset."""
+
+    def __init__(self, blob: bytes, ends: np.ndarray):
+        self.blob, self.ends = blob, np.asarray(ends, dtype=np.int64)
+
+    def __len__(self) -> int:
+        return int(self.ends.size)
+
+    def lines(self) -> list[bytes]:
+        starts = np.concatenate([[0], self.ends[:-1]]) if self.ends.size else self.ends
+        return [self.blob[a:b] for a, b in zip(starts.tolist(), self.ends.tolist())]
+
+    def rows(self) -> list[list[str]]:
+        """Parsed back into fields (tests / small consumers)."""
+        return list(csv.reader(io.StringIO(self.blob.decode("utf-8", "replace"))))
+
+
+def _native_format(fields: list[tuple[int, object]], n: int) -> Rendered:
+    import ctypes as C
+
+    from ..ops import native
+    native.register("oni_csv_format", [C.c_int64, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_char_p,
+                                       C.c_int64, C.c_void_p], C.c_int64)
+    L = native.lib()
+    keep, ptrs, offs, kinds = [], [], [], []
+    for kind, v in fields:
+        if kind == K_STR:
+            keep += [v.chars if v.chars.size else np.zeros(1, np.uint8), v.offsets]
+            ptrs.append(keep[-2].ctypes.data)
+            offs.append(v.offsets.ctypes.data)
+        else:
+            dt = {K_INT: np.int64, K_IP: np.uint32, K_TIME: np.int64, K_FLOAT: np.float64, K_SCORE: np.float32,
+                  K_FLOWWORD: np.uint32}[kind]
+            a = np.ascontiguousarray(v, dtype=dt)
+            if a.size != n:
+                raise ValueError("result column length mismatch")
+            keep.append(a)
+            ptrs.append(a.ctypes.data)
+            offs.append(None)
+        kinds.append(kind)
+    nc = len(kinds)
+    kind_a = (C.c_int32 * nc)(*kinds)
+    ptr_a = (C.c_void_p * nc)(*ptrs)
+    off_a = (C.c_void_p * nc)(*offs)
+    ends = np.zeros(max(n, 1), dtype=np.int64)
+    cap = max(n * 16 * max(nc, 1), 1024)  # typical fields are < 16 bytes; retried once if short
+    for _ in range(2):
+        buf = np.empty(cap, dtype=np.uint8)  # not zeroed: only [0, m) is read back
+        m = L.oni_csv_format(n, nc, kind_a, ptr_a, off_a, buf.ctypes.data_as(C.c_char_p), cap, ends.ctypes.data)
+        if m < 0:
+            raise ValueError("bad result column kind")
+        if m <= cap:
+            return Rendered(buf[:m].tobytes(), ends[:n].copy())
+        cap = int(m)
+    raise RuntimeError("csv formatter did not converge")
+
+
+def _col_field(c: str, v, rows: np.ndarray, ip_cols=(), time_cols=(), float_cols=()):
+    if v is None:
+        return K_STR, _EMPTY.take(np.zeros(rows.size, np.int64))
+    if hasattr(v, "offsets"):
+        return K_STR, v.take(rows)
+    a = np.asarray(v)[rows]
+    if c in ip_cols:
+        return K_IP, a.astype(np.int64).astype(np.uint32) if a.dtype != np.uint32 else a
+    if c in time_cols:
+        return K_TIME, a
+    if c in float_cols or a.dtype.kind == "f":
+        return K_FLOAT, a
+    return K_INT, a
+
+
+def format_flow(cols: dict, local_rows, src_words, dst_words, src_scores, dst_scores, scores) -> Rendered:
+    rows = np.asarray(local_rows, dtype=np.int64)
+    f = [_col_field(c, cols[c], rows, schema.FLOW_IP_COLUMNS, schema.FLOW_TIME_COLUMNS, schema.FLOW_FLOAT_COLUMNS)
+         for c in schema.FLOW_COLUMNS]
+    f += [(K_FLOWWORD, np.asarray(src_words).astype(np.uint32)), (K_FLOWWORD, np.asarray(dst_words).astype(np.uint32)),
+          (K_SCORE, src_scores), (K_SCORE, dst_scores), (K_SCORE, scores)]
+    return _native_format(f, rows.size)
+
+
+def format_events(source: str, cols: dict, local_rows, words: list[str], scores) -> Rendered:
+    rows = np.asarray(local_rows, dtype=np.int64)
+    f = [_col_field(c, cols.get(c), rows, _EVENT_IP_COLUMNS) for c in schema.raw_columns(source)]
+    if source == "dns" and rows.size:
+        ft = f[0][1]
+        empty = (ft.offsets[1:] - ft.offsets[:-1]) == 0
+        if empty.any():
+            # frame_time missing: render it from unix_tstamp (the decoder's own format)
+            vals = ft.to_list()
+            for i in np.nonzero(empty)[0]:
+                vals[i] = _fmt_time(cols["unix_tstamp"][rows[i]])
+            f[0] = (K_STR, StringColumn.from_list(vals))
+    f += [(K_STR, StringColumn.from_list(words)), (K_SCORE, scores)]
+    return _native_format(f, rows.size)
+
+
+def render_result(source: str, cols: dict, res, row_off: int, comm=None) -> Rendered:
+    """Result rows of a pipeline run (FlowResult / SingleResult) as CSV text, ascending score.
+
+    Each rank formats the result rows it holds (``cols`` is its shard, starting at global row
+    ``row_off``) with the native formatter; with a process group the formatted rows are gathered
+    (collective X06's payload) and every rank returns the full, globally ordered text."""
     rows_local = res.rows - row_off
     if source == "flow":
         mine = (rows_local >= 0) & (rows_local < len(cols["sip"]))
-        rendered = flow_rows(cols, rows_local[mine], res.src_words[mine], res.dst_words[mine],
-                             res.src_scores[mine], res.dst_scores[mine], res.scores[mine])
+        rendered = format_flow(cols, rows_local[mine], res.src_words[mine], res.dst_words[mine],
+                               res.src_scores[mine], res.dst_scores[mine], res.scores[mine])
     else:
         if source == "dns":
             from ..pipeline.dns import word_str
@@ -90,23 +199,39 @@ def render_result(source: str, cols: dict, res, row_off: int, comm=None) -> list
             from ..pipeline.proxy import word_str
         ncol = len(cols["ip_dst" if source == "dns" else "clientip"])
         mine = (rows_local >= 0) & (rows_local < ncol)
-        rendered = event_rows(source, cols, rows_local[mine], [word_str(w) for w in res.words[mine]],
-                              res.scores[mine])
+        rendered = format_events(source, cols, rows_local[mine], [word_str(w) for w in res.words[mine]],
+                                 res.scores[mine])
     if comm is None or not comm.dist:
         return rendered
     import torch.distributed as dist
     gids = res.rows[mine].tolist()
     allp = [None] * comm.world
-    dist.all_gather_object(allp, (gids, rendered), group=comm.group)
-    by_gid = {g: r for gl, rl in allp for g, r in zip(gl, rl)}
-    return [by_gid[int(g)] for g in res.rows.tolist()]
+    dist.all_gather_object(allp, (gids, rendered.blob, rendered.ends), group=comm.group)
+    by_gid = {}
+    for gl, blob, ends in allp:
+        for g, line in zip(gl, Rendered(blob, ends).lines()):
+            by_gid[g] = line
+    lines = [by_gid[int(g)] for g in res.rows.tolist()]
+    ends = np.cumsum([len(x) for x in lines]).astype(np.int64) if lines else np.zeros(0, np.int64)
+    return Rendered(b"".join(lines), ends)
+
+
+def write_rendered(path: str, header: list[str], rendered: Rendered) -> str:
+    """Header + pre-formatted rows (atomic rename)."""
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    tmp = path + ".tmp"
+    with open(tmp, "wb") as f:
+        f.write((",".join(header) + "\n").encode())
+        f.write(rendered.blob)
+    os.replace(tmp, path)
+    return path
 
 
 def write_csv(path: str, header: list[str], rows: list[list], with_header: bool = True) -> str:
     os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
     tmp = path + ".tmp"
     with open(tmp, "w", newline="") as f:
-        w = csv.writer(f)
+        w = csv.writer(f, lineterminator="\n")
         if with_header:
             w.writerow(header)
         w.writerows(rows)

@@ -97,15 +97,25 @@ def auto_chunk_len(T_global: int, G: int, lo: int = 32, hi: int = 128) -> int:
     return int(min(max(L, lo), hi))
 
 
+# device builds go through the hand-written K08/K09 kernels (csrc/kernels/corpus.hip); the torch
+# build below stays as the CPU path and as the bitwise reference of the native one
+NATIVE_DEVICE_BUILD = True
+
+
 @traced("oni:build_corpus")
 def build_corpus(tdoc: torch.Tensor, tword: torch.Tensor, D: int, V: int, doc_keys: torch.Tensor, G: int,
-                 L: int = 256, weight: torch.Tensor | None = None) -> Corpus:
-    """Build pairs/CSR/SELL from token (doc id, word id[, weight]) arrays (any device)."""
+                 L: int = 256, weight: torch.Tensor | None = None, pairs=None, native: bool | None = None) -> Corpus:
+    """Build pairs/CSR/SELL from token (doc id, word id[, weight]) arrays (any device).
+
+    On a GPU the native kernels run (``pairs``: an already built :class:`oni355.ops.corpus.PairSet`
+    of exactly these tokens); ``native=False`` forces the torch reference build."""
     dev = tdoc.device
     if tdoc.numel() != tword.numel():
         raise ValueError("tdoc/tword length mismatch")
     if L < 1 or L > (1 << 20):
         raise ValueError("chunk length L out of range")
+    if dev.type == "cuda" and (NATIVE_DEVICE_BUILD if native is None else native):
+        return _build_corpus_native(tdoc, tword, D, V, doc_keys, G, L, weight, pairs)
     S = 64 // G
     key = tdoc.to(torch.int64) * V + tword.to(torch.int64)
     if weight is None:
@@ -187,6 +197,19 @@ def build_corpus(tdoc: torch.Tensor, tword: torch.Tensor, D: int, V: int, doc_ke
                   chunk_key=chunk_key, chunk_multi=chunk_multi, tok_word=tok_word, long_rows=long_rows,
                   wsorted=wsorted.contiguous(), wslot=wslot.contiguous(), tile_wlo=tile_wlo.contiguous(),
                   tile_whi=tile_whi.contiguous(), wpos=wpos)
+
+
+def _build_corpus_native(tdoc, tword, D, V, doc_keys, G, L, weight, pairs) -> Corpus:
+    from ..ops import corpus as oc
+    if weight is not None and bool((weight < 1).any()):
+        raise ValueError("token weights must be >= 1 (DUPFACTOR >= 1)")
+    if pairs is None:
+        pairs = oc.pair_build(tdoc.to(torch.int32).contiguous(), tword.to(torch.int32).contiguous(), D, V,
+                              weight.to(torch.int32).contiguous() if weight is not None else None)
+    lay = oc.corpus_layout(pairs, doc_keys, G, L, ops.RECOUNT_TILE)
+    T = lay.pop("T")
+    return Corpus(D=D, V=V, T=T, G=G, L=L, doc_keys=doc_keys.to(torch.int32), pair_doc=pairs.pair_doc,
+                  pair_word=pairs.pair_word, pair_cnt=pairs.pair_cnt, **lay)
 
 
 def canonical_tokens(c: Corpus) -> tuple[torch.Tensor, torch.Tensor]:

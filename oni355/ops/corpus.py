@@ -1,0 +1,147 @@
+"""K08 / K09 device ops: dictionary encoding, (doc, word) pair build and the SELL corpus layout
+(csrc/kernels/corpus.hip). Device tensors only -- the CPU path keeps the torch reference build in
+:mod:`oni355.models.corpus`, which these kernels reproduce bit for bit.
+
+Host synchronisation: one 8-byte read per dictionary, one per pair build, one 24-byte read for the
+(T, chunks, long docs) totals and one for the SELL slot count -- instead of the dozens of implicit
+syncs (``int(tensor)``, ``nonzero``, ``unique``) of the torch build.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+
+vp, i64, ci = C.c_void_p, C.c_int64, C.c_int
+_SZ = C.POINTER(C.c_size_t)
+_lib.register_optional("oni_dict_encode", [vp, i64, ci, vp, vp, vp, vp, _SZ, vp])
+_lib.register_optional("oni_pair_build", [vp, vp, vp, i64, i64, i64, vp, vp, vp, vp, vp, vp, i64, vp, _SZ, vp])
+_lib.register_optional("oni_doc_layout", [vp, vp, i64, i64, ci, vp, vp, vp, vp, vp, vp, vp, _SZ, vp])
+_lib.register_optional("oni_chunk_layout", [vp, vp, vp, i64, i64, ci, ci, vp, vp, vp, vp, vp, vp, vp, vp, _SZ, vp])
+_lib.register_optional("oni_word_index", [vp, i64, i64, i64, ci, vp, vp, vp, vp, vp, vp, _SZ, vp])
+
+
+def _call(name: str, *args) -> None:
+    """Two-phase launcher: size query (tmp = NULL), scratch from torch's caching allocator, run."""
+    L = _lib.lib()
+    fn = getattr(L, name)
+    nb = C.c_size_t(0)
+    _lib.check(fn(*args, None, C.byref(nb), _lib.stream()), name + " (size)")
+    tmp = torch.empty(max(int(nb.value), 1), dtype=torch.uint8, device="cuda")
+    # every launch is on torch's current stream, so the caching allocator may hand this block out
+    # again once it is freed here: any later user is stream-ordered behind these kernels
+    _lib.check(fn(*args, tmp.data_ptr(), C.byref(nb), _lib.stream()), name)
+
+
+def _p(t):
+    return _lib.ptr(t)
+
+
+def bits_for(maxv: int) -> int:
+    return max(int(maxv).bit_length(), 1)
+
+
+def dict_encode(keys64: torch.Tensor, key_bits: int = 64) -> tuple[torch.Tensor, torch.Tensor]:
+    """Sorted unique keys (int64) and the int32 id of every key (``torch.unique(return_inverse)``)."""
+    if keys64.dtype != torch.int64 or not keys64.is_contiguous():
+        raise TypeError("dict_encode: contiguous int64 keys")
+    n = keys64.numel()
+    dev = keys64.device
+    uniq = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    ids = torch.empty(n, dtype=torch.int32, device=dev)
+    nu = torch.zeros(1, dtype=torch.int64, device=dev)
+    _call("oni_dict_encode", _p(keys64), n, int(min(max(key_bits, 1), 64)), _p(uniq), _p(ids) if n else None, _p(nu))
+    return uniq[: int(nu.item())], ids
+
+
+@dataclass
+class PairSet:
+    """Distinct (doc, word) pairs of a token list (doc-major, word-sorted) + per-token pair index."""
+    pair_doc: torch.Tensor   # int32 [nnz]
+    pair_word: torch.Tensor  # int32 [nnz]
+    pair_cnt: torch.Tensor   # int32 [nnz] Σ weights
+    tok_pair: torch.Tensor   # int32 [n] pair of every token
+    order0: torch.Tensor | None  # int64 [n0] tokens < n0 in (pair, position) order
+    D: int
+    V: int
+
+    @property
+    def nnz(self) -> int:
+        return int(self.pair_doc.numel())
+
+
+def pair_build(doc: torch.Tensor, word: torch.Tensor, D: int, V: int, weight: torch.Tensor | None = None,
+               n0: int = 0) -> PairSet:
+    n = doc.numel()
+    for t, nm in ((doc, "doc"), (word, "word")):
+        if t.dtype != torch.int32 or not t.is_contiguous() or t.numel() != n:
+            raise TypeError(f"pair_build: {nm} must be contiguous int32 [{n}]")
+    if weight is not None and (weight.dtype != torch.int32 or weight.numel() != n):
+        raise TypeError("pair_build: weight must be int32 [n]")
+    if not 0 <= n0 <= n:
+        raise ValueError("pair_build: n0 out of range")
+    dev = doc.device
+    pd = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    pw = torch.empty_like(pd)
+    pc = torch.empty_like(pd)
+    tp = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    nnz = torch.zeros(1, dtype=torch.int64, device=dev)
+    o0 = torch.empty(max(n0, 1), dtype=torch.int32, device=dev) if n0 > 0 else None
+    _call("oni_pair_build", _p(doc), _p(word), _p(weight.contiguous()) if weight is not None else None, n, int(D), int(V),
+          _p(pd), _p(pw), _p(pc), _p(tp), _p(nnz), _p(o0) if o0 is not None else None, int(n0))
+    m = int(nnz.item())
+    return PairSet(pd[:m], pw[:m], pc[:m], tp[:n], o0.to(torch.int64) if o0 is not None else None, int(D), int(V))
+
+
+def corpus_layout(ps: PairSet, doc_keys: torch.Tensor, G: int, L: int, recount_tile: int):
+    """CSR + chunk + SELL + word-index tables of :class:`oni355.models.corpus.Corpus` from pairs."""
+    from .. import ops
+    dev = ps.pair_doc.device
+    D, V, nnz = ps.D, ps.V, ps.nnz
+    S = 64 // G
+    i64t, i32t = torch.int64, torch.int32
+    doc_pair_ptr = torch.empty(D + 1, dtype=i64t, device=dev)
+    doc_tok_ptr = torch.empty(D + 1, dtype=i64t, device=dev)
+    pair_tokoff = torch.empty(max(nnz, 1), dtype=i64t, device=dev)
+    chunk_first = torch.empty(D + 1, dtype=i64t, device=dev)
+    long_rows = torch.empty(max(D, 1), dtype=i32t, device=dev)
+    scal = torch.zeros(3, dtype=i64t, device=dev)
+    _call("oni_doc_layout", _p(ps.pair_doc) if nnz else None, _p(ps.pair_cnt) if nnz else None, nnz, D, int(L),
+          _p(doc_pair_ptr), _p(doc_tok_ptr), _p(pair_tokoff), _p(chunk_first), _p(long_rows), _p(scal))
+    T, n_chunks, n_long = (int(x) for x in scal.tolist())
+    ns = (n_chunks + S - 1) // S
+    dk = doc_keys.to(i32t).contiguous()
+    chunk_doc = torch.empty(max(ns * S, 1), dtype=i32t, device=dev)
+    chunk_pos0 = torch.empty_like(chunk_doc)
+    chunk_len = torch.empty_like(chunk_doc)
+    chunk_multi = torch.empty(max(ns * S, 1), dtype=torch.uint8, device=dev)
+    chunk_key = torch.empty_like(chunk_doc)
+    slice_len = torch.empty(max(ns, 1), dtype=i32t, device=dev)
+    slice_off = torch.empty(ns + 1, dtype=i64t, device=dev)
+    _call("oni_chunk_layout", _p(chunk_first), _p(doc_tok_ptr), _p(dk) if D else None, D, n_chunks, int(L), S,
+          _p(chunk_doc), _p(chunk_pos0), _p(chunk_len), _p(chunk_multi), _p(chunk_key), _p(slice_len),
+          _p(slice_off))
+    total = int(slice_off[-1].item())
+    chunk_doc, chunk_pos0, chunk_len = chunk_doc[: ns * S], chunk_pos0[: ns * S], chunk_len[: ns * S]
+    chunk_multi, chunk_key, slice_len = chunk_multi[: ns * S], chunk_key[: ns * S], slice_len[:ns]
+    tok_word = torch.full((max(total, 1),), -1, dtype=i32t, device=dev)
+    if n_chunks:
+        ops.sell_fill(chunk_doc, chunk_pos0, chunk_len, S, slice_off[:ns].contiguous(), doc_pair_ptr,
+                      pair_tokoff[:nnz].contiguous(), ps.pair_word, ps.pair_cnt, tok_word)
+    slots = tok_word.numel()
+    n_tiles = (T + recount_tile - 1) // recount_tile
+    wsorted = torch.empty(max(T, 1), dtype=i32t, device=dev)
+    wslot = torch.empty_like(wsorted)
+    wpos = torch.empty(slots, dtype=i32t, device=dev)
+    tile_wlo = torch.empty(max(n_tiles, 1), dtype=i32t, device=dev)
+    tile_whi = torch.empty_like(tile_wlo)
+    _call("oni_word_index", _p(tok_word), slots, T, V, int(recount_tile), _p(wsorted), _p(wslot), _p(wpos),
+          _p(tile_wlo), _p(tile_whi))
+    return dict(T=T, doc_pair_ptr=doc_pair_ptr, doc_tok_ptr=doc_tok_ptr, pair_tokoff=pair_tokoff[:nnz],
+                slice_off=slice_off[:ns].contiguous(), slice_len=slice_len, chunk_doc=chunk_doc,
+                chunk_pos0=chunk_pos0, chunk_len=chunk_len, chunk_key=chunk_key, chunk_multi=chunk_multi,
+                tok_word=tok_word, long_rows=long_rows[:n_long], wsorted=wsorted[:T], wslot=wslot[:T],
+                tile_wlo=tile_wlo[:n_tiles], tile_whi=tile_whi[:n_tiles], wpos=wpos)

@@ -33,13 +33,38 @@ def i64_to_u32bits(t: torch.Tensor) -> torch.Tensor:
 
 
 @traced("oni:vocab")
+def encode_words(word_keys64: torch.Tensor, comm: Comm | None, key_bits: int = 64):
+    """(global sorted vocabulary int64, int32 word id of every key) -- K08 + collective X02.
+
+    On a GPU the local dictionary is the native radix-sort encoder (ops.corpus.dict_encode, sorting
+    only ``key_bits`` bits); with a process group the local unique keys are all-gathered and merged,
+    and local ids are remapped through the (small) local-unique → global table."""
+    if word_keys64.is_cuda:
+        from ..ops import corpus as oc
+        luniq, lids = oc.dict_encode(word_keys64.contiguous(), key_bits)
+    else:
+        luniq, inv = torch.unique(word_keys64, return_inverse=True)
+        lids = inv.to(torch.int32)
+    if comm is None or not comm.dist:
+        return luniq, lids
+    parts = comm.allgather_var(luniq)
+    vocab = torch.unique(torch.cat([p.to(luniq.device) for p in parts]))
+    remap = torch.searchsorted(vocab, luniq).to(torch.int32)
+    return vocab, remap[lids.long()]
+
+
 def global_vocab(keys64: torch.Tensor, comm: Comm | None) -> torch.Tensor:
     """Sorted unique int64 word keys over all ranks (collective X02)."""
-    loc = torch.unique(keys64)
-    if comm is None or not comm.dist:
-        return loc
-    parts = comm.allgather_var(loc)
-    return torch.unique(torch.cat([p.to(loc.device) for p in parts]))
+    return encode_words(keys64, comm)[0]
+
+
+def encode_docs(doc_keys64: torch.Tensor, key_bits: int = 32):
+    """(sorted unique doc keys int64, int32 doc id of every token)."""
+    if doc_keys64.is_cuda:
+        from ..ops import corpus as oc
+        return oc.dict_encode(doc_keys64.contiguous(), key_bits)
+    u, inv = torch.unique(doc_keys64, return_inverse=True)
+    return u, inv.to(torch.int32)
 
 
 def doc_owner(doc_keys64: torch.Tensor, world: int) -> torch.Tensor:
@@ -105,39 +130,52 @@ class LdaRun:
     doc_keys64: torch.Tensor  # sorted unique local doc keys (row i of θ)
     vocab: torch.Tensor        # sorted global word keys (row i of φ)
     timings: dict = field(default_factory=dict)
+    pairs: object = None       # world 1 on a GPU: the corpus PairSet (score plan of the events, K15)
 
 
 @traced("oni:build_and_train")
-def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor, weights: torch.Tensor | None,
+def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, weights: torch.Tensor | None,
                     vocab: torch.Tensor, K: int, alpha: float | None, beta: float, seed: int, sweeps: int,
                     chunk_len: int, comm: Comm | None, eval_every: int = 0, ckpt=None, log=None,
                     train: bool = True, timer: StageTimer | None = None, ldac_dir: str | None = None,
-                    ldac_lag: int = 0) -> LdaRun:
+                    ldac_lag: int = 0, word_ids: torch.Tensor | None = None, n_event0: int = 0) -> LdaRun:
     """Token keys → owner routing → local corpus → Gibbs LDA trained for ``sweeps`` sweeps.
 
+    ``word_ids`` (int32, from :func:`encode_words`) skips the vocabulary lookup of ``word_keys64``.
+    ``n_event0``: the first ``n_event0`` tokens are the events' first endpoints (world 1: the
+    corpus pair build then also yields the score plan's event order, see :func:`plan_from_pairs`).
     ``ldac_dir`` + ``ldac_lag`` > 0 emit lda-c ``NNN.{beta,gamma,other}`` snapshots every
     ``ldac_lag`` sweeps (oni-lda-c's LAG); ``final.*`` is written by the caller."""
     dev = doc_keys64.device
     timer = timer or StageTimer(dev)
+    dist_on = comm is not None and comm.dist
     with timer.stage("corpus"):
-        word_ids = torch.searchsorted(vocab, word_keys64)
+        if word_ids is None:
+            word_ids = torch.searchsorted(vocab, word_keys64).to(torch.int32)
+        use_w = weights is not None
         if weights is None:
             weights = torch.ones_like(word_ids)
         dk, wi, wt = route_to_owners(doc_keys64, word_ids, weights, comm)
-        udoc, inv = torch.unique(dk, return_inverse=True)
+        udoc, inv = encode_docs(dk)
         G, _ = ops.choose_tiling(K)
         if chunk_len <= 0:
             T_glob = float(wt.sum()) if wt.numel() else 0.0
-            if comm is not None and comm.dist:
+            if dist_on:
                 T_glob = comm.allreduce_scalar(T_glob, "sum")
             chunk_len = auto_chunk_len(int(T_glob), G)
-        use_w = bool((wt != 1).any()) if wt.numel() else False
-        corpus = build_corpus(inv, wi, int(udoc.numel()), int(vocab.numel()), i64_to_u32bits(udoc), G, chunk_len,
-                              weight=wt if use_w else None)
+        D, V = int(udoc.numel()), int(vocab.numel())
+        pairs = None
+        if dev.type == "cuda":
+            from ..ops import corpus as oc
+            pairs = oc.pair_build(inv, wi.to(torch.int32).contiguous(), D, V,
+                                  wt.to(torch.int32).contiguous() if use_w else None,
+                                  n0=0 if dist_on else int(n_event0))
+        corpus = build_corpus(inv, wi, D, V, i64_to_u32bits(udoc), G, chunk_len,
+                              weight=wt if use_w else None, pairs=pairs)
     with timer.stage("init"):
         model = GibbsLDA(corpus, GibbsConfig(K=K, alpha=alpha, beta=beta, seed=seed), comm=comm,
                          V_global=int(vocab.numel()))
-        run = LdaRun(corpus, model, udoc, vocab, {})
+        run = LdaRun(corpus, model, udoc, vocab, {}, pairs=None if dist_on else pairs)
         if not train:
             return run
         if ckpt is not None and ckpt.exists():
@@ -329,6 +367,42 @@ def score_plan(dkeys: torch.Tensor, vocab: torch.Tensor, sides, tiles: bool | No
     return plan
 
 
+def plan_from_pairs(ps, n: int, n_sides: int, doc_rows: torch.Tensor | None = None) -> ScorePlan:
+    """Score plan straight from a pair build over the events' tokens (side-major: tokens
+    [i·n, (i+1)·n) are the i-th endpoints): the distinct pairs are the SDDMM items, ``tok_pair`` is
+    every endpoint's pair index and ``order0`` the first-endpoint event order -- no unique /
+    searchsorted pass over the events. ``doc_rows`` maps the pair build's doc ids to θ rows."""
+    pdoc = ps.pair_doc if doc_rows is None else doc_rows[ps.pair_doc.long()].to(torch.int32)
+    invs = [ps.tok_pair[i * n:(i + 1) * n] for i in range(n_sides)]
+    plan = ScorePlan(pdoc.contiguous(), ps.pair_word, invs)
+    if SCORE_SORT_EVENTS and ps.order0 is not None:
+        order = ps.order0
+        rank = torch.empty_like(order)
+        rank[order] = torch.arange(order.numel(), dtype=order.dtype, device=order.device)
+        plan.order, plan.rank = order, rank
+        plan.inv_sorted = [x[order].contiguous() for x in invs]
+    return plan
+
+
+@traced("oni:score_plan")
+def event_score_plan(run: LdaRun, dkeys: torch.Tensor, vocab: torch.Tensor, doc_sides: list, word_ids_ev: torch.Tensor,
+                     word_sides: list, comm: Comm | None) -> ScorePlan:
+    """Score plan of this rank's events (``doc_sides``: doc keys per endpoint, ``word_ids_ev``: the
+    endpoints' word ids, side-major). GPU, world 1: the corpus pair build already holds it. GPU with
+    a process group: a local pair build over the events (owner routing moved the corpus tokens
+    away), its doc ids mapped to rows of the gathered θ (``dkeys``) through the local unique docs
+    only. CPU: the torch reference :func:`score_plan`."""
+    n = int(doc_sides[0].numel())
+    if not doc_sides[0].is_cuda or SCORE_TILES:
+        return score_plan(dkeys, vocab, list(zip(doc_sides, word_sides)))
+    if run.pairs is not None:
+        return plan_from_pairs(run.pairs, n, len(doc_sides))
+    from ..ops import corpus as oc
+    ludoc, lids = encode_docs(torch.cat(doc_sides) if len(doc_sides) > 1 else doc_sides[0].contiguous())
+    eps = oc.pair_build(lids, word_ids_ev.to(torch.int32).contiguous(), int(ludoc.numel()), int(vocab.numel()), n0=n)
+    return plan_from_pairs(eps, n, len(doc_sides), doc_rows=lookup(dkeys, ludoc))
+
+
 @traced("oni:score")
 def plan_score(theta: torch.Tensor, phi: torch.Tensor, plan: ScorePlan, tol: float, hist=None, want_parts=False):
     """(score, s1, s2) per event in PLAN order (event order unless plan.order is set; map plan
@@ -379,22 +453,24 @@ def run_single_doc_events(doc_keys64: torch.Tensor, word_keys64: torch.Tensor, K
                           maxresults: int, alpha, beta: float, seed: int, chunk_len: int, comm: Comm | None,
                           feedback=None, row_offset: int = 0, eval_every: int = 0, ckpt=None, log=None,
                           timer: StageTimer | None = None, ldac_dir: str | None = None,
-                          ldac_lag: int = 0) -> SingleResult:
+                          ldac_lag: int = 0, key_bits: int = 64) -> SingleResult:
     """Shared DNS/proxy path: one (doc, word) token per event; score = θ_doc·φ_word (C24)."""
     dev = doc_keys64.device
     timer = timer or StageTimer(dev)
     with timer.stage("vocab"):
         dk, wk, wts = doc_keys64, word_keys64, None
         if feedback is not None:
-            wts = torch.cat([torch.ones_like(wk), feedback[2]])
+            wts = torch.cat([torch.ones_like(wk), feedback[2]]).to(torch.int32)
             dk = torch.cat([dk, feedback[0]])
             wk = torch.cat([wk, feedback[1]])
-        vocab = global_vocab(wk, comm)
-    run = build_and_train(dk, wk, wts, vocab, K, alpha, beta, seed, sweeps, chunk_len, comm, eval_every=eval_every,
-                          ckpt=ckpt, log=log, timer=timer, ldac_dir=ldac_dir, ldac_lag=ldac_lag)
+        vocab, wids = encode_words(wk.contiguous(), comm, key_bits)
+    n = int(doc_keys64.numel())
+    run = build_and_train(dk, None, wts, vocab, K, alpha, beta, seed, sweeps, chunk_len, comm, eval_every=eval_every,
+                          ckpt=ckpt, log=log, timer=timer, ldac_dir=ldac_dir, ldac_lag=ldac_lag, word_ids=wids,
+                          n_event0=n)
     with timer.stage("score_prep"):
         dkeys, theta = gather_theta(run, comm)
-        plan = score_plan(dkeys, vocab, [(doc_keys64, word_keys64)])
+        plan = event_score_plan(run, dkeys, vocab, [doc_keys64], wids[:n], [word_keys64], comm)
     with timer.stage("score"):
         hist = torch.zeros(2048, dtype=torch.int32, device=dev)
         score, _, _ = plan_score(theta, run.model.phi(), plan, tol, hist=hist)

@@ -125,7 +125,8 @@ def run_dns(cols: dict, K: int = 50, sweeps: int = 200, tol: float = 1.0, maxres
         fb = (fdoc, fw, torch.full_like(fw, int(dupfactor)))
     res = common.run_single_doc_events(docs, words, K, sweeps, tol, maxresults, alpha, beta, seed, chunk_len, comm,
                                        feedback=fb, row_offset=row_offset, eval_every=eval_every, ckpt=ckpt, log=log,
-                                       timer=timer, ldac_dir=ldac_dir, ldac_lag=ldac_lag)
+                                       timer=timer, ldac_dir=ldac_dir, ldac_lag=ldac_lag,
+                                       key_bits=40)
     res.stats["cuts"] = {k: [int(x) for x in v] for k, v in cuts.items()}
     res.stats["features"] = feats
     return res

@@ -113,26 +113,28 @@ def run_flow(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxre
         cuts = compute_cuts(d, comm)
         sw, dw = wordify(d, cuts)
     with timer.stage("vocab"):
+        n = d["sip"].numel()
         doc_keys = torch.cat([common.u32_to_i64(d["sip"]), common.u32_to_i64(d["dip"])])
         word_keys = torch.cat([common.u32_to_i64(sw), common.u32_to_i64(dw)])
         weights = None
         fb = feedback_tokens(feedback, cuts, device, dupfactor)
         if fb is not None:
-            weights = torch.cat([torch.ones_like(word_keys), fb[2]])
+            weights = torch.cat([torch.ones_like(word_keys), fb[2]]).to(torch.int32)
             doc_keys = torch.cat([doc_keys, fb[0]])
             word_keys = torch.cat([word_keys, fb[1]])
-        vocab = common.global_vocab(word_keys, comm)
-    run = common.build_and_train(doc_keys, word_keys, weights, vocab, K, alpha, beta, seed, sweeps, chunk_len, comm,
+        # flow words are 29-bit keys (spec.flow_word_str layout)
+        vocab, wids = common.encode_words(word_keys, comm, key_bits=32)
+    run = common.build_and_train(doc_keys, None, weights, vocab, K, alpha, beta, seed, sweeps, chunk_len, comm,
                                  eval_every=eval_every, ckpt=ckpt, log=log, timer=timer, ldac_dir=ldac_dir,
-                                 ldac_lag=ldac_lag)
+                                 ldac_lag=ldac_lag, word_ids=wids, n_event0=n)
 
     # ---- scoring --------------------------------------------------------------------------------
     with timer.stage("score_prep"):
         dkeys, theta = common.gather_theta(run, comm)
         phi = run.model.phi()
-        n = d["sip"].numel()
-        plan = common.score_plan(dkeys, vocab, [(common.u32_to_i64(d["sip"]), common.u32_to_i64(sw)),
-                                                (common.u32_to_i64(d["dip"]), common.u32_to_i64(dw))])
+        sip, dip = common.u32_to_i64(d["sip"]), common.u32_to_i64(d["dip"])
+        plan = common.event_score_plan(run, dkeys, vocab, [sip, dip], wids[: 2 * n],
+                                       [common.u32_to_i64(sw), common.u32_to_i64(dw)], comm)
     with timer.stage("score"):
         hist = torch.zeros(2048, dtype=torch.int32, device=theta.device)
         score, s1, s2 = common.plan_score(theta, phi, plan, tol, hist=hist, want_parts=True)

@@ -147,6 +147,7 @@ def run_proxy(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxr
         fb = (fdoc, fw, torch.full_like(fw, int(dupfactor)))
     res = common.run_single_doc_events(docs, words, K, sweeps, tol, maxresults, alpha, beta, seed, chunk_len, comm,
                                        feedback=fb, row_offset=row_offset, eval_every=eval_every, ckpt=ckpt, log=log,
-                                       timer=timer, ldac_dir=ldac_dir, ldac_lag=ldac_lag)
+                                       timer=timer, ldac_dir=ldac_dir, ldac_lag=ldac_lag,
+                                       key_bits=34)
     res.stats["cuts"] = {k: [int(x) for x in v] for k, v in cuts.items()}
     return res

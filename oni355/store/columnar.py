@@ -45,6 +45,16 @@ class StringColumn:
         idx = np.arange(len(self))[i] if isinstance(i, slice) else np.asarray(i)
         return StringColumn.from_list([self[int(j)] for j in idx])
 
+    def take(self, idx) -> "StringColumn":
+        """Gather rows ``idx`` (vectorised: one fancy-index over the bytes, no per-row Python)."""
+        idx = np.asarray(idx, dtype=np.int64)
+        lo, hi = self.offsets[idx], self.offsets[idx + 1]
+        ln = hi - lo
+        off = np.zeros(idx.size + 1, dtype=np.int64)
+        np.cumsum(ln, out=off[1:])
+        src = np.repeat(lo - off[:-1], ln) + np.arange(int(off[-1]), dtype=np.int64)
+        return StringColumn(off, self.chars[src])
+
     def slice(self, lo: int, hi: int) -> "StringColumn":
         o = self.offsets[lo:hi + 1]
         return StringColumn(o - o[0], self.chars[o[0]:o[-1]])

@@ -1,0 +1,92 @@
+"""Native K08/K09 (csrc/kernels/corpus.hip) == the torch reference build, field by field, at awkward
+and bench-like sizes; dictionary encode == torch.unique; pair-derived score plans == score_plan."""
+import numpy as np
+import pytest
+import torch
+
+from oni355.models.corpus import build_corpus
+from oni355.ops import corpus as oc
+from oni355.pipeline import common
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("pair_doc", "pair_word", "pair_cnt", "doc_pair_ptr", "doc_tok_ptr", "pair_tokoff", "slice_off",
+          "slice_len", "chunk_doc", "chunk_pos0", "chunk_len", "chunk_key", "chunk_multi", "tok_word", "long_rows",
+          "wsorted", "wslot", "tile_wlo", "tile_whi", "wpos", "doc_keys")
+
+
+def _tokens(n, D, V, seed, zipf=True):
+    r = np.random.default_rng(seed)
+    if zipf:
+        p = 1.0 / np.arange(1, D + 1) ** 1.1
+        doc = r.choice(D, n, p=p / p.sum())
+    else:
+        doc = r.integers(0, D, n)
+    word = np.minimum(r.zipf(1.3, n) - 1, V - 1)
+    doc[:D] = np.arange(D)  # every doc id present (dense ids, as after dictionary encoding)
+    return torch.from_numpy(doc.astype(np.int64)), torch.from_numpy(word.astype(np.int64))
+
+
+@pytest.mark.parametrize("n,D,V,G,L,weighted", [(1, 1, 1, 1, 32, False), (65, 63, 64, 1, 32, False),
+                                                (5000, 300, 200, 1, 64, True), (20000, 700, 900, 4, 128, False),
+                                                (200_003, 4000, 3000, 8, 128, True), (2_000_000, 60_000, 6000, 1, 128, False)])
+def test_native_corpus_equals_torch_build(gpu, n, D, V, G, L, weighted):
+    tdoc, tword = _tokens(n, D, V, seed=n)
+    keys = (torch.arange(D, dtype=torch.int64) * 2654435761 & 0xFFFFFFFF).to(torch.int64)
+    keys32 = common.i64_to_u32bits(keys)
+    w = None
+    if weighted:
+        w = torch.ones(n, dtype=torch.int64)
+        w[::97] = 1000
+    ref = build_corpus(tdoc.to(gpu), tword.to(gpu), D, V, keys32.to(gpu), G, L=L,
+                       weight=None if w is None else w.to(gpu), native=False)
+    nat = build_corpus(tdoc.to(gpu), tword.to(gpu), D, V, keys32.to(gpu), G, L=L,
+                       weight=None if w is None else w.to(gpu), native=True)
+    assert nat.T == ref.T and nat.D == ref.D
+    for f in FIELDS:
+        a, b = getattr(ref, f), getattr(nat, f)
+        assert a.dtype == b.dtype, f
+        assert torch.equal(a.cpu(), b.cpu()), f
+
+
+@pytest.mark.parametrize("n,bits", [(1, 32), (1000, 32), (3_000_001, 32), (100_000, 40), (77, 64)])
+def test_dict_encode_equals_unique(gpu, n, bits):
+    r = np.random.default_rng(n)
+    table = r.integers(0, 2 ** min(bits, 62), max(n // 3, 1), dtype=np.int64)
+    keys = torch.from_numpy(table[r.integers(0, table.size, n)])
+    u, inv = torch.unique(keys, return_inverse=True)
+    nu, ni = oc.dict_encode(keys.to(gpu).contiguous(), bits)
+    assert torch.equal(u, nu.cpu()) and torch.equal(inv.to(torch.int32), ni.cpu())
+
+
+def test_pair_plan_equals_score_plan(gpu):
+    r = np.random.default_rng(5)
+    n, D, V = 50_000, 900, 700
+    dkeys = torch.from_numpy(np.sort(r.choice(2**32, D, replace=False)).astype(np.int64))
+    vocab = torch.from_numpy(np.sort(r.choice(2**29, V, replace=False)).astype(np.int64))
+    sides = [(dkeys[torch.from_numpy(r.integers(0, D, n))], vocab[torch.from_numpy(r.integers(0, V, n))])
+             for _ in range(2)]
+    g = [(a.to(gpu), b.to(gpu)) for a, b in sides]
+    ref = common.score_plan(dkeys.to(gpu), vocab.to(gpu), g, tiles=False, sort_events=True)
+    doc_all = torch.cat([a for a, _ in g])
+    ud, dids = common.encode_docs(doc_all)
+    wids = torch.searchsorted(vocab.to(gpu), torch.cat([b for _, b in g])).to(torch.int32)
+    ps = oc.pair_build(dids, wids.contiguous(), int(ud.numel()), V, n0=n)
+    plan = common.plan_from_pairs(ps, n, 2, doc_rows=common.lookup(dkeys.to(gpu), ud))
+    assert torch.equal(ref.pdoc, plan.pdoc) and torch.equal(ref.pword, plan.pword)
+    for a, b in zip(ref.inv, plan.inv):
+        assert torch.equal(a, b)
+    assert torch.equal(ref.order, plan.order) and torch.equal(ref.rank, plan.rank)
+
+
+def test_flow_pipeline_native_equals_torch_corpus(gpu, monkeypatch):
+    """End to end: the run with the native corpus/score plan == the run with the torch builds."""
+    from oni355.models import corpus as cm
+    from oni355.pipeline.flow import run_flow
+    from oni355.synth.flow import generate_flows
+    day = generate_flows(30_000, seed=8)
+    a = run_flow(day.cols, K=20, sweeps=6, maxresults=300, device="cuda:0")
+    monkeypatch.setattr(cm, "NATIVE_DEVICE_BUILD", False)
+    b = run_flow(day.cols, K=20, sweeps=6, maxresults=300, device="cuda:0")
+    assert np.array_equal(a.rows, b.rows) and np.array_equal(a.scores, b.scores)
+    assert a.stats["loglik"] == b.stats["loglik"]

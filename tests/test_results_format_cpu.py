@@ -1,0 +1,63 @@
+"""Native result formatter (csrc/native/csv_format.cpp) == the pure-Python row specification."""
+import csv
+import io
+
+import numpy as np
+
+from oni355 import schema
+from oni355.io import results as rio
+from oni355.store.columnar import StringColumn
+from oni355.synth.dns import generate_dns
+from oni355.synth.flow import generate_flows
+from oni355.synth.proxy import generate_proxy
+
+
+def _parse(rendered):
+    return list(csv.reader(io.StringIO(rendered.blob.decode())))
+
+
+def test_flow_rows_native_equals_python():
+    day = generate_flows(3000, seed=4)
+    r = np.random.default_rng(0)
+    rows = r.choice(3000, 257, replace=False)
+    sw = r.integers(0, 1 << 29, 257).astype(np.uint32)
+    sw[:5] = [65536 << 11, (65537 << 11) | (1 << 28), 53 << 11, 0, (1 << 28) | (80 << 11) | 0x7F]
+    dw = r.integers(0, 1 << 29, 257).astype(np.uint32)
+    s1, s2 = r.random(257).astype(np.float32) * 1e-3, r.random(257).astype(np.float32)
+    sc = np.minimum(s1, s2)
+    sc[0], sc[1] = np.float32(1e-30), np.float32(0.0)
+    want = rio.flow_rows(day.cols, rows, sw, dw, s1, s2, sc)
+    got = rio.format_flow(day.cols, rows, sw, dw, s1, s2, sc)
+    assert len(got) == 257 and _parse(got) == want
+    assert got.lines()[3] == got.blob[got.ends[2]:got.ends[3]]
+
+
+def test_event_rows_native_equals_python_with_quoting():
+    for source, day in (("dns", generate_dns(2000, seed=3)), ("proxy", generate_proxy(2000, seed=3))):
+        cols = dict(day.cols)
+        if source == "proxy":
+            ua = cols["useragent"].to_list()
+            ua[0], ua[1], ua[2] = 'Mozilla/5.0 (X11, "quoted")', "a,b", "line\nbreak"
+            cols["useragent"] = StringColumn.from_list(ua)
+        rows = np.arange(0, 2000, 7)
+        words = [f"{i}_1_2" for i in range(rows.size)]
+        sc = np.linspace(1e-9, 1e-3, rows.size).astype(np.float32)
+        want = rio.event_rows(source, cols, rows, words, sc)
+        got = rio.format_events(source, cols, rows, words, sc)
+        assert _parse(got) == want, source
+
+
+def test_string_column_take():
+    c = StringColumn.from_list(["ab", "", "cde", "f"])
+    t = c.take([2, 1, 0, 2])
+    assert t.to_list() == ["cde", "", "ab", "cde"]
+    assert c.take([]).to_list() == []
+
+
+def test_write_rendered_roundtrip(tmp_path):
+    day = generate_flows(500, seed=1)
+    rend = rio.format_flow(day.cols, np.arange(10), np.zeros(10, np.uint32), np.zeros(10, np.uint32),
+                           np.ones(10, np.float32), np.ones(10, np.float32), np.ones(10, np.float32))
+    p = rio.write_rendered(str(tmp_path / "x" / "flow_results.csv"), schema.FLOW_RESULT_COLUMNS, rend)
+    header, body = rio.read_csv(p)
+    assert header == schema.FLOW_RESULT_COLUMNS and len(body) == 10

@@ -12,6 +12,7 @@
 #   prof[:<args>]         rocprofv3 --kernel-trace --stats -- python bench.py <args>
 #   pmc:<ctrs>[:<args>]   rocprofv3 --pmc <ctrs> --kernel-trace --stats (ctrs comma-separated)
 #   py:<script>[:<args>]  python <script> <args>
+#   list                  rocprofv3 --list-avail (PMC counter names of this GPU)
 # TAG env var (default "run") names the output directory.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -46,6 +47,8 @@ for step in "$@"; do
       IFS=',' read -r -a args <<< "$bargs"
       timeout -s KILL 300 rocprofv3 --pmc ${ctrs//,/ } --kernel-trace --stats --output-format csv -d "$OUT/pmc_$n" -o run \
         -- python3 -u bench.py "${args[@]}" > "$OUT/pmc_$n.log" 2>&1; rc=$? ;;
+    list)
+      timeout -k 10 120 rocprofv3 --list-avail > "$OUT/counters_$n.txt" 2>&1; rc=$? ;;
     py)
       script="${rest%%:*}"; pargs=""; [[ "$rest" == *:* ]] && pargs="${rest#*:}"
       IFS=',' read -r -a args <<< "$pargs"
