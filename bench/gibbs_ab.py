@@ -22,7 +22,7 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--sweeps", type=int, default=20)
     ap.add_argument("--burn", type=int, default=30)
-    ap.add_argument("--modes", default="delta,delta+qpf,recount,dual", help="count_mode[+sampler]")
+    ap.add_argument("--modes", default="delta,delta+qpf,recount,dual", help="count_mode[+sampler], separated by , or /")
     ap.add_argument("--chunk-len", type=int, default=128)
     ap.add_argument("--chunk-lens", default="", help="extra A/B: comma list of L values (dual+qpf)")
     ap.add_argument("--lds", action="store_true", help="chunk-length A/B with the LDS-count sampler")
@@ -47,7 +47,7 @@ def main() -> int:
                                  train=False)
     c = run.corpus
     print(json.dumps({"corpus": c.stats()}), flush=True)
-    modes = a.modes.split(",")
+    modes = a.modes.replace("/", ",").split(",")
     models = {m: GibbsLDA(c, GibbsConfig(K=a.topics, count_mode=m.split("+")[0],
                                          sampler=m.split("+")[1] if "+" in m else "auto"))
               for m in modes}
