@@ -53,13 +53,19 @@ __global__ void k_heads(const K* __restrict__ k, int64_t n, int32_t* __restrict_
 
 __global__ void k_dict_scatter(const uint64_t* __restrict__ ks, const int32_t* __restrict__ perm,
                                const int32_t* __restrict__ rank, int64_t n, uint64_t* __restrict__ uniq,
-                               int32_t* __restrict__ ids, int64_t* __restrict__ n_uniq) {
+                               int32_t* __restrict__ ids, int64_t* __restrict__ n_uniq, int64_t* __restrict__ head) {
   const int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
   if (i >= n) return;
   const int32_t r = rank[i] - 1;
   ids[perm[i]] = r;
-  if (i == 0 || ks[i] != ks[i - 1]) uniq[r] = ks[i];
-  if (i == n - 1) *n_uniq = (int64_t)r + 1;
+  if (i == 0 || ks[i] != ks[i - 1]) {
+    uniq[r] = ks[i];
+    if (head) head[r] = i;
+  }
+  if (i == n - 1) {
+    *n_uniq = (int64_t)r + 1;
+    if (head) head[r + 1] = n;
+  }
 }
 
 __global__ void k_pair_keys(const int32_t* __restrict__ doc, const int32_t* __restrict__ word, int64_t n, int64_t V,
@@ -101,6 +107,15 @@ __global__ void k_pair_counts(const int64_t* __restrict__ head_pos, const int64_
   const int64_t a = head_pos[r], b = head_pos[r + 1];
   const int64_t s = psum[b - 1] - (a > 0 ? psum[a - 1] : 0);
   cnt[r] = (int32_t)(s < 0x7FFFFFFF ? s : 0x7FFFFFFF);
+}
+
+// sums[r] = Σ sorted weights of run r (64-bit; dictionary counts)
+__global__ void k_run_sums(const int64_t* __restrict__ head_pos, const int64_t* __restrict__ psum,
+                           const int64_t* __restrict__ nr_p, int64_t* __restrict__ sums) {
+  const int64_t r = (int64_t)blockIdx.x * kB + threadIdx.x;
+  if (r >= *nr_p) return;
+  const int64_t a = head_pos[r], b = head_pos[r + 1];
+  sums[r] = psum[b - 1] - (a > 0 ? psum[a - 1] : 0);
 }
 
 struct BelowN {
@@ -260,8 +275,12 @@ int bits_for(uint64_t maxv) {  // number of bits needed to represent values in [
 
 // ------------------------------------------------------------------------------------------------
 // dict_encode: keys[n] (u64) → uniq (sorted, n_uniq on device) + ids[n] (int32 rank of each key)
+// Optional counts[n] (int64): Σ weight (1 per key without ``weight``) of every unique key -- the
+// per-document token counts the data-parallel placement needs, read off the sorted runs instead of
+// a same-address-atomic index_add (power-law documents serialise those: 12 ms at 25M tokens).
 ONI_API int oni_dict_encode(const uint64_t* keys, int64_t n, int key_bits, uint64_t* uniq, int32_t* ids,
-                            int64_t* n_uniq, void* tmp, size_t* tmp_bytes, hipStream_t s) {
+                            int64_t* n_uniq, const int32_t* weight, int64_t* counts, void* tmp, size_t* tmp_bytes,
+                            hipStream_t s) {
   if (n >= (int64_t)1 << 31) return (int)hipErrorInvalidValue;
   Arena ar{static_cast<char*>(tmp)};
   uint64_t* ks = ar.take<uint64_t>(n);
@@ -269,10 +288,16 @@ ONI_API int oni_dict_encode(const uint64_t* keys, int64_t n, int key_bits, uint6
   int32_t* perm = ar.take<int32_t>(n);
   int32_t* flag = ar.take<int32_t>(n);
   int32_t* rank = ar.take<int32_t>(n);
-  size_t sb = 0, cb = 0;
+  int64_t* head = counts ? ar.take<int64_t>(n + 1) : nullptr;
+  int64_t* ws = counts ? ar.take<int64_t>(n) : nullptr;
+  int64_t* psum = counts ? ar.take<int64_t>(n) : nullptr;
+  size_t sb = 0, cb = 0, wb = 0;
   ONI_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, sb, keys, ks, iota, perm, (int)n, 0, key_bits, s));
   ONI_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, cb, flag, rank, (int)n, s));
-  void* cub = ar.take<char>(sb > cb ? sb : cb);
+  if (counts) ONI_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, wb, ws, psum, (int)n, s));
+  size_t cbytes = sb > cb ? sb : cb;
+  if (wb > cbytes) cbytes = wb;
+  void* cub = ar.take<char>(cbytes);
   if (!tmp) {
     *tmp_bytes = ar.used + 256;
     return 0;
@@ -281,12 +306,16 @@ ONI_API int oni_dict_encode(const uint64_t* keys, int64_t n, int key_bits, uint6
     ONI_TRY(hipMemsetAsync(n_uniq, 0, sizeof(int64_t), s));
     return (int)hipGetLastError();
   }
-  size_t cbytes = sb > cb ? sb : cb;
   k_iota<<<nblk(n), kB, 0, s>>>(iota, n);
   ONI_TRY(hipcub::DeviceRadixSort::SortPairs(cub, cbytes, keys, ks, iota, perm, (int)n, 0, key_bits, s));
   k_heads<uint64_t><<<nblk(n), kB, 0, s>>>(ks, n, flag);
   ONI_TRY(hipcub::DeviceScan::InclusiveSum(cub, cbytes, flag, rank, (int)n, s));
-  k_dict_scatter<<<nblk(n), kB, 0, s>>>(ks, perm, rank, n, uniq, ids, n_uniq);
+  k_dict_scatter<<<nblk(n), kB, 0, s>>>(ks, perm, rank, n, uniq, ids, n_uniq, head);
+  if (counts) {
+    k_weights_sorted<<<nblk(n), kB, 0, s>>>(weight, perm, n, ws);
+    ONI_TRY(hipcub::DeviceScan::InclusiveSum(cub, cbytes, ws, psum, (int)n, s));
+    k_run_sums<<<nblk(n), kB, 0, s>>>(head, psum, n_uniq, counts);
+  }
   return (int)hipGetLastError();
 }
 

@@ -49,6 +49,11 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--ckpt-every", type=int, default=None)
     ap.add_argument("--eval-every", type=int, default=None)
     ap.add_argument("--ldac-out", default=None, help="write lda-c files (final.beta/gamma/other, likelihood.dat)")
+    ap.add_argument("--ldac-lag", type=int, default=0, help="also write lda-c NNN.* snapshots every N sweeps")
+    ap.add_argument("--burnin", type=int, default=None, help="sweeps before the likelihood trace / snapshots")
+    ap.add_argument("--max-restarts", type=int, default=0,
+                    help="supervise the run: after a failure (crash, watchdog exit, numerical fault) start a "
+                         "fresh child process that resumes from the last checkpoint, up to R times")
     ap.add_argument("--quiet", action="store_true")
     return ap
 
@@ -63,6 +68,51 @@ def _relaunch(n: int, argv: list[str]) -> int:
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     return subprocess.run(cmd, env=env).returncode
+
+
+def _strip_opt(argv: list[str], name: str) -> list[str]:
+    out, skip = [], False
+    for i, x in enumerate(argv):
+        if skip:
+            skip = False
+            continue
+        if x == name:
+            skip = True
+            continue
+        if x.startswith(name + "="):
+            continue
+        out.append(x)
+    return out
+
+
+def supervise(a, argv: list[str], cfg) -> int:
+    """``--max-restarts R``: run the job as a child process; when it fails, start a FRESH child
+    (never an exec, nothing here touches the GPU) that resumes from the last checkpoint, up to R
+    times -- the role Spark/YARN task retry played for oni-ml. Checkpoints go to
+    ``--ckpt-dir`` (default ``<LPATH>/<source>/<date>/.ckpt``, every ``--ckpt-every`` sweeps,
+    default 20). Each child sees ``ONI_RESTART_COUNT`` (the attempt number), which
+    ``ONI_FAULT=...,attempt:A`` uses to fail only a given attempt."""
+    import shutil
+    child = _strip_opt(argv, "--max-restarts")
+    own_dir = a.ckpt_dir is None
+    ck = a.ckpt_dir or os.path.join(cfg.LPATH, a.source, a.date, ".ckpt")
+    if own_dir:
+        shutil.rmtree(ck, ignore_errors=True)
+        child += ["--ckpt-dir", ck]
+    if a.ckpt_every is None and cfg.CKPT_EVERY <= 0:
+        child += ["--ckpt-every", "20"]
+    rc = 1
+    for attempt in range(a.max_restarts + 1):
+        env = dict(os.environ, ONI_SUPERVISED="1", ONI_RESTART_COUNT=str(attempt))
+        rc = subprocess.run([sys.executable, "-m", "oni355.cli.ml", *child], env=env).returncode
+        if rc == 0:
+            break
+        print(f"[oni-ml] attempt {attempt} failed (exit {rc})"
+              + ("; restarting from the last checkpoint" if attempt < a.max_restarts else "; giving up"),
+              file=sys.stderr, flush=True)
+    if rc == 0 and own_dir:
+        shutil.rmtree(ck, ignore_errors=True)
+    return rc
 
 
 def _expand(inputs: list[str]) -> list[str]:
@@ -147,7 +197,9 @@ def main(argv=None) -> int:
                       TOPIC_COUNT=a.topics, SWEEPS=a.sweeps, SEED=a.seed, BETA=a.beta, CHUNK_LEN=a.chunk_len,
                       DUPFACTOR=a.dupfactor, USER_DOMAIN=a.user_domain, LPATH=a.lpath, EVAL_EVERY=a.eval_every,
                       CKPT_EVERY=a.ckpt_every, TOP_DOMAINS=a.top_domains, TOL=a.tol, MAXRESULTS=a.maxresults,
-                      ALPHA=a.alpha)
+                      ALPHA=a.alpha, BURNIN=a.burnin)
+    if a.max_restarts > 0 and os.environ.get("ONI_SUPERVISED") != "1":
+        return supervise(a, argv, cfg)
     gpus = a.gpus if a.gpus is not None else cfg.PROCESS_COUNT
     if gpus > 1 and "WORLD_SIZE" not in os.environ:
         return _relaunch(gpus, argv)
@@ -182,7 +234,11 @@ def main(argv=None) -> int:
     alpha = cfg.ALPHA if cfg.ALPHA > 0 else None
     common_kw = dict(K=cfg.TOPIC_COUNT, sweeps=cfg.SWEEPS, tol=cfg.TOL, maxresults=cfg.MAXRESULTS, alpha=alpha,
                      beta=cfg.BETA, seed=cfg.SEED, chunk_len=cfg.CHUNK_LEN, device=device, comm=comm, feedback=fb,
-                     dupfactor=cfg.DUPFACTOR, row_offset=row_off, eval_every=cfg.EVAL_EVERY, ckpt=ckpt, log=log)
+                     dupfactor=cfg.DUPFACTOR, row_offset=row_off, eval_every=cfg.EVAL_EVERY, burnin=cfg.BURNIN,
+                     ckpt=ckpt, log=log)
+    if a.ldac_out and a.ldac_lag > 0:
+        common_kw.update(ldac_dir=os.path.join(a.ldac_out, f"rank{rank}") if world > 1 else a.ldac_out,
+                         ldac_lag=a.ldac_lag)
     if a.source == "flow":
         from ..pipeline.flow import run_flow
         res = run_flow(cols, **common_kw)

@@ -57,6 +57,8 @@ class GibbsConfig:
     auto_delta: str = field(default_factory=lambda: os.environ.get("ONI_AUTO_DELTA", "wdelta"))
     # debug: verify count invariants after every sweep() call (ONI_CHECK_INVARIANTS=1)
     check_invariants: bool = field(default_factory=lambda: os.environ.get("ONI_CHECK_INVARIANTS", "0") == "1")
+    # cheap numerical health check after every sweep() call (ONI_HEALTH_CHECK=0 disables)
+    health_check: bool = field(default_factory=lambda: os.environ.get("ONI_HEALTH_CHECK", "1") != "0")
     # sweep kernel: "auto" (default: "qpf" for K ≤ 32, "lds" above — the measured winners),
     # "qpf" one-step q-row prefetch, "plain" q-row load on each word change, "pp" ping-pong
     # registers + 2-step token prefetch, "lds" LDS-staged doc counts (fma numerics; for K > 32 the
@@ -376,23 +378,31 @@ class GibbsLDA:
                 self._watchdog.disarm()
         if self.cfg.check_invariants:
             self.check_invariants()
-        if self._corrupted:
+        if self.cfg.health_check:
             self.check_health()
 
     def _corrupt(self) -> None:
-        """ONI_FAULT kind:nan -- poison the state the way a bad DMA / bit flip would."""
-        self.nwk[0, 0] = -1 - self.nwk[0, 0].abs()
+        """ONI_FAULT kind:nan -- poison the state the way a bad DMA / bit flip would: a negative
+        doc-topic count (carried from sweep to sweep by the sampler) and a NaN in the q table."""
+        if self.c.D:
+            self.ndk_cur[0, 0] = -1 - self.ndk_cur[0, 0].abs()
         self.q[0, 0] = float("nan")
         self._corrupted = True
 
     def check_health(self) -> None:
-        """Cheap numerical health check: finite q table, no negative topic totals. Raises
+        """Numerical health check after every ``sweep()`` call (one device reduction, one host
+        read): finite q table, no negative word-topic / topic / doc-topic count. Raises
         fault.NumericalFault (the supervisor then restarts from the last good checkpoint)."""
-        bad_q = not bool(torch.isfinite(self.q[:, : self.K]).all())
-        bad_n = bool((self.nk_cur[: self.K] < 0).any()) or bool((self.nwk[:, : self.K] < 0).any())
-        if bad_q or bad_n:
-            raise fault.NumericalFault(f"corrupt model state after sweep {self.sweeps_done}: "
-                                       f"non-finite q={bad_q}, negative counts={bad_n}")
+        K = self.K
+        flags = torch.stack([
+            (~torch.isfinite(self.q[:, :K])).any(),
+            (self.nk_cur[:K] < 0).any() | (self.nwk[:, :K] < 0).any(),
+            (self.ndk_cur[: self.c.D, :K] < 0).any() if self.c.D else torch.zeros((), dtype=torch.bool,
+                                                                                   device=self.device),
+        ]).cpu().tolist()
+        if any(flags):
+            raise fault.NumericalFault(f"corrupt model state after sweep {self.sweeps_done}: non-finite q={flags[0]}, "
+                                       f"negative counts={flags[1] or flags[2]}")
 
     def close(self) -> None:
         """Stop the watchdog thread (training finished)."""

@@ -17,7 +17,8 @@ from . import _lib
 
 vp, i64, ci = C.c_void_p, C.c_int64, C.c_int
 _SZ = C.POINTER(C.c_size_t)
-_lib.register_optional("oni_dict_encode", [vp, i64, ci, vp, vp, vp, vp, _SZ, vp])
+_lib.register_optional("oni_dict_encode", [vp, i64, ci, vp, vp, vp, vp, vp, vp, _SZ, vp])
+_lib.register_optional("oni_route_pack", [vp, vp, vp, vp, vp, i64, ci, vp, vp, vp, vp, _SZ, vp])
 _lib.register_optional("oni_pair_build", [vp, vp, vp, i64, i64, i64, vp, vp, vp, vp, vp, vp, i64, vp, _SZ, vp])
 _lib.register_optional("oni_doc_layout", [vp, vp, i64, i64, ci, vp, vp, vp, vp, vp, vp, vp, _SZ, vp])
 _lib.register_optional("oni_chunk_layout", [vp, vp, vp, i64, i64, ci, ci, vp, vp, vp, vp, vp, vp, vp, vp, _SZ, vp])
@@ -44,17 +45,50 @@ def bits_for(maxv: int) -> int:
     return max(int(maxv).bit_length(), 1)
 
 
-def dict_encode(keys64: torch.Tensor, key_bits: int = 64) -> tuple[torch.Tensor, torch.Tensor]:
-    """Sorted unique keys (int64) and the int32 id of every key (``torch.unique(return_inverse)``)."""
+def dict_encode(keys64: torch.Tensor, key_bits: int = 64, weights: torch.Tensor | None = None,
+                counts: bool = False):
+    """Sorted unique keys (int64) and the int32 id of every key (``torch.unique(return_inverse)``).
+
+    ``counts=True`` also returns Σ weights (int64; 1 per key without ``weights``) of every unique
+    key, read off the sorted runs (``torch.unique(return_counts)`` with weights)."""
     if keys64.dtype != torch.int64 or not keys64.is_contiguous():
         raise TypeError("dict_encode: contiguous int64 keys")
     n = keys64.numel()
+    if weights is not None and (weights.dtype != torch.int32 or weights.numel() != n):
+        raise TypeError("dict_encode: weights must be int32 [n]")
     dev = keys64.device
     uniq = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
     ids = torch.empty(n, dtype=torch.int32, device=dev)
     nu = torch.zeros(1, dtype=torch.int64, device=dev)
-    _call("oni_dict_encode", _p(keys64), n, int(min(max(key_bits, 1), 64)), _p(uniq), _p(ids) if n else None, _p(nu))
-    return uniq[: int(nu.item())], ids
+    cnt = torch.empty(max(n, 1), dtype=torch.int64, device=dev) if counts else None
+    _call("oni_dict_encode", _p(keys64), n, int(min(max(key_bits, 1), 64)), _p(uniq), _p(ids) if n else None, _p(nu),
+          _p(weights.contiguous()) if weights is not None else None, _p(cnt) if counts else None)
+    u = int(nu.item())
+    return (uniq[:u], ids, cnt[:u]) if counts else (uniq[:u], ids)
+
+
+def route_pack(owner_of_id: torch.Tensor, ids: torch.Tensor, keys64: torch.Tensor, word: torch.Tensor,
+               weight: torch.Tensor | None, world: int):
+    """All-to-all send buffer of the token routing (csrc/kernels/route.hip): (send int32 [n, 2|3]
+    grouped by owner rank, order int32 [n] = token of each slot, counts int64 [world])."""
+    n = ids.numel()
+    for t, nm, dt in ((owner_of_id, "owner_of_id", torch.int32), (ids, "ids", torch.int32),
+                      (keys64, "keys64", torch.int64), (word, "word", torch.int32)):
+        if t.dtype != dt or not t.is_contiguous():
+            raise TypeError(f"route_pack: {nm} must be contiguous {dt}")
+    if keys64.numel() != n or word.numel() != n or (weight is not None and weight.numel() != n):
+        raise ValueError("route_pack: token arrays differ in length")
+    if not 1 <= world <= 256:
+        raise ValueError("route_pack: 1 <= world <= 256")
+    dev = ids.device
+    C = 3 if weight is not None else 2
+    send = torch.empty((n, C), dtype=torch.int32, device=dev)
+    order = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    counts = torch.empty(world, dtype=torch.int64, device=dev)
+    _call("oni_route_pack", _p(owner_of_id), _p(ids), _p(keys64), _p(word),
+          _p(weight.to(torch.int32).contiguous()) if weight is not None else None, n, int(world), _p(send),
+          _p(order), _p(counts))
+    return send, order[:n], counts
 
 
 @dataclass

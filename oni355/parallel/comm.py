@@ -110,19 +110,28 @@ class Comm:
         dist.all_gather(outs, pad, group=self.group)
         return [o[:s] for o, s in zip(outs, sizes)]
 
-    def alltoallv(self, t: torch.Tensor, send_counts: torch.Tensor) -> torch.Tensor:
-        """Exchange rows: rows [off_r, off_r + send_counts[r]) of ``t`` go to rank r."""
+    def alltoallv(self, t: torch.Tensor, send_counts, recv_counts=None, return_recv_counts: bool = False):
+        """Exchange rows: rows [off_r, off_r + send_counts[r]) of ``t`` go to rank r.
+
+        ``recv_counts`` (when the caller already knows them, e.g. the way back of a routed
+        exchange) skips the count exchange. ``return_recv_counts`` also returns them (list)."""
         if not self.dist:
-            return t
+            return (t, [int(t.shape[0])]) if return_recv_counts else t
+        sc = [int(x) for x in (send_counts.tolist() if torch.is_tensor(send_counts) else send_counts)]
         if self._via_host and t.is_cuda:
-            return self._host_view().alltoallv(t.cpu(), send_counts.cpu()).to(self.device)
-        sc = send_counts.to(torch.int64).to(self.device)
-        rc = torch.empty_like(sc)
-        dist.all_to_all_single(rc, sc, group=self.group)
-        out = torch.empty((int(rc.sum()), *t.shape[1:]), dtype=t.dtype, device=self.device)
-        dist.all_to_all_single(out, t.to(self.device).contiguous(), output_split_sizes=rc.tolist(),
-                               input_split_sizes=sc.tolist(), group=self.group)
-        return out
+            r = self._host_view().alltoallv(t.cpu(), sc, recv_counts, return_recv_counts)
+            return (r[0].to(self.device), r[1]) if return_recv_counts else r.to(self.device)
+        if recv_counts is None:
+            sct = torch.tensor(sc, dtype=torch.int64, device=self.device)
+            rct = torch.empty_like(sct)
+            dist.all_to_all_single(rct, sct, group=self.group)
+            rc = rct.tolist()
+        else:
+            rc = [int(x) for x in recv_counts]
+        out = torch.empty((sum(rc), *t.shape[1:]), dtype=t.dtype, device=self.device)
+        dist.all_to_all_single(out, t.to(self.device).contiguous(), output_split_sizes=rc,
+                               input_split_sizes=sc, group=self.group)
+        return (out, rc) if return_recv_counts else out
 
     def _host_view(self) -> "Comm":
         return Comm(self.rank, self.world, torch.device("cpu"), self.group, forced=self.dist, backend="gloo")

@@ -74,53 +74,142 @@ def doc_owner(doc_keys64: torch.Tensor, world: int) -> torch.Tensor:
 
 
 HEAVY_DOCS_PER_RANK = 4096
+PLACEMENT_BUCKETS_PER_RANK = 64
 
 
-def balanced_owner(doc_keys64: torch.Tensor, weights: torch.Tensor, comm: Comm) -> torch.Tensor:
+def lpt_place(counts: np.ndarray, load: np.ndarray) -> np.ndarray:
+    """Longest-processing-time greedy: each count (already in placement order) goes to the rank
+    with the smallest load so far, ties to the lowest rank. ``load`` is updated in place.
+    Native (csrc/native/placement.cpp); the NumPy loop is the reference used when the host
+    library is absent."""
+    counts = np.ascontiguousarray(counts, dtype=np.int64)
+    owner = np.zeros(counts.size, dtype=np.int32)
+    try:
+        from ..ops import native
+        L = native.lib()
+        fn = L.oni_lpt_place
+    except (RuntimeError, AttributeError):
+        fn = None
+    if fn is not None:
+        import ctypes as C
+        fn.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p]
+        fn.restype = C.c_int
+        if fn(counts.ctypes.data, counts.size, int(load.size), load.ctypes.data, owner.ctypes.data):
+            raise ValueError("oni_lpt_place: bad arguments")
+        return owner
+    for i, c in enumerate(counts.tolist()):
+        r = int(np.argmin(load))
+        load[r] += c
+        owner[i] = r
+    return owner
+
+
+def place_docs(doc_keys64: torch.Tensor, weights: torch.Tensor | None, comm: Comm, per_doc: bool = False):
     """Owner rank of each token's document, balanced by global token counts.
 
     IP documents are power-law sized (one synthetic 100M-flow day puts ~8 % of all tokens on a
     single IP), so a plain hash leaves the busiest rank ~1.5× the mean at 8 ranks and every sweep
-    waits for it. Here the per-doc token counts are all-gathered once, the heaviest
-    ``HEAVY_DOCS_PER_RANK × world`` docs are placed by longest-processing-time greedy on top of the
-    hash load of the rest, and everything else keeps the hash owner. Deterministic on every rank
-    (same gathered input, ties → lowest rank); results stay world-size invariant because the
-    sampler's chain never depends on placement.
-    """
+    waits for it. Every rank proposes its ``HEAVY_DOCS_PER_RANK`` locally heaviest documents; the
+    union of the proposals gets exact global counts (one all-reduce over the candidates, not an
+    all-gather of every document); every other document falls into one of
+    ``PLACEMENT_BUCKETS_PER_RANK × world`` hash buckets, and candidates and buckets together are
+    placed by longest-processing-time greedy (:func:`lpt_place`). Collective volume is
+    O(candidates · world), independent of the number of documents.
+    Deterministic on every rank (same candidate set and counts; order count desc, key asc; ties →
+    lowest rank); results stay world-size invariant because the sampler's chain never depends on
+    placement. Returns the owner of every token, or with ``per_doc`` (owner of every local
+    document int32, document id of every token int32)."""
     W = comm.world
-    ukeys, inv = torch.unique(doc_keys64, return_inverse=True)
-    ucnt = torch.zeros(ukeys.numel(), dtype=torch.int64, device=ukeys.device).index_add_(0, inv, weights.to(torch.int64))
-    keys = torch.cat(comm.allgather_var(ukeys)).cpu()
-    cnts = torch.cat(comm.allgather_var(ucnt)).cpu()
-    gkeys, ginv = torch.unique(keys, return_inverse=True)
-    gcnt = torch.zeros(gkeys.numel(), dtype=torch.int64).index_add_(0, ginv, cnts)
-    gown = doc_owner(gkeys, W)
-    order = torch.argsort(gcnt, descending=True, stable=True)
-    heavy = order[: HEAVY_DOCS_PER_RANK * W]
-    light = torch.ones(gkeys.numel(), dtype=torch.bool)
-    light[heavy] = False
-    load = torch.bincount(gown[light], weights=gcnt[light].to(torch.float64), minlength=W).tolist()
-    hc = gcnt[heavy].tolist()
-    assign = []
-    for c in hc:
-        r = min(range(W), key=lambda i: (load[i], i))
-        load[r] += c
-        assign.append(r)
-    gown[heavy] = torch.tensor(assign, dtype=torch.int64)
-    return gown.to(doc_keys64.device)[torch.searchsorted(gkeys.to(doc_keys64.device), doc_keys64)]
+    dev = doc_keys64.device
+    if doc_keys64.is_cuda:
+        from ..ops import corpus as oc
+        ukeys, inv, ucnt = oc.dict_encode(doc_keys64.contiguous(), 32,
+                                          weights.to(torch.int32) if weights is not None else None, counts=True)
+    else:
+        ukeys, inv = encode_docs(doc_keys64.contiguous())
+        w = weights.to(torch.int64) if weights is not None else torch.ones(inv.numel(), dtype=torch.int64)
+        ucnt = torch.zeros(ukeys.numel(), dtype=torch.int64).index_add_(0, inv.long(), w)
+    U = int(ukeys.numel())
+    # local proposals: heaviest first, ties by key (ukeys is ascending, the sort is stable)
+    top = torch.argsort(ucnt, descending=True, stable=True)[: min(HEAVY_DOCS_PER_RANK, U)]
+    cand = torch.unique(torch.cat([p.to(dev) for p in comm.allgather_var(ukeys[top].contiguous())]))
+    if U:
+        pos = torch.searchsorted(ukeys, cand).clamp_(max=U - 1)
+        hit = ukeys[pos] == cand
+    else:
+        pos = torch.zeros_like(cand)
+        hit = torch.zeros(cand.numel(), dtype=torch.bool, device=dev)
+    ccnt = torch.where(hit, ucnt[pos] if U else torch.zeros_like(cand), torch.zeros_like(cand))
+    is_cand = torch.zeros(U, dtype=torch.bool, device=dev)
+    is_cand[pos[hit]] = True
+    # all other documents are hashed into B buckets that are placed like documents, so the rank
+    # that takes a huge IP takes correspondingly fewer light ones
+    B = PLACEMENT_BUCKETS_PER_RANK * W
+    hb = doc_owner(ukeys, B)
+    bload = torch.zeros(B, dtype=torch.int64, device=dev).index_add_(0, hb[~is_cand], ucnt[~is_cand])
+    both = torch.cat([ccnt, bload])  # one collective for candidate counts + bucket loads
+    comm.allreduce_(both)
+    nc = int(cand.numel())
+    o = torch.argsort(both, descending=True, stable=True)  # candidates (by key) before buckets on ties
+    assign = lpt_place(both[o].cpu().numpy(), np.zeros(W, dtype=np.int64))
+    iown = torch.empty(nc + B, dtype=torch.int64)
+    iown[o.cpu()] = torch.from_numpy(assign.astype(np.int64))
+    iown = iown.to(dev)
+    uown = iown[nc:][hb]
+    uown[pos[hit]] = iown[:nc][hit]
+    if per_doc:
+        return uown.to(torch.int32), inv
+    return uown[inv.long()]
+
+
+def balanced_owner(doc_keys64: torch.Tensor, weights: torch.Tensor, comm: Comm) -> torch.Tensor:
+    """Alias of :func:`place_docs` (round-1 name)."""
+    return place_docs(doc_keys64, weights, comm)
+
+
+@dataclass
+class Route:
+    """How this rank's tokens were sent to their document owners (for the way back)."""
+    order: torch.Tensor     # int [n_sent]: slot i of the owner-grouped send buffer holds token order[i]
+    send_counts: list       # tokens sent to each rank
+    recv_counts: list       # tokens received from each rank (the owner side's layout)
 
 
 @traced("oni:route_to_owners")
-def route_to_owners(doc_keys64: torch.Tensor, word_ids: torch.Tensor, weights: torch.Tensor, comm: Comm | None):
-    """Send each token to its document's owner rank (alltoallv). Returns local (doc, word, weight)."""
+def route_to_owners(doc_keys64: torch.Tensor, word_ids: torch.Tensor, weights: torch.Tensor | None,
+                    comm: Comm | None):
+    """Send each token to its document's owner rank (alltoallv of packed int32 columns: 8 B per
+    token, 12 B with weights). Returns local (doc keys int64, word ids int32, weights int32, Route)."""
     if comm is None or not comm.dist:
-        return doc_keys64, word_ids, weights
-    owner = balanced_owner(doc_keys64, weights, comm)
-    order = torch.argsort(owner, stable=True)
-    counts = torch.bincount(owner, minlength=comm.world)
-    packed = torch.stack([doc_keys64[order], word_ids[order].to(torch.int64), weights[order].to(torch.int64)], 1)
-    recv = comm.alltoallv(packed, counts)
-    return recv[:, 0].contiguous(), recv[:, 1].contiguous(), recv[:, 2].contiguous()
+        w = weights if weights is not None else torch.ones_like(word_ids, dtype=torch.int32)
+        return doc_keys64, word_ids, w, None
+    if doc_keys64.is_cuda:
+        from ..ops import corpus as oc
+        uown, ids = place_docs(doc_keys64, weights, comm, per_doc=True)
+        send, order, counts = oc.route_pack(uown, ids, doc_keys64.contiguous(), word_ids.to(torch.int32).contiguous(),
+                                            weights, comm.world)
+    else:
+        owner = place_docs(doc_keys64, weights, comm)
+        order = torch.argsort(owner, stable=True)
+        counts = torch.bincount(owner, minlength=comm.world)
+        cols = [i64_to_u32bits(doc_keys64[order]), word_ids[order].to(torch.int32)]
+        if weights is not None:
+            cols.append(weights[order].to(torch.int32))
+        send = torch.stack(cols, 1).contiguous()
+    recv, rc = comm.alltoallv(send, counts, return_recv_counts=True)
+    dk = u32_to_i64(recv[:, 0])
+    wi = recv[:, 1].contiguous()
+    wt = recv[:, 2].contiguous() if weights is not None else torch.ones_like(wi)
+    return dk, wi, wt, Route(order, counts.tolist(), rc)
+
+
+def return_to_origin(x: torch.Tensor, route: Route, comm: Comm) -> torch.Tensor:
+    """Inverse of :func:`route_to_owners` for a per-received-token value ``x`` (owner layout):
+    returns the value of every token this rank sent, in its original token order."""
+    back = comm.alltoallv(x.contiguous(), route.recv_counts, recv_counts=route.send_counts)
+    out = torch.empty_like(back)
+    out[route.order.to(back.device).long()] = back
+    return out
 
 
 @dataclass
@@ -130,13 +219,17 @@ class LdaRun:
     doc_keys64: torch.Tensor  # sorted unique local doc keys (row i of θ)
     vocab: torch.Tensor        # sorted global word keys (row i of φ)
     timings: dict = field(default_factory=dict)
-    pairs: object = None       # world 1 on a GPU: the corpus PairSet (score plan of the events, K15)
+    # the corpus PairSet (ops.corpus.PairSet on a GPU, TorchPairs on the CPU): world 1 on a GPU it
+    # is also the events' score plan (K15); with a process group it maps every received token to
+    # its (doc, word) pair for owner-side scoring (owner_token_scores)
+    pairs: object = None
+    route: Route | None = None  # with a process group: how this rank's tokens went to their owners
 
 
 @traced("oni:build_and_train")
 def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, weights: torch.Tensor | None,
                     vocab: torch.Tensor, K: int, alpha: float | None, beta: float, seed: int, sweeps: int,
-                    chunk_len: int, comm: Comm | None, eval_every: int = 0, ckpt=None, log=None,
+                    chunk_len: int, comm: Comm | None, eval_every: int = 0, burnin: int = 0, ckpt=None, log=None,
                     train: bool = True, timer: StageTimer | None = None, ldac_dir: str | None = None,
                     ldac_lag: int = 0, word_ids: torch.Tensor | None = None, n_event0: int = 0) -> LdaRun:
     """Token keys → owner routing → local corpus → Gibbs LDA trained for ``sweeps`` sweeps.
@@ -145,7 +238,10 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
     ``n_event0``: the first ``n_event0`` tokens are the events' first endpoints (world 1: the
     corpus pair build then also yields the score plan's event order, see :func:`plan_from_pairs`).
     ``ldac_dir`` + ``ldac_lag`` > 0 emit lda-c ``NNN.{beta,gamma,other}`` snapshots every
-    ``ldac_lag`` sweeps (oni-lda-c's LAG); ``final.*`` is written by the caller."""
+    ``ldac_lag`` sweeps (oni-lda-c's LAG); ``final.*`` is written by the caller.
+    ``burnin``: sweeps before the chain is considered mixed -- the ``eval_every`` likelihood trace
+    and the LAG snapshots only sample sweeps after it (BURNIN in duxbay.conf / ``burnin`` in the
+    lda-c settings file); θ/φ always come from the final sweep."""
     dev = doc_keys64.device
     timer = timer or StageTimer(dev)
     dist_on = comm is not None and comm.dist
@@ -153,9 +249,7 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
         if word_ids is None:
             word_ids = torch.searchsorted(vocab, word_keys64).to(torch.int32)
         use_w = weights is not None
-        if weights is None:
-            weights = torch.ones_like(word_ids)
-        dk, wi, wt = route_to_owners(doc_keys64, word_ids, weights, comm)
+        dk, wi, wt, route = route_to_owners(doc_keys64, word_ids, weights, comm)
         udoc, inv = encode_docs(dk)
         G, _ = ops.choose_tiling(K)
         if chunk_len <= 0:
@@ -170,12 +264,14 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
             pairs = oc.pair_build(inv, wi.to(torch.int32).contiguous(), D, V,
                                   wt.to(torch.int32).contiguous() if use_w else None,
                                   n0=0 if dist_on else int(n_event0))
+        elif dist_on:
+            pairs = torch_pairs(inv, wi, V)
         corpus = build_corpus(inv, wi, D, V, i64_to_u32bits(udoc), G, chunk_len,
-                              weight=wt if use_w else None, pairs=pairs)
+                              weight=wt if use_w else None, pairs=pairs if dev.type == "cuda" else None)
     with timer.stage("init"):
         model = GibbsLDA(corpus, GibbsConfig(K=K, alpha=alpha, beta=beta, seed=seed), comm=comm,
                          V_global=int(vocab.numel()))
-        run = LdaRun(corpus, model, udoc, vocab, {}, pairs=None if dist_on else pairs)
+        run = LdaRun(corpus, model, udoc, vocab, {}, pairs=pairs, route=route)
         if not train:
             return run
         if ckpt is not None and ckpt.exists():
@@ -195,13 +291,14 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
                 n = min(n, lag - (model.sweeps_done % lag))
             model.sweep(n)
             remaining -= n
-            if eval_every > 0 and model.sweeps_done % eval_every == 0:
+            mixed = model.sweeps_done > burnin
+            if eval_every > 0 and model.sweeps_done % eval_every == 0 and mixed:
                 ll = model.record_likelihood()
                 if log:
                     log(f"sweep {model.sweeps_done} loglik {ll:.6e}")
             if ck_every and model.sweeps_done % ck_every == 0:
                 ckpt.save(model)
-            if lag and model.sweeps_done % lag == 0 and remaining > 0:
+            if lag and model.sweeps_done % lag == 0 and remaining > 0 and mixed:
                 from ..io import ldac
                 ldac.export_gibbs(ldac_dir, model, prefix=f"{model.sweeps_done:03d}")
     model.close()
@@ -209,6 +306,43 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
         model.record_likelihood()
     run.timings.update({"sweeps": sweeps})
     return run
+
+
+@dataclass
+class TorchPairs:
+    """CPU counterpart of ops.corpus.PairSet (only the fields owner-side scoring reads)."""
+    pair_doc: torch.Tensor
+    pair_word: torch.Tensor
+    tok_pair: torch.Tensor
+
+
+def torch_pairs(doc_ids: torch.Tensor, word_ids: torch.Tensor, V: int) -> TorchPairs:
+    u, inv = torch.unique(doc_ids.to(torch.int64) * V + word_ids.to(torch.int64), return_inverse=True)
+    return TorchPairs((u // V).to(torch.int32), (u % V).to(torch.int32), inv.to(torch.int32))
+
+
+@traced("oni:owner_scores")
+def owner_token_scores(run: LdaRun, comm: Comm) -> torch.Tensor:
+    """Data-parallel scoring (K15 with a process group): every owner scores the distinct
+    (doc, word) pairs of the tokens it received with its own θ rows and the global φ, and sends
+    each token's score back to the rank the token came from (the reverse of the owner routing,
+    4 B per token). Returns the score of every token this rank routed, in its original order.
+
+    This replaces an all-gather of every θ row to every rank (D_global·K·4 B per rank, 320 MB at
+    the 100M-flow day) plus a per-rank pair build over the events: θ never leaves its owner. The
+    per-pair dot is the same kernel as world 1 (k_pair_score), so scores stay bitwise equal."""
+    ps = ops.pair_score(run.model.theta(), run.model.phi(), run.pairs.pair_doc, run.pairs.pair_word)
+    return return_to_origin(ps[run.pairs.tok_pair.long()], run.route, comm)
+
+
+def owner_event_scores(ts: torch.Tensor, n: int, n_sides: int, tol: float, hist: torch.Tensor,
+                       want_parts: bool = False):
+    """(score, s1, s2) per local event from owner-side token scores ``ts`` (tokens
+    [i·n, (i+1)·n) are the events' i-th endpoints), in event order, with the fused order-key
+    histogram."""
+    idx = torch.arange(n_sides * n, dtype=torch.int32, device=ts.device)
+    return ops.event_min(ts, idx[:n], idx[n:2 * n] if n_sides > 1 else None, tol=tol, want_parts=want_parts,
+                         hist=hist)
 
 
 @traced("oni:gather_theta")
@@ -451,7 +585,7 @@ class SingleResult:
 
 def run_single_doc_events(doc_keys64: torch.Tensor, word_keys64: torch.Tensor, K: int, sweeps: int, tol: float,
                           maxresults: int, alpha, beta: float, seed: int, chunk_len: int, comm: Comm | None,
-                          feedback=None, row_offset: int = 0, eval_every: int = 0, ckpt=None, log=None,
+                          feedback=None, row_offset: int = 0, eval_every: int = 0, burnin: int = 0, ckpt=None, log=None,
                           timer: StageTimer | None = None, ldac_dir: str | None = None,
                           ldac_lag: int = 0, key_bits: int = 64) -> SingleResult:
     """Shared DNS/proxy path: one (doc, word) token per event; score = θ_doc·φ_word (C24)."""
@@ -465,16 +599,23 @@ def run_single_doc_events(doc_keys64: torch.Tensor, word_keys64: torch.Tensor, K
             wk = torch.cat([wk, feedback[1]])
         vocab, wids = encode_words(wk.contiguous(), comm, key_bits)
     n = int(doc_keys64.numel())
-    run = build_and_train(dk, None, wts, vocab, K, alpha, beta, seed, sweeps, chunk_len, comm, eval_every=eval_every,
+    run = build_and_train(dk, None, wts, vocab, K, alpha, beta, seed, sweeps, chunk_len, comm, eval_every=eval_every, burnin=burnin,
                           ckpt=ckpt, log=log, timer=timer, ldac_dir=ldac_dir, ldac_lag=ldac_lag, word_ids=wids,
                           n_event0=n)
-    with timer.stage("score_prep"):
-        dkeys, theta = gather_theta(run, comm)
-        plan = event_score_plan(run, dkeys, vocab, [doc_keys64], wids[:n], [word_keys64], comm)
-    with timer.stage("score"):
-        hist = torch.zeros(2048, dtype=torch.int32, device=dev)
-        score, _, _ = plan_score(theta, run.model.phi(), plan, tol, hist=hist)
-        rows, scs = top_n(score, tol, maxresults, comm, row_offset, hist=hist, order=plan.order)
+    hist = torch.zeros(2048, dtype=torch.int32, device=dev)
+    if run.route is not None:
+        with timer.stage("score_prep"):
+            ts = owner_token_scores(run, comm)
+        with timer.stage("score"):
+            score, _, _ = owner_event_scores(ts, n, 1, tol, hist)
+            rows, scs = top_n(score, tol, maxresults, comm, row_offset, hist=hist)
+    else:
+        with timer.stage("score_prep"):
+            dkeys, theta = gather_theta(run, comm)
+            plan = event_score_plan(run, dkeys, vocab, [doc_keys64], wids[:n], [word_keys64], comm)
+        with timer.stage("score"):
+            score, _, _ = plan_score(theta, run.model.phi(), plan, tol, hist=hist)
+            rows, scs = top_n(score, tol, maxresults, comm, row_offset, hist=hist, order=plan.order)
     t = timer.summary()
     t.update(run.timings)
     t["records_scored"] = int(doc_keys64.numel())

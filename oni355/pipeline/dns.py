@@ -102,7 +102,7 @@ def featurize(d: dict, comm: Comm | None, topset: HashSet | None, user_domain: s
 def run_dns(cols: dict, K: int = 50, sweeps: int = 200, tol: float = 1.0, maxresults: int = 3000,
             alpha: float | None = None, beta: float = 0.01, seed: int = 0x0D15EA5E, chunk_len: int = 0,
             device="cpu", comm: Comm | None = None, top_domains=None, user_domain: str = "",
-            feedback: dict | None = None, dupfactor: int = 1000, row_offset: int = 0, eval_every: int = 0,
+            feedback: dict | None = None, dupfactor: int = 1000, row_offset: int = 0, eval_every: int = 0, burnin: int = 0,
             ckpt=None, log=None, ldac_dir: str | None = None, ldac_lag: int = 0) -> common.SingleResult:
     timer = StageTimer(device)
     with timer.stage("h2d"):
@@ -124,7 +124,7 @@ def run_dns(cols: dict, K: int = 50, sweeps: int = 200, tol: float = 1.0, maxres
         fdoc = common.u32_to_i64(fd["ip_dst"])
         fb = (fdoc, fw, torch.full_like(fw, int(dupfactor)))
     res = common.run_single_doc_events(docs, words, K, sweeps, tol, maxresults, alpha, beta, seed, chunk_len, comm,
-                                       feedback=fb, row_offset=row_offset, eval_every=eval_every, ckpt=ckpt, log=log,
+                                       feedback=fb, row_offset=row_offset, eval_every=eval_every, burnin=burnin, ckpt=ckpt, log=log,
                                        timer=timer, ldac_dir=ldac_dir, ldac_lag=ldac_lag,
                                        key_bits=40)
     res.stats["cuts"] = {k: [int(x) for x in v] for k, v in cuts.items()}

@@ -103,7 +103,7 @@ def feedback_tokens(fb_cols: dict | None, cuts: FlowCuts, device, dupfactor: int
 def run_flow(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxresults: int = 3000,
              alpha: float | None = None, beta: float = 0.01, seed: int = 0x0D15EA5E, chunk_len: int = 0,
              device="cpu", comm: Comm | None = None, feedback: dict | None = None, dupfactor: int = 1000,
-             row_offset: int = 0, eval_every: int = 0, ckpt=None, log=None, ldac_dir: str | None = None,
+             row_offset: int = 0, eval_every: int = 0, burnin: int = 0, ckpt=None, log=None, ldac_dir: str | None = None,
              ldac_lag: int = 0) -> FlowResult:
     """Full suspicious-connects for one (rank-local shard of a) day of flows."""
     timer = StageTimer(device)
@@ -125,20 +125,29 @@ def run_flow(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxre
         # flow words are 29-bit keys (spec.flow_word_str layout)
         vocab, wids = common.encode_words(word_keys, comm, key_bits=32)
     run = common.build_and_train(doc_keys, None, weights, vocab, K, alpha, beta, seed, sweeps, chunk_len, comm,
-                                 eval_every=eval_every, ckpt=ckpt, log=log, timer=timer, ldac_dir=ldac_dir,
+                                 eval_every=eval_every, burnin=burnin, ckpt=ckpt, log=log, timer=timer, ldac_dir=ldac_dir,
                                  ldac_lag=ldac_lag, word_ids=wids, n_event0=n)
 
     # ---- scoring --------------------------------------------------------------------------------
-    with timer.stage("score_prep"):
-        dkeys, theta = common.gather_theta(run, comm)
-        phi = run.model.phi()
-        sip, dip = common.u32_to_i64(d["sip"]), common.u32_to_i64(d["dip"])
-        plan = common.event_score_plan(run, dkeys, vocab, [sip, dip], wids[: 2 * n],
-                                       [common.u32_to_i64(sw), common.u32_to_i64(dw)], comm)
-    with timer.stage("score"):
-        hist = torch.zeros(2048, dtype=torch.int32, device=theta.device)
-        score, s1, s2 = common.plan_score(theta, phi, plan, tol, hist=hist, want_parts=True)
-        rows, scs = common.top_n(score, tol, maxresults, comm, row_offset, hist=hist, order=plan.order)
+    hist = torch.zeros(2048, dtype=torch.int32, device=d["sip"].device)
+    plan = None
+    if run.route is not None:
+        # data parallel: pairs are scored where their θ rows live, token scores come back (X05')
+        with timer.stage("score_prep"):
+            ts = common.owner_token_scores(run, comm)
+        with timer.stage("score"):
+            score, s1, s2 = common.owner_event_scores(ts, n, 2, tol, hist, want_parts=True)
+            rows, scs = common.top_n(score, tol, maxresults, comm, row_offset, hist=hist)
+    else:
+        with timer.stage("score_prep"):
+            dkeys, theta = common.gather_theta(run, comm)
+            phi = run.model.phi()
+            sip, dip = common.u32_to_i64(d["sip"]), common.u32_to_i64(d["dip"])
+            plan = common.event_score_plan(run, dkeys, vocab, [sip, dip], wids[: 2 * n],
+                                           [common.u32_to_i64(sw), common.u32_to_i64(dw)], comm)
+        with timer.stage("score"):
+            score, s1, s2 = common.plan_score(theta, phi, plan, tol, hist=hist, want_parts=True)
+            rows, scs = common.top_n(score, tol, maxresults, comm, row_offset, hist=hist, order=plan.order)
     t = timer.summary()
     t.update(run.timings)
     t["records_scored"] = n
@@ -146,7 +155,7 @@ def run_flow(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxre
     loc = rows - row_offset
     mine = (loc >= 0) & (loc < n)
     li = loc[mine]
-    pi = plan.rank[li] if plan.rank is not None else li  # plan positions of the result events
+    pi = plan.rank[li] if plan is not None and plan.rank is not None else li  # positions of the result events
     parts = torch.stack([s1[pi], s2[pi]], 1) if s1 is not None else torch.zeros(0, 2)
     wparts = torch.stack([sw[li], dw[li]], 1)
     if comm is not None and comm.dist:

@@ -76,6 +76,9 @@ def test_balanced_owner_evens_out_power_law_docs():
         def allgather_var(self, t):
             return [t]
 
+        def allreduce_(self, t):
+            return t
+
     r = np.random.default_rng(0)
     keys = torch.from_numpy(r.zipf(1.1, 400_000).astype(np.int64) * 7919 % (2**32))  # top doc ~9 % < 1/8
     w = torch.ones_like(keys)
@@ -87,3 +90,21 @@ def test_balanced_owner_evens_out_power_law_docs():
     u, inv = torch.unique(keys, return_inverse=True)
     first = torch.zeros(u.numel(), dtype=torch.int64).scatter_(0, inv, own)
     assert torch.equal(first[inv], own)
+
+
+def test_lpt_place_native_matches_numpy_reference():
+    from oni355.ops import native
+    from oni355.pipeline import common
+    r = np.random.default_rng(3)
+    counts = np.sort(r.zipf(1.3, 5000).astype(np.int64))[::-1].copy()
+    load0 = r.integers(0, 1000, 8).astype(np.int64)
+    l1 = load0.copy()
+    own = common.lpt_place(counts, l1)
+    l2 = load0.copy()
+    ref = np.zeros(counts.size, np.int32)
+    for i, c in enumerate(counts):
+        k = int(np.argmin(l2))
+        l2[k] += c
+        ref[i] = k
+    assert native.lib().oni_lpt_place is not None
+    assert np.array_equal(own, ref) and np.array_equal(l1, l2)

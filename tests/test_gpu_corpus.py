@@ -90,3 +90,37 @@ def test_flow_pipeline_native_equals_torch_corpus(gpu, monkeypatch):
     b = run_flow(day.cols, K=20, sweeps=6, maxresults=300, device="cuda:0")
     assert np.array_equal(a.rows, b.rows) and np.array_equal(a.scores, b.scores)
     assert a.stats["loglik"] == b.stats["loglik"]
+
+
+@pytest.mark.parametrize("n,weighted", [(1, False), (5000, True), (2_000_000, False), (1_000_003, True)])
+def test_dict_encode_counts_equal_weighted_unique(gpu, n, weighted):
+    """Per-key token counts (the DP placement's document loads) == torch.unique counts / index_add."""
+    r = np.random.default_rng(n + 7)
+    keys = torch.from_numpy((r.zipf(1.2, n) * 2654435761 % 2**32).astype(np.int64))
+    w = torch.from_numpy(r.integers(1, 1000, n).astype(np.int32)) if weighted else None
+    u, inv = torch.unique(keys, return_inverse=True)
+    ref = torch.zeros(u.numel(), dtype=torch.int64).index_add_(0, inv, w.to(torch.int64) if weighted else
+                                                              torch.ones(n, dtype=torch.int64))
+    nu, ni, nc = oc.dict_encode(keys.to(gpu).contiguous(), 32, w.to(gpu) if weighted else None, counts=True)
+    assert torch.equal(u, nu.cpu()) and torch.equal(inv.to(torch.int32), ni.cpu())
+    assert torch.equal(ref, nc.cpu())
+
+
+@pytest.mark.parametrize("n,W,weighted", [(1, 1, False), (1000, 2, True), (777_777, 3, False), (2_000_000, 8, True)])
+def test_route_pack_is_stable_owner_partition(gpu, n, W, weighted):
+    """route_pack == stable argsort by owner + gathered (doc key, word[, weight]) columns + counts."""
+    r = np.random.default_rng(n)
+    U = max(n // 5, 1)
+    ids = torch.from_numpy(r.integers(0, U, n).astype(np.int32))
+    own = torch.from_numpy(r.integers(0, W, U).astype(np.int32))
+    keys = torch.from_numpy(r.integers(0, 2**32, n, dtype=np.int64))
+    word = torch.from_numpy(r.integers(0, 10**6, n).astype(np.int32))
+    wt = torch.from_numpy(r.integers(1, 5, n).astype(np.int32)) if weighted else None
+    send, order, counts = oc.route_pack(own.to(gpu), ids.to(gpu), keys.to(gpu), word.to(gpu),
+                                        wt.to(gpu) if weighted else None, W)
+    tok_own = own[ids.long()].long()
+    ref_order = torch.argsort(tok_own, stable=True)
+    assert torch.equal(order.cpu().long(), ref_order)
+    assert torch.equal(counts.cpu(), torch.bincount(tok_own, minlength=W))
+    cols = [common.i64_to_u32bits(keys[ref_order]), word[ref_order]] + ([wt[ref_order]] if weighted else [])
+    assert torch.equal(send.cpu(), torch.stack(cols, 1))
