@@ -53,6 +53,8 @@ def parse(argv=None):
     ap.add_argument("--source", choices=["flow", "dns", "proxy"], default="flow")
     ap.add_argument("--from-pcap", action="store_true",
                     help="dns: every step decodes the shard's pcap file (config 3 'pcap→word pipeline')")
+    ap.add_argument("--realistic-vocab", action="store_true",
+                    help="flow: long-tail service ports and wider bins (V ~ 1e5-1e6 words, SURVEY §7.5)")
     ap.add_argument("--chunk-len", type=int, default=0, help="0 = auto (global token count)")
     ap.add_argument("--maxresults", type=int, default=3000)
     ap.add_argument("--seed", type=int, default=7)
@@ -134,7 +136,8 @@ def make_shard(a, comm):
     n_total = per * world
     if a.source == "flow":
         from oni355.synth.flow import generate_flows
-        day = generate_flows(per, seed=a.seed, rank=rank, n_hosts=max(64, n_total // 25))
+        day = generate_flows(per, seed=a.seed, rank=rank, n_hosts=max(64, n_total // 25),
+                             wide_vocab=a.realistic_vocab)
     elif a.source == "dns":
         from oni355.synth.dns import generate_dns
         day = generate_dns(per, seed=a.seed, rank=rank, n_clients=max(32, n_total // 40))
@@ -240,7 +243,8 @@ def run_pipeline_mode(a, comm) -> dict:
         "vs_baseline": None,
         "dtype": "fp32",
         "data": f"synthetic {a.source} (oni355.synth.{a.source}: random-init topic priors, Zipf hosts, planted anomalies)"
-                + (", decoded from pcap every step" if pcap else ""),
+                + (", decoded from pcap every step" if pcap else "")
+                + (", realistic (long-tail) vocabulary" if a.realistic_vocab else ""),
         "config": {"model": f"oni-suspicious-connects-{a.source}-lda", "topics": K, "global_batch": n_total,
                    "events_per_gpu": per, "seq_len": 2 if a.source == "flow" else 1, "parallelism": f"dp{world}",
                    "sweeps_per_step": a.sweeps, "maxresults": a.maxresults, "baseline_config": baseline_cfg},

@@ -145,6 +145,34 @@ class GibbsLDA:
         self._ar_events: list = []
         self._capturing = False
         self._corrupted = False
+        self._x01 = None
+        if (comm is not None and comm.dist and self.KS % 2 == 0
+                and os.environ.get("ONI_X01_PACK", "1") != "0"):
+            self._setup_x01()
+
+    def _setup_x01(self) -> None:
+        """Packed X01 payload (csrc/kernels/x01.hip): words whose local token count is at most
+        O = ⌊32767 / W⌋ on every rank travel as two offset 16-bit halves per int32 word. Their
+        per-rank value (an absolute local count in recount sweeps, a delta otherwise) is bounded by
+        that local count, so the packed ring sum is exact; everything else stays int32."""
+        W = self.comm.world
+        O = 32767 // W
+        if os.environ.get("ONI_X01_LIGHT_MAX"):  # tests: force a light/heavy mix on small days
+            O = min(O, int(os.environ["ONI_X01_LIGHT_MAX"]))
+        V, KS = self.V, self.KS
+        dev = self.device
+        cnt = torch.zeros(V, dtype=torch.int64, device=dev)
+        if self.c.T:
+            cnt += torch.bincount(self.c.wsorted.to(torch.int64), minlength=V)[:V]
+        self.comm.allreduce_(cnt, op="max")
+        light = torch.nonzero(cnt <= O).flatten().to(torch.int32)
+        heavy = torch.nonzero(cnt > O).flatten().to(torch.int32)
+        tail_off, tail_len = V * KS, self.dn[0].numel() - V * KS
+        n = ops.x01_packed_len(light.numel(), heavy.numel(), KS, tail_len)
+        if n >= self.dn[0].numel():
+            return
+        self._x01 = dict(light=light.contiguous(), heavy=heavy.contiguous(), O=O, WO=W * O, tail_off=tail_off,
+                         tail_len=tail_len, buf=torch.zeros(n, dtype=torch.int32, device=dev))
 
     # ---------------------------------------------------------------------------------------------
     def _state(self, init: bool) -> dict:
@@ -292,7 +320,13 @@ class GibbsLDA:
         if timed:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record()
-        self.comm.allreduce_(buf)
+        x = self._x01
+        if x is not None:
+            ops.x01_pack(buf, x["light"], x["heavy"], self.KS, x["tail_off"], x["tail_len"], x["O"], x["buf"])
+            self.comm.allreduce_(x["buf"])
+            ops.x01_unpack(x["buf"], x["light"], x["heavy"], self.KS, x["tail_off"], x["tail_len"], x["WO"], buf)
+        else:
+            self.comm.allreduce_(buf)
         if timed:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record()
@@ -303,7 +337,8 @@ class GibbsLDA:
         """Bytes each rank contributes to X01 per sweep (0 without a process group)."""
         if self.comm is None or not self.comm.dist:
             return 0
-        return int(self.dn[0].numel() * self.dn[0].element_size())
+        b = self._x01["buf"] if self._x01 is not None else self.dn[0]
+        return int(b.numel() * b.element_size())
 
     def allreduce_ms_per_sweep(self, probe_reps: int = 20) -> float | None:
         """Median device time of the per-sweep Δ all-reduce (ms). Uses the events of eager sweeps;
@@ -316,7 +351,7 @@ class GibbsLDA:
             self._ar_events[-1][1].synchronize()
             times = [a.elapsed_time(b) for a, b in self._ar_events]
         if not times:
-            scratch = torch.zeros_like(self.dn[0])
+            scratch = torch.zeros_like(self._x01["buf"] if self._x01 is not None else self.dn[0])
             for _ in range(probe_reps):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()

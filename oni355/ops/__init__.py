@@ -417,6 +417,49 @@ def copy_rows(src, dst, rows, KS):
 
 
 # ------------------------------------------------------------------------------------------------
+# X01 payload packing (csrc/kernels/x01.hip)
+# ------------------------------------------------------------------------------------------------
+def x01_packed_len(L: int, H: int, KS: int, tail_len: int) -> int:
+    return L * (KS // 2) + H * KS + tail_len
+
+
+def x01_pack(dn, light, heavy, KS: int, tail_off: int, tail_len: int, O: int, out) -> None:
+    """Light rows as two offset 16-bit halves per int32 word, heavy rows + tail as int32."""
+    L, H = light.numel(), heavy.numel()
+    if not _is_dev(dn):
+        half = KS // 2
+        rows = dn[: tail_off].view(-1, KS)
+        lv = (rows[light.long()].to(torch.int64) + O).view(L, half, 2)
+        nl = L * half
+        out[:nl] = (lv[..., 0] | (lv[..., 1] << 16)).reshape(-1).to(torch.int32) if L else out[:0]
+        out[nl:nl + H * KS] = rows[heavy.long()].reshape(-1)
+        out[nl + H * KS:nl + H * KS + tail_len] = dn[tail_off:tail_off + tail_len]
+        return
+    _lib.check(_lib.lib().oni_x01_pack(_lib.ptr(dn), _lib.ptr(light), L, _lib.ptr(heavy), H, KS, tail_off, tail_len,
+                                       O, _lib.ptr(out), _lib.stream()), "oni_x01_pack")
+
+
+def x01_unpack(packed, light, heavy, KS: int, tail_off: int, tail_len: int, WO: int, dn) -> None:
+    """Inverse of :func:`x01_pack` after the sum over W ranks (``WO`` = W·O)."""
+    L, H = light.numel(), heavy.numel()
+    if not _is_dev(dn):
+        half = KS // 2
+        nl = L * half
+        v = packed[:nl].to(torch.int64) & 0xFFFFFFFF
+        rows = dn[: tail_off].view(-1, KS)
+        if L:
+            lo = ((v & 0xFFFF) - WO).to(torch.int32).view(L, half)
+            hi = ((v >> 16) - WO).to(torch.int32).view(L, half)
+            rows[light.long()] = torch.stack([lo, hi], 2).view(L, KS)
+        if H:
+            rows[heavy.long()] = packed[nl:nl + H * KS].view(H, KS)
+        dn[tail_off:tail_off + tail_len] = packed[nl + H * KS:nl + H * KS + tail_len]
+        return
+    _lib.check(_lib.lib().oni_x01_unpack(_lib.ptr(packed), _lib.ptr(light), L, _lib.ptr(heavy), H, KS, tail_off,
+                                         tail_len, WO, _lib.ptr(dn), _lib.stream()), "oni_x01_unpack")
+
+
+# ------------------------------------------------------------------------------------------------
 # scoring / selection
 # ------------------------------------------------------------------------------------------------
 def score(theta, phi, d1, w1, d2=None, w2=None, tol: float = float("inf"), want_parts=False, hist=None):

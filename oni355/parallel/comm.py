@@ -39,14 +39,15 @@ class Comm:
         self.dist = world > 1 or forced
 
     # -- basic ------------------------------------------------------------------------------------
-    def allreduce_(self, t: torch.Tensor) -> torch.Tensor:
+    def allreduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
         if self.dist:
+            rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
             if self._via_host and t.is_cuda:
                 h = t.cpu()
-                dist.all_reduce(h, group=self.group)
+                dist.all_reduce(h, op=rop, group=self.group)
                 t.copy_(h)
             else:
-                dist.all_reduce(t, group=self.group)
+                dist.all_reduce(t, op=rop, group=self.group)
         return t
 
     def allreduce_np(self, a) -> np.ndarray:

@@ -78,8 +78,13 @@ def str_to_ip(s: str) -> int:
 
 def generate_flows(n: int, seed: int = 7, n_hosts: int | None = None, n_profiles: int = 20,
                    alpha_true: float = 0.08, zipf_a: float = 1.15, n_anomalies: int | None = None,
-                   date=(2016, 7, 8), rank: int = 0) -> FlowDay:
-    """Generate ``n`` flows. ``rank`` offsets the RNG stream (weak-scaling shards of one day)."""
+                   date=(2016, 7, 8), rank: int = 0, wide_vocab: bool = False) -> FlowDay:
+    """Generate ``n`` flows. ``rank`` offsets the RNG stream (weak-scaling shards of one day).
+
+    ``wide_vocab``: a realistic-vocabulary day (SURVEY.md §7.5 sizing, V ≈ 1e5–1e6 flow words):
+    half of the flows use a long-tail (Zipf) service port anywhere in 1..1024 instead of their
+    profile's ports, hours and volumes are spread wider, and 20 % of the flows are server-to-server
+    (both ports low / both high), so every (port, time, bytes, packets, direction) bin fills."""
     rng = np.random.default_rng([seed, rank])
     n_profiles = min(n_profiles, len(_PROFILES))
     prof = _PROFILES[:n_profiles]
@@ -120,6 +125,14 @@ def generate_flows(n: int, seed: int = 7, n_hosts: int | None = None, n_profiles
         hour_f[m] = rng.normal(peak, hsd, size=cnt)
         lbytes[m] = rng.normal(mu, sd, size=cnt)
         bpp[m] = bp * np.exp(rng.normal(0, 0.2, size=cnt))
+    if wide_vocab:
+        # long-tail services: Zipf over a random permutation of the well-known port range
+        lt = rng.random(n) < 0.5
+        perm = np.random.default_rng([seed, 0x5EED]).permutation(np.arange(1, 1025))
+        port_of[lt] = perm[np.minimum(rng.zipf(1.2, int(lt.sum())) - 1, 1023)]
+        hour_f += rng.normal(0.0, 4.0, size=n)
+        lbytes += rng.normal(0.0, 2.0, size=n)
+        bpp *= np.exp(rng.normal(0.0, 0.8, size=n))
     srv = rng.integers(0, n_srv, size=n)
     dip = _ip(172, 16, z & 255, srv & 255).astype(np.uint32)
     sip = host_ips[src]
@@ -128,6 +141,11 @@ def generate_flows(n: int, seed: int = 7, n_hosts: int | None = None, n_profiles
     flip = rng.random(n) < 0.15
     sport = np.where(flip, port_of, eph)
     dport = np.where(flip, eph, port_of)
+    if wide_vocab:
+        s2s = rng.random(n) < 0.2  # server-to-server: both low (111111) or both high (333333)
+        both_low = s2s & (rng.random(n) < 0.5)
+        sport = np.where(both_low, rng.integers(1, 1025, size=n), np.where(s2s, rng.integers(1025, 65536, size=n), sport))
+        dport = np.where(s2s & ~both_low, rng.integers(1025, 65536, size=n), dport)
     sip2 = np.where(flip, dip, sip)
     dip2 = np.where(flip, sip, dip)
 

@@ -19,7 +19,8 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, n_total, out_q):
+def _worker(rank, world, port, n_total, out_q, env=None):
+    os.environ.update(env or {})
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     torch.set_num_threads(1)
@@ -39,11 +40,11 @@ def _worker(rank, world, port, n_total, out_q):
     pc.shutdown()
 
 
-def _run_world(world, n_total):
+def _run_world(world, n_total, env=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_total, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_total, q, env)) for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=600)
@@ -53,11 +54,13 @@ def _run_world(world, n_total):
     return res
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_dp_matches_single_process(world):
+@pytest.mark.parametrize("world,env", [(2, None), (3, None), (3, {"ONI_X01_LIGHT_MAX": "40"}),
+                                       (2, {"ONI_X01_PACK": "0"})])
+def test_dp_matches_single_process(world, env):
+    """Also with the packed X01 payload forced into a light/heavy word mix, and unpacked."""
     n = 6000
     one = _run_world(1, n)
-    many = _run_world(world, n)
+    many = _run_world(world, n, env)
     assert np.array_equal(one[0], many[0])
     assert np.array_equal(one[1], many[1])
     assert np.array_equal(one[2], many[2]) and np.array_equal(one[3], many[3])
@@ -108,3 +111,30 @@ def test_lpt_place_native_matches_numpy_reference():
         ref[i] = k
     assert native.lib().oni_lpt_place is not None
     assert np.array_equal(own, ref) and np.array_equal(l1, l2)
+
+
+@pytest.mark.parametrize("W", [1, 2, 3, 8])
+def test_x01_packed_sum_is_exact(W):
+    """Σ over W ranks of packed buffers (int32 wrap-around, as RCCL sums) unpacks to the exact
+    per-entry sum whenever every light value is within ±O."""
+    from oni355 import ops
+    r = np.random.default_rng(W)
+    V, KS, tail = 300, 20, 37
+    O = 32767 // W
+    heavy = torch.from_numpy(np.sort(r.choice(V, 40, replace=False)).astype(np.int32))
+    light = torch.from_numpy(np.setdiff1d(np.arange(V), heavy.numpy()).astype(np.int32))
+    n = ops.x01_packed_len(light.numel(), heavy.numel(), KS, tail)
+    total = torch.zeros(V * KS + tail, dtype=torch.int64)
+    acc = torch.zeros(n, dtype=torch.int64)
+    for _ in range(W):
+        dn = torch.from_numpy(r.integers(-O, O + 1, V * KS + tail).astype(np.int32))
+        dn.view(-1)[: V * KS].view(V, KS)[heavy.long()] = torch.from_numpy(
+            r.integers(-2**24, 2**24, (heavy.numel(), KS)).astype(np.int32))
+        total += dn.to(torch.int64)
+        out = torch.zeros(n, dtype=torch.int32)
+        ops.x01_pack(dn, light, heavy, KS, V * KS, tail, O, out)
+        acc += out.to(torch.int64) & 0xFFFFFFFF
+    summed = ((acc + 2**31) % 2**32 - 2**31).to(torch.int32)  # int32 wrap-around sum
+    back = torch.zeros(V * KS + tail, dtype=torch.int32)
+    ops.x01_unpack(summed, light, heavy, KS, V * KS, tail, W * O, back)
+    assert torch.equal(back.to(torch.int64), total)
