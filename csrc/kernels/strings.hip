@@ -2,7 +2,8 @@
 //
 // Reference behaviour (oni-ml DNSWordCreation / DomainProcessor.extractDomainInfo / Entropy /
 // TopDomains, ProxyWordCreation; SURVEY.md §2.2 C17/C18, §2.8, [U-M]): split a name into
-// subdomain / registered domain / TLD with country-code awareness, flag user-domain and
+// subdomain / registered domain / public suffix (table-driven PSL rules, oni355/ref/psl.py),
+// flag user-domain and
 // top-1M membership, measure subdomain length, Shannon entropy and dot count.
 //
 // Layout: N strings as int64 offsets [N+1] + UTF-8 bytes (the columnar store's native form).
@@ -75,58 +76,73 @@ struct DomainOut {
   int32_t* sub_off;     // [N][2] subdomain / registered-domain start offsets (relative)
 };
 
-// second-level labels that make a ccTLD a two-label public suffix (co.uk, com.br, ac.jp, ...)
-__device__ __forceinline__ bool is_sld(const uint8_t* p, int64_t a, int64_t b) {
-  const int n = (int)(b - a);
-  if (n < 2 || n > 4) return false;
-  char s[4] = {0, 0, 0, 0};
-  for (int i = 0; i < n; ++i) s[i] = (char)lower(p[a + i]);
-  const uint32_t v = (uint32_t)(uint8_t)s[0] | ((uint32_t)(uint8_t)s[1] << 8) | ((uint32_t)(uint8_t)s[2] << 16) |
-                     ((uint32_t)(uint8_t)s[3] << 24);
-#define W(a, b, c, d) ((uint32_t)(a) | ((uint32_t)(b) << 8) | ((uint32_t)(c) << 16) | ((uint32_t)(d) << 24))
-  switch (v) {
-    case W('c', 'o', 0, 0): case W('a', 'c', 0, 0): case W('o', 'r', 0, 0): case W('n', 'e', 0, 0):
-    case W('g', 'o', 0, 0): case W('c', 'o', 'm', 0): case W('n', 'e', 't', 0): case W('o', 'r', 'g', 0):
-    case W('g', 'o', 'v', 0): case W('e', 'd', 'u', 0): case W('m', 'i', 'l', 0): case W('n', 'i', 'c', 0):
-    case W('l', 't', 'd', 0): case W('p', 'l', 'c', 0): case W('s', 'c', 'h', 0): case W('n', 'o', 'm', 0):
-    case W('g', 'o', 'b', 0): case W('g', 'e', 'n', 0): case W('b', 'i', 'z', 0): case W('i', 'n', 'f', 'o'):
-    case W('g', 'o', 'u', 'v'): case W('a', 's', 's', 'o'):
-      return true;
-    default:
-      return false;
+// Public-suffix rules (oni355/ref/psl.py): two open-addressing FNV-1a sets, exact / wildcard rules
+// (the latter stored as "*.rest") and exceptions (without the '!').
+struct Psl {
+  const uint64_t* rules;
+  uint64_t rules_mask;
+  const uint64_t* exc;
+  uint64_t exc_mask;
+  int max_labels;  // ≤ kMaxLabels
+};
+constexpr int kMaxLabels = 6;
+
+__device__ __forceinline__ uint64_t fnv_cont(uint64_t h, const uint8_t* p, int64_t a, int64_t b) {
+  for (int64_t i = a; i < b; ++i) h = (h ^ lower(p[i])) * kFnvPrime;
+  return h;
+}
+
+// Start of the registered domain of [a, b): public suffix by the PSL algorithm (longest deciding
+// suffix; exception → one label shorter; no rule → last label), plus one more label.
+// dots[j] = position of the (j+1)-th '.' from the right (at most max_labels of them, nd found).
+__device__ int64_t registered_start(const uint8_t* __restrict__ p, int64_t a, int64_t b, const int64_t* dots, int nd,
+                                    const Psl& psl) {
+  const int nlab = b > a ? nd + 1 : 0;
+  // FNV state after "*." (wildcard rules)
+  const uint64_t wild0 = (((kFnvOff ^ (uint64_t)'*') * kFnvPrime) ^ (uint64_t)'.') * kFnvPrime;
+  int ps = 1;
+  const int kmax = nlab < psl.max_labels ? nlab : psl.max_labels;
+  for (int k = kmax; k >= 1; --k) {
+    const int64_t sk = k <= nd ? dots[k - 1] + 1 : a;
+    const uint64_t h = fnv_range(p, sk, b);
+    if (set_probe(psl.exc, psl.exc_mask, h)) {
+      ps = k - 1;
+      break;
+    }
+    bool hit = set_probe(psl.rules, psl.rules_mask, h);
+    if (!hit && k >= 2) {
+      const int64_t sk1 = (k - 1) <= nd ? dots[k - 2] + 1 : a;
+      hit = set_probe(psl.rules, psl.rules_mask, fnv_cont(wild0, p, sk1, b));
+    }
+    if (hit) {
+      ps = k;
+      break;
+    }
   }
-#undef W
+  if (nlab <= ps) return a;
+  return ps + 1 <= nd ? dots[ps] + 1 : a;
 }
 
 __global__ __launch_bounds__(256) void k_domain_features(const int64_t* __restrict__ off, const uint8_t* __restrict__ p,
                                                          int64_t n, const uint64_t* __restrict__ top_tab,
                                                          uint64_t top_mask, uint64_t user_hash, int user_is_label,
                                                          const float* __restrict__ clogc, const float* __restrict__ lg,
-                                                         DomainOut o) {
+                                                         Psl psl, DomainOut o) {
   __shared__ uint8_t hist[256][kBins];
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const int64_t a = off[i];
     int64_t b = off[i + 1];
     while (b > a && p[b - 1] == '.') --b;  // trailing root dot
-    // last three dot positions
-    int64_t d1 = -1, d2 = -1, d3 = -1;
-    int per = 0;
+    // dot positions from the right (as many as the suffix rules can look at) + the total count
+    int64_t dots[kMaxLabels];
+    int nd = 0, per = 0;
     for (int64_t j = b - 1; j >= a; --j)
       if (p[j] == '.') {
         ++per;
-        if (d1 < 0) d1 = j;
-        else if (d2 < 0) d2 = j;
-        else if (d3 < 0) d3 = j;
+        if (nd < psl.max_labels) dots[nd++] = j;
       }
-    // TLD = (d1, b); second label = (d2, d1); third = (d3, d2)
-    int64_t reg = a;  // start of registered domain
-    if (d1 >= 0) {
-      const bool cc = (b - d1 - 1) == 2;  // 2-letter TLD = country code
-      if (cc && d2 >= 0 && is_sld(p, d2 + 1, d1)) reg = d3 >= 0 ? d3 + 1 : a;
-      else reg = d2 >= 0 ? d2 + 1 : a;
-      if (cc && d2 < 0 && is_sld(p, a, d1)) reg = a;  // bare "co.uk"
-    }
+    const int64_t reg = registered_start(p, a, b, dots, nd, psl);  // start of registered domain
     const int64_t sub_end = reg > a ? reg - 1 : a;  // subdomain = [a, reg-1)
     const uint64_t rh = fnv_range(p, reg, b);
     // registered label only (for USER_DOMAIN given as a bare label, e.g. "intel")
@@ -176,11 +192,15 @@ __global__ void k_set_probe(const uint64_t* __restrict__ h, int64_t n, const uin
 
 ONI_API int oni_domain_features(const int64_t* off, const uint8_t* chars, int64_t n, const uint64_t* top_tab,
                                 uint64_t top_mask, uint64_t user_hash, int user_is_label, const float* clogc,
-                                const float* lg, uint64_t* reg_hash, uint8_t* top, int32_t* sub_len, float* sub_ent,
-                                int32_t* periods, hipStream_t s) {
+                                const float* lg, const uint64_t* psl_rules, uint64_t psl_rules_mask,
+                                const uint64_t* psl_exc, uint64_t psl_exc_mask, int psl_max_labels,
+                                uint64_t* reg_hash, uint8_t* top, int32_t* sub_len, float* sub_ent, int32_t* periods,
+                                hipStream_t s) {
+  if (psl_max_labels < 1 || psl_max_labels > kMaxLabels) return (int)hipErrorInvalidValue;
   DomainOut o{reg_hash, top, sub_len, sub_ent, periods, nullptr};
+  const Psl psl{psl_rules, psl_rules_mask, psl_exc, psl_exc_mask, psl_max_labels};
   k_domain_features<<<oni::grid_for(n, 256, 2048), 256, 0, s>>>(off, chars, n, top_tab, top_mask, user_hash,
-                                                                 user_is_label, clogc, lg, o);
+                                                                 user_is_label, clogc, lg, psl, o);
   return (int)hipGetLastError();
 }
 

@@ -200,6 +200,8 @@ def main(argv=None) -> int:
                       ALPHA=a.alpha, BURNIN=a.burnin)
     if a.max_restarts > 0 and os.environ.get("ONI_SUPERVISED") != "1":
         return supervise(a, argv, cfg)
+    if cfg.PUBLIC_SUFFIX:
+        os.environ["ONI_PUBLIC_SUFFIX"] = cfg.PUBLIC_SUFFIX  # read by oni355.ref.psl.default_rules
     gpus = a.gpus if a.gpus is not None else cfg.PROCESS_COUNT
     if gpus > 1 and "WORLD_SIZE" not in os.environ:
         return _relaunch(gpus, argv)

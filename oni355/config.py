@@ -39,6 +39,7 @@ class OniConfig:
     HPATH: str = ""                 # unused (no HDFS); kept for duxbay.conf compatibility
     DATA_ROOT: str = "./oni_store"  # columnar day store
     TOP_DOMAINS: str = ""           # top-1M list (Alexa-style CSV: rank,domain)
+    PUBLIC_SUFFIX: str = ""         # public suffix list (Mozilla PSL format); "" = built-in oni355/data list
     # OA
     IPLOC: str = ""                 # geo ip-range CSV
     NETWORK_CONTEXT: str = ""       # network context CSV

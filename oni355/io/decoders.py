@@ -205,15 +205,99 @@ def read_proxy_log(path: str, threads: int = 0) -> dict:
             out[c] = StringColumn.from_list(["-"] * n)
     for c in ("respcode", "uriport"):
         out[c] = np.asarray(out[c]).astype(np.int32)
-    sch, host, port, pth, qry = (out[k].to_list() if hasattr(out[k], "to_list") else out[k]
-                                 for k in ("urischeme", "host", "uriport", "uripath", "uriquery"))
-    full = []
-    for s, h, p, pa, q in zip(sch, host, port, pth, qry):
-        u = f"{s}://{h}" + (f":{p}" if p not in (0, 80, 443) else "") + (pa if pa != "-" else "")
-        full.append(u + (q if q not in ("-", "") else ""))
-    out["fulluri"] = StringColumn.from_list(full)
+    out["fulluri"] = full_uri(out["urischeme"], out["host"], np.asarray(out["uriport"]), out["uripath"],
+                              out["uriquery"])
     out["_bad_rows"] = bad
     return out
+
+
+def _is_dash(c: StringColumn, allow_empty: bool = False) -> np.ndarray:
+    ln = np.diff(c.offsets)
+    first = np.zeros(len(c), np.uint8)
+    nz = ln > 0
+    first[nz] = c.chars[c.offsets[:-1][nz]]
+    m = (ln == 1) & (first == ord("-"))
+    return m | (ln == 0) if allow_empty else m
+
+
+def full_uri(scheme: StringColumn, host: StringColumn, port: np.ndarray, path: StringColumn,
+             query: StringColumn) -> StringColumn:
+    """``scheme://host[:port]path[query]`` per row (port omitted for 0/80/443, '-' fields
+    dropped), vectorised (StringColumn.join_rows) -- no per-row Python at 1e8 rows."""
+    port = np.asarray(port).astype(np.int64)
+    up, inv = np.unique(port, return_inverse=True)
+    pstr = StringColumn.from_list([f":{p}" for p in up.tolist()]).take(inv)
+    return StringColumn.join_rows([(scheme, None), (b"://", None), (host, None),
+                                   (pstr, ~np.isin(port, (0, 80, 443))), (path, ~_is_dash(path)),
+                                   (query, ~_is_dash(query, allow_empty=True))])
+
+
+_MONTHS = np.frombuffer(b"JanFebMarAprMayJunJulAugSepOctNovDec", np.uint8).reshape(12, 3)
+_DIGITS2 = np.frombuffer("".join(f"{i:02d}" for i in range(100)).encode(), np.uint8).reshape(100, 2)
+
+
+def frame_times(ts_ns: np.ndarray) -> StringColumn:
+    """tshark ``frame.time`` text ("%b %d, %Y %H:%M:%S.%f UTC", fixed 32 bytes) of nanosecond
+    timestamps, vectorised (numpy datetime64 fields + digit arithmetic)."""
+    ts_ns = np.asarray(ts_ns, np.int64)
+    n = ts_ns.size
+    us = ts_ns // 1000
+    dt = us.astype("datetime64[us]")
+    day = dt.astype("datetime64[D]")
+    ym = dt.astype("datetime64[M]")
+    year = ym.astype(np.int64) // 12 + 1970
+    month = ym.astype(np.int64) % 12
+    mday = (day - ym.astype("datetime64[D]")).astype(np.int64) + 1
+    sod = us - day.astype("datetime64[us]").astype(np.int64)
+    hh, mm, ss, frac = sod // 3_600_000_000, sod // 60_000_000 % 60, sod // 1_000_000 % 60, sod % 1_000_000
+    out = np.empty((n, 32), np.uint8)
+
+    def put(col, v, w):  # w-digit zero-padded decimal (w even) via a two-digit table
+        for k in range(0, w, 2):
+            out[:, col + w - 2 - k:col + w - k] = _DIGITS2[(v // 10 ** k) % 100]
+
+    out[:, 0:3] = _MONTHS[month]
+    out[:, 3] = 32
+    put(4, mday, 2)
+    out[:, 6], out[:, 7] = 44, 32
+    put(8, year, 4)
+    out[:, 12] = 32
+    put(13, hh, 2)
+    out[:, 15] = 58
+    put(16, mm, 2)
+    out[:, 18] = 58
+    put(19, ss, 2)
+    out[:, 21] = 46
+    put(22, frac, 6)
+    out[:, 28:32] = np.frombuffer(b" UTC", np.uint8)
+    return StringColumn.from_fixed(out)
+
+
+class FrameTimeColumn(StringColumn):
+    """``frame_time`` of a decoded pcap, formatted lazily: the ML path never reads the text (it
+    uses ``unix_tstamp``), so only the rows that are rendered (the top-N results) or stored are
+    ever formatted (:func:`frame_times`). Behaves as a StringColumn everywhere else."""
+
+    def __init__(self, ts_ns: np.ndarray):  # noqa: super().__init__ deliberately not called
+        self.ts_ns = np.asarray(ts_ns, np.int64)
+        self._mat = None
+
+    def _m(self) -> StringColumn:
+        if self._mat is None:
+            self._mat = frame_times(self.ts_ns)
+        return self._mat
+
+    offsets = property(lambda self: self._m().offsets)
+    chars = property(lambda self: self._m().chars)
+
+    def __len__(self) -> int:
+        return int(self.ts_ns.size)
+
+    def take(self, idx) -> StringColumn:
+        return frame_times(self.ts_ns[np.asarray(idx, dtype=np.int64)])
+
+    def slice(self, lo: int, hi: int) -> "FrameTimeColumn":
+        return FrameTimeColumn(self.ts_ns[lo:hi])
 
 
 # ------------------------------------------------------------------------------------------------
@@ -244,8 +328,7 @@ def read_pcap_dns(path: str, threads: int = 0) -> dict:
         L.oni_pcap_dns_free(h)
     unix = ts // 1_000_000_000
     return {
-        "frame_time": StringColumn.from_list([_dt.datetime.fromtimestamp(t / 1e9, tz=_dt.timezone.utc)
-                                              .strftime("%b %d, %Y %H:%M:%S.%f UTC") for t in ts.tolist()]),
+        "frame_time": FrameTimeColumn(ts),
         "unix_tstamp": unix,
         "frame_len": flen,
         "ip_src": src,

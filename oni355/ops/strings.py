@@ -22,14 +22,23 @@ class OniPack(C.Structure):
     ]
 
 
-_lib.register_optional("oni_domain_features", [vp, vp, i64, vp, C.c_uint64, C.c_uint64, C.c_int, vp, vp, vp, vp, vp,
-                                               vp, vp, vp])
+_lib.register_optional("oni_domain_features", [vp, vp, i64, vp, C.c_uint64, C.c_uint64, C.c_int, vp, vp,
+                                               vp, C.c_uint64, vp, C.c_uint64, C.c_int,
+                                               vp, vp, vp, vp, vp, vp])
 _lib.register_optional("oni_string_features", [vp, vp, i64, vp, vp, vp, vp, vp, vp])
 _lib.register_optional("oni_set_probe", [vp, i64, vp, C.c_uint64, vp, vp])
 _lib.register_optional("oni_pack_words", [C.POINTER(OniPack), vp])
 _lib.register_optional("oni_pack_sizeof", [])
 
 _tables: dict = {}
+
+
+def _dev_psl(device, rules):
+    key = (str(device), id(rules))
+    if key not in _tables:
+        _tables[key] = (torch.from_numpy(rules.rule_set.table.view(np.int64)).to(device),
+                        torch.from_numpy(rules.exc_set.table.view(np.int64)).to(device))
+    return _tables[key]
 
 
 def _dev_tables(device):
@@ -44,11 +53,15 @@ def _u64(t: torch.Tensor) -> np.ndarray:
     return t.cpu().numpy().view(np.uint64)
 
 
-def domain_features(offsets: torch.Tensor, chars: torch.Tensor, topset: ss.HashSet | None, user_domain: str = ""):
-    """Returns (reg_hash int64(u64 bits), top u8, sub_len i32, sub_ent f32, periods i32)."""
+def domain_features(offsets: torch.Tensor, chars: torch.Tensor, topset: ss.HashSet | None, user_domain: str = "",
+                    rules=None):
+    """Returns (reg_hash int64(u64 bits), top u8, sub_len i32, sub_ent f32, periods i32).
+    ``rules``: public-suffix rules (oni355.ref.psl.SuffixRules; default: the built-in list)."""
+    from ..ref import psl
+    rules = rules or psl.default_rules()
     n = offsets.numel() - 1
     if offsets.device.type != "cuda":
-        rh, top, sl, en, per = ss.domain_features(offsets.numpy(), chars.numpy(), topset, user_domain)
+        rh, top, sl, en, per = ss.domain_features(offsets.numpy(), chars.numpy(), topset, user_domain, rules)
         return (torch.from_numpy(rh.view(np.int64)), torch.from_numpy(top), torch.from_numpy(sl),
                 torch.from_numpy(en), torch.from_numpy(per))
     dev = offsets.device
@@ -60,9 +73,12 @@ def domain_features(offsets: torch.Tensor, chars: torch.Tensor, topset: ss.HashS
             torch.empty(n, dtype=torch.int32, device=dev), torch.empty(n, dtype=torch.float32, device=dev),
             torch.empty(n, dtype=torch.int32, device=dev))
     ch = chars if chars.numel() else torch.zeros(1, dtype=torch.uint8, device=dev)
+    prt, pet = _dev_psl(dev, rules)
     _lib.check(_lib.lib().oni_domain_features(_lib.ptr(offsets), _lib.ptr(ch), n, _lib.ptr(tab), mask, uh,
                                               1 if "." not in user_domain else 0, _lib.ptr(clogc), _lib.ptr(lg),
-                                              *map(_lib.ptr, outs), _lib.stream()), "oni_domain_features")
+                                              _lib.ptr(prt), rules.rule_set.mask, _lib.ptr(pet), rules.exc_set.mask,
+                                              rules.max_labels, *map(_lib.ptr, outs), _lib.stream()),
+               "oni_domain_features")
     return outs
 
 

@@ -1,7 +1,7 @@
 """NumPy/Python oracle for the string kernels (csrc/kernels/strings.hip, pack_words.hip).
 
 Bit-exact mirror: FNV-1a over lowercased bytes, the 64-bin character classes, the f32 entropy
-tables and their summation order, the ccTLD / second-level-label rule, the open-addressing set.
+tables and their summation order, the public-suffix rule (psl.py), the open-addressing set.
 """
 from __future__ import annotations
 
@@ -13,8 +13,6 @@ F32 = np.float32
 FNV_OFF = 1469598103934665603
 FNV_PRIME = 1099511628211
 M64 = (1 << 64) - 1
-SLD = {"co", "ac", "or", "ne", "go", "com", "net", "org", "gov", "edu", "mil", "nic", "ltd", "plc", "sch", "nom",
-       "gob", "gen", "biz", "info", "gouv", "asso"}
 
 
 def tables() -> tuple[np.ndarray, np.ndarray]:
@@ -65,26 +63,15 @@ def entropy(b: bytes) -> np.float32:
     return F32(_LG[min(n, 255)] - F32(s / F32(n)))
 
 
-def split_domain(name: bytes) -> tuple[int, int, int]:
-    """(registered-domain start, end, periods) for a name (trailing dots stripped)."""
+def split_domain(name: bytes, rules=None) -> tuple[int, int, int]:
+    """(registered-domain start, end, periods) for a name (trailing dots stripped); the
+    registered domain is the public suffix (oni355/ref/psl.py rules) plus one label."""
+    from .psl import registered_start
     b = len(name)
     while b > 0 and name[b - 1] == 46:
         b -= 1
-    dots = [j for j in range(b - 1, -1, -1) if name[j] == 46]
-    per = len(dots)
-    d1 = dots[0] if len(dots) > 0 else -1
-    d2 = dots[1] if len(dots) > 1 else -1
-    d3 = dots[2] if len(dots) > 2 else -1
-    reg = 0
-    if d1 >= 0:
-        cc = (b - d1 - 1) == 2
-        if cc and d2 >= 0 and _lower(name[d2 + 1:d1]).decode("latin1") in SLD:
-            reg = d3 + 1 if d3 >= 0 else 0
-        else:
-            reg = d2 + 1 if d2 >= 0 else 0
-        if cc and d2 < 0 and _lower(name[0:d1]).decode("latin1") in SLD:
-            reg = 0
-    return reg, b, per
+    per = sum(1 for j in range(b) if name[j] == 46)
+    return registered_start(name, b, rules), b, per
 
 
 class HashSet:
@@ -118,7 +105,7 @@ class HashSet:
         return False
 
 
-def domain_features(offsets, chars, topset: HashSet | None, user_domain: str = ""):
+def domain_features(offsets, chars, topset: HashSet | None, user_domain: str = "", rules=None):
     offsets = np.asarray(offsets, dtype=np.int64)
     raw = bytes(np.asarray(chars, dtype=np.uint8))
     n = offsets.size - 1
@@ -131,7 +118,7 @@ def domain_features(offsets, chars, topset: HashSet | None, user_domain: str = "
     per = np.zeros(n, np.int32)
     for i in range(n):
         name = raw[offsets[i]:offsets[i + 1]]
-        reg, b, p = split_domain(name)
+        reg, b, p = split_domain(name, rules)
         sub_end = reg - 1 if reg > 0 else 0
         rh = fnv1a(name[reg:b])
         lab_end = reg

@@ -63,6 +63,49 @@ class StringColumn:
         return [self[i] for i in range(len(self))]
 
     @staticmethod
+    def join_rows(pieces: list) -> "StringColumn":
+        """Row-wise concatenation without per-row Python: ``pieces`` are (StringColumn | bytes,
+        include-mask or None) pairs; row i of the result is the concatenation of every piece whose
+        mask is true at i (a bytes piece is the same literal on every row)."""
+        n = None
+        for c, m in pieces:
+            if isinstance(c, StringColumn):
+                n = len(c)
+            elif m is not None:
+                n = len(m)
+            if n is not None:
+                break
+        n = 0 if n is None else n
+        lens = []
+        for c, m in pieces:
+            ln = (np.diff(c.offsets) if isinstance(c, StringColumn) else np.full(n, len(c), np.int64))
+            lens.append(ln if m is None else np.where(m, ln, 0))
+        tot = np.sum(lens, axis=0) if lens else np.zeros(n, np.int64)
+        off = np.zeros(n + 1, np.int64)
+        np.cumsum(tot, out=off[1:])
+        out = np.empty(int(off[-1]), np.uint8)
+        pos = off[:-1].copy()
+        for (c, m), ln in zip(pieces, lens):
+            k = int(ln.sum())
+            if k:
+                dst = np.repeat(pos, ln) + (np.arange(k, dtype=np.int64) - np.repeat(np.cumsum(ln) - ln, ln))
+                if isinstance(c, StringColumn):
+                    src = np.repeat(c.offsets[:-1], ln) + (dst - np.repeat(pos, ln))
+                    out[dst] = c.chars[src]
+                else:
+                    lit = np.frombuffer(c, np.uint8)
+                    out[dst] = lit[dst - np.repeat(pos, ln)]
+            pos += ln
+        return StringColumn(off, out)
+
+    @staticmethod
+    def from_fixed(a: np.ndarray) -> "StringColumn":
+        """[n, w] uint8 rows (fixed-width strings) → StringColumn."""
+        a = np.ascontiguousarray(a, dtype=np.uint8)
+        n, w = a.shape
+        return StringColumn(np.arange(n + 1, dtype=np.int64) * w, a.reshape(-1))
+
+    @staticmethod
     def concat(parts: list["StringColumn"]) -> "StringColumn":
         if not parts:
             return StringColumn(np.zeros(1, np.int64), np.zeros(0, np.uint8))

@@ -65,3 +65,22 @@ def test_proxy_pipeline_gpu_matches_cpu(gpu):
     rc = run_proxy(day.cols, K=20, sweeps=5, maxresults=100, device="cpu", top_domains=["google.com"])
     rg = run_proxy(day.cols, K=20, sweeps=5, maxresults=100, device=gpu, top_domains=["google.com"])
     assert np.array_equal(rc.rows, rg.rows) and np.array_equal(rc.scores, rg.scores)
+
+
+def test_domain_features_public_suffix_table_bitwise(gpu, tmp_path):
+    """The kernel's table-driven registered-domain split == the oracle on adversarial names, with the
+    built-in list and with a custom PSL file (deep, wildcard and exception rules)."""
+    from oni355.ref import psl
+    from oni355.store.columnar import StringColumn
+    names = ["a.b.www.ck", "x.y.ck", "ck", "www.ck", "x.city.kawasaki.jp", "a.b.c.d.e.f.g.h.example.co.uk",
+             "co.uk", ".", "..", "a..b.com", "", "x", "cdn.foo.github.io", "WWW.BBC.CO.UK.", "q.keep.dyn.example.com",
+             "z.x.y.dyn.example.com", "s.school.pvt.k12.ma.us", "evil.co.zz", "-.-.-", "a" * 250 + ".com"]
+    p = tmp_path / "psl.dat"
+    p.write_text("com\nexample.com\n*.dyn.example.com\n!keep.dyn.example.com\npvt.k12.ma.us\nus\n")
+    for rules in (psl.default_rules(), psl.SuffixRules.load(str(p))):
+        sc = StringColumn.from_list(names)
+        want = ss.domain_features(sc.offsets, sc.chars, None, "", rules)
+        got = sops.domain_features(torch.from_numpy(sc.offsets).to(gpu), torch.from_numpy(sc.chars).to(gpu), None, "",
+                                   rules)
+        for w, g in zip(want, got):
+            assert np.array_equal(np.asarray(w).view(np.uint8), g.cpu().numpy().view(np.uint8))

@@ -21,7 +21,7 @@ from oni355.ops import strings      # noqa: F401  registers its launchers late
 missing = [n for n in _lib._OPTIONAL_SIGS if hasattr(h, n) and getattr(h, n).argtypes is None]
 missing += [n for n in _lib._SIGS if getattr(h, n).argtypes is None]
 assert not missing, missing
-assert h.oni_domain_features.argtypes[0] is C.c_void_p and len(h.oni_domain_features.argtypes) == 15
+assert h.oni_domain_features.argtypes[0] is C.c_void_p and len(h.oni_domain_features.argtypes) == 20
 print("bound", len(_lib._SIGS) + len(_lib._OPTIONAL_SIGS))
 """
 

@@ -1,4 +1,4 @@
-"""DNS/proxy featurization spec (CPU): domain split with ccTLD rule, entropy, top-1M set, pcap."""
+"""DNS/proxy featurization spec (CPU): domain split by the public-suffix table, entropy, top-1M set, pcap."""
 import math
 
 import numpy as np
@@ -19,6 +19,13 @@ from oni355.store.columnar import StringColumn
     ("58.31.225.10.in-addr.arpa", "in-addr.arpa", "58.31.225.10", 5),
     ("co.uk", "co.uk", "", 1),
     ("x.amazon.co.jp", "amazon.co.jp", "x", 3),
+    # table-driven public suffixes (oni355/data/public_suffix_list.dat): wildcard / exception / private rules
+    ("a.b.www.ck", "www.ck", "a.b", 3),                # !www.ck exception under *.ck
+    ("x.y.ck", "x.y.ck", "", 2),                       # *.ck wildcard: y.ck is a public suffix
+    ("x.city.kawasaki.jp", "city.kawasaki.jp", "x", 3),
+    ("cdn.foo.github.io", "foo.github.io", "cdn", 3),  # private-section rule
+    ("evil.co.zz", "co.zz", "evil", 2),                # unknown TLD: the implicit "*" rule
+    ("WWW.BBC.CO.UK", "BBC.CO.UK", "WWW", 3),          # case-insensitive
 ])
 def test_split_domain(name, reg, sub, periods):
     b = name.encode()
@@ -91,3 +98,20 @@ def test_pcap_truncated_and_garbage(tmp_path):
     (tmp_path / "bad.pcap").write_bytes(b"\x00" * 100)
     with pytest.raises(OSError):
         read_pcap_dns(str(tmp_path / "bad.pcap"))
+
+
+def test_custom_suffix_list_drives_the_split(tmp_path):
+    """A PSL file (Mozilla format) replaces the built-in rules: deep, wildcard and exception rules."""
+    from oni355.ref import psl
+    p = tmp_path / "psl.dat"
+    p.write_text("// test list\ncom\nexample.com\n*.dyn.example.com\n!keep.dyn.example.com\npvt.k12.ma.us\nus\n")
+    rules = psl.SuffixRules.load(str(p))
+    cases = {b"a.b.example.com": b"b.example.com", b"x.y.dyn.example.com": b"x.y.dyn.example.com",
+             b"z.x.y.dyn.example.com": b"x.y.dyn.example.com", b"q.keep.dyn.example.com": b"keep.dyn.example.com",
+             b"s.school.pvt.k12.ma.us": b"school.pvt.k12.ma.us", b"www.google.com": b"google.com"}
+    for name, reg in cases.items():
+        r, e, _ = ss.split_domain(name, rules)
+        assert name[r:e] == reg, (name, name[r:e])
+    # the built-in list still splits co.uk names; the custom one does not know .uk rules
+    r, e, _ = ss.split_domain(b"news.bbc.co.uk", rules)
+    assert b"news.bbc.co.uk"[r:e] == b"co.uk"
