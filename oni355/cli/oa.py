@@ -4,7 +4,10 @@ SURVEY.md §2.2 C27/C33, §3.5).
   oni-oa -d 20160708 -t flow -l 3000             # enrich results → <LPATH>/flow/20160708/flow_scores.csv
   oni-oa score -d 20160708 -t flow --ip 10.0.0.5 --sev 3    # analyst verdict
   oni-oa publish -d 20160708 -t flow             # copy day scores → <LPATH>/flow_scores.csv (ML feedback)
-  oni-oa report -d 20160708 -t flow --html out.html          # static HTML table of the scores
+  oni-oa details -d 20160708 -t flow -l 10        # edge/chord/dendro/timeline TSVs of the top rows
+  oni-oa threat -d 20160708 -t flow --ip 10.0.0.5 --title T --comment C   # storyboard entry
+  oni-oa report -d 20160708 -t flow              # static pages: suspicious / threat-<ip> /
+                                                 # storyboard / ingest_summary (<day>/ui/*.html)
 """
 from __future__ import annotations
 
@@ -18,7 +21,7 @@ import sys
 def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     cmd = "enrich"
-    if argv and argv[0] in ("enrich", "score", "publish", "report"):
+    if argv and argv[0] in ("enrich", "score", "publish", "report", "details", "threat"):
         cmd = argv.pop(0)
     ap = argparse.ArgumentParser(prog=f"oni-oa {cmd}")
     ap.add_argument("-d", "--date", required=True)
@@ -33,7 +36,11 @@ def main(argv=None) -> int:
     ap.add_argument("--word", default=None)
     ap.add_argument("--rows", default=None, help="comma-separated row indices")
     ap.add_argument("--sev", type=int, default=None)
-    ap.add_argument("--html", default=None)
+    ap.add_argument("--html", default=None, help="report: also write the plain scores table here")
+    ap.add_argument("--data-root", default=None, help="details: columnar store with the day's raw events")
+    ap.add_argument("--input", action="append", default=[], help="details: raw input files instead of the store")
+    ap.add_argument("--title", default="")
+    ap.add_argument("--comment", default="")
     a = ap.parse_args(argv)
     from ..config import load_config
     from ..oa import enrich as en
@@ -61,9 +68,28 @@ def main(argv=None) -> int:
         shutil.copyfile(scores_csv, dst)
         print(f"{scores_csv} -> {dst}")
         return 0
+    day = os.path.dirname(scores_csv)
+    if cmd == "details":
+        from ..oa import details as det
+        cols = _day_columns(a, cfg)
+        idx = det.write_details(a.type, res_csv, cols, os.path.join(day, "details"), a.limit or 10)
+        print(f"{len(idx['rows'])} rows, {len(idx['ips'])} IPs -> {os.path.join(day, 'details')}")
+        return 0
+    from ..oa import pages
+    if cmd == "threat":
+        if not a.ip:
+            ap.error("--ip is required")
+        th = pages.add_threat(os.path.join(day, "threats.json"), a.ip, a.title or f"Threat {a.ip}", a.comment,
+                              a.sev if a.sev is not None else 1)
+        print(f"{len(th)} threats in {os.path.join(day, 'threats.json')}")
+        return 0
+    written = pages.render_all(a.type, a.date, day, limit=a.limit or 500)
+    print("\n".join(written))
+    if not a.html:
+        return 0
     from ..io import results as rio
     header, rows = rio.read_csv(scores_csv)
-    out = a.html or scores_csv.replace(".csv", ".html")
+    out = a.html
     with open(out, "w") as f:
         f.write(f"<html><head><title>ONI {a.type} {a.date}</title></head><body><h1>{a.type} suspicious "
                 f"connects {a.date}</h1><table border=1><tr>")
@@ -73,6 +99,28 @@ def main(argv=None) -> int:
         f.write("</table></body></html>\n")
     print(out)
     return 0
+
+
+def _day_columns(a, cfg) -> dict:
+    """The day's raw events for the detail queries: decoded ``--input`` files, else the store."""
+    if a.input:
+        from .ml import _concat, _expand
+        from ..io import decoders
+        parts = []
+        for f in _expand(a.input):
+            if a.type == "flow":
+                if f.endswith((".csv", ".txt")):
+                    parts.append(decoders.read_flow_csv(f)[0])
+                else:
+                    from ..io import nfcapd
+                    parts.append(nfcapd.read_nfcapd(f))
+            elif a.type == "dns":
+                parts.append(decoders.read_pcap_dns(f))
+            else:
+                parts.append(decoders.read_proxy_log(f))
+        return _concat(parts)
+    from ..store import columnar
+    return columnar.read_day(a.data_root or cfg.DATA_ROOT, a.type, a.date)
 
 
 if __name__ == "__main__":

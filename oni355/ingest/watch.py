@@ -39,24 +39,52 @@ def decode_file(source: str, path: str) -> dict:
     return {k: v for k, v in decoders.read_proxy_log(path).items() if not k.startswith("_")}
 
 
-def _row_days(source: str, cols: dict) -> np.ndarray:
+def _fixed_digits(col, offs: list[int]) -> np.ndarray:
+    """Integer made of the ASCII digits at byte offsets ``offs`` of every string (fixed-width
+    fields such as p_date "YYYY-MM-DD" / p_time "HH:MM:SS"), vectorised; short strings -> 0."""
+    o, ln = col.offsets[:-1], np.diff(col.offsets)
+    ok = ln > max(offs)
+    v = np.zeros(len(col), np.int64)
+    for k in offs:
+        d = np.zeros(len(col), np.int64)
+        d[ok] = col.chars[o[ok] + k].astype(np.int64) - 48
+        v = v * 10 + d
+    return np.where(ok, v, 0)
+
+
+def _row_day_hour(source: str, cols: dict) -> tuple[np.ndarray, np.ndarray]:
+    """(days since epoch, hour of day) of every row."""
     if source in ("flow", "dns"):
         t = np.asarray(cols["unix_tstamp"], np.int64)
-        return (t // 86400).astype(np.int64)
-    d = cols["p_date"].to_list()
-    return np.array([(_dt.date.fromisoformat(x) - _dt.date(1970, 1, 1)).days if x else 0 for x in d], np.int64)
+        return (t // 86400).astype(np.int64), (t % 86400) // 3600
+    y = _fixed_digits(cols["p_date"], [0, 1, 2, 3])
+    m = _fixed_digits(cols["p_date"], [5, 6])
+    d = _fixed_digits(cols["p_date"], [8, 9])
+    ok = (y > 0) & (m >= 1) & (m <= 12) & (d >= 1)
+    months = np.where(ok, (y - 1970) * 12 + (m - 1), 0).astype("datetime64[M]")
+    days = (months.astype("datetime64[D]").astype(np.int64) + np.where(ok, d - 1, 0))
+    return np.where(ok, days, 0), np.clip(_fixed_digits(cols["p_time"], [0, 1]), 0, 23)
 
 
-def store_rows(root: str, source: str, cols: dict) -> dict[str, int]:
-    """Append decoded rows to their day partitions; returns {YYYYMMDD: rows}."""
-    days = _row_days(source, cols)
-    out = {}
-    for day in np.unique(days):
-        idx = np.nonzero(days == day)[0]
-        part = {k: (v[idx] if not hasattr(v, "offsets") else v[idx]) for k, v in cols.items()}
+def _row_days(source: str, cols: dict) -> np.ndarray:
+    return _row_day_hour(source, cols)[0]
+
+
+def store_rows(root: str, source: str, cols: dict, hourly: bool = True) -> dict[str, int]:
+    """Append decoded rows to their day (and hour) partitions; returns {YYYYMMDD: rows}."""
+    days, hrs = _row_day_hour(source, cols)
+    key = days * 24 + hrs if hourly else days
+    out: dict[str, int] = {}
+    order = np.argsort(key, kind="stable")
+    uk, first = np.unique(key[order], return_index=True)
+    bounds = list(first) + [key.size]
+    for j, k in enumerate(uk.tolist()):
+        idx = order[bounds[j]:bounds[j + 1]]
+        part = {c: (v.take(idx) if hasattr(v, "offsets") else np.asarray(v)[idx]) for c, v in cols.items()}
+        day = k // 24 if hourly else k
         date = (_dt.date(1970, 1, 1) + _dt.timedelta(days=int(day))).strftime("%Y%m%d")
-        columnar.append_part(root, source, date, part)
-        out[date] = int(idx.size)
+        columnar.append_part(root, source, date, part, hour=int(k % 24) if hourly else None)
+        out[date] = out.get(date, 0) + int(idx.size)
     return out
 
 

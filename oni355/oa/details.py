@@ -7,6 +7,7 @@ filters over the day's columnar store (or any loaded column dict).
 from __future__ import annotations
 
 import csv
+import glob
 import os
 
 import numpy as np
@@ -64,20 +65,24 @@ def timeline(cols: dict, ip, bucket_s: int = 3600) -> list[tuple[int, int]]:
         m = np.asarray(cols["ip_dst"], np.uint32) == x
     else:
         m = np.asarray(cols["clientip"], np.uint32) == x
-    t = np.asarray(cols["unix_tstamp"], np.int64)[m] // bucket_s * bucket_s
+    if "unix_tstamp" in cols:
+        t = np.asarray(cols["unix_tstamp"], np.int64)[m] // bucket_s * bucket_s
+    else:  # proxy logs carry p_date/p_time only: hour-of-day buckets (seconds into the day)
+        t = event_hours(cols, "proxy")[m] * 3600 // bucket_s * bucket_s
     u, c = np.unique(t, return_counts=True)
     return list(zip(u.tolist(), c.tolist()))
 
 
 def ingest_summary(root: str, source: str, date: str) -> list[tuple[int, int]]:
-    """Events per hour of a stored day (the OA ingest-summary page)."""
+    """Events per hour of a stored day (the OA ingest-summary page); hour partitions are counted
+    from their metadata without reading any column."""
+    hs = columnar.hours(root, source, date)
+    if hs and not os.path.exists(os.path.join(columnar.day_dir(root, source, date), "_schema.json")) and \
+            not glob.glob(os.path.join(columnar.day_dir(root, source, date), "part-*")):
+        c = {h: columnar.rows(root, source, date, hours=[h]) for h in hs}
+        return [(i, int(c.get(i, 0))) for i in range(24)]
     cols = columnar.read_day(root, source, date, columns=["unix_tstamp"] if source != "proxy" else ["p_time"])
-    if source == "proxy":
-        h = np.array([int(s[:2]) if s else 0 for s in cols["p_time"].to_list()], np.int64)
-    else:
-        h = (np.asarray(cols["unix_tstamp"], np.int64) % 86400) // 3600
-    c = np.bincount(h, minlength=24)
-    return [(i, int(c[i])) for i in range(24)]
+    return ingest_summary_cols(cols, source)
 
 
 def write_tsv(path: str, header: list[str], rows) -> str:
@@ -88,3 +93,147 @@ def write_tsv(path: str, header: list[str], rows) -> str:
         for r in rows:
             w.writerow(list(r.values()) if isinstance(r, dict) else list(r))
     return path
+
+
+# ------------------------------------------------------------------------------------------------
+# per-suspicious-row detail files (oni-oa "details": edge / chord / dendrogram / timeline TSVs)
+# ------------------------------------------------------------------------------------------------
+def str_eq_mask(col, s: str) -> np.ndarray:
+    """Rows of a StringColumn equal to ``s`` (case-insensitive), vectorised: length filter, then
+    one [candidates × len] byte comparison."""
+    b = np.frombuffer(s.lower().encode(), np.uint8)
+    ln = np.diff(col.offsets)
+    cand = np.nonzero(ln == b.size)[0]
+    m = np.zeros(len(col), bool)
+    if cand.size == 0:
+        return m
+    if b.size == 0:
+        m[cand] = True
+        return m
+    g = col.chars[col.offsets[cand][:, None] + np.arange(b.size)[None, :]]
+    g = np.where((g >= 65) & (g <= 90), g + 32, g)
+    m[cand[(g == b[None, :]).all(1)]] = True
+    return m
+
+
+def event_hours(cols: dict, source: str) -> np.ndarray:
+    if source == "flow" and "trhour" in cols:
+        return np.asarray(cols["trhour"], np.int64)
+    if source == "proxy":
+        from ..ingest.watch import _fixed_digits
+        return _fixed_digits(cols["p_time"], [0, 1])
+    return (np.asarray(cols["unix_tstamp"], np.int64) % 86400) // 3600
+
+
+def ingest_summary_cols(cols: dict, source: str) -> list[tuple[int, int]]:
+    c = np.bincount(np.clip(event_hours(cols, source), 0, 23), minlength=24)
+    return [(i, int(c[i])) for i in range(24)]
+
+
+def dns_edge(cols: dict, qname: str, hour: int | None = None, limit: int = 1000) -> list[tuple]:
+    """Every query for one name (optionally within one hour) -- the DNS edge view."""
+    m = str_eq_mask(cols["dns_qry_name"], qname)
+    if hour is not None:
+        m &= event_hours(cols, "dns") == hour
+    idx = np.nonzero(m)[0][:limit]
+    names, ans = cols["dns_qry_name"].take(idx).to_list(), cols["dns_a"].take(idx).to_list() if "dns_a" in cols else \
+        [""] * idx.size
+    t = np.asarray(cols["unix_tstamp"], np.int64)
+    return [(int(t[i]), ip_str(cols["ip_src"][i]), ip_str(cols["ip_dst"][i]), names[j],
+             int(cols["dns_qry_type"][i]), int(cols["dns_qry_rcode"][i]), ans[j]) for j, i in enumerate(idx)]
+
+
+def dns_dendro(cols: dict, ip, top: int = 200) -> list[tuple[str, str, int]]:
+    """(registered domain, subdomain, queries) for one client IP -- the DNS dendrogram query."""
+    from ..ref.strings_spec import split_domain
+    x = _ip(ip)
+    idx = np.nonzero(np.asarray(cols["ip_dst"], np.uint32) == x)[0]
+    cnt: dict = {}
+    for name in cols["dns_qry_name"].take(idx).to_list():
+        b = name.encode()
+        r, e, _ = split_domain(b)
+        key = (b[r:e].decode(), b[: r - 1].decode() if r > 0 else "")
+        cnt[key] = cnt.get(key, 0) + 1
+    return sorted(((d, s, c) for (d, s), c in cnt.items()), key=lambda t: (-t[2], t[0], t[1]))[:top]
+
+
+def proxy_edge(cols: dict, clientip, host: str, hour: int | None = None, limit: int = 1000) -> list[tuple]:
+    """Requests of one client to one host (optionally within one hour) -- the proxy edge view."""
+    x = _ip(clientip)
+    m = (np.asarray(cols["clientip"], np.uint32) == x) & str_eq_mask(cols["host"], host)
+    if hour is not None:
+        m &= event_hours(cols, "proxy") == hour
+    idx = np.nonzero(m)[0][:limit]
+    get = {c: cols[c].take(idx).to_list() for c in ("p_date", "p_time", "reqmethod", "useragent", "fulluri")
+           if c in cols}
+    out = []
+    for j, i in enumerate(idx):
+        out.append((get["p_date"][j], get["p_time"][j], ip_str(cols["clientip"][i]), host, get["reqmethod"][j],
+                    get["useragent"][j], int(cols["respcode"][i]), get["fulluri"][j], int(cols["scbytes"][i]),
+                    int(cols["csbytes"][i])))
+    return out
+
+
+EDGE_HEADERS = {
+    "flow": ["unix_tstamp", "sip", "dip", "sport", "dport", "proto", "ipkt", "ibyt", "opkt", "obyt", "tdur"],
+    "dns": ["unix_tstamp", "ip_src", "ip_dst", "dns_qry_name", "dns_qry_type", "dns_qry_rcode", "dns_a"],
+    "proxy": ["p_date", "p_time", "clientip", "host", "reqmethod", "useragent", "respcode", "fulluri", "scbytes",
+              "csbytes"],
+}
+
+
+def _safe(s: str) -> str:
+    return "".join(c if c.isalnum() or c in ".-_" else "_" for c in s)[:120]
+
+
+def write_details(source: str, results_csv: str, cols: dict, out_dir: str, limit: int = 10) -> dict:
+    """Detail TSVs for the ``limit`` most suspicious result rows (the reference's per-row
+    ``edge-*.tsv`` / ``chord-*.tsv`` / dendrogram / timeline files + the ingest summary); returns
+    the index that the static pages (oni355.oa.pages) read, also written as ``index.json``."""
+    import json
+    from ..io import results as rio
+    header, rows = rio.read_csv(results_csv)
+    ix = {h: i for i, h in enumerate(header)}
+    os.makedirs(out_dir, exist_ok=True)
+    index = {"source": source, "rows": [], "ips": {}}
+    index["ingest_summary"] = os.path.basename(write_tsv(os.path.join(out_dir, "ingest_summary.tsv"),
+                                                         ["hour", "events"], ingest_summary_cols(cols, source)))
+
+    def per_ip(ip: str) -> None:
+        if ip in index["ips"]:
+            return
+        ent = {"timeline": os.path.basename(write_tsv(os.path.join(out_dir, f"timeline-{ip}.tsv"),
+                                                      ["bucket_start", "events"], timeline(cols, ip)))}
+        if source == "flow":
+            ent["chord"] = os.path.basename(write_tsv(os.path.join(out_dir, f"chord-{ip}.tsv"),
+                                                      ["ip", "peer", "bytes", "packets"], chord(cols, ip)))
+        elif source == "dns":
+            ent["dendro"] = os.path.basename(write_tsv(os.path.join(out_dir, f"dendro-{ip}.tsv"),
+                                                       ["domain", "subdomain", "queries"], dns_dendro(cols, ip)))
+        index["ips"][ip] = ent
+
+    for rank, r in enumerate(rows[:limit]):
+        if source == "flow":
+            sip, dip, hh = r[ix["sip"]], r[ix["dip"]], int(r[ix["trhour"]])
+            e = edge_details(cols, sip, dip, hour=hh)
+            f = write_tsv(os.path.join(out_dir, f"edge-{sip}-{dip}-{hh:02d}.tsv"), EDGE_HEADERS["flow"], e)
+            ip, peer = sip, dip
+            per_ip(sip)
+            per_ip(dip)
+        elif source == "dns":
+            ip, peer = r[ix["ip_dst"]], r[ix["dns_qry_name"]]
+            hh = int(int(float(r[ix["unix_tstamp"]])) % 86400 // 3600)
+            e = dns_edge(cols, peer, hour=hh)
+            f = write_tsv(os.path.join(out_dir, f"edge-{_safe(peer)}-{hh:02d}.tsv"), EDGE_HEADERS["dns"], e)
+            per_ip(ip)
+        else:
+            ip, peer = r[ix["clientip"]], r[ix["host"]]
+            hh = int(r[ix["p_time"]][:2] or 0)
+            e = proxy_edge(cols, ip, peer, hour=hh)
+            f = write_tsv(os.path.join(out_dir, f"edge-{ip}-{_safe(peer)}-{hh:02d}.tsv"), EDGE_HEADERS["proxy"], e)
+            per_ip(ip)
+        index["rows"].append({"rank": rank, "ip": ip, "peer": peer, "hour": hh, "edge": os.path.basename(f),
+                              "edge_rows": len(e), "score": r[ix["score"]]})
+    with open(os.path.join(out_dir, "index.json"), "w") as fh:
+        json.dump(index, fh, indent=1)
+    return index

@@ -1,4 +1,4 @@
-"""Day-partitioned columnar store (replaces the reference's HDFS + Hive/Parquet tables partitioned
+"""Day/hour-partitioned columnar store (replaces the reference's HDFS + Hive/Parquet tables partitioned
 by y/m/d/h).
 
 Layout::
@@ -7,6 +7,7 @@ Layout::
     <root>/<source>/<YYYYMMDD>/<col>.npy           numeric column (np.save, no pickle)
     <root>/<source>/<YYYYMMDD>/<col>.off.npy       string column: int64 offsets [N+1]
     <root>/<source>/<YYYYMMDD>/<col>.chars.bin     string column: UTF-8 bytes
+    <root>/<source>/<YYYYMMDD>/hHH/part-XXXXX/      hour partitions written by ingest (y/m/d/h)
 
 Numeric columns are memory-mapped on read, so a rank of a data-parallel job touches only its own
 row range; strings stay as offsets+bytes (the GPU string kernels' native layout). Appends
@@ -157,11 +158,17 @@ def write_day(root: str, source: str, date: str, cols: dict) -> str:
     return d
 
 
-def append_part(root: str, source: str, date: str, cols: dict) -> str:
-    """Append one ingested file's rows as a new part (used by the ingest workers)."""
-    d = day_dir(root, source, date)
+def hour_dir(root: str, source: str, date: str, hour: int) -> str:
+    return os.path.join(day_dir(root, source, date), f"h{int(hour):02d}")
+
+
+def append_part(root: str, source: str, date: str, cols: dict, hour: int | None = None) -> str:
+    """Append one ingested file's rows as a new part (used by the ingest workers). With ``hour``
+    the part goes to the day's hour partition ``hHH/`` (the reference's y/m/d/h Hive
+    partitioning), so hourly OA drill-downs read only that hour."""
+    d = day_dir(root, source, date) if hour is None else hour_dir(root, source, date, hour)
     os.makedirs(d, exist_ok=True)
-    existing = sorted(glob.glob(os.path.join(d, "part-*")))
+    existing = sorted(p for p in glob.glob(os.path.join(d, "part-*")) if not p.endswith(".tmp"))
     nxt = 0 if not existing else int(os.path.basename(existing[-1])[5:]) + 1
     p = os.path.join(d, f"part-{nxt:05d}")
     _write_part(p + ".tmp", cols)
@@ -169,25 +176,41 @@ def append_part(root: str, source: str, date: str, cols: dict) -> str:
     return p
 
 
-def _parts(d: str) -> list[str]:
+def hours(root: str, source: str, date: str) -> list[int]:
+    """Hour partitions present for a day."""
+    d = day_dir(root, source, date)
+    return sorted(int(os.path.basename(h)[1:]) for h in glob.glob(os.path.join(d, "h[0-9][0-9]")) if os.path.isdir(h))
+
+
+def _parts(d: str, hour_list=None) -> list[str]:
+    """Day-level table + day-level parts (unless only some hours are asked for), then the parts of
+    every hour partition in hour order."""
     parts = []
-    if os.path.exists(os.path.join(d, "_schema.json")):
-        parts.append(d)
-    parts += sorted(p for p in glob.glob(os.path.join(d, "part-*")) if not p.endswith(".tmp"))
+    if hour_list is None:
+        if os.path.exists(os.path.join(d, "_schema.json")):
+            parts.append(d)
+        parts += sorted(p for p in glob.glob(os.path.join(d, "part-*")) if not p.endswith(".tmp"))
+    for h in sorted(glob.glob(os.path.join(d, "h[0-9][0-9]"))):
+        if hour_list is not None and int(os.path.basename(h)[1:]) not in hour_list:
+            continue
+        parts += sorted(p for p in glob.glob(os.path.join(h, "part-*")) if not p.endswith(".tmp"))
     return parts
 
 
-def rows(root: str, source: str, date: str) -> int:
+def rows(root: str, source: str, date: str, hours: list[int] | None = None) -> int:
     total = 0
-    for p in _parts(day_dir(root, source, date)):
+    for p in _parts(day_dir(root, source, date), hours):
         with open(os.path.join(p, "_schema.json")) as f:
             total += json.load(f)["rows"]
     return total
 
 
-def read_day(root: str, source: str, date: str, columns=None, row_range: tuple[int, int] | None = None) -> dict:
+def read_day(root: str, source: str, date: str, columns=None, row_range: tuple[int, int] | None = None,
+             hours: list[int] | None = None) -> dict:
+    """Columns of a stored day (all partitions, or only the hour partitions in ``hours``);
+    ``row_range`` selects global rows [lo, hi) of that view (a data-parallel rank's shard)."""
     d = day_dir(root, source, date)
-    parts = _parts(d)
+    parts = _parts(d, hours)
     if not parts:
         raise FileNotFoundError(f"no {source} data for {date} under {root}")
     out: dict[str, list] = {}
