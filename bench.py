@@ -60,6 +60,8 @@ def parse(argv=None):
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-prefetch", action="store_true",
+                    help="flow: upload each day inside its step instead of overlapping it with the previous one")
     a = ap.parse_args(argv)
     a.topics_set = a.topics is not None
     if a.topics is None:
@@ -165,17 +167,32 @@ def run_pipeline_mode(a, comm) -> dict:
         pcap = os.path.join(tmp, f"dns_rank{rank}.pcap")
         write_pcap(day, pcap)
     top = day.top_domains if a.source == "dns" else None
-    setup_s = time.perf_counter() - t_setup
 
     kw = dict(K=a.topics, sweeps=a.sweeps, tol=1.0, maxresults=a.maxresults, chunk_len=a.chunk_len, device=dev,
               comm=comm, row_offset=row_off)
+    # flow days stream in through a double-buffered prefetcher: the loader's pinned buffers are
+    # uploaded on a copy stream while the previous day computes (every step still uploads its day)
+    pf, pinned = None, None
+    if a.source == "flow" and dev.type == "cuda" and not a.no_prefetch:
+        from oni355.io.staging import Prefetcher
+        from oni355.pipeline.flow import DEVICE_COLS
+        pinned = Prefetcher.pin(day.cols, DEVICE_COLS)
+        pf = Prefetcher(dev)
+        pf.submit(pinned)
+    setup_s = time.perf_counter() - t_setup
 
     def step():
         t0 = time.perf_counter()
         if a.source == "flow":
             from oni355.pipeline.flow import run_flow
             cols = day.cols
-            res = run_flow(cols, **kw)
+            dcols = None
+            if pf is not None:
+                dcols = pf.take()
+                pf.submit(pinned)  # the next day's upload overlaps this day's compute
+            res = run_flow(cols, device_cols=dcols, **kw)
+            if pf is not None:
+                res.timings["h2d_copy_dev_s"] = pf.copy_ms() / 1e3
         elif a.source == "dns":
             from oni355.pipeline.dns import run_dns
             if pcap is not None:
@@ -249,7 +266,8 @@ def run_pipeline_mode(a, comm) -> dict:
                    "events_per_gpu": per, "seq_len": 2 if a.source == "flow" else 1, "parallelism": f"dp{world}",
                    "sweeps_per_step": a.sweeps, "maxresults": a.maxresults, "baseline_config": baseline_cfg},
         "step": "one full oni-ml day run per step: host columns -> H2D -> featurize -> corpus -> "
-                f"{a.sweeps} Gibbs sweeps -> score -> top-{a.maxresults} -> CSV rows",
+                f"{a.sweeps} Gibbs sweeps -> score -> top-{a.maxresults} -> CSV rows"
+                + ("; each step's H2D upload runs on a copy stream during the previous step" if pf is not None else ""),
         "gibbs_iters_per_sec": round(a.sweeps / train_s, 2) if train_s > 0 else None,
         "ms_per_sweep_in_training": round(train_s / a.sweeps * 1e3, 4) if train_s > 0 else None,
         "tokens_per_sec_training": round(tokens * a.sweeps / train_s, 1) if train_s > 0 else None,

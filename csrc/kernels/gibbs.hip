@@ -175,6 +175,10 @@ __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
   // sampling, so their latency hides behind the math and stores of step s
   uint32_t w_nx = len > 0 ? a.tok_word[off + c] : oni::kPadWord;
   int z_nx = (!INIT && len > 0) ? (int)a.tok_z[off + c] : 0;
+  // MODE 3/4: the token's word-sorted position streams with its word/topic (a load issued only
+  // once the draw is known would expose a full memory latency on almost every step)
+  constexpr bool WPF = !INIT && (MODE == 3 || MODE == 4);
+  int32_t p_nx = (WPF && len > 0) ? a.wpos[off + c] : 0;
   // QPF: the next token's q row is also fetched one step ahead (needs only its word id)
   float qn[KP];
 #pragma unroll
@@ -184,9 +188,11 @@ __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
     const int64_t idx = off + (int64_t)s * S + c;
     const uint32_t w = w_nx;
     const int zo = z_nx;
+    const int32_t pw = p_nx;
     if (s + 1 < len) {
       w_nx = a.tok_word[idx + S];
       if (!INIT) z_nx = a.tok_z[idx + S];
+      if (WPF) p_nx = a.wpos[idx + S];
     }
     if (w == oni::kPadWord) continue;  // uniform across the G lanes of a unit
     const uint32_t pos = pos0 + (uint32_t)s;
@@ -245,8 +251,8 @@ __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
       if (zn != zo && g == 0) {
         ++nchg;
         a.tok_z[idx] = (uint8_t)zn;
-        if constexpr (MODE == 3) a.z_w[a.wpos[idx]] = (uint8_t)zn;
-        if constexpr (MODE == 4) mark_changed_w(a, a.wpos[idx], zo, zn);
+        if constexpr (MODE == 3) a.z_w[pw] = (uint8_t)zn;
+        if constexpr (MODE == 4) mark_changed_w(a, pw, zo, zn);
         if (ATOMIC) {
           atomicAdd(&a.dnwk[(int64_t)w * KS + zo], -1);
           atomicAdd(&a.dnwk[(int64_t)w * KS + zn], 1);

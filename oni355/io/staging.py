@@ -109,3 +109,59 @@ def stats() -> dict:
     out = (C.c_int64 * 2)()
     _lib.check(_lib.lib().oni_stager_stats(_handle, out), "oni_stager_stats")
     return {"bytes": int(out[0]), "chunks": int(out[1])}
+
+
+class Prefetcher:
+    """Double-buffered host → HBM upload of the NEXT day's device columns on a dedicated copy
+    stream, overlapping the current day's compute (SURVEY.md §2.4 P7 stage overlap).
+
+    A loader that owns pinned host buffers (:meth:`pin`, done once per buffer) submits day k+1
+    while day k trains; :meth:`take` makes the compute stream wait for the copies (an event, no
+    host sync) and hands the tensors over. Each submitted day is a full upload; only its timing
+    overlaps. ``copy_ms()`` reports the device time of the last completed upload."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.stream = torch.cuda.Stream(self.device)
+        self._pending = None
+        self._last = None
+
+    @staticmethod
+    def pin(cols: dict, specs: dict) -> dict:
+        """Page-locked host copies of ``cols`` converted to the device dtypes of ``specs``."""
+        out = {}
+        for name, dt in specs.items():
+            a = np.asarray(cols[name])
+            if a.dtype == np.uint32:
+                a = a.view(np.int32)
+            t = torch.from_numpy(np.ascontiguousarray(a)).to(dt)
+            out[name] = t.pin_memory()
+        return out
+
+    def submit(self, pinned: dict) -> None:
+        if self._pending is not None:
+            raise RuntimeError("Prefetcher: take() the pending upload first")
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.stream):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record(self.stream)
+            out = {k: t.to(self.device, non_blocking=True) for k, t in pinned.items()}
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record(self.stream)
+        self._pending = (out, e0, e1)
+
+    def take(self) -> dict:
+        out, e0, e1 = self._pending
+        self._pending = None
+        cur = torch.cuda.current_stream(self.device)
+        cur.wait_event(e1)
+        for t in out.values():
+            t.record_stream(cur)  # allocated on the copy stream, consumed and freed on the compute stream
+        self._last = (e0, e1)
+        return out
+
+    def copy_ms(self) -> float | None:
+        if self._last is None:
+            return None
+        self._last[1].synchronize()
+        return self._last[0].elapsed_time(self._last[1])

@@ -104,11 +104,13 @@ def run_flow(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxre
              alpha: float | None = None, beta: float = 0.01, seed: int = 0x0D15EA5E, chunk_len: int = 0,
              device="cpu", comm: Comm | None = None, feedback: dict | None = None, dupfactor: int = 1000,
              row_offset: int = 0, eval_every: int = 0, burnin: int = 0, ckpt=None, log=None, ldac_dir: str | None = None,
-             ldac_lag: int = 0) -> FlowResult:
-    """Full suspicious-connects for one (rank-local shard of a) day of flows."""
+             ldac_lag: int = 0, device_cols: dict | None = None) -> FlowResult:
+    """Full suspicious-connects for one (rank-local shard of a) day of flows. ``device_cols``:
+    the day's :data:`DEVICE_COLS` already on the device (e.g. from io.staging.Prefetcher, which
+    uploaded them while the previous day computed); ``cols`` still supplies the host rows."""
     timer = StageTimer(device)
     with timer.stage("h2d"):
-        d = to_device(cols, device)
+        d = dict(device_cols) if device_cols is not None else to_device(cols, device)
     with timer.stage("featurize"):
         cuts = compute_cuts(d, comm)
         sw, dw = wordify(d, cuts)
