@@ -9,14 +9,17 @@
 //
 // Supported: classic pcap (µs / ns, either byte order), pcapng (SHB/IDB/EPB/SPB/OPB);
 // link types Ethernet (VLAN/QinQ), raw IPv4/IPv6, Linux cooked (SLL, SLL2), NULL/loopback;
-// IPv4 (non-fragmented) and IPv6 (no extension headers) over UDP with source port 53;
-// DNS header + first question (with name-compression pointers) + A answers.
+// IPv4 (fragmented datagrams reassembled in a serial pass after the parallel decode) and IPv6 (no
+// extension headers); DNS over UDP from port 53 and over TCP from port 53 (every complete
+// length-prefixed message inside a segment); DNS header + first question (with name-compression
+// pointers) + A answers.
 #include <fcntl.h>
 #include <omp.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstring>
 #include <ctime>
 #include <string>
@@ -165,13 +168,73 @@ int read_name(const uint8_t* m, size_t mlen, size_t o, std::string* name) {
   return -1;
 }
 
+struct Frag {
+  uint32_t src, dst, off;
+  uint16_t id;
+  uint8_t proto;
+  bool more;
+  int64_t ts_ns, pkt;
+  uint32_t origlen;
+  std::vector<uint8_t> data;
+};
+
 struct Rows {
   std::vector<int64_t> ts_ns;
   std::vector<int32_t> frame_len, qtype, qclass, rcode;
   std::vector<uint32_t> ip_src, ip_dst;
   std::vector<int64_t> name_end, a_end;  // running offsets into chars
+  std::vector<int64_t> pkt;              // packet index of each row (packet order)
   std::string names, as;
+  std::vector<Frag> frags;               // IPv4 fragments seen by this thread
+  int64_t tcp_partial = 0, frag_incomplete = 0;
 };
+
+// append rows [0, src.size) of `s` to `a` (offsets rebased)
+void append_rows(Rows& a, const Rows& s) {
+  const int64_t nb = (int64_t)a.names.size(), ab = (int64_t)a.as.size();
+  a.ts_ns.insert(a.ts_ns.end(), s.ts_ns.begin(), s.ts_ns.end());
+  a.frame_len.insert(a.frame_len.end(), s.frame_len.begin(), s.frame_len.end());
+  a.ip_src.insert(a.ip_src.end(), s.ip_src.begin(), s.ip_src.end());
+  a.ip_dst.insert(a.ip_dst.end(), s.ip_dst.begin(), s.ip_dst.end());
+  a.qtype.insert(a.qtype.end(), s.qtype.begin(), s.qtype.end());
+  a.qclass.insert(a.qclass.end(), s.qclass.begin(), s.qclass.end());
+  a.rcode.insert(a.rcode.end(), s.rcode.begin(), s.rcode.end());
+  a.pkt.insert(a.pkt.end(), s.pkt.begin(), s.pkt.end());
+  for (auto e : s.name_end) a.name_end.push_back(e + nb);
+  for (auto e : s.a_end) a.a_end.push_back(e + ab);
+  a.names += s.names;
+  a.as += s.as;
+  a.tcp_partial += s.tcp_partial;
+  a.frag_incomplete += s.frag_incomplete;
+}
+
+// rows in packet order (reassembled datagrams were appended after the parallel pass)
+Rows packet_order(const Rows& a) {
+  const size_t n = a.ts_ns.size();
+  std::vector<size_t> o(n);
+  for (size_t i = 0; i < n; ++i) o[i] = i;
+  std::stable_sort(o.begin(), o.end(), [&](size_t x, size_t y) { return a.pkt[x] < a.pkt[y]; });
+  Rows b;
+  b.tcp_partial = a.tcp_partial;
+  b.frag_incomplete = a.frag_incomplete;
+  for (size_t k = 0; k < n; ++k) {
+    const size_t i = o[k];
+    b.ts_ns.push_back(a.ts_ns[i]);
+    b.frame_len.push_back(a.frame_len[i]);
+    b.ip_src.push_back(a.ip_src[i]);
+    b.ip_dst.push_back(a.ip_dst[i]);
+    b.qtype.push_back(a.qtype[i]);
+    b.qclass.push_back(a.qclass[i]);
+    b.rcode.push_back(a.rcode[i]);
+    b.pkt.push_back(a.pkt[i]);
+    const int64_t n0 = i ? a.name_end[i - 1] : 0, a0 = i ? a.a_end[i - 1] : 0;
+    b.names.append(a.names, (size_t)n0, (size_t)(a.name_end[i] - n0));
+    b.as.append(a.as, (size_t)a0, (size_t)(a.a_end[i] - a0));
+    b.name_end.push_back((int64_t)b.names.size());
+    b.a_end.push_back((int64_t)b.as.size());
+  }
+  return b;
+}
 
 uint32_t fold_ipv6(const uint8_t* a) {
   uint32_t h = 2166136261u;
@@ -179,7 +242,84 @@ uint32_t fold_ipv6(const uint8_t* a) {
   return h;
 }
 
-void decode(const uint8_t* base, const Pkt& p, Rows* r) {
+// one DNS message (UDP payload, or one length-prefixed TCP message) → a row (responses only)
+void parse_dns(const uint8_t* m, size_t ml, int64_t ts_ns, uint32_t origlen, uint32_t src, uint32_t dst, int64_t pkt,
+               Rows* r) {
+  if (ml < 12) return;
+  const uint16_t flags = be16(m + 2);
+  if (!(flags & 0x8000)) return;  // responses only
+  const int qd = be16(m + 4), an = be16(m + 6);
+  if (qd < 1) return;
+  std::string name;
+  int c = read_name(m, ml, 12, &name);
+  if (c < 0 || (size_t)(12 + c + 4) > ml) return;
+  size_t pos = 12 + c;
+  const int qtype = be16(m + pos), qclass = be16(m + pos + 2);
+  pos += 4;
+  for (int q = 1; q < qd; ++q) {  // skip further questions
+    std::string tmp;
+    int cc = read_name(m, ml, pos, &tmp);
+    if (cc < 0) return;
+    pos += cc + 4;
+  }
+  std::string answers;
+  for (int a = 0; a < an && pos < ml; ++a) {
+    std::string tmp;
+    int cc = read_name(m, ml, pos, &tmp);
+    if (cc < 0 || pos + cc + 10 > ml) break;
+    pos += cc;
+    const int type = be16(m + pos), rdlen = be16(m + pos + 8);
+    pos += 10;
+    if (pos + rdlen > ml) break;
+    if (type == 1 && rdlen == 4) {
+      char buf[20];
+      std::snprintf(buf, sizeof buf, "%u.%u.%u.%u", m[pos], m[pos + 1], m[pos + 2], m[pos + 3]);
+      if (!answers.empty()) answers.push_back(',');
+      answers += buf;
+    }
+    pos += rdlen;
+  }
+  r->ts_ns.push_back(ts_ns);
+  r->frame_len.push_back((int32_t)origlen);
+  r->ip_src.push_back(src);
+  r->ip_dst.push_back(dst);
+  r->qtype.push_back(qtype);
+  r->qclass.push_back(qclass);
+  r->rcode.push_back(flags & 0x000F);
+  r->names += name;
+  r->name_end.push_back((int64_t)r->names.size());
+  r->as += answers;
+  r->a_end.push_back((int64_t)r->as.size());
+  r->pkt.push_back(pkt);
+}
+
+// transport payload → DNS messages: UDP from port 53 (one message); TCP from port 53 (every
+// complete 2-byte-length-prefixed message inside this segment; messages split across segments
+// would need stream reassembly and are counted in Rows::tcp_partial instead)
+void parse_transport(const uint8_t* t, size_t tl, int proto, int64_t ts_ns, uint32_t origlen, uint32_t src,
+                     uint32_t dst, int64_t pkt, Rows* r) {
+  if (proto == 17) {
+    if (tl < 8 || be16(t) != 53) return;
+    parse_dns(t + 8, tl - 8, ts_ns, origlen, src, dst, pkt, r);
+  } else if (proto == 6) {
+    if (tl < 20 || be16(t) != 53) return;
+    const size_t hl = (size_t)(t[12] >> 4) * 4;
+    if (hl < 20 || hl > tl) return;
+    size_t o = hl;
+    while (o + 2 <= tl) {
+      const size_t len = be16(t + o);
+      if (len == 0) break;
+      if (o + 2 + len > tl) {
+        ++r->tcp_partial;
+        break;
+      }
+      parse_dns(t + o + 2, len, ts_ns, origlen, src, dst, pkt, r);
+      o += 2 + len;
+    }
+  }
+}
+
+void decode(const uint8_t* base, const Pkt& p, int64_t pkt, Rows* r) {
   const uint8_t* d = base + p.off;
   size_t n = p.caplen, o = 0;
   int ethertype = 0;
@@ -213,72 +353,87 @@ void decode(const uint8_t* base, const Pkt& p, Rows* r) {
       ethertype = (d[0] >> 4) == 6 ? 0x86DD : 0x0800;
       o = 0;
   }
-  uint32_t src, dst;
-  size_t udp;
   if (ethertype == 0x0800) {
     if (o + 20 > n) return;
     const int ihl = (d[o] & 0x0F) * 4;
-    if ((d[o] >> 4) != 4 || ihl < 20 || d[o + 9] != 17) return;
-    if ((be16(d + o + 6) & 0x3FFF) != 0) return;  // fragment
-    src = be32(d + o + 12);
-    dst = be32(d + o + 16);
-    udp = o + ihl;
-  } else if (ethertype == 0x86DD) {
-    if (o + 40 > n || d[o + 6] != 17) return;
-    src = fold_ipv6(d + o + 8);
-    dst = fold_ipv6(d + o + 24);
-    udp = o + 40;
-  } else {
-    return;
-  }
-  if (udp + 8 > n || be16(d + udp) != 53) return;
-  const uint8_t* m = d + udp + 8;
-  const size_t ml = n - udp - 8;
-  if (ml < 12) return;
-  const uint16_t flags = be16(m + 2);
-  if (!(flags & 0x8000)) return;  // responses only
-  const int qd = be16(m + 4), an = be16(m + 6);
-  if (qd < 1) return;
-  std::string name;
-  int c = read_name(m, ml, 12, &name);
-  if (c < 0 || 12 + c + 4 > ml) return;
-  size_t pos = 12 + c;
-  const int qtype = be16(m + pos), qclass = be16(m + pos + 2);
-  pos += 4;
-  for (int q = 1; q < qd; ++q) {  // skip further questions
-    std::string tmp;
-    int cc = read_name(m, ml, pos, &tmp);
-    if (cc < 0) return;
-    pos += cc + 4;
-  }
-  std::string answers;
-  for (int a = 0; a < an && pos < ml; ++a) {
-    std::string tmp;
-    int cc = read_name(m, ml, pos, &tmp);
-    if (cc < 0 || pos + cc + 10 > ml) break;
-    pos += cc;
-    const int type = be16(m + pos), rdlen = be16(m + pos + 8);
-    pos += 10;
-    if (pos + rdlen > ml) break;
-    if (type == 1 && rdlen == 4) {
-      char buf[20];
-      std::snprintf(buf, sizeof buf, "%u.%u.%u.%u", m[pos], m[pos + 1], m[pos + 2], m[pos + 3]);
-      if (!answers.empty()) answers.push_back(',');
-      answers += buf;
+    const int proto = d[o + 9];
+    if ((d[o] >> 4) != 4 || ihl < 20 || o + ihl > n || (proto != 17 && proto != 6)) return;
+    const uint32_t src = be32(d + o + 12), dst = be32(d + o + 16);
+    const uint16_t ff = be16(d + o + 6);
+    size_t end = o + be16(d + o + 2);  // IP total length bounds the payload (Ethernet padding)
+    if (end > n || end < o + ihl) end = n;
+    if ((ff & 0x3FFF) != 0) {  // IPv4 fragment: kept for the serial reassembly pass
+      Frag f;
+      f.src = src;
+      f.dst = dst;
+      f.id = be16(d + o + 4);
+      f.proto = (uint8_t)proto;
+      f.off = (uint32_t)(ff & 0x1FFF) * 8u;
+      f.more = (ff & 0x2000) != 0;
+      f.ts_ns = p.ts_ns;
+      f.origlen = p.origlen;
+      f.pkt = pkt;
+      f.data.assign(d + o + ihl, d + end);
+      r->frags.push_back(std::move(f));
+      return;
     }
-    pos += rdlen;
+    parse_transport(d + o + ihl, end - o - ihl, proto, p.ts_ns, p.origlen, src, dst, pkt, r);
+  } else if (ethertype == 0x86DD) {
+    if (o + 40 > n) return;
+    const int nh = d[o + 6];
+    if (nh != 17 && nh != 6) return;
+    parse_transport(d + o + 40, n - o - 40, nh, p.ts_ns, p.origlen, fold_ipv6(d + o + 8), fold_ipv6(d + o + 24), pkt, r);
   }
-  r->ts_ns.push_back(p.ts_ns);
-  r->frame_len.push_back((int32_t)p.origlen);
-  r->ip_src.push_back(src);
-  r->ip_dst.push_back(dst);
-  r->qtype.push_back(qtype);
-  r->qclass.push_back(qclass);
-  r->rcode.push_back(flags & 0x000F);
-  r->names += name;
-  r->name_end.push_back((int64_t)r->names.size());
-  r->as += answers;
-  r->a_end.push_back((int64_t)r->as.size());
+}
+
+// IPv4 fragment reassembly (RFC 791): fragments grouped by (src, dst, id, proto); a datagram is
+// complete when its pieces cover [0, end of the last (MF = 0) fragment) without a hole. The row
+// takes the frame time / length / index of the fragment that completed it (tshark's view).
+void reassemble(std::vector<Frag>& fr, Rows* r) {
+  std::stable_sort(fr.begin(), fr.end(), [](const Frag& a, const Frag& b) {
+    if (a.src != b.src) return a.src < b.src;
+    if (a.dst != b.dst) return a.dst < b.dst;
+    if (a.id != b.id) return a.id < b.id;
+    if (a.proto != b.proto) return a.proto < b.proto;
+    return a.off < b.off;
+  });
+  size_t i = 0;
+  while (i < fr.size()) {
+    size_t j = i;
+    while (j < fr.size() && fr[j].src == fr[i].src && fr[j].dst == fr[i].dst && fr[j].id == fr[i].id &&
+           fr[j].proto == fr[i].proto)
+      ++j;
+    size_t total = 0;
+    bool last = false;
+    const Frag* newest = &fr[i];
+    for (size_t k = i; k < j; ++k) {
+      if (!fr[k].more) {
+        last = true;
+        total = fr[k].off + fr[k].data.size();
+      }
+      if (fr[k].pkt > newest->pkt) newest = &fr[k];
+    }
+    if (last && total <= 65535) {
+      std::vector<uint8_t> buf(total);
+      size_t covered = 0;
+      bool ok = true;
+      for (size_t k = i; k < j && ok; ++k) {  // sorted by offset: require no hole
+        const Frag& f = fr[k];
+        if (f.off > covered) ok = false;
+        const size_t e = f.off + f.data.size();
+        if (ok && e > f.off && f.off < total) std::memcpy(buf.data() + f.off, f.data.data(), std::min(e, total) - f.off);
+        if (e > covered) covered = e;
+      }
+      if (ok && covered >= total)
+        parse_transport(buf.data(), total, fr[i].proto, newest->ts_ns, newest->origlen, fr[i].src, fr[i].dst,
+                        newest->pkt, r);
+      else
+        ++r->frag_incomplete;
+    } else {
+      ++r->frag_incomplete;
+    }
+    i = j;
+  }
 }
 
 struct Handle {
@@ -309,22 +464,23 @@ ONI_NATIVE_API void* oni_pcap_dns_open(const char* path, int threads) {
 #pragma omp parallel for num_threads(T) schedule(static, 1)
     for (int t = 0; t < T; ++t) {
       const size_t lo = pk.size() * (size_t)t / T, hi = pk.size() * (size_t)(t + 1) / T;
-      for (size_t i = lo; i < hi; ++i) decode(b, pk[i], &loc[t]);
+      for (size_t i = lo; i < hi; ++i) decode(b, pk[i], (int64_t)i, &loc[t]);
     }
     Rows& a = h->all;
+    std::vector<Frag> frags;
     for (auto& r : loc) {
-      const int64_t nb = (int64_t)a.names.size(), ab = (int64_t)a.as.size();
-      a.ts_ns.insert(a.ts_ns.end(), r.ts_ns.begin(), r.ts_ns.end());
-      a.frame_len.insert(a.frame_len.end(), r.frame_len.begin(), r.frame_len.end());
-      a.ip_src.insert(a.ip_src.end(), r.ip_src.begin(), r.ip_src.end());
-      a.ip_dst.insert(a.ip_dst.end(), r.ip_dst.begin(), r.ip_dst.end());
-      a.qtype.insert(a.qtype.end(), r.qtype.begin(), r.qtype.end());
-      a.qclass.insert(a.qclass.end(), r.qclass.begin(), r.qclass.end());
-      a.rcode.insert(a.rcode.end(), r.rcode.begin(), r.rcode.end());
-      for (auto e : r.name_end) a.name_end.push_back(e + nb);
-      for (auto e : r.a_end) a.a_end.push_back(e + ab);
-      a.names += r.names;
-      a.as += r.as;
+      append_rows(a, r);
+      for (auto& f : r.frags) frags.push_back(std::move(f));
+    }
+    if (!frags.empty()) {  // serial pass: fragments of one datagram may sit in different chunks
+      Rows re;
+      reassemble(frags, &re);
+      if (!re.ts_ns.empty()) {
+        append_rows(a, re);
+        a = packet_order(a);
+      } else {
+        a.frag_incomplete += re.frag_incomplete;
+      }
     }
   }
   if (b && b != MAP_FAILED) munmap((void*)b, n);
@@ -361,6 +517,14 @@ ONI_NATIVE_API int oni_pcap_dns_fetch(void* hp, int64_t* ts_ns, int32_t* frame_l
   std::memcpy(a_off + 1, a.a_end.data(), n * 8);
   std::memcpy(names, a.names.data(), a.names.size());
   std::memcpy(as, a.as.data(), a.as.size());
+  return 0;
+}
+
+// decoder counters: [0] TCP messages split across segments (skipped), [1] incomplete IPv4 datagrams
+ONI_NATIVE_API int oni_pcap_dns_stats(void* hp, int64_t* out) {
+  auto* h = (Handle*)hp;
+  out[0] = h->all.tcp_partial;
+  out[1] = h->all.frag_incomplete;
   return 0;
 }
 

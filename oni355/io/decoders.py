@@ -25,6 +25,7 @@ native.register("oni_pcap_dns_open", [C.c_char_p, i32], vp)
 native.register("oni_pcap_dns_sizes", [vp, vp, vp, vp, vp], i32)
 native.register("oni_pcap_dns_fetch", [vp] + [vp] * 11, i32)
 native.register("oni_pcap_dns_free", [vp], None)
+native.register("oni_pcap_dns_stats", [vp, vp], i32)
 native.register("oni_pcap_dns_write", [C.c_char_p, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32], i64)
 
 SKIP, I64, F64, IPV4, PROTO, FLAGS, TIME, STR = range(8)
@@ -324,6 +325,8 @@ def read_pcap_dns(path: str, threads: int = 0) -> dict:
         aoff = np.zeros(n + 1, np.int64)
         aa = np.zeros(max(ab.value, 1), np.uint8)
         L.oni_pcap_dns_fetch(h, *(x.ctypes.data for x in (ts, flen, src, dst, qt, qc, rc_, noff, names, aoff, aa)))
+        st = np.zeros(2, np.int64)
+        L.oni_pcap_dns_stats(h, st.ctypes.data)
     finally:
         L.oni_pcap_dns_free(h)
     unix = ts // 1_000_000_000
@@ -339,6 +342,8 @@ def read_pcap_dns(path: str, threads: int = 0) -> dict:
         "dns_qry_rcode": rc_,
         "dns_a": StringColumn(aoff, aa[: ab.value]),
         "_packets": pk.value,
+        "_tcp_partial": int(st[0]),       # DNS-over-TCP messages split across segments (skipped)
+        "_frag_incomplete": int(st[1]),   # IPv4 datagrams with missing fragments (skipped)
     }
 
 

@@ -1,0 +1,72 @@
+"""pcap DNS decoder (csrc/io/pcap_dns.cpp): DNS over TCP (length-prefixed messages inside one
+segment) and IPv4-fragmented UDP responses reassembled across the parallel decode's chunks, rows
+in packet order; split TCP messages and incomplete datagrams are counted, not decoded."""
+import struct
+
+import numpy as np
+import pytest
+
+from oni355.io.decoders import read_pcap_dns
+
+
+def _dns_response(qid: int, name: str, qtype: int = 1, answers=(), pad: int = 0) -> bytes:
+    q = b"".join(bytes([len(l)]) + l.encode() for l in name.split(".")) + b"\0"
+    msg = struct.pack(">HHHHHH", qid, 0x8180, 1, len(answers), 0, 0) + q + struct.pack(">HH", qtype, 1)
+    for ip in answers:
+        msg += b"\xc0\x0c" + struct.pack(">HHIH", 1, 1, 60, 4) + bytes(int(x) for x in ip.split("."))
+    return msg + b"\0" * pad
+
+
+def _ipv4(src, dst, proto, payload, ident=1, frag_off=0, more=False):
+    ff = (0x2000 if more else 0) | (frag_off // 8)
+    hdr = struct.pack(">BBHHHBBH4s4s", 0x45, 0, 20 + len(payload), ident, ff, 64, proto, 0,
+                      bytes(int(x) for x in src.split(".")), bytes(int(x) for x in dst.split(".")))
+    return hdr + payload
+
+
+def _eth(ip: bytes) -> bytes:
+    return b"\x00" * 12 + b"\x08\x00" + ip
+
+
+def _udp(sport, dport, data):
+    return struct.pack(">HHHH", sport, dport, 8 + len(data), 0) + data
+
+
+def _tcp(sport, dport, data):
+    return struct.pack(">HHIIBBHHH", sport, dport, 1, 1, 5 << 4, 0x18, 65535, 0, 0) + data
+
+
+def _write(path, frames):
+    with open(path, "wb") as f:
+        f.write(struct.pack("<IHHiIII", 0xa1b2c3d4, 2, 4, 0, 0, 65535, 1))
+        for i, fr in enumerate(frames):
+            f.write(struct.pack("<IIII", 1467936000 + i, 0, len(fr), len(fr)))
+            f.write(fr)
+
+
+def test_tcp_messages_and_fragment_reassembly(tmp_path):
+    srv, cli = "10.0.0.53", "10.1.2.3"
+    big = _udp(53, 5555, _dns_response(7, "big.example.com", answers=["1.2.3.4"], pad=900))
+    f1, f2, f3 = big[:400], big[400:800], big[800:]
+    frames = [
+        _eth(_ipv4(srv, cli, 17, _udp(53, 4000, _dns_response(1, "a.example.com", answers=["9.9.9.9"])))),   # 0
+        _eth(_ipv4(srv, cli, 6, _tcp(53, 4001, b"".join(struct.pack(">H", len(m)) + m for m in (
+            _dns_response(2, "t1.example.org", qtype=16), _dns_response(3, "t2.example.org")))))),      # 1: 2 msgs
+        _eth(_ipv4(srv, cli, 17, f3, ident=77, frag_off=800)),                                          # 2 (last)
+        _eth(_ipv4(srv, cli, 17, f1, ident=77, frag_off=0, more=True)),                                 # 3
+        _eth(_ipv4(srv, cli, 6, _tcp(53, 4002, struct.pack(">H", 300) + b"\x00" * 40))),                # 4 partial
+        _eth(_ipv4(srv, cli, 17, f2, ident=77, frag_off=400, more=True)),                               # 5 completes
+        _eth(_ipv4(srv, cli, 17, big[:400], ident=99, frag_off=0, more=True)),                          # 6 no tail
+        _eth(_ipv4(srv, cli, 17, _udp(53, 4003, _dns_response(4, "z.example.net"))))                     # 7
+    ]
+    p = str(tmp_path / "x.pcap")
+    _write(p, frames)
+    for threads in (1, 3):
+        c = read_pcap_dns(p, threads=threads)
+        names = c["dns_qry_name"].to_list()
+        assert names == ["a.example.com", "t1.example.org", "t2.example.org", "big.example.com", "z.example.net"]
+        assert c["dns_qry_type"].tolist() == [1, 16, 1, 1, 1]
+        assert c["dns_a"].to_list()[3] == "1.2.3.4"
+        # the reassembled datagram carries the frame that completed it (packet 5)
+        assert c["unix_tstamp"].tolist() == [1467936000, 1467936001, 1467936001, 1467936005, 1467936007]
+        assert c["_tcp_partial"] == 1 and c["_frag_incomplete"] == 1
