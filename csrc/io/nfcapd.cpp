@@ -221,6 +221,7 @@ bool lz4_decompress(const uint8_t* in, size_t in_len, std::vector<uint8_t>* out)
 struct Flow {
   int64_t first_ms, last_ms, received_ms;
   uint32_t sip, dip, rip;
+  uint8_t v6, a6[32];  // IPv6 record: source (16 B) + destination (16 B) address, sip/dip = 0
   int32_t sport, dport, proto, flags, fwd, stos, dtos, dir, input, output, sas, das;
   int64_t ipkt, ibyt, opkt, obyt;
 };
@@ -230,12 +231,6 @@ struct Handle {
   std::string err;
   int64_t blocks = 0, skipped_records = 0;
 };
-
-inline uint32_t fold16(const uint8_t* a) {
-  uint32_t h = 2166136261u;
-  for (int i = 0; i < 16; ++i) h = (h ^ a[i]) * 16777619u;
-  return h;
-}
 
 void decode_block(const uint8_t* b, size_t n, std::vector<std::vector<uint16_t>>* maps, Handle* h) {
   size_t pos = 0;
@@ -280,10 +275,11 @@ void decode_block(const uint8_t* b, size_t n, std::vector<std::vector<uint16_t>>
       f.first_ms = (int64_t)first * 1000 + msf;
       f.last_ms = (int64_t)last * 1000 + msl;
       size_t o = 32;
-      if (flags & 1) {
+      if (flags & 1) {  // IPv6: carried verbatim (the pipeline keys v6 documents exactly)
         if (o + 32 > size) goto skip;
-        f.sip = fold16(r + o);
-        f.dip = fold16(r + o + 16);
+        f.v6 = 1;
+        std::memcpy(f.a6, r + o, 32);
+        f.sip = f.dip = 0;
         o += 32;
       } else {
         if (o + 8 > size) goto skip;
@@ -466,6 +462,18 @@ ONI_NATIVE_API int oni_nfcapd_fetch(void* hp, int64_t* out_i64, int32_t* out_i32
   return 0;
 }
 
+// IPv6 records: is_v6[n] (1 for IPv6 flows) and addrs[n][32] (source 16 B | destination 16 B)
+ONI_NATIVE_API int oni_nfcapd_fetch_v6(void* hp, uint8_t* is_v6, uint8_t* addrs) {
+  auto* h = (Handle*)hp;
+  for (size_t i = 0; i < h->flows.size(); ++i) {
+    const Flow& f = h->flows[i];
+    is_v6[i] = f.v6;
+    if (f.v6) std::memcpy(addrs + i * 32, f.a6, 32);
+    else std::memset(addrs + i * 32, 0, 32);
+  }
+  return 0;
+}
+
 ONI_NATIVE_API void oni_nfcapd_free(void* hp) { delete (Handle*)hp; }
 
 ONI_NATIVE_API int oni_lzo1x_decompress(const uint8_t* in, int64_t n, uint8_t* out, int64_t cap, int64_t* out_len) {
@@ -495,7 +503,8 @@ ONI_NATIVE_API int64_t oni_nfcapd_write(const char* path, int64_t n, const int64
                                         const int32_t* tflags, const int64_t* ipkt, const int64_t* ibyt,
                                         const int64_t* opkt, const int64_t* obyt, const int32_t* input,
                                         const int32_t* output, const int32_t* sas, const int32_t* das,
-                                        const uint32_t* rip, int compression, int per_block) {
+                                        const uint32_t* rip, const uint8_t* is_v6, const uint8_t* addrs6,
+                                        int compression, int per_block) {
   FILE* f = std::fopen(path, "wb");
   if (!f) return -1;
   std::vector<uint8_t> hdr(140 + 160, 0);
@@ -586,10 +595,11 @@ ONI_NATIVE_API int64_t oni_nfcapd_write(const char* path, int64_t n, const int64
   std::vector<uint8_t> raw;
   uint32_t nrec = 0;
   for (int64_t i = 0; i < n; ++i) {
-    const uint16_t type = 10, size = 32 + 8 + 8 + 8 + 4 + 4 + 4 + 8 + 8 + 4 + 8;
-    uint8_t r[size];
+    const bool v6 = is_v6 && addrs6 && is_v6[i];
+    const uint16_t type = 10, size = (uint16_t)(32 + (v6 ? 32 : 8) + 8 + 8 + 4 + 4 + 4 + 8 + 8 + 4 + 8);
+    uint8_t r[32 + 32 + 8 + 8 + 4 + 4 + 4 + 8 + 8 + 4 + 8];
     std::memset(r, 0, size);
-    const uint16_t fl = 2 | 4, ext = 0, msf = (uint16_t)(first_ms[i] % 1000), msl = (uint16_t)(last_ms[i] % 1000);
+    const uint16_t fl = (uint16_t)(2 | 4 | (v6 ? 1 : 0)), ext = 0, msf = (uint16_t)(first_ms[i] % 1000), msl = (uint16_t)(last_ms[i] % 1000);
     const uint32_t first = (uint32_t)(first_ms[i] / 1000), last = (uint32_t)(last_ms[i] / 1000);
     std::memcpy(r, &type, 2);
     std::memcpy(r + 2, &size, 2);
@@ -605,9 +615,14 @@ ONI_NATIVE_API int64_t oni_nfcapd_write(const char* path, int64_t n, const int64
     std::memcpy(r + 24, &sp, 2);
     std::memcpy(r + 26, &dp, 2);
     size_t o = 32;
-    std::memcpy(r + o, &sip[i], 4);
-    std::memcpy(r + o + 4, &dip[i], 4);
-    o += 8;
+    if (v6) {
+      std::memcpy(r + o, addrs6 + i * 32, 32);
+      o += 32;
+    } else {
+      std::memcpy(r + o, &sip[i], 4);
+      std::memcpy(r + o + 4, &dip[i], 4);
+      o += 8;
+    }
     const uint64_t pk = (uint64_t)ipkt[i], by = (uint64_t)ibyt[i];
     std::memcpy(r + o, &pk, 8);
     std::memcpy(r + o + 8, &by, 8);

@@ -17,6 +17,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <arpa/inet.h>
+
 #include <ctime>
 #include <string>
 #include <vector>
@@ -27,6 +29,7 @@ extern "C" {
 void* oni_nfcapd_open(const char* path);
 int oni_nfcapd_info(void* hp, int64_t* n_flows, int64_t* blocks, int64_t* skipped, char* err, int err_len);
 int oni_nfcapd_fetch(void* hp, int64_t* out_i64, int32_t* out_i32, uint32_t* out_rip);
+int oni_nfcapd_fetch_v6(void* hp, uint8_t* is_v6, uint8_t* addrs);
 void oni_nfcapd_free(void* hp);
 }
 
@@ -132,7 +135,9 @@ int main(int argc, char** argv) {
       std::vector<int64_t> a64((size_t)n * 8);
       std::vector<int32_t> a32((size_t)n * 14);
       std::vector<uint32_t> rip((size_t)n);
+      std::vector<uint8_t> v6((size_t)n), a6((size_t)n * 32);
       oni_nfcapd_fetch(h, a64.data(), a32.data(), rip.data());
+      oni_nfcapd_fetch_v6(h, v6.data(), a6.data());
       oni_nfcapd_free(h);
       char fl[8], td[32];
       for (int64_t i = 0; i < n; ++i) {
@@ -153,7 +158,14 @@ int main(int argc, char** argv) {
         } else {
           o.time(first_s); o.c(); o.time(x[1] / 1000); o.c(); o.str(td); o.c();
         }
-        o.ip((uint32_t)y[12]); o.c(); o.ip((uint32_t)y[13]); o.c();
+        if (v6[(size_t)i]) {  // IPv6 flow: RFC 5952 text of both addresses
+          char a[INET6_ADDRSTRLEN], b[INET6_ADDRSTRLEN];
+          inet_ntop(AF_INET6, &a6[(size_t)i * 32], a, sizeof a);
+          inet_ntop(AF_INET6, &a6[(size_t)i * 32 + 16], b, sizeof b);
+          o.str(a); o.c(); o.str(b); o.c();
+        } else {
+          o.ip((uint32_t)y[12]); o.c(); o.ip((uint32_t)y[13]); o.c();
+        }
         o.i64(y[0]); o.c(); o.i64(y[1]); o.c();
         if (pn) o.str(pn); else o.i64(y[2]);
         o.c(); o.str(fl); o.c();

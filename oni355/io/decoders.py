@@ -28,23 +28,61 @@ native.register("oni_pcap_dns_free", [vp], None)
 native.register("oni_pcap_dns_stats", [vp, vp], i32)
 native.register("oni_pcap_dns_write", [C.c_char_p, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32], i64)
 
+native.register("oni_ip_parse_spans", [vp, vp, i64, vp, vp, vp], i64)
+native.register("oni_ipv6_text", [vp, i64, vp, i64, vp, vp], i32)
+
 SKIP, I64, F64, IPV4, PROTO, FLAGS, TIME, STR = range(8)
+IPANY = -1  # Python-side kind: parsed as text spans, then IPv4 -> u32 column, IPv6 -> "<col>6" text column
+
+
+def ipv6_text(addrs: np.ndarray, is_v6: np.ndarray, stride: int = 16) -> StringColumn:
+    """RFC 5952 text of the 16-byte addresses of the IPv6 rows (empty strings elsewhere)."""
+    a = np.ascontiguousarray(addrs, dtype=np.uint8)
+    f = np.ascontiguousarray(is_v6, dtype=np.uint8)
+    n = f.size
+    off = np.zeros(n + 1, np.int64)
+    L = native.lib()
+    if L.oni_ipv6_text(a.ctypes.data, stride, f.ctypes.data, n, off.ctypes.data, None):
+        raise ValueError("bad IPv6 address")
+    buf = np.zeros(max(int(off[-1]), 1), np.uint8)
+    L.oni_ipv6_text(a.ctypes.data, stride, f.ctypes.data, n, off.ctypes.data, buf.ctypes.data)
+    return StringColumn(off, buf[: off[-1]])
+
+
+def parse_ip_spans(buf: np.ndarray, spans: np.ndarray):
+    """(u32 IPv4 [n], IPv6 16-byte rows [n,16], kind [n]: 0 v4, 1 v6, 2 unparsable) of text spans."""
+    sp = np.ascontiguousarray(spans, dtype=np.int64).reshape(-1, 2)
+    n = sp.shape[0]
+    b = np.ascontiguousarray(buf, dtype=np.uint8) if len(buf) else np.zeros(1, np.uint8)
+    v4 = np.zeros(n, np.uint32)
+    v6 = np.zeros((n, 16), np.uint8)
+    kind = np.zeros(n, np.uint8)
+    native.lib().oni_ip_parse_spans(b.ctypes.data, sp.ctypes.data, n, v4.ctypes.data, v6.ctypes.data,
+                                    kind.ctypes.data)
+    return v4, v6, kind
+
+
+def attach_ipv6(cols: dict, name: str, v6: np.ndarray, kind: np.ndarray) -> None:
+    """Add the ``<name>6`` text column when any row is IPv6 (sip6 / dip6)."""
+    if np.any(kind == 1):
+        cols[name + "6"] = ipv6_text(v6, (kind == 1).astype(np.uint8))
 
 # ONI flow CSV (oni-nfdump output order == Hive flow schema minus unix_tstamp)
 _ONI_FLOW_FIELDS = [
     ("treceived", TIME), ("tryear", I64), ("trmonth", I64), ("trday", I64), ("trhour", I64), ("trminute", I64),
-    ("trsec", I64), ("tdur", F64), ("sip", IPV4), ("dip", IPV4), ("sport", I64), ("dport", I64), ("proto", PROTO),
+    ("trsec", I64), ("tdur", F64), ("sip", IPANY), ("dip", IPANY), ("sport", I64), ("dport", I64), ("proto", PROTO),
     ("flag", FLAGS), ("fwd", I64), ("stos", I64), ("ipkt", I64), ("ibyt", I64), ("opkt", I64), ("obyt", I64),
     ("input", I64), ("output", I64), ("sas", I64), ("das", I64), ("dtos", I64), ("dir", I64), ("rip", IPV4),
 ]
 # stock nfdump -o csv header names -> (our column, kind)
 _NFDUMP_MAP = {
-    "ts": ("treceived", TIME), "td": ("tdur", F64), "sa": ("sip", IPV4), "da": ("dip", IPV4), "sp": ("sport", I64),
+    "ts": ("treceived", TIME), "td": ("tdur", F64), "sa": ("sip", IPANY), "da": ("dip", IPANY), "sp": ("sport", I64),
     "dp": ("dport", I64), "pr": ("proto", PROTO), "flg": ("flag", FLAGS), "fwd": ("fwd", I64), "stos": ("stos", I64),
     "ipkt": ("ipkt", I64), "ibyt": ("ibyt", I64), "opkt": ("opkt", I64), "obyt": ("obyt", I64), "in": ("input", I64),
     "out": ("output", I64), "sas": ("sas", I64), "das": ("das", I64), "dtos": ("dtos", I64), "dir": ("dir", I64),
     "ra": ("rip", IPV4),
 }
+FLOW_V6_COLUMNS = ("sip6", "dip6")
 _INT32_COLS = {"tryear", "trmonth", "trday", "trhour", "trminute", "trsec", "sport", "dport", "proto", "flag", "fwd",
                "stos", "input", "output", "sas", "das", "dtos", "dir"}
 
@@ -88,7 +126,21 @@ def read_flow_csv(path: str, threads: int = 0) -> tuple[dict, int]:
         fields = list(_ONI_FLOW_FIELDS)
     else:
         fields = list(_ONI_FLOW_FIELDS)
-    cols, bad = _parse(path, fields, has_header, threads=threads)
+    anyip = [name for name, k in fields if k == IPANY]
+    cols, bad = _parse(path, [(nm, STR if k == IPANY else k) for nm, k in fields], has_header, threads=threads)
+    if anyip:
+        buf = np.memmap(path, dtype=np.uint8, mode="r") if os.path.getsize(path) else np.zeros(0, np.uint8)
+        keep = None
+        for name in anyip:
+            v4, v6, kind = parse_ip_spans(buf, cols[name])
+            cols[name] = v4
+            attach_ipv6(cols, name, v6, kind)
+            ok = kind != 2
+            keep = ok if keep is None else keep & ok
+        if keep is not None and not keep.all():  # unparsable address text: a bad row, as before
+            bad += int((~keep).sum())
+            idx = np.nonzero(keep)[0]
+            cols = {k: (v.take(idx) if hasattr(v, "offsets") else v[idx]) for k, v in cols.items()}
     return finish_flow_cols(cols), bad
 
 
@@ -97,13 +149,13 @@ def finish_flow_cols(cols: dict) -> dict:
     t = cols.get("treceived", np.zeros(n, np.int64))
     cols["unix_tstamp"] = t.copy()
     if "trhour" not in cols:
-        dt = t.astype("datetime64[s]")
+        dt = np.asarray(t, np.int64).astype("datetime64[s]")
         days = dt.astype("datetime64[D]")
         secs = (dt - days).astype(np.int64)
-        ymd = days.astype(object)
-        cols["tryear"] = np.array([d.year for d in ymd], np.int32) if n else np.zeros(0, np.int32)
-        cols["trmonth"] = np.array([d.month for d in ymd], np.int32) if n else np.zeros(0, np.int32)
-        cols["trday"] = np.array([d.day for d in ymd], np.int32) if n else np.zeros(0, np.int32)
+        ym = days.astype("datetime64[M]")
+        cols["tryear"] = (ym.astype(np.int64) // 12 + 1970).astype(np.int32)
+        cols["trmonth"] = (ym.astype(np.int64) % 12 + 1).astype(np.int32)
+        cols["trday"] = ((days - ym.astype("datetime64[D]")).astype(np.int64) + 1).astype(np.int32)
         cols["trhour"] = (secs // 3600).astype(np.int32)
         cols["trminute"] = (secs // 60 % 60).astype(np.int32)
         cols["trsec"] = (secs % 60).astype(np.int32)
@@ -120,6 +172,9 @@ def finish_flow_cols(cols: dict) -> dict:
         elif c == "tdur":
             v = v.astype(np.float32)
         out[c] = v
+    for c in FLOW_V6_COLUMNS:  # IPv6 endpoints (text), present only when the input had any
+        if c in cols:
+            out[c] = cols[c]
     return out
 
 
@@ -136,8 +191,9 @@ def write_flow_csv(path: str, cols: dict, header: bool = True) -> None:
                 v = cols[c][i]
                 if k == TIME:
                     row.append(_dt.datetime.fromtimestamp(int(v), tz=_dt.timezone.utc).strftime("%Y-%m-%d %H:%M:%S"))
-                elif k == IPV4:
-                    row.append(ip_str(v))
+                elif k in (IPV4, IPANY):
+                    t6 = cols[c + "6"][i] if k == IPANY and (c + "6") in cols else ""
+                    row.append(t6 or ip_str(v))
                 elif k == F64:
                     row.append(f"{float(v):.3f}")
                 else:

@@ -6,14 +6,15 @@ import ctypes as C
 import numpy as np
 
 from ..ops import native
-from .decoders import finish_flow_cols
+from .decoders import finish_flow_cols, ipv6_text, parse_ip_spans
 
 vp, i64 = C.c_void_p, C.c_int64
 native.register("oni_nfcapd_open", [C.c_char_p], vp)
 native.register("oni_nfcapd_info", [vp, vp, vp, vp, C.c_char_p, C.c_int], C.c_int)
 native.register("oni_nfcapd_fetch", [vp, vp, vp, vp], C.c_int)
+native.register("oni_nfcapd_fetch_v6", [vp, vp, vp], C.c_int)
 native.register("oni_nfcapd_free", [vp], None)
-native.register("oni_nfcapd_write", [C.c_char_p, i64] + [vp] * 18 + [C.c_int, C.c_int], i64)
+native.register("oni_nfcapd_write", [C.c_char_p, i64] + [vp] * 20 + [C.c_int, C.c_int], i64)
 native.register("oni_lzo1x_decompress", [vp, i64, vp, i64, vp], C.c_int)
 native.register("oni_lz4_decompress", [vp, i64, vp, i64, vp], C.c_int)
 
@@ -31,6 +32,9 @@ def read_nfcapd(path: str) -> dict:
         a32 = np.zeros((m, 14), np.int32)
         rip = np.zeros(m, np.uint32)
         L.oni_nfcapd_fetch(h, a64.ctypes.data, a32.ctypes.data, rip.ctypes.data)
+        is6 = np.zeros(m, np.uint8)
+        a6 = np.zeros((m, 32), np.uint8)
+        L.oni_nfcapd_fetch_v6(h, is6.ctypes.data, a6.ctypes.data)
     finally:
         L.oni_nfcapd_free(h)
     first_s = a64[:, 0] // 1000
@@ -41,7 +45,11 @@ def read_nfcapd(path: str) -> dict:
         "sas": a32[:, 10], "das": a32[:, 11], "sip": a32[:, 12].view(np.uint32), "dip": a32[:, 13].view(np.uint32),
         "ipkt": a64[:, 3], "ibyt": a64[:, 4], "opkt": a64[:, 5], "obyt": a64[:, 6], "rip": rip,
     }
-    return finish_flow_cols({k: np.ascontiguousarray(v) for k, v in cols.items()})
+    cols = {k: np.ascontiguousarray(v) for k, v in cols.items()}
+    if is6.any():  # IPv6 flows: addresses as text columns (sip/dip stay 0 until the pipeline keys them)
+        cols["sip6"] = ipv6_text(np.ascontiguousarray(a6[:, :16]), is6)
+        cols["dip6"] = ipv6_text(np.ascontiguousarray(a6[:, 16:]), is6)
+    return finish_flow_cols(cols)
 
 
 def write_nfcapd(path: str, cols: dict, compression: str = "none", per_block: int = 4096) -> int:
@@ -58,8 +66,17 @@ def write_nfcapd(path: str, cols: dict, compression: str = "none", per_block: in
             np.asarray(cols.get("sas", z32), np.int32), np.asarray(cols.get("das", z32), np.int32),
             np.asarray(cols.get("rip", np.zeros(n)), np.uint32)]
     arrs = [np.ascontiguousarray(a) for a in arrs]
+    is6, a6 = None, None
+    if "sip6" in cols and "dip6" in cols:
+        s6, d6 = cols["sip6"], cols["dip6"]
+        _, sb, sk = parse_ip_spans(s6.chars, np.stack([s6.offsets[:-1], s6.offsets[1:]], 1))
+        _, db, dk = parse_ip_spans(d6.chars, np.stack([d6.offsets[:-1], d6.offsets[1:]], 1))
+        is6 = np.ascontiguousarray(((sk == 1) & (dk == 1)).astype(np.uint8))
+        a6 = np.ascontiguousarray(np.concatenate([sb, db], 1))
     comp = {"none": 0, "lzo": 1, "lz4": 2, "bz2": 3}[compression]
-    r = native.lib().oni_nfcapd_write(path.encode(), n, *(a.ctypes.data for a in arrs), comp, per_block)
+    r = native.lib().oni_nfcapd_write(path.encode(), n, *(a.ctypes.data for a in arrs),
+                                      is6.ctypes.data if is6 is not None else None,
+                                      a6.ctypes.data if a6 is not None else None, comp, per_block)
     if r != n:
         raise OSError(f"nfcapd write failed: {path}")
     return r

@@ -156,9 +156,18 @@ def _col_field(c: str, v, rows: np.ndarray, ip_cols=(), time_cols=(), float_cols
     return K_INT, a
 
 
+def _ip_text_field(cols: dict, c: str, rows: np.ndarray):
+    """sip / dip of result rows as text when the day has IPv6 flows: the IPv6 address where the
+    row has one, dotted IPv4 otherwise (only the few result rows are formatted here)."""
+    v6 = cols[c + "6"].take(rows).to_list()
+    v4 = np.asarray(cols[c])[rows]
+    return K_STR, StringColumn.from_list([t if t else ip_str(x) for t, x in zip(v6, v4)])
+
+
 def format_flow(cols: dict, local_rows, src_words, dst_words, src_scores, dst_scores, scores) -> Rendered:
     rows = np.asarray(local_rows, dtype=np.int64)
-    f = [_col_field(c, cols[c], rows, schema.FLOW_IP_COLUMNS, schema.FLOW_TIME_COLUMNS, schema.FLOW_FLOAT_COLUMNS)
+    f = [_ip_text_field(cols, c, rows) if (c + "6") in cols else
+         _col_field(c, cols[c], rows, schema.FLOW_IP_COLUMNS, schema.FLOW_TIME_COLUMNS, schema.FLOW_FLOAT_COLUMNS)
          for c in schema.FLOW_COLUMNS]
     f += [(K_FLOWWORD, np.asarray(src_words).astype(np.uint32)), (K_FLOWWORD, np.asarray(dst_words).astype(np.uint32)),
           (K_SCORE, src_scores), (K_SCORE, dst_scores), (K_SCORE, scores)]

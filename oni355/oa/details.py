@@ -23,48 +23,72 @@ def _ip(s) -> int:
     return (a << 24) | (b << 16) | (c << 8) | d
 
 
+def _is_v6(ip) -> bool:
+    return isinstance(ip, str) and ":" in ip
+
+
+def ip_mask(cols: dict, col: str, ip) -> np.ndarray:
+    """Rows whose ``col`` endpoint is ``ip`` (IPv6 text matches the ``<col>6`` text column)."""
+    if _is_v6(ip):
+        c6 = cols.get(col + "6")
+        return str_eq_mask(c6, ip) if c6 is not None else np.zeros(len(cols[col]), bool)
+    m = np.asarray(cols[col], np.uint32) == _ip(ip)
+    if col + "6" in cols:
+        m &= np.diff(cols[col + "6"].offsets) == 0  # an IPv6 row's u32 column is 0, not an address
+    return m
+
+
+def _ip_texts(cols: dict, col: str, idx: np.ndarray) -> list[str]:
+    v4 = [ip_str(x) for x in np.asarray(cols[col])[idx]]
+    if col + "6" not in cols:
+        return v4
+    return [t or a for t, a in zip(cols[col + "6"].take(idx).to_list(), v4)]
+
+
 def edge_details(cols: dict, src_ip, dst_ip, hour: int | None = None, limit: int = 1000) -> list[dict]:
-    """All flows between two hosts (either direction), optionally within one hour."""
-    s, d = _ip(src_ip), _ip(dst_ip)
-    sip, dip = np.asarray(cols["sip"], np.uint32), np.asarray(cols["dip"], np.uint32)
-    m = ((sip == s) & (dip == d)) | ((sip == d) & (dip == s))
+    """All flows between two hosts (either direction, IPv4 or IPv6), optionally within one hour."""
+    m = ((ip_mask(cols, "sip", src_ip) & ip_mask(cols, "dip", dst_ip))
+         | (ip_mask(cols, "sip", dst_ip) & ip_mask(cols, "dip", src_ip)))
     if hour is not None:
         m &= np.asarray(cols["trhour"]) == hour
     idx = np.nonzero(m)[0][:limit]
     keys = ["unix_tstamp", "sip", "dip", "sport", "dport", "proto", "ipkt", "ibyt", "opkt", "obyt", "tdur"]
+    txt = {c: _ip_texts(cols, c, idx) for c in ("sip", "dip")}
     out = []
-    for i in idx:
-        rec = {k: (ip_str(cols[k][i]) if k in ("sip", "dip") else cols[k][i].item()) for k in keys if k in cols}
+    for j, i in enumerate(idx):
+        rec = {k: (txt[k][j] if k in ("sip", "dip") else cols[k][i].item()) for k in keys if k in cols}
         out.append(rec)
     return out
 
 
 def chord(cols: dict, ip, top: int = 50) -> list[tuple[str, str, int, int]]:
     """Bytes/packets exchanged between ``ip`` and each peer (the chord-diagram query)."""
-    x = _ip(ip)
-    sip, dip = np.asarray(cols["sip"], np.uint32), np.asarray(cols["dip"], np.uint32)
-    m = (sip == x) | (dip == x)
-    peer = np.where(sip[m] == x, dip[m], sip[m])
-    byt = np.asarray(cols["ibyt"], np.int64)[m]
-    pkt = np.asarray(cols["ipkt"], np.int64)[m]
-    if peer.size == 0:
+    ms, md = ip_mask(cols, "sip", ip), ip_mask(cols, "dip", ip)
+    m = ms | md
+    idx = np.nonzero(m)[0]
+    if idx.size == 0:
         return []
-    up, inv = np.unique(peer, return_inverse=True)
+    s_txt, d_txt = _ip_texts(cols, "sip", idx), _ip_texts(cols, "dip", idx)
+    peer = np.array([d if a else s for a, s, d in zip(ms[idx], s_txt, d_txt)], dtype=object)
+    byt = np.asarray(cols["ibyt"], np.int64)[idx]
+    pkt = np.asarray(cols["ipkt"], np.int64)[idx]
+    up, inv = np.unique(peer.astype(str), return_inverse=True)
     b = np.bincount(inv, weights=byt).astype(np.int64)
     p = np.bincount(inv, weights=pkt).astype(np.int64)
     order = np.argsort(-b, kind="stable")[:top]
-    return [(ip_str(x), ip_str(up[i]), int(b[i]), int(p[i])) for i in order]
+    me = ip if _is_v6(ip) else ip_str(_ip(ip))
+    return [(me, str(up[i]), int(b[i]), int(p[i])) for i in order]
 
 
 def timeline(cols: dict, ip, bucket_s: int = 3600) -> list[tuple[int, int]]:
     """Events per time bucket for one IP (flow: either endpoint; dns: client; proxy: client)."""
-    x = _ip(ip)
     if "sip" in cols:
-        m = (np.asarray(cols["sip"], np.uint32) == x) | (np.asarray(cols["dip"], np.uint32) == x)
+        m = ip_mask(cols, "sip", ip) | ip_mask(cols, "dip", ip)
     elif "ip_dst" in cols:
+        x = _ip(ip)
         m = np.asarray(cols["ip_dst"], np.uint32) == x
     else:
-        m = np.asarray(cols["clientip"], np.uint32) == x
+        m = np.asarray(cols["clientip"], np.uint32) == _ip(ip)
     if "unix_tstamp" in cols:
         t = np.asarray(cols["unix_tstamp"], np.int64)[m] // bucket_s * bucket_s
     else:  # proxy logs carry p_date/p_time only: hour-of-day buckets (seconds into the day)
@@ -183,6 +207,7 @@ EDGE_HEADERS = {
 
 
 def _safe(s: str) -> str:
+    """File-name form of an IP / name (IPv6 ':' would read as a URL scheme in the pages' links)."""
     return "".join(c if c.isalnum() or c in ".-_" else "_" for c in s)[:120]
 
 
@@ -202,13 +227,13 @@ def write_details(source: str, results_csv: str, cols: dict, out_dir: str, limit
     def per_ip(ip: str) -> None:
         if ip in index["ips"]:
             return
-        ent = {"timeline": os.path.basename(write_tsv(os.path.join(out_dir, f"timeline-{ip}.tsv"),
+        ent = {"page": f"threat-{_safe(ip)}.html", "timeline": os.path.basename(write_tsv(os.path.join(out_dir, f"timeline-{_safe(ip)}.tsv"),
                                                       ["bucket_start", "events"], timeline(cols, ip)))}
         if source == "flow":
-            ent["chord"] = os.path.basename(write_tsv(os.path.join(out_dir, f"chord-{ip}.tsv"),
+            ent["chord"] = os.path.basename(write_tsv(os.path.join(out_dir, f"chord-{_safe(ip)}.tsv"),
                                                       ["ip", "peer", "bytes", "packets"], chord(cols, ip)))
         elif source == "dns":
-            ent["dendro"] = os.path.basename(write_tsv(os.path.join(out_dir, f"dendro-{ip}.tsv"),
+            ent["dendro"] = os.path.basename(write_tsv(os.path.join(out_dir, f"dendro-{_safe(ip)}.tsv"),
                                                        ["domain", "subdomain", "queries"], dns_dendro(cols, ip)))
         index["ips"][ip] = ent
 
@@ -216,7 +241,7 @@ def write_details(source: str, results_csv: str, cols: dict, out_dir: str, limit
         if source == "flow":
             sip, dip, hh = r[ix["sip"]], r[ix["dip"]], int(r[ix["trhour"]])
             e = edge_details(cols, sip, dip, hour=hh)
-            f = write_tsv(os.path.join(out_dir, f"edge-{sip}-{dip}-{hh:02d}.tsv"), EDGE_HEADERS["flow"], e)
+            f = write_tsv(os.path.join(out_dir, f"edge-{_safe(sip)}-{_safe(dip)}-{hh:02d}.tsv"), EDGE_HEADERS["flow"], e)
             ip, peer = sip, dip
             per_ip(sip)
             per_ip(dip)

@@ -48,7 +48,12 @@ def load_feedback(path: str, source: str, sev: int = schema.SEV_LOW) -> dict | N
 
     if source == "flow":
         ts = [_dt.datetime.strptime(t.strip()[:19], "%Y-%m-%d %H:%M:%S") for t in col("tstart", "1970-01-01 00:00:00")]
-        return {
+        v6 = {}
+        for c, name in (("srcIP", "sip6"), ("dstIP", "dip6")):
+            txt = [x.strip() if ":" in x else "" for x in col(c)]
+            if any(txt):  # IPv6 endpoints: keyed by the pipeline's day dictionary (flow.with_ipv6_keys)
+                v6[name] = StringColumn.from_list(txt)
+        return {**v6,
             "trhour": np.array([t.hour for t in ts], np.int32), "trminute": np.array([t.minute for t in ts], np.int32),
             "trsec": np.array([t.second for t in ts], np.int32),
             "sip": np.array([_ip(x) for x in col("srcIP")], np.uint32),

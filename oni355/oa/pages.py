@@ -125,7 +125,8 @@ def render_all(source: str, date: str, day_dir: str, out_dir: str | None = None,
             r = list(csv.reader(f))
         header, rows = (r[0], r[1:]) if r else ([], [])
     ipcols = [header.index(c) for c in ("srcIP", "dstIP", "ip_dst", "clientip") if c in header]
-    links = {j: (lambda row, j=j: f"threat-{row[j]}.html" if row[j] in ips else None) for j in ipcols}
+    links = {j: (lambda row, j=j: ips[row[j]].get("page", f"threat-{row[j]}.html") if row[j] in ips else None)
+             for j in ipcols}
     body = _table(header, rows, limit, row_style=lambda row: SEV_COLORS.get(row[0], "#fff"), link_col=links)
     p = os.path.join(out_dir, "suspicious.html")
     with open(p, "w") as f:
@@ -152,12 +153,12 @@ def render_all(source: str, date: str, day_dir: str, out_dir: str | None = None,
                 hd, ed = _read_tsv(os.path.join(det, row["edge"]))
                 parts.append(f"<h2>Edge {html.escape(row['ip'])} ↔ {html.escape(row['peer'])} hour {row['hour']:02d} "
                              f"(score {html.escape(row['score'])})</h2>" + _table(hd, ed, 200))
-        p = os.path.join(out_dir, f"threat-{ip}.html")
+        p = os.path.join(out_dir, ent.get("page", f"threat-{ip}.html"))
         with open(p, "w") as f:
             f.write(_page(f"Threat investigation {ip}", "".join(parts), source, date))
         written.append(p)
     # storyboard
-    sb = "".join(f"<h2><a href='threat-{html.escape(t['ip'])}.html'>{html.escape(t['title'])}</a> "
+    sb = "".join(f"<h2><a href='{html.escape(ips.get(t['ip'], {}).get('page', 'threat-' + t['ip'] + '.html'))}'>{html.escape(t['title'])}</a> "
                  f"({html.escape(t['ip'])}, sev {t['sev']})</h2><p>{html.escape(t['comment'])}</p>"
                  for t in threats.values()) or "<p>No threats recorded (oni-oa threat ...).</p>"
     p = os.path.join(out_dir, "storyboard.html")

@@ -29,6 +29,64 @@ DEVICE_COLS = {"trhour": torch.int32, "trminute": torch.int32, "trsec": torch.in
                "dip": torch.int32}
 
 
+# IPv6 documents: every distinct IPv6 address of the day gets the 32-bit key V6_KEY_BASE + its
+# rank in the day's sorted IPv6 dictionary (exact, identical on every rank). 240.0.0.0/4 is the
+# reserved, never-routed IPv4 block, so the keys cannot collide with a real IPv4 document.
+V6_KEY_BASE = 0xF0000000
+V6_KEY_MAX = 1 << 28
+
+
+def _fixed(col, w: int = 48) -> np.ndarray:
+    """StringColumn → fixed-width bytes array (dtype S<w>), vectorised."""
+    off = col.offsets
+    ln = np.minimum(np.diff(off), w)
+    m = np.zeros((len(col), w), np.uint8)
+    if ln.sum():
+        r = np.repeat(np.arange(len(col)), ln)
+        k = np.arange(int(ln.sum())) - np.repeat(np.cumsum(ln) - ln, ln)
+        m[r, k] = col.chars[np.repeat(off[:-1], ln) + k]
+    return m.view(f"S{w}").reshape(-1)
+
+
+def with_ipv6_keys(cols: dict, comm: Comm | None = None, others: tuple = ()) -> dict:
+    """Columns with ``sip``/``dip`` of IPv6 rows replaced by their day-dictionary keys
+    (:data:`V6_KEY_BASE` + rank); ``others`` (e.g. analyst feedback rows) share the dictionary and
+    are returned keyed too. No IPv6 columns anywhere: the inputs come back unchanged."""
+    sets = [c for c in (cols, *others) if c]
+    have = any(k in c for c in sets for k in ("sip6", "dip6"))
+    if comm is not None and comm.dist:
+        have = comm.allreduce_scalar(1.0 if have else 0.0, "max") > 0
+    if not have:
+        return cols if not others else (cols, *others)
+    parts = []
+    for c in sets:
+        for k in ("sip6", "dip6"):
+            if k in c:
+                f = _fixed(c[k])
+                parts.append(f[f != b""])
+    uniq = np.unique(np.concatenate(parts)) if parts else np.zeros(0, "S48")
+    if comm is not None and comm.dist:
+        import torch.distributed as dist
+        allp = [None] * comm.world
+        dist.all_gather_object(allp, uniq.tolist(), group=comm.group)
+        uniq = np.unique(np.array([x for p in allp for x in p], dtype="S48"))
+    if uniq.size >= V6_KEY_MAX:
+        raise ValueError(f"{uniq.size} distinct IPv6 addresses exceed the 2^28 key space")
+
+    def keyed(c: dict) -> dict:
+        out = dict(c)
+        for k4, k6 in (("sip", "sip6"), ("dip", "dip6")):
+            if k6 in c:
+                f = _fixed(c[k6])
+                v6 = f != b""
+                key = (V6_KEY_BASE + np.searchsorted(uniq, f)).astype(np.uint32)
+                out[k4] = np.where(v6, key, np.asarray(c[k4]).astype(np.uint32))
+        return out
+
+    res = [keyed(c) if c else c for c in (cols, *others)]
+    return res[0] if not others else tuple(res)
+
+
 def to_device(cols: dict, device) -> dict:
     """Host columns → device through the pinned staging ring (io/staging.py): the host-side
     dtype conversion of column j+1 overlaps the DMA of column j."""
@@ -109,6 +167,8 @@ def run_flow(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxre
     the day's :data:`DEVICE_COLS` already on the device (e.g. from io.staging.Prefetcher, which
     uploaded them while the previous day computed); ``cols`` still supplies the host rows."""
     timer = StageTimer(device)
+    if device_cols is None:
+        cols, feedback = with_ipv6_keys(cols, comm, (feedback,)) if feedback else (with_ipv6_keys(cols, comm), None)
     with timer.stage("h2d"):
         d = dict(device_cols) if device_cols is not None else to_device(cols, device)
     with timer.stage("featurize"):

@@ -78,7 +78,7 @@ def str_to_ip(s: str) -> int:
 
 def generate_flows(n: int, seed: int = 7, n_hosts: int | None = None, n_profiles: int = 20,
                    alpha_true: float = 0.08, zipf_a: float = 1.15, n_anomalies: int | None = None,
-                   date=(2016, 7, 8), rank: int = 0, wide_vocab: bool = False) -> FlowDay:
+                   date=(2016, 7, 8), rank: int = 0, wide_vocab: bool = False, ipv6_frac: float = 0.0) -> FlowDay:
     """Generate ``n`` flows. ``rank`` offsets the RNG stream (weak-scaling shards of one day).
 
     ``wide_vocab``: a realistic-vocabulary day (SURVEY.md §7.5 sizing, V ≈ 1e5–1e6 flow words):
@@ -171,6 +171,13 @@ def generate_flows(n: int, seed: int = 7, n_hosts: int | None = None, n_profiles
         flood = rng.random(na) < 0.5
         ipkt[anomaly_rows] = np.where(flood, rng.integers(400_000, 600_000, size=na), rng.integers(1, 3, size=na))
 
+    v6_rows = None
+    if ipv6_frac > 0:
+        v6_host = np.random.default_rng([seed, 0x6666]).random(n_hosts) < ipv6_frac
+        v6_rows = v6_host[src]
+        if na:
+            v6_rows[anomaly_rows] = False
+
     y, mo, d = date
     unix = (np.int64(1467936000) + hour * 3600 + minute * 60 + second).astype(np.int64)
     cols = {
@@ -203,4 +210,20 @@ def generate_flows(n: int, seed: int = 7, n_hosts: int | None = None, n_profiles
         "dir": np.zeros(n, dtype=np.int32),
         "rip": np.zeros(n, dtype=np.uint32),
     }
+    if v6_rows is not None and v6_rows.any():
+        from ..store.columnar import StringColumn
+
+        import ipaddress
+
+        def v6_text(ip4: np.ndarray) -> list[str]:  # 2001:db8:<ip4 hi>:<ip4 lo>::1 in RFC 5952 form
+            base = int(ipaddress.IPv6Address("2001:db8::1"))
+            return [ipaddress.IPv6Address(base | (x << 64)).compressed for x in ip4.astype(np.int64).tolist()]
+
+        idx = np.nonzero(v6_rows)[0]
+        for k4, k6 in (("sip", "sip6"), ("dip", "dip6")):
+            txt = [""] * n
+            for i, t in zip(idx.tolist(), v6_text(cols[k4][idx])):
+                txt[i] = t
+            cols[k6] = StringColumn.from_list(txt)
+            cols[k4] = np.where(v6_rows, 0, cols[k4]).astype(np.uint32)
     return FlowDay(cols=cols, theta_true=theta, host_ips=host_ips, anomaly_rows=anomaly_rows)

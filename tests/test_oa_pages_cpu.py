@@ -39,10 +39,10 @@ def test_flow_details_threat_and_pages(tmp_path):
     assert len(idx["rows"]) == 10
     for ent, r in zip(idx["rows"], rows):
         sip, dip, hh = r[header.index("sip")], r[header.index("dip")], int(r[header.index("trhour")])
-        assert ent["edge"] == f"edge-{sip}-{dip}-{hh:02d}.tsv"
+        assert ent["edge"] == f"edge-{sip}-{dip}-{hh:02d}.tsv"  # IPv4 names are already file-safe
         lines = open(os.path.join(det, ent["edge"])).read().splitlines()
         assert ent["edge_rows"] >= 1 and len(lines) == ent["edge_rows"] + 1  # the event itself is in its edge
-        assert os.path.exists(os.path.join(det, f"chord-{sip}.tsv")) and os.path.exists(os.path.join(det, f"timeline-{sip}.tsv"))
+        assert os.path.exists(os.path.join(det, idx["ips"][sip]["chord"])) and os.path.exists(os.path.join(det, idx["ips"][sip]["timeline"]))
     summ = open(os.path.join(det, "ingest_summary.tsv")).read().splitlines()
     assert sum(int(x.split("\t")[1]) for x in summ[1:]) == 6000
     ip = idx["rows"][0]["ip"]
