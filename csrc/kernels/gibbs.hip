@@ -972,7 +972,10 @@ int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s)
   const unsigned grid = (unsigned)((a.n_slices + kWavesPerBlock - 1) / kWavesPerBlock);
   if (grid == 0) return 0;
   if (init) {
-    k_gibbs<G, KP, true, 1, false><<<grid, kBlock, 0, s>>>(a);  // init always builds n_wk by atomics
+    // mode 1: n_wk by per-token atomics (same-address contention on frequent words: 1.5 ms at 25M
+    // tokens); mode 0: no n_wk bookkeeping, the caller rebuilds it with the word-sorted recount
+    if (mode == 0) k_gibbs<G, KP, true, 0, false><<<grid, kBlock, 0, s>>>(a);
+    else k_gibbs<G, KP, true, 1, false><<<grid, kBlock, 0, s>>>(a);
     return (int)hipGetLastError();
   }
   if (mode == 4) {  // word-sorted change bitmap

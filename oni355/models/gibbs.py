@@ -197,8 +197,11 @@ class GibbsLDA:
         self.tok_z.zero_()
         self.a = self.b = 0
         self.cn = 0
+        # topics drawn without n_wk atomics, then n_wk rebuilt by the word-sorted recount (integer
+        # counts: identical to the atomic build, without its same-address contention)
         ops.gibbs_pass(self._state(True), self.G, self.KP, self.K, self.alpha, self.cfg.seed, True,
-                       self.sweep_ctr, self.c.chunk_len, host_sweep=0)
+                       self.sweep_ctr, self.c.chunk_len, host_sweep=0, mode=0)
+        ops.recount(self.c.wsorted, self.c.wslot, self.tok_z, self.nwk, self.KS)
         if self.comm is not None and self.comm.dist:
             self.comm.allreduce_(self.nwk)
             self.comm.allreduce_(self.nk[0])
