@@ -314,6 +314,156 @@ __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
   }
 }
 
+// ---- two-deep token stream, q row issued a full step ahead (G = 1) -----------------------------
+// k_gibbs<.., QPF = true> fetches the next token's q row at the END of a step and consumes it at
+// the top of the next one: with ~11 % of tokens starting a new word, some lane of a wave needs a
+// row on almost every step, so that L2 round trip is exposed once per step (the dominant
+// s_waitcnt stall in the K = 20 counters). Here token words/topics/slots stream two steps ahead,
+// so token s+1's word is already in registers at the top of step s: its q row is issued there,
+// before step s's math and stores, and waited for only when the step ends. Same arithmetic as
+// k_gibbs (mul + add chain), so the same draws bitwise.
+template <int KP, int MODE>
+__global__ __launch_bounds__(kBlock) void k_gibbs_q2(const OniGibbs a) {
+  constexpr bool ATOMIC = MODE == 1;
+  constexpr int S = oni::kWave;
+  constexpr int KS = KP;
+  __shared__ int32_t red[kWavesPerBlock][KS];
+
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int c = lane;
+  const int64_t slice = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  const bool valid = slice < a.n_slices;
+  const int64_t chunk = slice * S + c;
+  const int doc = valid ? a.chunk_doc[chunk] : -1;
+  const bool live = doc >= 0;
+
+  int32_t n[KP];
+#pragma unroll
+  for (int j = 0; j < KP; ++j) n[j] = 0;
+  if (live) load_row_i<KP>(a.ndk_src + (int64_t)doc * KS, n);
+
+  const int len = valid ? a.slice_len[slice] : 0;
+  const int64_t off = valid ? a.slice_off[slice] : 0;
+  const uint32_t key = live ? a.chunk_key[chunk] : 0u;
+  const uint32_t pos0 = live ? (uint32_t)a.chunk_pos0[chunk] : 0u;
+  const uint32_t sweep = *a.sweep_ctr;
+
+  constexpr bool WPF = MODE == 3 || MODE == 4;
+  // token stream: (w0, z0, p0) = token s, (w1, z1, p1) = token s + 1
+  uint32_t w0 = len > 0 ? a.tok_word[off + c] : oni::kPadWord;
+  int z0 = len > 0 ? (int)a.tok_z[off + c] : 0;
+  int32_t p0 = (WPF && len > 0) ? a.wpos[off + c] : 0;
+  uint32_t w1 = len > 1 ? a.tok_word[off + S + c] : oni::kPadWord;
+  int z1 = len > 1 ? (int)a.tok_z[off + S + c] : 0;
+  int32_t p1 = (WPF && len > 1) ? a.wpos[off + S + c] : 0;
+  float qv[KP], qn[KP];
+#pragma unroll
+  for (int j = 0; j < KP; ++j) qv[j] = qn[j] = 0.f;
+  if (w0 != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)w0 * KS, qv);
+
+  oni::U4 r{0, 0, 0, 0};
+  int nchg = 0;
+  for (int s = 0; s < len; ++s) {
+    const int64_t idx = off + (int64_t)s * S + c;
+    const uint32_t w = w0;
+    const int zo = z0;
+    const int32_t pw = p0;
+    // token s+1's q row now (consumed after this step's math): a full step of latency hiding
+    const bool fetch = w1 != oni::kPadWord && w1 != w;
+    if (fetch) load_row_f<KP>(a.q + (int64_t)w1 * KS, qn);
+    // advance the token stream: token s+2's loads queue behind the q row
+    w0 = w1;
+    z0 = z1;
+    p0 = p1;
+    if (s + 2 < len) {
+      w1 = a.tok_word[idx + 2 * S];
+      z1 = a.tok_z[idx + 2 * S];
+      if (WPF) p1 = a.wpos[idx + 2 * S];
+    } else {
+      w1 = oni::kPadWord;
+    }
+    if (w != oni::kPadWord) {
+      const uint32_t pos = pos0 + (uint32_t)s;
+      if (s == 0 || (pos & 3u) == 0u) r = oni::philox10(oni::U4{pos >> 2, key, sweep, 1u}, a.seed0, a.seed1);
+      const uint32_t rr = oni::pick4(r, pos & 3u);
+#pragma unroll
+      for (int j = 0; j < KP; ++j) n[j] -= (j == zo);
+      float loc[KP];
+      float run = 0.f;
+#pragma unroll
+      for (int j = 0; j < KP; ++j) {
+        run = run + ((float)n[j] + a.alpha) * qv[j];
+        loc[j] = run;
+      }
+      const float thr = oni::u01(rr) * run;
+      int cnt = 0;
+#pragma unroll
+      for (int j = 0; j < KP; ++j) cnt += (loc[j] <= thr);
+      const int zn = cnt < a.K - 1 ? cnt : a.K - 1;
+#pragma unroll
+      for (int j = 0; j < KP; ++j) n[j] += (j == zn);
+      if (zn != zo) {
+        ++nchg;
+        a.tok_z[idx] = (uint8_t)zn;
+        if constexpr (MODE == 3) a.z_w[pw] = (uint8_t)zn;
+        if constexpr (MODE == 4) mark_changed_w(a, pw, zo, zn);
+        if (ATOMIC) {
+          atomicAdd(&a.dnwk[(int64_t)w * KS + zo], -1);
+          atomicAdd(&a.dnwk[(int64_t)w * KS + zn], 1);
+        }
+      }
+      if constexpr (MODE == 2) {
+        const uint64_t m = __ballot(zn != zo);
+        if (lane == 0) a.chg_mask[(off + (int64_t)s * S) / S] = m;
+      }
+    }
+    if (fetch) {
+#pragma unroll
+      for (int j = 0; j < KP; ++j) qv[j] = qn[j];
+    }
+  }
+
+  // ---- epilogue: doc rows + per-topic totals (as k_gibbs, G = 1) --------------------------------
+  if (a.chg_count) add_wave_count(a.chg_count, nchg);
+  int32_t d[KP];
+#pragma unroll
+  for (int j = 0; j < KP; ++j) d[j] = 0;
+  if (live) {
+    int32_t* dst = a.ndk_dst + (int64_t)doc * KS;
+    int32_t n0[KP];
+    load_row_i<KP>(a.ndk_src + (int64_t)doc * KS, n0);
+#pragma unroll
+    for (int j = 0; j < KP; ++j) d[j] = n[j] - n0[j];
+    if (!a.chunk_multi[chunk]) {
+#pragma unroll
+      for (int j = 0; j < KP; j += 4) *reinterpret_cast<int4*>(dst + j) = make_int4(n[j], n[j + 1], n[j + 2], n[j + 3]);
+    }
+  }
+  {
+    const bool multi = live && a.chunk_multi[chunk];
+    if (__ballot(multi)) flush_multi_rows<1, KP>(a.ndk_dst, KS, doc, multi, 0, d);
+  }
+#pragma unroll
+  for (int j = 0; j < KP; ++j) {
+    int v = d[j];
+#pragma unroll
+    for (int m = 1; m < oni::kWave; m <<= 1) v += __shfl_xor(v, m);
+    d[j] = v;
+  }
+  if (c == 0) {
+#pragma unroll
+    for (int j = 0; j < KP; ++j) red[wave][j] = d[j];
+  }
+  __syncthreads();
+  if (threadIdx.x < KS) {
+    int v = 0;
+#pragma unroll
+    for (int w = 0; w < kWavesPerBlock; ++w) v += red[w][threadIdx.x];
+    if (v) atomicAdd(&a.dnk[(int)(blockIdx.x & (unsigned)(a.nk_rep - 1)) * KS + threadIdx.x], v);
+  }
+}
+
 // ---- ping-pong register sampler (the default sweep kernel) ------------------------------------
 // Same numerics as k_gibbs (mul + add weight chain, bitwise identical), restructured for issue
 // rate: the loop is unrolled by two so the q row of the next token always lands in the other half
@@ -969,8 +1119,21 @@ int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s)
   // 2 = k_gibbs_lds (G = 1) / k_gibbs_ldsg (G > 1): LDS-staged counts, fma numerics
   if (a.KS != G * KP || mode < 0 || mode > 4) return (int)hipErrorInvalidValue;
   if (G == 1 && qpf == 5) qpf = 2;  // q-prefetching LDS sampler is the multi-lane variant
+  if (G > 1 && qpf == 6) qpf = 4;   // the two-deep stream variant is written for G = 1
   const unsigned grid = (unsigned)((a.n_slices + kWavesPerBlock - 1) / kWavesPerBlock);
   if (grid == 0) return 0;
+  if constexpr (G == 1) {
+    if (!init && qpf == 6) {
+      switch (mode) {
+        case 0: k_gibbs_q2<KP, 0><<<grid, kBlock, 0, s>>>(a); break;
+        case 1: k_gibbs_q2<KP, 1><<<grid, kBlock, 0, s>>>(a); break;
+        case 2: k_gibbs_q2<KP, 2><<<grid, kBlock, 0, s>>>(a); break;
+        case 3: k_gibbs_q2<KP, 3><<<grid, kBlock, 0, s>>>(a); break;
+        default: k_gibbs_q2<KP, 4><<<grid, kBlock, 0, s>>>(a); break;
+      }
+      return (int)hipGetLastError();
+    }
+  }
   if (init) {
     // mode 1: n_wk by per-token atomics (same-address contention on frequent words: 1.5 ms at 25M
     // tokens); mode 0: no n_wk bookkeeping, the caller rebuilds it with the word-sorted recount

@@ -28,7 +28,7 @@ from .corpus import Corpus, canonical_tokens
 
 
 NK_REP = 32
-SAMPLERS = {"pp": 1, "plain": 0, "lds": 2, "qpf": 4, "ldsq": 5}  # -> oni_gibbs_launch qpf argument
+SAMPLERS = {"pp": 1, "plain": 0, "lds": 2, "qpf": 4, "ldsq": 5, "q2": 6}  # -> oni_gibbs_launch qpf argument
 
 
 @dataclass

@@ -70,6 +70,8 @@ def _toy_tokens(n_docs, V, seed, heavy=True):
                                     (50, "wdelta+lds"), (100, "wdelta+lds"), (100, "atomic+lds"), (64, "delta+lds"),
                                     (40, "dual+lds"), (80, "wdelta+lds"), (128, "recount+lds"), (200, "atomic+lds"),
                                     (50, "recount+ldsq"), (100, "wdelta+ldsq"), (64, "delta+ldsq"), (100, "dual+ldsq"),
+                                    (20, "wdelta+q2"), (20, "recount+q2"), (20, "delta+q2"), (20, "dual+q2"),
+                                    (20, "atomic+q2"), (7, "wdelta+q2"), (32, "wdelta+q2"),
                                     (200, "atomic+ldsq"), (50, "dual+plain"), (100, "wdelta+plain"),
                                     (100, "atomic+plain"), (64, "delta+pp"), (20, "wdelta+lds"), (7, "wdelta+lds"),
                                     (32, "wdelta+lds"), (20, "recount+lds")])
