@@ -103,6 +103,10 @@ def lib() -> C.CDLL:
                 _bind(h, name, args)
         if h.oni_gibbs_sizeof_args() != C.sizeof(OniGibbs):
             raise RuntimeError("OniGibbs ABI mismatch between Python and liboni_hip.so; rebuild")
+        from ..utils import provenance
+        h.oni_hip_src_hash.restype = C.c_char_p
+        h.oni_hip_src_hash.argtypes = []
+        provenance.check("hip", h.oni_hip_src_hash().decode(), HIP_LIB_PATH)
         _lib = h
         return h
 

@@ -35,6 +35,10 @@ def lib() -> C.CDLL:
                 if hasattr(h, name):
                     fn = getattr(h, name)
                     fn.argtypes, fn.restype = args, res
+            from ..utils import provenance
+            h.oni_native_src_hash.restype = C.c_char_p
+            h.oni_native_src_hash.argtypes = []
+            provenance.check("native", h.oni_native_src_hash().decode(), NATIVE_LIB_PATH)
             _lib = h
     return _lib
 

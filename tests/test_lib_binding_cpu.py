@@ -34,3 +34,19 @@ def test_late_registered_launchers_are_bound():
                        env={**os.environ, "PYTHONPATH": ROOT})
     assert r.returncode == 0, r.stderr[-2000:]
     assert "bound" in r.stdout
+
+
+def test_libraries_embed_the_hash_of_this_trees_sources():
+    """Build provenance: each library reports the content hash of the sources it was built from,
+    which must equal this tree's (the loader refuses a stale build; a GPU run of this test
+    therefore proves its kernels came from the committed sources)."""
+    from oni355.ops import _lib, native
+    from oni355.utils import provenance
+    if not os.path.exists(_lib.HIP_LIB_PATH):
+        pytest.skip("liboni_hip.so not built")
+    assert _lib.lib().oni_hip_src_hash().decode() == provenance.tree_hash("hip")
+    assert native.lib().oni_native_src_hash().decode() == provenance.tree_hash("native")
+    r = subprocess.run([sys.executable, "-c", "from oni355.utils import provenance as p; "
+                        "p.check('hip', 'deadbeefdeadbeef', 'x.so')"], cwd=ROOT, capture_output=True, text=True,
+                       env={**os.environ, "PYTHONPATH": ROOT})
+    assert r.returncode != 0 and "rebuild" in r.stderr

@@ -11,7 +11,11 @@ Produces, in-tree (so the artefacts travel with a ``gpurun`` snapshot):
 * ``oni355/_lib/bin/lda``          -- standalone ``lda est|inf`` CLI (oni-lda-c equivalent).
 * ``oni355/_lib/bin/oni-nfdump``   -- standalone nfcapd → CSV decoder (oni-nfdump equivalent).
 
-Incremental: an object is rebuilt when its source or any header in ``csrc/`` is newer.
+Incremental by content: an object is rebuilt when the hash of its source + every header in
+``csrc/`` + its compile flags differs from the one recorded next to it (``<obj>.sha``), never by
+mtime. The libraries embed the content hash of the sources they were built from
+(``oni_hip_src_hash()`` / ``oni_native_src_hash()``, oni355/utils/provenance.py), which the package
+checks when it loads them.
 Usage: ``python tools/build.py [--jobs N] [--only hip|native] [--sanitize] [-v]``.
 """
 from __future__ import annotations
@@ -19,6 +23,7 @@ from __future__ import annotations
 import argparse
 import concurrent.futures as cf
 import glob
+import hashlib
 import os
 import shlex
 import subprocess
@@ -47,16 +52,40 @@ CXX_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-fopenmp", "-Wall", "-Wno-unused-fun
              "-I", os.path.join(CSRC, "native")]
 
 
-def _newest_header() -> float:
-    hs = glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)
-    return max((os.path.getmtime(h) for h in hs), default=0.0)
+sys.path.insert(0, ROOT)
+from oni355.utils import provenance  # noqa: E402
 
 
-def _stale(src: str, obj: str, hdr_t: float) -> bool:
-    if not os.path.exists(obj):
+def _headers_digest() -> str:
+    h = hashlib.sha256()
+    for p in sorted(glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)):
+        h.update(p.encode())
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def _obj_key(src: str, cmd: list[str], hdr: str) -> str:
+    h = hashlib.sha256()
+    with open(src, "rb") as f:
+        h.update(f.read())
+    h.update(hdr.encode())
+    h.update("\0".join(cmd).encode())
+    return h.hexdigest()
+
+
+def _stale(obj: str, key: str) -> bool:
+    sha = obj + ".sha"
+    if not (os.path.exists(obj) and os.path.exists(sha)):
         return True
-    t = os.path.getmtime(obj)
-    return os.path.getmtime(src) > t or hdr_t > t
+    with open(sha) as f:
+        return f.read().strip() != key
+
+
+def _mark(jobs: list) -> None:
+    for _, o, key in jobs:
+        with open(o + ".sha", "w") as f:
+            f.write(key)
 
 
 def _run(cmd: list[str], verbose: bool) -> None:
@@ -70,24 +99,29 @@ def _run(cmd: list[str], verbose: bool) -> None:
         sys.stderr.write(r.stderr)
 
 
-def _compile_all(jobs: list[tuple[list[str], str]], n: int, verbose: bool) -> None:
+def _compile_all(jobs: list, n: int, verbose: bool) -> None:
     with cf.ThreadPoolExecutor(max_workers=n) as ex:
-        futs = [ex.submit(_run, cmd, verbose) for cmd, _ in jobs]
+        futs = [ex.submit(_run, job[0], verbose) for job in jobs]
         for f in futs:
             f.result()
+    _mark(jobs)
 
 
 def build_hip(n_jobs: int, verbose: bool) -> str:
     os.makedirs(os.path.join(OBJ, "hip"), exist_ok=True)
     os.makedirs(LIBDIR, exist_ok=True)
-    hdr_t = _newest_header()
+    hdr = _headers_digest()
+    src_hash = provenance.tree_hash("hip")
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     objs, jobs = [], []
     for s in srcs:
         o = os.path.join(OBJ, "hip", os.path.basename(s) + ".o")
         objs.append(o)
-        if _stale(s, o, hdr_t):
-            jobs.append(([HIPCC, *HIP_FLAGS, "-c", s, "-o", o], o))
+        extra = [f'-DONI_SRC_HASH="{src_hash}"'] if os.path.basename(s) == "build_info.hip" else []
+        cmd = [HIPCC, *HIP_FLAGS, *extra, "-c", s, "-o", o]
+        key = _obj_key(s, cmd, hdr)
+        if _stale(o, key):
+            jobs.append((cmd, o, key))
     _compile_all(jobs, n_jobs, verbose)
     out = os.path.join(LIBDIR, "liboni_hip.so")
     if jobs or not os.path.exists(out) or any(os.path.getmtime(o) > os.path.getmtime(out) for o in objs):
@@ -99,7 +133,8 @@ def build_hip(n_jobs: int, verbose: bool) -> str:
 def build_native(n_jobs: int, verbose: bool, sanitize: bool) -> list[str]:
     os.makedirs(os.path.join(OBJ, "native"), exist_ok=True)
     os.makedirs(BINDIR, exist_ok=True)
-    hdr_t = _newest_header()
+    hdr = _headers_digest()
+    src_hash = provenance.tree_hash("native")
     flags = list(CXX_FLAGS)
     if sanitize:
         flags += ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-O1", "-g"]
@@ -114,8 +149,11 @@ def build_native(n_jobs: int, verbose: bool, sanitize: bool) -> list[str]:
         o = os.path.join(OBJ, "native", f"{os.path.basename(s)}.{tag}.o")
         if s in lib_srcs:
             objs.append(o)
-        if _stale(s, o, hdr_t):
-            jobs.append(([CXX, *flags, "-c", s, "-o", o], o))
+        extra = [f'-DONI_SRC_HASH="{src_hash}"'] if os.path.basename(s) == "version.cpp" else []
+        cmd = [CXX, *flags, *extra, "-c", s, "-o", o]
+        key = _obj_key(s, cmd, hdr)
+        if _stale(o, key):
+            jobs.append((cmd, o, key))
     _compile_all(jobs, n_jobs, verbose)
     outs = []
     suffix = "_asan" if sanitize else ""
