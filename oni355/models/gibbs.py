@@ -162,8 +162,10 @@ class GibbsLDA:
         V, KS = self.V, self.KS
         dev = self.device
         cnt = torch.zeros(V, dtype=torch.int64, device=dev)
-        if self.c.T:
-            cnt += torch.bincount(self.c.wsorted.to(torch.int64), minlength=V)[:V]
+        if self.c.T:  # wsorted is sorted: run lengths by binary search, no contended histogram
+            ws = self.c.wsorted.to(torch.int64)
+            edges = torch.searchsorted(ws, torch.arange(V + 1, dtype=torch.int64, device=dev))
+            cnt += edges[1:] - edges[:-1]
         self.comm.allreduce_(cnt, op="max")
         light = torch.nonzero(cnt <= O).flatten().to(torch.int32)
         heavy = torch.nonzero(cnt > O).flatten().to(torch.int32)

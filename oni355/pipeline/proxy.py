@@ -66,9 +66,14 @@ def _codes_by_hash(col: StringColumn, dev, fn) -> torch.Tensor:
 
 
 def _unique_first(h: torch.Tensor):
-    uniq, inv = torch.unique(h, return_inverse=True)
-    first = torch.full((uniq.numel(),), h.numel(), dtype=torch.int64, device=h.device)
-    first.scatter_reduce_(0, inv, torch.arange(h.numel(), device=h.device), reduce="amin")
+    """(sorted unique values, first row of each (CPU), inverse). Sort-based: an atomic-min
+    scatter_reduce here serialised 2M rows onto a handful of distinct values (27 ms per call)."""
+    sh, order = torch.sort(h, stable=True)
+    uniq, counts = torch.unique_consecutive(sh, return_counts=True)
+    starts = torch.cumsum(counts, 0) - counts
+    first = order[starts]
+    inv = torch.empty_like(order)
+    inv[order] = torch.repeat_interleave(torch.arange(uniq.numel(), device=h.device), counts)
     return uniq, first.cpu(), inv
 
 
