@@ -134,12 +134,13 @@ def _concat(parts: list[dict]) -> dict:
         if k.startswith("_"):
             continue
         v = [p[k] for p in parts]
-        out[k] = StringColumn.concat(v) if hasattr(v[0], "offsets") else np.concatenate(v)
+        out[k] = StringColumn.concat(v) if isinstance(v[0], StringColumn) else np.concatenate(v)
     return out
 
 
 def _slice(cols: dict, lo: int, hi: int) -> dict:
-    return {k: (v.slice(lo, hi) if hasattr(v, "offsets") else v[lo:hi]) for k, v in cols.items() if not k.startswith("_")}
+    from ..store.columnar import StringColumn
+    return {k: (v.slice(lo, hi) if isinstance(v, StringColumn) else v[lo:hi]) for k, v in cols.items() if not k.startswith("_")}
 
 
 def load_events(a, cfg, source: str, rank: int, world: int) -> tuple[dict, int, int]:

@@ -23,6 +23,7 @@ import time
 import numpy as np
 
 from ..store import columnar
+from ..store.columnar import StringColumn
 
 DEFAULT_PATTERNS = {"flow": ["nfcapd.*", "*.csv"], "dns": ["*.pcap", "*.pcapng"], "proxy": ["*.log"]}
 
@@ -80,7 +81,7 @@ def store_rows(root: str, source: str, cols: dict, hourly: bool = True) -> dict[
     bounds = list(first) + [key.size]
     for j, k in enumerate(uk.tolist()):
         idx = order[bounds[j]:bounds[j + 1]]
-        part = {c: (v.take(idx) if hasattr(v, "offsets") else np.asarray(v)[idx]) for c, v in cols.items()}
+        part = {c: (v.take(idx) if isinstance(v, StringColumn) else np.asarray(v)[idx]) for c, v in cols.items()}
         day = k // 24 if hourly else k
         date = (_dt.date(1970, 1, 1) + _dt.timedelta(days=int(day))).strftime("%Y%m%d")
         columnar.append_part(root, source, date, part, hour=int(k % 24) if hourly else None)

@@ -140,7 +140,7 @@ def read_flow_csv(path: str, threads: int = 0) -> tuple[dict, int]:
         if keep is not None and not keep.all():  # unparsable address text: a bad row, as before
             bad += int((~keep).sum())
             idx = np.nonzero(keep)[0]
-            cols = {k: (v.take(idx) if hasattr(v, "offsets") else v[idx]) for k, v in cols.items()}
+            cols = {k: (v.take(idx) if isinstance(v, StringColumn) else v[idx]) for k, v in cols.items()}
     return finish_flow_cols(cols), bad
 
 

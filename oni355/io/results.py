@@ -65,7 +65,7 @@ def event_rows(source: str, cols: dict, local_rows, words: list[str], scores) ->
             v = cols.get(c)
             if v is None:
                 row.append("")
-            elif hasattr(v, "offsets"):
+            elif isinstance(v, StringColumn):
                 row.append(v[int(r)])
             elif c in _EVENT_IP_COLUMNS:
                 row.append(ip_str(v[r]))
@@ -144,7 +144,7 @@ def _native_format(fields: list[tuple[int, object]], n: int) -> Rendered:
 def _col_field(c: str, v, rows: np.ndarray, ip_cols=(), time_cols=(), float_cols=()):
     if v is None:
         return K_STR, _EMPTY.take(np.zeros(rows.size, np.int64))
-    if hasattr(v, "offsets"):
+    if isinstance(v, StringColumn):
         return K_STR, v.take(rows)
     a = np.asarray(v)[rows]
     if c in ip_cols:

@@ -141,6 +141,6 @@ def write_log(day: ProxyDay, path: str) -> None:
             vals = []
             for name in order:
                 v = c[name]
-                s = v[i] if hasattr(v, "offsets") else (ip_str(v[i]) if name in ("clientip", "serverip") else str(v[i]))
+                s = v[i] if isinstance(v, StringColumn) else (ip_str(v[i]) if name in ("clientip", "serverip") else str(v[i]))
                 vals.append(f'"{s}"' if (" " in s or s == "") else s)
             f.write(" ".join(vals) + "\n")

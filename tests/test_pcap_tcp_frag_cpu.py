@@ -70,3 +70,23 @@ def test_tcp_messages_and_fragment_reassembly(tmp_path):
         # the reassembled datagram carries the frame that completed it (packet 5)
         assert c["unix_tstamp"].tolist() == [1467936000, 1467936001, 1467936001, 1467936005, 1467936007]
         assert c["_tcp_partial"] == 1 and c["_frag_incomplete"] == 1
+
+
+def test_frame_time_is_formatted_only_for_rendered_rows(tmp_path):
+    """pcap frame_time text is lazy: rendering the result rows formats just those rows (formatting
+    every packet's time cost 0.27 s per 2M-packet day)."""
+    from oni355.io import results as rio
+    from oni355.io.decoders import FrameTimeColumn, frame_times
+    from oni355.synth.dns import generate_dns, write_pcap
+    day = generate_dns(3000, seed=5)
+    p = str(tmp_path / "d.pcap")
+    write_pcap(day, p)
+    cols = read_pcap_dns(p)
+    ft = cols["frame_time"]
+    assert isinstance(ft, FrameTimeColumn)
+    rows = np.array([5, 17, 2999])
+    r = rio.format_events("dns", cols, rows, ["w"] * 3, np.zeros(3, np.float32))
+    assert ft._mat is None
+    want = frame_times(ft.ts_ns[rows]).to_list()
+    import csv
+    assert [row[0] for row in csv.reader(ln.decode() for ln in r.lines())] == want
