@@ -82,6 +82,22 @@ def method_code(s: str) -> int:
     return METHODS.index(s) if s in METHODS else 0
 
 
+_HOUR_TABLES: dict = {}
+
+
+def _hour_table(dev) -> torch.Tensor:
+    """f32 (h + m/60) + s/3600 for every second of the day, computed on the host exactly as the
+    word spec does, then kept on the device (a p_time → hour lookup)."""
+    key = str(dev)
+    if key not in _HOUR_TABLES:
+        sod = np.arange(86400, dtype=np.int64)
+        hh, mm, ss = sod // 3600, sod // 60 % 60, sod % 60
+        t = (torch.from_numpy(hh.astype(np.float32)) + torch.from_numpy(mm.astype(np.float32)) / 60.0) \
+            + torch.from_numpy(ss.astype(np.float32)) / 3600.0
+        _HOUR_TABLES[key] = t.to(dev)
+    return _HOUR_TABLES[key]
+
+
 @traced("oni:proxy.featurize")
 def featurize(cols: dict, device, comm: Comm | None, topset, allreduce_counts: bool = True):
     dev = torch.device(device)
@@ -94,16 +110,21 @@ def featurize(cols: dict, device, comm: Comm | None, topset, allreduce_counts: b
 
     ho, hc = strcol("host")
     _, top, _, _, _ = sops.domain_features(ho, hc, topset, "")
-    # time of day from p_time "HH:MM:SS"
-    pt = cols["p_time"]
-    ptb = np.frombuffer(pt.chars.tobytes(), dtype=np.uint8) if pt.chars.size else np.zeros(0, np.uint8)
-    o = pt.offsets[:-1]
-    def dig(k):
-        return (ptb[o + k].astype(np.int64) - 48) if n else np.zeros(0, np.int64)
-    hh, mm, ss = dig(0) * 10 + dig(1), dig(3) * 10 + dig(4), dig(6) * 10 + dig(7)
-    t = (torch.from_numpy(hh.astype(np.float32)) + torch.from_numpy(mm.astype(np.float32)) / 60.0) \
-        + torch.from_numpy(ss.astype(np.float32)) / 3600.0
-    tkey = ops.f32_keys(t.to(dev).contiguous())
+    # time of day from p_time "HH:MM:SS": the digits are read on the device, the f32 hour value
+    # comes from a 86400-entry table built with the reference formula (bitwise the host result)
+    po, pc = strcol("p_time")
+    if n:
+        base = po[:-1]
+        ok = (po[1:] - base) >= 8  # malformed / short times read as 00:00:00
+        last = pc.numel() - 1
+
+        def dig(k):
+            return torch.where(ok, pc[(base + k).clamp(max=last)].to(torch.int64) - 48, 0)
+        sod = (dig(0) * 10 + dig(1)) * 3600 + (dig(3) * 10 + dig(4)) * 60 + (dig(6) * 10 + dig(7))
+        t = _hour_table(dev)[sod.clamp_(0, 86399)]
+    else:
+        t = torch.zeros(0, dtype=torch.float32, device=dev)
+    tkey = ops.f32_keys(t.contiguous())
     # user-agent frequency over the day (global across ranks)
     uo, uc = strcol("useragent")
     uh, _, _ = sops.string_features(uo, uc)
