@@ -141,10 +141,12 @@ bool index_pcap(const uint8_t* b, size_t n, std::vector<Pkt>* out, std::string* 
   return true;
 }
 
-// read a (possibly compressed) DNS name at `o` into `name`; returns bytes consumed at o, or -1
-int read_name(const uint8_t* m, size_t mlen, size_t o, std::string* name) {
-  name->clear();
-  size_t pos = o;
+// read a (possibly compressed) DNS name at `o`, appending it to `out` when given (nothing is
+// appended on failure); returns bytes consumed at o, or -1. No allocation: the decoder calls this
+// for every packet, so names go straight into the thread's column buffer.
+int read_name(const uint8_t* m, size_t mlen, size_t o, std::string* out) {
+  const size_t base = out ? out->size() : 0;
+  size_t pos = o, len = 0;
   int consumed = -1;
   int jumps = 0;
   while (pos < mlen) {
@@ -154,18 +156,33 @@ int read_name(const uint8_t* m, size_t mlen, size_t o, std::string* name) {
       return consumed;
     }
     if ((l & 0xC0) == 0xC0) {
-      if (pos + 1 >= mlen || ++jumps > 32) return -1;
+      if (pos + 1 >= mlen || ++jumps > 32) break;
       if (consumed < 0) consumed = (int)(pos + 2 - o);
       pos = ((size_t)(l & 0x3F) << 8) | m[pos + 1];
       continue;
     }
-    if ((l & 0xC0) != 0 || pos + 1 + l > mlen) return -1;
-    if (!name->empty()) name->push_back('.');
-    name->append((const char*)m + pos + 1, l);
-    if (name->size() > 255) return -1;
+    if ((l & 0xC0) != 0 || pos + 1 + l > mlen) break;
+    len += (len ? 1 : 0) + l;
+    if (len > 255) break;
+    if (out) {
+      if (out->size() > base) out->push_back('.');
+      out->append((const char*)m + pos + 1, l);
+    }
     pos += 1 + l;
   }
+  if (out) out->resize(base);
   return -1;
+}
+
+// dotted IPv4 text appended without snprintf
+void put_ipv4(std::string* s, const uint8_t* a) {
+  for (int k = 0; k < 4; ++k) {
+    if (k) s->push_back('.');
+    const unsigned v = a[k];
+    if (v >= 100) s->push_back((char)('0' + v / 100));
+    if (v >= 10) s->push_back((char)('0' + (v / 10) % 10));
+    s->push_back((char)('0' + v % 10));
+  }
 }
 
 struct Frag {
@@ -250,32 +267,33 @@ void parse_dns(const uint8_t* m, size_t ml, int64_t ts_ns, uint32_t origlen, uin
   if (!(flags & 0x8000)) return;  // responses only
   const int qd = be16(m + 4), an = be16(m + 6);
   if (qd < 1) return;
-  std::string name;
-  int c = read_name(m, ml, 12, &name);
-  if (c < 0 || (size_t)(12 + c + 4) > ml) return;
+  const size_t name0 = r->names.size(), a0 = r->as.size();
+  int c = read_name(m, ml, 12, &r->names);
+  if (c < 0 || (size_t)(12 + c + 4) > ml) {
+    r->names.resize(name0);
+    return;
+  }
   size_t pos = 12 + c;
   const int qtype = be16(m + pos), qclass = be16(m + pos + 2);
   pos += 4;
   for (int q = 1; q < qd; ++q) {  // skip further questions
-    std::string tmp;
-    int cc = read_name(m, ml, pos, &tmp);
-    if (cc < 0) return;
+    int cc = read_name(m, ml, pos, nullptr);
+    if (cc < 0) {
+      r->names.resize(name0);
+      return;
+    }
     pos += cc + 4;
   }
-  std::string answers;
   for (int a = 0; a < an && pos < ml; ++a) {
-    std::string tmp;
-    int cc = read_name(m, ml, pos, &tmp);
+    int cc = read_name(m, ml, pos, nullptr);
     if (cc < 0 || pos + cc + 10 > ml) break;
     pos += cc;
     const int type = be16(m + pos), rdlen = be16(m + pos + 8);
     pos += 10;
     if (pos + rdlen > ml) break;
     if (type == 1 && rdlen == 4) {
-      char buf[20];
-      std::snprintf(buf, sizeof buf, "%u.%u.%u.%u", m[pos], m[pos + 1], m[pos + 2], m[pos + 3]);
-      if (!answers.empty()) answers.push_back(',');
-      answers += buf;
+      if (r->as.size() > a0) r->as.push_back(',');
+      put_ipv4(&r->as, m + pos);
     }
     pos += rdlen;
   }
@@ -286,9 +304,7 @@ void parse_dns(const uint8_t* m, size_t ml, int64_t ts_ns, uint32_t origlen, uin
   r->qtype.push_back(qtype);
   r->qclass.push_back(qclass);
   r->rcode.push_back(flags & 0x000F);
-  r->names += name;
   r->name_end.push_back((int64_t)r->names.size());
-  r->as += answers;
   r->a_end.push_back((int64_t)r->as.size());
   r->pkt.push_back(pkt);
 }
@@ -437,8 +453,8 @@ void reassemble(std::vector<Frag>& fr, Rows* r) {
 }
 
 struct Handle {
-  Rows all;
-  int64_t packets = 0;
+  std::vector<Rows> parts;  // per-thread rows in packet order (one part after a reassembly pass)
+  int64_t packets = 0, rows = 0, name_bytes = 0, a_bytes = 0, tcp_partial = 0, frag_incomplete = 0;
   std::string err;
 };
 
@@ -455,32 +471,42 @@ ONI_NATIVE_API void* oni_pcap_dns_open(const char* path, int threads) {
   fstat(fd, &st);
   const size_t n = (size_t)st.st_size;
   const uint8_t* b = nullptr;
-  if (n) b = (const uint8_t*)mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
+  // MAP_POPULATE: the file is read whole anyway; prefaulting beats 4 KB demand faults in the
+  // sequential index pass
+  if (n) b = (const uint8_t*)mmap(nullptr, n, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
   std::vector<Pkt> pk;
   if (b && b != MAP_FAILED && index_pcap(b, n, &pk, &h->err)) {
     h->packets = (int64_t)pk.size();
     const int T = threads > 0 ? threads : omp_get_max_threads();
-    std::vector<Rows> loc(T);
+    std::vector<Rows>& loc = h->parts;
+    loc.resize(T);
 #pragma omp parallel for num_threads(T) schedule(static, 1)
     for (int t = 0; t < T; ++t) {
       const size_t lo = pk.size() * (size_t)t / T, hi = pk.size() * (size_t)(t + 1) / T;
       for (size_t i = lo; i < hi; ++i) decode(b, pk[i], (int64_t)i, &loc[t]);
     }
-    Rows& a = h->all;
     std::vector<Frag> frags;
-    for (auto& r : loc) {
-      append_rows(a, r);
+    for (auto& r : loc)
       for (auto& f : r.frags) frags.push_back(std::move(f));
-    }
     if (!frags.empty()) {  // serial pass: fragments of one datagram may sit in different chunks
       Rows re;
       reassemble(frags, &re);
       if (!re.ts_ns.empty()) {
+        Rows a;
+        for (auto& r : loc) append_rows(a, r);
         append_rows(a, re);
-        a = packet_order(a);
+        loc.clear();
+        loc.push_back(packet_order(a));
       } else {
-        a.frag_incomplete += re.frag_incomplete;
+        loc[0].frag_incomplete += re.frag_incomplete;
       }
+    }
+    for (auto& r : loc) {
+      h->rows += (int64_t)r.ts_ns.size();
+      h->name_bytes += (int64_t)r.names.size();
+      h->a_bytes += (int64_t)r.as.size();
+      h->tcp_partial += r.tcp_partial;
+      h->frag_incomplete += r.frag_incomplete;
     }
   }
   if (b && b != MAP_FAILED) munmap((void*)b, n);
@@ -491,40 +517,55 @@ ONI_NATIVE_API void* oni_pcap_dns_open(const char* path, int threads) {
 ONI_NATIVE_API int oni_pcap_dns_sizes(void* hp, int64_t* rows, int64_t* name_bytes, int64_t* a_bytes,
                                       int64_t* packets) {
   auto* h = (Handle*)hp;
-  *rows = (int64_t)h->all.ts_ns.size();
-  *name_bytes = (int64_t)h->all.names.size();
-  *a_bytes = (int64_t)h->all.as.size();
+  *rows = h->rows;
+  *name_bytes = h->name_bytes;
+  *a_bytes = h->a_bytes;
   *packets = h->packets;
   return h->err.empty() ? 0 : 1;
 }
 
+// columns of every part copied straight into the caller's arrays, parts in parallel
 ONI_NATIVE_API int oni_pcap_dns_fetch(void* hp, int64_t* ts_ns, int32_t* frame_len, uint32_t* ip_src, uint32_t* ip_dst,
                                       int32_t* qtype, int32_t* qclass, int32_t* rcode, int64_t* name_off,
                                       uint8_t* names, int64_t* a_off, uint8_t* as) {
   auto* h = (Handle*)hp;
-  const Rows& a = h->all;
-  const size_t n = a.ts_ns.size();
-  std::memcpy(ts_ns, a.ts_ns.data(), n * 8);
-  std::memcpy(frame_len, a.frame_len.data(), n * 4);
-  std::memcpy(ip_src, a.ip_src.data(), n * 4);
-  std::memcpy(ip_dst, a.ip_dst.data(), n * 4);
-  std::memcpy(qtype, a.qtype.data(), n * 4);
-  std::memcpy(qclass, a.qclass.data(), n * 4);
-  std::memcpy(rcode, a.rcode.data(), n * 4);
+  const size_t P = h->parts.size();
+  std::vector<int64_t> r0(P + 1, 0), n0(P + 1, 0), b0(P + 1, 0);
+  for (size_t p = 0; p < P; ++p) {
+    r0[p + 1] = r0[p] + (int64_t)h->parts[p].ts_ns.size();
+    n0[p + 1] = n0[p] + (int64_t)h->parts[p].names.size();
+    b0[p + 1] = b0[p] + (int64_t)h->parts[p].as.size();
+  }
   name_off[0] = 0;
   a_off[0] = 0;
-  std::memcpy(name_off + 1, a.name_end.data(), n * 8);
-  std::memcpy(a_off + 1, a.a_end.data(), n * 8);
-  std::memcpy(names, a.names.data(), a.names.size());
-  std::memcpy(as, a.as.data(), a.as.size());
+#pragma omp parallel for schedule(static, 1)
+  for (size_t p = 0; p < P; ++p) {
+    const Rows& a = h->parts[p];
+    const size_t n = a.ts_ns.size(), o = (size_t)r0[p];
+    if (n) {
+      std::memcpy(ts_ns + o, a.ts_ns.data(), n * 8);
+      std::memcpy(frame_len + o, a.frame_len.data(), n * 4);
+      std::memcpy(ip_src + o, a.ip_src.data(), n * 4);
+      std::memcpy(ip_dst + o, a.ip_dst.data(), n * 4);
+      std::memcpy(qtype + o, a.qtype.data(), n * 4);
+      std::memcpy(qclass + o, a.qclass.data(), n * 4);
+      std::memcpy(rcode + o, a.rcode.data(), n * 4);
+      for (size_t i = 0; i < n; ++i) {
+        name_off[o + i + 1] = a.name_end[i] + n0[p];
+        a_off[o + i + 1] = a.a_end[i] + b0[p];
+      }
+    }
+    if (!a.names.empty()) std::memcpy(names + n0[p], a.names.data(), a.names.size());
+    if (!a.as.empty()) std::memcpy(as + b0[p], a.as.data(), a.as.size());
+  }
   return 0;
 }
 
 // decoder counters: [0] TCP messages split across segments (skipped), [1] incomplete IPv4 datagrams
 ONI_NATIVE_API int oni_pcap_dns_stats(void* hp, int64_t* out) {
   auto* h = (Handle*)hp;
-  out[0] = h->all.tcp_partial;
-  out[1] = h->all.frag_incomplete;
+  out[0] = h->tcp_partial;
+  out[1] = h->frag_incomplete;
   return 0;
 }
 

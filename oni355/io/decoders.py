@@ -369,17 +369,17 @@ def read_pcap_dns(path: str, threads: int = 0) -> dict:
         if rc != 0:
             raise OSError(f"cannot decode {path}")
         n = rows.value
-        ts = np.zeros(n, np.int64)
-        flen = np.zeros(n, np.int32)
-        src = np.zeros(n, np.uint32)
-        dst = np.zeros(n, np.uint32)
-        qt = np.zeros(n, np.int32)
-        qc = np.zeros(n, np.int32)
-        rc_ = np.zeros(n, np.int32)
-        noff = np.zeros(n + 1, np.int64)
-        names = np.zeros(max(nb.value, 1), np.uint8)
-        aoff = np.zeros(n + 1, np.int64)
-        aa = np.zeros(max(ab.value, 1), np.uint8)
+        ts = np.empty(n, np.int64)
+        flen = np.empty(n, np.int32)
+        src = np.empty(n, np.uint32)
+        dst = np.empty(n, np.uint32)
+        qt = np.empty(n, np.int32)
+        qc = np.empty(n, np.int32)
+        rc_ = np.empty(n, np.int32)
+        noff = np.empty(n + 1, np.int64)
+        names = np.empty(max(nb.value, 1), np.uint8)
+        aoff = np.empty(n + 1, np.int64)
+        aa = np.empty(max(ab.value, 1), np.uint8)
         L.oni_pcap_dns_fetch(h, *(x.ctypes.data for x in (ts, flen, src, dst, qt, qc, rc_, noff, names, aoff, aa)))
         st = np.zeros(2, np.int64)
         L.oni_pcap_dns_stats(h, st.ctypes.data)
