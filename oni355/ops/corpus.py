@@ -18,6 +18,8 @@ from . import _lib
 vp, i64, ci = C.c_void_p, C.c_int64, C.c_int
 _SZ = C.POINTER(C.c_size_t)
 _lib.register_optional("oni_dict_encode", [vp, i64, ci, vp, vp, vp, vp, vp, vp, _SZ, vp])
+_lib.register_optional("oni_hashdict_build", [vp, i64, i64, vp, vp, vp, vp, vp])
+_lib.register_optional("oni_hashdict_finish", [vp, i64, ci, i64, vp, vp, vp, i64, vp, vp, vp, _SZ, vp])
 _lib.register_optional("oni_route_pack", [vp, vp, vp, vp, vp, i64, ci, vp, vp, vp, vp, _SZ, vp])
 _lib.register_optional("oni_pair_build", [vp, vp, vp, i64, i64, i64, vp, vp, vp, vp, vp, vp, i64, vp, _SZ, vp])
 _lib.register_optional("oni_doc_layout", [vp, vp, i64, i64, ci, vp, vp, vp, vp, vp, vp, vp, _SZ, vp])
@@ -41,8 +43,37 @@ def _p(t):
     return _lib.ptr(t)
 
 
+HASH_DICT = True  # tests flip this to compare the two dictionary paths
+
+
 def bits_for(maxv: int) -> int:
     return max(int(maxv).bit_length(), 1)
+
+
+HASH_DICT_MIN_KEYS = 1 << 20   # below this the sort path is as fast
+HASH_DICT_SLOTS = 1 << 22      # open-addressing table (48 MB): up to 2M distinct keys
+
+
+def dict_encode_hash(keys64: torch.Tensor, key_bits: int, table_slots: int = HASH_DICT_SLOTS):
+    """Hash-table dictionary (csrc/kernels/hashdict.hip): identical output to the sort path, or
+    None when the keys have too many distinct values for the table."""
+    n = keys64.numel()
+    dev = keys64.device
+    M = int(table_slots)
+    tab = torch.empty(M, dtype=torch.int64, device=dev)
+    val = torch.empty(M, dtype=torch.int32, device=dev)
+    uns = torch.empty(M // 2 + 1, dtype=torch.int64, device=dev)
+    status = torch.zeros(3, dtype=torch.int32, device=dev)
+    _lib.check(_lib.lib().oni_hashdict_build(_p(keys64), n, M, _p(tab), _p(val), _p(uns), _p(status), _lib.stream()),
+               "oni_hashdict_build")
+    nu, ovf, _ = (int(x) for x in status.tolist())
+    if ovf or nu > M // 2:
+        return None
+    uniq = torch.empty(max(nu, 1), dtype=torch.int64, device=dev)
+    ids = torch.empty(n, dtype=torch.int32, device=dev)
+    _call("oni_hashdict_finish", _p(keys64), n, int(min(max(key_bits, 1), 64)), M, _p(tab), _p(val), _p(uns), nu,
+          _p(uniq), _p(ids))
+    return uniq[:nu], ids
 
 
 def dict_encode(keys64: torch.Tensor, key_bits: int = 64, weights: torch.Tensor | None = None,
@@ -50,10 +81,15 @@ def dict_encode(keys64: torch.Tensor, key_bits: int = 64, weights: torch.Tensor 
     """Sorted unique keys (int64) and the int32 id of every key (``torch.unique(return_inverse)``).
 
     ``counts=True`` also returns Σ weights (int64; 1 per key without ``weights``) of every unique
-    key, read off the sorted runs (``torch.unique(return_counts)`` with weights)."""
+    key, read off the sorted runs (``torch.unique(return_counts)`` with weights). Large inputs of
+    keys below 2^63 take the hash-table path (:func:`dict_encode_hash`) first."""
     if keys64.dtype != torch.int64 or not keys64.is_contiguous():
         raise TypeError("dict_encode: contiguous int64 keys")
     n = keys64.numel()
+    if not counts and n >= HASH_DICT_MIN_KEYS and key_bits <= 62 and HASH_DICT:
+        r = dict_encode_hash(keys64, key_bits)
+        if r is not None:
+            return r
     if weights is not None and (weights.dtype != torch.int32 or weights.numel() != n):
         raise TypeError("dict_encode: weights must be int32 [n]")
     dev = keys64.device

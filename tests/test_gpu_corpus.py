@@ -124,3 +124,23 @@ def test_route_pack_is_stable_owner_partition(gpu, n, W, weighted):
     assert torch.equal(counts.cpu(), torch.bincount(tok_own, minlength=W))
     cols = [common.i64_to_u32bits(keys[ref_order]), word[ref_order]] + ([wt[ref_order]] if weighted else [])
     assert torch.equal(send.cpu(), torch.stack(cols, 1))
+
+
+@pytest.mark.parametrize("n,distinct,bits", [(1 << 20, 6000, 30), (3_000_001, 400_000, 32), (2_000_000, 3, 8),
+                                             (1_500_000, 1_400_000, 40), (25_000_000, 5733, 29)])
+def test_hash_dictionary_equals_sort_path(gpu, n, distinct, bits):
+    """The hash-table dictionary (hashdict.hip) == the radix-sort dictionary, bitwise, incl. Zipf
+    hot keys; a key set too large for the table falls back to the sort path."""
+    r = np.random.default_rng(n)
+    table = np.unique(r.integers(0, 2 ** bits, distinct * 2, dtype=np.int64))[:distinct]
+    p = 1.0 / np.arange(1, table.size + 1) ** 1.1
+    keys = torch.from_numpy(table[r.choice(table.size, n, p=p / p.sum())]).to(gpu).contiguous()
+    oc.HASH_DICT = False
+    try:
+        su, si = oc.dict_encode(keys, bits)
+    finally:
+        oc.HASH_DICT = True
+    hu, hi = oc.dict_encode(keys, bits)
+    assert torch.equal(su, hu) and torch.equal(si, hi)
+    small = oc.dict_encode_hash(keys, bits, table_slots=1 << 10)
+    assert (small is None) == (int(su.numel()) > (1 << 9))
