@@ -20,6 +20,7 @@ constexpr int kB = 256;
 constexpr uint64_t kEmpty = ~0ull;  // never a key: word keys < 2^62, document keys < 2^32 (the build rejects nothing: a key
                                     // equal to it would be dropped, so callers pass keys < 2^63)
 constexpr int kLSlots = 2048;       // block-local LDS set (16 KB)
+constexpr int kLProbe = 8;          // LDS probe limit
 constexpr int kPerThread = 16;      // keys per thread in the insert pass
 constexpr int kMaxProbe = 4096;
 
@@ -56,7 +57,9 @@ __global__ __launch_bounds__(kB) void k_hd_insert(const uint64_t* __restrict__ k
     const unsigned long long k = keys[i];
     bool fresh = true;
     uint32_t h = mix(k) & (kLSlots - 1);
-    for (int p = 0; p < kLSlots; ++p) {
+    // short local probe chains: with more distinct keys than the LDS set holds (documents) the
+    // set fills up, and a key not found nearby simply goes to the global table
+    for (int p = 0; p < kLProbe; ++p) {
       const unsigned long long old = atomicCAS(&ls[h], (unsigned long long)kEmpty, k);
       if (old == kEmpty) break;           // first sighting in this block
       if (old == k) {                     // seen by this block already

@@ -77,16 +77,18 @@ def dict_encode_hash(keys64: torch.Tensor, key_bits: int, table_slots: int = HAS
 
 
 def dict_encode(keys64: torch.Tensor, key_bits: int = 64, weights: torch.Tensor | None = None,
-                counts: bool = False):
+                counts: bool = False, hashed: bool = False):
     """Sorted unique keys (int64) and the int32 id of every key (``torch.unique(return_inverse)``).
 
     ``counts=True`` also returns Σ weights (int64; 1 per key without ``weights``) of every unique
-    key, read off the sorted runs (``torch.unique(return_counts)`` with weights). Large inputs of
-    keys below 2^63 take the hash-table path (:func:`dict_encode_hash`) first."""
+    key, read off the sorted runs (``torch.unique(return_counts)`` with weights). ``hashed``: large
+    inputs of keys below 2^63 try the hash-table path (:func:`dict_encode_hash`) first -- a win for
+    few distinct keys (the word vocabulary: 2.06 -> 1.01 ms at 25M keys / 5.7k words), a loss for
+    many (IP documents: 370k distinct, the sort path stays 1.6 ms faster)."""
     if keys64.dtype != torch.int64 or not keys64.is_contiguous():
         raise TypeError("dict_encode: contiguous int64 keys")
     n = keys64.numel()
-    if not counts and n >= HASH_DICT_MIN_KEYS and key_bits <= 62 and HASH_DICT:
+    if hashed and not counts and n >= HASH_DICT_MIN_KEYS and key_bits <= 62 and HASH_DICT:
         r = dict_encode_hash(keys64, key_bits)
         if r is not None:
             return r

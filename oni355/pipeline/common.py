@@ -41,7 +41,7 @@ def encode_words(word_keys64: torch.Tensor, comm: Comm | None, key_bits: int = 6
     and local ids are remapped through the (small) local-unique → global table."""
     if word_keys64.is_cuda:
         from ..ops import corpus as oc
-        luniq, lids = oc.dict_encode(word_keys64.contiguous(), key_bits)
+        luniq, lids = oc.dict_encode(word_keys64.contiguous(), key_bits, hashed=True)
     else:
         luniq, inv = torch.unique(word_keys64, return_inverse=True)
         lids = inv.to(torch.int32)

@@ -140,7 +140,7 @@ def test_hash_dictionary_equals_sort_path(gpu, n, distinct, bits):
         su, si = oc.dict_encode(keys, bits)
     finally:
         oc.HASH_DICT = True
-    hu, hi = oc.dict_encode(keys, bits)
+    hu, hi = oc.dict_encode(keys, bits, hashed=True)
     assert torch.equal(su, hu) and torch.equal(si, hi)
     small = oc.dict_encode_hash(keys, bits, table_slots=1 << 10)
     assert (small is None) == (int(su.numel()) > (1 << 9))
