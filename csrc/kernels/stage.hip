@@ -64,9 +64,96 @@ void par_memcpy(void* dst, const void* src, size_t n, int threads) {
   for (auto& w : ws) w.join();
 }
 
+// Copy-engine-free upload: the CUs pull page-locked host memory over PCIe. A bulk hipMemcpyAsync
+// occupies the DMA engine, and every later small transfer in either direction -- a histogram
+// read-back, a .item(), a count upload before an all-to-all -- queues behind it
+// (bench/overlap_probe.py: a 32 KB D2H waits 11 ms behind a 550 MB upload; kernels, graph
+// replays, D2D copies and RCCL collectives do not). Pulling with a few workgroups leaves the DMA
+// engine to those small transfers. 4 × 16 B loads per thread in flight; stores bypass L2 residency.
+constexpr int kPullThreads = 256;
+constexpr int kPullUnroll = 4;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(kPullThreads) void k_pull(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                       int64_t n16) {
+  const int64_t stride = (int64_t)gridDim.x * kPullThreads * kPullUnroll;
+  for (int64_t base = (int64_t)blockIdx.x * kPullThreads * kPullUnroll + threadIdx.x; base < n16; base += stride) {
+    u32x4 v[kPullUnroll];
+#pragma unroll
+    for (int u = 0; u < kPullUnroll; ++u) {
+      const int64_t i = base + (int64_t)u * kPullThreads;
+      if (i < n16) v[u] = src[i];
+    }
+#pragma unroll
+    for (int u = 0; u < kPullUnroll; ++u) {
+      const int64_t i = base + (int64_t)u * kPullThreads;
+      if (i < n16) __builtin_nontemporal_store(v[u], dst + i);
+    }
+  }
+}
+
+__global__ void k_pull_tail(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int n) {
+  if ((int)threadIdx.x < n) dst[threadIdx.x] = src[threadIdx.x];
+}
+
+// Device → page-locked host words written by a kernel (the read-back twin of k_pull): small
+// values the host polls during a run (the sampler's changed-token count) do not wait behind a
+// bulk upload on the DMA engine. One vector store per word, then a system-scope fence.
+__global__ void k_push_words(const uint32_t* __restrict__ src, uint32_t* dst, int n) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i < n) {
+    __builtin_nontemporal_store(src[i], dst + i);
+    __threadfence_system();
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+// Copy `words` 32-bit words from device `src` into page-locked host memory `host_dst` on `stream`
+// with a kernel. The host reads them after an event recorded behind this call has completed.
+// hipErrorInvalidValue when `host_dst` is not device-visible pinned memory.
+int oni_d2h_push(const void* src, void* host_dst, int64_t words, hipStream_t stream) {
+  if (words <= 0) return 0;
+  if (words > (int64_t)1 << 24) return (int)hipErrorInvalidValue;
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, host_dst, 0) != hipSuccess || d == nullptr) {
+    (void)hipGetLastError();
+    return (int)hipErrorInvalidValue;
+  }
+  const int n = (int)words;
+  k_push_words<<<(n + 255) / 256, 256, 0, stream>>>(static_cast<const uint32_t*>(src), static_cast<uint32_t*>(d), n);
+  return (int)hipGetLastError();
+}
+
+// Upload `bytes` from page-locked host memory `src` (hipHostMalloc / torch pin_memory) to `dst` on
+// `stream` with `blocks` workgroups (0 → 64) instead of the DMA engine. Asynchronous like
+// hipMemcpyAsync. Returns hipErrorInvalidValue when `src` is not device-visible pinned memory (the
+// caller then uses hipMemcpyAsync).
+int oni_h2d_pull(const void* src, void* dst, int64_t bytes, int blocks, hipStream_t stream) {
+  if (bytes <= 0) return 0;
+  void* dsrc = nullptr;
+  if (hipHostGetDevicePointer(&dsrc, const_cast<void*>(src), 0) != hipSuccess || dsrc == nullptr) {
+    (void)hipGetLastError();
+    return (int)hipErrorInvalidValue;
+  }
+  const bool aligned = ((uintptr_t)dsrc % 16 == 0) && ((uintptr_t)dst % 16 == 0);
+  if (!aligned && bytes > 4096) return (int)hipErrorInvalidValue;  // caller falls back to the DMA copy
+  const int64_t n16 = aligned ? bytes / 16 : 0;
+  const int64_t done = n16 * 16;
+  if (n16 > 0) {
+    const int64_t per_block = (int64_t)kPullThreads * kPullUnroll;
+    const int64_t need = (n16 + per_block - 1) / per_block;
+    const int grid = (int)std::min<int64_t>(need, blocks > 0 ? blocks : 64);
+    k_pull<<<grid, kPullThreads, 0, stream>>>(static_cast<const u32x4*>(dsrc), static_cast<u32x4*>(dst), n16);
+  }
+  for (int64_t off = done; off < bytes; off += 256) {  // remainder (< 16 B, or a small unaligned buffer)
+    const int n = (int)std::min<int64_t>(256, bytes - off);
+    k_pull_tail<<<1, 256, 0, stream>>>(static_cast<const uint8_t*>(dsrc) + off, static_cast<uint8_t*>(dst) + off, n);
+  }
+  return (int)hipGetLastError();
+}
 
 // Create a ring of `nbuf` pinned buffers of `chunk_bytes`; `threads` host threads fill each one.
 // Returns 0 on success, the hipError otherwise; *out receives the handle.

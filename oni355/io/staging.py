@@ -35,6 +35,16 @@ _lib.register_optional("oni_stager_sync", [vp])
 _lib.register_optional("oni_stager_stats", [vp, vp])
 _lib.register_optional("oni_stager_destroy", [vp])
 _lib.register_optional("oni_h2d_registered", [vp, vp, i64, vp])
+_lib.register_optional("oni_h2d_pull", [vp, vp, i64, C.c_int, vp])
+_lib.register_optional("oni_d2h_push", [vp, vp, i64, vp])
+
+# Prefetcher uploads: "dma" (hipMemcpyAsync) or "pull" (CUs read the pinned host buffers and the
+# DMA engine stays free). Measured (bench/overlap_probe.py, profiles/r2_copy_overlap_probe.txt):
+# behind a 550 MB DMA upload, kernels / graph replays / D2D / RCCL on the compute stream run at
+# full speed and only small H2D/D2H transfers wait; behind the pull kernel every kernel waits.
+# So "dma" is the default and the run avoids DMA transfers while an upload is in flight.
+PREFETCH_COPY = os.environ.get("ONI_PREFETCH_COPY", "dma")
+PULL_BLOCKS = int(os.environ.get("ONI_PULL_BLOCKS", "64"))
 
 CHUNK_BYTES = int(os.environ.get("ONI_STAGE_CHUNK_MB", "32")) << 20
 N_BUF = 3
@@ -96,6 +106,40 @@ def upload(a, device, dtype: torch.dtype | None = None) -> torch.Tensor:
     return upload_tensor(t, device)
 
 
+def pull_upload(src: torch.Tensor, device, stream=None, blocks: int = PULL_BLOCKS) -> torch.Tensor:
+    """Pinned CPU tensor → device tensor copied by a kernel (``oni_h2d_pull``) on ``stream``
+    (default: the current stream), not by the DMA engine. Falls back to a non-blocking DMA copy
+    when the source is not device-visible pinned memory."""
+    device = torch.device(device)
+    out = torch.empty(src.shape, dtype=src.dtype, device=device)
+    nbytes = src.numel() * src.element_size()
+    if nbytes == 0:
+        return out
+    st = stream if stream is not None else torch.cuda.current_stream(device)
+    rc = _lib.lib().oni_h2d_pull(src.data_ptr(), out.data_ptr(), nbytes, int(blocks), st.cuda_stream) \
+        if src.is_pinned() else -1
+    if rc != 0:
+        with torch.cuda.stream(st):
+            out.copy_(src, non_blocking=True)
+    return out
+
+
+def push_to_host(src: torch.Tensor, dst: torch.Tensor) -> None:
+    """Queue a copy of the 4-byte-element device tensor ``src`` into the pinned CPU tensor ``dst``
+    by a kernel on the current stream (``oni_d2h_push``), so a small read-back does not queue
+    behind a bulk upload on the DMA engine. Read ``dst`` after an event recorded behind this call
+    has completed. Falls back to a non-blocking DMA copy."""
+    if src.element_size() != 4 or dst.element_size() != 4 or src.numel() != dst.numel():
+        raise ValueError("push_to_host: 4-byte elements of equal count")
+    src = src.contiguous()
+    rc = -1
+    if dst.is_pinned() and dst.is_contiguous():
+        rc = _lib.lib().oni_d2h_push(src.data_ptr(), dst.data_ptr(), src.numel(),
+                                     torch.cuda.current_stream(src.device).cuda_stream)
+    if rc != 0:
+        dst.copy_(src, non_blocking=True)
+
+
 def sync() -> None:
     """Block until every queued chunk has landed."""
     if _handle is not None:
@@ -118,11 +162,20 @@ class Prefetcher:
     A loader that owns pinned host buffers (:meth:`pin`, done once per buffer) submits day k+1
     while day k trains; :meth:`take` makes the compute stream wait for the copies (an event, no
     host sync) and hands the tensors over. Each submitted day is a full upload; only its timing
-    overlaps. ``copy_ms()`` reports the device time of the last completed upload."""
+    overlaps. ``copy_ms()`` reports the device time of the last completed upload.
+
+    The copy stream is high priority: with a default-priority stream (and a process group
+    initialised) every small read-back or upload of the day being computed -- quantile histograms,
+    all-to-all counts, ``.item()`` -- waited for the whole 550 MB upload (10 ms of a forced 1-rank
+    day, ``bench/featurize_probe.py``). The sampler's own polling read-back is a kernel store
+    (:func:`push_to_host`) either way."""
 
     def __init__(self, device):
         self.device = torch.device(device)
-        self.stream = torch.cuda.Stream(self.device)
+        # a high-priority stream gets its own hardware queue: with a process group initialised, a
+        # default-priority copy stream made every small H2D/D2H of the compute stream wait for the
+        # whole upload (bench/featurize_probe.py: 10.2 ms → 0.06 ms per read-back)
+        self.stream = torch.cuda.Stream(self.device, priority=int(os.environ.get("ONI_PREFETCH_PRIORITY", "-1")))
         self._pending = None
         self._last = None
 
@@ -145,7 +198,10 @@ class Prefetcher:
         with torch.cuda.stream(self.stream):
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record(self.stream)
-            out = {k: t.to(self.device, non_blocking=True) for k, t in pinned.items()}
+            if PREFETCH_COPY == "pull":
+                out = {k: pull_upload(t, self.device, self.stream) for k, t in pinned.items()}
+            else:
+                out = {k: t.to(self.device, non_blocking=True) for k, t in pinned.items()}
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record(self.stream)
         self._pending = (out, e0, e1)

@@ -231,8 +231,9 @@ class GibbsLDA:
             return
         src = self.dn[1 - self.b][self._aux_off:self._aux_off + 1]
         if self.device.type == "cuda":
+            from ..io import staging
             buf = torch.empty(1, dtype=torch.int32, pin_memory=True)
-            buf.copy_(src, non_blocking=True)
+            staging.push_to_host(src, buf)  # a kernel store: not queued behind a bulk H2D upload
             ev = torch.cuda.Event()
             ev.record()
         else:

@@ -120,11 +120,17 @@ def quantile_cuts(keys: torch.Tensor, fracs, allreduce=None, n_global: int | Non
             hist.zero_()
             _lib.check(L.oni_radix_hist(_lib.ptr(keys), keys.numel(), shift, nbits, _lib.ptr(pre_t), P, mask,
                                         _lib.ptr(hist), _lib.stream()), "oni_radix_hist")
-            h = hist.cpu().numpy().view(np.uint32).astype(np.int64).reshape(P, B)
+            if allreduce is not None and getattr(allreduce, "accepts_tensors", False):
+                # X03 on the device histogram (int64: a bin's global count may pass 2^31)
+                h = np.asarray(allreduce(hist.to(torch.int64) & 0xFFFFFFFF), dtype=np.int64).reshape(P, B)
+            else:
+                h = hist.cpu().numpy().view(np.uint32).astype(np.int64).reshape(P, B)
+                if allreduce is not None:
+                    h = np.asarray(allreduce(h), dtype=np.int64).reshape(P, B)
         else:
             h = spec.radix_hist(knp, shift, nbits, uniq.astype(np.uint32), mask)
-        if allreduce is not None:
-            h = np.asarray(allreduce(h), dtype=np.int64).reshape(P, B)
+            if allreduce is not None:
+                h = np.asarray(allreduce(h), dtype=np.int64).reshape(P, B)
         cum = np.cumsum(h, axis=1)
         for qi in range(len(fracs)):
             c = cum[inv[qi]]

@@ -51,18 +51,36 @@ class Comm:
         return t
 
     def allreduce_np(self, a) -> np.ndarray:
+        """Sum over ranks → host array. ``a``: a host array, or a device tensor (reduced where it
+        lives -- no host→device copy; the caller's tensor is left unchanged)."""
+        if torch.is_tensor(a):
+            if not self.dist:
+                return a.cpu().numpy()
+            t = a.to(self._coll_device, copy=True)
+            dist.all_reduce(t, group=self.group)
+            return t.cpu().numpy()
         a = np.asarray(a)
         if not self.dist:
             return a
         # a private copy: on CPU collectives torch.from_numpy would alias (and reduce into) ``a``
-        t = torch.from_numpy(np.array(a, copy=True)).to(self._coll_device)
+        t = self._small_tensor(a) if a.size == 1 else torch.from_numpy(np.array(a, copy=True)).to(self._coll_device)
         dist.all_reduce(t, group=self.group)
-        return t.cpu().numpy()
+        return t.cpu().numpy().reshape(a.shape)
+
+    allreduce_np.accepts_tensors = True  # quantile_cuts hands it device histograms
+
+    def _small_tensor(self, a) -> torch.Tensor:
+        """A 1-element collective buffer written by a fill kernel rather than a host→device copy:
+        while the next day's columns stream in on the copy engine (io.staging.Prefetcher) a small
+        pageable upload queues behind them (measured: ~10 ms of a forced 1-rank day)."""
+        a = np.asarray(a)
+        return torch.full((1,), a.reshape(-1)[0].item(), dtype=torch.from_numpy(a[:0].reshape(0)).dtype,
+                          device=self._coll_device)
 
     def allreduce_scalar(self, x: float, op: str = "sum") -> float:
         if not self.dist:
             return float(x)
-        t = torch.tensor([float(x)], dtype=torch.float64, device=self._coll_device)
+        t = torch.full((1,), float(x), dtype=torch.float64, device=self._coll_device)
         dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
                                "min": dist.ReduceOp.MIN}[op], group=self.group)
         return float(t.item())
@@ -100,7 +118,7 @@ class Comm:
             return [t]
         if self._via_host and t.is_cuda:
             return [o.to(self.device) for o in self._host_view().allgather_var(t.cpu())]
-        n = torch.tensor([t.shape[0]], dtype=torch.int64, device=self.device)
+        n = torch.full((1,), t.shape[0], dtype=torch.int64, device=self.device)
         ns = [torch.zeros_like(n) for _ in range(self.world)]
         dist.all_gather(ns, n, group=self.group)
         sizes = [int(x.item()) for x in ns]

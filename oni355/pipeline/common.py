@@ -231,7 +231,8 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
                     vocab: torch.Tensor, K: int, alpha: float | None, beta: float, seed: int, sweeps: int,
                     chunk_len: int, comm: Comm | None, eval_every: int = 0, burnin: int = 0, ckpt=None, log=None,
                     train: bool = True, timer: StageTimer | None = None, ldac_dir: str | None = None,
-                    ldac_lag: int = 0, word_ids: torch.Tensor | None = None, n_event0: int = 0) -> LdaRun:
+                    ldac_lag: int = 0, word_ids: torch.Tensor | None = None, n_event0: int = 0,
+                    on_train=None) -> LdaRun:
     """Token keys → owner routing → local corpus → Gibbs LDA trained for ``sweeps`` sweeps.
 
     ``word_ids`` (int32, from :func:`encode_words`) skips the vocabulary lookup of ``word_keys64``.
@@ -241,7 +242,10 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
     ``ldac_lag`` sweeps (oni-lda-c's LAG); ``final.*`` is written by the caller.
     ``burnin``: sweeps before the chain is considered mixed -- the ``eval_every`` likelihood trace
     and the LAG snapshots only sample sweeps after it (BURNIN in duxbay.conf / ``burnin`` in the
-    lda-c settings file); θ/φ always come from the final sweep."""
+    lda-c settings file); θ/φ always come from the final sweep.
+    ``on_train()`` is called as the sweeps start (e.g. to queue the next day's upload on a copy
+    stream: training needs no host↔device transfers, while the collectives of the earlier stages
+    would wait behind a bulk copy on the DMA engine)."""
     dev = doc_keys64.device
     timer = timer or StageTimer(dev)
     dist_on = comm is not None and comm.dist
@@ -279,6 +283,8 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
         else:
             model.initialize()
     with timer.stage("train"):
+        if on_train is not None:
+            on_train()
         remaining = sweeps - model.sweeps_done
         step = eval_every if eval_every > 0 else remaining
         ck_every = ckpt.every if ckpt is not None and ckpt.every > 0 else 0

@@ -162,10 +162,11 @@ def run_flow(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxre
              alpha: float | None = None, beta: float = 0.01, seed: int = 0x0D15EA5E, chunk_len: int = 0,
              device="cpu", comm: Comm | None = None, feedback: dict | None = None, dupfactor: int = 1000,
              row_offset: int = 0, eval_every: int = 0, burnin: int = 0, ckpt=None, log=None, ldac_dir: str | None = None,
-             ldac_lag: int = 0, device_cols: dict | None = None) -> FlowResult:
+             ldac_lag: int = 0, device_cols: dict | None = None, on_train=None) -> FlowResult:
     """Full suspicious-connects for one (rank-local shard of a) day of flows. ``device_cols``:
     the day's :data:`DEVICE_COLS` already on the device (e.g. from io.staging.Prefetcher, which
-    uploaded them while the previous day computed); ``cols`` still supplies the host rows."""
+    uploaded them while the previous day computed); ``cols`` still supplies the host rows.
+    ``on_train``: see :func:`common.build_and_train`."""
     timer = StageTimer(device)
     if device_cols is None:
         cols, feedback = with_ipv6_keys(cols, comm, (feedback,)) if feedback else (with_ipv6_keys(cols, comm), None)
@@ -188,7 +189,7 @@ def run_flow(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxre
         vocab, wids = common.encode_words(word_keys, comm, key_bits=32)
     run = common.build_and_train(doc_keys, None, weights, vocab, K, alpha, beta, seed, sweeps, chunk_len, comm,
                                  eval_every=eval_every, burnin=burnin, ckpt=ckpt, log=log, timer=timer, ldac_dir=ldac_dir,
-                                 ldac_lag=ldac_lag, word_ids=wids, n_event0=n)
+                                 ldac_lag=ldac_lag, word_ids=wids, n_event0=n, on_train=on_train)
 
     # ---- scoring --------------------------------------------------------------------------------
     hist = torch.zeros(2048, dtype=torch.int32, device=d["sip"].device)

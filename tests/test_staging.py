@@ -47,3 +47,50 @@ def test_flow_to_device_staged_matches_plain(gpu, monkeypatch, m):
     want = flow.to_device(day.cols, gpu)
     for k in want:
         assert got[k].dtype == want[k].dtype and torch.equal(got[k], want[k]), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nbytes", [1, 15, 16, 4095, 4096 * 257 + 3, 64 << 20])
+def test_pull_upload_bitwise(gpu, nbytes):
+    """oni_h2d_pull (CUs read the pinned buffer, no DMA engine) == the source bytes; an unaligned
+    pinned view falls back to the DMA copy and is still exact."""
+    g = torch.Generator().manual_seed(nbytes)
+    src = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, generator=g).pin_memory()
+    out = staging.pull_upload(src, "cuda")
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu(), src)
+    if nbytes > 8192:
+        view = src[1:]  # 1-byte offset: not 16-B aligned
+        out2 = staging.pull_upload(view, "cuda")
+        torch.cuda.synchronize()
+        assert torch.equal(out2.cpu(), view)
+
+
+@pytest.mark.gpu
+def test_prefetcher_pull_matches_source(gpu):
+    cols = {"a": np.arange(1_000_003, dtype=np.int64), "b": np.arange(77, dtype=np.uint32)}
+    specs = {"a": torch.int64, "b": torch.int32}
+    pinned = staging.Prefetcher.pin(cols, specs)
+    pf = staging.Prefetcher("cuda")
+    pf.submit(pinned)
+    got = pf.take()
+    torch.cuda.synchronize()
+    assert torch.equal(got["a"].cpu(), torch.from_numpy(cols["a"]))
+    assert torch.equal(got["b"].cpu(), torch.from_numpy(cols["b"].view(np.int32)))
+    assert pf.copy_ms() >= 0
+
+
+@pytest.mark.gpu
+def test_push_to_host_kernel_readback(gpu):
+    src = torch.arange(-5, 1000, dtype=torch.int32, device="cuda") * 7
+    dst = torch.zeros(src.numel(), dtype=torch.int32, pin_memory=True)
+    staging.push_to_host(src, dst)
+    ev = torch.cuda.Event()
+    ev.record()
+    ev.synchronize()
+    assert torch.equal(dst, src.cpu())
+    f = torch.randn(33, device="cuda")
+    fd = torch.empty(33, pin_memory=True)
+    staging.push_to_host(f, fd)
+    torch.cuda.synchronize()
+    assert torch.equal(fd, f.cpu())
