@@ -54,7 +54,9 @@ def parse(argv=None):
     ap.add_argument("--from-pcap", action="store_true",
                     help="dns: every step decodes the shard's pcap file (config 3 'pcap→word pipeline')")
     ap.add_argument("--realistic-vocab", action="store_true",
-                    help="flow: long-tail service ports and wider bins (V ~ 1e5-1e6 words, SURVEY §7.5)")
+                    help="long-tail synthetic vocabulary (SURVEY §7.5 sizing): flow -- service ports and wider "
+                         "bins (V ~ 4e5); dns / proxy -- half the rows from the long tail of record types, "
+                         "rcodes, name shapes / methods, content types, statuses, user agents, URIs")
     ap.add_argument("--chunk-len", type=int, default=0, help="0 = auto (global token count)")
     ap.add_argument("--maxresults", type=int, default=3000)
     ap.add_argument("--seed", type=int, default=7)
@@ -145,10 +147,12 @@ def make_shard(a, comm):
                              wide_vocab=a.realistic_vocab)
     elif a.source == "dns":
         from oni355.synth.dns import generate_dns
-        day = generate_dns(per, seed=a.seed, rank=rank, n_clients=max(32, n_total // 40))
+        day = generate_dns(per, seed=a.seed, rank=rank, n_clients=max(32, n_total // 40),
+                           wide_vocab=0.5 if a.realistic_vocab else 0.0)
     else:
         from oni355.synth.proxy import generate_proxy
-        day = generate_proxy(per, seed=a.seed, rank=rank, n_clients=max(32, n_total // 40))
+        day = generate_proxy(per, seed=a.seed, rank=rank, n_clients=max(32, n_total // 40),
+                             wide_vocab=0.5 if a.realistic_vocab else 0.0)
     return day, per, n_total
 
 

@@ -63,9 +63,36 @@ def top_domain_list(n_extra: int = 2000, seed: int = 1) -> list[str]:
     return _POPULAR + _CDN + _MAIL + ["microsoft.com", "icloud.com", "app-measurement.com", "crashlytics.com"] + extra
 
 
+# long-tail record types / rcodes of a real resolver day (A, AAAA, PTR, MX, TXT, SRV, CNAME, NS, SOA,
+# HTTPS, SVCB, ANY, NULL, DS, DNSKEY, NAPTR, CAA, TLSA) with Zipf-like weights
+_WIDE_QTYPES = [1, 28, 12, 15, 16, 33, 5, 2, 6, 65, 64, 255, 10, 43, 48, 35, 257, 52]
+_WIDE_RCODES = [0, 3, 2, 5, 1, 4]
+_ALPHABETS = [b"abcdefghijklmnopqrstuvwxyz", b"0123456789abcdef", b"abcdefghijklmnopqrstuvwxyz0123456789-",
+              b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789"]
+
+
+def _wide_names(rng, m: int, domains: list[str]) -> list[str]:
+    """Names of every shape: 0-5 labels of 1-24 characters over alphabets of 16-62 symbols under a
+    Zipf-chosen registered domain (subdomain length / entropy / period quintiles all spread)."""
+    nlab = rng.integers(0, 6, size=m)
+    dz = 1.0 / np.arange(1, len(domains) + 1)
+    dsel = rng.choice(len(domains), size=m, p=dz / dz.sum())
+    alph = rng.integers(0, len(_ALPHABETS), size=m)
+    out = []
+    for j in range(m):
+        a = np.frombuffer(_ALPHABETS[alph[j]], dtype=np.uint8)
+        labs = [bytes(a[rng.integers(0, a.size, size=int(rng.integers(1, 25)))]).decode() for _ in range(nlab[j])]
+        out.append(".".join(labs + [domains[dsel[j]]]))
+    return out
+
+
 def generate_dns(n: int, seed: int = 5, n_clients: int | None = None, user_domain: str = "intel",
                  alpha_true: float = 0.1, n_anomalies: int | None = None, rank: int = 0,
-                 date_unix: int = 1467936000) -> DnsDay:
+                 date_unix: int = 1467936000, wide_vocab: float = 0.0) -> DnsDay:
+    """``wide_vocab``: fraction of (non-anomalous) rows drawn from the long tail instead of a
+    behaviour profile -- any of 18 record types and 6 rcodes, names of every shape under ~2000
+    domains, any hour -- which takes the day's vocabulary from ~4k words to ~1e5 (the sizing of
+    SURVEY.md §7.5)."""
     rng = np.random.default_rng([seed, rank])
     hrng = np.random.default_rng([seed, 0xD5])
     P = len(_PROFILES)
@@ -116,6 +143,16 @@ def generate_dns(n: int, seed: int = 5, n_clients: int | None = None, user_domai
             sv = rng.integers(0, len(_SERVICE), size=m)
             for j, i in enumerate(idx):
                 names[i] = f"{_SERVICE[sv[j]]}.{doms[dsel[j]]}"
+    if wide_vocab > 0:
+        wide = np.nonzero(rng.random(n) < wide_vocab)[0]
+        m = wide.size
+        qz = 1.0 / np.arange(1, len(_WIDE_QTYPES) + 1) ** 1.2
+        qtype[wide] = rng.choice(_WIDE_QTYPES, size=m, p=qz / qz.sum())
+        rz = np.array([0.8, 0.1, 0.05, 0.03, 0.015, 0.005])
+        rcode[wide] = rng.choice(_WIDE_RCODES, size=m, p=rz / rz.sum())
+        hour_f[wide] = rng.uniform(0, 24, size=m)
+        for i, nm in zip(wide.tolist(), _wide_names(rng, m, top_domain_list())):
+            names[i] = nm
     hour = np.mod(np.floor(hour_f), 24).astype(np.int64)
     # planted tunnelling / DGA
     anomaly_rows = np.sort(rng.choice(n, size=min(n_anomalies, n), replace=False))

@@ -51,8 +51,44 @@ class ProxyDay:
         return int(len(self.cols["clientip"]))
 
 
+_WIDE_METHODS = ["GET", "POST", "HEAD", "PUT", "OPTIONS", "CONNECT", "DELETE", "PATCH", "TRACE", "PROPFIND"]
+_WIDE_CTYPES = ["text/html", "text/plain", "text/css", "text/javascript", "image/png", "image/jpeg", "image/gif",
+                "image/webp", "application/javascript", "application/json", "application/xml", "application/pdf",
+                "application/octet-stream", "application/zip", "application/x-protobuf", "video/mp4", "video/webm",
+                "audio/mpeg", "multipart/form-data", "font/woff2", "-", ""]
+_WIDE_STATUS = [200, 304, 302, 404, 204, 301, 206, 403, 500, 401, 503, 400, 407, 502, 504, 405, 307, 429, 410, 501]
+
+
+def _wide_rows(rng, m: int):
+    """Long-tail request fields: (host, method, user agent, content type, path, status) per row."""
+    mz = 1.0 / np.arange(1, len(_WIDE_METHODS) + 1) ** 1.5
+    cz = 1.0 / np.arange(1, len(_WIDE_CTYPES) + 1)
+    sz = 1.0 / np.arange(1, len(_WIDE_STATUS) + 1) ** 1.3
+    meth = rng.choice(len(_WIDE_METHODS), size=m, p=mz / mz.sum())
+    ct = rng.choice(len(_WIDE_CTYPES), size=m, p=cz / cz.sum())
+    st = np.asarray(_WIDE_STATUS)[rng.choice(len(_WIDE_STATUS), size=m, p=sz / sz.sum())]
+    # ~20k distinct user agents, Zipf: the UA-frequency quintile then spreads over all 5 values
+    uz = 1.0 / np.arange(1, 20001) ** 0.9
+    uas = rng.choice(20000, size=m, p=uz / uz.sum())
+    hosts = rng.integers(0, 50000, size=m)
+    alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789-_=%", np.uint8)
+    plen = rng.integers(1, 160, size=m)
+    pk = rng.integers(8, alpha.size + 1, size=m)  # alphabet prefix: path entropy spreads too
+    rows = []
+    for j in range(m):
+        path = "/" + bytes(alpha[rng.integers(0, pk[j], size=int(plen[j]))]).decode()
+        rows.append((f"h{hosts[j]}.site{hosts[j] % 997}.com", _WIDE_METHODS[meth[j]],
+                     f"Agent/{uas[j] % 97}.{uas[j]} (build {uas[j] * 7919 % 10007})", _WIDE_CTYPES[ct[j]], path,
+                     int(st[j])))
+    return rows
+
+
 def generate_proxy(n: int, seed: int = 9, n_clients: int | None = None, alpha_true: float = 0.15,
-                   n_anomalies: int | None = None, rank: int = 0, date: str = "2016-07-08") -> ProxyDay:
+                   n_anomalies: int | None = None, rank: int = 0, date: str = "2016-07-08",
+                   wide_vocab: float = 0.0) -> ProxyDay:
+    """``wide_vocab``: fraction of (non-anomalous) rows drawn from the long tail -- 10 methods, 22
+    content types, 20 status codes, ~20k user agents, URIs of every length and alphabet, any hour
+    -- instead of a behaviour profile (vocabulary ~4e4 → ~1e5+; SURVEY.md §7.5 sizing)."""
     rng = np.random.default_rng([seed, rank])
     hrng = np.random.default_rng([seed, 0xB1])
     P = len(_PROFILES)
@@ -87,6 +123,11 @@ def generate_proxy(n: int, seed: int = 9, n_clients: int | None = None, alpha_tr
             host[i], ctype[i], method[i], ua[i] = hs[hsel[j]], cts[csel[j]], meths[msel[j]], _UAS[usel[j]]
             path[i] = "/" + "/".join(f"p{rng.integers(0, 50)}" for _ in range(depth[j])) + ".html"
     status = np.where(rng.random(n) < 0.92, 200, rng.choice([304, 404, 302, 500], size=n))
+    if wide_vocab > 0:
+        wide = np.nonzero(rng.random(n) < wide_vocab)[0]
+        hour_f[wide] = rng.uniform(0, 24, size=wide.size)
+        for i, (h, mt, u, c, p, st) in zip(wide.tolist(), _wide_rows(rng, wide.size)):
+            host[i], method[i], ua[i], ctype[i], path[i], status[i] = h, mt, u, c, p, st
     hour = np.mod(np.floor(hour_f), 24).astype(int)
     anomaly_rows = np.sort(rng.choice(n, size=min(n_anomalies, n), replace=False))
     quiet = np.argsort(w)[: max(1, n_clients // 10)]

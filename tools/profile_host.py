@@ -17,6 +17,8 @@ def main() -> int:
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 2_000_000
     pcap = "--pcap" in sys.argv
     import torch
+    from oni355.parallel.comm import init_from_env
+    comm = init_from_env("cuda")  # ONI_FORCE_DIST=1: the data-parallel code path on one GPU
     if src == "dns":
         from oni355.synth.dns import generate_dns, write_pcap
         day = generate_dns(n, seed=7)
@@ -46,7 +48,7 @@ def main() -> int:
         day = generate_flows(n, seed=7)
 
         def go():
-            return run_flow(day.cols, K=20, sweeps=200, device="cuda")
+            return run_flow(day.cols, K=20, sweeps=200, device=comm.device, comm=comm)
     go()
     torch.cuda.synchronize()
     pr = cProfile.Profile()
@@ -57,7 +59,7 @@ def main() -> int:
     pr.disable()
     print(f"{src} day: {time.perf_counter() - t:.3f} s; timings {res.timings}")
     s = io.StringIO()
-    pstats.Stats(pr, stream=s).sort_stats("cumulative").print_stats(35)
+    pstats.Stats(pr, stream=s).sort_stats("cumulative").print_stats(int(os.environ.get("PROFILE_LINES", "35")))
     print(s.getvalue())
     return 0
 
