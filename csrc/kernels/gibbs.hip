@@ -630,11 +630,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
 // Delta apply + q refresh: n_wk += Δ; n_k' = n_k + Δn_k; q = (n_wk+β)/(n_k'+Vβ); zero the other
 // delta buffer for the next sweep; bump the device sweep counter. nk/dnwk are ping-ponged by the
 // host so no block ever reads what another block of this launch writes.
+// With n_rows > 0 the same launch also seeds the NEXT sweep's long-document rows (rdst[r] :=
+// rsrc[r]: chunked documents add their Δn_dk atomically into a copy of the current counts), which
+// saves the separate k_copy_rows launch per sweep.
 __global__ __launch_bounds__(256) void k_apply(int32_t* __restrict__ nwk, const int32_t* __restrict__ dcur,
                                                 int32_t* __restrict__ dother, const int32_t* __restrict__ nk_cur,
                                                 int32_t* __restrict__ nk_next, float* __restrict__ q, int64_t V,
                                                 int K, int KS, float beta, float vbeta, uint32_t* sweep_ctr,
-                                                int bump, int absolute, int nk_rep) {
+                                                int bump, int absolute, int nk_rep, const int32_t* __restrict__ rsrc,
+                                                int32_t* __restrict__ rdst, const int32_t* __restrict__ rows,
+                                                int64_t n_rows) {
   __shared__ float den[256];
   __shared__ int32_t nkn[256];
   __shared__ int32_t part[256];
@@ -681,6 +686,12 @@ __global__ __launch_bounds__(256) void k_apply(int32_t* __restrict__ nwk, const 
     qo.z = k0 + 2 < K ? ((float)nv.z + beta) / den[k0 + 2] : 0.f;
     qo.w = k0 + 3 < K ? ((float)nv.w + beta) / den[k0 + 3] : 0.f;
     reinterpret_cast<float4*>(q)[i] = qo;
+  }
+  const int64_t rtotal = n_rows * KS;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rtotal; i += stride) {
+    const int64_t r = rows[i / KS];
+    const int k = (int)(i % KS);
+    rdst[r * KS + k] = rsrc[r * KS + k];
   }
 }
 
@@ -1505,12 +1516,18 @@ ONI_API int oni_gibbs_launch(const OniGibbs* a, int G, int KP, int init, int mod
 
 ONI_API int oni_gibbs_sizeof_args() { return (int)sizeof(OniGibbs); }
 
+// rsrc/rdst/rows/n_rows: optional fused long-row copy for the next sweep (n_rows = 0: none).
 ONI_API int oni_gibbs_apply(int32_t* nwk, const int32_t* dcur, int32_t* dother, const int32_t* nk_cur,
                             int32_t* nk_next, float* q, int64_t V, int K, int KS, float beta, float vbeta,
-                            uint32_t* sweep_ctr, int bump, int absolute, int nk_rep, hipStream_t s) {
+                            uint32_t* sweep_ctr, int bump, int absolute, int nk_rep, const int32_t* rsrc,
+                            int32_t* rdst, const int32_t* rows, int64_t n_rows, hipStream_t s) {
   if (KS % 4 != 0 || KS > 256 || nk_rep < 1 || (nk_rep & (nk_rep - 1))) return (int)hipErrorInvalidValue;
-  k_apply<<<oni::grid_for(V * KS / 4, 256, 2048), 256, 0, s>>>(nwk, dcur, dother, nk_cur, nk_next, q, V, K, KS, beta,
-                                                                vbeta, sweep_ctr, bump, absolute, nk_rep);
+  if (n_rows < 0 || (n_rows > 0 && (rsrc == nullptr || rdst == nullptr || rows == nullptr)))
+    return (int)hipErrorInvalidValue;
+  const int64_t work = V * KS / 4 > n_rows * KS ? V * KS / 4 : n_rows * KS;
+  k_apply<<<oni::grid_for(work, 256, 2048), 256, 0, s>>>(nwk, dcur, dother, nk_cur, nk_next, q, V, K, KS, beta,
+                                                          vbeta, sweep_ctr, bump, absolute, nk_rep, rsrc, rdst, rows,
+                                                          n_rows);
   return (int)hipGetLastError();
 }
 

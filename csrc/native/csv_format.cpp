@@ -9,6 +9,12 @@
 //   0 int64 decimal          1 uint32 IPv4 dotted quad      2 unix seconds → "YYYY-MM-DD HH:MM:SS"
 //   3 float64 "%g"           4 float32 "%.9g" (scores)      5 string (int64 offsets + bytes),
 //   6 packed flow word (u32: dir@28 | port@11 | tbin@7 | bbin@3 | pbin, spec.flow_word_str)
+//   7 packed u64 word rendered as '_'-joined decimal fields (DNS / proxy word_str); offs[c] holds
+//     the field spec [n_fields, shift_0, mask_0, shift_1, mask_1, ...]
+//   8 string, or -- where it is empty -- unix seconds as kind 2 (DNS frame_time of synthetic /
+//     columnar rows); data[c] → StrCol {chars, offsets, rows, unix seconds (per output row)}
+//   9 string read straight from a whole column: data[c] → StrCol {chars, offsets, rows}; output
+//     row r is column row rows[r] (no host-side gather of the selected strings)
 //
 // Strings follow Python csv.QUOTE_MINIMAL: quoted (with "" doubling) when they contain a comma,
 // a quote, CR or LF. Lines end in '\n'.
@@ -17,6 +23,9 @@
 #include <cstdio>
 #include <cstring>
 #include <ctime>
+#include <atomic>
+#include <thread>
+#include <vector>
 
 #include "oni_native.h"
 
@@ -137,15 +146,44 @@ void put_flow_word(Buf& b, uint32_t w) {
   put_u32(b, pb);
 }
 
-}  // namespace
+void put_packed(Buf& b, uint64_t w, const int64_t* spec) {
+  const int64_t nf = spec[0];
+  for (int64_t f = 0; f < nf; ++f) {
+    if (f) b.ch('_');
+    char t[24];
+    const uint64_t v = (w >> spec[1 + 2 * f]) & (uint64_t)spec[2 + 2 * f];
+    const auto r = std::to_chars(t, t + sizeof t, v);
+    b.put(t, (size_t)(r.ptr - t));
+  }
+}
 
-// Format n_rows × n_cols fields. data[c] points at the column's values (or the chars of a string
-// column, whose offsets are offs[c]). Returns the byte length written (rows end at row_end[i]);
-// if that exceeds cap nothing is guaranteed and the caller retries with a larger buffer.
-ONI_NATIVE_API int64_t oni_csv_format(int64_t n_rows, int n_cols, const int32_t* kinds, const void* const* data,
-                                      const int64_t* const* offs, char* out, int64_t cap, int64_t* row_end) {
-  Buf b{out, cap};
-  for (int64_t r = 0; r < n_rows; ++r) {
+struct StrCol {
+  const uint8_t* chars;
+  const int64_t* offs;
+  const int64_t* rows;  // nullable: identity
+  const int64_t* unix_s;
+};
+
+// Rows [r0, r1) into b; row_end[r] is relative to b's start. Returns false on an unknown kind.
+// The string columns are read at random rows of day-sized columns: each field is a cache miss, so
+// the offsets of row r + 2·kAhead and the characters of row r + kAhead are prefetched.
+constexpr int64_t kAhead = 8;
+
+void prefetch_row(int n_cols, const int32_t* kinds, const void* const* data, int64_t r, bool chars) {
+  for (int c = 0; c < n_cols; ++c) {
+    if (kinds[c] != 8 && kinds[c] != 9) continue;
+    const auto* st = static_cast<const StrCol*>(data[c]);
+    const int64_t i = st->rows ? st->rows[r] : r;
+    if (chars) __builtin_prefetch(st->chars + st->offs[i]);
+    else __builtin_prefetch(st->offs + i);
+  }
+}
+
+bool format_rows(int64_t r0, int64_t r1, int n_cols, const int32_t* kinds, const void* const* data,
+                 const int64_t* const* offs, Buf& b, int64_t* row_end) {
+  for (int64_t r = r0; r < r1; ++r) {
+    if (r + 2 * kAhead < r1) prefetch_row(n_cols, kinds, data, r + 2 * kAhead, false);
+    if (r + kAhead < r1) prefetch_row(n_cols, kinds, data, r + kAhead, true);
     for (int c = 0; c < n_cols; ++c) {
       if (c) b.ch(',');
       switch (kinds[c]) {
@@ -170,11 +208,79 @@ ONI_NATIVE_API int64_t oni_csv_format(int64_t n_rows, int n_cols, const int32_t*
           break;
         }
         case 6: put_flow_word(b, static_cast<const uint32_t*>(data[c])[r]); break;
-        default: return -1;
+        case 7: put_packed(b, static_cast<const uint64_t*>(data[c])[r], offs[c]); break;
+        case 8:
+        case 9: {
+          const auto* st = static_cast<const StrCol*>(data[c]);
+          const int64_t i = st->rows ? st->rows[r] : r;
+          const int64_t len = st->offs[i + 1] - st->offs[i];
+          if (len || kinds[c] == 9) put_str(b, st->chars + st->offs[i], len);
+          else put_time(b, st->unix_s[r]);
+          break;
+        }
+        default: return false;
       }
     }
     b.ch('\n');
     row_end[r] = b.n;
   }
-  return b.n;
+  return true;
+}
+
+}  // namespace
+
+// Format n_rows × n_cols fields. data[c] points at the column's values (or the chars of a string
+// column, whose offsets are offs[c]). Returns the byte length written (rows end at row_end[i]);
+// if that exceeds cap nothing is guaranteed and the caller retries with a larger buffer; -1 on an
+// unknown kind. Large row counts are formatted in parallel row blocks (private buffers, then one
+// copy into `out`), which also overlaps the cache misses of the random-row string reads.
+ONI_NATIVE_API int64_t oni_csv_format(int64_t n_rows, int n_cols, const int32_t* kinds, const void* const* data,
+                                      const int64_t* const* offs, char* out, int64_t cap, int64_t* row_end) {
+  const int64_t kBlockRows = 512;  // ≥ 2 blocks before threads start (thread start ≈ tens of µs)
+  const int64_t nb = (n_rows + kBlockRows - 1) / kBlockRows;
+  if (nb <= 1) {
+    Buf b{out, cap};
+    if (!format_rows(0, n_rows, n_cols, kinds, data, offs, b, row_end)) return -1;
+    return b.n;
+  }
+  std::vector<std::vector<char>> parts((size_t)nb);
+  std::vector<int64_t> len((size_t)nb, 0);
+  std::atomic<int> bad{0};
+  std::atomic<int64_t> next{0};
+  auto work = [&] {
+    for (int64_t k = next.fetch_add(1); k < nb; k = next.fetch_add(1)) {
+      const int64_t r0 = k * kBlockRows, r1 = std::min(n_rows, r0 + kBlockRows);
+      std::vector<char>& v = parts[(size_t)k];
+      v.resize((size_t)std::max<int64_t>(4096, cap / nb + 4096));
+      for (;;) {
+        Buf b{v.data(), (int64_t)v.size()};
+        if (!format_rows(r0, r1, n_cols, kinds, data, offs, b, row_end)) {
+          bad = 1;
+          break;
+        }
+        if (!b.overflow) {
+          len[(size_t)k] = b.n;
+          break;
+        }
+        v.resize((size_t)b.n);
+      }
+    }
+  };
+  const int nt = (int)std::min<int64_t>(nb, std::max(1u, std::min(8u, std::thread::hardware_concurrency())));
+  std::vector<std::thread> ts;
+  for (int t = 1; t < nt; ++t) ts.emplace_back(work);
+  work();
+  for (auto& t : ts) t.join();
+  if (bad) return -1;
+  int64_t total = 0;
+  for (int64_t k = 0; k < nb; ++k) total += len[(size_t)k];
+  if (total > cap) return total;
+  int64_t base = 0;
+  for (int64_t k = 0; k < nb; ++k) {
+    const int64_t r0 = k * kBlockRows, r1 = std::min(n_rows, r0 + kBlockRows);
+    std::memcpy(out + base, parts[(size_t)k].data(), (size_t)len[(size_t)k]);
+    for (int64_t r = r0; r < r1; ++r) row_end[r] += base;
+    base += len[(size_t)k];
+  }
+  return total;
 }

@@ -80,7 +80,7 @@ def event_rows(source: str, cols: dict, local_rows, words: list[str], scores) ->
 # ------------------------------------------------------------------------------------------------
 # native rendering (csrc/native/csv_format.cpp): typed result columns → CSV text in one C++ pass
 # ------------------------------------------------------------------------------------------------
-K_INT, K_IP, K_TIME, K_FLOAT, K_SCORE, K_STR, K_FLOWWORD = range(7)
+K_INT, K_IP, K_TIME, K_FLOAT, K_SCORE, K_STR, K_FLOWWORD, K_PACKED, K_STR_OR_TIME, K_STR_ROWS = range(10)
 
 
 class Rendered:
@@ -109,11 +109,36 @@ def _native_format(fields: list[tuple[int, object]], n: int) -> Rendered:
                                        C.c_int64, C.c_void_p], C.c_int64)
     L = native.lib()
     keep, ptrs, offs, kinds = [], [], [], []
+    str_bytes = 0
     for kind, v in fields:
         if kind == K_STR:
             keep += [v.chars if v.chars.size else np.zeros(1, np.uint8), v.offsets]
             ptrs.append(keep[-2].ctypes.data)
             offs.append(v.offsets.ctypes.data)
+            str_bytes += int(v.offsets[-1] - v.offsets[0]) if len(v) else 0
+        elif kind == K_PACKED:
+            words, spec_fields = v
+            a = np.ascontiguousarray(words, dtype=np.uint64)
+            sp = np.asarray([len(spec_fields)] + [x for sm in spec_fields for x in sm], dtype=np.int64)
+            if a.size != n:
+                raise ValueError("result column length mismatch")
+            keep += [a, sp]
+            ptrs.append(a.ctypes.data)
+            offs.append(sp.ctypes.data)
+        elif kind in (K_STR_OR_TIME, K_STR_ROWS):
+            # a whole string column read through a row index (no gather of the strings on the host)
+            col, rows, unix = v if kind == K_STR_OR_TIME else (*v, None)
+            r = np.ascontiguousarray(rows, dtype=np.int64)
+            if r.size != n:
+                raise ValueError("result column length mismatch")
+            u = np.ascontiguousarray(unix, dtype=np.int64) if unix is not None else None
+            ch = col.chars if col.chars.size else np.zeros(1, np.uint8)
+            st = (C.c_void_p * 4)(ch.ctypes.data, col.offsets.ctypes.data, r.ctypes.data,
+                                  u.ctypes.data if u is not None else None)
+            keep += [r, u, ch, col.offsets, st]
+            ptrs.append(C.addressof(st))
+            offs.append(None)
+            str_bytes += int((col.offsets[r + 1] - col.offsets[r]).sum()) if r.size else 0
         else:
             dt = {K_INT: np.int64, K_IP: np.uint32, K_TIME: np.int64, K_FLOAT: np.float64, K_SCORE: np.float32,
                   K_FLOWWORD: np.uint32}[kind]
@@ -129,7 +154,7 @@ def _native_format(fields: list[tuple[int, object]], n: int) -> Rendered:
     ptr_a = (C.c_void_p * nc)(*ptrs)
     off_a = (C.c_void_p * nc)(*offs)
     ends = np.zeros(max(n, 1), dtype=np.int64)
-    cap = max(n * 16 * max(nc, 1), 1024)  # typical fields are < 16 bytes; retried once if short
+    cap = max(n * 24 * max(nc, 1) + 2 * str_bytes, 1024)  # typical non-string fields < 24 bytes; retried once if short
     for _ in range(2):
         buf = np.empty(cap, dtype=np.uint8)  # not zeroed: only [0, m) is read back
         m = L.oni_csv_format(n, nc, kind_a, ptr_a, off_a, buf.ctypes.data_as(C.c_char_p), cap, ends.ctypes.data)
@@ -145,7 +170,9 @@ def _col_field(c: str, v, rows: np.ndarray, ip_cols=(), time_cols=(), float_cols
     if v is None:
         return K_STR, _EMPTY.take(np.zeros(rows.size, np.int64))
     if isinstance(v, StringColumn):
-        return K_STR, v.take(rows)
+        if type(v) is not StringColumn:  # lazily formatted columns (pcap frame_time): only these rows
+            return K_STR, v.take(rows)
+        return K_STR_ROWS, (v, rows)
     a = np.asarray(v)[rows]
     if c in ip_cols:
         return K_IP, a.astype(np.int64).astype(np.uint32) if a.dtype != np.uint32 else a
@@ -174,19 +201,21 @@ def format_flow(cols: dict, local_rows, src_words, dst_words, src_scores, dst_sc
     return _native_format(f, rows.size)
 
 
-def format_events(source: str, cols: dict, local_rows, words: list[str], scores) -> Rendered:
+def format_events(source: str, cols: dict, local_rows, words, scores) -> Rendered:
+    """``words``: rendered strings, or ``(packed u64 words, [(shift, mask), ...])`` rendered by the
+    native formatter ('_'-joined fields, :func:`word_fields`)."""
     rows = np.asarray(local_rows, dtype=np.int64)
     f = [_col_field(c, cols.get(c), rows, _EVENT_IP_COLUMNS) for c in schema.raw_columns(source)]
     if source == "dns" and rows.size:
-        ft = f[0][1]
-        empty = (ft.offsets[1:] - ft.offsets[:-1]) == 0
-        if empty.any():
-            # frame_time missing: render it from unix_tstamp (the decoder's own format)
-            vals = ft.to_list()
-            for i in np.nonzero(empty)[0]:
-                vals[i] = _fmt_time(cols["unix_tstamp"][rows[i]])
-            f[0] = (K_STR, StringColumn.from_list(vals))
-    f += [(K_STR, StringColumn.from_list(words)), (K_SCORE, scores)]
+        col, r = f[0][1] if f[0][0] == K_STR_ROWS else (f[0][1], np.arange(rows.size))
+        if ((col.offsets[r + 1] - col.offsets[r]) == 0).any():
+            # frame_time missing: rendered from unix_tstamp where empty
+            f[0] = (K_STR_OR_TIME, (col, r, np.asarray(cols["unix_tstamp"])[rows]))
+    if isinstance(words, tuple):
+        f += [(K_PACKED, words)]
+    else:
+        f += [(K_STR, StringColumn.from_list(words))]
+    f += [(K_SCORE, scores)]
     return _native_format(f, rows.size)
 
 
@@ -202,13 +231,9 @@ def render_result(source: str, cols: dict, res, row_off: int, comm=None) -> Rend
         rendered = format_flow(cols, rows_local[mine], res.src_words[mine], res.dst_words[mine],
                                res.src_scores[mine], res.dst_scores[mine], res.scores[mine])
     else:
-        if source == "dns":
-            from ..pipeline.dns import word_str
-        else:
-            from ..pipeline.proxy import word_str
         ncol = len(cols["ip_dst" if source == "dns" else "clientip"])
         mine = (rows_local >= 0) & (rows_local < ncol)
-        rendered = format_events(source, cols, rows_local[mine], [word_str(w) for w in res.words[mine]],
+        rendered = format_events(source, cols, rows_local[mine], (res.words[mine], word_fields(source)),
                                  res.scores[mine])
     if comm is None or not comm.dist:
         return rendered
@@ -223,6 +248,22 @@ def render_result(source: str, cols: dict, res, row_off: int, comm=None) -> Rend
     lines = [by_gid[int(g)] for g in res.rows.tolist()]
     ends = np.cumsum([len(x) for x in lines]).astype(np.int64) if lines else np.zeros(0, np.int64)
     return Rendered(b"".join(lines), ends)
+
+
+def word_fields(source: str) -> list[tuple[int, int]]:
+    """(shift, mask) of every field of a DNS / proxy word, in ``word_str`` order."""
+    from ..ref import spec as sp
+    if source == "dns":
+        from ..pipeline import dns as m
+        out = [(m.TOP_SHIFT, 3)] + [(s, 15 if fr is sp.DECILES else 7) for _, fr, s in m.BINNED]
+        return out + [(s, mk) for _, mk, s in m.RAW]
+    from ..pipeline import proxy as m
+    fields = {"top": (m.TOP_SHIFT, 3)}
+    for name, fr, s in m.BINNED:
+        fields[name] = (s, 15 if fr is sp.DECILES else 7)
+    for name, mk, s in m.RAW:
+        fields[name] = (s, mk)
+    return [fields[k] for k in ("top", "time", "method", "ua_freq", "ctype", "uri_ent", "uri_len", "respcode")]
 
 
 def write_rendered(path: str, header: list[str], rendered: Rendered) -> str:

@@ -275,7 +275,8 @@ class GibbsLDA:
         VK = self.V * self.KS
         self.dn[0].zero_()
         ops.gibbs_apply(self.nwk, self.dn[0], self.dn[1], self.nk[self.cn], self.nk[1 - self.cn], self.q, self.V,
-                        self.K, self.KS, self.beta, self.vbeta, self.sweep_ctr, bump=False)
+                        self.K, self.KS, self.beta, self.vbeta, self.sweep_ctr, bump=False,
+                        rows_copy=(self.ndk[self.a], self.ndk[1 - self.a], self.c.long_rows))
         self.cn = 1 - self.cn
         self.sweep_ctr.fill_(self.sweeps_done + 1)
         _ = VK
@@ -287,7 +288,8 @@ class GibbsLDA:
         if mode == self.mode and mode in (2, 4) and not self._aux_synced:
             self._sync_aux_z()  # entering a delta mode: z_prev / z_w := z (eager, outside graphs)
         self._aux_synced = self._keeps_aux(mode)
-        ops.copy_rows(self.ndk[self.a], self.ndk[1 - self.a], c.long_rows, self.KS)
+        # long (chunked) documents add their Δn_dk into ndk[1-a] rows that hold a copy of ndk[a]:
+        # every apply -- the previous sweep's, or _prime()'s after init / resume -- seeds that copy
         ops.gibbs_pass(self._state(False), self.G, self.KP, self.K, self.alpha, self.cfg.seed, False,
                        self.sweep_ctr, c.chunk_len, host_sweep=self.sweeps_done + 1, mode=mode,
                        prefetch_q=self.qpf,
@@ -311,7 +313,7 @@ class GibbsLDA:
             self._allreduce_dn(self.dn[self.b])
         ops.gibbs_apply(self.nwk, self.dn[self.b], self.dn[1 - self.b], self.nk[self.cn], self.nk[1 - self.cn],
                         self.q, self.V, self.K, self.KS, self.beta, self.vbeta, self.sweep_ctr, bump=True,
-                        absolute=mode in (0, 3))
+                        absolute=mode in (0, 3), rows_copy=(self.ndk[1 - self.a], self.ndk[self.a], c.long_rows))
         self.a, self.b, self.cn = 1 - self.a, 1 - self.b, 1 - self.cn
         self.sweeps_done += 1
 

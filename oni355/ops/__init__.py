@@ -386,11 +386,13 @@ def recount(wsorted, wslot, tok_z, nwk_out, KS: int) -> None:
 STREAM_RECOUNT = True  # k_recount_reg (register runs) 0.065 ms vs k_recount (LDS) 0.093 ms, both at 8 KB LDS
 
 
-def gibbs_apply(nwk, dcur, dother, nk_cur, nk_next, q, V, K, KS, beta, vbeta, sweep_ctr, bump=True, absolute=False):
+def gibbs_apply(nwk, dcur, dother, nk_cur, nk_next, q, V, K, KS, beta, vbeta, sweep_ctr, bump=True, absolute=False,
+                rows_copy=None):
     """n_wk ← Δ (or absolute), n_k ← n_k + Σ_replicas Δn_k, q refresh; zeroes ``dother``.
 
     ``dcur``/``dother`` are [V·KS + R·KS + DN_AUX]: the Δn_wk table, R replicas of Δn_k, then
-    DN_AUX auxiliary words ([0] = tokens that changed topic; all-reduced with the rest)."""
+    DN_AUX auxiliary words ([0] = tokens that changed topic; all-reduced with the rest).
+    ``rows_copy = (src, dst, rows)``: also :func:`copy_rows` in the same launch."""
     nk_rep = (dcur.numel() - V * KS - DN_AUX) // KS
     if nk_rep < 1 or V * KS + nk_rep * KS + DN_AUX != dcur.numel():
         raise ValueError("Δ buffer must be [V*KS + nk_rep*KS + DN_AUX]")
@@ -405,10 +407,16 @@ def gibbs_apply(nwk, dcur, dother, nk_cur, nk_next, q, V, K, KS, beta, vbeta, sw
         dother.zero_()
         if bump:
             sweep_ctr += 1
+        if rows_copy is not None:
+            copy_rows(*rows_copy, KS)
         return
+    rs, rd, rr = rows_copy if rows_copy is not None and rows_copy[2].numel() else (None, None, None)
     _lib.check(_lib.lib().oni_gibbs_apply(*map(_lib.ptr, (nwk, dcur, dother, nk_cur, nk_next, q)), V, K, KS,
                                           float(beta), float(vbeta), _lib.ptr(sweep_ctr), 1 if bump else 0,
-                                          1 if absolute else 0, nk_rep, _lib.stream()), "oni_gibbs_apply")
+                                          1 if absolute else 0, nk_rep, _lib.ptr(rs) if rs is not None else None,
+                                          _lib.ptr(rd) if rd is not None else None,
+                                          _lib.ptr(rr) if rr is not None else None, rr.numel() if rr is not None else 0,
+                                          _lib.stream()), "oni_gibbs_apply")
 
 
 def copy_rows(src, dst, rows, KS):

@@ -49,7 +49,8 @@ _SIGS = {
     "oni_sell_perm_z": [vp, vp, vp, i64, C.c_int, vp, vp, vp, vp, C.c_int, vp],
     "oni_gibbs_launch": [C.POINTER(OniGibbs), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp],
     "oni_gibbs_sizeof_args": [],
-    "oni_gibbs_apply": [vp, vp, vp, vp, vp, vp, i64, C.c_int, C.c_int, f32, f32, vp, C.c_int, C.c_int, C.c_int, vp],
+    "oni_gibbs_apply": [vp, vp, vp, vp, vp, vp, i64, C.c_int, C.c_int, f32, f32, vp, C.c_int, C.c_int, C.c_int,
+                        vp, vp, vp, i64, vp],
     "oni_recount": [vp, vp, vp, i64, vp, C.c_int, C.c_int, C.c_int, vp],
     "oni_recount_stream": [vp, vp, i64, vp, C.c_int, C.c_int, C.c_int, vp],
     "oni_delta_recount": [vp, vp, vp, vp, vp, vp, vp, i64, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp],

@@ -61,3 +61,23 @@ def test_write_rendered_roundtrip(tmp_path):
     p = rio.write_rendered(str(tmp_path / "x" / "flow_results.csv"), schema.FLOW_RESULT_COLUMNS, rend)
     header, body = rio.read_csv(p)
     assert header == schema.FLOW_RESULT_COLUMNS and len(body) == 10
+
+
+def test_native_event_rendering_many_rows_matches_spec():
+    """Several formatter row blocks (parallel path), string columns read through the row index,
+    packed DNS / proxy words rendered natively, empty frame_time falling back to unix_tstamp."""
+    import numpy as np
+
+    from oni355.io import results as rio
+    from oni355.pipeline.dns import word_str as dws
+    from oni355.pipeline.proxy import word_str as pws
+    from oni355.synth.dns import generate_dns
+    from oni355.synth.proxy import generate_proxy
+    rng = np.random.default_rng(5)
+    for src, day, ws in (("dns", generate_dns(20_000, seed=2), dws), ("proxy", generate_proxy(20_000, seed=2), pws)):
+        rows = rng.permutation(20_000)[:2500]  # score order: not ascending rows
+        w = rng.integers(0, 2**40, rows.size).astype(np.uint64)
+        sc = rng.random(rows.size).astype(np.float32)
+        got = rio.format_events(src, day.cols, rows, (w, rio.word_fields(src)), sc)
+        assert got.rows() == rio.event_rows(src, day.cols, rows, [ws(x) for x in w], sc)
+        assert len(got) == rows.size and got.ends[-1] == len(got.blob)
