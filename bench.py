@@ -180,31 +180,35 @@ def run_pipeline_mode(a, comm) -> dict:
     # flow days stream in through a double-buffered prefetcher: the loader's pinned buffers are
     # uploaded on a copy stream while the previous day computes (every step still uploads its day)
     pf, pinned = None, None
-    if a.source == "flow" and dev.type == "cuda" and not a.no_prefetch:
+    if dev.type == "cuda" and not a.no_prefetch and pcap is None:
         from oni355.io.staging import Prefetcher
-        from oni355.pipeline.flow import DEVICE_COLS
-        pinned = Prefetcher.pin(day.cols, DEVICE_COLS)
+        if a.source == "flow":
+            from oni355.pipeline.flow import DEVICE_COLS
+            pinned = Prefetcher.pin(day.cols, DEVICE_COLS)
+        elif a.source == "dns":
+            from oni355.pipeline.dns import host_arrays
+            pinned = Prefetcher.pin_arrays(host_arrays(day.cols))
+        else:
+            from oni355.pipeline.proxy import host_arrays
+            pinned = Prefetcher.pin_arrays(host_arrays(day.cols))
         pf = Prefetcher(dev)
         pf.submit(pinned)
     setup_s = time.perf_counter() - t_setup
 
     def step():
         t0 = time.perf_counter()
+        dcols, on_train = None, None
+        if pf is not None:
+            dcols = pf.take()
+            # the next day's upload overlaps this day's compute
+            if a.prefetch_at == "start" or a.source != "flow":
+                pf.submit(pinned)
+            else:
+                on_train = lambda: pf.submit(pinned)  # noqa: E731
         if a.source == "flow":
             from oni355.pipeline.flow import run_flow
             cols = day.cols
-            dcols = None
-            on_train = None
-            if pf is not None:
-                dcols = pf.take()
-                # the next day's upload overlaps this day's compute
-                if a.prefetch_at == "start":
-                    pf.submit(pinned)
-                else:
-                    on_train = lambda: pf.submit(pinned)  # noqa: E731
             res = run_flow(cols, device_cols=dcols, on_train=on_train, **kw)
-            if pf is not None:
-                res.timings["h2d_copy_dev_s"] = pf.copy_ms() / 1e3
         elif a.source == "dns":
             from oni355.pipeline.dns import run_dns
             if pcap is not None:
@@ -213,12 +217,14 @@ def run_pipeline_mode(a, comm) -> dict:
             else:
                 cols = day.cols
             t_dec = time.perf_counter() - t0
-            res = run_dns(cols, top_domains=top, user_domain="intel", **kw)
+            res = run_dns(cols, top_domains=top, user_domain="intel", device_cols=dcols, **kw)
             res.timings["decode_s"] = t_dec
         else:
             from oni355.pipeline.proxy import run_proxy
             cols = day.cols
-            res = run_proxy(cols, **kw)
+            res = run_proxy(cols, device_cols=dcols, **kw)
+        if pf is not None:
+            res.timings["h2d_copy_dev_s"] = pf.copy_ms() / 1e3
         t1 = time.perf_counter()
         rendered = rio.render_result(a.source, cols, res, row_off, comm)
         if rank == 0:

@@ -191,6 +191,11 @@ class Prefetcher:
             out[name] = t.pin_memory()
         return out
 
+    @staticmethod
+    def pin_arrays(arrays: dict) -> dict:
+        """Page-locked host copies of ready-typed arrays (e.g. a pipeline's ``host_arrays``)."""
+        return {k: torch.from_numpy(np.ascontiguousarray(a)).pin_memory() for k, a in arrays.items()}
+
     def submit(self, pinned: dict) -> None:
         if self._pending is not None:
             raise RuntimeError("Prefetcher: take() the pending upload first")

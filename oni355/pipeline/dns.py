@@ -56,18 +56,21 @@ def load_top_domains(path: str) -> list[str]:
     return out
 
 
-def to_device(cols: dict, device) -> dict:
-    up = staging.upload
-    d = {}
-    for k in ("unix_tstamp",):
-        d[k] = up(np.asarray(cols[k], np.int64), device)
+def host_arrays(cols: dict) -> dict:
+    """The host arrays the DNS model reads, in their device dtypes (what :func:`to_device` uploads;
+    a loader can pin and prefetch them, ``run_dns(device_cols=...)``)."""
+    d = {"unix_tstamp": np.asarray(cols["unix_tstamp"], np.int64)}
     for k in ("frame_len", "dns_qry_type", "dns_qry_rcode"):
-        d[k] = up(np.asarray(cols[k]).astype(np.int32), device)
-    d["ip_dst"] = up(np.asarray(cols["ip_dst"], np.uint32).view(np.int32), device)
+        d[k] = np.asarray(cols[k]).astype(np.int32, copy=False)
+    d["ip_dst"] = np.asarray(cols["ip_dst"], np.uint32).view(np.int32)
     nm: StringColumn = cols["dns_qry_name"]
-    d["name_off"] = up(nm.offsets, device)
-    d["name_chars"] = up(nm.chars if nm.chars.size else np.zeros(1, np.uint8), device)
+    d["name_off"] = nm.offsets
+    d["name_chars"] = nm.chars if nm.chars.size else np.zeros(1, np.uint8)
     return d
+
+
+def to_device(cols: dict, device) -> dict:
+    return {k: staging.upload(a, device) for k, a in host_arrays(cols).items()}
 
 
 def time_keys(unix: torch.Tensor) -> torch.Tensor:
@@ -103,10 +106,13 @@ def run_dns(cols: dict, K: int = 50, sweeps: int = 200, tol: float = 1.0, maxres
             alpha: float | None = None, beta: float = 0.01, seed: int = 0x0D15EA5E, chunk_len: int = 0,
             device="cpu", comm: Comm | None = None, top_domains=None, user_domain: str = "",
             feedback: dict | None = None, dupfactor: int = 1000, row_offset: int = 0, eval_every: int = 0, burnin: int = 0,
-            ckpt=None, log=None, ldac_dir: str | None = None, ldac_lag: int = 0) -> common.SingleResult:
+            ckpt=None, log=None, ldac_dir: str | None = None, ldac_lag: int = 0,
+            device_cols: dict | None = None) -> common.SingleResult:
+    """``device_cols``: :func:`host_arrays` already on the device (e.g. prefetched by
+    io.staging.Prefetcher while the previous day computed)."""
     timer = StageTimer(device)
     with timer.stage("h2d"):
-        d = to_device(cols, device)
+        d = dict(device_cols) if device_cols is not None else to_device(cols, device)
     with timer.stage("featurize"):
         topset = top_set(top_domains)
         words, cuts, feats = featurize(d, comm, topset, user_domain)

@@ -54,10 +54,26 @@ def word_str(w: int) -> str:
     return "_".join(str(vals[k]) for k in ("top", "time", "method", "ua_freq", "ctype", "uri_ent", "uri_len", "respcode"))
 
 
-def _codes_by_hash(col: StringColumn, dev, fn) -> torch.Tensor:
+STRING_COLS = ("host", "p_time", "useragent", "fulluri", "reqmethod", "resconttype")
+
+
+def host_arrays(cols: dict) -> dict:
+    """The host arrays the proxy model reads, in their device dtypes: ``<col>.off`` / ``<col>.chars``
+    of the string columns, ``respcode``, ``clientip`` (a loader can pin and prefetch them,
+    ``run_proxy(device_cols=...)``)."""
+    out = {}
+    for name in STRING_COLS:
+        c: StringColumn = cols[name]
+        out[name + ".off"] = c.offsets
+        out[name + ".chars"] = c.chars if c.chars.size else np.zeros(1, np.uint8)
+    out["respcode"] = np.asarray(cols["respcode"]).astype(np.int32, copy=False)
+    out["clientip"] = np.asarray(cols["clientip"], np.uint32).view(np.int32)
+    return out
+
+
+def _codes_by_hash(col: StringColumn, off: torch.Tensor, ch: torch.Tensor, fn) -> torch.Tensor:
     """Categorical code per row via the distinct values only (few distinct methods / types)."""
-    off = staging.upload(col.offsets, dev)
-    ch = staging.upload(col.chars if col.chars.size else np.zeros(1, np.uint8), dev)
+    dev = off.device
     h, _, _ = sops.string_features(off, ch)
     uniq, first_idx, inv = _unique_first(h)
     labels = [fn(col[int(i)]) for i in first_idx.tolist()]
@@ -99,14 +115,15 @@ def _hour_table(dev) -> torch.Tensor:
 
 
 @traced("oni:proxy.featurize")
-def featurize(cols: dict, device, comm: Comm | None, topset, allreduce_counts: bool = True):
+def featurize(cols: dict, device, comm: Comm | None, topset, allreduce_counts: bool = True, d: dict | None = None):
+    """``d``: :func:`host_arrays` already on the device (else uploaded here)."""
     dev = torch.device(device)
     n = len(cols["clientip"])
+    if d is None:
+        d = {k: staging.upload(a, dev) for k, a in host_arrays(cols).items()}
 
     def strcol(name):
-        c: StringColumn = cols[name]
-        return (staging.upload(c.offsets, dev),
-                staging.upload(c.chars if c.chars.size else np.zeros(1, np.uint8), dev))
+        return d[name + ".off"], d[name + ".chars"]
 
     ho, hc = strcol("host")
     _, top, _, _, _ = sops.domain_features(ho, hc, topset, "")
@@ -145,9 +162,9 @@ def featurize(cols: dict, device, comm: Comm | None, topset, allreduce_counts: b
         ar = comm.allreduce_np
         n_glob = int(comm.allreduce_np(np.array([n], np.int64))[0])
     cuts = {name: ops.quantile_cuts(keys[name], fr, ar, n_glob) for name, fr, _ in BINNED}
-    raws = {"method": _codes_by_hash(cols["reqmethod"], dev, method_code),
-            "ctype": _codes_by_hash(cols["resconttype"], dev, ctype_class),
-            "respcode": staging.upload(np.asarray(cols["respcode"]).astype(np.int32), dev)}
+    raws = {"method": _codes_by_hash(cols["reqmethod"], *strcol("reqmethod"), method_code),
+            "ctype": _codes_by_hash(cols["resconttype"], *strcol("resconttype"), ctype_class),
+            "respcode": d["respcode"]}
     words = sops.pack_words([keys[nm] for nm, _, _ in BINNED], [cuts[nm] for nm, _, _ in BINNED],
                             [s for _, _, s in BINNED], [raws[nm] for nm, _, _ in RAW], [m for _, m, _ in RAW],
                             [s for _, _, s in RAW], raw8=top, r8mask=3, r8shift=TOP_SHIFT)
@@ -159,17 +176,22 @@ def run_proxy(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxr
               alpha: float | None = None, beta: float = 0.01, seed: int = 0x0D15EA5E, chunk_len: int = 0,
               device="cpu", comm: Comm | None = None, top_domains=None, feedback: dict | None = None,
               dupfactor: int = 1000, row_offset: int = 0, eval_every: int = 0, burnin: int = 0, ckpt=None,
-              log=None, ldac_dir: str | None = None, ldac_lag: int = 0) -> common.SingleResult:
+              log=None, ldac_dir: str | None = None, ldac_lag: int = 0,
+              device_cols: dict | None = None) -> common.SingleResult:
+    """``device_cols``: :func:`host_arrays` already on the device (e.g. prefetched by
+    io.staging.Prefetcher while the previous day computed)."""
     timer = StageTimer(device)
+    with timer.stage("h2d"):
+        d = dict(device_cols) if device_cols is not None else \
+            {k: staging.upload(a, device) for k, a in host_arrays(cols).items()}
     with timer.stage("featurize"):
         topset = top_set(top_domains)
-        words, cuts = featurize(cols, device, comm, topset)
-        dev = words.device
-        docs = staging.upload(np.asarray(cols["clientip"], np.uint32).astype(np.int64), dev)
+        words, cuts = featurize(cols, device, comm, topset, d=d)
+        docs = common.u32_to_i64(d["clientip"])
     fb = None
     if feedback and len(feedback.get("clientip", [])):
         fw, _ = featurize(feedback, device, None, topset)
-        fdoc = torch.from_numpy(np.asarray(feedback["clientip"], np.uint32).astype(np.int64)).to(dev)
+        fdoc = torch.from_numpy(np.asarray(feedback["clientip"], np.uint32).astype(np.int64)).to(words.device)
         fb = (fdoc, fw, torch.full_like(fw, int(dupfactor)))
     res = common.run_single_doc_events(docs, words, K, sweeps, tol, maxresults, alpha, beta, seed, chunk_len, comm,
                                        feedback=fb, row_offset=row_offset, eval_every=eval_every, burnin=burnin, ckpt=ckpt, log=log,
