@@ -66,7 +66,8 @@ def parse(argv=None):
                     help="when the next day's upload is queued: at step start (default) or as the sweeps "
                          "start (measured 8 ms slower: the sweeps run slower beside the upload)")
     ap.add_argument("--no-prefetch", action="store_true",
-                    help="flow: upload each day inside its step instead of overlapping it with the previous one")
+                    help="upload (and, --from-pcap, decode) each day inside its step instead of overlapping "
+                         "it with the previous day's compute")
     a = ap.parse_args(argv)
     a.topics_set = a.topics is not None
     if a.topics is None:
@@ -179,7 +180,14 @@ def run_pipeline_mode(a, comm) -> dict:
               comm=comm, row_offset=row_off)
     # flow days stream in through a double-buffered prefetcher: the loader's pinned buffers are
     # uploaded on a copy stream while the previous day computes (every step still uploads its day)
-    pf, pinned = None, None
+    pf, pinned, ahead = None, None, None
+    if pcap is not None:
+        from oni355.io.decoders import read_pcap_dns
+        if not a.no_prefetch:
+            # every step decodes its day's pcap; the decode of day k+1 runs on a host thread while
+            # day k computes
+            from oni355.io.staging import HostAhead
+            ahead = HostAhead(read_pcap_dns, pcap)
     if dev.type == "cuda" and not a.no_prefetch and pcap is None:
         from oni355.io.staging import Prefetcher
         if a.source == "flow":
@@ -212,8 +220,7 @@ def run_pipeline_mode(a, comm) -> dict:
         elif a.source == "dns":
             from oni355.pipeline.dns import run_dns
             if pcap is not None:
-                from oni355.io.decoders import read_pcap_dns
-                cols = read_pcap_dns(pcap)
+                cols = ahead.take() if ahead is not None else read_pcap_dns(pcap)
             else:
                 cols = day.cols
             t_dec = time.perf_counter() - t0
@@ -285,7 +292,9 @@ def run_pipeline_mode(a, comm) -> dict:
                    "sweeps_per_step": a.sweeps, "maxresults": a.maxresults, "baseline_config": baseline_cfg},
         "step": "one full oni-ml day run per step: host columns -> H2D -> featurize -> corpus -> "
                 f"{a.sweeps} Gibbs sweeps -> score -> top-{a.maxresults} -> CSV rows"
-                + ("; each step's H2D upload runs on a copy stream during the previous step" if pf is not None else ""),
+                + ("; each step's H2D upload runs on a copy stream during the previous step" if pf is not None else "")
+                + ("; each step's pcap decode runs on a host thread during the previous step" if ahead is not None
+                   else ""),
         "gibbs_iters_per_sec": round(a.sweeps / train_s, 2) if train_s > 0 else None,
         "ms_per_sweep_in_training": round(train_s / a.sweeps * 1e3, 4) if train_s > 0 else None,
         "tokens_per_sec_training": round(tokens * a.sweeps / train_s, 1) if train_s > 0 else None,

@@ -226,3 +226,26 @@ class Prefetcher:
             return None
         self._last[1].synchronize()
         return self._last[0].elapsed_time(self._last[1])
+
+
+class HostAhead:
+    """Run a host-side producer (a decoder: pcap → columns) one item ahead on a worker thread,
+    so decoding day k+1 overlaps the GPU work of day k (SURVEY.md §2.4 P7 "decode ‖ H2D ‖
+    compute"). The C++ decoders release the GIL. ``take()`` returns the next item (waiting for it if
+    needed) and immediately starts producing the one after."""
+
+    def __init__(self, fn, *args, **kw):
+        from concurrent.futures import ThreadPoolExecutor
+        self._fn, self._args, self._kw = fn, args, kw
+        self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="oni-ahead")
+        self._fut = self._pool.submit(fn, *args, **kw)
+
+    def take(self):
+        out = self._fut.result()
+        self._fut = self._pool.submit(self._fn, *self._args, **self._kw)
+        return out
+
+    def close(self) -> None:
+        self._fut.cancel()
+        self._pool.shutdown(wait=True)
+

@@ -94,3 +94,17 @@ def test_push_to_host_kernel_readback(gpu):
     staging.push_to_host(f, fd)
     torch.cuda.synchronize()
     assert torch.equal(fd, f.cpu())
+
+
+def test_host_ahead_produces_in_order_one_ahead():
+    calls = []
+
+    def produce(tag):
+        calls.append(tag)
+        return len(calls)
+
+    ah = staging.HostAhead(produce, "day")
+    assert ah.take() == 1
+    assert ah.take() == 2  # the second item was started when the first was taken
+    ah.close()
+    assert calls[:2] == ["day", "day"]
