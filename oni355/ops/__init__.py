@@ -142,6 +142,60 @@ def quantile_cuts(keys: torch.Tensor, fracs, allreduce=None, n_global: int | Non
     return prefix.astype(np.uint32)
 
 
+def quantile_cuts_multi(keys_list: list, fracs_list: list, allreduce=None, n_global: int | None = None) -> list:
+    """:func:`quantile_cuts` of several key arrays of the same length at once: each radix pass
+    launches every feature's histogram, then ONE read-back (and, with ``allreduce``, one
+    collective) serves them all -- 3 host round trips for a day's features instead of 3 per
+    feature. Results are identical to calling :func:`quantile_cuts` per array."""
+    if not keys_list:
+        return []
+    if not all(_is_dev(k) for k in keys_list):
+        return [quantile_cuts(k, f, allreduce, n_global) for k, f in zip(keys_list, fracs_list)]
+    for k in keys_list:
+        _need(k, torch.int32, "keys")
+    n = keys_list[0].numel() if n_global is None else int(n_global)
+    if n == 0:
+        return [np.zeros(len(f), dtype=np.uint32) for f in fracs_list]
+    L = _lib.lib()
+    dev = keys_list[0].device
+    F = len(keys_list)
+    ranks = [spec.quantile_ranks(n, f).astype(np.int64) for f in fracs_list]
+    prefix = [np.zeros(len(f), dtype=np.uint64) for f in fracs_list]
+    hist_buf = torch.zeros(F * (16 << 11), dtype=torch.int32, device=dev)
+    dev_ar = allreduce is not None and getattr(allreduce, "accepts_tensors", False)
+    for shift, nbits in _PASSES:
+        top = shift + nbits
+        mask = 0 if top >= 32 else (0xFFFFFFFF << top) & 0xFFFFFFFF
+        B = 1 << nbits
+        uq = [np.unique(p, return_inverse=True) for p in prefix]
+        sizes = [len(u) * B for u, _ in uq]
+        offs = np.concatenate([[0], np.cumsum(sizes)])
+        hist = hist_buf[: offs[-1]]
+        hist.zero_()
+        pre_all = torch.from_numpy(np.concatenate([u for u, _ in uq]).astype(np.uint32).view(np.int32)).to(dev)
+        po = np.concatenate([[0], np.cumsum([len(u) for u, _ in uq])])
+        for f in range(F):
+            _lib.check(L.oni_radix_hist(_lib.ptr(keys_list[f]), keys_list[f].numel(), shift, nbits,
+                                        pre_all.data_ptr() + 4 * int(po[f]), len(uq[f][0]), mask,
+                                        hist.data_ptr() + 4 * int(offs[f]), _lib.stream()), "oni_radix_hist")
+        if dev_ar:
+            h_all = np.asarray(allreduce(hist.to(torch.int64) & 0xFFFFFFFF), dtype=np.int64)
+        else:
+            h_all = hist.cpu().numpy().view(np.uint32).astype(np.int64)
+            if allreduce is not None:
+                h_all = np.asarray(allreduce(h_all), dtype=np.int64)
+        for f in range(F):
+            uniq, inv = uq[f]
+            cum = np.cumsum(h_all[offs[f]:offs[f + 1]].reshape(len(uniq), B), axis=1)
+            for qi in range(len(fracs_list[f])):
+                c = cum[inv[qi]]
+                digit = min(int(np.searchsorted(c, ranks[f][qi], side="right")), B - 1)
+                if digit > 0:
+                    ranks[f][qi] -= c[digit - 1]
+                prefix[f][qi] |= np.uint64(digit << shift)
+    return [p.astype(np.uint32) for p in prefix]
+
+
 def bin_keys(keys: torch.Tensor, cuts: np.ndarray) -> torch.Tensor:
     _need(keys, torch.int32, "keys")
     if not _is_dev(keys):

@@ -93,7 +93,9 @@ def featurize(d: dict, comm: Comm | None, topset: HashSet | None, user_domain: s
     if comm is not None and comm.dist:
         ar = comm.allreduce_np
         n_glob = int(comm.allreduce_np(np.array([n], np.int64))[0])
-    cuts = {name: ops.quantile_cuts(keys[name].contiguous(), fr, ar, n_glob) for name, fr, _ in BINNED}
+    cuts = dict(zip([name for name, _, _ in BINNED],
+                    ops.quantile_cuts_multi([keys[name].contiguous() for name, _, _ in BINNED],
+                                            [fr for _, fr, _ in BINNED], ar, n_glob)))
     words = sops.pack_words([keys[name].contiguous() for name, _, _ in BINNED], [cuts[name] for name, _, _ in BINNED],
                             [s for _, _, s in BINNED], [d[name] for name, _, _ in RAW], [m for _, m, _ in RAW],
                             [s for _, _, s in RAW], raw8=top, r8mask=3, r8shift=TOP_SHIFT)

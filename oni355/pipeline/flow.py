@@ -119,8 +119,7 @@ def compute_cuts(d: dict, comm: Comm | None) -> FlowCuts:
     if comm is not None and comm.dist:
         ar = comm.allreduce_np
         n_glob = int(comm.allreduce_np(np.array([n], dtype=np.int64))[0])
-    cuts = FlowCuts(ops.quantile_cuts(tk, spec.DECILES, ar, n_glob), ops.quantile_cuts(bk, spec.DECILES, ar, n_glob),
-                    ops.quantile_cuts(pk, spec.QUINTILES, ar, n_glob))
+    cuts = FlowCuts(*ops.quantile_cuts_multi([tk, bk, pk], [spec.DECILES, spec.DECILES, spec.QUINTILES], ar, n_glob))
     d["_keys"] = (tk, bk, pk)
     return cuts
 
@@ -177,8 +176,8 @@ def run_flow(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxre
         sw, dw = wordify(d, cuts)
     with timer.stage("vocab"):
         n = d["sip"].numel()
-        doc_keys = torch.cat([common.u32_to_i64(d["sip"]), common.u32_to_i64(d["dip"])])
-        word_keys = torch.cat([common.u32_to_i64(sw), common.u32_to_i64(dw)])
+        doc_keys = common.u32_to_i64(torch.cat([d["sip"], d["dip"]]))
+        word_keys = common.u32_to_i64(torch.cat([sw, dw]))
         weights = None
         fb = feedback_tokens(feedback, cuts, device, dupfactor)
         if fb is not None:
@@ -205,9 +204,11 @@ def run_flow(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxre
         with timer.stage("score_prep"):
             dkeys, theta = common.gather_theta(run, comm)
             phi = run.model.phi()
-            sip, dip = common.u32_to_i64(d["sip"]), common.u32_to_i64(d["dip"])
-            plan = common.event_score_plan(run, dkeys, vocab, [sip, dip], wids[: 2 * n],
-                                           [common.u32_to_i64(sw), common.u32_to_i64(dw)], comm)
+            if run.pairs is not None and not common.SCORE_TILES:
+                plan = common.plan_from_pairs(run.pairs, n, 2)  # the corpus pair build holds the plan
+            else:
+                plan = common.event_score_plan(run, dkeys, vocab, [doc_keys[:n], doc_keys[n: 2 * n]], wids[: 2 * n],
+                                               [word_keys[:n], word_keys[n: 2 * n]], comm)
         with timer.stage("score"):
             score, s1, s2 = common.plan_score(theta, phi, plan, tol, hist=hist, want_parts=True)
             rows, scs = common.top_n(score, tol, maxresults, comm, row_offset, hist=hist, order=plan.order)

@@ -161,7 +161,9 @@ def featurize(cols: dict, device, comm: Comm | None, topset, allreduce_counts: b
     if comm is not None and comm.dist:
         ar = comm.allreduce_np
         n_glob = int(comm.allreduce_np(np.array([n], np.int64))[0])
-    cuts = {name: ops.quantile_cuts(keys[name], fr, ar, n_glob) for name, fr, _ in BINNED}
+    cuts = dict(zip([name for name, _, _ in BINNED],
+                    ops.quantile_cuts_multi([keys[name].contiguous() for name, _, _ in BINNED],
+                                            [fr for _, fr, _ in BINNED], ar, n_glob)))
     raws = {"method": _codes_by_hash(cols["reqmethod"], *strcol("reqmethod"), method_code),
             "ctype": _codes_by_hash(cols["resconttype"], *strcol("resconttype"), ctype_class),
             "respcode": d["respcode"]}

@@ -49,6 +49,20 @@ def test_quantile_cuts_exact(gpu, n):
         assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("n", [1, 1000, 1_000_003])
+def test_quantile_cuts_multi_equals_single(gpu, n):
+    """One read-back per radix pass for all features == per-feature cuts == the NumPy oracle."""
+    r = np.random.default_rng(n + 1)
+    xs = [r.normal(size=n).astype(np.float32), r.integers(0, 50, n).astype(np.float32),
+          np.concatenate([r.exponential(size=n // 3), np.full(n - n // 3, 7.0)]).astype(np.float32)]
+    keys = [torch.from_numpy(spec.f32_key(x).view(np.int32)).to(gpu) for x in xs]
+    frs = [spec.DECILES, spec.QUINTILES, spec.DECILES]
+    got = ops.quantile_cuts_multi(keys, frs)
+    for g, k, x, fr in zip(got, keys, xs, frs):
+        assert np.array_equal(g, ops.quantile_cuts(k, fr))
+        assert np.array_equal(g, spec.quantile_cuts(spec.f32_key(x), fr))
+
+
 def _toy_tokens(n_docs, V, seed, heavy=True):
     r = np.random.default_rng(seed)
     lens = r.zipf(1.6, n_docs).clip(1, 3000)
