@@ -50,16 +50,44 @@ __global__ void k_owner_hist(const uint8_t* __restrict__ okey, int64_t n, int W,
     if (h[b]) atomicAdd(&counts[b], (unsigned long long)h[b]);
 }
 
-template <int C>
+// column 0 of a send row: the token's doc key (u32: IPv4 / 32-bit hashes), or with DOCVAL the
+// per-document value doc_val[ids[t]] (the doc's position in the key list sent to its owner)
+template <int C, bool DOCVAL>
 __global__ void k_route_gather(const int32_t* __restrict__ order, const int64_t* __restrict__ keys,
+                               const int32_t* __restrict__ ids, const int32_t* __restrict__ doc_val,
                                const int32_t* __restrict__ word, const int32_t* __restrict__ weight, int64_t n,
                                int32_t* __restrict__ send) {
   const int64_t j = (int64_t)blockIdx.x * kB + threadIdx.x;
   if (j >= n) return;
   const int32_t t = order[j];
-  send[j * C] = (int32_t)(uint32_t)(uint64_t)keys[t];  // doc keys are u32 (IPv4 / 32-bit hashes)
+  if constexpr (DOCVAL) send[j * C] = doc_val[ids[t]];
+  else send[j * C] = (int32_t)(uint32_t)(uint64_t)keys[t];
   send[j * C + 1] = word[t];
   if constexpr (C == 3) send[j * C + 2] = weight[t];
+}
+
+// Owner side of the id routing: row j of the received buffer came from the source rank whose
+// segment [seg[s], seg[s+1]) holds it; its column 0 indexes that source's key list, whose
+// dictionary ids start at kid + koff[s]. Writes the token's owner-local doc id, word and weight.
+__global__ void k_route_unpack(const int32_t* __restrict__ recv, int64_t n, int C, const int64_t* __restrict__ seg,
+                               const int64_t* __restrict__ koff, int W, const int32_t* __restrict__ kid,
+                               int32_t* __restrict__ doc, int32_t* __restrict__ word, int32_t* __restrict__ wt) {
+  __shared__ int64_t s_seg[257];
+  __shared__ int64_t s_koff[256];
+  for (int i = threadIdx.x; i <= W; i += kB) s_seg[i] = seg[i];
+  for (int i = threadIdx.x; i < W; i += kB) s_koff[i] = koff[i];
+  __syncthreads();
+  const int64_t j = (int64_t)blockIdx.x * kB + threadIdx.x;
+  if (j >= n) return;
+  int lo = 0, hi = W - 1;  // last source s with seg[s] <= j
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (s_seg[mid] <= j) lo = mid;
+    else hi = mid - 1;
+  }
+  doc[j] = kid[s_koff[lo] + recv[j * C]];
+  word[j] = recv[j * C + 1];
+  if (wt) wt[j] = C == 3 ? recv[j * C + 2] : 1;
 }
 
 #define ONI_TRY(x)                          \
@@ -74,9 +102,11 @@ __global__ void k_route_gather(const int32_t* __restrict__ order, const int64_t*
 // keys[n]: the documents' u32 keys (int64 storage); word[n]; weight[n] or null.
 // Outputs: send[n * (weight ? 3 : 2)] grouped by owner rank (stable), order[n] (token of each
 // send slot), counts[W] (tokens per owner). W ≤ 256.
-ONI_API int oni_route_pack(const int32_t* owner_of_id, const int32_t* ids, const int64_t* keys, const int32_t* word,
-                           const int32_t* weight, int64_t n, int W, int32_t* send, int32_t* order, int64_t* counts,
-                           void* tmp, size_t* tmp_bytes, hipStream_t s) {
+// doc_val (optional, int32 [U]): column 0 carries doc_val[ids[t]] instead of the token's key.
+static int route_pack_impl(const int32_t* owner_of_id, const int32_t* ids, const int64_t* keys,
+                           const int32_t* doc_val, const int32_t* word, const int32_t* weight, int64_t n, int W,
+                           int32_t* send, int32_t* order, int64_t* counts, void* tmp, size_t* tmp_bytes,
+                           hipStream_t s) {
   if (n >= (int64_t)1 << 31 || W < 1 || W > 256) return (int)hipErrorInvalidValue;
   int bits = 1;
   while (bits < 8 && ((W - 1) >> bits)) ++bits;
@@ -97,9 +127,40 @@ ONI_API int oni_route_pack(const int32_t* owner_of_id, const int32_t* ids, const
   ONI_TRY(hipcub::DeviceRadixSort::SortPairs(cub, sb, okey, osort, iota, order, (int)n, 0, bits, s));
   const unsigned hb = nblk(n) < 1024u ? nblk(n) : 1024u;
   k_owner_hist<<<hb, kB, 0, s>>>(okey, n, W, reinterpret_cast<unsigned long long*>(counts));
-  if (weight)
-    k_route_gather<3><<<nblk(n), kB, 0, s>>>(order, keys, word, weight, n, send);
-  else
-    k_route_gather<2><<<nblk(n), kB, 0, s>>>(order, keys, word, nullptr, n, send);
+  if (doc_val) {
+    if (weight)
+      k_route_gather<3, true><<<nblk(n), kB, 0, s>>>(order, keys, ids, doc_val, word, weight, n, send);
+    else
+      k_route_gather<2, true><<<nblk(n), kB, 0, s>>>(order, keys, ids, doc_val, word, nullptr, n, send);
+  } else {
+    if (weight)
+      k_route_gather<3, false><<<nblk(n), kB, 0, s>>>(order, keys, ids, doc_val, word, weight, n, send);
+    else
+      k_route_gather<2, false><<<nblk(n), kB, 0, s>>>(order, keys, ids, doc_val, word, nullptr, n, send);
+  }
+  return (int)hipGetLastError();
+}
+
+ONI_API int oni_route_pack(const int32_t* owner_of_id, const int32_t* ids, const int64_t* keys, const int32_t* word,
+                           const int32_t* weight, int64_t n, int W, int32_t* send, int32_t* order, int64_t* counts,
+                           void* tmp, size_t* tmp_bytes, hipStream_t s) {
+  return route_pack_impl(owner_of_id, ids, keys, nullptr, word, weight, n, W, send, order, counts, tmp, tmp_bytes, s);
+}
+
+ONI_API int oni_route_pack_ids(const int32_t* owner_of_id, const int32_t* ids, const int32_t* doc_val,
+                               const int32_t* word, const int32_t* weight, int64_t n, int W, int32_t* send,
+                               int32_t* order, int64_t* counts, void* tmp, size_t* tmp_bytes, hipStream_t s) {
+  return route_pack_impl(owner_of_id, ids, nullptr, doc_val, word, weight, n, W, send, order, counts, tmp, tmp_bytes,
+                         s);
+}
+
+// recv[n * C] rows grouped by source rank (seg[W + 1] row offsets), column 0 an index into that
+// source's key list; kid: dictionary id of every entry of the concatenated key lists, koff[W]: the
+// start of each source's list in it. Outputs doc/word (and wt, optional) int32 [n].
+ONI_API int oni_route_unpack(const int32_t* recv, int64_t n, int C, const int64_t* seg, const int64_t* koff, int W,
+                             const int32_t* kid, int32_t* doc, int32_t* word, int32_t* wt, hipStream_t s) {
+  if (W < 1 || W > 256 || (C != 2 && C != 3) || n < 0) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  k_route_unpack<<<nblk(n), kB, 0, s>>>(recv, n, C, seg, koff, W, kid, doc, word, wt);
   return (int)hipGetLastError();
 }

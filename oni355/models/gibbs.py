@@ -28,6 +28,8 @@ from .corpus import Corpus, canonical_tokens
 
 
 NK_REP = 32
+# X01 payload packing pays only once the all-reduce is bandwidth-bound (see GibbsLDA._x01_wanted)
+X01_PACK_MIN_BYTES = 4 << 20
 SAMPLERS = {"pp": 1, "plain": 0, "lds": 2, "qpf": 4, "ldsq": 5, "q2": 6}  # -> oni_gibbs_launch qpf argument
 
 
@@ -158,9 +160,19 @@ class GibbsLDA:
         self._capturing = False
         self._corrupted = False
         self._x01 = None
-        if (comm is not None and comm.dist and self.KS % 2 == 0
-                and os.environ.get("ONI_X01_PACK", "1") != "0"):
+        if comm is not None and comm.dist and self.KS % 2 == 0 and self._x01_wanted():
             self._setup_x01()
+
+    def _x01_wanted(self) -> bool:
+        """``ONI_X01_PACK``: "1" always packs, "0" never, "auto" (default) packs when the dense Δ
+        buffer is at least ``ONI_X01_PACK_MIN_BYTES`` (default 4 MiB). Below that the all-reduce
+        is latency-bound (a 0.46 MB flow-day buffer costs about the same as half of it) and the
+        pack + unpack kernels would be two extra graph nodes per sweep for nothing."""
+        mode = os.environ.get("ONI_X01_PACK", "auto")
+        if mode in ("0", "1"):
+            return mode == "1"
+        min_bytes = int(os.environ.get("ONI_X01_PACK_MIN_BYTES", str(X01_PACK_MIN_BYTES)))
+        return self.dn[0].numel() * self.dn[0].element_size() >= min_bytes
 
     def _setup_x01(self) -> None:
         """Packed X01 payload (csrc/kernels/x01.hip): words whose local token count is at most

@@ -21,6 +21,8 @@ _lib.register_optional("oni_dict_encode", [vp, i64, ci, vp, vp, vp, vp, vp, vp, 
 _lib.register_optional("oni_hashdict_build", [vp, i64, i64, vp, vp, vp, vp, vp])
 _lib.register_optional("oni_hashdict_finish", [vp, i64, ci, i64, vp, vp, vp, i64, vp, vp, vp, _SZ, vp])
 _lib.register_optional("oni_route_pack", [vp, vp, vp, vp, vp, i64, ci, vp, vp, vp, vp, _SZ, vp])
+_lib.register_optional("oni_route_pack_ids", [vp, vp, vp, vp, vp, i64, ci, vp, vp, vp, vp, _SZ, vp])
+_lib.register_optional("oni_route_unpack", [vp, i64, ci, vp, vp, ci, vp, vp, vp, vp, vp])
 _lib.register_optional("oni_pair_build", [vp, vp, vp, i64, i64, i64, vp, vp, vp, vp, vp, vp, i64, vp, _SZ, vp])
 _lib.register_optional("oni_doc_layout", [vp, vp, i64, i64, ci, vp, vp, vp, vp, vp, vp, vp, _SZ, vp])
 _lib.register_optional("oni_chunk_layout", [vp, vp, vp, i64, i64, ci, ci, vp, vp, vp, vp, vp, vp, vp, vp, _SZ, vp])
@@ -127,6 +129,62 @@ def route_pack(owner_of_id: torch.Tensor, ids: torch.Tensor, keys64: torch.Tenso
           _p(weight.to(torch.int32).contiguous()) if weight is not None else None, n, int(world), _p(send),
           _p(order), _p(counts))
     return send, order[:n], counts
+
+
+def route_pack_ids(owner_of_id: torch.Tensor, ids: torch.Tensor, doc_val: torch.Tensor, word: torch.Tensor,
+                   weight: torch.Tensor | None, world: int):
+    """:func:`route_pack` whose column 0 carries ``doc_val[ids[t]]`` (int32 per local document:
+    its index in the key list sent to the owner) instead of the token's doc key."""
+    n = ids.numel()
+    for t, nm in ((owner_of_id, "owner_of_id"), (ids, "ids"), (doc_val, "doc_val"), (word, "word")):
+        if t.dtype != torch.int32 or not t.is_contiguous():
+            raise TypeError(f"route_pack_ids: {nm} must be contiguous int32")
+    if doc_val.numel() != owner_of_id.numel():
+        raise ValueError("route_pack_ids: doc_val and owner_of_id cover different documents")
+    if word.numel() != n or (weight is not None and weight.numel() != n):
+        raise ValueError("route_pack_ids: token arrays differ in length")
+    if not 1 <= world <= 256:
+        raise ValueError("route_pack_ids: 1 <= world <= 256")
+    dev = ids.device
+    C = 3 if weight is not None else 2
+    send = torch.empty((n, C), dtype=torch.int32, device=dev)
+    order = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    counts = torch.empty(world, dtype=torch.int64, device=dev)
+    _call("oni_route_pack_ids", _p(owner_of_id), _p(ids), _p(doc_val), _p(word),
+          _p(weight.to(torch.int32).contiguous()) if weight is not None else None, n, int(world), _p(send),
+          _p(order), _p(counts))
+    return send, order[:n], counts
+
+
+def route_unpack(recv: torch.Tensor, recv_counts: list, key_counts: list, kid: torch.Tensor, weights: bool):
+    """Owner side of :func:`route_pack_ids`: ``recv`` [n, C] int32 rows grouped by source rank
+    (``recv_counts`` rows each), column 0 an index into that source's key list (``key_counts``
+    entries each, concatenated in rank order; ``kid`` = dictionary id of every entry). Returns
+    (doc id, word id, weight) int32 [n] (weight all ones without ``weights``)."""
+    W = len(recv_counts)
+    if len(key_counts) != W or not 1 <= W <= 256:
+        raise ValueError("route_unpack: one count per source rank, 1 <= world <= 256")
+    if recv.dtype != torch.int32 or recv.dim() != 2 or not recv.is_contiguous():
+        raise TypeError("route_unpack: recv must be contiguous int32 [n, C]")
+    n, C = int(recv.shape[0]), int(recv.shape[1])
+    if n != sum(int(x) for x in recv_counts) or kid.numel() < sum(int(x) for x in key_counts):
+        raise ValueError("route_unpack: counts do not match the buffers")
+    if kid.dtype != torch.int32 or not kid.is_contiguous():
+        raise TypeError("route_unpack: kid must be contiguous int32")
+    dev = recv.device
+    seg = [0]
+    for x in recv_counts:
+        seg.append(seg[-1] + int(x))
+    koff = [0]
+    for x in key_counts[:-1]:
+        koff.append(koff[-1] + int(x))
+    meta = torch.tensor(seg + koff, dtype=torch.int64).to(dev, non_blocking=True)
+    doc = torch.empty(n, dtype=torch.int32, device=dev)
+    word = torch.empty(n, dtype=torch.int32, device=dev)
+    wt = torch.empty(n, dtype=torch.int32, device=dev)
+    _lib.check(_lib.lib().oni_route_unpack(_p(recv), n, C, _p(meta), _lib.ptr(meta) + 8 * (W + 1), W, _p(kid),
+                                           _p(doc), _p(word), _p(wt), _lib.stream()), "oni_route_unpack")
+    return doc, word, wt
 
 
 @dataclass

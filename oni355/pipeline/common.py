@@ -118,7 +118,7 @@ def place_docs(doc_keys64: torch.Tensor, weights: torch.Tensor | None, comm: Com
     Deterministic on every rank (same candidate set and counts; order count desc, key asc; ties →
     lowest rank); results stay world-size invariant because the sampler's chain never depends on
     placement. Returns the owner of every token, or with ``per_doc`` (owner of every local
-    document int32, document id of every token int32)."""
+    document int32, document id of every token int32, sorted unique local doc keys int64)."""
     W = comm.world
     dev = doc_keys64.device
     if doc_keys64.is_cuda:
@@ -158,7 +158,7 @@ def place_docs(doc_keys64: torch.Tensor, weights: torch.Tensor | None, comm: Com
     uown = iown[nc:][hb]
     uown[pos[hit]] = iown[:nc][hit]
     if per_doc:
-        return uown.to(torch.int32), inv
+        return uown.to(torch.int32), inv, ukeys
     return uown[inv.long()]
 
 
@@ -178,29 +178,58 @@ class Route:
 @traced("oni:route_to_owners")
 def route_to_owners(doc_keys64: torch.Tensor, word_ids: torch.Tensor, weights: torch.Tensor | None,
                     comm: Comm | None):
-    """Send each token to its document's owner rank (alltoallv of packed int32 columns: 8 B per
-    token, 12 B with weights). Returns local (doc keys int64, word ids int32, weights int32, Route)."""
+    """Send each token to its document's owner rank and dictionary-encode the owner's documents.
+
+    Returns (sorted unique owner-local doc keys int64, doc id int32, word id int32, weight int32
+    of every received token, Route) -- what ``encode_docs`` of the received keys would give.
+
+    GPU: the sender already holds its documents' dictionary (:func:`place_docs`), so each owner
+    gets the sorted list of the document keys it owns from every source (one small alltoallv,
+    ≤ the local distinct documents) and the tokens carry an index into that list (packed int32
+    columns: 8 B per token, 12 B with weights). The owner then dictionary-encodes only the
+    concatenated key lists (Σ per-source distinct docs, not its ~T/W tokens) and maps every token
+    through them in one kernel (``route_unpack``). CPU: the tokens carry their keys."""
     if comm is None or not comm.dist:
         w = weights if weights is not None else torch.ones_like(word_ids, dtype=torch.int32)
-        return doc_keys64, word_ids, w, None
+        udoc, inv = encode_docs(doc_keys64)
+        return udoc, inv, word_ids, w, None
     if doc_keys64.is_cuda:
         from ..ops import corpus as oc
-        uown, ids = place_docs(doc_keys64, weights, comm, per_doc=True)
-        send, order, counts = oc.route_pack(uown, ids, doc_keys64.contiguous(), word_ids.to(torch.int32).contiguous(),
-                                            weights, comm.world)
-    else:
-        owner = place_docs(doc_keys64, weights, comm)
-        order = torch.argsort(owner, stable=True)
-        counts = torch.bincount(owner, minlength=comm.world)
-        cols = [i64_to_u32bits(doc_keys64[order]), word_ids[order].to(torch.int32)]
-        if weights is not None:
-            cols.append(weights[order].to(torch.int32))
-        send = torch.stack(cols, 1).contiguous()
+        uown, ids, ukeys = place_docs(doc_keys64, weights, comm, per_doc=True)
+        U = int(ukeys.numel())
+        # key lists per owner: the local docs grouped by owner, ascending keys inside a group
+        kperm = torch.argsort(uown, stable=True)
+        kcounts = torch.bincount(uown.long(), minlength=comm.world)
+        kstart = _excl_cumsum(kcounts)
+        pos = torch.empty(U, dtype=torch.int32, device=ukeys.device)
+        pos[kperm] = (torch.arange(U, dtype=torch.int64, device=ukeys.device)
+                      - kstart[uown[kperm].long()]).to(torch.int32)
+        ksend = i64_to_u32bits(ukeys[kperm]).to(torch.int32).contiguous()
+        send, order, counts = oc.route_pack_ids(uown, ids, pos, word_ids.to(torch.int32).contiguous(),
+                                                weights, comm.world)
+        # both count vectors travel in one small exchange, then the two payload alltoallvs
+        sc = torch.stack([counts.to(torch.int64), kcounts.to(torch.int64)], 1).reshape(-1).contiguous()
+        rcm = comm.alltoallv(sc.view(comm.world, 2), [1] * comm.world, recv_counts=[1] * comm.world).reshape(-1).tolist()
+        rc, krc = rcm[0::2], rcm[1::2]
+        scl, kcl = counts.tolist(), kcounts.tolist()
+        rkeys = comm.alltoallv(ksend, kcl, recv_counts=krc)
+        recv = comm.alltoallv(send, scl, recv_counts=rc)
+        udoc, kid = encode_docs(u32_to_i64(rkeys.view(-1)).contiguous())
+        inv, wi, wt = oc.route_unpack(recv.contiguous(), rc, krc, kid, weights is not None)
+        return udoc, inv, wi, wt, Route(order, scl, rc)
+    owner = place_docs(doc_keys64, weights, comm)
+    order = torch.argsort(owner, stable=True)
+    counts = torch.bincount(owner, minlength=comm.world)
+    cols = [i64_to_u32bits(doc_keys64[order]), word_ids[order].to(torch.int32)]
+    if weights is not None:
+        cols.append(weights[order].to(torch.int32))
+    send = torch.stack(cols, 1).contiguous()
     recv, rc = comm.alltoallv(send, counts, return_recv_counts=True)
     dk = u32_to_i64(recv[:, 0])
     wi = recv[:, 1].contiguous()
     wt = recv[:, 2].contiguous() if weights is not None else torch.ones_like(wi)
-    return dk, wi, wt, Route(order, counts.tolist(), rc)
+    udoc, inv = encode_docs(dk)
+    return udoc, inv, wi, wt, Route(order, counts.tolist(), rc)
 
 
 def return_to_origin(x: torch.Tensor, route: Route, comm: Comm) -> torch.Tensor:
@@ -253,8 +282,7 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
         if word_ids is None:
             word_ids = torch.searchsorted(vocab, word_keys64).to(torch.int32)
         use_w = weights is not None
-        dk, wi, wt, route = route_to_owners(doc_keys64, word_ids, weights, comm)
-        udoc, inv = encode_docs(dk)
+        udoc, inv, wi, wt, route = route_to_owners(doc_keys64, word_ids, weights, comm)
         G, _ = ops.choose_tiling(K)
         if chunk_len <= 0:
             T_glob = float(wt.sum()) if wt.numel() else 0.0
@@ -629,15 +657,19 @@ def run_single_doc_events(doc_keys64: torch.Tensor, word_keys64: torch.Tensor, K
     mine = (loc >= 0) & (loc < doc_keys64.numel())
     words = word_keys64[loc[mine]]
     if comm is not None and comm.dist:
-        gid_all = torch.cat(comm.allgather_var(rows[mine]))
-        words = torch.cat(comm.allgather_var(words))
-        pos = {int(g): i for i, g in enumerate(gid_all.tolist())}
-        words = words.cpu()[torch.tensor([pos[int(g)] for g in rows.tolist()], dtype=torch.int64)]
+        allp = torch.cat(comm.allgather_var(torch.stack([rows[mine].to(torch.int64), words.to(torch.int64)], 1))).cpu()
+        words = allp[rows_in_order(allp[:, 0], rows.cpu()), 1]
     stats = run.corpus.stats()
     stats.update({"events": int(doc_keys64.numel()),
                   "loglik": run.model.likelihoods[-1][1] if run.model.likelihoods else None})
     return SingleResult(rows=rows.cpu().numpy(), scores=scs.cpu().numpy(),
                         words=words.cpu().numpy().view(np.uint64), timings=t, stats=stats, lda=run)
+
+
+def rows_in_order(gid_all: torch.Tensor, rows: torch.Tensor) -> torch.Tensor:
+    """Index of every id of ``rows`` in ``gid_all`` (a permutation of the same distinct ids)."""
+    o = torch.argsort(gid_all)
+    return o[torch.searchsorted(gid_all[o], rows)]
 
 
 def _top_n_from_hist(score, hist, tol, maxresults, comm, row_offset, order=None):
@@ -663,8 +695,10 @@ def _top_n_from_hist(score, hist, tol, maxresults, comm, row_offset, order=None)
     o2 = torch.argsort(sc, stable=True)
     gid, sc = gid[o2][:maxresults], sc[o2][:maxresults]
     if comm is not None and comm.dist:
-        gid = torch.cat(comm.allgather_var(gid))
-        sc = torch.cat(comm.allgather_var(sc))
+        # one all-gather of (global id, score bits) pairs
+        both = torch.cat(comm.allgather_var(torch.stack([gid.to(torch.int64),
+                                                         sc.view(torch.int32).to(torch.int64)], 1)))
+        gid, sc = both[:, 0].contiguous(), both[:, 1].to(torch.int32).view(torch.float32)
         o1 = torch.argsort(gid, stable=True)
         gid, sc = gid[o1], sc[o1]
         o2 = torch.argsort(sc, stable=True)

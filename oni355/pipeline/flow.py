@@ -223,13 +223,14 @@ def run_flow(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxre
     parts = torch.stack([s1[pi], s2[pi]], 1) if s1 is not None else torch.zeros(0, 2)
     wparts = torch.stack([sw[li], dw[li]], 1)
     if comm is not None and comm.dist:
-        gid_all = torch.cat(comm.allgather_var(rows[mine]))
-        parts = torch.cat(comm.allgather_var(parts))
-        wparts = torch.cat(comm.allgather_var(wparts))
-        pos = {int(g): i for i, g in enumerate(gid_all.tolist())}
-        order = torch.tensor([pos[int(g)] for g in rows.tolist()], dtype=torch.int64)
-        parts = parts.cpu()[order]
-        wparts = wparts.cpu()[order]
+        # one all-gather of (global row id, both parts' f32 bits, both words) for this rank's rows
+        packed = torch.cat([rows[mine].to(torch.int64).view(-1, 1), parts.to(torch.float32).view(torch.int32).to(torch.int64),
+                            wparts.to(torch.int64) & common.U32MASK], 1)
+        allp = torch.cat(comm.allgather_var(packed.contiguous())).cpu()
+        order = common.rows_in_order(allp[:, 0], rows.cpu())
+        allp = allp[order]
+        parts = allp[:, 1:3].to(torch.int32).view(torch.float32)
+        wparts = allp[:, 3:5].to(torch.int32)
     stats = run.corpus.stats()
     stats.update({"n_flows": n, "loglik": run.model.likelihoods[-1][1] if run.model.likelihoods else None})
     return FlowResult(rows=rows.cpu().numpy(), scores=scs.cpu().numpy(), src_scores=parts[:, 0].cpu().numpy(),

@@ -54,8 +54,9 @@ def _run_world(world, n_total, env=None):
     return res
 
 
-@pytest.mark.parametrize("world,env", [(2, None), (3, None), (3, {"ONI_X01_LIGHT_MAX": "40"}),
-                                       (2, {"ONI_X01_PACK": "0"})])
+@pytest.mark.parametrize("world,env", [(2, None), (3, None), (2, {"ONI_X01_PACK": "1"}),
+                                       (3, {"ONI_X01_PACK": "1", "ONI_X01_LIGHT_MAX": "40"}),
+                                       (2, {"ONI_X01_PACK": "auto", "ONI_X01_PACK_MIN_BYTES": "0"})])
 def test_dp_matches_single_process(world, env):
     """Also with the packed X01 payload forced into a light/heavy word mix, and unpacked."""
     n = 6000
@@ -138,3 +139,53 @@ def test_x01_packed_sum_is_exact(W):
     back = torch.zeros(V * KS + tail, dtype=torch.int32)
     ops.x01_unpack(summed, light, heavy, KS, V * KS, tail, W * O, back)
     assert torch.equal(back.to(torch.int64), total)
+
+
+def _single_worker(rank, world, port, source, n_total, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from oni355.parallel import comm as pc
+    from oni355.store.columnar import StringColumn
+    comm = pc.init_from_env("cpu") if world > 1 else None
+    if source == "dns":
+        from oni355.pipeline.dns import run_dns as run
+        from oni355.synth.dns import generate_dns as gen
+        K = 10
+    else:
+        from oni355.pipeline.proxy import run_proxy as run
+        from oni355.synth.proxy import generate_proxy as gen
+        K = 20
+    cols = gen(n_total, seed=4).cols
+    per = n_total // world
+    lo = rank * per
+    hi = n_total if rank == world - 1 else lo + per
+    cols = {k: (v.slice(lo, hi) if isinstance(v, StringColumn) else v[lo:hi]) for k, v in cols.items()
+            if not k.startswith("_")}
+    res = run(cols, K=K, sweeps=4, maxresults=120, device="cpu", comm=comm, row_offset=lo)
+    if rank == 0:
+        out_q.put((res.rows, res.scores, res.words))
+    if comm is not None:
+        comm.barrier()
+        pc.shutdown()
+
+
+@pytest.mark.parametrize("source", ["dns", "proxy"])
+def test_dns_proxy_dp_matches_single_process(source):
+    """DNS / proxy (one token per event, owner-side scoring, result words gathered from the rank
+    that holds each row) on 2 gloo ranks == one process: rows, scores and words."""
+    ctx = mp.get_context("spawn")
+    out = []
+    for world in (1, 2):
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_single_worker, args=(r, world, port, source, 5000, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        out.append(q.get(timeout=600))
+        for p in procs:
+            p.join(timeout=120)
+            assert p.exitcode == 0
+    (r1, s1, w1), (r2, s2, w2) = out
+    assert r1.size > 0
+    assert np.array_equal(r1, r2) and np.array_equal(s1, s2) and np.array_equal(w1, w2)

@@ -126,6 +126,52 @@ def test_route_pack_is_stable_owner_partition(gpu, n, W, weighted):
     assert torch.equal(send.cpu(), torch.stack(cols, 1))
 
 
+@pytest.mark.parametrize("W,weighted", [(1, False), (3, True), (8, False)])
+def test_route_ids_unpack_equals_key_routing(gpu, W, weighted):
+    """Id routing (route_pack_ids at every source + key lists + route_unpack at the owner) gives
+    the owner exactly encode_docs() of the doc keys it would have received, with the same words
+    and weights in the same row order. W source ranks are simulated on one device."""
+    r = np.random.default_rng(W)
+    uni = np.unique(r.integers(0, 2**32, 50_000, dtype=np.int64))
+    srcs = []
+    for s_ in range(W):
+        n = int(r.integers(100_000, 300_000))
+        keys = torch.from_numpy(uni[(r.zipf(1.3, n) - 1) % uni.size]).to(gpu)
+        word = torch.from_numpy(r.integers(0, 10**5, n).astype(np.int32)).to(gpu)
+        wt = torch.from_numpy(r.integers(1, 5, n).astype(np.int32)).to(gpu) if weighted else None
+        ukeys, ids = oc.dict_encode(keys, 32)
+        own = ((ukeys * 0x9E3779B1 & 0xFFFFFFFF) >> 16) % W
+        uown = own.to(torch.int32).contiguous()
+        kperm = torch.argsort(uown, stable=True)
+        kcnt = torch.bincount(uown.long(), minlength=W)
+        kst = torch.cat([torch.zeros(1, dtype=torch.int64, device=gpu), torch.cumsum(kcnt, 0)])
+        pos = torch.empty_like(uown)
+        pos[kperm] = (torch.arange(ukeys.numel(), device=gpu) - kst[uown[kperm].long()]).to(torch.int32)
+        send, order, counts = oc.route_pack_ids(uown, ids, pos, word, wt, W)
+        ref_send, ref_order, ref_counts = oc.route_pack(uown, ids, keys, word, wt, W)
+        assert torch.equal(order, ref_order) and torch.equal(counts, ref_counts)
+        assert torch.equal(send[:, 1:], ref_send[:, 1:])
+        srcs.append((send, counts.tolist(), ukeys[kperm], kcnt.tolist(), ref_send))
+    for o in range(W):
+        rows, rc, klists, krc, ref_rows = [], [], [], [], []
+        for send, counts, klist, kcnt, ref_send in srcs:
+            a = sum(counts[:o])
+            rows.append(send[a:a + counts[o]])
+            ref_rows.append(ref_send[a:a + counts[o]])
+            rc.append(counts[o])
+            b = sum(kcnt[:o])
+            klists.append(klist[b:b + kcnt[o]])
+            krc.append(kcnt[o])
+        recv = torch.cat(rows).contiguous()
+        udoc, kid = oc.dict_encode(torch.cat(klists).contiguous(), 32)
+        doc, word, wt = oc.route_unpack(recv, rc, krc, kid, weighted)
+        ref = torch.cat(ref_rows)
+        rdoc_u, rdoc = oc.dict_encode(common.u32_to_i64(ref[:, 0]).contiguous(), 32)
+        assert torch.equal(udoc, rdoc_u) and torch.equal(doc, rdoc)
+        assert torch.equal(word, ref[:, 1])
+        assert torch.equal(wt, ref[:, 2] if weighted else torch.ones_like(word))
+
+
 @pytest.mark.parametrize("n,distinct,bits", [(1 << 20, 6000, 30), (3_000_001, 400_000, 32), (2_000_000, 3, 8),
                                              (1_500_000, 1_400_000, 40), (25_000_000, 5733, 29)])
 def test_hash_dictionary_equals_sort_path(gpu, n, distinct, bits):
