@@ -219,12 +219,9 @@ def format_events(source: str, cols: dict, local_rows, words, scores) -> Rendere
     return _native_format(f, rows.size)
 
 
-def render_result(source: str, cols: dict, res, row_off: int, comm=None) -> Rendered:
-    """Result rows of a pipeline run (FlowResult / SingleResult) as CSV text, ascending score.
-
-    Each rank formats the result rows it holds (``cols`` is its shard, starting at global row
-    ``row_off``) with the native formatter; with a process group the formatted rows are gathered
-    (collective X06's payload) and every rank returns the full, globally ordered text."""
+def render_local(source: str, cols: dict, res, row_off: int):
+    """(global row ids, Rendered) of the result rows this rank holds (``cols`` is its shard,
+    starting at global row ``row_off``), formatted by the native formatter. No collectives."""
     rows_local = res.rows - row_off
     if source == "flow":
         mine = (rows_local >= 0) & (rows_local < len(cols["sip"]))
@@ -235,19 +232,77 @@ def render_result(source: str, cols: dict, res, row_off: int, comm=None) -> Rend
         mine = (rows_local >= 0) & (rows_local < ncol)
         rendered = format_events(source, cols, rows_local[mine], (res.words[mine], word_fields(source)),
                                  res.scores[mine])
+    return res.rows[mine], rendered
+
+
+def gather_rendered(all_rows: np.ndarray, gids: np.ndarray, rendered: Rendered, comm=None) -> Rendered:
+    """Merge every rank's locally rendered rows into the full text in ``all_rows`` order (collective
+    X06's payload; every rank returns it). Identity without a process group."""
     if comm is None or not comm.dist:
         return rendered
     import torch.distributed as dist
-    gids = res.rows[mine].tolist()
     allp = [None] * comm.world
-    dist.all_gather_object(allp, (gids, rendered.blob, rendered.ends), group=comm.group)
+    dist.all_gather_object(allp, (np.asarray(gids, dtype=np.int64).tolist(), rendered.blob, rendered.ends),
+                           group=comm.group)
     by_gid = {}
     for gl, blob, ends in allp:
         for g, line in zip(gl, Rendered(blob, ends).lines()):
             by_gid[g] = line
-    lines = [by_gid[int(g)] for g in res.rows.tolist()]
+    lines = [by_gid[int(g)] for g in np.asarray(all_rows).tolist()]
     ends = np.cumsum([len(x) for x in lines]).astype(np.int64) if lines else np.zeros(0, np.int64)
     return Rendered(b"".join(lines), ends)
+
+
+def render_result(source: str, cols: dict, res, row_off: int, comm=None) -> Rendered:
+    """Result rows of a pipeline run (FlowResult / SingleResult) as CSV text, ascending score.
+
+    Each rank formats the result rows it holds with the native formatter; with a process group the
+    formatted rows are gathered and every rank returns the full, globally ordered text."""
+    gids, rendered = render_local(source, cols, res, row_off)
+    return gather_rendered(res.rows, gids, rendered, comm)
+
+
+class ResultPipe:
+    """Day-pipelined result output: day k's rows are formatted on a worker thread while day k+1
+    computes; the cross-rank gather and the write of day k happen on the caller's thread at the
+    next :meth:`submit` / :meth:`drain`, so every rank issues its collectives in program order.
+
+    ``write(rendered)`` is called with each day's full text (on every rank; rank 0 usually
+    writes). The native formatter runs outside the GIL."""
+
+    def __init__(self, source: str, comm=None, write=None):
+        from concurrent.futures import ThreadPoolExecutor
+
+        self.source = source
+        self.comm = comm
+        self.write = write
+        self._pool = ThreadPoolExecutor(1, thread_name_prefix="oni-results")
+        self._pending = None  # (future of (gids, Rendered), all result rows)
+
+    def submit(self, cols: dict, res, row_off: int) -> None:
+        """Queue this day's formatting; finishes the previous day first."""
+        self._finish()
+        fut = self._pool.submit(render_local, self.source, cols, res, row_off)
+        self._pending = (fut, res.rows)
+
+    def _finish(self):
+        if self._pending is None:
+            return None
+        fut, rows = self._pending
+        self._pending = None
+        gids, rendered = fut.result()
+        full = gather_rendered(rows, gids, rendered, self.comm)
+        if self.write is not None:
+            self.write(full)
+        return full
+
+    def drain(self):
+        """Finish the last queued day (its full Rendered text, or None)."""
+        return self._finish()
+
+    def close(self) -> None:
+        self._finish()
+        self._pool.shutdown(wait=True)
 
 
 def word_fields(source: str) -> list[tuple[int, int]]:

@@ -81,3 +81,28 @@ def test_native_event_rendering_many_rows_matches_spec():
         got = rio.format_events(src, day.cols, rows, (w, rio.word_fields(src)), sc)
         assert got.rows() == rio.event_rows(src, day.cols, rows, [ws(x) for x in w], sc)
         assert len(got) == rows.size and got.ends[-1] == len(got.blob)
+
+
+def test_result_pipe_writes_each_day_like_render_result():
+    """ResultPipe (format on a worker thread, gather + write at the next submit / drain) emits
+    exactly render_result's text for every day, in day order."""
+    from types import SimpleNamespace
+
+    day = generate_flows(2000, seed=6)
+    r = np.random.default_rng(1)
+    days = []
+    for k in range(3):
+        n = 50 + 10 * k
+        rows = r.choice(2000, n, replace=False).astype(np.int64)
+        s = np.sort(r.random(n).astype(np.float32))
+        days.append(SimpleNamespace(rows=rows, scores=s, src_scores=s, dst_scores=s + 1,
+                                    src_words=r.integers(0, 1 << 29, n).astype(np.uint32),
+                                    dst_words=r.integers(0, 1 << 29, n).astype(np.uint32)))
+    out = []
+    pipe = rio.ResultPipe("flow", None, write=out.append)
+    for res in days:
+        pipe.submit(day.cols, res, 0)
+    assert len(out) == 2
+    assert pipe.drain() is not None and pipe.drain() is None
+    pipe.close()
+    assert [o.blob for o in out] == [rio.render_result("flow", day.cols, res, 0).blob for res in days]
