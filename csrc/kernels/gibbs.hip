@@ -135,7 +135,7 @@ __device__ __forceinline__ void mark_changed_w(const OniGibbs& a, int32_t p, int
 //       3 = changed topics also scattered into the word-sorted copy z_w (streaming recount afterwards)
 //       4 = changed tokens marked in a word-sorted bitmap + (old, new) topic copies (k_wdelta_recount)
 template <int G, int KP, bool INIT, int MODE, bool QPF>
-__global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_gibbs(const OniGibbs a) {
   constexpr bool ATOMIC = MODE == 1;
   constexpr int S = oni::kWave / G;
   constexpr int KS = G * KP;
@@ -166,6 +166,9 @@ __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
 
   oni::U4 r{0, 0, 0, 0};
   uint32_t wprev = oni::kPadWord;
+  // QPF: qn always holds the q row of the current token's word (it is refilled at the end of a
+  // step only when the next word differs, so a repeated word finds its row still there) and the
+  // math reads it directly; without QPF qv holds the row loaded on a word change
   float qv[KP];
 #pragma unroll
   for (int j = 0; j < KP; ++j) qv[j] = 0.f;
@@ -209,20 +212,17 @@ __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
     } else {
 #pragma unroll
       for (int j = 0; j < KP; ++j) n[j] -= (kbase + j == zo);
-      if (w != wprev) {
-        if (QPF) {
-#pragma unroll
-          for (int j = 0; j < KP; ++j) qv[j] = qn[j];
-        } else {
+      if constexpr (!QPF) {
+        if (w != wprev) {
           load_row_f<KP>(a.q + (int64_t)w * KS + kbase, qv);
+          wprev = w;
         }
-        wprev = w;
       }
       float loc[KP];
       float run = 0.f;
 #pragma unroll
       for (int j = 0; j < KP; ++j) {
-        run = run + ((float)n[j] + a.alpha) * qv[j];
+        run = run + ((float)n[j] + a.alpha) * (QPF ? qn[j] : qv[j]);
         loc[j] = run;
       }
       float excl = 0.f, total = run;
@@ -323,7 +323,7 @@ __global__ __launch_bounds__(kBlock) void k_gibbs(const OniGibbs a) {
 // before step s's math and stores, and waited for only when the step ends. Same arithmetic as
 // k_gibbs (mul + add chain), so the same draws bitwise.
 template <int KP, int MODE>
-__global__ __launch_bounds__(kBlock) void k_gibbs_q2(const OniGibbs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_gibbs_q2(const OniGibbs a) {
   constexpr bool ATOMIC = MODE == 1;
   constexpr int S = oni::kWave;
   constexpr int KS = KP;
