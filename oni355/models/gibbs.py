@@ -128,7 +128,17 @@ class GibbsLDA:
         self._chg_q: list = []    # (sweep index, host buffer, event) of pending change-count copies
         self.T_global = corpus.T
         self.change_log: list[tuple[int, float]] = []
-        if self.mode == 3:
+        # auto's early (high change rate) sweeps: "recount" (0, default) rebuilds n_wk by the
+        # gathered recount; "dual" (3) keeps a word-sorted z copy current for changed tokens so the
+        # recount streams it (1 B per token) -- measured slower on the 12.5M-flow day (0.2673 ->
+        # 0.2718 ms/sweep: the sampler's scattered byte stores cost more than the gather saves).
+        # ONI_AUTO_EARLY overrides.
+        early = os.environ.get("ONI_AUTO_EARLY", "recount")
+        if early not in ("dual", "recount"):
+            raise ValueError(f"unknown ONI_AUTO_EARLY {early}")
+        self.early = 3 if (self.auto and self.mode == 4 and early == "dual") else 0
+        self._zw_synced = False  # z_w == tok_z in word-sorted order
+        if self.mode == 3 or self.early == 3:
             self.z_w = torch.zeros(max(corpus.T, 1), dtype=torch.uint8, device=dev)
         if self.mode == 4:
             # word-sorted change bitmap (+ slack word) and (old | new << 8) of each changed token;
@@ -245,8 +255,8 @@ class GibbsLDA:
             return self._force_mode
         if self.auto:
             if self.cfg.auto_switch > 0:
-                return 0 if sweep < self.cfg.auto_switch else self.mode
-            return self.mode if self._delta_on else 0
+                return self.early if sweep < self.cfg.auto_switch else self.mode
+            return self.mode if self._delta_on else self.early
         return self.mode
 
     def _note_changes(self) -> None:
@@ -280,6 +290,12 @@ class GibbsLDA:
                 self._delta_on = True
                 self._chg_q.clear()
 
+    def _ensure_zw(self) -> None:
+        """Word-sorted z copy := tok_z before a dual-mode (3) sweep (eager, never captured)."""
+        if not self._zw_synced and self.c.T:
+            self.z_w[: self.c.T] = self.tok_z[self.c.wslot.long()]
+        self._zw_synced = True
+
     def _sync_aux_z(self) -> None:
         """Bring the auxiliary topic copies (z_prev / word-sorted z) in line with tok_z."""
         if self.mode == 2:
@@ -296,6 +312,7 @@ class GibbsLDA:
 
     def _prime(self) -> None:
         # zero-delta apply: q from n_wk, nk[1] = nk[0]; leaves dn[0], dn[1] zero
+        self._zw_synced = False  # tok_z was (re)written outside the sweeps (init / restore)
         VK = self.V * self.KS
         self.dn[0].zero_()
         ops.gibbs_apply(self.nwk, self.dn[0], self.dn[1], self.nk[self.cn], self.nk[1 - self.cn], self.q, self.V,
@@ -312,6 +329,8 @@ class GibbsLDA:
         if mode == self.mode and mode in (2, 4) and not self._aux_synced:
             self._sync_aux_z()  # entering a delta mode: z_prev / z_w := z (eager, outside graphs)
         self._aux_synced = self._keeps_aux(mode)
+        if mode == 3 and not self._capturing:
+            self._ensure_zw()
         # long (chunked) documents add their Δn_dk into ndk[1-a] rows that hold a copy of ndk[a]:
         # every apply -- the previous sweep's, or _prime()'s after init / resume -- seeds that copy
         ops.gibbs_pass(self._state(False), self.G, self.KP, self.K, self.alpha, self.cfg.seed, False,
@@ -340,6 +359,8 @@ class GibbsLDA:
                         absolute=mode in (0, 3), rows_copy=(self.ndk[1 - self.a], self.ndk[self.a], c.long_rows))
         self.a, self.b, self.cn = 1 - self.a, 1 - self.b, 1 - self.cn
         self.sweeps_done += 1
+        if not self._capturing:
+            self._zw_synced = mode == 3
 
     def _allreduce_dn(self, buf: torch.Tensor) -> None:
         """X01: all-reduce of the sweep's Δ buffer (Δn_wk ‖ Δn_k replicas ‖ aux words).
@@ -514,6 +535,8 @@ class GibbsLDA:
                 continue
             if m1 == self.mode and m1 in (2, 4) and not self._aux_synced:
                 self._sync_aux_z()
+            if m1 == 3:
+                self._ensure_zw()
             entry = self._graphs.get(m1)
             if entry is not None and entry[1] != (self.a, self.b, self.cn):
                 self._one_sweep()  # realign parities with the captured pair
@@ -522,12 +545,13 @@ class GibbsLDA:
                 continue
             if entry is None:
                 entry = self._capture(m1)
-                if self.auto and self.cfg.auto_switch == 0 and m1 == 0 and self.mode not in self._graphs:
+                if self.auto and self.cfg.auto_switch == 0 and m1 == self.early and self.mode not in self._graphs:
                     self._capture(self.mode)  # capture the delta pair now: no capture stall at the switch
             self._graph = entry[0]
             entry[0].replay()
             self.sweeps_done += 2
             self._aux_synced = self._keeps_aux(m1)
+            self._zw_synced = m1 == 3
             self._note_changes()
             done += 2
             if self._watchdog is not None:

@@ -245,3 +245,27 @@ def test_wdelta_count_mode_matches_recount():
         m.sweep(5)
     assert torch.equal(a.tok_z, b.tok_z) and torch.equal(a.nwk, b.nwk) and torch.equal(a.nk_cur, b.nk_cur)
     assert not bool(a.wbits.any())  # the recount clears every bit it consumed
+
+
+def test_auto_with_dual_early_sweeps_matches_recount(monkeypatch):
+    """ONI_AUTO_EARLY=dual (word-sorted z copy kept current in the early sweeps, streamed recount)
+    leaves the chain bitwise equal to the plain recount mode."""
+    import torch
+
+    from oni355.models.corpus import build_corpus
+    from oni355.models.gibbs import GibbsConfig, GibbsLDA
+
+    monkeypatch.setenv("ONI_AUTO_EARLY", "dual")
+    r = np.random.default_rng(8)
+    lens = r.integers(1, 200, 60)
+    tdoc = torch.from_numpy(np.repeat(np.arange(60), lens))
+    tword = torch.from_numpy(r.integers(0, 40, int(lens.sum())))
+    keys = torch.arange(60, dtype=torch.int32) * 11 + 3
+    c = build_corpus(tdoc, tword, 60, 40, keys, 1, L=64)
+    a = GibbsLDA(c, GibbsConfig(K=20, seed=5, count_mode="auto", auto_switch=4))
+    assert a.early == 3
+    b = GibbsLDA(c, GibbsConfig(K=20, seed=5, count_mode="recount"))
+    for m in (a, b):
+        m.initialize()
+        m.sweep(9)
+    assert torch.equal(a.tok_z, b.tok_z) and torch.equal(a.nwk, b.nwk) and torch.equal(a.ndk_cur, b.ndk_cur)
