@@ -105,14 +105,15 @@ class GibbsLDA:
         self.device = dev
         D, V, KS = corpus.D, self.V, self.KS
         i32 = torch.int32
-        self.tok_z = torch.zeros(corpus.sell_slots, dtype=torch.uint8, device=dev)
-        self.ndk = [torch.zeros(max(D, 1), KS, dtype=i32, device=dev) for _ in range(2)]
-        self.nwk = torch.zeros(V, KS, dtype=i32, device=dev)
-        self.nk = [torch.zeros(KS, dtype=i32, device=dev) for _ in range(2)]
+        # count tables and z are zeroed by initialize() / load_canonical_z() before any use
+        self.tok_z = torch.empty(corpus.sell_slots, dtype=torch.uint8, device=dev)
+        self.ndk = [torch.empty(max(D, 1), KS, dtype=i32, device=dev) for _ in range(2)]
+        self.nwk = torch.empty(V, KS, dtype=i32, device=dev)
+        self.nk = [torch.empty(KS, dtype=i32, device=dev) for _ in range(2)]
         # Δn_k in NK_REP replicas (block b adds into b % NK_REP): the per-block topic totals
         # would otherwise queue thousands of same-address atomics on KS words
         self._aux_off = V * KS + NK_REP * KS
-        self.dn = [torch.zeros(self._aux_off + ops.DN_AUX, dtype=i32, device=dev) for _ in range(2)]
+        self.dn = [torch.empty(self._aux_off + ops.DN_AUX, dtype=i32, device=dev) for _ in range(2)]
         self.q = torch.zeros(V, KS, dtype=torch.float32, device=dev)
         self.sweep_ctr = torch.zeros(1, dtype=i32, device=dev)
         if cfg.count_mode not in ("auto", "dual", "delta", "recount", "atomic", "wdelta"):
@@ -139,12 +140,12 @@ class GibbsLDA:
         self.early = 3 if (self.auto and self.mode == 4 and early == "dual") else 0
         self._zw_synced = False  # z_w == tok_z in word-sorted order
         if self.mode == 3 or self.early == 3:
-            self.z_w = torch.zeros(max(corpus.T, 1), dtype=torch.uint8, device=dev)
+            self.z_w = torch.empty(max(corpus.T, 1), dtype=torch.uint8, device=dev)  # synced before use
         if self.mode == 4:
             # word-sorted change bitmap (+ slack word) and (old | new << 8) of each changed token;
             # zz_w is only read where a bit is set, so it never needs a sync with tok_z
-            self.wbits = torch.zeros((corpus.T + 31) // 32 + 1, dtype=torch.int32, device=dev)
-            self.zz_w = torch.zeros(max(corpus.T, 1), dtype=torch.int16, device=dev)
+            self.wbits = torch.empty((corpus.T + 31) // 32 + 1, dtype=torch.int32, device=dev)  # _sync_aux_z zeroes
+            self.zz_w = torch.empty(max(corpus.T, 1), dtype=torch.int16, device=dev)
         if self.mode == 2:
             self.tok_zprev = torch.zeros_like(self.tok_z)
             self.chg_mask = torch.zeros(max(corpus.sell_slots // corpus.S, 1), dtype=torch.int64, device=dev)
