@@ -1507,7 +1507,7 @@ ONI_API int oni_gibbs_launch(const OniGibbs* a, int G, int KP, int init, int mod
   if (G == g_ && KP == kp_) return launch_gibbs<g_, kp_>(*a, init != 0, mode, qpf, s);
   ONI_CASE(1, 4) ONI_CASE(1, 8) ONI_CASE(1, 12) ONI_CASE(1, 16) ONI_CASE(1, 20) ONI_CASE(1, 24) ONI_CASE(1, 28)
   ONI_CASE(1, 32)
-  ONI_CASE(4, 8) ONI_CASE(4, 12) ONI_CASE(4, 16)
+  ONI_CASE(4, 8) ONI_CASE(4, 12) ONI_CASE(4, 16) ONI_CASE(4, 20) ONI_CASE(4, 24) ONI_CASE(4, 28)
   ONI_CASE(8, 8) ONI_CASE(8, 12) ONI_CASE(8, 16)
   ONI_CASE(16, 8) ONI_CASE(16, 16)
 #undef ONI_CASE

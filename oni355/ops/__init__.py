@@ -9,6 +9,8 @@ the same bits; kernels reinterpret them.
 """
 from __future__ import annotations
 
+import os
+
 import ctypes as C
 
 import numpy as np
@@ -57,6 +59,11 @@ def choose_tiling(K: int) -> tuple[int, int]:
         return 4, 12
     if K <= 64:
         return 4, 16
+    # 4-lane units up to KS = 112 (default "wide"): K = 100 pads to 112 topics instead of 128,
+    # 0.848 vs 1.188 ms per 25M-token sweep on MI355X (profiles/r2s4/bench_k100_*.json);
+    # ONI_TILING=narrow restores the 8-lane units above K = 64
+    if os.environ.get("ONI_TILING", "wide") == "wide" and K <= 112:
+        return 4, r4((K + 3) // 4)
     if K <= 96:
         return 8, 12
     if K <= 128:
