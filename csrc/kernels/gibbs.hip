@@ -910,6 +910,20 @@ __device__ __forceinline__ int count_le(const float (&P)[KP], float excl, float 
     const float c0 = b1 ? P[2] : P[0], c1 = b1 ? P[6] : P[4];
     const bool b0 = excl + (b2 ? c1 : c0) <= thr;
     return (b2 ? 4 : 0) + (b1 ? 2 : 0) + (b0 ? 1 : 0);
+  } else if constexpr (KP > 16 && KP <= 32) {
+    // upper or lower 16 by one compare, then the 16-wide search over the selected half (entries
+    // past KP read +inf: never counted, thr is finite)
+    const bool hi = excl + P[15] <= thr;
+    float Q[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) Q[j] = hi ? (16 + j < KP ? P[(16 + j) % KP] : __builtin_inff()) : P[j];
+    return (hi ? 16 : 0) + count_le<16>(Q, excl, thr);
+  } else if constexpr (KP > 8 && KP < 16) {
+    const bool hi = excl + P[7] <= thr;
+    float Q[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Q[j] = hi ? (8 + j < KP ? P[(8 + j) % KP] : __builtin_inff()) : P[j];
+    return (hi ? 8 : 0) + count_le<8>(Q, excl, thr);
   } else {
     int cnt = 0;
 #pragma unroll
