@@ -50,7 +50,7 @@ struct OniGibbs {
   float alpha;
   uint32_t seed0, seed1;
   int32_t nk_rep;              // dnk holds nk_rep replicas of [KS] (power of 2): block b adds into b % nk_rep
-  int32_t pad_;
+  int32_t flags;               // bit 0: LDS samplers may keep n + α in their rows (exact in f32 here)
 };
 
 namespace {
@@ -974,7 +974,10 @@ __device__ __forceinline__ float group_scan_dpp(float x, int g) {
 // QP = 1: the q row of the next token is prefetched one step ahead (token words stream two steps
 // ahead so the prefetch address is known early) and copied in on a word change; QP = 0 loads the
 // row when the word changes.
-template <int G, int KP, int MODE, int QP>
+// AIR: the LDS rows hold n_dk + α instead of n_dk (the host sets it only when every n + α of this
+// corpus is exact in f32, e.g. α = 50/K ∈ {2.5, 1, 0.5} with documents below 2^22 tokens), which
+// drops the per-topic "+ α" from the inner product -- same values, bitwise the same draws.
+template <int G, int KP, int MODE, int QP, bool AIR = false>
 __global__ __launch_bounds__(kBlock) void k_gibbs_ldsg(const OniGibbs a) {
   static_assert(G > 1, "G = 1 uses k_gibbs_lds");
   constexpr int S = oni::kWave / G;
@@ -999,9 +1002,11 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_ldsg(const OniGibbs a) {
 #pragma unroll
     for (int j = 0; j < KP; ++j) n0[j] = 0;
     if (live) load_row_i<KP>(a.ndk_src + (int64_t)doc * KS + kbase, n0);
+    const float a0 = AIR ? a.alpha : 0.f;
 #pragma unroll
     for (int j = 0; j < KP / 4; ++j)
-      row[j] = make_float4((float)n0[4 * j], (float)n0[4 * j + 1], (float)n0[4 * j + 2], (float)n0[4 * j + 3]);
+      row[j] = make_float4((float)n0[4 * j] + a0, (float)n0[4 * j + 1] + a0, (float)n0[4 * j + 2] + a0,
+                           (float)n0[4 * j + 3] + a0);
   }
   const int len = valid ? a.slice_len[slice] : 0;
   const int64_t off = valid ? a.slice_off[slice] : 0;
@@ -1059,13 +1064,13 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_ldsg(const OniGibbs a) {
 #pragma unroll
     for (int j = 0; j < KP / 4; ++j) {
       const float4 av = row[j];
-      run = fmaf(av.x + a.alpha, qv[4 * j + 0], run);
+      run = fmaf(AIR ? av.x : av.x + a.alpha, qv[4 * j + 0], run);
       P[4 * j + 0] = run;
-      run = fmaf(av.y + a.alpha, qv[4 * j + 1], run);
+      run = fmaf(AIR ? av.y : av.y + a.alpha, qv[4 * j + 1], run);
       P[4 * j + 1] = run;
-      run = fmaf(av.z + a.alpha, qv[4 * j + 2], run);
+      run = fmaf(AIR ? av.z : av.z + a.alpha, qv[4 * j + 2], run);
       P[4 * j + 2] = run;
-      run = fmaf(av.w + a.alpha, qv[4 * j + 3], run);
+      run = fmaf(AIR ? av.w : av.w + a.alpha, qv[4 * j + 3], run);
       P[4 * j + 3] = run;
     }
     const float incl = group_scan_dpp<G>(run, g);
@@ -1099,7 +1104,7 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_ldsg(const OniGibbs a) {
   int32_t d[KP], n[KP];
 #pragma unroll
   for (int j = 0; j < KP; ++j) {
-    n[j] = (int32_t)rowf[j];
+    n[j] = (int32_t)(AIR ? rowf[j] - a.alpha : rowf[j]);
     d[j] = 0;
   }
   if (live) {
@@ -1170,6 +1175,7 @@ int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s)
     if constexpr (G > 1) {
       if (qpf == 2 || qpf == 5) {
         if (qpf == 5) k_gibbs_ldsg<G, KP, 4, 1><<<grid, kBlock, 0, s>>>(a);
+        else if (a.flags & 1) k_gibbs_ldsg<G, KP, 4, 0, true><<<grid, kBlock, 0, s>>>(a);
         else k_gibbs_ldsg<G, KP, 4, 0><<<grid, kBlock, 0, s>>>(a);
         return (int)hipGetLastError();
       }
@@ -1195,7 +1201,12 @@ int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s)
     }
   } else {
     if (qpf == 2) {
-      if (mode == 0) k_gibbs_ldsg<G, KP, 0, 0><<<grid, kBlock, 0, s>>>(a);
+      if (a.flags & 1) {
+        if (mode == 0) k_gibbs_ldsg<G, KP, 0, 0, true><<<grid, kBlock, 0, s>>>(a);
+        else if (mode == 1) k_gibbs_ldsg<G, KP, 1, 0, true><<<grid, kBlock, 0, s>>>(a);
+        else if (mode == 2) k_gibbs_ldsg<G, KP, 2, 0, true><<<grid, kBlock, 0, s>>>(a);
+        else k_gibbs_ldsg<G, KP, 3, 0, true><<<grid, kBlock, 0, s>>>(a);
+      } else if (mode == 0) k_gibbs_ldsg<G, KP, 0, 0><<<grid, kBlock, 0, s>>>(a);
       else if (mode == 1) k_gibbs_ldsg<G, KP, 1, 0><<<grid, kBlock, 0, s>>>(a);
       else if (mode == 2) k_gibbs_ldsg<G, KP, 2, 0><<<grid, kBlock, 0, s>>>(a);
       else k_gibbs_ldsg<G, KP, 3, 0><<<grid, kBlock, 0, s>>>(a);

@@ -73,6 +73,18 @@ class GibbsConfig:
         return float(self.alpha) if self.alpha is not None else 50.0 / self.K
 
 
+def _alpha_in_row_exact(alpha: float, max_doc_len: int) -> bool:
+    """May the LDS samplers keep n + α (f32) in their rows? Only if every n + α with
+    0 ≤ n ≤ max_doc_len is exact in f32, so the rows' ±1 updates reproduce fl(n) + α bit for bit."""
+    a = float(np.float32(alpha))
+    if not (a > 0 and math.isfinite(a)):
+        return False
+    f = 0
+    while f <= 23 and a * (1 << f) != math.floor(a * (1 << f)):
+        f += 1
+    return f <= 23 and max_doc_len + math.ceil(a) < (1 << (24 - f))
+
+
 _CAPTURE_STREAMS: dict = {}
 
 
@@ -158,6 +170,7 @@ class GibbsLDA:
             self.qpf = 2  # "ldsq" (LDS counts + q-row prefetch) is the multi-lane variant; G = 1 has "lds"
         if self.qpf in (2, 5) and corpus.max_doc_len() >= (1 << 24):
             self.qpf = 1  # LDS rows hold counts as f32: exact below 2^24
+        self._air = _alpha_in_row_exact(self.alpha, corpus.max_doc_len())
         self.a = 0  # ndk parity
         self.b = 0  # delta-buffer parity
         self.cn = 0  # nk parity
@@ -338,7 +351,7 @@ class GibbsLDA:
                        self.sweep_ctr, c.chunk_len, host_sweep=self.sweeps_done + 1, mode=mode,
                        prefetch_q=self.qpf,
                        chg_mask=self.wbits if mode == 4 else getattr(self, "chg_mask", None), wpos=c.wpos,
-                       z_w=getattr(self, "z_w", None), zz_w=getattr(self, "zz_w", None))
+                       z_w=getattr(self, "z_w", None), zz_w=getattr(self, "zz_w", None), alpha_in_row=self._air)
         head = self.dn[self.b][: self.V * self.KS].view(self.V, self.KS)
         if mode == 4:
             # dn[b] head := Δn_wk of the tokens marked in the word-sorted change bitmap

@@ -295,7 +295,8 @@ def sell_perm_z(chunk_doc, chunk_pos0, chunk_len, S, slice_off, doc_tok_ptr, tok
 def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init: bool, sweep_ctr: torch.Tensor,
                chunk_len: torch.Tensor, host_sweep: int | None = None, mode: int = 1,
                prefetch_q: bool | int = False, chg_mask: torch.Tensor | None = None, wpos: torch.Tensor | None = None,
-               z_w: torch.Tensor | None = None, zz_w: torch.Tensor | None = None) -> None:
+               z_w: torch.Tensor | None = None, zz_w: torch.Tensor | None = None,
+               alpha_in_row: bool = False) -> None:
     """Launch one init/sweep pass. ``st`` holds the OniGibbs tensors (see csrc/kernels/gibbs.hip).
 
     ``mode`` 1: accumulate Δn_wk with per-token atomics; 0: the caller rebuilds n_wk with
@@ -366,6 +367,8 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
         a.chg_count = _lib.ptr(st["chg_count"])
     a.n_slices, a.K, a.KS, a.alpha, a.seed0, a.seed1 = n_slices, K, KS, float(alpha), s0, s1
     a.nk_rep = nk_rep
+    # the caller vouches that n + α is exact in f32 for every doc-topic count of this corpus
+    a.flags = 1 if alpha_in_row else 0
     _lib.check(_lib.lib().oni_gibbs_launch(C.byref(a), G, KP, 1 if init else 0, int(mode),
                                            int(prefetch_q), _lib.stream()),
                "oni_gibbs_launch")

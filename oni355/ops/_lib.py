@@ -34,7 +34,7 @@ class OniGibbs(C.Structure):
         ("ndk_src", vp), ("ndk_dst", vp), ("q", vp), ("dnwk", vp), ("dnk", vp), ("sweep_ctr", vp), ("chg_mask", vp),
         ("wpos", vp), ("z_w", vp), ("zz_w", vp), ("chg_count", vp),
         ("n_slices", i64), ("K", i32), ("KS", i32), ("alpha", f32), ("seed0", u32), ("seed1", u32),
-        ("nk_rep", i32), ("pad_", i32),
+        ("nk_rep", i32), ("flags", i32),
     ]
 
 
