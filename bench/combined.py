@@ -2,7 +2,8 @@
 """Config 5 of BASELINE.json: combined flow + DNS + proxy day, one LDA model per source
 (as ml_ops.sh runs one model per data source), K = 100 by default, data parallel over the node.
 
-One timed *step* = one full Gibbs sweep of each of the three models (all three resident in HBM);
+One timed *step* = one full Gibbs sweep of each of the three models (all three resident in HBM;
+the models take turns in chunks of ``--chunk`` sweeps);
 ``value`` = all events of the node-wide day × steps / s. Also reports per-model ms/sweep, the
 measured HBM peak next to the sizing model (oni355.utils.sizing) and that model's projection for
 the named 1B-event / 8-GPU configuration.
@@ -30,6 +31,7 @@ def main(argv=None) -> int:
     ap.add_argument("--topics", type=int, default=100)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--chunk", type=int, default=10, help="sweeps per model between model switches")
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--device", default="cuda")
     a = ap.parse_args(argv)
@@ -78,9 +80,14 @@ def main(argv=None) -> int:
     comm.barrier()
     per_model = {}
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    # each model runs its sweeps in chunks (graph-replayed pairs, one health check per chunk),
+    # as oni-ml runs a model's sweeps back to back; the total work is a.steps sweeps per model
+    done = 0
+    while done < a.steps:
+        n = min(a.chunk, a.steps - done)
         for su in sources:
-            su.model.sweep(1)
+            su.model.sweep(n)
+        done += n
     sync()
     comm.barrier()
     dt = comm.allreduce_scalar(time.perf_counter() - t0, "max")
