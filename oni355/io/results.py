@@ -280,8 +280,16 @@ class ResultPipe:
         self._pending = None  # (future of (gids, Rendered), all result rows)
 
     def submit(self, cols: dict, res, row_off: int) -> None:
-        """Queue this day's formatting; finishes the previous day first."""
+        """Queue this day's formatting; finishes the previous day first. ``ONI_RESULT_PIPE=0``
+        formats and writes inline (no worker thread)."""
         self._finish()
+        if os.environ.get("ONI_RESULT_PIPE", "1") == "0":
+            from concurrent.futures import Future
+            fut = Future()
+            fut.set_result(render_local(self.source, cols, res, row_off))
+            self._pending = (fut, res.rows)
+            self._finish()
+            return
         fut = self._pool.submit(render_local, self.source, cols, res, row_off)
         self._pending = (fut, res.rows)
 
