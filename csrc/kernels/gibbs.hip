@@ -14,8 +14,8 @@
 //  * A wave = one SELL slice of S = 64/G chunks; tokens are step-major so per-step word/topic
 //    loads are coalesced. The q row is re-used while consecutive tokens share a word (tokens of
 //    one (doc, word) pair are adjacent).
-//  * G = 1 for K ≤ 32 (one lane owns all topics: no cross-lane traffic at all); G ∈ {4, 8, 16}
-//    for K = 50/100 with a DPP-free __shfl_up scan across the unit.
+//  * G = 1 for K ≤ 32 (one lane owns all topics: no cross-lane traffic at all); G ∈ {2, 4, 8, 16}
+//    above (2 lanes up to K = 56, 4 up to 112) with DPP / __shfl_up scans across the unit.
 //  * Draws are Philox4x32-10 keyed by (seed) with counter (pos/4, doc key, sweep, stream): the
 //    chain is a pure function of the data + seed — bitwise identical for any GPU count, shard
 //    plan, chunk packing or resume point (tested against the NumPy oracle, oni355/ref/spec.py).
@@ -932,14 +932,14 @@ __device__ __forceinline__ int count_le(const float (&P)[KP], float excl, float 
   }
 }
 
-// Sum of an int over each aligned group of G ∈ {4, 8, 16} lanes with DPP butterflies (no LDS
+// Sum of an int over each aligned group of G ∈ {2, 4, 8, 16} lanes with DPP butterflies (no LDS
 // crossbar round trip): quad_perm swaps for 1 and 2, half-row / row mirrors for 4 and 8 (after the
 // lower levels every lane of a sub-group holds the sub-group sum, so any cross pairing works).
 template <int G>
 __device__ __forceinline__ int group_sum_dpp(int v) {
-  static_assert(G == 4 || G == 8 || G == 16, "DPP group sums need G in {4, 8, 16}");
+  static_assert(G == 2 || G == 4 || G == 8 || G == 16, "DPP group sums need G in {2, 4, 8, 16}");
   v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, true);   // quad_perm [1,0,3,2]
-  v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, true);   // quad_perm [2,3,0,1]
+  if constexpr (G >= 4) v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, true);   // quad_perm [2,3,0,1]
   if constexpr (G >= 8) v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, true);  // row_half_mirror
   if constexpr (G >= 16) v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, true);  // row_mirror
   return v;
@@ -955,11 +955,13 @@ __device__ __forceinline__ float dpp_row_shr(float x) {
 
 template <int G>
 __device__ __forceinline__ float group_scan_dpp(float x, int g) {
-  static_assert(G == 4 || G == 8 || G == 16, "DPP group scans need G in {4, 8, 16}");
+  static_assert(G == 2 || G == 4 || G == 8 || G == 16, "DPP group scans need G in {2, 4, 8, 16}");
   float y = dpp_row_shr<1>(x);
   if (g >= 1) x = x + y;
-  y = dpp_row_shr<2>(x);
-  if (g >= 2) x = x + y;
+  if constexpr (G >= 4) {
+    y = dpp_row_shr<2>(x);
+    if (g >= 2) x = x + y;
+  }
   if constexpr (G >= 8) {
     y = dpp_row_shr<4>(x);
     if (g >= 4) x = x + y;
@@ -1532,6 +1534,7 @@ ONI_API int oni_gibbs_launch(const OniGibbs* a, int G, int KP, int init, int mod
   if (G == g_ && KP == kp_) return launch_gibbs<g_, kp_>(*a, init != 0, mode, qpf, s);
   ONI_CASE(1, 4) ONI_CASE(1, 8) ONI_CASE(1, 12) ONI_CASE(1, 16) ONI_CASE(1, 20) ONI_CASE(1, 24) ONI_CASE(1, 28)
   ONI_CASE(1, 32)
+  ONI_CASE(2, 20) ONI_CASE(2, 24) ONI_CASE(2, 28)
   ONI_CASE(4, 8) ONI_CASE(4, 12) ONI_CASE(4, 16) ONI_CASE(4, 20) ONI_CASE(4, 24) ONI_CASE(4, 28)
   ONI_CASE(8, 8) ONI_CASE(8, 12) ONI_CASE(8, 16)
   ONI_CASE(16, 8) ONI_CASE(16, 16)

@@ -55,6 +55,9 @@ def choose_tiling(K: int) -> tuple[int, int]:
     r4 = lambda x: (x + 3) // 4 * 4  # noqa: E731
     if K <= 32:
         return 1, r4(K)
+    wide = os.environ.get("ONI_TILING", "wide") == "wide"
+    if wide and K <= 56:
+        return 2, r4((K + 1) // 2)  # K = 50: 2 lanes x 28 topics (KS = 56 instead of 64)
     if K <= 48:
         return 4, 12
     if K <= 64:
@@ -62,7 +65,7 @@ def choose_tiling(K: int) -> tuple[int, int]:
     # 4-lane units up to KS = 112 (default "wide"): K = 100 pads to 112 topics instead of 128,
     # 0.848 vs 1.188 ms per 25M-token sweep on MI355X (profiles/r2s4/bench_k100_*.json);
     # ONI_TILING=narrow restores the 8-lane units above K = 64
-    if os.environ.get("ONI_TILING", "wide") == "wide" and K <= 112:
+    if wide and K <= 112:
         return 4, r4((K + 3) // 4)
     if K <= 96:
         return 8, 12
