@@ -726,7 +726,10 @@ struct LdsRow {
 // One token step of k_gibbs_lds. Token words/topics (and MODE-3 word-sorted slots) are
 // streamed two steps ahead in a parity-indexed register pair (P is the compile-time parity of s),
 // the q row one step ahead into the other half of the q ping-pong.
-template <int KP, int MODE, int P>
+template <int KP>
+__device__ __forceinline__ int count_le(const float (&P)[KP], float excl, float thr);
+
+template <int KP, int MODE, int P, bool AIR>
 __device__ __forceinline__ void lds_step(const OniGibbs& a, int s, int len, int64_t off, int lane, uint32_t key,
                                          uint32_t pos0, uint32_t sweep, float4* __restrict__ row, oni::U4& r,
                                          uint32_t (&wq)[2], int (&zq)[2], int32_t (&pq)[2], const float (&qc)[KP],
@@ -754,19 +757,17 @@ __device__ __forceinline__ void lds_step(const OniGibbs& a, int s, int len, int6
 #pragma unroll
     for (int j = 0; j < KP / 4; ++j) {
       const float4 av = row[j];
-      run = fmaf(av.x + a.alpha, qc[4 * j + 0], run);
+      run = fmaf(AIR ? av.x : av.x + a.alpha, qc[4 * j + 0], run);
       Pc[4 * j + 0] = run;
-      run = fmaf(av.y + a.alpha, qc[4 * j + 1], run);
+      run = fmaf(AIR ? av.y : av.y + a.alpha, qc[4 * j + 1], run);
       Pc[4 * j + 1] = run;
-      run = fmaf(av.z + a.alpha, qc[4 * j + 2], run);
+      run = fmaf(AIR ? av.z : av.z + a.alpha, qc[4 * j + 2], run);
       Pc[4 * j + 2] = run;
-      run = fmaf(av.w + a.alpha, qc[4 * j + 3], run);
+      run = fmaf(AIR ? av.w : av.w + a.alpha, qc[4 * j + 3], run);
       Pc[4 * j + 3] = run;
     }
     const float thr = oni::u01(rr) * run;
-    int cnt = 0;
-#pragma unroll
-    for (int j = 0; j < KP; ++j) cnt += Pc[j] <= thr;
+    const int cnt = count_le<KP>(Pc, 0.f, thr);  // 0 + P_j == P_j: the same compares
     const int zn = cnt < a.K - 1 ? cnt : a.K - 1;
     rowf[zn] = rowf[zn] + 1.0f;
     changed = zn != zo;
@@ -787,7 +788,7 @@ __device__ __forceinline__ void lds_step(const OniGibbs& a, int s, int len, int6
   }
 }
 
-template <int KP, int MODE>
+template <int KP, int MODE, bool AIR = false>
 __global__ __launch_bounds__(kBlock) void k_gibbs_lds(const OniGibbs a) {
   constexpr int KS = KP;
   constexpr int kSlots = LdsRow<KP>::kSlots;
@@ -806,9 +807,11 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_lds(const OniGibbs a) {
 #pragma unroll
     for (int j = 0; j < KP; ++j) n0[j] = 0;
     if (live) load_row_i<KP>(a.ndk_src + (int64_t)doc * KS, n0);
+    const float a0 = AIR ? a.alpha : 0.f;  // AIR: rows hold n + α (see k_gibbs_ldsg)
 #pragma unroll
     for (int j = 0; j < KP / 4; ++j)
-      row[j] = make_float4((float)n0[4 * j], (float)n0[4 * j + 1], (float)n0[4 * j + 2], (float)n0[4 * j + 3]);
+      row[j] = make_float4((float)n0[4 * j] + a0, (float)n0[4 * j + 1] + a0, (float)n0[4 * j + 2] + a0,
+                           (float)n0[4 * j + 3] + a0);
   }
   const int len = valid ? a.slice_len[slice] : 0;
   const int64_t off = valid ? a.slice_off[slice] : 0;
@@ -833,9 +836,9 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_lds(const OniGibbs a) {
   }
   if (wq[0] != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)wq[0] * KS, qa);
   for (int s = 0; s < len; s += 2) {
-    lds_step<KP, MODE, 0>(a, s, len, off, lane, key, pos0, sweep, row, r, wq, zq, pq, qa, qb, chg_word, nchg);
+    lds_step<KP, MODE, 0, AIR>(a, s, len, off, lane, key, pos0, sweep, row, r, wq, zq, pq, qa, qb, chg_word, nchg);
     if (s + 1 < len)
-      lds_step<KP, MODE, 1>(a, s + 1, len, off, lane, key, pos0, sweep, row, r, wq, zq, pq, qb, qa, chg_word, nchg);
+      lds_step<KP, MODE, 1, AIR>(a, s + 1, len, off, lane, key, pos0, sweep, row, r, wq, zq, pq, qb, qa, chg_word, nchg);
   }
   if (a.chg_count) add_wave_count(a.chg_count, nchg);
   // epilogue: counts back to ints, doc rows, per-topic totals (n0 re-read: keeps it out of VGPRs)
@@ -846,7 +849,7 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_lds(const OniGibbs a) {
   if (live) load_row_i<KP>(a.ndk_src + (int64_t)doc * KS, n0);
 #pragma unroll
   for (int j = 0; j < KP; ++j) {
-    n[j] = (int32_t)rowf[j];
+    n[j] = (int32_t)(AIR ? rowf[j] - a.alpha : rowf[j]);
     d[j] = n[j] - n0[j];
   }
   const bool multi = live && a.chunk_multi[chunk];
@@ -1183,7 +1186,8 @@ int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s)
       }
     } else {
       if (qpf == 2) {
-        k_gibbs_lds<KP, 4><<<grid, kBlock, 0, s>>>(a);
+        if (a.flags & 1) k_gibbs_lds<KP, 4, true><<<grid, kBlock, 0, s>>>(a);
+        else k_gibbs_lds<KP, 4><<<grid, kBlock, 0, s>>>(a);
         return (int)hipGetLastError();
       }
     }
@@ -1195,7 +1199,12 @@ int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s)
   }
   if constexpr (G == 1) {
     if (qpf == 2) {
-      if (mode == 0) k_gibbs_lds<KP, 0><<<grid, kBlock, 0, s>>>(a);
+      if (a.flags & 1) {
+        if (mode == 0) k_gibbs_lds<KP, 0, true><<<grid, kBlock, 0, s>>>(a);
+        else if (mode == 1) k_gibbs_lds<KP, 1, true><<<grid, kBlock, 0, s>>>(a);
+        else if (mode == 2) k_gibbs_lds<KP, 2, true><<<grid, kBlock, 0, s>>>(a);
+        else k_gibbs_lds<KP, 3, true><<<grid, kBlock, 0, s>>>(a);
+      } else if (mode == 0) k_gibbs_lds<KP, 0><<<grid, kBlock, 0, s>>>(a);
       else if (mode == 1) k_gibbs_lds<KP, 1><<<grid, kBlock, 0, s>>>(a);
       else if (mode == 2) k_gibbs_lds<KP, 2><<<grid, kBlock, 0, s>>>(a);
       else k_gibbs_lds<KP, 3><<<grid, kBlock, 0, s>>>(a);
