@@ -433,14 +433,23 @@ class ScorePlan:
     tiles: TilePlan | None = None
     # events regrouped by their first endpoint's pair (SCORE_SORT_EVENTS): the gather of that
     # endpoint's pair score becomes a monotone stream instead of a random 4-B read per event;
-    # ``order`` maps plan position → event, ``rank`` event → plan position
+    # ``order`` maps plan position → event, ``rank`` event → plan position (built on first use:
+    # the pipelines map result rows through top_n's positions and never need the full inverse)
     order: torch.Tensor | None = None
-    rank: torch.Tensor | None = None
     inv_sorted: list | None = None
+    _rank: torch.Tensor | None = None
 
     @property
     def n_pairs(self) -> int:
         return int(self.pdoc.numel())
+
+    @property
+    def rank(self) -> torch.Tensor | None:
+        if self._rank is None and self.order is not None:
+            order = self.order
+            self._rank = torch.empty_like(order)
+            self._rank[order] = torch.arange(order.numel(), dtype=order.dtype, device=order.device)
+        return self._rank
 
 
 def tile_plan(pdoc: torch.Tensor, pword: torch.Tensor, D: int, V: int) -> tuple[TilePlan, torch.Tensor]:
@@ -528,9 +537,7 @@ def score_plan(dkeys: torch.Tensor, vocab: torch.Tensor, sides, tiles: bool | No
     plan = ScorePlan(pdoc.to(torch.int32).contiguous(), pword.to(torch.int32).contiguous(), invs, tp)
     if SCORE_SORT_EVENTS if sort_events is None else sort_events:
         order = torch.argsort(invs[0], stable=True)
-        rank = torch.empty_like(order)
-        rank[order] = torch.arange(order.numel(), dtype=order.dtype, device=order.device)
-        plan.order, plan.rank = order, rank
+        plan.order = order
         plan.inv_sorted = [x[order].contiguous() for x in invs]
     return plan
 
@@ -544,11 +551,8 @@ def plan_from_pairs(ps, n: int, n_sides: int, doc_rows: torch.Tensor | None = No
     invs = [ps.tok_pair[i * n:(i + 1) * n] for i in range(n_sides)]
     plan = ScorePlan(pdoc.contiguous(), ps.pair_word, invs)
     if SCORE_SORT_EVENTS and ps.order0 is not None:
-        order = ps.order0
-        rank = torch.empty_like(order)
-        rank[order] = torch.arange(order.numel(), dtype=order.dtype, device=order.device)
-        plan.order, plan.rank = order, rank
-        plan.inv_sorted = [x[order].contiguous() for x in invs]
+        plan.order = ps.order0
+        plan.inv_sorted = [x[ps.order0].contiguous() for x in invs]
     return plan
 
 
@@ -593,18 +597,19 @@ def to_event_order(plan: ScorePlan, x: torch.Tensor | None) -> torch.Tensor | No
 
 @traced("oni:top_n")
 def top_n(score: torch.Tensor, tol: float, maxresults: int, comm: Comm | None, row_offset: int = 0,
-          hist: torch.Tensor | None = None, order: torch.Tensor | None = None):
+          hist: torch.Tensor | None = None, order: torch.Tensor | None = None, return_pos: bool = False):
     """Lowest ``maxresults`` scores below ``tol`` (ties by global row id), merged over ranks (X06).
 
     ``hist`` is the 2048-bucket histogram of score order keys (top 11 bits) of events under tol,
     as produced by the fused score kernel; computed here when absent. Returns (global row ids
     int64, scores f32), ascending, identical on every rank. ``order`` (a score plan's event order)
-    maps positions of ``score`` to local event ids.
+    maps positions of ``score`` to local event ids. ``return_pos`` (no process group) also returns
+    each result row's position in ``score``.
     """
     if hist is None:
         b = u32_to_i64(ops.f32_keys(score)) >> 21
         hist = torch.bincount(b[score < tol], minlength=2048)
-    return _top_n_from_hist(score, hist, tol, maxresults, comm, row_offset, order)
+    return _top_n_from_hist(score, hist, tol, maxresults, comm, row_offset, order, return_pos)
 
 
 @dataclass
@@ -672,7 +677,7 @@ def rows_in_order(gid_all: torch.Tensor, rows: torch.Tensor) -> torch.Tensor:
     return o[torch.searchsorted(gid_all[o], rows)]
 
 
-def _top_n_from_hist(score, hist, tol, maxresults, comm, row_offset, order=None):
+def _top_n_from_hist(score, hist, tol, maxresults, comm, row_offset, order=None, return_pos=False):
     h_loc = hist.to(torch.int64).cpu().numpy()
     h = comm.allreduce_np(h_loc) if comm is not None and comm.dist else h_loc
     cum = np.cumsum(h)
@@ -680,20 +685,23 @@ def _top_n_from_hist(score, hist, tol, maxresults, comm, row_offset, order=None)
         bmax = 2047 if maxresults > 0 else -1
     else:
         bmax = int(np.searchsorted(cum, min(maxresults, int(cum[-1])), side="left"))
+    if return_pos and comm is not None and comm.dist:
+        raise ValueError("top_n: positions are only defined without a process group")
     if bmax < 0:
         e = torch.zeros(0, dtype=torch.int64, device=score.device)
-        return e, torch.zeros(0, dtype=torch.float32, device=score.device)
+        out = (e, torch.zeros(0, dtype=torch.float32, device=score.device))
+        return out + (e,) if return_pos else out
     # the local histogram already counts this rank's candidates: no extra pass over the scores
     cap = int(np.cumsum(h_loc)[bmax])
-    idx, sc = ops.select_below(score, tol, bmax, cap=max(cap, 1))
-    if order is not None:
-        idx = order[idx]
+    pos, sc = ops.select_below(score, tol, bmax, cap=max(cap, 1))
+    idx = order[pos] if order is not None else pos
     gid = idx + row_offset
     # exact order: (score, global id); keep local top-N then merge
     o1 = torch.argsort(gid, stable=True)
-    gid, sc = gid[o1], sc[o1]
-    o2 = torch.argsort(sc, stable=True)
-    gid, sc = gid[o2][:maxresults], sc[o2][:maxresults]
+    o2 = o1[torch.argsort(sc[o1], stable=True)][:maxresults]
+    gid, sc = gid[o2], sc[o2]
+    if return_pos:
+        return gid, sc, pos[o2]
     if comm is not None and comm.dist:
         # one all-gather of (global id, score bits) pairs
         both = torch.cat(comm.allgather_var(torch.stack([gid.to(torch.int64),

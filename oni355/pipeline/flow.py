@@ -211,7 +211,8 @@ def run_flow(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxre
                                                [word_keys[:n], word_keys[n: 2 * n]], comm)
         with timer.stage("score"):
             score, s1, s2 = common.plan_score(theta, phi, plan, tol, hist=hist, want_parts=True)
-            rows, scs = common.top_n(score, tol, maxresults, comm, row_offset, hist=hist, order=plan.order)
+            rows, scs, rpos = common.top_n(score, tol, maxresults, comm, row_offset, hist=hist, order=plan.order,
+                                           return_pos=True)
     t = timer.summary()
     t.update(run.timings)
     t["records_scored"] = n
@@ -219,7 +220,7 @@ def run_flow(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxre
     loc = rows - row_offset
     mine = (loc >= 0) & (loc < n)
     li = loc[mine]
-    pi = plan.rank[li] if plan is not None and plan.rank is not None else li  # positions of the result events
+    pi = rpos[mine] if plan is not None else li  # positions of the result events in score order
     parts = torch.stack([s1[pi], s2[pi]], 1) if s1 is not None else torch.zeros(0, 2)
     wparts = torch.stack([sw[li], dw[li]], 1)
     if comm is not None and comm.dist:
