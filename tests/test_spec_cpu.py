@@ -269,3 +269,22 @@ def test_auto_with_dual_early_sweeps_matches_recount(monkeypatch):
         m.initialize()
         m.sweep(9)
     assert torch.equal(a.tok_z, b.tok_z) and torch.equal(a.nwk, b.nwk) and torch.equal(a.ndk_cur, b.ndk_cur)
+
+
+def test_tiling_choice_and_alpha_in_row_rule(monkeypatch):
+    """Unit widths: 1 lane to K = 32, 2 lanes to 56, 4 lanes to 112 (wide, default), the old
+    4/8/16-lane units with ONI_TILING=narrow; KS = G·KP covers K with KP a multiple of 4. The
+    n + α LDS rows are allowed only where every n + α is exact in f32."""
+    from oni355 import ops
+    from oni355.models.gibbs import _alpha_in_row_exact
+
+    for K in range(1, 256):
+        G, KP = ops.choose_tiling(K)
+        assert G * KP >= K and KP % 4 == 0 and G in (1, 2, 4, 8, 16)
+    assert ops.choose_tiling(20) == (1, 20) and ops.choose_tiling(50) == (2, 28)
+    assert ops.choose_tiling(100) == (4, 28) and ops.choose_tiling(120) == (8, 16)
+    monkeypatch.setenv("ONI_TILING", "narrow")
+    assert ops.choose_tiling(50) == (4, 16) and ops.choose_tiling(100) == (8, 16)
+    assert _alpha_in_row_exact(2.5, 10**6) and _alpha_in_row_exact(0.5, (1 << 22))
+    assert not _alpha_in_row_exact(0.5, 1 << 23)  # 2^23 + 0.5 needs 25 significant bits
+    assert not _alpha_in_row_exact(0.1, 10) and not _alpha_in_row_exact(50 / 7, 10)
