@@ -53,6 +53,15 @@ def _u64(t: torch.Tensor) -> np.ndarray:
     return t.cpu().numpy().view(np.uint64)
 
 
+def _dev_topset(topset, dev) -> torch.Tensor:
+    """The hash set's table on ``dev``, uploaded once per set object and device."""
+    cache = topset.__dict__.setdefault("_dev_tables", {})
+    key = str(dev)
+    if key not in cache:
+        cache[key] = torch.from_numpy(topset.table.view(np.int64)).to(dev)
+    return cache[key]
+
+
 def domain_features(offsets: torch.Tensor, chars: torch.Tensor, topset: ss.HashSet | None, user_domain: str = "",
                     rules=None):
     """Returns (reg_hash int64(u64 bits), top u8, sub_len i32, sub_ent f32, periods i32).
@@ -66,7 +75,7 @@ def domain_features(offsets: torch.Tensor, chars: torch.Tensor, topset: ss.HashS
                 torch.from_numpy(en), torch.from_numpy(per))
     dev = offsets.device
     clogc, lg = _dev_tables(dev)
-    tab = torch.from_numpy(topset.table.view(np.int64)).to(dev) if topset is not None else None
+    tab = _dev_topset(topset, dev) if topset is not None else None
     mask = topset.mask if topset is not None else 0
     uh = ss.fnv1a(user_domain.encode()) if user_domain else 0
     outs = (torch.empty(n, dtype=torch.int64, device=dev), torch.empty(n, dtype=torch.uint8, device=dev),

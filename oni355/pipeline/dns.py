@@ -39,10 +39,19 @@ def word_str(w: int) -> str:
     return "_".join(str(p) for p in parts)
 
 
+_TOP_CACHE: list = []  # [(domains object, HashSet)]: one entry, the list the pipeline keeps passing
+
+
 def top_set(domains) -> HashSet | None:
+    """Top-domain hash set of ``domains`` (built once per list object: hashing and inserting a
+    top-1M list in Python takes seconds, and every day of a run passes the same list)."""
     if not domains:
         return None
-    return HashSet([fnv1a(d.strip().lower().encode()) for d in domains if d.strip()])
+    if _TOP_CACHE and _TOP_CACHE[0][0] is domains and _TOP_CACHE[0][2] == len(domains):
+        return _TOP_CACHE[0][1]
+    hs = HashSet([fnv1a(d.strip().lower().encode()) for d in domains if d.strip()])
+    _TOP_CACHE[:] = [(domains, hs, len(domains))]
+    return hs
 
 
 def load_top_domains(path: str) -> list[str]:
