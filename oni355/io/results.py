@@ -237,18 +237,32 @@ def render_local(source: str, cols: dict, res, row_off: int):
 
 def gather_rendered(all_rows: np.ndarray, gids: np.ndarray, rendered: Rendered, comm=None) -> Rendered:
     """Merge every rank's locally rendered rows into the full text in ``all_rows`` order (collective
-    X06's payload; every rank returns it). Identity without a process group."""
+    X06's payload; every rank returns it). Identity without a process group.
+
+    Each rank's (row ids, line ends, text) travel as one byte tensor through ``Comm.allgather_var``
+    (a size exchange + one all-gather on the collective device) -- no pickling."""
     if comm is None or not comm.dist:
         return rendered
-    import torch.distributed as dist
-    allp = [None] * comm.world
-    dist.all_gather_object(allp, (np.asarray(gids, dtype=np.int64).tolist(), rendered.blob, rendered.ends),
-                           group=comm.group)
+    import torch
+
+    g = np.ascontiguousarray(gids, dtype=np.int64)
+    e = np.ascontiguousarray(rendered.ends, dtype=np.int64)
+    blob = np.frombuffer(rendered.blob, dtype=np.uint8)
+    payload = np.concatenate([np.array([g.size, blob.size], np.int64).view(np.uint8), g.view(np.uint8),
+                              e.view(np.uint8), blob])
+    t = torch.from_numpy(payload)
+    if comm.device.type == "cuda":
+        t = t.to(comm.device)
     by_gid = {}
-    for gl, blob, ends in allp:
-        for g, line in zip(gl, Rendered(blob, ends).lines()):
-            by_gid[g] = line
-    lines = [by_gid[int(g)] for g in np.asarray(all_rows).tolist()]
+    for part in comm.allgather_var(t):
+        b = part.cpu().numpy()
+        n, nb = (int(x) for x in b[:16].view(np.int64))
+        pg = b[16:16 + 8 * n].view(np.int64)
+        pe = b[16 + 8 * n:16 + 16 * n].view(np.int64)
+        text = b[16 + 16 * n:16 + 16 * n + nb].tobytes()
+        for gid, line in zip(pg.tolist(), Rendered(text, pe).lines()):
+            by_gid[gid] = line
+    lines = [by_gid[int(x)] for x in np.asarray(all_rows).tolist()]
     ends = np.cumsum([len(x) for x in lines]).astype(np.int64) if lines else np.zeros(0, np.int64)
     return Rendered(b"".join(lines), ends)
 

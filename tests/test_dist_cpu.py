@@ -163,8 +163,10 @@ def _single_worker(rank, world, port, source, n_total, out_q):
     cols = {k: (v.slice(lo, hi) if isinstance(v, StringColumn) else v[lo:hi]) for k, v in cols.items()
             if not k.startswith("_")}
     res = run(cols, K=K, sweeps=4, maxresults=120, device="cpu", comm=comm, row_offset=lo)
+    from oni355.io import results as rio
+    text = rio.render_result(source, cols, res, lo, comm).blob  # rows rendered where they live, gathered
     if rank == 0:
-        out_q.put((res.rows, res.scores, res.words))
+        out_q.put((res.rows, res.scores, res.words, text))
     if comm is not None:
         comm.barrier()
         pc.shutdown()
@@ -173,7 +175,8 @@ def _single_worker(rank, world, port, source, n_total, out_q):
 @pytest.mark.parametrize("source", ["dns", "proxy"])
 def test_dns_proxy_dp_matches_single_process(source):
     """DNS / proxy (one token per event, owner-side scoring, result words gathered from the rank
-    that holds each row) on 2 gloo ranks == one process: rows, scores and words."""
+    that holds each row) on 2 gloo ranks == one process: rows, scores, words and the rendered CSV
+    rows (each formatted on the rank holding the raw row, gathered as one byte tensor)."""
     ctx = mp.get_context("spawn")
     out = []
     for world in (1, 2):
@@ -186,6 +189,7 @@ def test_dns_proxy_dp_matches_single_process(source):
         for p in procs:
             p.join(timeout=120)
             assert p.exitcode == 0
-    (r1, s1, w1), (r2, s2, w2) = out
+    (r1, s1, w1, t1), (r2, s2, w2, t2) = out
     assert r1.size > 0
     assert np.array_equal(r1, r2) and np.array_equal(s1, s2) and np.array_equal(w1, w2)
+    assert t1 == t2 and t1.count(b"\n") == r1.size  # the CSV rows, gathered from both ranks
