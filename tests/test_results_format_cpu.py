@@ -106,3 +106,21 @@ def test_result_pipe_writes_each_day_like_render_result():
     assert pipe.drain() is not None and pipe.drain() is None
     pipe.close()
     assert [o.blob for o in out] == [rio.render_result("flow", day.cols, res, 0).blob for res in days]
+
+
+def test_result_pipe_inline_mode(monkeypatch):
+    """ONI_RESULT_PIPE=0 formats and writes each day at its own submit (no worker thread)."""
+    from types import SimpleNamespace
+
+    monkeypatch.setenv("ONI_RESULT_PIPE", "0")
+    day = generate_flows(1000, seed=2)
+    rows = np.arange(0, 40, dtype=np.int64)
+    s = np.linspace(0, 1, 40).astype(np.float32)
+    res = SimpleNamespace(rows=rows, scores=s, src_scores=s, dst_scores=s,
+                          src_words=np.zeros(40, np.uint32), dst_words=np.ones(40, np.uint32))
+    out = []
+    pipe = rio.ResultPipe("flow", None, write=out.append)
+    pipe.submit(day.cols, res, 0)
+    assert len(out) == 1 and out[0].blob == rio.render_result("flow", day.cols, res, 0).blob
+    assert pipe.drain() is None
+    pipe.close()

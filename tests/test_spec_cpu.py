@@ -288,3 +288,28 @@ def test_tiling_choice_and_alpha_in_row_rule(monkeypatch):
     assert _alpha_in_row_exact(2.5, 10**6) and _alpha_in_row_exact(0.5, (1 << 22))
     assert not _alpha_in_row_exact(0.5, 1 << 23)  # 2^23 + 0.5 needs 25 significant bits
     assert not _alpha_in_row_exact(0.1, 10) and not _alpha_in_row_exact(50 / 7, 10)
+
+
+def test_x01_pack_policy(monkeypatch):
+    """ONI_X01_PACK: "1" always, "0" never, "auto" only for Δ buffers of at least
+    ONI_X01_PACK_MIN_BYTES (default 4 MiB: the flow day's 0.46 MB buffer stays unpacked)."""
+    import torch
+
+    from oni355.models import gibbs as gm
+    from oni355.models.corpus import build_corpus
+
+    r = np.random.default_rng(3)
+    c = build_corpus(torch.from_numpy(r.integers(0, 20, 500)), torch.from_numpy(r.integers(0, 300, 500)),
+                     20, 300, torch.arange(20, dtype=torch.int32), 1, L=64)
+    m = gm.GibbsLDA(c, gm.GibbsConfig(K=20, seed=1))
+    nbytes = m.dn[0].numel() * 4
+    assert nbytes < gm.X01_PACK_MIN_BYTES
+    monkeypatch.delenv("ONI_X01_PACK", raising=False)
+    assert not m._x01_wanted()
+    monkeypatch.setenv("ONI_X01_PACK_MIN_BYTES", str(nbytes))
+    assert m._x01_wanted()
+    monkeypatch.setenv("ONI_X01_PACK", "0")
+    assert not m._x01_wanted()
+    monkeypatch.setenv("ONI_X01_PACK", "1")
+    monkeypatch.setenv("ONI_X01_PACK_MIN_BYTES", str(1 << 40))
+    assert m._x01_wanted()
