@@ -85,11 +85,15 @@ def _unique_first(h: torch.Tensor):
     """(sorted unique values, first row of each (CPU), inverse). Sort-based: an atomic-min
     scatter_reduce here serialised 2M rows onto a handful of distinct values (27 ms per call)."""
     sh, order = torch.sort(h, stable=True)
-    uniq, counts = torch.unique_consecutive(sh, return_counts=True)
-    starts = torch.cumsum(counts, 0) - counts
-    first = order[starts]
+    head = torch.ones_like(sh, dtype=torch.bool)
+    if sh.numel() > 1:
+        head[1:] = sh[1:] != sh[:-1]
+    # group id of every sorted row by a scan over the run heads (repeat_interleave of the few run
+    # lengths put one thread on each run: 436 µs per call on 2M rows with 5 distinct methods)
+    grp = torch.cumsum(head, 0) - 1
+    uniq, first = sh[head], order[head]
     inv = torch.empty_like(order)
-    inv[order] = torch.repeat_interleave(torch.arange(uniq.numel(), device=h.device), counts)
+    inv[order] = grp
     return uniq, first.cpu(), inv
 
 
