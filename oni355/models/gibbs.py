@@ -168,9 +168,10 @@ class GibbsLDA:
                                                                          SAMPLERS["lds"])
         if self.qpf == 5 and self.G == 1:
             self.qpf = 2  # "ldsq" (LDS counts + q-row prefetch) is the multi-lane variant; G = 1 has "lds"
-        if self.qpf in (2, 5) and corpus.max_doc_len() >= (1 << 24):
+        max_len = corpus.max_doc_len()  # one device read
+        if self.qpf in (2, 5) and max_len >= (1 << 24):
             self.qpf = 1  # LDS rows hold counts as f32: exact below 2^24
-        self._air = _alpha_in_row_exact(self.alpha, corpus.max_doc_len())
+        self._air = _alpha_in_row_exact(self.alpha, max_len)
         self.a = 0  # ndk parity
         self.b = 0  # delta-buffer parity
         self.cn = 0  # nk parity
@@ -255,7 +256,9 @@ class GibbsLDA:
         if self.comm is not None and self.comm.dist:
             self.comm.allreduce_(self.nwk)
             self.comm.allreduce_(self.nk[0])
-        self.T_global = int(self.nk[0][: self.K].sum())
+        # world 1: every token holds one topic, so Σ n_k = T (no device read); DP: the global sum
+        self.T_global = (int(self.nk[0][: self.K].sum()) if self.comm is not None and self.comm.dist
+                         else int(self.c.T))
         self._delta_on = False
         self._chg_q = []
         self._sync_aux_z()
@@ -533,6 +536,7 @@ class GibbsLDA:
         assert int(nwk.min()) >= 0 and int(ndk.min()) >= 0 and int(nk.min()) >= 0, "negative count"
         assert int(nwk.sum()) == tg, f"sum n_wk {int(nwk.sum())} != tokens {tg}"
         assert torch.equal(nwk.sum(0), nk), "n_k != column sums of n_wk"
+        assert int(nk.sum()) == self.T_global, "Σ n_k != token count"
         assert int(ndk.sum()) == tl, f"sum n_dk {int(ndk.sum())} != local tokens {tl}"
         assert not bool(self.nwk[:, K:].any()) and not bool(self.ndk_cur[:, K:].any()), "padding topics used"
 
