@@ -168,10 +168,13 @@ class GibbsLDA:
                                                                          SAMPLERS["lds"])
         if self.qpf == 5 and self.G == 1:
             self.qpf = 2  # "ldsq" (LDS counts + q-row prefetch) is the multi-lane variant; G = 1 has "lds"
-        max_len = corpus.max_doc_len()  # one device read
-        if self.qpf in (2, 5) and max_len >= (1 << 24):
-            self.qpf = 1  # LDS rows hold counts as f32: exact below 2^24
-        self._air = _alpha_in_row_exact(self.alpha, max_len)
+        self._air = False  # n + α LDS rows (LDS samplers only)
+        if self.qpf in (2, 5):
+            max_len = corpus.max_doc_len()  # one device read, only the LDS samplers need it
+            if max_len >= (1 << 24):
+                self.qpf = 1  # LDS rows hold counts as f32: exact below 2^24
+            else:
+                self._air = _alpha_in_row_exact(self.alpha, max_len)
         self.a = 0  # ndk parity
         self.b = 0  # delta-buffer parity
         self.cn = 0  # nk parity
