@@ -23,6 +23,8 @@
 #include <cstring>
 #include <ctime>
 #include <string>
+#include <map>
+#include <tuple>
 #include <vector>
 
 #include "../native/oni_native.h"
@@ -402,54 +404,75 @@ void decode(const uint8_t* base, const Pkt& p, int64_t pkt, Rows* r) {
   }
 }
 
-// IPv4 fragment reassembly (RFC 791): fragments grouped by (src, dst, id, proto); a datagram is
-// complete when its pieces cover [0, end of the last (MF = 0) fragment) without a hole. The row
-// takes the frame time / length / index of the fragment that completed it (tshark's view).
-void reassemble(std::vector<Frag>& fr, Rows* r) {
-  std::stable_sort(fr.begin(), fr.end(), [](const Frag& a, const Frag& b) {
-    if (a.src != b.src) return a.src < b.src;
-    if (a.dst != b.dst) return a.dst < b.dst;
-    if (a.id != b.id) return a.id < b.id;
-    if (a.proto != b.proto) return a.proto < b.proto;
-    return a.off < b.off;
-  });
-  size_t i = 0;
-  while (i < fr.size()) {
-    size_t j = i;
-    while (j < fr.size() && fr[j].src == fr[i].src && fr[j].dst == fr[i].dst && fr[j].id == fr[i].id &&
-           fr[j].proto == fr[i].proto)
-      ++j;
-    size_t total = 0;
-    bool last = false;
-    const Frag* newest = &fr[i];
-    for (size_t k = i; k < j; ++k) {
-      if (!fr[k].more) {
-        last = true;
-        total = fr[k].off + fr[k].data.size();
-      }
-      if (fr[k].pkt > newest->pkt) newest = &fr[k];
+// IPv4 fragment reassembly (RFC 791), in packet order. Fragments are grouped by (src, dst, id,
+// proto) into OPEN datagrams; a datagram closes as soon as its pieces cover [0, end of the last
+// (MF = 0) fragment) without a hole, and the row takes the frame time / length / index of the
+// fragment that completed it (tshark's view). The 16-bit IP id wraps within a day-long capture, so
+// a group is also closed (as incomplete) when a fragment offset it already holds shows up again --
+// that is the next datagram with the same id -- or when the new fragment arrives more than
+// kFragTimeoutNs of frame time after the group's first one (the kernel's ipfrag_time is 30 s).
+constexpr int64_t kFragTimeoutNs = 30ll * 1000000000ll;
+
+struct OpenDgram {
+  std::vector<const Frag*> parts;
+  int64_t first_ts = 0;
+};
+
+// complete? → parse into r and return true
+bool try_complete(const OpenDgram& g, Rows* r) {
+  size_t total = 0;
+  bool last = false;
+  const Frag* newest = g.parts[0];
+  for (const Frag* f : g.parts) {
+    if (!f->more) {
+      last = true;
+      total = f->off + f->data.size();
     }
-    if (last && total <= 65535) {
-      std::vector<uint8_t> buf(total);
-      size_t covered = 0;
-      bool ok = true;
-      for (size_t k = i; k < j && ok; ++k) {  // sorted by offset: require no hole
-        const Frag& f = fr[k];
-        if (f.off > covered) ok = false;
-        const size_t e = f.off + f.data.size();
-        if (ok && e > f.off && f.off < total) std::memcpy(buf.data() + f.off, f.data.data(), std::min(e, total) - f.off);
-        if (e > covered) covered = e;
-      }
-      if (ok && covered >= total)
-        parse_transport(buf.data(), total, fr[i].proto, newest->ts_ns, newest->origlen, fr[i].src, fr[i].dst,
-                        newest->pkt, r);
-      else
-        ++r->frag_incomplete;
-    } else {
-      ++r->frag_incomplete;
-    }
-    i = j;
+    if (f->pkt > newest->pkt) newest = f;
   }
+  if (!last || total > 65535) return false;
+  std::vector<const Frag*> o(g.parts);
+  std::stable_sort(o.begin(), o.end(), [](const Frag* a, const Frag* b) { return a->off < b->off; });
+  size_t covered = 0;
+  for (const Frag* f : o) {
+    if (f->off > covered) return false;  // hole
+    const size_t e = f->off + f->data.size();
+    if (e > covered) covered = e;
+  }
+  if (covered < total) return false;
+  std::vector<uint8_t> buf(total);
+  for (const Frag* f : o) {
+    const size_t e = f->off + f->data.size();
+    if (e > f->off && f->off < total) std::memcpy(buf.data() + f->off, f->data.data(), std::min(e, total) - f->off);
+  }
+  const Frag& h = *o[0];
+  parse_transport(buf.data(), total, h.proto, newest->ts_ns, newest->origlen, h.src, h.dst, newest->pkt, r);
+  return true;
+}
+
+void reassemble(std::vector<Frag>& fr, Rows* r) {
+  std::stable_sort(fr.begin(), fr.end(), [](const Frag& a, const Frag& b) { return a.pkt < b.pkt; });
+  std::map<std::tuple<uint32_t, uint32_t, uint16_t, uint8_t>, OpenDgram> open;
+  for (const Frag& f : fr) {
+    const auto key = std::make_tuple(f.src, f.dst, f.id, f.proto);
+    auto it = open.find(key);
+    if (it != open.end()) {
+      bool restart = f.ts_ns - it->second.first_ts > kFragTimeoutNs;
+      for (const Frag* p : it->second.parts) restart |= p->off == f.off;
+      if (restart) {
+        ++r->frag_incomplete;
+        open.erase(it);
+        it = open.end();
+      }
+    }
+    if (it == open.end()) {
+      it = open.emplace(key, OpenDgram{}).first;
+      it->second.first_ts = f.ts_ns;
+    }
+    it->second.parts.push_back(&f);
+    if (try_complete(it->second, r)) open.erase(it);
+  }
+  r->frag_incomplete += (int64_t)open.size();
 }
 
 struct Handle {

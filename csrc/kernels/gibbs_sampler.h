@@ -134,16 +134,75 @@ __device__ __forceinline__ void mark_changed_w(const OniGibbs& a, int32_t p, int
   atomicOr(reinterpret_cast<uint32_t*>(a.chg_mask) + (p >> 5), 1u << (p & 31));
 }
 
+// ---- deferred topic bookkeeping (DZ) ------------------------------------------------------------
+// On CDNA every vector-memory operation -- load, store or atomic -- retires through one in-order
+// vmcnt counter per wave. A sampler that writes a changed topic (tok_z byte, plus in MODE 4 the
+// zz_w pair and the bitmap atomicOr, which stays counted for ~600-3000 cycles) inside its token
+// loop therefore makes the NEXT step's wait for its q row also wait for those stores. The DZ
+// variant keeps the slice's topics in LDS instead (staged once in the prologue, 64 B per step:
+// step s, lane c at byte s·64 + c), so the token loop issues loads only; the epilogue writes the
+// slice back with 16-B stores and does the per-mode bookkeeping for the bytes that changed
+// (compared against the untouched global copy). Same draws, bit for bit: only where the topic
+// lives during the sweep changes. Slices up to kDzMaxLen steps (the auto chunk length is ≤ 128).
+constexpr int kDzMaxLen = 128;
+
+template <int MODE>
+__device__ __forceinline__ void dz_note_change(const OniGibbs& a, int64_t slot, int zo, int zn) {
+  if constexpr (MODE == 1) {
+    const int64_t w = (int64_t)a.tok_word[slot];
+    atomicAdd(&a.dnwk[w * a.KS + zo], -1);
+    atomicAdd(&a.dnwk[w * a.KS + zn], 1);
+  } else if constexpr (MODE == 3) {
+    a.z_w[a.wpos[slot]] = (uint8_t)zn;
+  } else if constexpr (MODE == 4) {
+    mark_changed_w(a, a.wpos[slot], zo, zn);
+  }
+}
+
+// Write a wave's LDS topic stage (len steps × 64 B) back to tok_z and do the MODE bookkeeping of
+// every changed byte. Called by all 64 lanes of the wave after a barrier.
+template <int MODE>
+__device__ __forceinline__ void dz_flush(const OniGibbs& a, const uint32_t* __restrict__ zs, int64_t off, int len,
+                                         int lane) {
+  const uint4* stage = reinterpret_cast<const uint4*>(zs);
+  uint4* dst = reinterpret_cast<uint4*>(a.tok_z + off);
+  for (int i = lane; i < len * 4; i += oni::kWave) {
+    const uint4 nw = stage[i];
+    const uint4 od = dst[i];
+    const uint32_t n4[4] = {nw.x, nw.y, nw.z, nw.w}, o4[4] = {od.x, od.y, od.z, od.w};
+    bool any = false;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) any |= n4[d] != o4[d];
+    if (!any) continue;
+    dst[i] = nw;
+    if constexpr (MODE == 1 || MODE == 3 || MODE == 4) {
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        uint32_t x = n4[d] ^ o4[d];
+        while (x) {
+          const int b = (__ffs(x) - 1) >> 3;
+          x &= ~(0xFFu << (8 * b));
+          dz_note_change<MODE>(a, off + (int64_t)i * 16 + d * 4 + b, (int)((o4[d] >> (8 * b)) & 0xFFu),
+                               (int)((n4[d] >> (8 * b)) & 0xFFu));
+        }
+      }
+    }
+  }
+}
+
 // MODE: 0 = no n_wk bookkeeping (full recount afterwards), 1 = per-token Δ atomics,
 //       2 = changed-slot ballot mask per step (delta recount afterwards),
 //       3 = changed topics also scattered into the word-sorted copy z_w (streaming recount afterwards)
 //       4 = changed tokens marked in a word-sorted bitmap + (old, new) topic copies (k_wdelta_recount)
-template <int G, int KP, bool INIT, int MODE, bool QPF>
+// DZ (G = 1, MODE != 2, not INIT): topics staged in LDS, bookkeeping in the epilogue (see dz_flush).
+template <int G, int KP, bool INIT, int MODE, bool QPF, bool DZ = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_gibbs(const OniGibbs a) {
-  constexpr bool ATOMIC = MODE == 1;
+  static_assert(!DZ || (G == 1 && !INIT && MODE != 2), "DZ: one-lane units, sweeps, MODE != 2");
+  constexpr bool ATOMIC = MODE == 1 && !DZ;
   constexpr int S = oni::kWave / G;
   constexpr int KS = G * KP;
   __shared__ int32_t red[kWavesPerBlock][KS];
+  __shared__ uint32_t zstage[DZ ? kWavesPerBlock : 1][DZ ? kDzMaxLen * 16 : 1];
 
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
@@ -178,13 +237,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) 
   for (int j = 0; j < KP; ++j) qv[j] = 0.f;
 
   int nchg = 0;
+  uint8_t* zb = DZ ? reinterpret_cast<uint8_t*>(zstage[wave]) : nullptr;
+  if constexpr (DZ) {
+    // the slice's topics → LDS (slice_off is a multiple of 64 B: 16-B aligned pieces)
+    const uint4* src = reinterpret_cast<const uint4*>(a.tok_z + off);
+    uint4* stg = reinterpret_cast<uint4*>(zstage[wave]);
+    for (int i = lane; i < len * 4; i += oni::kWave) stg[i] = src[i];
+    __syncthreads();
+  }
   // software-pipelined token stream: step s+1's word/topic loads are issued before step s's
   // sampling, so their latency hides behind the math and stores of step s
   uint32_t w_nx = len > 0 ? a.tok_word[off + c] : oni::kPadWord;
-  int z_nx = (!INIT && len > 0) ? (int)a.tok_z[off + c] : 0;
+  int z_nx = (!INIT && len > 0) ? (DZ ? (int)zb[c] : (int)a.tok_z[off + c]) : 0;
   // MODE 3/4: the token's word-sorted position streams with its word/topic (a load issued only
   // once the draw is known would expose a full memory latency on almost every step)
-  constexpr bool WPF = !INIT && (MODE == 3 || MODE == 4);
+  constexpr bool WPF = !INIT && !DZ && (MODE == 3 || MODE == 4);
   int32_t p_nx = (WPF && len > 0) ? a.wpos[off + c] : 0;
   // QPF: the next token's q row is also fetched one step ahead (needs only its word id)
   float qn[KP];
@@ -198,7 +265,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) 
     const int32_t pw = p_nx;
     if (s + 1 < len) {
       w_nx = a.tok_word[idx + S];
-      if (!INIT) z_nx = a.tok_z[idx + S];
+      if (!INIT) z_nx = DZ ? (int)zb[(s + 1) * S + c] : (int)a.tok_z[idx + S];
       if (WPF) p_nx = a.wpos[idx + S];
     }
     if (w == oni::kPadWord) continue;  // uniform across the G lanes of a unit
@@ -252,7 +319,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) 
       const int zn = cnt < a.K - 1 ? cnt : a.K - 1;
 #pragma unroll
       for (int j = 0; j < KP; ++j) n[j] += (kbase + j == zn);
-      if (zn != zo && g == 0) {
+      if constexpr (DZ) {
+        // LDS only: no vector-memory store in the token loop
+        nchg += zn != zo;
+        if (zn != zo) zb[s * S + c] = (uint8_t)zn;
+      } else if (zn != zo && g == 0) {
         ++nchg;
         a.tok_z[idx] = (uint8_t)zn;
         if constexpr (MODE == 3) a.z_w[pw] = (uint8_t)zn;
@@ -262,7 +333,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) 
           atomicAdd(&a.dnwk[(int64_t)w * KS + zn], 1);
         }
       }
-      if constexpr (MODE == 2) {
+      if constexpr (MODE == 2 && !DZ) {
         // lane 0 (c = 0) owns the slice's longest chunk, so it is active at every step
         const uint64_t m = __ballot(zn != zo && g == 0);
         if (lane == 0) a.chg_mask[(off + (int64_t)s * S) / S] = m;
@@ -274,6 +345,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) 
 
   // ---- epilogue: doc rows + per-topic totals -------------------------------------------------
   if (!INIT && a.chg_count) add_wave_count(a.chg_count, nchg);
+  if constexpr (DZ) {
+    __syncthreads();  // every lane's LDS topic writes before the wave reads the stage back
+    dz_flush<MODE>(a, zstage[wave], off, len, lane);
+  }
   int32_t d[KP];
 #pragma unroll
   for (int j = 0; j < KP; ++j) d[j] = 0;
@@ -326,12 +401,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) 
 // so token s+1's word is already in registers at the top of step s: its q row is issued there,
 // before step s's math and stores, and waited for only when the step ends. Same arithmetic as
 // k_gibbs (mul + add chain), so the same draws bitwise.
-template <int KP, int MODE>
+// DZ: the topics live in LDS during the sweep (see dz_flush): the loop issues loads only.
+template <int KP, int MODE, bool DZ = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_gibbs_q2(const OniGibbs a) {
-  constexpr bool ATOMIC = MODE == 1;
+  static_assert(!DZ || MODE != 2, "DZ: MODE != 2");
+  constexpr bool ATOMIC = MODE == 1 && !DZ;
   constexpr int S = oni::kWave;
   constexpr int KS = KP;
   __shared__ int32_t red[kWavesPerBlock][KS];
+  __shared__ uint32_t zstage[DZ ? kWavesPerBlock : 1][DZ ? kDzMaxLen * 16 : 1];
 
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
@@ -353,13 +431,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) 
   const uint32_t pos0 = live ? (uint32_t)a.chunk_pos0[chunk] : 0u;
   const uint32_t sweep = *a.sweep_ctr;
 
-  constexpr bool WPF = MODE == 3 || MODE == 4;
+  uint8_t* zb = DZ ? reinterpret_cast<uint8_t*>(zstage[wave]) : nullptr;
+  if constexpr (DZ) {
+    const uint4* src = reinterpret_cast<const uint4*>(a.tok_z + off);
+    uint4* stg = reinterpret_cast<uint4*>(zstage[wave]);
+    for (int i = lane; i < len * 4; i += oni::kWave) stg[i] = src[i];
+    __syncthreads();
+  }
+  constexpr bool WPF = !DZ && (MODE == 3 || MODE == 4);
   // token stream: (w0, z0, p0) = token s, (w1, z1, p1) = token s + 1
   uint32_t w0 = len > 0 ? a.tok_word[off + c] : oni::kPadWord;
-  int z0 = len > 0 ? (int)a.tok_z[off + c] : 0;
+  int z0 = len > 0 ? (DZ ? (int)zb[c] : (int)a.tok_z[off + c]) : 0;
   int32_t p0 = (WPF && len > 0) ? a.wpos[off + c] : 0;
   uint32_t w1 = len > 1 ? a.tok_word[off + S + c] : oni::kPadWord;
-  int z1 = len > 1 ? (int)a.tok_z[off + S + c] : 0;
+  int z1 = len > 1 ? (DZ ? (int)zb[S + c] : (int)a.tok_z[off + S + c]) : 0;
   int32_t p1 = (WPF && len > 1) ? a.wpos[off + S + c] : 0;
   float qv[KP], qn[KP];
 #pragma unroll
@@ -382,7 +467,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) 
     p0 = p1;
     if (s + 2 < len) {
       w1 = a.tok_word[idx + 2 * S];
-      z1 = a.tok_z[idx + 2 * S];
+      z1 = DZ ? (int)zb[(s + 2) * S + c] : (int)a.tok_z[idx + 2 * S];
       if (WPF) p1 = a.wpos[idx + 2 * S];
     } else {
       w1 = oni::kPadWord;
@@ -407,7 +492,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) 
       const int zn = cnt < a.K - 1 ? cnt : a.K - 1;
 #pragma unroll
       for (int j = 0; j < KP; ++j) n[j] += (j == zn);
-      if (zn != zo) {
+      if constexpr (DZ) {
+        nchg += zn != zo;
+        if (zn != zo) zb[s * S + c] = (uint8_t)zn;
+      } else if (zn != zo) {
         ++nchg;
         a.tok_z[idx] = (uint8_t)zn;
         if constexpr (MODE == 3) a.z_w[pw] = (uint8_t)zn;
@@ -417,7 +505,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) 
           atomicAdd(&a.dnwk[(int64_t)w * KS + zn], 1);
         }
       }
-      if constexpr (MODE == 2) {
+      if constexpr (MODE == 2 && !DZ) {
         const uint64_t m = __ballot(zn != zo);
         if (lane == 0) a.chg_mask[(off + (int64_t)s * S) / S] = m;
       }
@@ -430,6 +518,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) 
 
   // ---- epilogue: doc rows + per-topic totals (as k_gibbs, G = 1) --------------------------------
   if (a.chg_count) add_wave_count(a.chg_count, nchg);
+  if constexpr (DZ) {
+    __syncthreads();
+    dz_flush<MODE>(a, zstage[wave], off, len, lane);
+  }
   int32_t d[KP];
 #pragma unroll
   for (int j = 0; j < KP; ++j) d[j] = 0;
@@ -1080,9 +1172,31 @@ int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s)
   if (a.KS != G * KP || mode < 0 || mode > 4) return (int)hipErrorInvalidValue;
   if (G == 1 && qpf == 5) qpf = 2;  // q-prefetching LDS sampler is the multi-lane variant
   if (G > 1 && qpf == 6) qpf = 4;   // the two-deep stream variant is written for G = 1
+  // qpf 7 = DZ (LDS-staged topics, deferred bookkeeping): G = 1 sweeps of slices ≤ kDzMaxLen steps
+  // in MODE 0/1/3/4; the caller guarantees the slice bound (slice_len[0] is the longest)
+  if (qpf == 7 && (G != 1 || init || mode == 2)) qpf = 4;
+  if (qpf == 8 && (G != 1 || init || mode == 2)) qpf = G == 1 ? 6 : 4;  // 8 = k_gibbs_q2 + DZ
   const unsigned grid = (unsigned)((a.n_slices + kWavesPerBlock - 1) / kWavesPerBlock);
   if (grid == 0) return 0;
   if constexpr (G == 1) {
+    if (qpf == 8) {
+      switch (mode) {
+        case 0: k_gibbs_q2<KP, 0, true><<<grid, kBlock, 0, s>>>(a); break;
+        case 1: k_gibbs_q2<KP, 1, true><<<grid, kBlock, 0, s>>>(a); break;
+        case 3: k_gibbs_q2<KP, 3, true><<<grid, kBlock, 0, s>>>(a); break;
+        default: k_gibbs_q2<KP, 4, true><<<grid, kBlock, 0, s>>>(a); break;
+      }
+      return (int)hipGetLastError();
+    }
+    if (qpf == 7) {
+      switch (mode) {
+        case 0: k_gibbs<1, KP, false, 0, true, true><<<grid, kBlock, 0, s>>>(a); break;
+        case 1: k_gibbs<1, KP, false, 1, true, true><<<grid, kBlock, 0, s>>>(a); break;
+        case 3: k_gibbs<1, KP, false, 3, true, true><<<grid, kBlock, 0, s>>>(a); break;
+        default: k_gibbs<1, KP, false, 4, true, true><<<grid, kBlock, 0, s>>>(a); break;
+      }
+      return (int)hipGetLastError();
+    }
     if (!init && qpf == 6) {
       switch (mode) {
         case 0: k_gibbs_q2<KP, 0><<<grid, kBlock, 0, s>>>(a); break;

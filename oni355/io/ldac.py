@@ -99,7 +99,7 @@ def export_gibbs(directory: str, model, prefix: str = "final", word_assignments:
     from ..models.corpus import canonical_tokens
     K = model.K
     phi = model.phi()[:, :K].double().cpu().numpy()  # [V, K]
-    gamma = (model.ndk_cur[: model.c.D, :K].double() + model.alpha).cpu().numpy()
+    gamma = (model.ndk_cur[: model.c.D_own, :K].double() + model.alpha).cpu().numpy()
     write_model(directory, prefix, np.log(phi.T), gamma, model.alpha)
     if model.likelihoods:
         write_likelihood(os.path.join(directory, "likelihood.dat"), model.likelihoods)

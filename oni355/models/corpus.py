@@ -50,6 +50,16 @@ class Corpus:
     tile_wlo: torch.Tensor | None = None  # int32 [n_tiles] first word of each recount tile
     tile_whi: torch.Tensor | None = None  # int32 [n_tiles] last word of each recount tile
     wpos: torch.Tensor | None = None      # int32 [SELL slots] word-sorted position of each slot (-1: pad)
+    # data parallel with heavy documents cut across ranks (pipeline.common.apply_split): rows
+    # [D_own, D) are pieces of split documents; chunk_rng0 is every chunk's GLOBAL canonical
+    # position (the Philox counter), chunk_pos0 stays the position inside the local row
+    split: dict | None = None
+    chunk_rng0: torch.Tensor | None = None
+
+    @property
+    def D_own(self) -> int:
+        """Rows that are this rank's documents (θ / outputs); the rest are split pieces."""
+        return int(self.split["D_own"]) if self.split is not None else self.D
 
     @property
     def S(self) -> int:
@@ -71,7 +81,9 @@ class Corpus:
         return self.doc_tok_ptr[1:] - self.doc_tok_ptr[:-1]
 
     def max_doc_len(self) -> int:
-        return int(self.doc_lengths().max()) if self.D else 0
+        """Largest doc-topic count a row can hold (a split document's rows hold its global counts)."""
+        m = int(self.doc_lengths().max()) if self.D else 0
+        return max(m, int(self.split["max_count"])) if self.split is not None else m
 
     def stats(self) -> dict:
         return {"D": self.D, "V": self.V, "T": self.T, "nnz": self.nnz, "slices": self.n_slices,

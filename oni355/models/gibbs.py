@@ -30,7 +30,8 @@ from .corpus import Corpus, canonical_tokens
 NK_REP = 32
 # X01 payload packing pays only once the all-reduce is bandwidth-bound (see GibbsLDA._x01_wanted)
 X01_PACK_MIN_BYTES = 4 << 20
-SAMPLERS = {"pp": 1, "plain": 0, "lds": 2, "qpf": 4, "ldsq": 5, "q2": 6}  # -> oni_gibbs_launch qpf argument
+DZ_MAX_LEN = 128  # kDzMaxLen (csrc/kernels/gibbs_sampler.h)
+SAMPLERS = {"pp": 1, "plain": 0, "lds": 2, "qpf": 4, "ldsq": 5, "q2": 6, "dz": 7, "q2dz": 8}  # -> oni_gibbs_launch qpf argument
 
 
 @dataclass
@@ -125,7 +126,18 @@ class GibbsLDA:
         # Δn_k in NK_REP replicas (block b adds into b % NK_REP): the per-block topic totals
         # would otherwise queue thousands of same-address atomics on KS words
         self._aux_off = V * KS + NK_REP * KS
-        self.dn = [torch.empty(self._aux_off + ops.DN_AUX, dtype=i32, device=dev) for _ in range(2)]
+        # heavy documents cut across ranks (pipeline.common.SplitPlan): their per-rank Δn_dk rows
+        # ride at the end of the X01 buffer ([V·KS | NK_REP·KS | DN_AUX | n_split·KS])
+        self._split = None
+        sp = corpus.split
+        if sp is not None and comm is not None and comm.dist and int(sp["n_split"]) > 0:
+            pr, qr = sp["piece_rows"].to(dev), sp["prim_rows"].to(dev)
+            pj, qj = sp["piece_j"].to(dev), sp["prim_j"].to(dev)
+            self._split = dict(n=int(sp["n_split"]), piece_rows=pr, piece_j=pj, all_rows=torch.cat([pr, qr]),
+                               all_j=torch.cat([pj, qj]))
+        self._split_off = self._aux_off + ops.DN_AUX
+        n_split = self._split["n"] if self._split is not None else 0
+        self.dn = [torch.empty(self._split_off + n_split * KS, dtype=i32, device=dev) for _ in range(2)]
         self.q = torch.zeros(V, KS, dtype=torch.float32, device=dev)
         self.sweep_ctr = torch.zeros(1, dtype=i32, device=dev)
         if cfg.count_mode not in ("auto", "dual", "delta", "recount", "atomic", "wdelta"):
@@ -167,7 +179,9 @@ class GibbsLDA:
         self.qpf = SAMPLERS[cfg.sampler] if cfg.sampler != "auto" else (SAMPLERS["qpf"] if self.G == 1 else
                                                                          SAMPLERS["lds"])
         if self.qpf == 5 and self.G == 1:
-            self.qpf = 2  # "ldsq" (LDS counts + q-row prefetch) is the multi-lane variant; G = 1 has "lds"
+            self.qpf = 2
+        if self.qpf in (7, 8) and (self.G != 1 or corpus.L > DZ_MAX_LEN):
+            self.qpf = 4  # "dz" stages one slice's topics in LDS: one-lane units, chunks ≤ 128 tokens  # "ldsq" (LDS counts + q-row prefetch) is the multi-lane variant; G = 1 has "lds"
         self._air = False  # n + α LDS rows (LDS samplers only)
         if self.qpf in (2, 5):
             max_len = corpus.max_doc_len()  # one device read, only the LDS samplers need it
@@ -231,9 +245,10 @@ class GibbsLDA:
     # ---------------------------------------------------------------------------------------------
     def _state(self, init: bool) -> dict:
         c = self.c
+        # the sampler reads chunk_pos0 only as the Philox position: split pieces use global ones
         st = dict(tok_word=c.tok_word, tok_z=self.tok_z, slice_off=c.slice_off, slice_len=c.slice_len,
-                  chunk_doc=c.chunk_doc, chunk_pos0=c.chunk_pos0, chunk_key=c.chunk_key, chunk_multi=c.chunk_multi,
-                  q=self.q)
+                  chunk_doc=c.chunk_doc, chunk_pos0=c.chunk_rng0 if c.chunk_rng0 is not None else c.chunk_pos0,
+                  chunk_key=c.chunk_key, chunk_multi=c.chunk_multi, q=self.q)
         VK = self.V * self.KS
         if init:
             st.update(ndk_src=self.ndk[0], ndk_dst=self.ndk[0], dnwk=self.nwk, dnk=self.nk[0])
@@ -256,6 +271,7 @@ class GibbsLDA:
         ops.gibbs_pass(self._state(True), self.G, self.KP, self.K, self.alpha, self.cfg.seed, True,
                        self.sweep_ctr, self.c.chunk_len, host_sweep=0, mode=0)
         ops.recount(self.c.wsorted, self.c.wslot, self.tok_z, self.nwk, self.KS)
+        self._split_sync_absolute(self.ndk[0])
         if self.comm is not None and self.comm.dist:
             self.comm.allreduce_(self.nwk)
             self.comm.allreduce_(self.nk[0])
@@ -268,6 +284,33 @@ class GibbsLDA:
         self.sweeps_done = 0
         self._graph = None
         self._prime()
+
+    # ---- split documents: one n_dk row per document across its pieces ---------------------------
+    def _split_sync_absolute(self, ndk: torch.Tensor) -> None:
+        """Rows of split documents := the sum of their pieces' counts over all ranks (after the
+        init pass or a restore, when piece rows hold local counts and primary rows nothing)."""
+        sp = self._split
+        if sp is None:
+            return
+        tot = torch.zeros(sp["n"], self.KS, dtype=torch.int32, device=self.device)
+        tot.index_add_(0, sp["piece_j"], ndk.index_select(0, sp["piece_rows"]))
+        self.comm.allreduce_(tot)
+        ndk.index_copy_(0, sp["all_rows"], tot.index_select(0, sp["all_j"]))
+
+    def _split_delta(self, buf: torch.Tensor, src: torch.Tensor, dst: torch.Tensor) -> None:
+        """X01 tail := this rank's Δn_dk of every split document (Σ over its pieces)."""
+        sp = self._split
+        reg = buf[self._split_off:].view(sp["n"], self.KS)
+        reg.zero_()
+        r = sp["piece_rows"]
+        reg.index_add_(0, sp["piece_j"], dst.index_select(0, r) - src.index_select(0, r))
+
+    def _split_apply(self, buf: torch.Tensor, src: torch.Tensor, dst: torch.Tensor) -> None:
+        """After the all-reduce: every row of a split document := sweep-start row + global Δ."""
+        sp = self._split
+        reg = buf[self._split_off:].view(sp["n"], self.KS)
+        r = sp["all_rows"]
+        dst.index_copy_(0, r, src.index_select(0, r) + reg.index_select(0, sp["all_j"]))
 
     def _sweep_mode(self, sweep: int) -> int:
         """Count mode used by (1-based) sweep ``sweep``."""
@@ -335,7 +378,8 @@ class GibbsLDA:
         self._zw_synced = False  # tok_z was (re)written outside the sweeps (init / restore)
         VK = self.V * self.KS
         self.dn[0].zero_()
-        ops.gibbs_apply(self.nwk, self.dn[0], self.dn[1], self.nk[self.cn], self.nk[1 - self.cn], self.q, self.V,
+        so = self._split_off
+        ops.gibbs_apply(self.nwk, self.dn[0][:so], self.dn[1][:so], self.nk[self.cn], self.nk[1 - self.cn], self.q, self.V,
                         self.K, self.KS, self.beta, self.vbeta, self.sweep_ctr, bump=False,
                         rows_copy=(self.ndk[self.a], self.ndk[1 - self.a], self.c.long_rows))
         self.cn = 1 - self.cn
@@ -372,9 +416,14 @@ class GibbsLDA:
             # dn[b] head := Δn_wk of the tokens that changed topic this sweep
             ops.delta_recount(c.wslot, c.tile_wlo, c.tile_whi, self.chg_mask, c.tok_word, self.tok_z, self.tok_zprev,
                               head, self.KS, self.G)
+        if self._split is not None:
+            self._split_delta(self.dn[self.b], self.ndk[self.a], self.ndk[1 - self.a])
         if self.comm is not None and self.comm.dist:
             self._allreduce_dn(self.dn[self.b])
-        ops.gibbs_apply(self.nwk, self.dn[self.b], self.dn[1 - self.b], self.nk[self.cn], self.nk[1 - self.cn],
+        if self._split is not None:
+            self._split_apply(self.dn[self.b], self.ndk[self.a], self.ndk[1 - self.a])
+        so = self._split_off
+        ops.gibbs_apply(self.nwk, self.dn[self.b][:so], self.dn[1 - self.b][:so], self.nk[self.cn], self.nk[1 - self.cn],
                         self.q, self.V, self.K, self.KS, self.beta, self.vbeta, self.sweep_ctr, bump=True,
                         absolute=mode in (0, 3), rows_copy=(self.ndk[1 - self.a], self.ndk[self.a], c.long_rows))
         self.a, self.b, self.cn = 1 - self.a, 1 - self.b, 1 - self.cn
@@ -529,13 +578,15 @@ class GibbsLDA:
         tokens, no negative count, n_k = column sums of n_wk. Raises AssertionError."""
         K = self.K
         T_loc = torch.tensor([float(self.c.T)], dtype=torch.float64, device=self.device)
+        # rows [0, D_own) are this rank's documents (split documents held whole by their primary)
+        T_rows = int(self.c.split["own_tokens"]) if self.c.split is not None else int(self.c.T)
         T_glob = T_loc.clone()
         if self.comm is not None and self.comm.dist:
             self.comm.allreduce_(T_glob)
         nwk = self.nwk[:, :K].to(torch.int64)
         nk = self.nk_cur[:K].to(torch.int64)
-        ndk = self.ndk_cur[: self.c.D, :K].to(torch.int64)
-        tg, tl = int(T_glob.item()), int(T_loc.item())
+        ndk = self.ndk_cur[: self.c.D_own, :K].to(torch.int64)
+        tg, tl = int(T_glob.item()), T_rows
         assert int(nwk.min()) >= 0 and int(ndk.min()) >= 0 and int(nk.min()) >= 0, "negative count"
         assert int(nwk.sum()) == tg, f"sum n_wk {int(nwk.sum())} != tokens {tg}"
         assert torch.equal(nwk.sum(0), nk), "n_k != column sums of n_wk"
@@ -607,9 +658,10 @@ class GibbsLDA:
         nk = self.nk_cur[:K].to(torch.float64)
         word = (K * (math.lgamma(V * b) - V * math.lgamma(b)) + torch.lgamma(nwk + b).sum()
                 - torch.lgamma(nk + V * b).sum())
-        ndk = self.ndk_cur[: self.c.D, :K].to(torch.float64)
+        D_own = self.c.D_own
+        ndk = self.ndk_cur[:D_own, :K].to(torch.float64)
         nd = ndk.sum(1)
-        doc = (self.c.D * (math.lgamma(K * a) - K * math.lgamma(a)) + torch.lgamma(ndk + a).sum()
+        doc = (D_own * (math.lgamma(K * a) - K * math.lgamma(a)) + torch.lgamma(ndk + a).sum()
                - torch.lgamma(nd + K * a).sum())
         doc_v = doc.reshape(1)
         if self.comm is not None and self.comm.dist:
@@ -647,6 +699,7 @@ class GibbsLDA:
         self.ndk[0].view(-1).index_add_(0, tdoc * KS + zz, torch.ones_like(zz, dtype=torch.int32))
         self.nwk.view(-1).index_add_(0, tword * KS + zz, torch.ones_like(zz, dtype=torch.int32))
         self.nk[0].index_add_(0, zz, torch.ones_like(zz, dtype=torch.int32))
+        self._split_sync_absolute(self.ndk[0])
         if self.comm is not None and self.comm.dist:
             self.comm.allreduce_(self.nwk)
             self.comm.allreduce_(self.nk[0])

@@ -9,6 +9,7 @@ sample -- are independent of the GPU count.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -30,6 +31,14 @@ def u32_to_i64(t: torch.Tensor) -> torch.Tensor:
 
 def i64_to_u32bits(t: torch.Tensor) -> torch.Tensor:
     return (t & U32MASK).to(torch.int64).to(torch.int32) if t.dtype == torch.int64 else t
+
+
+def feedback_here(comm: Comm | None) -> bool:
+    """Does this rank contribute the analyst feedback tokens (C19)? Every rank reads the same
+    scores CSV, but its sev = 3 rows must enter the GLOBAL corpus once -- DUPFACTOR times, not
+    world × DUPFACTOR -- so only rank 0 adds them; owner routing then sends each token to the rank
+    that owns its document, and the corpus equals the single-GPU one."""
+    return comm is None or not comm.dist or comm.rank == 0
 
 
 @traced("oni:vocab")
@@ -75,6 +84,47 @@ def doc_owner(doc_keys64: torch.Tensor, world: int) -> torch.Tensor:
 
 HEAVY_DOCS_PER_RANK = 4096
 PLACEMENT_BUCKETS_PER_RANK = 64
+# A document holding more than 1/(SPLIT_DEN · world) of the day's tokens (one NAT gateway or
+# resolver) is cut into chunk-aligned pieces that are placed like documents;
+# ONI_SPLIT_DEN=0 places every document whole.
+SPLIT_DEN = float(os.environ.get("ONI_SPLIT_DEN", "2"))
+# smallest world that splits (tests set 1 to run the piece machinery on a forced 1-rank group)
+SPLIT_MIN_WORLD = int(os.environ.get("ONI_SPLIT_MIN_WORLD", "2"))
+
+
+@dataclass
+class SplitPlan:
+    """Heavy documents cut across ranks. Piece k of document j covers canonical token positions
+    [p0, p1) of j (multiples of the chunk length L, so every piece is a run of whole chunks of the
+    single-GPU layout); pieces are sampled where they are placed, against the sweep-start n_dk row
+    of the whole document, and their Δn_dk rows ride in the X01 all-reduce (models/gibbs.py).
+    The primary (owner of piece 0) receives all of the document's tokens for scoring and holds its
+    θ row like any owned document."""
+    keys: torch.Tensor        # int64 [n] doc keys of the split documents (ascending)
+    count: np.ndarray         # int64 [n] global token count of each
+    piece_doc: np.ndarray     # int64 [m] split index of each piece
+    piece_p0: np.ndarray      # int64 [m]
+    piece_p1: np.ndarray      # int64 [m]
+    piece_owner: np.ndarray   # int64 [m]
+    primary: np.ndarray       # int64 [n]
+    L: int
+
+    @property
+    def n(self) -> int:
+        return int(self.keys.numel())
+
+
+def _split_pieces(counts: np.ndarray, thr: float, L: int):
+    """(doc index, p0, p1) of the pieces of every count above ``thr``: runs of ⌊thr / L⌋ chunks."""
+    pc = max(1, int(thr // L))
+    doc, p0, p1 = [], [], []
+    for i, c in enumerate(counts.tolist()):
+        n_ch = -(-int(c) // L)
+        for k in range(0, n_ch, pc):
+            doc.append(i)
+            p0.append(k * L)
+            p1.append(min((k + pc) * L, int(c)))
+    return np.asarray(doc, np.int64), np.asarray(p0, np.int64), np.asarray(p1, np.int64)
 
 
 def lpt_place(counts: np.ndarray, load: np.ndarray) -> np.ndarray:
@@ -104,7 +154,8 @@ def lpt_place(counts: np.ndarray, load: np.ndarray) -> np.ndarray:
     return owner
 
 
-def place_docs(doc_keys64: torch.Tensor, weights: torch.Tensor | None, comm: Comm, per_doc: bool = False):
+def place_docs(doc_keys64: torch.Tensor, weights: torch.Tensor | None, comm: Comm, per_doc: bool = False,
+               split_L: int | None = None):
     """Owner rank of each token's document, balanced by global token counts.
 
     IP documents are power-law sized (one synthetic 100M-flow day puts ~8 % of all tokens on a
@@ -118,7 +169,10 @@ def place_docs(doc_keys64: torch.Tensor, weights: torch.Tensor | None, comm: Com
     Deterministic on every rank (same candidate set and counts; order count desc, key asc; ties →
     lowest rank); results stay world-size invariant because the sampler's chain never depends on
     placement. Returns the owner of every token, or with ``per_doc`` (owner of every local
-    document int32, document id of every token int32, sorted unique local doc keys int64)."""
+    document int32, document id of every token int32, sorted unique local doc keys int64).
+    ``split_L`` > 0 (the chunk length) also cuts candidates above 1/(SPLIT_DEN · world) of all
+    tokens into pieces (:class:`SplitPlan`, appended to the return value; a split document's
+    tokens go to its primary)."""
     W = comm.world
     dev = doc_keys64.device
     if doc_keys64.is_cuda:
@@ -150,16 +204,42 @@ def place_docs(doc_keys64: torch.Tensor, weights: torch.Tensor | None, comm: Com
     both = torch.cat([ccnt, bload])  # one collective for candidate counts + bucket loads
     comm.allreduce_(both)
     nc = int(cand.numel())
-    o = torch.argsort(both, descending=True, stable=True)  # candidates (by key) before buckets on ties
-    assign = lpt_place(both[o].cpu().numpy(), np.zeros(W, dtype=np.int64))
-    iown = torch.empty(nc + B, dtype=torch.int64)
-    iown[o.cpu()] = torch.from_numpy(assign.astype(np.int64))
-    iown = iown.to(dev)
-    uown = iown[nc:][hb]
-    uown[pos[hit]] = iown[:nc][hit]
+    bc = both.cpu().numpy().astype(np.int64)
+    ccg, bl = bc[:nc], bc[nc:]
+    sp = np.zeros(nc, bool)
+    if split_L and split_L > 0 and W >= SPLIT_MIN_WORLD and SPLIT_DEN > 0:
+        thr = float(bc.sum()) / (SPLIT_DEN * W)
+        sp = ccg > max(thr, 2.0 * split_L)
+    pdoc, pp0, pp1 = _split_pieces(ccg[sp], float(bc.sum()) / (SPLIT_DEN * W) if sp.any() else 1.0, max(split_L or 1, 1))
+    ns_idx = np.nonzero(~sp)[0]
+    # items in placement order: whole candidates (by key), pieces, buckets; LPT by count desc, stable
+    items = np.concatenate([ccg[ns_idx], pp1 - pp0, bl])
+    o = np.argsort(-items, kind="stable")
+    assign = lpt_place(items[o], np.zeros(W, dtype=np.int64))
+    iown = np.empty(items.size, np.int64)
+    iown[o] = assign
+    n_ns, n_p = ns_idx.size, pdoc.size
+    cown = np.empty(nc, np.int64)
+    cown[ns_idx] = iown[:n_ns]
+    piece_owner = iown[n_ns:n_ns + n_p]
+    sp_idx = np.nonzero(sp)[0]
+    primary = np.empty(sp_idx.size, np.int64)
+    if n_p:
+        first = np.r_[True, pdoc[1:] != pdoc[:-1]]
+        primary[:] = piece_owner[first]
+        cown[sp_idx] = primary
+    bown = torch.from_numpy(iown[n_ns + n_p:]).to(dev)
+    uown = bown[hb]
+    uown[pos[hit]] = torch.from_numpy(cown).to(dev)[hit]
+    plan = None
+    if sp.any():
+        plan = SplitPlan(keys=cand[torch.from_numpy(sp_idx).to(dev)].cpu(), count=ccg[sp], piece_doc=pdoc,
+                         piece_p0=pp0, piece_p1=pp1, piece_owner=piece_owner, primary=primary, L=int(split_L))
     if per_doc:
-        return uown.to(torch.int32), inv, ukeys
-    return uown[inv.long()]
+        out = (uown.to(torch.int32), inv, ukeys)
+    else:
+        out = uown[inv.long()]
+    return (out, plan) if split_L is not None else out
 
 
 def balanced_owner(doc_keys64: torch.Tensor, weights: torch.Tensor, comm: Comm) -> torch.Tensor:
@@ -173,11 +253,12 @@ class Route:
     order: torch.Tensor     # int [n_sent]: slot i of the owner-grouped send buffer holds token order[i]
     send_counts: list       # tokens sent to each rank
     recv_counts: list       # tokens received from each rank (the owner side's layout)
+    split: SplitPlan | None = None  # heavy documents cut across ranks (their tokens went to the primary)
 
 
 @traced("oni:route_to_owners")
 def route_to_owners(doc_keys64: torch.Tensor, word_ids: torch.Tensor, weights: torch.Tensor | None,
-                    comm: Comm | None):
+                    comm: Comm | None, split_L: int = 0):
     """Send each token to its document's owner rank and dictionary-encode the owner's documents.
 
     Returns (sorted unique owner-local doc keys int64, doc id int32, word id int32, weight int32
@@ -195,7 +276,7 @@ def route_to_owners(doc_keys64: torch.Tensor, word_ids: torch.Tensor, weights: t
         return udoc, inv, word_ids, w, None
     if doc_keys64.is_cuda:
         from ..ops import corpus as oc
-        uown, ids, ukeys = place_docs(doc_keys64, weights, comm, per_doc=True)
+        (uown, ids, ukeys), plan = place_docs(doc_keys64, weights, comm, per_doc=True, split_L=split_L)
         U = int(ukeys.numel())
         # key lists per owner: the local docs grouped by owner, ascending keys inside a group
         kperm = torch.argsort(uown, stable=True)
@@ -216,8 +297,8 @@ def route_to_owners(doc_keys64: torch.Tensor, word_ids: torch.Tensor, weights: t
         recv = comm.alltoallv(send, scl, recv_counts=rc)
         udoc, kid = encode_docs(u32_to_i64(rkeys.view(-1)).contiguous())
         inv, wi, wt = oc.route_unpack(recv.contiguous(), rc, krc, kid, weights is not None)
-        return udoc, inv, wi, wt, Route(order, scl, rc)
-    owner = place_docs(doc_keys64, weights, comm)
+        return udoc, inv, wi, wt, Route(order, scl, rc, plan)
+    owner, plan = place_docs(doc_keys64, weights, comm, split_L=split_L)
     order = torch.argsort(owner, stable=True)
     counts = torch.bincount(owner, minlength=comm.world)
     cols = [i64_to_u32bits(doc_keys64[order]), word_ids[order].to(torch.int32)]
@@ -229,7 +310,7 @@ def route_to_owners(doc_keys64: torch.Tensor, word_ids: torch.Tensor, weights: t
     wi = recv[:, 1].contiguous()
     wt = recv[:, 2].contiguous() if weights is not None else torch.ones_like(wi)
     udoc, inv = encode_docs(dk)
-    return udoc, inv, wi, wt, Route(order, counts.tolist(), rc)
+    return udoc, inv, wi, wt, Route(order, counts.tolist(), rc, plan)
 
 
 def return_to_origin(x: torch.Tensor, route: Route, comm: Comm) -> torch.Tensor:
@@ -239,6 +320,86 @@ def return_to_origin(x: torch.Tensor, route: Route, comm: Comm) -> torch.Tensor:
     out = torch.empty_like(back)
     out[route.order.to(back.device).long()] = back
     return out
+
+
+def split_corpus_tokens(plan: SplitPlan, udoc: torch.Tensor, inv: torch.Tensor, wi: torch.Tensor, wt: torch.Tensor,
+                        V: int, comm: Comm):
+    """Corpus token list of this rank with the split documents replaced by the pieces it was
+    assigned: (doc id int32, word id int32, weight int32, doc keys int64 [D_own + pieces], meta).
+
+    Each split document's primary contributes the document's (word, Σ weight) pairs (one
+    all-gather of ≤ V pairs per split document); every rank then expands the canonical order of
+    the documents it holds pieces of (pairs by word id, as :mod:`oni355.models.corpus` orders a
+    document) and clips it to each piece's [p0, p1): piece pairs enter the corpus as weighted
+    tokens of new rows D_own, D_own + 1, ... The primary's own row keeps the document's θ and
+    samples nothing."""
+    dev = inv.device
+    i64 = torch.int64
+    D_own = int(udoc.numel())
+    skeys = plan.keys.to(dev)
+    n = plan.n
+    row_j = torch.full((max(D_own, 1),), -1, dtype=i64, device=dev)
+    if D_own:
+        pos = torch.searchsorted(udoc, skeys).clamp_(max=D_own - 1)
+        hit = udoc[pos] == skeys
+        row_j[pos[hit]] = torch.arange(n, device=dev)[hit]
+    prim = torch.nonzero(row_j[:D_own] >= 0).flatten()
+    tokj = row_j[inv.long()] if inv.numel() else torch.zeros(0, dtype=i64, device=dev)
+    m = tokj >= 0
+    key = tokj[m] * V + wi[m].to(i64)
+    u, ui = torch.unique(key, return_inverse=True)
+    cnt = torch.zeros(u.numel(), dtype=i64, device=dev).index_add_(0, ui, wt[m].to(i64))
+    rows = torch.stack([u // V, u % V, cnt], 1).contiguous()
+    allp = torch.cat([p.to(dev) for p in comm.allgather_var(rows)]) if comm.world > 1 else rows
+    allp = allp[torch.argsort(allp[:, 0] * V + allp[:, 1])]
+    mine = np.nonzero(plan.piece_owner == comm.rank)[0]
+    pd, pw, pc = [], [], []
+    for t, k in enumerate(mine.tolist()):
+        pj = allp[allp[:, 0] == int(plan.piece_doc[k])]
+        e = torch.cumsum(pj[:, 2], 0)
+        ov = torch.clamp(torch.minimum(e, torch.tensor(int(plan.piece_p1[k]), device=dev))
+                         - torch.maximum(e - pj[:, 2], torch.tensor(int(plan.piece_p0[k]), device=dev)), min=0)
+        keep = ov > 0
+        pw.append(pj[keep, 1])
+        pc.append(ov[keep])
+        pd.append(torch.full((int(keep.sum()),), D_own + t, dtype=i64, device=dev))
+    keep_tok = ~m
+    z = torch.zeros(0, dtype=i64, device=dev)
+    tdoc = torch.cat([inv[keep_tok].to(i64), *pd, z]).to(torch.int32).contiguous()
+    tword = torch.cat([wi[keep_tok].to(i64), *pw, z]).to(torch.int32).contiguous()
+    twt = torch.cat([wt[keep_tok].to(i64), *pc, z]).to(torch.int32).contiguous()
+    pj_idx = torch.from_numpy(plan.piece_doc[mine]).to(dev)
+    dkeys = torch.cat([udoc, skeys[pj_idx]]) if mine.size else udoc
+    piece_tokens = int(sum(int(x.sum()) for x in pc))
+    meta = dict(D_own=D_own, n_split=n, piece_rows=torch.arange(D_own, D_own + mine.size, device=dev),
+                piece_j=pj_idx, piece_p0=torch.from_numpy(plan.piece_p0[mine]).to(dev), prim_rows=prim,
+                prim_j=row_j[prim], piece_tokens=piece_tokens,
+                prim_tokens=int(plan.count[row_j[prim].cpu().numpy()].sum()) if prim.numel() else 0,
+                max_count=int(plan.count.max()) if n else 0)
+    return tdoc, tword, twt, dkeys, meta
+
+
+def apply_split(corpus: Corpus, meta: dict) -> None:
+    """Attach the split metadata to a corpus built from :func:`split_corpus_tokens`: piece rows
+    sample like chunks of a long document (sweep-start row snapshot + atomic Δ into a seeded
+    copy), and their chunks draw from the document's GLOBAL canonical positions (Philox counter)."""
+    dev = corpus.chunk_doc.device
+    D = corpus.D
+    pos0 = torch.zeros(max(D, 1), dtype=torch.int64, device=dev)
+    is_piece = torch.zeros(max(D, 1), dtype=torch.bool, device=dev)
+    pr = meta["piece_rows"]
+    pos0[pr] = meta["piece_p0"]
+    is_piece[pr] = True
+    cd = corpus.chunk_doc.to(torch.int64)
+    live = cd >= 0
+    cdl = cd.clamp(min=0)
+    corpus.chunk_multi = (corpus.chunk_multi.bool() | (live & is_piece[cdl])).to(torch.uint8)
+    corpus.chunk_rng0 = torch.where(live, corpus.chunk_pos0.to(torch.int64) + pos0[cdl],
+                                    corpus.chunk_pos0.to(torch.int64)).to(torch.int32).contiguous()
+    corpus.long_rows = torch.unique(torch.cat([corpus.long_rows.to(torch.int64), pr])).to(torch.int32)
+    meta["doc_pos0"] = pos0[:D]
+    meta["own_tokens"] = corpus.T - meta["piece_tokens"] + meta["prim_tokens"]
+    corpus.split = meta
 
 
 @dataclass
@@ -282,13 +443,16 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
         if word_ids is None:
             word_ids = torch.searchsorted(vocab, word_keys64).to(torch.int32)
         use_w = weights is not None
-        udoc, inv, wi, wt, route = route_to_owners(doc_keys64, word_ids, weights, comm)
         G, _ = ops.choose_tiling(K)
         if chunk_len <= 0:
-            T_glob = float(wt.sum()) if wt.numel() else 0.0
+            # the global (weighted) token count picks L -- before routing: the placement cuts
+            # heavy documents at multiples of L
+            T_glob = float(weights.sum()) if use_w else float(doc_keys64.numel())
             if dist_on:
                 T_glob = comm.allreduce_scalar(T_glob, "sum")
             chunk_len = auto_chunk_len(int(T_glob), G)
+        udoc, inv, wi, wt, route = route_to_owners(doc_keys64, word_ids, weights, comm,
+                                                   split_L=chunk_len if dist_on else 0)
         D, V = int(udoc.numel()), int(vocab.numel())
         pairs = None
         if dev.type == "cuda":
@@ -298,8 +462,17 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
                                   n0=0 if dist_on else int(n_event0))
         elif dist_on:
             pairs = torch_pairs(inv, wi, V)
-        corpus = build_corpus(inv, wi, D, V, i64_to_u32bits(udoc), G, chunk_len,
-                              weight=wt if use_w else None, pairs=pairs if dev.type == "cuda" else None)
+        plan = route.split if route is not None else None
+        if plan is not None:
+            # heavy documents cut across ranks: the corpus holds this rank's pieces (pairs clipped
+            # to their canonical ranges) instead of the tokens the primary received for scoring
+            tdoc, tword, twt, dkeys, meta = split_corpus_tokens(plan, udoc, inv, wi, wt, V, comm)
+            corpus = build_corpus(tdoc, tword, int(dkeys.numel()), V, i64_to_u32bits(dkeys), G, chunk_len,
+                                  weight=twt)
+            apply_split(corpus, meta)
+        else:
+            corpus = build_corpus(inv, wi, D, V, i64_to_u32bits(udoc), G, chunk_len,
+                                  weight=wt if use_w else None, pairs=pairs if dev.type == "cuda" else None)
     with timer.stage("init"):
         model = GibbsLDA(corpus, GibbsConfig(K=K, alpha=alpha, beta=beta, seed=seed), comm=comm,
                          V_global=int(vocab.numel()))
@@ -382,7 +555,7 @@ def owner_event_scores(ts: torch.Tensor, n: int, n_sides: int, tol: float, hist:
 @traced("oni:gather_theta")
 def gather_theta(run: LdaRun, comm: Comm | None) -> tuple[torch.Tensor, torch.Tensor]:
     """Global (sorted doc keys, θ rows) on every rank (collective X05; local when world == 1)."""
-    th = run.model.theta()
+    th = run.model.theta()[: run.corpus.D_own]
     keys = run.doc_keys64
     if comm is None or not comm.dist:
         return keys, th
@@ -633,9 +806,12 @@ def run_single_doc_events(doc_keys64: torch.Tensor, word_keys64: torch.Tensor, K
     with timer.stage("vocab"):
         dk, wk, wts = doc_keys64, word_keys64, None
         if feedback is not None:
-            wts = torch.cat([torch.ones_like(wk), feedback[2]]).to(torch.int32)
-            dk = torch.cat([dk, feedback[0]])
-            wk = torch.cat([wk, feedback[1]])
+            # same feedback file on every rank: all carry weights, rank 0 adds the tokens
+            wts = torch.ones_like(wk, dtype=torch.int32)
+            if feedback_here(comm):
+                wts = torch.cat([wts, feedback[2].to(torch.int32)])
+                dk = torch.cat([dk, feedback[0]])
+                wk = torch.cat([wk, feedback[1]])
         vocab, wids = encode_words(wk.contiguous(), comm, key_bits)
     n = int(doc_keys64.numel())
     run = build_and_train(dk, None, wts, vocab, K, alpha, beta, seed, sweeps, chunk_len, comm, eval_every=eval_every, burnin=burnin,

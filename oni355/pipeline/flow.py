@@ -181,9 +181,13 @@ def run_flow(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxre
         weights = None
         fb = feedback_tokens(feedback, cuts, device, dupfactor)
         if fb is not None:
-            weights = torch.cat([torch.ones_like(word_keys), fb[2]]).to(torch.int32)
-            doc_keys = torch.cat([doc_keys, fb[0]])
-            word_keys = torch.cat([word_keys, fb[1]])
+            # every rank reads the same feedback file: all of them carry token weights (the
+            # routing exchanges the same columns everywhere), only rank 0 adds the tokens
+            weights = torch.ones_like(word_keys, dtype=torch.int32)
+            if common.feedback_here(comm):
+                weights = torch.cat([weights, fb[2].to(torch.int32)])
+                doc_keys = torch.cat([doc_keys, fb[0]])
+                word_keys = torch.cat([word_keys, fb[1]])
         # flow words are 29-bit keys (spec.flow_word_str layout)
         vocab, wids = common.encode_words(word_keys, comm, key_bits=32)
     run = common.build_and_train(doc_keys, None, weights, vocab, K, alpha, beta, seed, sweeps, chunk_len, comm,

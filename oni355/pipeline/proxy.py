@@ -119,8 +119,12 @@ def _hour_table(dev) -> torch.Tensor:
 
 
 @traced("oni:proxy.featurize")
-def featurize(cols: dict, device, comm: Comm | None, topset, allreduce_counts: bool = True, d: dict | None = None):
-    """``d``: :func:`host_arrays` already on the device (else uploaded here)."""
+def featurize(cols: dict, device, comm: Comm | None, topset, allreduce_counts: bool = True, d: dict | None = None,
+              day: tuple | None = None):
+    """(words, cuts, UA table). ``d``: :func:`host_arrays` already on the device (else uploaded
+    here). ``day`` = (cuts, UA table) of the day being scored: analyst feedback rows are worded
+    with the day's cuts and the day's user-agent frequencies (a UA absent from the day counts 0),
+    as the reference re-words feedback with the current model."""
     dev = torch.device(device)
     n = len(cols["clientip"])
     if d is None:
@@ -146,35 +150,61 @@ def featurize(cols: dict, device, comm: Comm | None, topset, allreduce_counts: b
     else:
         t = torch.zeros(0, dtype=torch.float32, device=dev)
     tkey = ops.f32_keys(t.contiguous())
-    # user-agent frequency over the day (global across ranks)
+    # K07: user-agent frequency over the day (global across ranks)
     uo, uc = strcol("useragent")
     uh, _, _ = sops.string_features(uo, uc)
-    uq, inv = torch.unique(uh, return_inverse=True)
-    cnt = torch.bincount(inv, minlength=uq.numel())
-    if comm is not None and comm.dist:
-        keys = torch.cat(comm.allgather_var(uq))
-        cnts = torch.cat(comm.allgather_var(cnt))
-        gk, ginv = torch.unique(keys, return_inverse=True)
-        gc = torch.zeros(gk.numel(), dtype=torch.int64, device=gk.device).index_add_(0, ginv, cnts.to(torch.int64))
-        cnt = gc[torch.searchsorted(gk, uq.to(gk.device))].to(dev)
-    ua_freq = cnt[inv].clamp(max=2**31 - 1).to(torch.int32).contiguous()
+    if day is not None:
+        tk, tc = day[1]
+        pos = torch.searchsorted(tk, uh).clamp_(max=max(tk.numel() - 1, 0))
+        hit = tk[pos] == uh if tk.numel() else torch.zeros_like(uh, dtype=torch.bool)
+        ua_freq = torch.where(hit, tc[pos] if tk.numel() else torch.zeros_like(uh), 0).clamp(max=2**31 - 1)
+        ua_freq = ua_freq.to(torch.int32).contiguous()
+        table = day[1]
+    else:
+        uq, inv, cnt = ua_histogram(uh)
+        if comm is not None and comm.dist:
+            keys = torch.cat(comm.allgather_var(uq))
+            cnts = torch.cat(comm.allgather_var(cnt))
+            gk, ginv = torch.unique(keys, return_inverse=True)
+            gc = torch.zeros(gk.numel(), dtype=torch.int64, device=gk.device).index_add_(0, ginv, cnts.to(torch.int64))
+            cnt = gc[torch.searchsorted(gk, uq.to(gk.device))].to(dev)
+        ua_freq = cnt[inv.long()].clamp(max=2**31 - 1).to(torch.int32).contiguous()
+        table = None
     fo, fc = strcol("fulluri")
     _, ulen, uent = sops.string_features(fo, fc)
     keys = {"time": tkey, "ua_freq": ua_freq, "uri_ent": ops.f32_keys(uent), "uri_len": ulen}
-    ar, n_glob = None, n
-    if comm is not None and comm.dist:
-        ar = comm.allreduce_np
-        n_glob = int(comm.allreduce_np(np.array([n], np.int64))[0])
-    cuts = dict(zip([name for name, _, _ in BINNED],
-                    ops.quantile_cuts_multi([keys[name].contiguous() for name, _, _ in BINNED],
-                                            [fr for _, fr, _ in BINNED], ar, n_glob)))
+    if day is not None:
+        cuts = day[0]
+    else:
+        ar, n_glob = None, n
+        if comm is not None and comm.dist:
+            ar = comm.allreduce_np
+            n_glob = int(comm.allreduce_np(np.array([n], np.int64))[0])
+        cuts = dict(zip([name for name, _, _ in BINNED],
+                        ops.quantile_cuts_multi([keys[name].contiguous() for name, _, _ in BINNED],
+                                                [fr for _, fr, _ in BINNED], ar, n_glob)))
     raws = {"method": _codes_by_hash(cols["reqmethod"], *strcol("reqmethod"), method_code),
             "ctype": _codes_by_hash(cols["resconttype"], *strcol("resconttype"), ctype_class),
             "respcode": d["respcode"]}
     words = sops.pack_words([keys[nm] for nm, _, _ in BINNED], [cuts[nm] for nm, _, _ in BINNED],
                             [s for _, _, s in BINNED], [raws[nm] for nm, _, _ in RAW], [m for _, m, _ in RAW],
                             [s for _, _, s in RAW], raw8=top, r8mask=3, r8shift=TOP_SHIFT)
-    return words, cuts
+    if table is None:
+        # the day's UA frequency table (signed-sorted keys, counts), for wording feedback rows
+        ks, o = torch.sort(uq.to(dev) if comm is None or not comm.dist else uq)
+        table = (ks, cnt[o].to(torch.int64))
+    return words, cuts, table
+
+
+def ua_histogram(uh: torch.Tensor):
+    """K07: (distinct user-agent hashes, id of every row, count of every distinct hash). On the
+    GPU one native radix pass (ops.corpus.dict_encode with run counts), no torch unique/bincount."""
+    if uh.is_cuda:
+        from ..ops import corpus as oc
+        uq, inv, cnt = oc.dict_encode(uh.contiguous(), 64, counts=True)
+        return uq, inv, cnt
+    uq, inv, cnt = torch.unique(uh, return_inverse=True, return_counts=True)
+    return uq, inv.to(torch.int32), cnt.to(torch.int64)
 
 
 @traced("oni:proxy.run")
@@ -192,11 +222,11 @@ def run_proxy(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxr
             {k: staging.upload(a, device) for k, a in host_arrays(cols).items()}
     with timer.stage("featurize"):
         topset = top_set(top_domains)
-        words, cuts = featurize(cols, device, comm, topset, d=d)
+        words, cuts, ua_table = featurize(cols, device, comm, topset, d=d)
         docs = common.u32_to_i64(d["clientip"])
     fb = None
     if feedback and len(feedback.get("clientip", [])):
-        fw, _ = featurize(feedback, device, None, topset)
+        fw, _, _ = featurize(feedback, device, None, topset, day=(cuts, ua_table))
         fdoc = torch.from_numpy(np.asarray(feedback["clientip"], np.uint32).astype(np.int64)).to(words.device)
         fb = (fdoc, fw, torch.full_like(fw, int(dupfactor)))
     res = common.run_single_doc_events(docs, words, K, sweeps, tol, maxresults, alpha, beta, seed, chunk_len, comm,

@@ -57,7 +57,7 @@ def build_source(source: str, per_rank: int, K: int, comm: Comm, seed: int = 7, 
         from ..synth.dns import top_domain_list
         from ..synth.proxy import generate_proxy
         day = generate_proxy(per_rank, seed=seed, rank=rank, n_clients=max(32, n_total // 40))
-        words, _ = src.featurize(day.cols, dev, comm, top_set(top_domain_list()))
+        words, _, _ = src.featurize(day.cols, dev, comm, top_set(top_domain_list()))
         from ..io import staging
         doc = staging.upload(np.asarray(day.cols["clientip"], np.uint32).astype(np.int64), dev)
         sides = [(doc, words.to(torch.int64))]

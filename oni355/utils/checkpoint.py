@@ -56,6 +56,9 @@ class Checkpointer:
             "sweep": int(model.sweeps_done),
             "doc_keys": c.doc_keys.cpu(),
             "doc_tok_ptr": c.doc_tok_ptr.cpu(),
+            # canonical position of each row's first token: non-zero only for pieces of documents
+            # cut across ranks (pipeline.common.SplitPlan)
+            "doc_pos0": _pos0(c).cpu(),
             "z": z,
             "likelihoods": list(model.likelihoods),
         }
@@ -84,6 +87,12 @@ class Checkpointer:
             for p in glob.glob(os.path.join(self.dir, f"ckpt_s{s}_r*")):
                 os.remove(p)
 
+    @staticmethod
+    def _split_keys(keys: torch.Tensor, pos0: torch.Tensor) -> torch.Tensor:
+        """Keys that are not one whole document in one row: pieces (pos0 > 0) or repeated keys."""
+        u, cnt = torch.unique(keys, return_counts=True)
+        return torch.unique(torch.cat([keys[pos0 > 0], u[cnt > 1]]))
+
     def restore(self, model) -> int:
         man = self.manifest()
         if man is None:
@@ -96,8 +105,13 @@ class Checkpointer:
         my_keys = c.doc_keys.cpu().to(torch.int64) & mask
         my_ptr = c.doc_tok_ptr.cpu().to(torch.int64)
         my_len = my_ptr[1:] - my_ptr[:-1]
+        my_pos0 = _pos0(c).cpu()
         z = torch.zeros(int(my_ptr[-1]) if my_ptr.numel() else 0, dtype=torch.uint8)
         found = torch.zeros(my_keys.numel(), dtype=torch.bool)
+        # documents cut into pieces (here or in the checkpoint's run): whole-document z is
+        # assembled from every shard's pieces, then sliced to this rank's ranges
+        my_split = torch.unique(torch.cat([self._split_keys(my_keys, my_pos0), my_keys[my_len == 0]]))
+        pieces: dict = {}
         # vectorised: every shard's documents are matched to this rank's by key (searchsorted) and
         # their token ranges copied with one index gather; shards holding none of them are skipped
         for p in sorted(glob.glob(os.path.join(self.dir, f"ckpt_s{sweep}_r*of{man['world']}.pt"))):
@@ -108,6 +122,21 @@ class Checkpointer:
             if keys.numel() == 0 or my_keys.numel() == 0:
                 continue
             ptr = d["doc_tok_ptr"].to(torch.int64)
+            pos0 = d.get("doc_pos0", torch.zeros(keys.numel(), dtype=torch.int64)).to(torch.int64)
+            sk_split = torch.unique(torch.cat([self._split_keys(keys, pos0), my_split]))
+            if sk_split.numel():
+                isp = torch.isin(keys, sk_split)
+                for r in torch.nonzero(isp).flatten().tolist():
+                    ln = int(ptr[r + 1] - ptr[r])
+                    if ln:
+                        pieces.setdefault(int(keys[r]), []).append((int(pos0[r]), d["z"][int(ptr[r]):int(ptr[r]) + ln]))
+                keep = ~isp
+                keys, ptr_lo, ptr_hi = keys[keep], ptr[:-1][keep], ptr[1:][keep]
+                if keys.numel() == 0:
+                    continue
+                ptr = None
+            else:
+                ptr_lo, ptr_hi = ptr[:-1], ptr[1:]
             order = torch.argsort(keys)
             sk = keys[order]
             pos = torch.searchsorted(sk, my_keys).clamp_(max=sk.numel() - 1)
@@ -116,17 +145,42 @@ class Checkpointer:
                 continue
             dst = torch.nonzero(hit).flatten()
             src = order[pos[dst]]
-            lens = ptr[src + 1] - ptr[src]
+            lens = ptr_hi[src] - ptr_lo[src]
             if not torch.equal(lens, my_len[dst]):
                 bad = dst[torch.nonzero(lens != my_len[dst]).flatten()[0]]
                 raise ValueError(f"checkpoint does not match corpus (doc key {int(my_keys[bad])})")
             n = int(lens.sum())
             rep = torch.repeat_interleave(torch.arange(dst.numel()), lens)
             within = torch.arange(n) - torch.repeat_interleave(torch.cumsum(lens, 0) - lens, lens)
-            z[my_ptr[dst][rep] + within] = d["z"][ptr[src][rep] + within]
+            z[my_ptr[dst][rep] + within] = d["z"][ptr_lo[src][rep] + within]
             found[dst] = True
+        for r in torch.nonzero(~found).flatten().tolist():
+            ln = int(my_len[r])
+            k = int(my_keys[r])
+            if ln == 0:  # a split document's primary row: θ only, no tokens here
+                found[r] = True
+                continue
+            if k not in pieces:
+                continue
+            full_len = max(p + int(v.numel()) for p, v in pieces[k])
+            whole = torch.zeros(full_len, dtype=torch.uint8)
+            cov = torch.zeros(full_len, dtype=torch.bool)
+            for p, v in pieces[k]:
+                whole[p:p + v.numel()] = v
+                cov[p:p + v.numel()] = True
+            p0 = int(my_pos0[r])
+            if p0 + ln <= full_len and bool(cov[p0:p0 + ln].all()):
+                z[int(my_ptr[r]):int(my_ptr[r]) + ln] = whole[p0:p0 + ln]
+                found[r] = True
         if not bool(found.all()):
             miss = int(my_keys[torch.nonzero(~found).flatten()[0]])
             raise ValueError(f"checkpoint does not match corpus (doc key {miss} missing)")
         model.load_canonical_z(z, sweep)
         return sweep
+
+
+def _pos0(c) -> torch.Tensor:
+    """Canonical position of each corpus row's first token (0 unless the row is a piece)."""
+    if c.split is not None and "doc_pos0" in c.split:
+        return c.split["doc_pos0"].to(torch.int64)
+    return torch.zeros(c.D, dtype=torch.int64)

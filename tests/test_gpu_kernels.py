@@ -88,7 +88,11 @@ def _toy_tokens(n_docs, V, seed, heavy=True):
                                     (20, "atomic+q2"), (7, "wdelta+q2"), (32, "wdelta+q2"),
                                     (200, "atomic+ldsq"), (50, "dual+plain"), (100, "wdelta+plain"),
                                     (100, "atomic+plain"), (64, "delta+pp"), (20, "wdelta+lds"), (7, "wdelta+lds"),
-                                    (32, "wdelta+lds"), (20, "recount+lds")])
+                                    (32, "wdelta+lds"), (20, "recount+lds"),
+                                    (20, "wdelta+dz"), (20, "recount+dz"), (20, "atomic+dz"), (20, "dual+dz"),
+                                    (20, "delta+dz"), (7, "wdelta+dz"), (32, "wdelta+dz"), (32, "recount+dz"),
+                                    (50, "wdelta+dz"), (20, "wdelta+q2dz"), (20, "recount+q2dz"), (20, "atomic+q2dz"),
+                                    (20, "dual+q2dz"), (7, "wdelta+q2dz")])
 def test_gibbs_bitwise_vs_oracle(gpu, K, mode):
     tdoc, tword, keys = _toy_tokens(300, 400, K)
     G, KP = ops.choose_tiling(K)
@@ -141,6 +145,27 @@ def test_graph_replay_matches_eager(gpu, mode, switch):
     if mode == "auto" and switch == 0:
         assert b._delta_on and a._delta_on
     assert torch.equal(a.tok_z, b.tok_z) and torch.equal(a.nwk, b.nwk) and torch.equal(a.ndk_cur, b.ndk_cur)
+
+
+@pytest.mark.parametrize("L", [32, 128, 256])
+def test_dz_sampler_graph_auto_matches_qpf(gpu, L):
+    """The LDS-staged-topic sampler (deferred bookkeeping) replays the default register sampler
+    bit for bit through the auto count mode's recount → wdelta switch, captured in graphs; at
+    L = 256 (> kDzMaxLen) it falls back to the register sampler."""
+    tdoc, tword, keys = _toy_tokens(3000, 700, 21)
+    c = build_corpus(tdoc.to(gpu), tword.to(gpu), 3000, 700, torch.from_numpy(keys).to(gpu), 1, L=L)
+    runs = []
+    for sampler in ("qpf", "dz", "q2dz"):
+        m = GibbsLDA(c, GibbsConfig(K=20, seed=77, count_mode="auto", auto_switch=5, sampler=sampler))
+        assert (m.qpf in (7, 8)) == (sampler != "qpf" and L <= 128)
+        m.initialize()
+        m.sweep(12)
+        runs.append(m)
+    a = runs[0]
+    for b in runs[1:]:
+        assert a._sweep_mode(a.sweeps_done) == 4 == b._sweep_mode(b.sweeps_done)
+        assert torch.equal(a.tok_z, b.tok_z) and torch.equal(a.nwk, b.nwk) and torch.equal(a.ndk_cur, b.ndk_cur)
+        assert torch.equal(a.q, b.q)
 
 
 def test_resume_bitwise(gpu):

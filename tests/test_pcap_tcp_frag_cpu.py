@@ -90,3 +90,42 @@ def test_frame_time_is_formatted_only_for_rendered_rows(tmp_path):
     want = frame_times(ft.ts_ns[rows]).to_list()
     import csv
     assert [row[0] for row in csv.reader(ln.decode() for ln in r.lines())] == want
+
+
+def _write_ts(path, frames_ts):
+    with open(path, "wb") as f:
+        f.write(struct.pack("<IHHiIII", 0xa1b2c3d4, 2, 4, 0, 0, 65535, 1))
+        for ts, fr in frames_ts:
+            f.write(struct.pack("<IIII", ts, 0, len(fr), len(fr)))
+            f.write(fr)
+
+
+def test_fragments_reusing_an_ip_id_are_separate_datagrams(tmp_path):
+    """The 16-bit IP id wraps in a day-long capture: two fragmented responses between the same
+    hosts with the same id are two datagrams (the repeated offset opens the second), and pieces
+    more than 30 s of frame time apart never join one datagram."""
+    srv, cli = "10.0.0.53", "10.1.2.3"
+    a = _udp(53, 5000, _dns_response(11, "first.example.com", answers=["1.1.1.1"], pad=600))
+    b = _udp(53, 5001, _dns_response(12, "second.example.com", answers=["2.2.2.2"], pad=600))
+    t0 = 1467936000
+    frames = [
+        (t0, _eth(_ipv4(srv, cli, 17, a[:400], ident=5, frag_off=0, more=True))),
+        (t0 + 1, _eth(_ipv4(srv, cli, 17, a[400:], ident=5, frag_off=400))),
+        (t0 + 2, _eth(_ipv4(srv, cli, 17, b[:400], ident=5, frag_off=0, more=True))),
+        (t0 + 3, _eth(_ipv4(srv, cli, 17, b[400:], ident=5, frag_off=400))),
+        # id 6: head, then its tail 40 s later -> two incomplete groups, no row
+        (t0 + 4, _eth(_ipv4(srv, cli, 17, a[:400], ident=6, frag_off=0, more=True))),
+        (t0 + 44, _eth(_ipv4(srv, cli, 17, a[400:], ident=6, frag_off=400))),
+        # id 7: a head whose datagram never completes, then a full datagram with the same id
+        (t0 + 45, _eth(_ipv4(srv, cli, 17, b[:400], ident=7, frag_off=0, more=True))),
+        (t0 + 46, _eth(_ipv4(srv, cli, 17, a[:400], ident=7, frag_off=0, more=True))),
+        (t0 + 47, _eth(_ipv4(srv, cli, 17, a[400:], ident=7, frag_off=400))),
+    ]
+    p = str(tmp_path / "wrap.pcap")
+    _write_ts(p, frames)
+    for threads in (1, 4):
+        c = read_pcap_dns(p, threads=threads)
+        assert c["dns_qry_name"].to_list() == ["first.example.com", "second.example.com", "first.example.com"]
+        assert c["dns_a"].to_list() == ["1.1.1.1", "2.2.2.2", "1.1.1.1"]
+        assert c["unix_tstamp"].tolist() == [t0 + 1, t0 + 3, t0 + 47]
+        assert c["_frag_incomplete"] == 3
