@@ -293,29 +293,30 @@ class ResultPipe:
         self._pool = ThreadPoolExecutor(1, thread_name_prefix="oni-results")
         self._pending = None  # (future of (gids, Rendered), all result rows)
 
-    def submit(self, cols: dict, res, row_off: int) -> None:
+    def submit(self, cols: dict, res, row_off: int, tag=None) -> None:
         """Queue this day's formatting; finishes the previous day first. ``ONI_RESULT_PIPE=0``
-        formats and writes inline (no worker thread)."""
+        formats and writes inline (no worker thread). ``tag`` (e.g. the day) is passed on to
+        ``write(rendered, tag)``."""
         self._finish()
         if os.environ.get("ONI_RESULT_PIPE", "1") == "0":
             from concurrent.futures import Future
             fut = Future()
             fut.set_result(render_local(self.source, cols, res, row_off))
-            self._pending = (fut, res.rows)
+            self._pending = (fut, res.rows, tag)
             self._finish()
             return
         fut = self._pool.submit(render_local, self.source, cols, res, row_off)
-        self._pending = (fut, res.rows)
+        self._pending = (fut, res.rows, tag)
 
     def _finish(self):
         if self._pending is None:
             return None
-        fut, rows = self._pending
+        fut, rows, tag = self._pending
         self._pending = None
         gids, rendered = fut.result()
         full = gather_rendered(rows, gids, rendered, self.comm)
         if self.write is not None:
-            self.write(full)
+            self.write(full) if tag is None else self.write(full, tag)
         return full
 
     def drain(self):

@@ -152,6 +152,19 @@ class Comm:
                                input_split_sizes=sc, group=self.group)
         return (out, rc) if return_recv_counts else out
 
+    def host_side(self) -> "Comm":
+        """A CPU communicator on a process group of its own (gloo), for host-side collectives
+        issued from a worker thread (the multi-day loader's IPv6 dictionary exchange) while the
+        main thread drives the device collectives: two groups, so the two threads' collectives
+        never interleave on one channel. Collective call: every rank creates it in the same order."""
+        if getattr(self, "_host_side", None) is None:
+            if not self.dist:
+                self._host_side = Comm(self.rank, self.world, torch.device("cpu"), backend="gloo")
+            else:
+                g = dist.new_group(backend="gloo")
+                self._host_side = Comm(self.rank, self.world, torch.device("cpu"), g, forced=True, backend="gloo")
+        return self._host_side
+
     def _host_view(self) -> "Comm":
         return Comm(self.rank, self.world, torch.device("cpu"), self.group, forced=self.dist, backend="gloo")
 

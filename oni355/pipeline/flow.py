@@ -34,6 +34,11 @@ DEVICE_COLS = {"trhour": torch.int32, "trminute": torch.int32, "trsec": torch.in
 # reserved, never-routed IPv4 block, so the keys cannot collide with a real IPv4 document.
 V6_KEY_BASE = 0xF0000000
 V6_KEY_MAX = 1 << 28
+V6_KEYED = "_v6_keyed"  # marker left in columns that went through with_ipv6_keys
+
+
+def _needs_v6_keys(c: dict | None) -> bool:
+    return bool(c) and any(k in c for k in ("sip6", "dip6")) and not c.get(V6_KEYED, False)
 
 
 def _fixed(col, w: int = 48) -> np.ndarray:
@@ -48,21 +53,42 @@ def _fixed(col, w: int = 48) -> np.ndarray:
     return m.view(f"S{w}").reshape(-1)
 
 
+def ip4(x: int) -> str:
+    return "%d.%d.%d.%d" % (x >> 24, (x >> 16) & 255, (x >> 8) & 255, x & 255)
+
+
 def with_ipv6_keys(cols: dict, comm: Comm | None = None, others: tuple = ()) -> dict:
     """Columns with ``sip``/``dip`` of IPv6 rows replaced by their day-dictionary keys
     (:data:`V6_KEY_BASE` + rank); ``others`` (e.g. analyst feedback rows) share the dictionary and
-    are returned keyed too. No IPv6 columns anywhere: the inputs come back unchanged."""
+    are returned keyed too. On such a day, IPv4 addresses inside 240.0.0.0/4 (bogons) go through
+    the dictionary as well, so no IPv4 document can share a key with an IPv6 one; their dotted
+    text lands in ``sip6``/``dip6`` for rendering. No IPv6 columns anywhere: the inputs come back
+    unchanged."""
     sets = [c for c in (cols, *others) if c]
     have = any(k in c for c in sets for k in ("sip6", "dip6"))
     if comm is not None and comm.dist:
         have = comm.allreduce_scalar(1.0 if have else 0.0, "max") > 0
     if not have:
         return cols if not others else (cols, *others)
+
+    def text(c: dict, k4: str, k6: str):
+        """Fixed-width dictionary text of the rows keyed through the dictionary: IPv6 rows, and
+        IPv4 rows inside 240.0.0.0/4 (class-E bogons would otherwise share the IPv6 key space)."""
+        v4 = np.asarray(c[k4]).astype(np.uint32) if k4 in c else None
+        f = _fixed(c[k6]) if k6 in c else (np.zeros(v4.size, "S48") if v4 is not None else None)
+        if v4 is not None:
+            ce = (f == b"") & (v4 >= np.uint32(V6_KEY_BASE))
+            if ce.any():
+                f = f.copy()
+                f[ce] = np.array([("v4:%d.%d.%d.%d" % (x >> 24, (x >> 16) & 255, (x >> 8) & 255, x & 255)).encode()
+                                  for x in v4[ce].tolist()], "S48")
+        return f
+
     parts = []
     for c in sets:
-        for k in ("sip6", "dip6"):
-            if k in c:
-                f = _fixed(c[k])
+        for k4, k6 in (("sip", "sip6"), ("dip", "dip6")):
+            if k6 in c or k4 in c:
+                f = text(c, k4, k6)
                 parts.append(f[f != b""])
     uniq = np.unique(np.concatenate(parts)) if parts else np.zeros(0, "S48")
     if comm is not None and comm.dist:
@@ -74,13 +100,25 @@ def with_ipv6_keys(cols: dict, comm: Comm | None = None, others: tuple = ()) -> 
         raise ValueError(f"{uniq.size} distinct IPv6 addresses exceed the 2^28 key space")
 
     def keyed(c: dict) -> dict:
+        from ..store.columnar import StringColumn
         out = dict(c)
+        out[V6_KEYED] = True
         for k4, k6 in (("sip", "sip6"), ("dip", "dip6")):
-            if k6 in c:
-                f = _fixed(c[k6])
-                v6 = f != b""
-                key = (V6_KEY_BASE + np.searchsorted(uniq, f)).astype(np.uint32)
-                out[k4] = np.where(v6, key, np.asarray(c[k4]).astype(np.uint32))
+            if k4 not in c:
+                continue
+            f = text(c, k4, k6)
+            v6 = f != b""
+            key = (V6_KEY_BASE + np.searchsorted(uniq, f)).astype(np.uint32)
+            out[k4] = np.where(v6, key, np.asarray(c[k4]).astype(np.uint32))
+            v4 = np.asarray(c[k4]).astype(np.uint32)
+            no6 = (_fixed(c[k6]) == b"") if k6 in c else np.ones(v4.size, bool)
+            ce = v6 & no6 & (v4 >= np.uint32(V6_KEY_BASE))
+            if k6 not in c:
+                if ce.any():  # class-E rows render their dotted address from the text column
+                    out[k6] = StringColumn.from_list([ip4(x) if m else "" for x, m in zip(v4.tolist(), ce.tolist())])
+            elif ce.any():
+                t = c[k6].to_list()
+                out[k6] = StringColumn.from_list([ip4(x) if m else s6 for s6, x, m in zip(t, v4.tolist(), ce.tolist())])
         return out
 
     res = [keyed(c) if c else c for c in (cols, *others)]
@@ -169,6 +207,12 @@ def run_flow(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxre
     timer = StageTimer(device)
     if device_cols is None:
         cols, feedback = with_ipv6_keys(cols, comm, (feedback,)) if feedback else (with_ipv6_keys(cols, comm), None)
+    elif _needs_v6_keys(cols) or _needs_v6_keys(feedback):
+        # prefetched device columns were uploaded from the host rows as they were: a day with IPv6
+        # rows must be keyed (with its feedback, one shared dictionary) BEFORE pinning, as the
+        # multi-day loader does (pipeline.daily.load_host_day)
+        raise ValueError("run_flow(device_cols=...): IPv6 rows must be keyed with with_ipv6_keys() before the "
+                         "columns are pinned and uploaded (feedback rows too)")
     with timer.stage("h2d"):
         d = dict(device_cols) if device_cols is not None else to_device(cols, device)
     with timer.stage("featurize"):

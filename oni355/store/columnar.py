@@ -148,14 +148,36 @@ def _write_part(d: str, cols: dict) -> int:
 
 
 def write_day(root: str, source: str, date: str, cols: dict) -> str:
-    """Replace the day's table with ``cols`` (idempotent rerun, like ``hdfs dfs -rm`` + load)."""
+    """Replace the day's table with ``cols`` (idempotent rerun, like ``hdfs dfs -rm`` + load);
+    a whole-day write is complete on return (``_SUCCESS``)."""
     d = day_dir(root, source, date)
     if os.path.isdir(d):
         for p in glob.glob(os.path.join(d, "**", "*"), recursive=True):
             if os.path.isfile(p):
                 os.remove(p)
     _write_part(d, cols)
+    mark_complete(root, source, date)
     return d
+
+
+def mark_complete(root: str, source: str, date: str) -> None:
+    """Declare a day's ingest finished (Hadoop's ``_SUCCESS`` marker): ``oni-ml --follow`` only
+    trains days that are complete."""
+    d = day_dir(root, source, date)
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "_SUCCESS"), "w"):
+        pass
+
+
+def days(root: str, source: str, complete_only: bool = True) -> list[str]:
+    """Stored days of a source (YYYYMMDD, ascending); ``complete_only``: only days with a
+    ``_SUCCESS`` marker."""
+    base = os.path.join(root, source)
+    out = []
+    for d in sorted(glob.glob(os.path.join(base, "[0-9]" * 8))):
+        if os.path.isdir(d) and (not complete_only or os.path.exists(os.path.join(d, "_SUCCESS"))):
+            out.append(os.path.basename(d))
+    return out
 
 
 def hour_dir(root: str, source: str, date: str, hour: int) -> str:

@@ -88,7 +88,7 @@ def _wide_names(rng, m: int, domains: list[str]) -> list[str]:
 
 def generate_dns(n: int, seed: int = 5, n_clients: int | None = None, user_domain: str = "intel",
                  alpha_true: float = 0.1, n_anomalies: int | None = None, rank: int = 0,
-                 date_unix: int = 1467936000, wide_vocab: float = 0.0) -> DnsDay:
+                 date_unix: int = 1467936000, wide_vocab: float = 0.0, anomaly_kind: str = "rare") -> DnsDay:
     """``wide_vocab``: fraction of (non-anomalous) rows drawn from the long tail instead of a
     behaviour profile -- any of 18 record types and 6 rcodes, names of every shape under ~2000
     domains, any hour -- which takes the day's vocabulary from ~4k words to ~1e5 (the sizing of
@@ -144,21 +144,36 @@ def generate_dns(n: int, seed: int = 5, n_clients: int | None = None, user_domai
             for j, i in enumerate(idx):
                 names[i] = f"{_SERVICE[sv[j]]}.{doms[dsel[j]]}"
     if wide_vocab > 0:
+        # long-tail rows come from a codebook of ~n/20 query behaviours (name shape, record type,
+        # rcode, hour), drawn uniformly: a wide vocabulary whose words still recur (~10 rows per
+        # behaviour at 2M rows) -- independent per-row draws make every other long-tail row a
+        # day-unique word, which P(word | doc) cannot tell from a planted one
         wide = np.nonzero(rng.random(n) < wide_vocab)[0]
         m = wide.size
+        crng = np.random.default_rng([seed, 0xC0DE])
+        W = max(200, n // 20)
         qz = 1.0 / np.arange(1, len(_WIDE_QTYPES) + 1) ** 1.2
-        qtype[wide] = rng.choice(_WIDE_QTYPES, size=m, p=qz / qz.sum())
+        cb_q = crng.choice(_WIDE_QTYPES, size=W, p=qz / qz.sum())
         rz = np.array([0.8, 0.1, 0.05, 0.03, 0.015, 0.005])
-        rcode[wide] = rng.choice(_WIDE_RCODES, size=m, p=rz / rz.sum())
-        hour_f[wide] = rng.uniform(0, 24, size=m)
-        for i, nm in zip(wide.tolist(), _wide_names(rng, m, top_domain_list())):
-            names[i] = nm
+        cb_r = crng.choice(_WIDE_RCODES, size=W, p=rz / rz.sum())
+        cb_h = crng.uniform(0, 24, size=W)
+        cb_n = _wide_names(crng, W, top_domain_list())
+        b = rng.integers(0, W, m)
+        qtype[wide] = cb_q[b]
+        rcode[wide] = cb_r[b]
+        hour_f[wide] = cb_h[b]
+        for i, j in zip(wide.tolist(), b.tolist()):
+            names[i] = cb_n[j]
     hour = np.mod(np.floor(hour_f), 24).astype(np.int64)
     # planted tunnelling / DGA
     anomaly_rows = np.sort(rng.choice(n, size=min(n_anomalies, n), replace=False))
     if anomaly_rows.size:
         quiet = np.argsort(w)[: max(1, n_clients // 10)]
-        cli[anomaly_rows] = quiet[rng.integers(0, quiet.size, size=anomaly_rows.size)]
+        q_draw = quiet[rng.integers(0, quiet.size, size=anomaly_rows.size)]
+        # "rare": planted on the least active tenth of the clients; "rare-active": on the row's own
+        # (activity-drawn) client
+        if anomaly_kind == "rare":
+            cli[anomaly_rows] = q_draw
         # each anomaly is an individually rare behaviour (tunnel/DGA-like name of varying shape, odd
         # record type, odd hour): a hundred copies of ONE pattern would form a topic of their own
         # and stop being rare for the model at large day sizes

@@ -10,7 +10,9 @@ with random-init topic priors" (BASELINE.json). Generative model:
 * host activity is Zipf-distributed (a few hosts own most flows: NAT gateways, resolvers);
 * each flow: profile z ~ θ*[src], server from the profile's pool, port/hour/bytes/packets from z;
 * ``n_anomalies`` planted flows with off-profile behaviour (rare service port at an odd hour with
-  outsized volume) -- ground truth for "planted anomalies rank in the top-N" tests.
+  outsized volume) on hosts drawn by activity -- ground truth for "planted anomalies rank in the
+  top-N" tests. The rare ports are kept out of the realistic day's long tail, so every planted
+  flow stays an individually rare word there too.
 
 Columns follow the flow schema of SURVEY.md §2.7 (nfdump CSV → Hive ``flow`` table).
 """
@@ -78,7 +80,8 @@ def str_to_ip(s: str) -> int:
 
 def generate_flows(n: int, seed: int = 7, n_hosts: int | None = None, n_profiles: int = 20,
                    alpha_true: float = 0.08, zipf_a: float = 1.15, n_anomalies: int | None = None,
-                   date=(2016, 7, 8), rank: int = 0, wide_vocab: bool = False, ipv6_frac: float = 0.0) -> FlowDay:
+                   date=(2016, 7, 8), rank: int = 0, wide_vocab: bool = False, ipv6_frac: float = 0.0,
+                   anomaly_hosts: str = "active") -> FlowDay:
     """Generate ``n`` flows. ``rank`` offsets the RNG stream (weak-scaling shards of one day).
 
     ``wide_vocab``: a realistic-vocabulary day (SURVEY.md §7.5 sizing, V ≈ 1e5–1e6 flow words):
@@ -126,13 +129,27 @@ def generate_flows(n: int, seed: int = 7, n_hosts: int | None = None, n_profiles
         lbytes[m] = rng.normal(mu, sd, size=cnt)
         bpp[m] = bp * np.exp(rng.normal(0, 0.2, size=cnt))
     if wide_vocab:
-        # long-tail services: Zipf over a random permutation of the well-known port range
-        lt = rng.random(n) < 0.5
-        perm = np.random.default_rng([seed, 0x5EED]).permutation(np.arange(1, 1025))
-        port_of[lt] = perm[np.minimum(rng.zipf(1.2, int(lt.sum())) - 1, 1023)]
-        hour_f += rng.normal(0.0, 4.0, size=n)
-        lbytes += rng.normal(0.0, 2.0, size=n)
-        bpp *= np.exp(rng.normal(0.0, 0.8, size=n))
+        # Half the flows come from a codebook of ~n/100 long-tail service behaviours (a well-known
+        # port of the ~1k-port pool, an hour, a volume and a packet size each), drawn uniformly:
+        # the day's vocabulary grows to V ≈ 4e5 flow words at 12.5M flows (SURVEY.md §7.5 sizing:
+        # the q table leaves L2) while every behaviour recurs ~50 times. A Zipf tail of
+        # independent port / hour / volume draws instead makes tens of thousands of day-unique
+        # normal words, which P(word | doc) ranks by topic-assignment luck, and no planted row can
+        # be told from them (profiles/r3/recall_sweep.jsonl). The anomalies' rare services are
+        # not in the pool.
+        lt = np.nonzero(rng.random(n) < 0.5)[0]
+        crng = np.random.default_rng([seed, 0xC0DE])
+        W = max(1000, n // 100)
+        pool = np.setdiff1d(np.arange(1, 1025), _ANOMALY_PORTS)
+        cb_port = pool[crng.integers(0, pool.size, W)]
+        cb_hour = crng.uniform(0.0, 24.0, W)
+        cb_lbytes = crng.uniform(4.0, 18.0, W)
+        cb_bpp = np.exp(crng.uniform(np.log(40.0), np.log(1500.0), W))
+        b = rng.integers(0, W, lt.size)
+        port_of[lt] = cb_port[b]
+        hour_f[lt] = cb_hour[b]
+        lbytes[lt] = cb_lbytes[b] + rng.normal(0.0, 0.02, lt.size)
+        bpp[lt] = cb_bpp[b]
     srv = rng.integers(0, n_srv, size=n)
     dip = _ip(172, 16, z & 255, srv & 255).astype(np.uint32)
     sip = host_ips[src]
@@ -144,8 +161,9 @@ def generate_flows(n: int, seed: int = 7, n_hosts: int | None = None, n_profiles
     if wide_vocab:
         s2s = rng.random(n) < 0.2  # server-to-server: both low (111111) or both high (333333)
         both_low = s2s & (rng.random(n) < 0.5)
-        sport = np.where(both_low, rng.integers(1, 1025, size=n), np.where(s2s, rng.integers(1025, 65536, size=n), sport))
-        dport = np.where(s2s & ~both_low, rng.integers(1025, 65536, size=n), dport)
+        both_high = s2s & ~both_low
+        sport = np.where(both_low, rng.integers(1, 1025, size=n), np.where(both_high, rng.integers(1025, 65536, size=n), sport))
+        dport = np.where(both_low, rng.integers(1, 1025, size=n), np.where(both_high, rng.integers(1025, 65536, size=n), dport))
     sip2 = np.where(flip, dip, sip)
     dip2 = np.where(flip, sip, dip)
 
@@ -155,12 +173,18 @@ def generate_flows(n: int, seed: int = 7, n_hosts: int | None = None, n_profiles
     ibyt = np.maximum(40, np.exp(lbytes)).astype(np.int64)
     ipkt = np.maximum(1, np.round(ibyt / np.maximum(bpp, 40))).astype(np.int64)
 
-    # planted anomalies: off-profile rare service, odd hour, huge volume, from low-activity hosts
+    # planted anomalies: off-profile rare service, odd hour, huge volume. anomaly_hosts "active"
+    # (default): the compromised hosts are drawn like any flow's source (by activity), so the
+    # anomaly is rare FOR A HOST WHOSE BEHAVIOUR IS KNOWN -- the case P(word | doc) scoring ranks;
+    # "quiet" plants them on the least active tenth of the hosts (round-1/2 generator)
     anomaly_rows = np.sort(rng.choice(n, size=min(n_anomalies, n), replace=False))
     na = anomaly_rows.size
     if na:
-        quiet = np.argsort(w)[: max(1, n_hosts // 10)]
-        a_src = quiet[rng.integers(0, quiet.size, size=na)]
+        if anomaly_hosts == "quiet":
+            quiet = np.argsort(w)[: max(1, n_hosts // 10)]
+            a_src = quiet[rng.integers(0, quiet.size, size=na)]
+        else:
+            a_src = src[anomaly_rows]
         sip2[anomaly_rows] = host_ips[a_src]
         dip2[anomaly_rows] = _ip(203, 0, 113, rng.integers(1, 255, size=na) & 255)
         sport[anomaly_rows] = rng.integers(1025, 65536, size=na)

@@ -85,8 +85,13 @@ def _wide_rows(rng, m: int):
 
 def generate_proxy(n: int, seed: int = 9, n_clients: int | None = None, alpha_true: float = 0.15,
                    n_anomalies: int | None = None, rank: int = 0, date: str = "2016-07-08",
-                   wide_vocab: float = 0.0) -> ProxyDay:
-    """``wide_vocab``: fraction of (non-anomalous) rows drawn from the long tail -- 10 methods, 22
+                   wide_vocab: float = 0.0, anomaly_kind: str = "rare") -> ProxyDay:
+    """``anomaly_kind``: "rare" -- individually rare requests (unique UA, odd method / content
+    type, long high-entropy URI, night hour) from the least active tenth of the clients;
+    "rare-active" -- the same requests from the row's own (activity-drawn) client;
+    "offprofile" -- a request of the client's least likely behaviour profile (common words, rare
+    for that client).
+    ``wide_vocab``: fraction of (non-anomalous) rows drawn from the long tail -- 10 methods, 22
     content types, 20 status codes, ~20k user agents, URIs of every length and alphabet, any hour
     -- instead of a behaviour profile (vocabulary ~4e4 → ~1e5+; SURVEY.md §7.5 sizing)."""
     rng = np.random.default_rng([seed, rank])
@@ -105,6 +110,13 @@ def generate_proxy(n: int, seed: int = 9, n_clients: int | None = None, alpha_tr
     cum[:, -1] = 1
     z = np.clip(np.searchsorted((cum + np.arange(n_clients)[:, None]).ravel(), cli + rng.random(n), side="right")
                 - cli * P, 0, P - 1)
+    # planted rows are chosen first (the long-tail rows below never overwrite them)
+    arng = np.random.default_rng([seed, rank, 0xA11])
+    anomaly_rows = np.sort(arng.choice(n, size=min(n_anomalies, n), replace=False))
+    if anomaly_kind == "offprofile" and anomaly_rows.size:
+        # behaviour its client never shows: the row comes from the client's least likely profile
+        # (globally common words, rare for this client -- the P(word | doc) anomaly)
+        z[anomaly_rows] = np.argmin(theta[cli[anomaly_rows]], axis=1)
     host, method, ua, ctype, path = [""] * n, [""] * n, [""] * n, [""] * n, [""] * n
     hour_f = np.zeros(n)
     for k, (key, meths, mw, uas, peak, hsd) in enumerate(_PROFILES):
@@ -124,19 +136,31 @@ def generate_proxy(n: int, seed: int = 9, n_clients: int | None = None, alpha_tr
             path[i] = "/" + "/".join(f"p{rng.integers(0, 50)}" for _ in range(depth[j])) + ".html"
     status = np.where(rng.random(n) < 0.92, 200, rng.choice([304, 404, 302, 500], size=n))
     if wide_vocab > 0:
+        # long-tail rows come from a codebook of ~n/20 request behaviours (host, method, agent,
+        # content type, URI, status, hour), drawn uniformly: a wide vocabulary whose words recur
+        # (~10 rows per behaviour) instead of a day-unique word on every other
+        # long-tail row (see synth.dns)
         wide = np.nonzero(rng.random(n) < wide_vocab)[0]
-        hour_f[wide] = rng.uniform(0, 24, size=wide.size)
-        for i, (h, mt, u, c, p, st) in zip(wide.tolist(), _wide_rows(rng, wide.size)):
-            host[i], method[i], ua[i], ctype[i], path[i], status[i] = h, mt, u, c, p, st
+        wide = wide[~np.isin(wide, anomaly_rows)]
+        crng = np.random.default_rng([seed, 0xC0DE])
+        W = max(200, n // 20)
+        cb = _wide_rows(crng, W)
+        cb_h = crng.uniform(0, 24, size=W)
+        b = rng.integers(0, W, wide.size)
+        hour_f[wide] = cb_h[b]
+        for i, j in zip(wide.tolist(), b.tolist()):
+            host[i], method[i], ua[i], ctype[i], path[i], status[i] = cb[j]
     hour = np.mod(np.floor(hour_f), 24).astype(int)
-    anomaly_rows = np.sort(rng.choice(n, size=min(n_anomalies, n), replace=False))
     quiet = np.argsort(w)[: max(1, n_clients // 10)]
     # individually rare behaviours (see synth.dns): varying method, content type, URI shape, hour
     a_methods = ["POST", "PUT", "CONNECT", "DELETE", "PROPFIND", "OPTIONS"]
     a_ctypes = ["application/x-www-form-urlencoded", "application/octet-stream", "application/x-msdownload",
                 "application/x-sh", "text/x-python"]
     for i in anomaly_rows:
-        cli[i] = quiet[rng.integers(0, quiet.size)]
+        if anomaly_kind == "rare":
+            cli[i] = quiet[rng.integers(0, quiet.size)]
+        if anomaly_kind == "offprofile":
+            continue
         host[i] = f"x{rng.integers(1000, 9999)}.badcdn-sync.biz"
         method[i] = a_methods[rng.integers(0, len(a_methods))]
         ua[i] = f"Mozilla/4.0 (compatible; agent-{rng.integers(10**6, 10**7)})"

@@ -41,6 +41,9 @@ def _check(out, n):
         assert stage in out["stage_median_s"], stage
     assert out["gibbs_iters_per_sec"] > 0 and out["config"]["sweeps_per_step"] == 6
     assert out["vs_baseline"] is None
+    # the realistic-vocabulary day of the same shape is reported next to the headline
+    rv = out["realistic_vocab"]
+    assert rv["value"] > 0 and rv["steps"] == 3 and rv["vocab"] > 0 and 0.0 <= rv["planted_anomaly_recall_topN"] <= 1.0
 
 
 def test_bench_single_process():

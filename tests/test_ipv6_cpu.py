@@ -121,3 +121,36 @@ def test_ipv6_dp_matches_single_process():
         p.join(timeout=120)
         assert p.exitcode == 0
     assert np.array_equal(one.rows, rows) and np.array_equal(one.scores, scores)
+
+
+def test_class_e_ipv4_never_shares_a_key_with_ipv6():
+    """On a day with IPv6, bogon IPv4 addresses in 240.0.0.0/4 go through the dictionary too: no
+    IPv4 document can alias an IPv6 one, and the result text keeps their dotted form."""
+    day = _day()
+    cols = dict(day.cols)
+    sip = np.asarray(cols["sip"]).copy()
+    v6 = np.array([bool(t) for t in cols["sip6"].to_list()])
+    v4rows = np.nonzero(~v6)[0][:5]
+    sip[v4rows] = V6_KEY_BASE + np.arange(5, dtype=np.uint32)  # exactly the first IPv6 keys
+    cols["sip"] = sip
+    k = with_ipv6_keys(cols)
+    keyed_e = k["sip"][v4rows]
+    keyed_6 = k["sip"][v6]
+    assert not np.isin(keyed_e, keyed_6).any()
+    assert np.all(keyed_e >= V6_KEY_BASE)
+    txt = k["sip6"].to_list()
+    assert [txt[i] for i in v4rows] == [f"240.0.0.{i}" for i in range(5)]
+    assert all(txt[i] == day.cols["sip6"].to_list()[i] for i in np.nonzero(v6)[0][:50])
+
+
+def test_prefetched_device_columns_must_be_ipv6_keyed():
+    import torch
+    from oni355.pipeline.flow import DEVICE_COLS, to_device
+    day = _day(3000)
+    with pytest.raises(ValueError, match="IPv6"):
+        run_flow(day.cols, K=8, sweeps=2, maxresults=50, device="cpu", device_cols=to_device(day.cols, "cpu"))
+    keyed = with_ipv6_keys(day.cols)
+    a = run_flow(keyed, K=8, sweeps=2, maxresults=50, device="cpu", device_cols=to_device(keyed, "cpu"))
+    b = run_flow(day.cols, K=8, sweeps=2, maxresults=50, device="cpu")
+    assert np.array_equal(a.rows, b.rows) and np.array_equal(a.scores, b.scores)
+    assert set(DEVICE_COLS) <= set(keyed) and torch is not None
