@@ -68,6 +68,10 @@ def parse(argv=None):
     ap.add_argument("--no-prefetch", action="store_true",
                     help="upload (and, --from-pcap, decode) each day inside its step instead of overlapping "
                          "it with the previous day's compute")
+    ap.add_argument("--from-store", action="store_true",
+                    help="every step reads its day from the columnar store (memory-mapped read + IPv6 keying + "
+                         "pinned copy on a loader thread, overlapping the previous day) -- what oni-ml does day "
+                         "after day (pipeline.daily); the store is written once at setup")
     ap.add_argument("--realistic-steps", type=int, default=3,
                     help="after the headline, also time this many steps (1 warm-up) of the realistic-vocabulary "
                          "day of the same size and report them under 'realistic_vocab' (0: skip)")
@@ -119,7 +123,8 @@ def main(argv=None) -> int:
         os.environ["ONI_NO_GRAPH"] = "1"
     comm = pc.init_from_env(a.device)
     out = run_sweep_mode(a, comm) if a.mode == "sweep" else run_pipeline_mode(a, comm)
-    if a.mode == "pipeline" and a.realistic_steps > 0 and not a.realistic_vocab and not a.from_pcap:
+    if (a.mode == "pipeline" and a.realistic_steps > 0 and not a.realistic_vocab and not a.from_pcap
+            and not a.from_store):
         # the same day shape with a long-tail vocabulary (V ~ 4e5 flow words: the q table leaves
         # L2), reported next to the headline, not instead of it
         import copy
@@ -198,7 +203,23 @@ def run_pipeline_mode(a, comm) -> dict:
             # day k computes
             from oni355.io.staging import HostAhead
             ahead = HostAhead(read_pcap_dns, pcap)
-    if dev.type == "cuda" and not a.no_prefetch and pcap is None:
+    store_pipe = None
+    if a.from_store:
+        # the product path: oni-ml's day pipeline over a stored day (re-read every step)
+        from oni355.io.staging import PinnedSlots
+        from oni355.pipeline.daily import DayPipeline, load_host_day
+        from oni355.store import columnar
+        root = os.path.join(tmp, "store")
+        columnar.write_day(root, a.source, "20160708", {k: v for k, v in day.cols.items() if not k.startswith("_")})
+        slots = PinnedSlots() if dev.type == "cuda" else None
+
+        def _load(date):
+            h = load_host_day(a.source, root, date, 0, 1, dev, None, None, slots=slots)
+            h.row_off = row_off
+            return h
+        store_pipe = DayPipeline(_load, dev, slots)
+        store_pipe.extend(["20160708"] * (a.warmup + a.steps))
+    if dev.type == "cuda" and not a.no_prefetch and pcap is None and store_pipe is None:
         from oni355.io.staging import Prefetcher
         if a.source == "flow":
             from oni355.pipeline.flow import DEVICE_COLS
@@ -216,6 +237,24 @@ def run_pipeline_mode(a, comm) -> dict:
     def step():
         t0 = time.perf_counter()
         dcols, on_train = None, None
+        if store_pipe is not None:
+            from oni355.pipeline.daily import run_day
+            w0 = store_pipe.wait_s
+            hday, dcols = store_pipe.take()
+            kw2 = dict(kw)
+            kw2.pop("comm")
+            kw2.pop("row_offset")
+            if a.source == "dns":
+                kw2.update(top_domains=top, user_domain="intel")
+            res = run_day(a.source, hday, dcols, comm, kw2)
+            res.timings["store_load_s"] = hday.load_s
+            res.timings["loader_wait_s"] = store_pipe.wait_s - w0
+            if store_pipe.pf is not None:
+                res.timings["h2d_copy_dev_s"] = (store_pipe.pf.copy_ms() or 0.0) / 1e3
+            t1 = time.perf_counter()
+            results.submit(hday.cols, res, row_off)
+            res.timings["results_s"] = time.perf_counter() - t1
+            return res
         if pf is not None:
             dcols = pf.take()
             # the next day's upload overlaps this day's compute
@@ -270,6 +309,8 @@ def run_pipeline_mode(a, comm) -> dict:
     results.drain()  # the last day's rows are part of the timed work
     _sync(dev)
     results.close()
+    if store_pipe is not None:
+        store_pipe.close()
     comm.barrier()
     _sync(dev)
     dt = comm.allreduce_scalar(time.perf_counter() - t0, "max")
@@ -306,11 +347,14 @@ def run_pipeline_mode(a, comm) -> dict:
         "dtype": "fp32",
         "data": f"synthetic {a.source} (oni355.synth.{a.source}: random-init topic priors, Zipf hosts, planted anomalies)"
                 + (", decoded from pcap every step" if pcap else "")
-                + (", realistic (long-tail) vocabulary" if a.realistic_vocab else ""),
+                + (", realistic (long-tail) vocabulary" if a.realistic_vocab else "")
+                + (", read from the columnar store every step" if a.from_store else ""),
         "config": {"model": f"oni-suspicious-connects-{a.source}-lda", "topics": K, "global_batch": n_total,
                    "events_per_gpu": per, "seq_len": 2 if a.source == "flow" else 1, "parallelism": f"dp{world}",
                    "sweeps_per_step": a.sweeps, "maxresults": a.maxresults, "baseline_config": baseline_cfg},
-        "step": "one full oni-ml day run per step: host columns -> H2D -> featurize -> corpus -> "
+        "step": ("one full oni-ml day per step, read from the columnar store (memory-mapped read, pinned copy "
+                 "and H2D of day k+1 on a loader thread / copy stream during day k) -> " if a.from_store else "")
+                + "one full oni-ml day run per step: host columns -> H2D -> featurize -> corpus -> "
                 f"{a.sweeps} Gibbs sweeps -> score -> top-{a.maxresults} -> CSV rows"
                 + ("; each step's H2D upload runs on a copy stream during the previous step" if pf is not None else "")
                 + ("; each step's pcap decode runs on a host thread during the previous step" if ahead is not None

@@ -24,7 +24,9 @@ import numpy as np
 
 def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(prog="oni-ml", description="MI355X suspicious-connects (ONI oni-ml equivalent)")
-    ap.add_argument("date", help="YYYYMMDD")
+    ap.add_argument("date", help="YYYYMMDD, a range YYYYMMDD-YYYYMMDD or a comma list (several days: one process "
+                                 "scores them back to back, each day's store read + pin + upload overlapping the "
+                                 "previous day's GPU work)")
     ap.add_argument("source", choices=["flow", "dns", "proxy"])
     ap.add_argument("tol", nargs="?", type=float, default=None, help="keep scores below TOL")
     ap.add_argument("maxresults", nargs="?", type=int, default=None)
@@ -54,6 +56,12 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--max-restarts", type=int, default=0,
                     help="supervise the run: after a failure (crash, watchdog exit, numerical fault) start a "
                          "fresh child process that resumes from the last checkpoint, up to R times")
+    ap.add_argument("--follow", action="store_true",
+                    help="after the given day(s), keep scoring every later day the store completes (_SUCCESS)")
+    ap.add_argument("--poll", type=float, default=5.0, help="--follow: seconds between store scans")
+    ap.add_argument("--idle-exit", type=float, default=3600.0,
+                    help="--follow: stop after this many seconds without a new complete day")
+    ap.add_argument("--max-days", type=int, default=0, help="stop after N days (0: no limit)")
     ap.add_argument("--quiet", action="store_true")
     return ap
 
@@ -217,6 +225,10 @@ def main(argv=None) -> int:
     comm = pc.init_from_env(device)
     rank, world = comm.rank, comm.world
     log = (lambda m: None) if (a.quiet or rank) else (lambda m: print(f"[oni-ml] {m}", file=sys.stderr, flush=True))
+    from ..pipeline.daily import parse_dates
+    dates = parse_dates(a.date)
+    if len(dates) > 1 or a.follow:
+        return _main_days(a, cfg, comm, device, dates, log)
     t0 = time.perf_counter()
     cols, row_off, n_total = load_events(a, cfg, a.source, rank, world)
     t_load = time.perf_counter() - t0
@@ -270,6 +282,43 @@ def main(argv=None) -> int:
     pc.shutdown()
     if rank == 0 and not a.quiet:
         print(json.dumps({"results": out, "rows": len(rendered), "timings": res.timings}))
+    return 0
+
+
+def _main_days(a, cfg, comm, device, dates: list[str], log) -> int:
+    """Several days (a range, a list, ``--follow``) from the columnar store in one process: the
+    day pipeline of oni355.pipeline.daily (store read + pin + upload of day k+1 overlap day k)."""
+    from ..io import results as rio
+    from ..parallel import comm as pc
+    from ..pipeline.daily import run_days
+    if a.synthetic or a.input:
+        raise SystemExit("oni-ml: several days / --follow read the columnar store (--data-root), not --synthetic/--input")
+    if a.ckpt_dir or a.ldac_out:
+        raise SystemExit("oni-ml: --ckpt-dir / --ldac-out apply to single-day runs")
+    root = a.data_root or cfg.DATA_ROOT
+    top = None
+    if cfg.TOP_DOMAINS:
+        from ..pipeline.dns import load_top_domains
+        top = load_top_domains(cfg.TOP_DOMAINS)
+    alpha = cfg.ALPHA if cfg.ALPHA > 0 else None
+    kw = dict(K=cfg.TOPIC_COUNT, sweeps=cfg.SWEEPS, tol=cfg.TOL, maxresults=cfg.MAXRESULTS, alpha=alpha,
+              beta=cfg.BETA, seed=cfg.SEED, chunk_len=cfg.CHUNK_LEN, device=device, dupfactor=cfg.DUPFACTOR,
+              eval_every=cfg.EVAL_EVERY, burnin=cfg.BURNIN, log=log)
+    if a.source == "dns":
+        kw.update(top_domains=top, user_domain=cfg.USER_DOMAIN)
+    elif a.source == "proxy":
+        kw.update(top_domains=top)
+    t0 = time.perf_counter()
+    recs = run_days(a.source, dates, root, cfg.LPATH, comm, kw, device, follow=a.follow, poll_s=a.poll,
+                    idle_exit_s=a.idle_exit, max_days=a.max_days,
+                    feedback_path=a.feedback or rio.scores_path(cfg.LPATH, a.source), log=log)
+    wall = time.perf_counter() - t0
+    comm.barrier()
+    pc.shutdown()
+    if comm.rank == 0 and not a.quiet:
+        print(json.dumps({"days": [r["date"] for r in recs], "wall_s": round(wall, 3),
+                          "s_per_day": round(wall / max(len(recs), 1), 4),
+                          "events": int(sum(r["events"] for r in recs))}))
     return 0
 
 

@@ -211,6 +211,11 @@ class Prefetcher:
             e1.record(self.stream)
         self._pending = (out, e0, e1)
 
+    def last_event(self):
+        """Event recorded after the pending upload's copies (a PinnedSlots slot may be reused once
+        it has completed)."""
+        return self._pending[2] if self._pending is not None else None
+
     def take(self) -> dict:
         out, e0, e1 = self._pending
         self._pending = None
@@ -226,6 +231,60 @@ class Prefetcher:
             return None
         self._last[1].synchronize()
         return self._last[0].elapsed_time(self._last[1])
+
+
+class PinnedSlots:
+    """Reusable page-locked buffers for the multi-day loader: ``n_slots`` sets of per-column
+    pinned tensors, refilled round-robin (allocating 550 MB of pinned memory per day cost more than
+    the copy into it). A slot is refilled only after the upload that last read it has finished
+    (``mark_used(slot, event)``). Columns are copied in parallel slices by ``threads`` workers --
+    numpy releases the GIL for the copies, so the loader thread is not one memcpy stream."""
+
+    def __init__(self, n_slots: int = 3, threads: int = 8):
+        from concurrent.futures import ThreadPoolExecutor
+        self.slots: list[dict] = [dict() for _ in range(n_slots)]
+        self.events: list = [None] * n_slots
+        self.k = 0
+        self.pool = ThreadPoolExecutor(threads, thread_name_prefix="oni-pincopy")
+        self.threads = threads
+
+    def _buf(self, slot: dict, name: str, n: int, dtype: torch.dtype) -> torch.Tensor:
+        t = slot.get(name)
+        if t is None or t.numel() < n or t.dtype != dtype:
+            t = torch.empty(max(n, 1), dtype=dtype).pin_memory()
+            slot[name] = t
+        return t[:n]
+
+    def fill(self, arrays: dict, dtypes: dict | None = None) -> tuple[int, dict]:
+        """(slot index, pinned tensors) holding ``arrays`` (name → array-like; memmaps are read
+        here), converted to ``dtypes[name]`` when given."""
+        i = self.k
+        self.k = (self.k + 1) % len(self.slots)
+        ev = self.events[i]
+        if ev is not None:
+            ev.synchronize()  # the upload that last read this slot has finished
+        slot = self.slots[i]
+        out, futs = {}, []
+        for name, a in arrays.items():
+            a = np.asarray(a)
+            if a.dtype == np.uint32:
+                a = a.view(np.int32)
+            dt = dtypes[name] if dtypes else torch.from_numpy(a[:0]).dtype
+            t = self._buf(slot, name, a.shape[0], dt)
+            dst = t.numpy()
+            step = max(1 << 20, -(-a.shape[0] // self.threads))
+            for lo in range(0, a.shape[0], step):
+                futs.append(self.pool.submit(np.copyto, dst[lo:lo + step], a[lo:lo + step], "unsafe"))
+            out[name] = t
+        for f in futs:
+            f.result()
+        return i, out
+
+    def mark_used(self, slot: int, event) -> None:
+        self.events[slot] = event
+
+    def close(self) -> None:
+        self.pool.shutdown(wait=True)
 
 
 class HostAhead:

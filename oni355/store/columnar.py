@@ -228,9 +228,12 @@ def rows(root: str, source: str, date: str, hours: list[int] | None = None) -> i
 
 
 def read_day(root: str, source: str, date: str, columns=None, row_range: tuple[int, int] | None = None,
-             hours: list[int] | None = None) -> dict:
+             hours: list[int] | None = None, mmap: bool = False) -> dict:
     """Columns of a stored day (all partitions, or only the hour partitions in ``hours``);
-    ``row_range`` selects global rows [lo, hi) of that view (a data-parallel rank's shard)."""
+    ``row_range`` selects global rows [lo, hi) of that view (a data-parallel rank's shard).
+    ``mmap``: a column held by one partition is returned as a read-only memory map of the file
+    (no copy: the multi-day loader reads only the device columns in full and renders a few
+    thousand result rows from the rest); columns spread over partitions are concatenated."""
     d = day_dir(root, source, date)
     parts = _parts(d, hours)
     if not parts:
@@ -250,13 +253,20 @@ def read_day(root: str, source: str, date: str, columns=None, row_range: tuple[i
             if columns is not None and name not in columns:
                 continue
             if kind == "string":
-                off = np.load(os.path.join(p, f"{name}.off.npy"), allow_pickle=False)
-                chars = np.fromfile(os.path.join(p, f"{name}.chars.bin"), dtype=np.uint8)
+                off = np.load(os.path.join(p, f"{name}.off.npy"), mmap_mode="r" if mmap else None, allow_pickle=False)
+                cpath = os.path.join(p, f"{name}.chars.bin")
+                if mmap and os.path.getsize(cpath):
+                    chars = np.memmap(cpath, dtype=np.uint8, mode="r")
+                else:
+                    chars = np.fromfile(cpath, dtype=np.uint8)
                 out.setdefault(name, []).append(StringColumn(off, chars).slice(plo, phi_))
             else:
                 a = np.load(os.path.join(p, f"{name}.npy"), mmap_mode="r", allow_pickle=False)
-                out.setdefault(name, []).append(np.array(a[plo:phi_]))
+                out.setdefault(name, []).append(a[plo:phi_] if mmap else np.array(a[plo:phi_]))
     res = {}
     for k, v in out.items():
-        res[k] = StringColumn.concat(v) if isinstance(v[0], StringColumn) else np.concatenate(v)
+        if len(v) == 1:
+            res[k] = v[0]  # one partition: no concatenation copy (a memory map with ``mmap``)
+        else:
+            res[k] = StringColumn.concat(v) if isinstance(v[0], StringColumn) else np.concatenate(v)
     return res
