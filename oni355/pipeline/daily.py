@@ -205,11 +205,13 @@ def run_days(source: str, dates: list[str], root: str, lpath: str, comm, kw: dic
                 continue
             day, dcols = got
             t0 = time.perf_counter()
+            wait_total, pipe_wait0 = pipe.wait_s, getattr(pipe, "_wait_reported", 0.0)
+            pipe._wait_reported = wait_total
             res = run_day(source, day, dcols, comm, kw)
             results.submit(day.cols, res, day.row_off, tag=day.date)
             rec = {"event": "oni-ml-day", "source": source, "date": day.date, "events": day.n_total, "ranks": world,
                    "load_s": round(day.load_s, 4), "day_s": round(time.perf_counter() - t0, 4),
-                   "loader_wait_s": round(pipe.wait_s, 4), **{k: v for k, v in res.timings.items()},
+                   "loader_wait_s": round(wait_total - pipe_wait0, 4), **{k: v for k, v in res.timings.items()},
                    **{k: v for k, v in res.stats.items() if isinstance(v, (int, float, str)) or v is None}}
             if dcols is not None and pipe.pf is not None:
                 rec["h2d_copy_dev_s"] = (pipe.pf.copy_ms() or 0.0) / 1e3
