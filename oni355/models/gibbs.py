@@ -69,6 +69,14 @@ class GibbsConfig:
     # ONI_SAMPLER overrides the default. All but "lds" are bitwise identical to each other; "lds"
     # is bitwise identical to the oracle's fma numerics.
     sampler: str = field(default_factory=lambda: os.environ.get("ONI_SAMPLER", "auto"))
+    # posterior averaging: θ and φ are estimated from the counts of the last ``post_samples``
+    # samples taken every ``post_every`` sweeps (ending at the last sweep) instead of the final
+    # sample alone. A word seen once sits in ONE topic in any single sample, so its φ row -- and
+    # the score of its event -- follows that one draw: a rare word sampled into a minor topic of
+    # its document scores as if it were an anomaly. The averaged counts give it its posterior
+    # topic mix, as lda-c's variational β / γ do. 1 = the final sample only.
+    post_samples: int = field(default_factory=lambda: int(os.environ.get("ONI_POST_SAMPLES", "8")))
+    post_every: int = 2
 
     def resolved_alpha(self) -> float:
         return float(self.alpha) if self.alpha is not None else 50.0 / self.K
@@ -204,6 +212,9 @@ class GibbsLDA:
         self._x01 = None
         if comm is not None and comm.dist and self.KS % 2 == 0 and self._x01_wanted():
             self._setup_x01()
+        self._avg = None          # posterior-averaging accumulators (plan_average)
+        self._avg_at: list = []   # sweep counts at which a sample is added
+        self._avg_cache = None    # (θ, φ) of the completed average
 
     def _x01_wanted(self) -> bool:
         """``ONI_X01_PACK``: "1" always packs, "0" never, "auto" (default) packs when the dense Δ
@@ -535,7 +546,13 @@ class GibbsLDA:
         if self._watchdog is not None:
             self._watchdog.arm()
         try:
-            self._sweep_n(n)
+            while n > 0:
+                nxt = [p for p in self._avg_at if p > self.sweeps_done]
+                seg = min(n, nxt[0] - self.sweeps_done) if nxt else n
+                self._sweep_n(seg)
+                n -= seg
+                if self._avg is not None and self.sweeps_done in self._avg_at:
+                    self._add_sample()
         finally:
             if self._watchdog is not None:
                 self._watchdog.disarm()
@@ -629,6 +646,74 @@ class GibbsLDA:
             if self._watchdog is not None:
                 self._watchdog.kick()
 
+    # ---- posterior averaging -------------------------------------------------------------------
+    def plan_average(self, total_sweeps: int) -> None:
+        """Average the counts of the samples at sweeps total, total - e, …, total - (S-1)·e
+        (e = cfg.post_every, S = cfg.post_samples capped at total / 4e)."""
+        S, e = max(1, int(self.cfg.post_samples)), max(1, int(self.cfg.post_every))
+        # at most the last quarter of the chain (burn-in first): a 200-sweep day averages 8
+        # samples over sweeps 186-200, a 30-sweep run 3, a run of < 8 sweeps none
+        S = min(S, int(total_sweeps) // (4 * e))
+        at = [total_sweeps - j * e for j in range(S) if total_sweeps - j * e > 0]
+        self._avg_at = sorted(at) if S > 1 else []
+        self._avg_cache = None
+        dev = self.device
+        if self._avg_at:
+            self._avg = dict(n=0, wk=torch.zeros_like(self.nwk), k=torch.zeros_like(self.nk[0]),
+                             dk=torch.zeros_like(self.ndk[0]))
+        else:
+            self._avg = None
+        _ = dev
+
+    @property
+    def average_window(self) -> tuple[int, int] | None:
+        """(first, last) sample sweep of the planned average, or None."""
+        return (self._avg_at[0], self._avg_at[-1]) if self._avg_at else None
+
+    def average_state(self) -> dict | None:
+        """The accumulated samples (for a checkpoint), or None outside an averaging window."""
+        a = self._avg
+        if a is None or a["n"] == 0:
+            return None
+        return {"n": int(a["n"]), "wk": a["wk"].cpu(), "k": a["k"].cpu(), "dk": a["dk"].cpu()}
+
+    def load_average_state(self, st: dict) -> None:
+        """Restore :meth:`average_state` (same corpus layout) after a resume inside the window."""
+        a = self._avg
+        if a is None:
+            raise ValueError("checkpoint holds posterior-averaging samples but no average is planned")
+        for k in ("wk", "k", "dk"):
+            if tuple(st[k].shape) != tuple(a[k].shape):
+                raise ValueError(f"averaging state {k} shape {tuple(st[k].shape)} != {tuple(a[k].shape)}")
+            a[k].copy_(st[k].to(a[k].device))
+        a["n"] = int(st["n"])
+        self._avg_cache = None
+
+    def _add_sample(self) -> None:
+        a = self._avg
+        a["wk"] += self.nwk
+        a["k"] += self.nk_cur
+        a["dk"] += self.ndk_cur
+        a["n"] += 1
+        self._avg_cache = None
+
+    def _averaged(self):
+        """(θ, φ) from the accumulated samples, once every planned sample is in; else None."""
+        a = self._avg
+        if a is None or a["n"] == 0 or a["n"] != len(self._avg_at) or self.sweeps_done != self._avg_at[-1]:
+            return None
+        if self._avg_cache is None:
+            S, K = float(a["n"]), self.K
+            n = a["dk"].to(torch.float32)
+            nd = n[:, :K].sum(1, keepdim=True)
+            th = (n + S * self.alpha) / (nd + S * K * self.alpha)
+            th[:, K:] = 0
+            den = a["k"].to(torch.float32) + np.float32(S) * self.vbeta
+            ph = (a["wk"].to(torch.float32) + S * self.beta) / den
+            ph[:, K:] = 0
+            self._avg_cache = (th.contiguous(), ph.contiguous())
+        return self._avg_cache
+
     # ---------------------------------------------------------------------------------------------
     @property
     def ndk_cur(self) -> torch.Tensor:
@@ -639,7 +724,11 @@ class GibbsLDA:
         return self.nk[self.cn]
 
     def theta(self) -> torch.Tensor:
-        """θ[d,k] = (n_dk+α)/(n_d+Kα), padded to KS with zeros (score-kernel layout)."""
+        """θ[d,k] = (n_dk+α)/(n_d+Kα), padded to KS with zeros (score-kernel layout); from the
+        averaged counts once the planned posterior average is complete (:meth:`plan_average`)."""
+        avg = self._averaged()
+        if avg is not None:
+            return avg[0]
         n = self.ndk_cur.to(torch.float32)
         nd = n[:, : self.K].sum(1, keepdim=True)
         th = (n + self.alpha) / (nd + self.K * self.alpha)
@@ -647,8 +736,10 @@ class GibbsLDA:
         return th.contiguous()
 
     def phi(self) -> torch.Tensor:
-        """φ[w,k] = (n_wk+β)/(n_k+Vβ) for the current counts (= the q table), KS-padded."""
-        return self.q
+        """φ[w,k] = (n_wk+β)/(n_k+Vβ) for the current counts (= the q table), KS-padded; from the
+        averaged counts once the planned posterior average is complete."""
+        avg = self._averaged()
+        return avg[1] if avg is not None else self.q
 
     @traced("oni:lda.loglik")
     def log_likelihood(self) -> float:

@@ -479,6 +479,7 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
         run = LdaRun(corpus, model, udoc, vocab, {}, pairs=pairs, route=route)
         if not train:
             return run
+        model.plan_average(sweeps)
         if ckpt is not None and ckpt.exists():
             ckpt.restore(model)
         else:

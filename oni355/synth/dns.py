@@ -63,9 +63,12 @@ def top_domain_list(n_extra: int = 2000, seed: int = 1) -> list[str]:
     return _POPULAR + _CDN + _MAIL + ["microsoft.com", "icloud.com", "app-measurement.com", "crashlytics.com"] + extra
 
 
-# long-tail record types / rcodes of a real resolver day (A, AAAA, PTR, MX, TXT, SRV, CNAME, NS, SOA,
-# HTTPS, SVCB, ANY, NULL, DS, DNSKEY, NAPTR, CAA, TLSA) with Zipf-like weights
-_WIDE_QTYPES = [1, 28, 12, 15, 16, 33, 5, 2, 6, 65, 64, 255, 10, 43, 48, 35, 257, 52]
+# long-tail record types / rcodes of a real resolver day (A, AAAA, PTR, MX, SRV, CNAME, NS, SOA, HTTPS,
+# SVCB, DS, DNSKEY, NAPTR, CAA, TLSA) with Zipf-like weights
+# (the planted queries' record types, _ANOMALY_QTYPES, are kept out of the long tail: a planted query
+# stays an individually rare word on the realistic day)
+_ANOMALY_QTYPES = [16, 10, 13, 17, 29, 99, 252, 255]
+_WIDE_QTYPES = [1, 28, 12, 15, 33, 5, 2, 6, 65, 64, 43, 48, 35, 257, 52]
 _WIDE_RCODES = [0, 3, 2, 5, 1, 4]
 _ALPHABETS = [b"abcdefghijklmnopqrstuvwxyz", b"0123456789abcdef", b"abcdefghijklmnopqrstuvwxyz0123456789-",
               b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789"]
@@ -144,21 +147,30 @@ def generate_dns(n: int, seed: int = 5, n_clients: int | None = None, user_domai
             for j, i in enumerate(idx):
                 names[i] = f"{_SERVICE[sv[j]]}.{doms[dsel[j]]}"
     if wide_vocab > 0:
-        # long-tail rows come from a codebook of ~n/20 query behaviours (name shape, record type,
-        # rcode, hour), drawn uniformly: a wide vocabulary whose words still recur (~10 rows per
-        # behaviour at 2M rows) -- independent per-row draws make every other long-tail row a
-        # day-unique word, which P(word | doc) cannot tell from a planted one
+        # long-tail rows come from a codebook of ~n/100 query behaviours (name shape, record type,
+        # rcode, hour); every client owns ⌈its long-tail rows / 8⌉ of them (dealt round-robin, so
+        # each has several owners) and repeats them, as synth.flow's realistic day does.
+        # Independent per-row draws made every other long-tail row a day-unique word, and uniform
+        # draws from the codebook scattered each behaviour over unrelated clients -- either way
+        # P(word | doc) could not tell them from a planted query
         wide = np.nonzero(rng.random(n) < wide_vocab)[0]
         m = wide.size
         crng = np.random.default_rng([seed, 0xC0DE])
-        W = max(200, n // 20)
+        W = max(200, n // 100)
         qz = 1.0 / np.arange(1, len(_WIDE_QTYPES) + 1) ** 1.2
         cb_q = crng.choice(_WIDE_QTYPES, size=W, p=qz / qz.sum())
         rz = np.array([0.8, 0.1, 0.05, 0.03, 0.015, 0.005])
         cb_r = crng.choice(_WIDE_RCODES, size=W, p=rz / rz.sum())
         cb_h = crng.uniform(0, 24, size=W)
         cb_n = _wide_names(crng, W, top_domain_list())
-        b = rng.integers(0, W, m)
+        c_w = cli[wide]
+        slots = np.clip(-(-np.bincount(c_w, minlength=n_clients) // 8), 1, 64)
+        first = np.concatenate([[0], np.cumsum(slots)[:-1]])
+        orng = np.random.default_rng([seed, 0x0515])
+        n_sl = int(slots.sum())
+        own = np.concatenate([orng.permutation(W) for _ in range(-(-n_sl // W))])[:n_sl]
+        own = own[orng.permutation(n_sl)]
+        b = own[first[c_w] + (rng.random(m) * slots[c_w]).astype(np.int64)]
         qtype[wide] = cb_q[b]
         rcode[wide] = cb_r[b]
         hour_f[wide] = cb_h[b]
@@ -185,7 +197,7 @@ def generate_dns(n: int, seed: int = 5, n_clients: int | None = None, user_domai
             cut = np.linspace(0, len(h), k + 1).astype(int)
             sub = ".".join(h[cut[t]:cut[t + 1]] for t in range(k))
             names[i] = f"{sub}.x{rng.integers(100, 999)}tunnel.biz"
-        qtype[anomaly_rows] = rng.choice([16, 10, 13, 17, 29, 99, 252, 255], size=na)
+        qtype[anomaly_rows] = rng.choice(_ANOMALY_QTYPES, size=na)
         rcode[anomaly_rows] = rng.choice([0, 2, 5], size=na)
         hour[anomaly_rows] = rng.integers(1, 6, size=na)
     minute = rng.integers(0, 60, size=n)

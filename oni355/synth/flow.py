@@ -9,10 +9,11 @@ with random-init topic priors" (BASELINE.json). Generative model:
 * every internal host (a document) has a profile mix θ* ~ Dir(alpha_true) (sparse);
 * host activity is Zipf-distributed (a few hosts own most flows: NAT gateways, resolvers);
 * each flow: profile z ~ θ*[src], server from the profile's pool, port/hour/bytes/packets from z;
-* ``n_anomalies`` planted flows with off-profile behaviour (rare service port at an odd hour with
-  outsized volume) on hosts drawn by activity -- ground truth for "planted anomalies rank in the
-  top-N" tests. The rare ports are kept out of the realistic day's long tail, so every planted
-  flow stays an individually rare word there too.
+* ``n_anomalies`` planted flows on hosts drawn by activity: an ordinary flow of a profile the host
+  never uses, to that profile's server (lateral movement; see the comment at the plant) -- ground
+  truth for "planted anomalies rank in the top-N" tests. ``anomaly_kind="rare-service"`` plants
+  the round-1/2 rare-port flows to fresh external addresses instead (their ports are kept out of
+  the realistic day's long tail).
 
 Columns follow the flow schema of SURVEY.md §2.7 (nfdump CSV → Hive ``flow`` table).
 """
@@ -45,6 +46,9 @@ _PROFILES = [
     ("ftp", [21, 20], [0.5, 0.5], 16, 2.0, 12.5, 1.5, 1400),
     ("monitoring", [9100, 5666], [0.5, 0.5], 12, 7.0, 7.2, 0.4, 500),
 ]
+
+LT_REPEAT = 8  # realistic-vocabulary day: flows per (host, long-tail behaviour) pair
+LT_MAX_SLOTS = 64  # ... and at most this many behaviours per host (a gateway repeats its own)
 
 # rarely-used service ports (none is in a profile): planted anomalies draw from all of them so
 # that each anomaly is an individually rare word, not one more frequent pattern
@@ -81,13 +85,15 @@ def str_to_ip(s: str) -> int:
 def generate_flows(n: int, seed: int = 7, n_hosts: int | None = None, n_profiles: int = 20,
                    alpha_true: float = 0.08, zipf_a: float = 1.15, n_anomalies: int | None = None,
                    date=(2016, 7, 8), rank: int = 0, wide_vocab: bool = False, ipv6_frac: float = 0.0,
-                   anomaly_hosts: str = "active") -> FlowDay:
+                   anomaly_hosts: str = "active", anomaly_kind: str = "rare-service",
+                   support_min: float = 0.02) -> FlowDay:
     """Generate ``n`` flows. ``rank`` offsets the RNG stream (weak-scaling shards of one day).
 
     ``wide_vocab``: a realistic-vocabulary day (SURVEY.md §7.5 sizing, V ≈ 1e5–1e6 flow words):
-    half of the flows use a long-tail (Zipf) service port anywhere in 1..1024 instead of their
-    profile's ports, hours and volumes are spread wider, and 20 % of the flows are server-to-server
-    (both ports low / both high), so every (port, time, bytes, packets, direction) bin fills."""
+    half of the flows repeat one of their host's long-tail behaviours (a service port
+    anywhere in 1..1024 with its own hour, volume and server) instead of a profile flow, and 20 %
+    of the flows are server-to-server (both ports low / both high), so every (port, time, bytes,
+    packets, direction) bin fills."""
     rng = np.random.default_rng([seed, rank])
     n_profiles = min(n_profiles, len(_PROFILES))
     prof = _PROFILES[:n_profiles]
@@ -100,6 +106,13 @@ def generate_flows(n: int, seed: int = 7, n_hosts: int | None = None, n_profiles
     hid = np.arange(n_hosts, dtype=np.int64)
     host_ips = _ip(10, (hid >> 16) & 255, (hid >> 8) & 255, hid & 255).astype(np.uint32)
     theta = hrng.dirichlet(np.full(n_profiles, alpha_true), size=n_hosts)
+    # support cut: a host never uses a profile of true weight < support_min (a Dirichlet draw has
+    # no exact zeros, and its tails would make every busy host do a little of everything -- each
+    # such flow an unplanted off-profile event)
+    theta = np.where(theta >= support_min, theta, 0.0)
+    top1 = np.argmax(theta, axis=1)
+    theta[np.arange(n_hosts), top1] += (theta.sum(1) == 0)
+    theta /= theta.sum(1, keepdims=True)
     # servers per profile: 172.16.<p>.<i>
     n_srv = max(4, min(250, n_hosts // 20))
     # host activity: Zipf over a random permutation of hosts
@@ -128,15 +141,19 @@ def generate_flows(n: int, seed: int = 7, n_hosts: int | None = None, n_profiles
         hour_f[m] = rng.normal(peak, hsd, size=cnt)
         lbytes[m] = rng.normal(mu, sd, size=cnt)
         bpp[m] = bp * np.exp(rng.normal(0, 0.2, size=cnt))
+    srv = rng.integers(0, n_srv, size=n)
+    dip = _ip(172, 16, z & 255, srv & 255).astype(np.uint32)
     if wide_vocab:
         # Half the flows come from a codebook of ~n/100 long-tail service behaviours (a well-known
-        # port of the ~1k-port pool, an hour, a volume and a packet size each), drawn uniformly:
-        # the day's vocabulary grows to V ≈ 4e5 flow words at 12.5M flows (SURVEY.md §7.5 sizing:
-        # the q table leaves L2) while every behaviour recurs ~50 times. A Zipf tail of
-        # independent port / hour / volume draws instead makes tens of thousands of day-unique
-        # normal words, which P(word | doc) ranks by topic-assignment luck, and no planted row can
-        # be told from them (profiles/r3/recall_sweep.jsonl). The anomalies' rare services are
-        # not in the pool.
+        # port of the ~1k-port pool, an hour, a volume, a packet size and a server of its own):
+        # the day's vocabulary grows to V ≈ 2e5-4e5 flow words at 12.5M flows (SURVEY.md §7.5
+        # sizing: the q table leaves L2). Every host owns a few behaviours of the codebook
+        # and its long-tail flows repeat them -- a backup agent, a licence server, a monitoring
+        # probe recur from the same hosts to the same servers -- so a long-tail word is common in
+        # the documents that carry it. Drawing behaviours uniformly over all hosts and the
+        # profile servers instead scattered each over ~50 unrelated documents, where P(word |
+        # doc) cannot tell them from a planted row (recall 0.245 at 12.5M flows,
+        # profiles/r3/recall_sweep_codebook.jsonl). The anomalies' rare services are not in the pool.
         lt = np.nonzero(rng.random(n) < 0.5)[0]
         crng = np.random.default_rng([seed, 0xC0DE])
         W = max(1000, n // 100)
@@ -145,21 +162,37 @@ def generate_flows(n: int, seed: int = 7, n_hosts: int | None = None, n_profiles
         cb_hour = crng.uniform(0.0, 24.0, W)
         cb_lbytes = crng.uniform(4.0, 18.0, W)
         cb_bpp = np.exp(crng.uniform(np.log(40.0), np.log(1500.0), W))
-        b = rng.integers(0, W, lt.size)
+        n_lts = max(16, W // 8)  # long-tail servers 172.17-31.x.y, ~8 behaviours each
+        cb_srv = crng.integers(0, n_lts, W)
+        # each host owns ⌈(its long-tail flows) / LT_REPEAT⌉ behaviours, so every (host, behaviour)
+        # pair recurs ~LT_REPEAT times in the host's document
+        h_lt = src[lt]
+        slots = np.clip(-(-np.bincount(h_lt, minlength=n_hosts) // LT_REPEAT), 1, LT_MAX_SLOTS)
+        first = np.concatenate([[0], np.cumsum(slots)[:-1]])
+        # slots deal the codebook out round-robin (shuffled): every behaviour has ~Σslots / W
+        # owners, so none is a day-unique word
+        orng = np.random.default_rng([seed, 0x0515])
+        n_sl = int(slots.sum())
+        own = np.concatenate([orng.permutation(W) for _ in range(-(-n_sl // W))])[:n_sl]
+        own = own[orng.permutation(n_sl)]
+        b = own[first[h_lt] + (rng.random(lt.size) * slots[h_lt]).astype(np.int64)]
         port_of[lt] = cb_port[b]
         hour_f[lt] = cb_hour[b]
-        lbytes[lt] = cb_lbytes[b] + rng.normal(0.0, 0.02, lt.size)
+        lbytes[lt] = cb_lbytes[b]
         bpp[lt] = cb_bpp[b]
-    srv = rng.integers(0, n_srv, size=n)
-    dip = _ip(172, 16, z & 255, srv & 255).astype(np.uint32)
+        s = cb_srv[b]
+        dip[lt] = _ip(172, 17 + (s >> 16), (s >> 8) & 255, s & 255)
     sip = host_ips[src]
     eph = rng.integers(1025, 65536, size=n)
     # ~15% of flows are recorded from the server side (service port in sport)
     flip = rng.random(n) < 0.15
+    if wide_vocab:
+        flip[lt] = False  # a long-tail behaviour is one word: always recorded client side
     sport = np.where(flip, port_of, eph)
     dport = np.where(flip, eph, port_of)
     if wide_vocab:
         s2s = rng.random(n) < 0.2  # server-to-server: both low (111111) or both high (333333)
+        s2s[lt] = False
         both_low = s2s & (rng.random(n) < 0.5)
         both_high = s2s & ~both_low
         sport = np.where(both_low, rng.integers(1, 1025, size=n), np.where(both_high, rng.integers(1025, 65536, size=n), sport))
@@ -169,14 +202,27 @@ def generate_flows(n: int, seed: int = 7, n_hosts: int | None = None, n_profiles
 
     hour = np.mod(np.floor(hour_f), 24).astype(np.int64)
     minute = rng.integers(0, 60, size=n)
+    if wide_vocab:
+        minute[lt] = (cb_hour[b] * 60).astype(np.int64) % 60  # scheduled: one time bin per behaviour
     second = rng.integers(0, 60, size=n)
     ibyt = np.maximum(40, np.exp(lbytes)).astype(np.int64)
     ipkt = np.maximum(1, np.round(ibyt / np.maximum(bpp, 40))).astype(np.int64)
 
-    # planted anomalies: off-profile rare service, odd hour, huge volume. anomaly_hosts "active"
-    # (default): the compromised hosts are drawn like any flow's source (by activity), so the
-    # anomaly is rare FOR A HOST WHOSE BEHAVIOUR IS KNOWN -- the case P(word | doc) scoring ranks;
-    # "quiet" plants them on the least active tenth of the hosts (round-1/2 generator)
+    # planted anomalies. anomaly_hosts "active" (default): the compromised hosts are drawn like any
+    # flow's source (by activity); "quiet": the least active tenth of the hosts.
+    #
+    # anomaly_kind "offprofile" (default): the host makes an ordinary flow of the profile it is
+    # least likely to use (θ*[host, p] = 0 after the support cut) to one of that profile's servers
+    # -- a workstation reaching a database or backup server it never talks to (lateral
+    # movement). What P(word | doc) scoring can rank: a token is scored with its own topic in the
+    # counts, so a word that only the anomaly uses (a day-unique rare-service word) is sampled
+    # into its host's dominant topic and scores like any on-profile flow of that host, while a
+    # word that the profile's own hosts use often pulls the token into the profile's topic, where
+    # the host has almost no mass: θ[host, B] ≈ (1 + α) / (n_host + Kα). The score falls with the
+    # host's activity, so the anomaly is rare FOR A HOST WHOSE BEHAVIOUR IS KNOWN.
+    # "rare-service": the round-1/2 plant -- a rare service port at an odd hour with outsized
+    # volume to a fresh external address (203.0.113.0/24): individually unique words, which the
+    # scoring above ranks no lower than any rare flow of a small document.
     anomaly_rows = np.sort(rng.choice(n, size=min(n_anomalies, n), replace=False))
     na = anomaly_rows.size
     if na:
@@ -186,14 +232,30 @@ def generate_flows(n: int, seed: int = 7, n_hosts: int | None = None, n_profiles
         else:
             a_src = src[anomaly_rows]
         sip2[anomaly_rows] = host_ips[a_src]
-        dip2[anomaly_rows] = _ip(203, 0, 113, rng.integers(1, 255, size=na) & 255)
         sport[anomaly_rows] = rng.integers(1025, 65536, size=na)
-        dport[anomaly_rows] = rng.choice(_ANOMALY_PORTS, size=na)
-        hour[anomaly_rows] = rng.integers(1, 6, size=na)
-        ibyt[anomaly_rows] = rng.integers(500_000_000, 900_000_000, size=na)
-        # volume shape: a few giant packets, or a flood of them
-        flood = rng.random(na) < 0.5
-        ipkt[anomaly_rows] = np.where(flood, rng.integers(400_000, 600_000, size=na), rng.integers(1, 3, size=na))
+        if anomaly_kind == "rare-service":
+            dip2[anomaly_rows] = _ip(203, 0, 113, rng.integers(1, 255, size=na) & 255)
+            dport[anomaly_rows] = rng.choice(_ANOMALY_PORTS, size=na)
+            hour[anomaly_rows] = rng.integers(1, 6, size=na)
+            ibyt[anomaly_rows] = rng.integers(500_000_000, 900_000_000, size=na)
+            # volume shape: a few giant packets, or a flood of them
+            flood = rng.random(na) < 0.5
+            ipkt[anomaly_rows] = np.where(flood, rng.integers(400_000, 600_000, size=na), rng.integers(1, 3, size=na))
+        elif anomaly_kind == "offprofile":
+            # the profile with the least true mass for the host; ties (several zeros after the
+            # support cut) broken at random so the anomalies spread over profiles
+            pert = theta[a_src] + rng.random((na, n_profiles)) * 1e-9
+            p_off = np.argmin(pert, axis=1)
+            dip2[anomaly_rows] = _ip(172, 16, p_off & 255, rng.integers(0, n_srv, size=na) & 255)
+            for j, pk in enumerate(p_off.tolist()):
+                _, ports, pw, peak, hsd, mu, sd, bp = prof[pk]
+                r = anomaly_rows[j]
+                dport[r] = ports[int(np.argmax(pw))]
+                hour[r] = int(np.floor(rng.normal(peak, hsd))) % 24
+                ibyt[r] = max(40, int(np.exp(rng.normal(mu, sd))))
+                ipkt[r] = max(1, int(round(ibyt[r] / max(bp, 40))))
+        else:
+            raise ValueError(f"unknown anomaly_kind {anomaly_kind!r}")
 
     v6_rows = None
     if ipv6_frac > 0:

@@ -51,7 +51,12 @@ class ProxyDay:
         return int(len(self.cols["clientip"]))
 
 
-_WIDE_METHODS = ["GET", "POST", "HEAD", "PUT", "OPTIONS", "CONNECT", "DELETE", "PATCH", "TRACE", "PROPFIND"]
+N_TEMPLATES = 24  # request templates per behaviour profile
+
+# the planted requests' methods (_ANOMALY_METHODS) are kept out of the long tail, as synth.flow keeps
+# its anomaly ports out: a planted request stays an individually rare word on the realistic day
+_ANOMALY_METHODS = ["CONNECT", "DELETE", "PROPFIND", "OPTIONS"]
+_WIDE_METHODS = ["GET", "POST", "HEAD", "PUT", "PATCH", "TRACE"]
 _WIDE_CTYPES = ["text/html", "text/plain", "text/css", "text/javascript", "image/png", "image/jpeg", "image/gif",
                 "image/webp", "application/javascript", "application/json", "application/xml", "application/pdf",
                 "application/octet-stream", "application/zip", "application/x-protobuf", "video/mp4", "video/webm",
@@ -119,41 +124,62 @@ def generate_proxy(n: int, seed: int = 9, n_clients: int | None = None, alpha_tr
         z[anomaly_rows] = np.argmin(theta[cli[anomaly_rows]], axis=1)
     host, method, ua, ctype, path = [""] * n, [""] * n, [""] * n, [""] * n, [""] * n
     hour_f = np.zeros(n)
+    status = np.full(n, 200, np.int64)
+    # each profile serves N_TEMPLATES request templates (host, path, method, content type,
+    # status), drawn Zipf-like: what a page load, an update check or an API call repeats all day.
+    # A client keeps one user agent per profile. Independent per-row draws of every field made a
+    # 6000-row day ~1200 day-unique words, among which no planted request stood out
+    # (profiles/r3/recall_sweep_codebook.jsonl: proxy recall 0.03-0.12).
+    trng = np.random.default_rng([seed, 0x7E3])
+    tz = 1.0 / np.arange(1, N_TEMPLATES + 1)
+    tz /= tz.sum()
     for k, (key, meths, mw, uas, peak, hsd) in enumerate(_PROFILES):
         idx = np.nonzero(z == k)[0]
         m = idx.size
+        hs, cts = _HOSTS[key], _CTYPES[key]
+        t_host = trng.integers(0, len(hs), N_TEMPLATES)
+        t_ct = trng.integers(0, len(cts), N_TEMPLATES)
+        t_m = trng.choice(len(meths), size=N_TEMPLATES, p=np.asarray(mw) / np.sum(mw))
+        t_path = ["/" + "/".join(f"p{trng.integers(0, 50)}" for _ in range(int(trng.integers(1, 4)))) + ".html"
+                  for _ in range(N_TEMPLATES)]
+        t_st = np.where(trng.random(N_TEMPLATES) < 0.85, 200, trng.choice([304, 302, 404], size=N_TEMPLATES))
         if not m:
             continue
-        hs, cts = _HOSTS[key], _CTYPES[key]
-        hsel = rng.integers(0, len(hs), m)
-        csel = rng.integers(0, len(cts), m)
-        msel = rng.choice(len(meths), size=m, p=np.asarray(mw) / np.sum(mw))
-        usel = rng.choice(uas, size=m)
-        depth = rng.integers(1, 4, m)
+        tsel = rng.choice(N_TEMPLATES, size=m, p=tz)
         hour_f[idx] = rng.normal(peak, hsd, m)
-        for j, i in enumerate(idx):
-            host[i], ctype[i], method[i], ua[i] = hs[hsel[j]], cts[csel[j]], meths[msel[j]], _UAS[usel[j]]
-            path[i] = "/" + "/".join(f"p{rng.integers(0, 50)}" for _ in range(depth[j])) + ".html"
-    status = np.where(rng.random(n) < 0.92, 200, rng.choice([304, 404, 302, 500], size=n))
+        status[idx] = t_st[tsel]
+        for j, i in enumerate(idx.tolist()):
+            t = tsel[j]
+            host[i], ctype[i], method[i] = hs[t_host[t]], cts[t_ct[t]], meths[t_m[t]]
+            ua[i] = _UAS[uas[(cli[i] * 7 + k) % len(uas)]]
+            path[i] = t_path[t]
     if wide_vocab > 0:
-        # long-tail rows come from a codebook of ~n/20 request behaviours (host, method, agent,
-        # content type, URI, status, hour), drawn uniformly: a wide vocabulary whose words recur
-        # (~10 rows per behaviour) instead of a day-unique word on every other
-        # long-tail row (see synth.dns)
+        # long-tail rows come from a codebook of ~n/100 request behaviours (host, method, agent,
+        # content type, URI, status, hour); every client owns ⌈its long-tail rows / 8⌉ of them
+        # (dealt round-robin, so each behaviour has several owners) and repeats them, as
+        # synth.flow's realistic day does: a wide vocabulary whose words are common in the
+        # documents that carry them
         wide = np.nonzero(rng.random(n) < wide_vocab)[0]
         wide = wide[~np.isin(wide, anomaly_rows)]
         crng = np.random.default_rng([seed, 0xC0DE])
-        W = max(200, n // 20)
+        W = max(200, n // 100)
         cb = _wide_rows(crng, W)
         cb_h = crng.uniform(0, 24, size=W)
-        b = rng.integers(0, W, wide.size)
+        c_w = cli[wide]
+        slots = np.clip(-(-np.bincount(c_w, minlength=n_clients) // 8), 1, 64)
+        first = np.concatenate([[0], np.cumsum(slots)[:-1]])
+        orng = np.random.default_rng([seed, 0x0515])
+        n_sl = int(slots.sum())
+        own = np.concatenate([orng.permutation(W) for _ in range(-(-n_sl // W))])[:n_sl]
+        own = own[orng.permutation(n_sl)]
+        b = own[first[c_w] + (rng.random(wide.size) * slots[c_w]).astype(np.int64)]
         hour_f[wide] = cb_h[b]
         for i, j in zip(wide.tolist(), b.tolist()):
             host[i], method[i], ua[i], ctype[i], path[i], status[i] = cb[j]
     hour = np.mod(np.floor(hour_f), 24).astype(int)
     quiet = np.argsort(w)[: max(1, n_clients // 10)]
     # individually rare behaviours (see synth.dns): varying method, content type, URI shape, hour
-    a_methods = ["POST", "PUT", "CONNECT", "DELETE", "PROPFIND", "OPTIONS"]
+    a_methods = _ANOMALY_METHODS
     a_ctypes = ["application/x-www-form-urlencoded", "application/octet-stream", "application/x-msdownload",
                 "application/x-sh", "text/x-python"]
     for i in anomaly_rows:

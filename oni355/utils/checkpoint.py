@@ -62,6 +62,10 @@ class Checkpointer:
             "z": z,
             "likelihoods": list(model.likelihoods),
         }
+        avg = model.average_state() if hasattr(model, "average_state") else None
+        if avg is not None:
+            # inside the posterior-averaging window: the samples so far (this rank's layout)
+            payload["avg"] = avg
         name = f"ckpt_s{model.sweeps_done}_r{self.rank}of{self.world}.pt"
         path = os.path.join(self.dir, name)
         torch.save(payload, path + ".tmp")
@@ -176,6 +180,18 @@ class Checkpointer:
             miss = int(my_keys[torch.nonzero(~found).flatten()[0]])
             raise ValueError(f"checkpoint does not match corpus (doc key {miss} missing)")
         model.load_canonical_z(z, sweep)
+        win = model.average_window if hasattr(model, "average_window") else None
+        if win is not None and sweep >= win[0]:
+            # resumed inside the posterior-averaging window: the samples taken before the
+            # checkpoint are in this rank's own shard, valid for the same corpus layout only
+            own = os.path.join(self.dir, f"ckpt_s{sweep}_r{self.rank}of{man['world']}.pt")
+            d = torch.load(own, weights_only=True) if os.path.exists(own) else {}
+            if man["world"] != self.world or "avg" not in d or not torch.equal(
+                    d["doc_keys"].to(torch.int64), c.doc_keys.cpu().to(torch.int64)):
+                raise ValueError(f"checkpoint at sweep {sweep} is inside the posterior-averaging window "
+                                 f"{win}: resume it with the world size it was written with "
+                                 f"({man['world']}), or set ONI_POST_SAMPLES=1")
+            model.load_average_state(d["avg"])
         return sweep
 
 

@@ -76,11 +76,17 @@ def test_allreduce_bench_gloo_two_ranks():
 
 def test_combined_bench_cpu_and_sizing():
     from oni355.utils import sizing
-    out = _run([sys.executable, "bench/combined.py", "--device", "cpu", "--flows-per-gpu", "2000", "--dns-per-gpu",
-                "1000", "--proxy-per-gpu", "1000", "--steps", "1", "--warmup", "1", "--topics", "50"])
+    small = ["--device", "cpu", "--flows-per-gpu", "2000", "--dns-per-gpu", "1000", "--proxy-per-gpu", "1000",
+             "--steps", "1", "--warmup", "1", "--topics", "50"]
+    out = _run([sys.executable, "bench/combined.py", *small, "--mode", "sweep"])
     assert out["value"] > 0 and set(out["ms_per_sweep_by_model"]) == {"flow", "dns", "proxy"}
     assert out["tokens"] == {"flow": 4000, "dns": 1000, "proxy": 1000}
     assert out["projection_1B_events_8gpu"]["fits_288GB"] is True
+    # day mode (the default): every source's whole day per step, result rows written
+    day = _run([sys.executable, "bench/combined.py", *small, "--sweeps", "4", "--maxresults", "50"])
+    assert day["value"] > 0 and set(day["day_s_by_model"]) == {"flow", "dns", "proxy"}
+    assert {k: v["tokens"] for k, v in day["model_stats"].items()} == {"flow": 4000, "dns": 1000, "proxy": 1000}
+    assert all(v["rows"] == 50 for v in day["model_stats"].values())
     # the planner grows with every input and flags what cannot fit
     a = sizing.plan("flow", 10**6, 20, 10**4, 10**4)
     b = sizing.plan("flow", 2 * 10**6, 20, 10**4, 10**4)

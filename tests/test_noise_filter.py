@@ -44,9 +44,10 @@ def _key(header, row, cols):
 
 
 def _run_loop(tmp_path, source, device):
-    n, top = _SIZES[source], 100
+    # every event is ranked (maxresults = the day): the test follows ranks, not top-N membership
+    n, top = _SIZES[source], 300
     lp = str(tmp_path / "lp")
-    args = ["20160708", source, "1.0", str(top), "--synthetic", str(n), "--device", device, "--sweeps", "30",
+    args = ["20160708", source, "1.0", str(n), "--synthetic", str(n), "--device", device, "--sweeps", "30",
             "--lpath", lp, "--quiet", "--config", str(tmp_path / "none.conf")]
     if source == "dns":
         args += ["--topics", "50"]
@@ -57,7 +58,7 @@ def _run_loop(tmp_path, source, device):
     cols = _KEY_COLS[source]
     planted = {tuple(int(np.asarray(day.cols[c])[i]) for c in cols) for i in day.anomaly_rows}
     keys = [_key(header, r, cols) for r in rows]
-    hits = [i for i, k in enumerate(keys) if k in planted]
+    hits = [i for i, k in enumerate(keys[:top]) if k in planted]
     assert hits, "no planted anomaly in the top-N"
     pos = hits[0]
     target = keys[pos]
@@ -69,18 +70,20 @@ def _run_loop(tmp_path, source, device):
     assert ml.main(args) == 0
     _, rows2 = _rows(res)
     keys2 = [_key(header, r, cols) for r in rows2]
-    new_pos = keys2.index(target) if target in keys2 else None
-    # control: the planted anomalies nobody marked stay suspicious (and the event keys still match)
+    assert sorted(keys2) == sorted(keys)  # the same events, re-ranked
+    new_pos = keys2.index(target)
+    # control: the planted anomalies nobody marked stay suspicious -- their median rank moves by
+    # less than 3x (the 1000 feedback tokens reshape one topic, not the whole model)
     others = [k for k in keys if k in planted and k != target]
-    if others:
-        kept = sum(k in keys2 for k in others)
-        assert kept >= 0.5 * len(others), (kept, len(others))
-    return pos, new_pos, len(rows2)
+    before = np.median([keys.index(k) + 1 for k in others])
+    after = np.median([keys2.index(k) + 1 for k in others])
+    assert after <= 3 * before + top // 10, (before, after)
+    return pos, new_pos, top
 
 
 def _check(pos, new_pos, top):
     # rank 0-based: "drops by >= 10x" on 1-based ranks, or the event left the top-N
-    assert new_pos is None or (new_pos + 1) >= 10 * (pos + 1), (pos, new_pos, top)
+    assert (new_pos + 1) >= 10 * (pos + 1) or new_pos >= top, (pos, new_pos, top)
 
 
 @pytest.mark.parametrize("source", ["flow", "dns", "proxy"])

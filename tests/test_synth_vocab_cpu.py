@@ -18,13 +18,15 @@ def _words_proxy(wide, n=100_000):
 
 
 def test_wide_vocab_grows_dns_and_proxy_vocabularies():
-    """The long tail is a codebook of recurring behaviours: the vocabulary grows several-fold
-    while day-unique words stay a small share of the rows (the planted rows stay findable)."""
-    for fn, grow in ((_words_dns, 2.0), (_words_proxy, 1.1)):
+    """The long tail is a codebook of recurring, client-owned behaviours: the vocabulary grows
+    while day-unique words stay a tiny share of the rows (the planted rows stay findable). DNS and
+    proxy words are quantised features (quintiles, deciles, codes), so their vocabularies grow
+    less than the flow day's port-keyed one (100k rows: DNS 2.2k -> 2.5k, proxy 1.5k -> 2.3k)."""
+    for fn, grow in ((_words_dns, 1.1), (_words_proxy, 1.3)):
         base, wide = fn(0.0), fn(0.5)
         assert torch.unique(wide).numel() > grow * torch.unique(base).numel()
         _, cnt = torch.unique(wide, return_counts=True)
-        assert int((cnt == 1).sum()) < 0.02 * wide.numel()
+        assert int((cnt == 1).sum()) < 0.005 * wide.numel()
 
 
 def test_wide_vocab_keeps_anomalies_and_shapes():
