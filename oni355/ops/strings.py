@@ -34,11 +34,14 @@ _tables: dict = {}
 
 
 def _dev_psl(device, rules):
-    key = (str(device), id(rules))
-    if key not in _tables:
-        _tables[key] = (torch.from_numpy(rules.rule_set.table.view(np.int64)).to(device),
-                        torch.from_numpy(rules.exc_set.table.view(np.int64)).to(device))
-    return _tables[key]
+    """The rule and exception hash tables of ``rules`` on ``device``, cached on the rules object
+    itself (an id()-keyed module cache could hand a new object the tables of a collected one)."""
+    cache = rules.__dict__.setdefault("_dev_tables", {})
+    key = str(device)
+    if key not in cache:
+        cache[key] = (torch.from_numpy(rules.rule_set.table.view(np.int64)).to(device),
+                      torch.from_numpy(rules.exc_set.table.view(np.int64)).to(device))
+    return cache[key]
 
 
 def _dev_tables(device):

@@ -121,7 +121,7 @@ class Comm:
         n = torch.full((1,), t.shape[0], dtype=torch.int64, device=self.device)
         ns = [torch.zeros_like(n) for _ in range(self.world)]
         dist.all_gather(ns, n, group=self.group)
-        sizes = [int(x.item()) for x in ns]
+        sizes = torch.cat(ns).tolist()  # one device read for all ranks' sizes
         m = max(sizes)
         pad = torch.zeros((m, *t.shape[1:]), dtype=t.dtype, device=self.device)
         pad[: t.shape[0]] = t.to(self.device)

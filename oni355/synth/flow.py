@@ -86,14 +86,15 @@ def generate_flows(n: int, seed: int = 7, n_hosts: int | None = None, n_profiles
                    alpha_true: float = 0.08, zipf_a: float = 1.15, n_anomalies: int | None = None,
                    date=(2016, 7, 8), rank: int = 0, wide_vocab: bool = False, ipv6_frac: float = 0.0,
                    anomaly_hosts: str = "active", anomaly_kind: str = "rare-service",
-                   support_min: float = 0.02) -> FlowDay:
+                   support_min: float = 0.02, lt_codebook: float = 0.01) -> FlowDay:
     """Generate ``n`` flows. ``rank`` offsets the RNG stream (weak-scaling shards of one day).
 
     ``wide_vocab``: a realistic-vocabulary day (SURVEY.md §7.5 sizing, V ≈ 1e5–1e6 flow words):
     half of the flows repeat one of their host's long-tail behaviours (a service port
     anywhere in 1..1024 with its own hour, volume and server) instead of a profile flow, and 20 %
     of the flows are server-to-server (both ports low / both high), so every (port, time, bytes,
-    packets, direction) bin fills."""
+    packets, direction) bin fills. ``lt_codebook``: long-tail behaviours per flow (codebook size
+    n · lt_codebook; 0.01 → V ≈ 1.7e5 flow words at 12.5M flows, 0.04 → V ≈ 4-5e5)."""
     rng = np.random.default_rng([seed, rank])
     n_profiles = min(n_profiles, len(_PROFILES))
     prof = _PROFILES[:n_profiles]
@@ -156,7 +157,7 @@ def generate_flows(n: int, seed: int = 7, n_hosts: int | None = None, n_profiles
         # profiles/r3/recall_sweep_codebook.jsonl). The anomalies' rare services are not in the pool.
         lt = np.nonzero(rng.random(n) < 0.5)[0]
         crng = np.random.default_rng([seed, 0xC0DE])
-        W = max(1000, n // 100)
+        W = max(1000, int(n * lt_codebook))
         pool = np.setdiff1d(np.arange(1, 1025), _ANOMALY_PORTS)
         cb_port = pool[crng.integers(0, pool.size, W)]
         cb_hour = crng.uniform(0.0, 24.0, W)

@@ -29,6 +29,7 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--chunk-len", type=int, default=0)
     ap.add_argument("--anomaly-kind", default=None, help="dns / proxy generators: rare | rare-active | offprofile")
+    ap.add_argument("--lt-codebook", type=float, default=0.01, help="flow --wide: long-tail behaviours per flow")
     a = ap.parse_args()
     import numpy as np
     K = a.topics or (50 if a.source == "dns" else 20)
@@ -36,7 +37,7 @@ def main() -> int:
     if a.source == "flow":
         from oni355.pipeline.flow import run_flow
         from oni355.synth.flow import generate_flows
-        day = generate_flows(a.n, seed=a.seed, n_hosts=max(64, a.n // 25), wide_vocab=a.wide)
+        day = generate_flows(a.n, seed=a.seed, n_hosts=max(64, a.n // 25), wide_vocab=a.wide, lt_codebook=a.lt_codebook)
         res = run_flow(day.cols, K=K, sweeps=a.sweeps, maxresults=a.n, device=a.device, chunk_len=a.chunk_len)
     elif a.source == "dns":
         from oni355.pipeline.dns import run_dns
@@ -56,6 +57,8 @@ def main() -> int:
     rank = {int(r): i for i, r in enumerate(res.rows)}
     ranks = np.array(sorted(rank.get(int(x), a.n) for x in day.anomaly_rows))
     out = {"source": a.source, "n": a.n, "wide": a.wide, "kind": a.anomaly_kind, "K": K, "sweeps": a.sweeps,
+           "lt_codebook": a.lt_codebook if a.source == "flow" and a.wide else None,
+           "ms_per_sweep": round(res.timings.get("train_dev_s", res.timings.get("train_s", 0)) / a.sweeps * 1e3, 4),
            "vocab": int(res.lda.vocab.numel()), "anomalies": int(ranks.size),
            "recall_topN": float(np.mean(ranks < a.maxresults)), "maxresults": a.maxresults,
            "rank_p50": int(np.median(ranks)), "rank_max": int(ranks.max()), "ranks_head": ranks[:20].tolist(),
