@@ -999,8 +999,10 @@ __device__ __forceinline__ float group_scan_dpp(float x, int g) {
 // AIR: the LDS rows hold n_dk + α instead of n_dk (the host sets it only when every n + α of this
 // corpus is exact in f32, e.g. α = 50/K ∈ {2.5, 1, 0.5} with documents below 2^22 tokens), which
 // drops the per-topic "+ α" from the inner product -- same values, bitwise the same draws.
-template <int G, int KP, int MODE, int QP, bool AIR = false>
-__global__ __launch_bounds__(kBlock) void k_gibbs_ldsg(const OniGibbs a) {
+// OCC: minimum waves per SIMD the register allocation must allow (1 = the compiler's default,
+// which lands at 98 VGPRs / 4 waves for (4, 28); 5 = 96 VGPRs, the LDS limit of 30.4 KB blocks).
+template <int G, int KP, int MODE, int QP, bool AIR = false, int OCC = 1>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void k_gibbs_ldsg(const OniGibbs a) {
   static_assert(G > 1, "G = 1 uses k_gibbs_lds");
   constexpr int S = oni::kWave / G;
   constexpr int KS = G * KP;
@@ -1176,6 +1178,8 @@ int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s)
   // in MODE 0/1/3/4; the caller guarantees the slice bound (slice_len[0] is the longest)
   if (qpf == 7 && (G != 1 || init || mode == 2)) qpf = 4;
   if (qpf == 8 && (G != 1 || init || mode == 2)) qpf = G == 1 ? 6 : 4;  // 8 = k_gibbs_q2 + DZ
+  // qpf 9 = k_gibbs_ldsg with a 5-wave register budget (G > 1, recount / wdelta sweeps)
+  if (qpf == 9 && (G == 1 || init || (mode != 0 && mode != 4))) qpf = 2;
   const unsigned grid = (unsigned)((a.n_slices + kWavesPerBlock - 1) / kWavesPerBlock);
   if (grid == 0) return 0;
   if constexpr (G == 1) {
@@ -1214,6 +1218,19 @@ int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s)
     if (mode == 0) k_gibbs<G, KP, true, 0, false><<<grid, kBlock, 0, s>>>(a);
     else k_gibbs<G, KP, true, 1, false><<<grid, kBlock, 0, s>>>(a);
     return (int)hipGetLastError();
+  }
+  if constexpr (G > 1) {
+    if (qpf == 9) {
+      if (mode == 4) {
+        if (a.flags & 1) k_gibbs_ldsg<G, KP, 4, 0, true, 5><<<grid, kBlock, 0, s>>>(a);
+        else k_gibbs_ldsg<G, KP, 4, 0, false, 5><<<grid, kBlock, 0, s>>>(a);
+      } else if (a.flags & 1) {
+        k_gibbs_ldsg<G, KP, 0, 0, true, 5><<<grid, kBlock, 0, s>>>(a);
+      } else {
+        k_gibbs_ldsg<G, KP, 0, 0, false, 5><<<grid, kBlock, 0, s>>>(a);
+      }
+      return (int)hipGetLastError();
+    }
   }
   if (mode == 4) {  // word-sorted change bitmap
     if constexpr (G > 1) {

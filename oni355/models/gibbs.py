@@ -31,7 +31,7 @@ NK_REP = 32
 # X01 payload packing pays only once the all-reduce is bandwidth-bound (see GibbsLDA._x01_wanted)
 X01_PACK_MIN_BYTES = 4 << 20
 DZ_MAX_LEN = 128  # kDzMaxLen (csrc/kernels/gibbs_sampler.h)
-SAMPLERS = {"pp": 1, "plain": 0, "lds": 2, "qpf": 4, "ldsq": 5, "q2": 6, "dz": 7, "q2dz": 8}  # -> oni_gibbs_launch qpf argument
+SAMPLERS = {"pp": 1, "plain": 0, "lds": 2, "qpf": 4, "ldsq": 5, "q2": 6, "dz": 7, "q2dz": 8, "lds5": 9}  # -> oni_gibbs_launch qpf argument
 
 
 @dataclass
@@ -186,12 +186,12 @@ class GibbsLDA:
             raise ValueError(f"unknown sampler {cfg.sampler}")
         self.qpf = SAMPLERS[cfg.sampler] if cfg.sampler != "auto" else (SAMPLERS["qpf"] if self.G == 1 else
                                                                          SAMPLERS["lds"])
-        if self.qpf == 5 and self.G == 1:
+        if self.qpf in (5, 9) and self.G == 1:
             self.qpf = 2
         if self.qpf in (7, 8) and (self.G != 1 or corpus.L > DZ_MAX_LEN):
             self.qpf = 4  # "dz" stages one slice's topics in LDS: one-lane units, chunks ≤ 128 tokens  # "ldsq" (LDS counts + q-row prefetch) is the multi-lane variant; G = 1 has "lds"
         self._air = False  # n + α LDS rows (LDS samplers only)
-        if self.qpf in (2, 5):
+        if self.qpf in (2, 5, 9):
             max_len = corpus.max_doc_len()  # one device read, only the LDS samplers need it
             if max_len >= (1 << 24):
                 self.qpf = 1  # LDS rows hold counts as f32: exact below 2^24

@@ -309,7 +309,7 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
     old | new << 8 in ``zz_w`` (int16, word-sorted) for :func:`wdelta_recount`.
     ``prefetch_q`` (sampler variant) 0: register sampler, q row loaded on a word change; 1: ping-pong
     register sampler; 4: one-step q prefetch; 2: LDS-staged doc counts with fma numerics (k_gibbs_lds
-    for G = 1, k_gibbs_ldsg for G > 1); 5: as 2 with a one-step q-row prefetch (G > 1).
+    for G = 1, k_gibbs_ldsg for G > 1); 5: as 2 with a one-step q-row prefetch (G > 1); 9: as 2 with a 5-wave register budget (G > 1).
     """
     atomic = mode == 1
     s0, s1 = spec.split_seed(seed)
@@ -332,7 +332,7 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
             npst["dnwk"] = np.zeros_like(npst["dnwk"])  # discarded: recount rebuilds n_wk
         spec.gibbs_pass(npst, G, KP, K, alpha, s0, s1, init,
                         int(host_sweep if host_sweep is not None else sweep_ctr.item()), chunk_len.numpy(),
-                        fma=(int(prefetch_q) in (2, 5) and not init))
+                        fma=(int(prefetch_q) in (2, 5, 9) and not init))
         if mode == 3:
             valid = wpos >= 0
             z_w[wpos[valid].long()] = st["tok_z"][valid]

@@ -92,7 +92,9 @@ def _toy_tokens(n_docs, V, seed, heavy=True):
                                     (20, "wdelta+dz"), (20, "recount+dz"), (20, "atomic+dz"), (20, "dual+dz"),
                                     (20, "delta+dz"), (7, "wdelta+dz"), (32, "wdelta+dz"), (32, "recount+dz"),
                                     (50, "wdelta+dz"), (20, "wdelta+q2dz"), (20, "recount+q2dz"), (20, "atomic+q2dz"),
-                                    (20, "dual+q2dz"), (7, "wdelta+q2dz")])
+                                    (20, "dual+q2dz"), (7, "wdelta+q2dz"), (100, "wdelta+lds5"),
+                                    (100, "recount+lds5"), (50, "recount+lds5"), (50, "wdelta+lds5"),
+                                    (100, "dual+lds5")])
 def test_gibbs_bitwise_vs_oracle(gpu, K, mode):
     tdoc, tword, keys = _toy_tokens(300, 400, K)
     G, KP = ops.choose_tiling(K)
@@ -103,10 +105,10 @@ def test_gibbs_bitwise_vs_oracle(gpu, K, mode):
     sampler = mode.split("+")[1] if "+" in mode else "auto"
     mg = GibbsLDA(cg, GibbsConfig(K=K, seed=1234, use_graph=False, count_mode=mode.split("+")[0], sampler=sampler))
     if sampler != "auto":
-        assert (mg.qpf in (2, 5)) == (sampler in ("lds", "ldsq"))
+        assert (mg.qpf in (2, 5, 9)) == (sampler in ("lds", "ldsq", "lds5"))
     # the oracle replays the numerics the device sampler uses (fma chain for the LDS samplers)
     mc = GibbsLDA(cc, GibbsConfig(K=K, seed=1234, use_graph=False, count_mode="atomic",
-                                  sampler="lds" if mg.qpf in (2, 5) else "plain"))
+                                  sampler="lds" if mg.qpf in (2, 5, 9) else "plain"))
     if mode.startswith("wdelta"):
         assert mg.mode == 4
     mc.initialize()
