@@ -31,7 +31,8 @@ NK_REP = 32
 # X01 payload packing pays only once the all-reduce is bandwidth-bound (see GibbsLDA._x01_wanted)
 X01_PACK_MIN_BYTES = 4 << 20
 DZ_MAX_LEN = 128  # kDzMaxLen (csrc/kernels/gibbs_sampler.h)
-SAMPLERS = {"pp": 1, "plain": 0, "lds": 2, "qpf": 4, "ldsq": 5, "q2": 6, "dz": 7, "q2dz": 8, "lds5": 9}  # -> oni_gibbs_launch qpf argument
+SAMPLERS = {"pp": 1, "plain": 0, "lds": 2, "qpf": 4, "ldsq": 5, "q2": 6, "dz": 7, "q2dz": 8, "lds5": 9,
+            "ws": 10, "wsa": 10}  # -> oni_gibbs_launch qpf argument
 
 
 @dataclass
@@ -186,15 +187,26 @@ class GibbsLDA:
             raise ValueError(f"unknown sampler {cfg.sampler}")
         self.qpf = SAMPLERS[cfg.sampler] if cfg.sampler != "auto" else (SAMPLERS["qpf"] if self.G == 1 else
                                                                          SAMPLERS["lds"])
+        # word-sparse sampler (k_gibbs_ws): "ws" on every sweep; "wsa" only in the sweeps after the
+        # auto count mode's switch (the word lists are short once topics have settled; the early
+        # sweeps keep the dense sampler)
+        self.ws = None
+        if cfg.sampler in ("ws", "wsa"):
+            if cfg.K > 240:
+                raise ValueError("the word-sparse sampler supports K <= 240")
+            self.ws = "delta" if (cfg.sampler == "wsa" and self.auto) else "always"
+            self.qpf = SAMPLERS["qpf"] if self.G == 1 else SAMPLERS["lds"]
+        self._ws_tabs = ops.ws_alloc(self.V, self.KS, dev) if self.ws else None
         if self.qpf in (5, 9) and self.G == 1:
             self.qpf = 2
         if self.qpf in (7, 8) and (self.G != 1 or corpus.L > DZ_MAX_LEN):
             self.qpf = 4  # "dz" stages one slice's topics in LDS: one-lane units, chunks ≤ 128 tokens  # "ldsq" (LDS counts + q-row prefetch) is the multi-lane variant; G = 1 has "lds"
         self._air = False  # n + α LDS rows (LDS samplers only)
-        if self.qpf in (2, 5, 9):
+        if self.qpf in (2, 5, 9) or self.ws:
             max_len = corpus.max_doc_len()  # one device read, only the LDS samplers need it
             if max_len >= (1 << 24):
                 self.qpf = 1  # LDS rows hold counts as f32: exact below 2^24
+                self.ws, self._ws_tabs = None, None
             else:
                 self._air = _alpha_in_row_exact(self.alpha, max_len)
         self.a = 0  # ndk parity
@@ -408,11 +420,16 @@ class GibbsLDA:
             self._ensure_zw()
         # long (chunked) documents add their Δn_dk into ndk[1-a] rows that hold a copy of ndk[a]:
         # every apply -- the previous sweep's, or _prime()'s after init / resume -- seeds that copy
+        use_ws = self.ws == "always" or (self.ws == "delta" and mode == self.mode)
+        if use_ws:
+            # the word side is the sweep-start snapshot: its sparse tables are built once per sweep
+            ops.ws_tables(self.nwk, self.nk[self.cn], self.K, self.beta, self.vbeta, self._ws_tabs)
         ops.gibbs_pass(self._state(False), self.G, self.KP, self.K, self.alpha, self.cfg.seed, False,
                        self.sweep_ctr, c.chunk_len, host_sweep=self.sweeps_done + 1, mode=mode,
-                       prefetch_q=self.qpf,
+                       prefetch_q=ops.WS_SAMPLER if use_ws else self.qpf,
                        chg_mask=self.wbits if mode == 4 else getattr(self, "chg_mask", None), wpos=c.wpos,
-                       z_w=getattr(self, "z_w", None), zz_w=getattr(self, "zz_w", None), alpha_in_row=self._air)
+                       z_w=getattr(self, "z_w", None), zz_w=getattr(self, "zz_w", None), alpha_in_row=self._air,
+                       ws_tabs=self._ws_tabs if use_ws else None, debug_flags=getattr(self, "_ablate_flags", 0))
         head = self.dn[self.b][: self.V * self.KS].view(self.V, self.KS)
         if mode == 4:
             # dn[b] head := Δn_wk of the tokens marked in the word-sorted change bitmap

@@ -299,7 +299,7 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
                chunk_len: torch.Tensor, host_sweep: int | None = None, mode: int = 1,
                prefetch_q: bool | int = False, chg_mask: torch.Tensor | None = None, wpos: torch.Tensor | None = None,
                z_w: torch.Tensor | None = None, zz_w: torch.Tensor | None = None,
-               alpha_in_row: bool = False) -> None:
+               alpha_in_row: bool = False, ws_tabs: dict | None = None, debug_flags: int = 0) -> None:
     """Launch one init/sweep pass. ``st`` holds the OniGibbs tensors (see csrc/kernels/gibbs.hip).
 
     ``mode`` 1: accumulate Δn_wk with per-token atomics; 0: the caller rebuilds n_wk with
@@ -309,8 +309,13 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
     old | new << 8 in ``zz_w`` (int16, word-sorted) for :func:`wdelta_recount`.
     ``prefetch_q`` (sampler variant) 0: register sampler, q row loaded on a word change; 1: ping-pong
     register sampler; 4: one-step q prefetch; 2: LDS-staged doc counts with fma numerics (k_gibbs_lds
-    for G = 1, k_gibbs_ldsg for G > 1); 5: as 2 with a one-step q-row prefetch (G > 1); 9: as 2 with a 5-wave register budget (G > 1).
+    for G = 1, k_gibbs_ldsg for G > 1); 5: as 2 with a one-step q-row prefetch (G > 1); 9: as 2 with a
+    5-wave register budget (G > 1); 10: the word-sparse sampler k_gibbs_ws (sweeps only; ``ws_tabs``
+    from :func:`ws_tables` of the sweep-start counts; any corpus unit width G).
     """
+    ws = int(prefetch_q) == WS_SAMPLER and not init
+    if ws and ws_tabs is None:
+        raise ValueError("the word-sparse sampler needs its per-sweep tables (ws_tables)")
     atomic = mode == 1
     s0, s1 = spec.split_seed(seed)
     KS = G * KP
@@ -330,9 +335,13 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
         npst["dnk"] = npst["dnk"][:KS]  # replica 0 (the sum over replicas is what counts)
         if not atomic:
             npst["dnwk"] = np.zeros_like(npst["dnwk"])  # discarded: recount rebuilds n_wk
-        spec.gibbs_pass(npst, G, KP, K, alpha, s0, s1, init,
-                        int(host_sweep if host_sweep is not None else sweep_ctr.item()), chunk_len.numpy(),
-                        fma=(int(prefetch_q) in (2, 5, 9) and not init))
+        sweep_no = int(host_sweep if host_sweep is not None else sweep_ctr.item())
+        if ws:
+            spec.gibbs_pass_ws(npst, G, K, alpha, s0, s1, sweep_no, chunk_len.numpy(),
+                               tuple(ws_tabs[k].numpy() for k in ("llen", "lk", "la", "b")))
+        else:
+            spec.gibbs_pass(npst, G, KP, K, alpha, s0, s1, init, sweep_no, chunk_len.numpy(),
+                            fma=(int(prefetch_q) in (2, 5, 9) and not init))
         if mode == 3:
             valid = wpos >= 0
             z_w[wpos[valid].long()] = st["tok_z"][valid]
@@ -371,10 +380,45 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
     a.n_slices, a.K, a.KS, a.alpha, a.seed0, a.seed1 = n_slices, K, KS, float(alpha), s0, s1
     a.nk_rep = nk_rep
     # the caller vouches that n + α is exact in f32 for every doc-topic count of this corpus
-    a.flags = 1 if alpha_in_row else 0
+    a.flags = (1 if alpha_in_row else 0) | (int(debug_flags) & ~0xFF)
+    if ws:
+        t = _lib.OniWsTabs()
+        t.llen, t.lk, t.la, t.b = (_lib.ptr(ws_tabs[k]) for k in ("llen", "lk", "la", "b"))
+        if ws_tabs.get("stats") is not None:  # diagnostics: see tools/ws_probe.py
+            t.stats = _lib.ptr(ws_tabs["stats"])
+        _lib.check(_lib.lib().oni_gibbs_ws_launch(C.byref(a), C.byref(t), G, int(mode), _lib.stream()),
+                   "oni_gibbs_ws_launch")
+        return
     _lib.check(_lib.lib().oni_gibbs_launch(C.byref(a), G, KP, 1 if init else 0, int(mode),
                                            int(prefetch_q), _lib.stream()),
                "oni_gibbs_launch")
+
+
+WS_SAMPLER = 10  # prefetch_q code of the word-sparse sampler (k_gibbs_ws)
+
+
+def ws_alloc(V: int, KS: int, device) -> dict:
+    """Device (or CPU) tables of the word-sparse sampler, rebuilt every sweep by :func:`ws_tables`."""
+    return dict(llen=torch.zeros(max(V, 1), dtype=torch.int32, device=device),
+                lk=torch.zeros(max(V, 1), KS, dtype=torch.uint8, device=device),
+                la=torch.zeros(max(V, 1), KS, dtype=torch.float32, device=device),
+                b=torch.zeros(KS, dtype=torch.float32, device=device))
+
+
+def ws_tables(nwk: torch.Tensor, nk: torch.Tensor, K: int, beta: float, vbeta: float, tabs: dict) -> None:
+    """Word-sparse sampler tables from the sweep-start n_wk / n_k (k_ws_tables): per word the topics
+    with n_wk > 0 (ascending) and a_wk = n_wk/(n_k + Vβ); b_k = β/(n_k + Vβ)."""
+    V, KS = nwk.shape
+    if not _is_dev(nwk):
+        llen, lk, la, b = spec.ws_tables(nwk.numpy(), nk.numpy(), K, beta, vbeta)
+        tabs["llen"][:V].copy_(torch.from_numpy(llen))
+        tabs["lk"][:V].copy_(torch.from_numpy(lk))
+        tabs["la"][:V].copy_(torch.from_numpy(la))
+        tabs["b"].copy_(torch.from_numpy(b))
+        return
+    _lib.check(_lib.lib().oni_ws_tables(_lib.ptr(nwk), _lib.ptr(nk), V, K, KS, float(beta), float(vbeta),
+                                        *(_lib.ptr(tabs[k]) for k in ("llen", "lk", "la", "b")), _lib.stream()),
+               "oni_ws_tables")
 
 
 def delta_recount(wslot, tile_wlo, tile_whi, chg_mask, tok_word, tok_z, tok_zprev, dnwk_out, KS: int, G: int) -> None:
@@ -640,3 +684,17 @@ def select_below(score_t: torch.Tensor, tol: float, bmax: int, cap: int):
     if k > cap:
         raise RuntimeError(f"select_below overflow: {k} > cap {cap}")
     return out_i[:k], out_s[:k]
+
+
+def widen_pair(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """[a ‖ b] as non-negative int64 for two int32 tensors holding u32 bits (k_widen_pair: one pass
+    instead of cat + int64 conversion + mask)."""
+    n = a.numel()
+    if b.numel() != n or a.dtype != torch.int32 or b.dtype != torch.int32:
+        raise ValueError("widen_pair: two int32 tensors of one length")
+    if not _is_dev(a):
+        return torch.cat([a, b]).to(torch.int64) & 0xFFFFFFFF
+    out = torch.empty(2 * n, dtype=torch.int64, device=a.device)
+    _lib.check(_lib.lib().oni_widen_pair(_lib.ptr(a.contiguous()), _lib.ptr(b.contiguous()), n, _lib.ptr(out),
+                                         _lib.stream()), "oni_widen_pair")
+    return out

@@ -38,6 +38,12 @@ class OniGibbs(C.Structure):
     ]
 
 
+class OniWsTabs(C.Structure):
+    """Mirror of ``struct OniWsTabs`` in csrc/kernels/gibbs_ws.hip (word-sparse sampler tables)."""
+
+    _fields_ = [("llen", vp), ("lk", vp), ("la", vp), ("b", vp), ("stats", vp)]
+
+
 _SIGS = {
     "oni_radix_hist": [vp, i64, C.c_int, C.c_int, vp, C.c_int, u32, vp, vp],
     "oni_f32_keys": [vp, i64, vp, vp],
@@ -49,6 +55,9 @@ _SIGS = {
     "oni_sell_perm_z": [vp, vp, vp, i64, C.c_int, vp, vp, vp, vp, C.c_int, vp],
     "oni_gibbs_launch": [C.POINTER(OniGibbs), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp],
     "oni_gibbs_sizeof_args": [],
+    "oni_gibbs_ws_launch": [C.POINTER(OniGibbs), C.POINTER(OniWsTabs), C.c_int, C.c_int, vp],
+    "oni_ws_tables": [vp, vp, i64, C.c_int, C.c_int, f32, f32, vp, vp, vp, vp, vp],
+    "oni_widen_pair": [vp, vp, i64, vp, vp],
     "oni_gibbs_apply": [vp, vp, vp, vp, vp, vp, i64, C.c_int, C.c_int, f32, f32, vp, C.c_int, C.c_int, C.c_int,
                         vp, vp, vp, i64, vp],
     "oni_recount": [vp, vp, vp, i64, vp, C.c_int, C.c_int, C.c_int, vp],

@@ -220,8 +220,8 @@ def run_flow(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxre
         sw, dw = wordify(d, cuts)
     with timer.stage("vocab"):
         n = d["sip"].numel()
-        doc_keys = common.u32_to_i64(torch.cat([d["sip"], d["dip"]]))
-        word_keys = common.u32_to_i64(torch.cat([sw, dw]))
+        doc_keys = ops.widen_pair(d["sip"], d["dip"])
+        word_keys = ops.widen_pair(sw, dw)
         weights = None
         fb = feedback_tokens(feedback, cuts, device, dupfactor)
         if fb is not None:

@@ -318,6 +318,97 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed0: int, seed
     st["dnk"] += d[live].sum(axis=0).astype(np.int32)
 
 
+def ws_tables(nwk: np.ndarray, nk: np.ndarray, K: int, beta: float, vbeta: float):
+    """Per-sweep tables of the word-sparse sampler (k_ws_tables): for every word the topics with
+    n_wk > 0 (ascending) and a_wk = n_wk / (n_k + Vβ), plus b_k = β / (n_k + Vβ)."""
+    V, KS = nwk.shape
+    den = nk.astype(F32) + F32(vbeta)
+    b = np.zeros(KS, dtype=F32)
+    b[:K] = F32(beta) / den[:K]
+    m = nwk[:, :K] > 0
+    llen = m.sum(axis=1).astype(np.int32)
+    lk = np.zeros((V, KS), dtype=np.uint8)
+    la = np.zeros((V, KS), dtype=F32)
+    wi, ki = np.nonzero(m)
+    pos = (np.cumsum(m, axis=1) - 1)[wi, ki]
+    lk[wi, pos] = ki
+    la[wi, pos] = nwk[wi, ki].astype(F32) / den[ki]
+    return llen, lk, la, b
+
+
+def gibbs_pass_ws(st: dict, G: int, K: int, alpha: float, seed0: int, seed1: int, sweep: int,
+                  chunk_len: np.ndarray, tabs: tuple):
+    """One sweep of the word-sparse sampler (k_gibbs_ws, csrc/kernels/gibbs_ws.hip) over numpy
+    state arrays, in place. ``tabs`` = :func:`ws_tables` of the sweep-start counts. The corpus may
+    be laid out for any unit width G (one chain per chunk either way)."""
+    S = 64 // G
+    KS = st["ndk_src"].shape[1]
+    llen, lk, la, b = tabs
+    slc, lane = _chunk_geometry(st, S)
+    doc = st["chunk_doc"]
+    live = doc >= 0
+    C = doc.shape[0]
+    n = np.zeros((C, KS), dtype=np.int32)
+    n[live] = st["ndk_src"][doc[live]]
+    n_start = n.copy()
+    clen = np.where(live, chunk_len, 0)
+    a32 = F32(alpha)
+    R = np.zeros(C, dtype=F32)
+    for k in range(K):
+        R = fma_f32(n[:, k].astype(F32) + a32, b[k], R)
+    for s in range(int(clen.max(initial=0))):
+        act = np.nonzero(clen > s)[0]
+        idx = st["slice_off"][slc[act]] + s * S + lane[act]
+        w = st["tok_word"][idx].astype(np.int64)
+        pos = st["chunk_pos0"][act].astype(U32) + U32(s)
+        rr = token_rand(pos, st["chunk_key"][act], sweep, 1, seed0, seed1)
+        zo = st["tok_z"][idx].astype(np.int64)
+        n[act, zo] -= 1
+        R[act] = R[act] - b[zo]
+        L = llen[w].astype(np.int64)
+        maxL = int(L.max(initial=0))
+        W = np.zeros(act.size, dtype=F32)
+        cum = np.zeros((act.size, max(maxL, 1)), dtype=F32)
+        for j in range(maxL):
+            m = j < L
+            kj = lk[w, j].astype(np.int64)
+            Wn = fma_f32(n[act, kj].astype(F32) + a32, la[w, j], W)
+            W = np.where(m, Wn, W)
+            cum[:, j] = W
+        thr = u01(rr) * (W + R[act])
+        zn = np.full(act.size, K - 1, dtype=np.int64)
+        inw = thr < W
+        if inw.any():
+            gt = (cum > thr[:, None]) & (np.arange(cum.shape[1])[None, :] < L[:, None])
+            jf = np.argmax(gt, axis=1)
+            zn[inw] = lk[w[inw], jf[inw]]
+        sm = np.nonzero(~inw)[0]
+        if sm.size:
+            tt = thr[sm] - W[sm]
+            acc = np.zeros(sm.size, dtype=F32)
+            found = np.zeros(sm.size, dtype=bool)
+            zs = np.full(sm.size, K - 1, dtype=np.int64)
+            rows = act[sm]
+            for k in range(K):
+                acc = fma_f32(n[rows, k].astype(F32) + a32, b[k], acc)
+                hit = ~found & (acc > tt)
+                zs[hit] = k
+                found |= hit
+            zn[sm] = zs
+        n[act, zn] += 1
+        R[act] = R[act] + b[zn]
+        ch = zn != zo
+        st["tok_z"][idx[ch]] = zn[ch].astype(np.uint8)
+        np.add.at(st["dnwk"], (w[ch], zo[ch]), -1)
+        np.add.at(st["dnwk"], (w[ch], zn[ch]), 1)
+    d = n - n_start
+    multi = live & (st["chunk_multi"] != 0)
+    single = live & ~multi
+    st["ndk_dst"][doc[single]] = n[single]
+    np.add.at(st["ndk_dst"], doc[multi], d[multi])
+    st["dnk"] += d[live].sum(axis=0).astype(np.int32)
+
+
 def gibbs_apply(nwk, dcur, dnk_cur, nk_cur, K, beta, vbeta):
     """Returns (nwk', nk', q) exactly as k_apply computes them."""
     nwk = nwk + dcur

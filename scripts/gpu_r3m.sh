@@ -1,0 +1,9 @@
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+O=gpurun_out/r3m; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "ws or word_sparse or multilane or widen" > $O/pytest_ws.log 2>&1 &&
+timeout -k 10 300 python -u tools/ws_probe.py --topics 100 > $O/ws_probe_k100.jsonl 2> $O/ws_probe_k100.err &&
+timeout -k 10 300 python -u tools/ws_probe.py --topics 20 > $O/ws_probe_k20.jsonl 2> $O/ws_probe_k20.err &&
+timeout -k 10 300 python -u bench/gibbs_ab.py --topics 100 --burn 100 --modes wdelta+lds,wdelta+ws --rounds 5 --sweeps 20 > $O/ab_ws_k100.json 2> $O/ab_ws_k100.err &&
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/prof -o ws -- python3 $GRAFT_REPO_ROOT/bench/gibbs_ab.py --topics 100 --burn 30 --modes wdelta+ws --rounds 1 --sweeps 10 > $GRAFT_REPO_ROOT/$O/prof_ab.log 2>&1

@@ -94,7 +94,9 @@ def _toy_tokens(n_docs, V, seed, heavy=True):
                                     (50, "wdelta+dz"), (20, "wdelta+q2dz"), (20, "recount+q2dz"), (20, "atomic+q2dz"),
                                     (20, "dual+q2dz"), (7, "wdelta+q2dz"), (100, "wdelta+lds5"),
                                     (100, "recount+lds5"), (50, "recount+lds5"), (50, "wdelta+lds5"),
-                                    (100, "dual+lds5")])
+                                    (100, "dual+lds5"), (100, "wdelta+ws"), (100, "recount+ws"), (100, "atomic+ws"),
+                                    (100, "dual+ws"), (100, "delta+ws"), (50, "wdelta+ws"), (20, "wdelta+ws"),
+                                    (20, "recount+ws"), (7, "atomic+ws"), (200, "wdelta+ws"), (32, "delta+ws")])
 def test_gibbs_bitwise_vs_oracle(gpu, K, mode):
     tdoc, tword, keys = _toy_tokens(300, 400, K)
     G, KP = ops.choose_tiling(K)
@@ -105,10 +107,10 @@ def test_gibbs_bitwise_vs_oracle(gpu, K, mode):
     sampler = mode.split("+")[1] if "+" in mode else "auto"
     mg = GibbsLDA(cg, GibbsConfig(K=K, seed=1234, use_graph=False, count_mode=mode.split("+")[0], sampler=sampler))
     if sampler != "auto":
-        assert (mg.qpf in (2, 5, 9)) == (sampler in ("lds", "ldsq", "lds5"))
+        assert (mg.qpf in (2, 5, 9)) == (sampler in ("lds", "ldsq", "lds5")) or sampler == "ws"
     # the oracle replays the numerics the device sampler uses (fma chain for the LDS samplers)
     mc = GibbsLDA(cc, GibbsConfig(K=K, seed=1234, use_graph=False, count_mode="atomic",
-                                  sampler="lds" if mg.qpf in (2, 5, 9) else "plain"))
+                                  sampler="ws" if sampler == "ws" else ("lds" if mg.qpf in (2, 5, 9) else "plain")))
     if mode.startswith("wdelta"):
         assert mg.mode == 4
     mc.initialize()
@@ -128,6 +130,31 @@ def test_gibbs_bitwise_vs_oracle(gpu, K, mode):
     T = cg.T
     assert int(mg.nwk[:, :K].sum()) == T == int(mg.ndk_cur[:, :K].sum()) == int(mg.nk_cur[:K].sum())
     assert int(mg.nwk.min()) >= 0 and int(mg.ndk_cur.min()) >= 0
+
+
+@pytest.mark.parametrize("K", [100, 50, 20])
+def test_gibbs_dense_then_word_sparse_vs_oracle(gpu, K):
+    """"wsa": the dense sampler until the auto count mode switches, the word-sparse one after it
+    (k_ws_tables + k_gibbs_ws inside the same sweeps), bitwise against the oracle doing the same."""
+    tdoc, tword, keys = _toy_tokens(300, 400, K)
+    G, _ = ops.choose_tiling(K)
+    models = []
+    for dev in ("cpu", gpu):
+        c = build_corpus(tdoc.to(dev), tword.to(dev), 300, 400, torch.from_numpy(keys).to(dev), G, L=64)
+        m = GibbsLDA(c, GibbsConfig(K=K, seed=77, use_graph=dev != "cpu", count_mode="auto", auto_switch=3,
+                                    sampler="wsa"))
+        m.initialize()
+        models.append(m)
+    mc, mg = models
+    assert mg.ws == "delta"
+    for _ in range(3):
+        mc.sweep(2)
+        mg.sweep(2)
+        assert torch.equal(mc.tok_z, mg.tok_z.cpu())
+        assert torch.equal(mc.ndk_cur, mg.ndk_cur.cpu())
+        assert torch.equal(mc.nwk, mg.nwk.cpu())
+    for k in ("llen", "b"):
+        assert torch.equal(mc._ws_tabs[k], mg._ws_tabs[k].cpu())
 
 
 @pytest.mark.parametrize("mode,switch", [("auto", 4), ("auto", 0), ("dual", 0), ("delta", 0), ("wdelta", 0)])
@@ -271,3 +298,14 @@ def test_tile_score_mfma_bitwise_vs_fma_oracle(gpu, KS):
     got = common.to_event_order(plan_g, common.plan_score(g(torch.from_numpy(th)), g(torch.from_numpy(ph)), plan_g,
                                                           0.3)[0])
     assert torch.equal(got.cpu(), want)
+
+
+def test_widen_pair_matches_torch_glue(gpu):
+    """k_widen_pair == torch.cat + int64 conversion + u32 mask (the flow day's key glue)."""
+    g = torch.Generator().manual_seed(5)
+    a = torch.randint(-2**31, 2**31 - 1, (100_003,), dtype=torch.int32, generator=g)
+    b = torch.randint(-2**31, 2**31 - 1, (100_003,), dtype=torch.int32, generator=g)
+    ref = torch.cat([a, b]).to(torch.int64) & 0xFFFFFFFF
+    out = ops.widen_pair(a.to(gpu), b.to(gpu))
+    assert out.dtype == torch.int64 and torch.equal(out.cpu(), ref)
+    assert torch.equal(ops.widen_pair(a, b), ref)
