@@ -49,14 +49,8 @@ def main() -> int:
     print(json.dumps({"corpus": c.stats()}), flush=True)
     modes = a.modes.replace("/", ",").split(",")
     models = {m: GibbsLDA(c, GibbsConfig(K=a.topics, count_mode=m.split("+")[0],
-                                         sampler=m.split("+")[1].split(":")[0] if "+" in m else "auto"))
+                                         sampler=m.split("+")[1] if "+" in m else "auto"))
               for m in modes}
-    for name, m in models.items():
-        # "mode+sampler:nostore": timing ablation of the word-sparse sampler without its bookkeeping
-        # stores (the chain is then wrong: for attributing time only)
-        if name.endswith(":nostore"):
-            m._ablate_flags = 512
-            m.cfg.health_check = False  # its counts stop matching the topics by construction
     for m in models.values():
         m.initialize()
         m.sweep(a.burn)

@@ -254,7 +254,7 @@ __global__ __launch_bounds__(64) void k_gibbs_ws(const OniGibbs a, const OniWsTa
       atomicAdd(&row[zn * 64 + lane], 1.0f);
       R = R + bt[zn];
       changed = zn != zo;
-      if (changed && !(a.flags & 512)) {  // flags bit 9: timing ablation only (drops the bookkeeping)
+      if (changed) {
         ++nchg;
         a.tok_z[idx] = (uint8_t)zn;
         if constexpr (MODE == 3) a.z_w[a.wpos[idx]] = (uint8_t)zn;

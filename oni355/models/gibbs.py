@@ -429,7 +429,7 @@ class GibbsLDA:
                        prefetch_q=ops.WS_SAMPLER if use_ws else self.qpf,
                        chg_mask=self.wbits if mode == 4 else getattr(self, "chg_mask", None), wpos=c.wpos,
                        z_w=getattr(self, "z_w", None), zz_w=getattr(self, "zz_w", None), alpha_in_row=self._air,
-                       ws_tabs=self._ws_tabs if use_ws else None, debug_flags=getattr(self, "_ablate_flags", 0))
+                       ws_tabs=self._ws_tabs if use_ws else None)
         head = self.dn[self.b][: self.V * self.KS].view(self.V, self.KS)
         if mode == 4:
             # dn[b] head := Δn_wk of the tokens marked in the word-sorted change bitmap

@@ -299,7 +299,7 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
                chunk_len: torch.Tensor, host_sweep: int | None = None, mode: int = 1,
                prefetch_q: bool | int = False, chg_mask: torch.Tensor | None = None, wpos: torch.Tensor | None = None,
                z_w: torch.Tensor | None = None, zz_w: torch.Tensor | None = None,
-               alpha_in_row: bool = False, ws_tabs: dict | None = None, debug_flags: int = 0) -> None:
+               alpha_in_row: bool = False, ws_tabs: dict | None = None) -> None:
     """Launch one init/sweep pass. ``st`` holds the OniGibbs tensors (see csrc/kernels/gibbs.hip).
 
     ``mode`` 1: accumulate Δn_wk with per-token atomics; 0: the caller rebuilds n_wk with
@@ -380,7 +380,7 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
     a.n_slices, a.K, a.KS, a.alpha, a.seed0, a.seed1 = n_slices, K, KS, float(alpha), s0, s1
     a.nk_rep = nk_rep
     # the caller vouches that n + α is exact in f32 for every doc-topic count of this corpus
-    a.flags = (1 if alpha_in_row else 0) | (int(debug_flags) & ~0xFF)
+    a.flags = 1 if alpha_in_row else 0
     if ws:
         t = _lib.OniWsTabs()
         t.llen, t.lk, t.la, t.b = (_lib.ptr(ws_tabs[k]) for k in ("llen", "lk", "la", "b"))
