@@ -57,6 +57,9 @@ def parse(argv=None):
                     help="long-tail synthetic vocabulary (SURVEY §7.5 sizing): flow -- service ports and wider "
                          "bins (V ~ 4e5); dns / proxy -- half the rows from the long tail of record types, "
                          "rcodes, name shapes / methods, content types, statuses, user agents, URIs")
+    ap.add_argument("--lt-codebook", type=float, default=0.01,
+                    help="flow --realistic-vocab: long-tail behaviours per flow (0.01 -> V ~ 1.7e5 at 12.5M "
+                         "flows, 0.04 -> V ~ 4-5e5)")
     ap.add_argument("--chunk-len", type=int, default=0, help="0 = auto (global token count)")
     ap.add_argument("--maxresults", type=int, default=3000)
     ap.add_argument("--seed", type=int, default=7)
@@ -160,7 +163,7 @@ def make_shard(a, comm):
     if a.source == "flow":
         from oni355.synth.flow import generate_flows
         day = generate_flows(per, seed=a.seed, rank=rank, n_hosts=max(64, n_total // 25),
-                             wide_vocab=a.realistic_vocab)
+                             wide_vocab=a.realistic_vocab, lt_codebook=a.lt_codebook)
     elif a.source == "dns":
         from oni355.synth.dns import generate_dns
         day = generate_dns(per, seed=a.seed, rank=rank, n_clients=max(32, n_total // 40),

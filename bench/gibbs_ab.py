@@ -26,6 +26,8 @@ def main() -> int:
     ap.add_argument("--chunk-len", type=int, default=128)
     ap.add_argument("--chunk-lens", default="", help="extra A/B: comma list of L values (dual+qpf)")
     ap.add_argument("--lds", action="store_true", help="chunk-length A/B with the LDS-count sampler")
+    ap.add_argument("--wide", action="store_true", help="realistic-vocabulary flow day (synth.flow wide_vocab)")
+    ap.add_argument("--lt-codebook", type=float, default=0.01, help="--wide: long-tail behaviours per flow")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -36,7 +38,8 @@ def main() -> int:
     from oni355.synth.flow import generate_flows
 
     dev = torch.device("cuda:0")
-    day = generate_flows(a.flows, seed=7, n_hosts=max(64, a.flows // 25))
+    day = generate_flows(a.flows, seed=7, n_hosts=max(64, a.flows // 25), wide_vocab=a.wide,
+                         lt_codebook=a.lt_codebook)
     d = flow.to_device(day.cols, dev)
     cuts = flow.compute_cuts(d, None)
     sw, dw = flow.wordify(d, cuts)

@@ -67,7 +67,41 @@ __global__ void k_bin_keys(const uint32_t* __restrict__ keys, int64_t n, const u
   }
 }
 
+// Device-side radix-select step (no host round trip between passes): thread q scans its query's
+// histogram (pass 1: the feature's single histogram, all prefixes being 0) for the first digit
+// whose cumulative count exceeds the query's remaining rank -- searchsorted(cumsum, rank, right)
+// capped at B-1, exactly the host step it replaces -- and narrows the prefix / rank.
+__global__ void k_quantile_pick(const uint32_t* __restrict__ hist, const int32_t* __restrict__ base, int nq, int B,
+                                int shift, uint32_t* __restrict__ prefix, int64_t* __restrict__ rank) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  const uint32_t* h = hist + base[q];
+  const int64_t r = rank[q];
+  int64_t cum = 0;
+  int digit = B - 1;
+  int64_t below = 0;
+  for (int b = 0; b < B; ++b) {
+    const int64_t nxt = cum + (int64_t)h[b];
+    if (nxt > r) {
+      digit = b;
+      below = cum;
+      break;
+    }
+    if (b == B - 2) below = nxt;
+    cum = nxt;
+  }
+  if (digit > 0) rank[q] = r - below;
+  prefix[q] |= (uint32_t)digit << shift;
+}
+
 }  // namespace
+
+ONI_API int oni_quantile_pick(const uint32_t* hist, const int32_t* base, int nq, int nbits, int shift, uint32_t* prefix,
+                              int64_t* rank, hipStream_t s) {
+  if (nq < 1 || nbits < 1 || nbits > 16) return (int)hipErrorInvalidValue;
+  k_quantile_pick<<<(nq + 63) / 64, 64, 0, s>>>(hist, base, nq, 1 << nbits, shift, prefix, rank);
+  return (int)hipGetLastError();
+}
 
 ONI_API int oni_radix_hist(const uint32_t* keys, int64_t n, int shift, int nbits, const uint32_t* prefixes, int P,
                            uint32_t mask, uint32_t* hist, hipStream_t s) {

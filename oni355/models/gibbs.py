@@ -221,6 +221,7 @@ class GibbsLDA:
         self._ar_events: list = []
         self._capturing = False
         self._corrupted = False
+        self._tail_cache = None  # (sweeps_done, device tail sums, host copy): see _tail()
         self._x01 = None
         if comm is not None and comm.dist and self.KS % 2 == 0 and self._x01_wanted():
             self._setup_x01()
@@ -398,6 +399,7 @@ class GibbsLDA:
 
     def _prime(self) -> None:
         # zero-delta apply: q from n_wk, nk[1] = nk[0]; leaves dn[0], dn[1] zero
+        self._tail_cache = None
         self._zw_synced = False  # tok_z was (re)written outside the sweeps (init / restore)
         VK = self.V * self.KS
         self.dn[0].zero_()
@@ -456,6 +458,7 @@ class GibbsLDA:
                         absolute=mode in (0, 3), rows_copy=(self.ndk[1 - self.a], self.ndk[self.a], c.long_rows))
         self.a, self.b, self.cn = 1 - self.a, 1 - self.b, 1 - self.cn
         self.sweeps_done += 1
+        self._tail_cache = None
         if not self._capturing:
             self._zw_synced = mode == 3
 
@@ -585,12 +588,23 @@ class GibbsLDA:
             self.ndk_cur[0, 0] = -1 - self.ndk_cur[0, 0].abs()
         self.q[0, 0] = float("nan")
         self._corrupted = True
+        self._tail_cache = None
 
     def check_health(self) -> None:
         """Numerical health check after every ``sweep()`` call (one device reduction, one host
         read): finite q table, no negative word-topic / topic / doc-topic count. Raises
         fault.NumericalFault (the supervisor then restarts from the last good checkpoint)."""
         K = self.K
+        if self.device.type == "cuda":
+            t = self._tail()[1]
+            extra = False
+            if self.c.D > self.c.D_own:  # split-document pieces: rows past D_own
+                extra = bool((self.ndk_cur[self.c.D_own: self.c.D, :K] < 0).any())
+            flags = [t[4] > 0, t[5] > 0, t[6] > 0 or extra]
+            if any(flags):
+                raise fault.NumericalFault(f"corrupt model state after sweep {self.sweeps_done}: non-finite "
+                                           f"q={flags[0]}, negative counts={flags[1] or flags[2]}")
+            return
         flags = torch.stack([
             (~torch.isfinite(self.q[:, :K])).any(),
             (self.nk_cur[:K] < 0).any() | (self.nwk[:, :K] < 0).any(),
@@ -719,6 +733,11 @@ class GibbsLDA:
         a = self._avg
         if a is None or a["n"] == 0 or a["n"] != len(self._avg_at) or self.sweeps_done != self._avg_at[-1]:
             return None
+        if self._avg_cache is None and self.device.type == "cuda":
+            S, K = float(a["n"]), self.K
+            th = ops.theta_rows(a["dk"], K, S * self.alpha, S * K * self.alpha)
+            ph = ops.phi_rows(a["wk"], a["k"], K, S * self.beta, float(np.float32(S) * np.float32(self.vbeta)))
+            self._avg_cache = (th, ph)
         if self._avg_cache is None:
             S, K = float(a["n"]), self.K
             n = a["dk"].to(torch.float32)
@@ -746,6 +765,8 @@ class GibbsLDA:
         avg = self._averaged()
         if avg is not None:
             return avg[0]
+        if self.device.type == "cuda":
+            return ops.theta_rows(self.ndk_cur, self.K, self.alpha, self.K * self.alpha)
         n = self.ndk_cur.to(torch.float32)
         nd = n[:, : self.K].sum(1, keepdim=True)
         th = (n + self.alpha) / (nd + self.K * self.alpha)
@@ -762,6 +783,15 @@ class GibbsLDA:
     def log_likelihood(self) -> float:
         """Collapsed joint log p(w, z) (Griffiths & Steyvers 2004), summed over ranks."""
         K, a, b, V = self.K, self.alpha, self.beta, self.V
+        if self.device.type == "cuda":
+            dev_t, host = self._tail()
+            cw = K * (math.lgamma(V * b) - V * math.lgamma(b))
+            cd = self.c.D_own * (math.lgamma(K * a) - K * math.lgamma(a))
+            if self.comm is not None and self.comm.dist:
+                doc_v = (dev_t[2] - dev_t[3] + cd).reshape(1)
+                self.comm.allreduce_(doc_v)
+                return float(cw + host[0] - host[1] + float(doc_v.cpu()[0]))
+            return float(cw + host[0] - host[1] + (cd + host[2] - host[3]))
         nwk = self.nwk[:, :K].to(torch.float64)
         nk = self.nk_cur[:K].to(torch.float64)
         word = (K * (math.lgamma(V * b) - V * math.lgamma(b)) + torch.lgamma(nwk + b).sum()
@@ -775,6 +805,16 @@ class GibbsLDA:
         if self.comm is not None and self.comm.dist:
             self.comm.allreduce_(doc_v)
         return float(word + doc_v[0])
+
+    def _tail(self):
+        """(device [8] tail sums, host list) of the current counts: log-likelihood lgamma sums and
+        health counts in one fused pass (ops.tail_sums), computed once per model state -- the
+        health check at the end of sweep() and the likelihood after training share it."""
+        if self._tail_cache is None or self._tail_cache[0] != self.sweeps_done:
+            t = ops.tail_sums(self.nwk, self.q, self.nk_cur, self.ndk_cur, self.c.D_own, self.K, self.alpha,
+                              self.beta, self.vbeta)
+            self._tail_cache = (self.sweeps_done, t, t.cpu().tolist())
+        return self._tail_cache[1], self._tail_cache[2]
 
     def record_likelihood(self) -> float:
         ll = self.log_likelihood()

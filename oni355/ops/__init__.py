@@ -206,6 +206,50 @@ def quantile_cuts_multi(keys_list: list, fracs_list: list, allreduce=None, n_glo
     return [p.astype(np.uint32) for p in prefix]
 
 
+def quantile_cuts_dev(keys_list: list, fracs_list: list, allreduce_=None, n_global: int | None = None) -> torch.Tensor:
+    """:func:`quantile_cuts_multi` without a host round trip: every pass's histograms, the
+    (optional, device) all-reduce ``allreduce_(tensor)`` and the digit pick (k_quantile_pick) stay
+    on the stream; returns the concatenated cuts of all features as a device int32 tensor (u32
+    bits), ready for the wordify kernels. Same cuts as :func:`quantile_cuts_multi`."""
+    for k in keys_list:
+        _need(k, torch.int32, "keys")
+    dev = keys_list[0].device
+    n = keys_list[0].numel() if n_global is None else int(n_global)
+    nq = [len(f) for f in fracs_list]
+    NQ = int(sum(nq))
+    ranks = np.concatenate([spec.quantile_ranks(n, f).astype(np.int64) for f in fracs_list])
+    qoff = np.concatenate([[0], np.cumsum(nq)]).astype(np.int64)
+    B = 1 << 11
+    hoff = qoff * B  # feature f's histograms start at hoff[f]
+    base_first = np.concatenate([np.full(nq[f], hoff[f]) for f in range(len(nq))]).astype(np.int32)
+    base_rest = np.concatenate([hoff[f] + np.arange(nq[f]) * B for f in range(len(nq))]).astype(np.int32)
+    # one pinned upload (non-blocking: a pageable copy would wait for the whole queue)
+    host = torch.empty(NQ * 2 + NQ * 2, dtype=torch.int32, pin_memory=dev.type == "cuda")
+    hv = host.numpy()
+    hv[: 2 * NQ] = ranks.view(np.int32)
+    hv[2 * NQ: 3 * NQ] = base_first
+    hv[3 * NQ:] = base_rest
+    st = host.to(dev, non_blocking=True)
+    rank = st[: 2 * NQ].view(torch.int64)
+    bases = (st[2 * NQ: 3 * NQ], st[3 * NQ:])
+    prefix = torch.zeros(NQ, dtype=torch.int32, device=dev)
+    hist = torch.empty(int(hoff[-1]), dtype=torch.int32, device=dev)
+    L = _lib.lib()
+    for pi, (shift, nbits) in enumerate(_PASSES):
+        top = shift + nbits
+        mask = 0 if top >= 32 else (0xFFFFFFFF << top) & 0xFFFFFFFF
+        hist.zero_()
+        for f, k in enumerate(keys_list):
+            P = 1 if pi == 0 else nq[f]
+            _lib.check(L.oni_radix_hist(_lib.ptr(k), k.numel(), shift, nbits, prefix.data_ptr() + 4 * int(qoff[f]), P,
+                                        mask, hist.data_ptr() + 4 * int(hoff[f]), _lib.stream()), "oni_radix_hist")
+        if allreduce_ is not None:
+            allreduce_(hist)
+        _lib.check(L.oni_quantile_pick(_lib.ptr(hist), _lib.ptr(bases[0 if pi == 0 else 1]), NQ, nbits, shift,
+                                       _lib.ptr(prefix), _lib.ptr(rank), _lib.stream()), "oni_quantile_pick")
+    return prefix
+
+
 def bin_keys(keys: torch.Tensor, cuts: np.ndarray) -> torch.Tensor:
     _need(keys, torch.int32, "keys")
     if not _is_dev(keys):
@@ -234,7 +278,9 @@ def flow_keys(hour, minute, second, ibyt, ipkt):
     return tuple(outs)
 
 
-def flow_wordify(sport, dport, tkey, bkey, pkey, tcuts, bcuts, pcuts):
+def flow_wordify(sport, dport, tkey, bkey, pkey, tcuts, bcuts, pcuts, dev_cuts: torch.Tensor | None = None):
+    """Flow words (K03). ``dev_cuts``: the three cut arrays already on the device, concatenated
+    (from :func:`quantile_cuts_dev`); ``tcuts``/``bcuts``/``pcuts`` then only give the counts."""
     n = sport.numel()
     _need(sport, torch.int32, "sport", n)
     _need(dport, torch.int32, "dport", n)
@@ -244,8 +290,14 @@ def flow_wordify(sport, dport, tkey, bkey, pkey, tcuts, bcuts, pcuts):
         sw, dw = spec.flow_wordify(sport.numpy(), dport.numpy(), _u32np(tkey), _u32np(bkey), _u32np(pkey),
                                    tcuts, bcuts, pcuts)
         return _from_u32(sw, sport.device), _from_u32(dw, sport.device)
-    cuts = np.concatenate([np.asarray(tcuts, np.uint32), np.asarray(bcuts, np.uint32), np.asarray(pcuts, np.uint32)])
-    c = _from_u32(cuts, sport.device)
+    if dev_cuts is not None:
+        if dev_cuts.numel() != len(tcuts) + len(bcuts) + len(pcuts) or dev_cuts.dtype != torch.int32:
+            raise ValueError("flow_wordify: device cuts must be the int32 concatenation of the three cut arrays")
+        c = dev_cuts
+    else:
+        cuts = np.concatenate([np.asarray(tcuts, np.uint32), np.asarray(bcuts, np.uint32),
+                               np.asarray(pcuts, np.uint32)])
+        c = _from_u32(cuts, sport.device)
     sw = torch.empty(n, dtype=torch.int32, device=sport.device)
     dw = torch.empty(n, dtype=torch.int32, device=sport.device)
     _lib.check(_lib.lib().oni_flow_wordify(_lib.ptr(sport), _lib.ptr(dport), _lib.ptr(tkey), _lib.ptr(bkey),
@@ -697,4 +749,37 @@ def widen_pair(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     out = torch.empty(2 * n, dtype=torch.int64, device=a.device)
     _lib.check(_lib.lib().oni_widen_pair(_lib.ptr(a.contiguous()), _lib.ptr(b.contiguous()), n, _lib.ptr(out),
                                          _lib.stream()), "oni_widen_pair")
+    return out
+
+
+def tail_sums(nwk: torch.Tensor, q: torch.Tensor, nk: torch.Tensor, ndk: torch.Tensor, D: int, K: int,
+              alpha: float, beta: float, vbeta: float) -> torch.Tensor:
+    """Device [8] float64: Σlgamma(n_wk+β), Σlgamma(n_k+Vβ), Σlgamma(n_dk+α), Σlgamma(n_d+Kα) over the
+    first ``D`` doc rows, then the health counts (#non-finite q, #negative n_wk/n_k, #negative n_dk)
+    -- one pass + a fixed-order reduction (k_tail_partials / k_tail_final), deterministic."""
+    V, KS = nwk.shape
+    lib = _lib.lib()
+    part = torch.empty(lib.oni_tail_grid() * 8, dtype=torch.float64, device=nwk.device)
+    out = torch.empty(8, dtype=torch.float64, device=nwk.device)
+    _lib.check(lib.oni_tail_sums(_lib.ptr(nwk), _lib.ptr(q), _lib.ptr(nk), _lib.ptr(ndk), V, int(D), int(K), KS,
+                                 float(alpha), float(beta), float(vbeta), float(K * alpha), _lib.ptr(part),
+                                 _lib.ptr(out), _lib.stream()), "oni_tail_sums")
+    return out
+
+
+def theta_rows(n: torch.Tensor, K: int, add: float, den_add: float) -> torch.Tensor:
+    """θ = (n + add) / (n_d + den_add) in f32 per row (k_theta_rows), zero past K."""
+    D, KS = n.shape
+    out = torch.empty(D, KS, dtype=torch.float32, device=n.device)
+    _lib.check(_lib.lib().oni_theta_rows(_lib.ptr(n), D, int(K), KS, float(np.float32(add)), float(np.float32(den_add)),
+                                         _lib.ptr(out), _lib.stream()), "oni_theta_rows")
+    return out
+
+
+def phi_rows(nw: torch.Tensor, nk: torch.Tensor, K: int, add: float, vb: float) -> torch.Tensor:
+    """φ = (n_wk + add) / (n_k + vb) in f32 (k_phi_rows), zero past K."""
+    V, KS = nw.shape
+    out = torch.empty(V, KS, dtype=torch.float32, device=nw.device)
+    _lib.check(_lib.lib().oni_phi_rows(_lib.ptr(nw), _lib.ptr(nk), V, int(K), KS, float(np.float32(add)),
+                                       float(np.float32(vb)), _lib.ptr(out), _lib.stream()), "oni_phi_rows")
     return out

@@ -58,6 +58,12 @@ _SIGS = {
     "oni_gibbs_ws_launch": [C.POINTER(OniGibbs), C.POINTER(OniWsTabs), C.c_int, C.c_int, vp],
     "oni_ws_tables": [vp, vp, i64, C.c_int, C.c_int, f32, f32, vp, vp, vp, vp, vp],
     "oni_widen_pair": [vp, vp, i64, vp, vp],
+    "oni_quantile_pick": [vp, vp, C.c_int, C.c_int, C.c_int, vp, vp, vp],
+    "oni_tail_grid": [],
+    "oni_tail_sums": [vp, vp, vp, vp, i64, i64, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double, C.c_double,
+                      vp, vp, vp],
+    "oni_theta_rows": [vp, i64, C.c_int, C.c_int, f32, f32, vp, vp],
+    "oni_phi_rows": [vp, vp, i64, C.c_int, C.c_int, f32, f32, vp, vp],
     "oni_gibbs_apply": [vp, vp, vp, vp, vp, vp, i64, C.c_int, C.c_int, f32, f32, vp, C.c_int, C.c_int, C.c_int,
                         vp, vp, vp, i64, vp],
     "oni_recount": [vp, vp, vp, i64, vp, C.c_int, C.c_int, C.c_int, vp],

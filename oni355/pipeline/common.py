@@ -872,6 +872,17 @@ def _top_n_from_hist(score, hist, tol, maxresults, comm, row_offset, order=None,
     cap = int(np.cumsum(h_loc)[bmax])
     pos, sc = ops.select_below(score, tol, bmax, cap=max(cap, 1))
     idx = order[pos] if order is not None else pos
+    if comm is None or not comm.dist:
+        # world 1: the ≤ a few thousand candidates come to the host in ONE copy and are ordered
+        # there (a chain of tiny device sorts / gathers was ~2 ms of launch and sync gaps per day);
+        # results are host tensors
+        packed = torch.stack([idx.to(torch.int64), pos.to(torch.int64),
+                              sc.view(torch.int32).to(torch.int64)]).cpu().numpy()
+        gid = packed[0] + int(row_offset)
+        sch = packed[2].astype(np.int32).view(np.float32)
+        o = np.lexsort((gid, sch))[:maxresults]  # by score, ties by global row id
+        out = (torch.from_numpy(gid[o].copy()), torch.from_numpy(sch[o].copy()))
+        return out + (torch.from_numpy(packed[1][o].copy()),) if return_pos else out
     gid = idx + row_offset
     # exact order: (score, global id); keep local top-N then merge
     o1 = torch.argsort(gid, stable=True)

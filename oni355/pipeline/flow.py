@@ -137,11 +137,26 @@ def to_device(cols: dict, device) -> dict:
     return out
 
 
-@dataclass
 class FlowCuts:
-    time: np.ndarray
-    ibyt: np.ndarray
-    ipkt: np.ndarray
+    """The day's quantile cuts (time deciles, ibyt deciles, ipkt quintiles). On a GPU they are
+    computed and consumed on the device (``dev``: the three arrays concatenated, int32 bits); the
+    host arrays are fetched only if something reads them."""
+
+    def __init__(self, time=None, ibyt=None, ipkt=None, dev: torch.Tensor | None = None, sizes=(9, 9, 4)):
+        self._host = None if time is None else (np.asarray(time), np.asarray(ibyt), np.asarray(ipkt))
+        self.dev = dev
+        self.sizes = tuple(sizes) if self._host is None else tuple(len(x) for x in self._host)
+
+    def _h(self):
+        if self._host is None:
+            a = self.dev.cpu().numpy().view(np.uint32)
+            t, b = self.sizes[0], self.sizes[0] + self.sizes[1]
+            self._host = (a[:t].copy(), a[t:b].copy(), a[b:].copy())
+        return self._host
+
+    time = property(lambda self: self._h()[0])
+    ibyt = property(lambda self: self._h()[1])
+    ipkt = property(lambda self: self._h()[2])
 
     def as_dict(self) -> dict:
         return {"time": [float(x) for x in spec.key_f32(self.time)], "ibyt": [int(x) for x in self.ibyt],
@@ -157,7 +172,13 @@ def compute_cuts(d: dict, comm: Comm | None) -> FlowCuts:
     if comm is not None and comm.dist:
         ar = comm.allreduce_np
         n_glob = int(comm.allreduce_np(np.array([n], dtype=np.int64))[0])
-    cuts = FlowCuts(*ops.quantile_cuts_multi([tk, bk, pk], [spec.DECILES, spec.DECILES, spec.QUINTILES], ar, n_glob))
+    fr = [spec.DECILES, spec.DECILES, spec.QUINTILES]
+    if tk.is_cuda:
+        # radix select entirely on the stream (X03: the histograms are all-reduced on the device)
+        dev_ar = comm.allreduce_ if comm is not None and comm.dist else None
+        cuts = FlowCuts(dev=ops.quantile_cuts_dev([tk, bk, pk], fr, dev_ar, n_glob), sizes=[len(f) for f in fr])
+    else:
+        cuts = FlowCuts(*ops.quantile_cuts_multi([tk, bk, pk], fr, ar, n_glob))
     d["_keys"] = (tk, bk, pk)
     return cuts
 
@@ -165,6 +186,10 @@ def compute_cuts(d: dict, comm: Comm | None) -> FlowCuts:
 @traced("oni:flow.wordify")
 def wordify(d: dict, cuts: FlowCuts) -> tuple[torch.Tensor, torch.Tensor]:
     tk, bk, pk = d.get("_keys") or ops.flow_keys(d["trhour"], d["trminute"], d["trsec"], d["ibyt"], d["ipkt"])
+    if cuts.dev is not None and tk.is_cuda:
+        nt, nb, npk = cuts.sizes
+        return ops.flow_wordify(d["sport"], d["dport"], tk, bk, pk, range(nt), range(nb), range(npk),
+                                dev_cuts=cuts.dev)
     return ops.flow_wordify(d["sport"], d["dport"], tk, bk, pk, cuts.time, cuts.ibyt, cuts.ipkt)
 
 
@@ -269,8 +294,16 @@ def run_flow(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxre
     mine = (loc >= 0) & (loc < n)
     li = loc[mine]
     pi = rpos[mine] if plan is not None else li  # positions of the result events in score order
-    parts = torch.stack([s1[pi], s2[pi]], 1) if s1 is not None else torch.zeros(0, 2)
-    wparts = torch.stack([sw[li], dw[li]], 1)
+    if s1 is not None and not pi.is_cuda and s1.is_cuda:
+        # host result positions (world 1): one upload of both index sets, one copy back
+        ix = torch.stack([pi, li]).to(s1.device, non_blocking=True)
+        got = torch.stack([s1[ix[0]], s2[ix[0]], sw[ix[1]].view(torch.float32),
+                           dw[ix[1]].view(torch.float32)]).cpu()
+        parts = got[:2].T.contiguous()
+        wparts = got[2:].T.contiguous().view(torch.int32)
+    else:
+        parts = torch.stack([s1[pi], s2[pi]], 1) if s1 is not None else torch.zeros(0, 2)
+        wparts = torch.stack([sw[li], dw[li]], 1)
     if comm is not None and comm.dist:
         # one all-gather of (global row id, both parts' f32 bits, both words) for this rank's rows
         packed = torch.cat([rows[mine].to(torch.int64).view(-1, 1), parts.to(torch.float32).view(torch.int32).to(torch.int64),

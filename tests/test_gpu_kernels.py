@@ -61,6 +61,9 @@ def test_quantile_cuts_multi_equals_single(gpu, n):
     for g, k, x, fr in zip(got, keys, xs, frs):
         assert np.array_equal(g, ops.quantile_cuts(k, fr))
         assert np.array_equal(g, spec.quantile_cuts(spec.f32_key(x), fr))
+    # the device-only pipeline (k_quantile_pick between passes, no read-back) gives the same cuts
+    dev = ops.quantile_cuts_dev(keys, frs).cpu().numpy().view(np.uint32)
+    assert np.array_equal(dev, np.concatenate(got))
 
 
 def _toy_tokens(n_docs, V, seed, heavy=True):
