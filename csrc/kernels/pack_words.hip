@@ -24,13 +24,25 @@ struct OniPack {
   int32_t nkeys, nraw;
   int64_t n;
   uint64_t* out;
+  const uint32_t* dcuts;            // optional: the cut lists on the device, concatenated in component
+                                    // order (ncuts[f] each; e.g. straight from the device quantile
+                                    // select) -- then ``cuts`` is ignored
 };
 
 namespace {
 
 __global__ __launch_bounds__(256) void k_pack(const OniPack a) {
   __shared__ uint32_t sc[kMaxBinned][kMaxCuts];
-  for (int i = threadIdx.x; i < kMaxBinned * kMaxCuts; i += blockDim.x) sc[i / kMaxCuts][i % kMaxCuts] = a.cuts[i / kMaxCuts][i % kMaxCuts];
+  if (a.dcuts) {
+    int off = 0;
+    for (int f = 0; f < a.nkeys; ++f) {
+      for (int c = threadIdx.x; c < a.ncuts[f]; c += blockDim.x) sc[f][c] = a.dcuts[off + c];
+      off += a.ncuts[f];
+    }
+  } else {
+    for (int i = threadIdx.x; i < kMaxBinned * kMaxCuts; i += blockDim.x)
+      sc[i / kMaxCuts][i % kMaxCuts] = a.cuts[i / kMaxCuts][i % kMaxCuts];
+  }
   __syncthreads();
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {

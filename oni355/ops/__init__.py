@@ -221,17 +221,20 @@ def quantile_cuts_dev(keys_list: list, fracs_list: list, allreduce_=None, n_glob
     qoff = np.concatenate([[0], np.cumsum(nq)]).astype(np.int64)
     B = 1 << 11
     hoff = qoff * B  # feature f's histograms start at hoff[f]
-    base_first = np.concatenate([np.full(nq[f], hoff[f]) for f in range(len(nq))]).astype(np.int32)
-    base_rest = np.concatenate([hoff[f] + np.arange(nq[f]) * B for f in range(len(nq))]).astype(np.int32)
+    # histogram of query q in a pass of b bits: pass 1 one shared histogram per feature (every
+    # prefix is 0), later passes one per query at q_local << b inside the feature's region
+    bases_np = [np.concatenate([np.full(nq[f], hoff[f]) for f in range(len(nq))])]
+    for _, nbits in _PASSES[1:]:
+        bases_np.append(np.concatenate([hoff[f] + (np.arange(nq[f]) << nbits) for f in range(len(nq))]))
     # one pinned upload (non-blocking: a pageable copy would wait for the whole queue)
-    host = torch.empty(NQ * 2 + NQ * 2, dtype=torch.int32, pin_memory=dev.type == "cuda")
+    host = torch.empty(NQ * 2 + NQ * len(_PASSES), dtype=torch.int32, pin_memory=dev.type == "cuda")
     hv = host.numpy()
     hv[: 2 * NQ] = ranks.view(np.int32)
-    hv[2 * NQ: 3 * NQ] = base_first
-    hv[3 * NQ:] = base_rest
+    for i, b_ in enumerate(bases_np):
+        hv[(2 + i) * NQ: (3 + i) * NQ] = b_.astype(np.int32)
     st = host.to(dev, non_blocking=True)
     rank = st[: 2 * NQ].view(torch.int64)
-    bases = (st[2 * NQ: 3 * NQ], st[3 * NQ:])
+    bases = [st[(2 + i) * NQ: (3 + i) * NQ] for i in range(len(_PASSES))]
     prefix = torch.zeros(NQ, dtype=torch.int32, device=dev)
     hist = torch.empty(int(hoff[-1]), dtype=torch.int32, device=dev)
     L = _lib.lib()
@@ -245,7 +248,7 @@ def quantile_cuts_dev(keys_list: list, fracs_list: list, allreduce_=None, n_glob
                                         mask, hist.data_ptr() + 4 * int(hoff[f]), _lib.stream()), "oni_radix_hist")
         if allreduce_ is not None:
             allreduce_(hist)
-        _lib.check(L.oni_quantile_pick(_lib.ptr(hist), _lib.ptr(bases[0 if pi == 0 else 1]), NQ, nbits, shift,
+        _lib.check(L.oni_quantile_pick(_lib.ptr(hist), _lib.ptr(bases[pi]), NQ, nbits, shift,
                                        _lib.ptr(prefix), _lib.ptr(rank), _lib.stream()), "oni_quantile_pick")
     return prefix
 

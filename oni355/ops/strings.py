@@ -19,6 +19,7 @@ class OniPack(C.Structure):
         ("cuts", (C.c_uint32 * K_MAX_CUTS) * K_MAX_BINNED), ("raw", vp * K_MAX_RAW),
         ("rmask", C.c_uint32 * K_MAX_RAW), ("rshift", C.c_int32 * K_MAX_RAW), ("raw8", vp), ("r8mask", C.c_uint32),
         ("r8shift", C.c_int32), ("nkeys", C.c_int32), ("nraw", C.c_int32), ("n", C.c_int64), ("out", vp),
+        ("dcuts", vp),
     ]
 
 
@@ -110,25 +111,40 @@ def string_features(offsets: torch.Tensor, chars: torch.Tensor):
     return outs
 
 
+def _split_cuts(flat: np.ndarray, sizes: list) -> list:
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    return [flat[off[i]:off[i + 1]] for i in range(len(sizes))]
+
+
 def pack_words(keys: list, cuts: list, kshift: list, raws: list, rmask: list, rshift: list, raw8=None, r8mask=0,
-               r8shift=0) -> torch.Tensor:
-    """Word keys (int64 holding u64 bits) from binned order keys + raw categorical fields."""
+               r8shift=0, dev_cuts: torch.Tensor | None = None) -> torch.Tensor:
+    """Word keys (int64 holding u64 bits) from binned order keys + raw categorical fields.
+    ``dev_cuts``: the cut lists already on the device, concatenated (int32 bits); ``cuts`` then
+    only gives each list's length."""
     ref = keys[0] if keys else raws[0]
     n = ref.numel()
+    if dev_cuts is not None and ref.device.type != "cuda":
+        dev_cuts, cuts = None, _split_cuts(dev_cuts.numpy().view(np.uint32), [len(c) for c in cuts])
     if ref.device.type != "cuda":
         w = ss.pack_words([k.numpy().view(np.uint32) for k in keys], cuts, kshift, [r.numpy() for r in raws], rmask,
                           rshift, None if raw8 is None else raw8.numpy(), r8mask, r8shift)
         return torch.from_numpy(w.view(np.int64))
     a = OniPack()
+    if dev_cuts is not None:
+        if dev_cuts.dtype != torch.int32 or dev_cuts.numel() != sum(len(c) for c in cuts):
+            raise ValueError("dev_cuts: int32 concatenation of every binned component's cut list")
+        a.dcuts = _lib.ptr(dev_cuts)
     for i, (k, c, s) in enumerate(zip(keys, cuts, kshift)):
-        c = np.asarray(c, np.uint32)
-        if c.size > K_MAX_CUTS or k.dtype != torch.int32 or k.numel() != n:
+        if dev_cuts is None:
+            c = np.asarray(c, np.uint32)
+        if len(c) > K_MAX_CUTS or k.dtype != torch.int32 or k.numel() != n:
             raise ValueError("bad binned component")
         a.key[i] = _lib.ptr(k)
-        a.ncuts[i] = c.size
+        a.ncuts[i] = len(c)
         a.kshift[i] = s
-        for j, v in enumerate(c.tolist()):
-            a.cuts[i][j] = v
+        if dev_cuts is None:
+            for j, v in enumerate(c.tolist()):
+                a.cuts[i][j] = v
     for i, (r, m, s) in enumerate(zip(raws, rmask, rshift)):
         if r.dtype != torch.int32 or r.numel() != n:
             raise ValueError("raw components must be int32 of length n")

@@ -24,6 +24,47 @@ from ..parallel.comm import Comm
 U32MASK = 0xFFFFFFFF
 
 
+class DayCuts:
+    """A day's quantile cut lists by feature name, computed on the device
+    (:func:`ops.quantile_cuts_dev`): kernels take ``dev`` (the lists concatenated, int32 bits);
+    the host arrays are fetched on first access (one copy)."""
+
+    def __init__(self, names: list, sizes: list, dev: torch.Tensor):
+        self.names, self.sizes, self.dev = list(names), [int(x) for x in sizes], dev
+        self._host = None
+
+    def _h(self) -> dict:
+        if self._host is None:
+            a = self.dev.cpu().numpy().view(np.uint32)
+            off = np.concatenate([[0], np.cumsum(self.sizes)]).astype(np.int64)
+            self._host = {n: a[off[i]:off[i + 1]].copy() for i, n in enumerate(self.names)}
+        return self._host
+
+    def __getitem__(self, k):
+        return self._h()[k]
+
+    def items(self):
+        return self._h().items()
+
+    def keys(self):
+        return list(self.names)
+
+
+def binned_cuts(keys: dict, binned: list, comm: Comm | None, n_glob: int):
+    """Quantile cuts of the BINNED features of a DNS / proxy day: on a GPU the radix select and
+    the digit picks stay on the stream (:class:`DayCuts`); on the CPU the oracle path. Returns
+    (cuts, device concatenation or None)."""
+    names = [name for name, _, _ in binned]
+    fr = [f for _, f, _ in binned]
+    kl = [keys[name].contiguous() for name in names]
+    if kl[0].is_cuda:
+        dev_ar = comm.allreduce_ if comm is not None and comm.dist else None
+        dc = ops.quantile_cuts_dev(kl, fr, dev_ar, n_glob)
+        return DayCuts(names, [len(f) for f in fr], dc), dc
+    ar = comm.allreduce_np if comm is not None and comm.dist else None
+    return dict(zip(names, ops.quantile_cuts_multi(kl, fr, ar, n_glob))), None
+
+
 def u32_to_i64(t: torch.Tensor) -> torch.Tensor:
     """int32 tensor holding u32 bits → non-negative int64."""
     return t.to(torch.int64) & U32MASK

@@ -98,16 +98,14 @@ def featurize(d: dict, comm: Comm | None, topset: HashSet | None, user_domain: s
     keys = {"frame_len": d["frame_len"], "time": time_keys(d["unix_tstamp"]), "sub_len": sub_len,
             "sub_ent": ops.f32_keys(sub_ent), "periods": per}
     n = d["frame_len"].numel()
-    ar, n_glob = None, n
+    n_glob = n
     if comm is not None and comm.dist:
-        ar = comm.allreduce_np
         n_glob = int(comm.allreduce_np(np.array([n], np.int64))[0])
-    cuts = dict(zip([name for name, _, _ in BINNED],
-                    ops.quantile_cuts_multi([keys[name].contiguous() for name, _, _ in BINNED],
-                                            [fr for _, fr, _ in BINNED], ar, n_glob)))
-    words = sops.pack_words([keys[name].contiguous() for name, _, _ in BINNED], [cuts[name] for name, _, _ in BINNED],
+    cuts, dev_cuts = common.binned_cuts(keys, BINNED, comm, n_glob)
+    words = sops.pack_words([keys[name].contiguous() for name, _, _ in BINNED],
+                            [range(len(fr)) if dev_cuts is not None else cuts[name] for name, fr, _ in BINNED],
                             [s for _, _, s in BINNED], [d[name] for name, _, _ in RAW], [m for _, m, _ in RAW],
-                            [s for _, _, s in RAW], raw8=top, r8mask=3, r8shift=TOP_SHIFT)
+                            [s for _, _, s in RAW], raw8=top, r8mask=3, r8shift=TOP_SHIFT, dev_cuts=dev_cuts)
     feats = {"top": top, "sub_len": sub_len, "sub_ent": sub_ent, "periods": per, "reg_hash": rh}
     return words, cuts, feats
 

@@ -174,21 +174,19 @@ def featurize(cols: dict, device, comm: Comm | None, topset, allreduce_counts: b
     _, ulen, uent = sops.string_features(fo, fc)
     keys = {"time": tkey, "ua_freq": ua_freq, "uri_ent": ops.f32_keys(uent), "uri_len": ulen}
     if day is not None:
-        cuts = day[0]
+        cuts, dev_cuts = day[0], None
     else:
-        ar, n_glob = None, n
+        n_glob = n
         if comm is not None and comm.dist:
-            ar = comm.allreduce_np
             n_glob = int(comm.allreduce_np(np.array([n], np.int64))[0])
-        cuts = dict(zip([name for name, _, _ in BINNED],
-                        ops.quantile_cuts_multi([keys[name].contiguous() for name, _, _ in BINNED],
-                                                [fr for _, fr, _ in BINNED], ar, n_glob)))
+        cuts, dev_cuts = common.binned_cuts(keys, BINNED, comm, n_glob)
     raws = {"method": _codes_by_hash(cols["reqmethod"], *strcol("reqmethod"), method_code),
             "ctype": _codes_by_hash(cols["resconttype"], *strcol("resconttype"), ctype_class),
             "respcode": d["respcode"]}
-    words = sops.pack_words([keys[nm] for nm, _, _ in BINNED], [cuts[nm] for nm, _, _ in BINNED],
+    words = sops.pack_words([keys[nm] for nm, _, _ in BINNED],
+                            [range(len(fr)) if dev_cuts is not None else cuts[nm] for nm, fr, _ in BINNED],
                             [s for _, _, s in BINNED], [raws[nm] for nm, _, _ in RAW], [m for _, m, _ in RAW],
-                            [s for _, _, s in RAW], raw8=top, r8mask=3, r8shift=TOP_SHIFT)
+                            [s for _, _, s in RAW], raw8=top, r8mask=3, r8shift=TOP_SHIFT, dev_cuts=dev_cuts)
     if table is None:
         # the day's UA frequency table (signed-sorted keys, counts), for wording feedback rows
         ks, o = torch.sort(uq.to(dev) if comm is None or not comm.dist else uq)

@@ -246,7 +246,9 @@ def test_flow_pipeline_gpu_matches_cpu(gpu):
     rg = run_flow(day.cols, K=20, sweeps=6, maxresults=200, device=gpu)
     assert np.array_equal(rc.rows, rg.rows)
     assert np.array_equal(rc.scores, rg.scores)
-    assert rc.stats["loglik"] == pytest.approx(rg.stats["loglik"], rel=1e-12)
+    # the device log-likelihood sums OCML's lgamma (≤ 2 ulp from libm's) over ~5e5 terms in one
+    # fused pass (k_tail_partials): equal to ~1e-10 relative, not bit for bit
+    assert rc.stats["loglik"] == pytest.approx(rg.stats["loglik"], rel=1e-8)
 
 
 @pytest.mark.parametrize("two", [True, False])
