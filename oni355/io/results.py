@@ -305,14 +305,27 @@ class ResultPipe:
             self._pending = (fut, res.rows, tag)
             self._finish()
             return
+        if self.comm is None or not self.comm.dist:
+            # no collective to keep in program order: the worker formats AND writes the day
+            self._pending = (self._pool.submit(self._local_day, cols, res, row_off, tag), None, "__done__")
+            return
         fut = self._pool.submit(render_local, self.source, cols, res, row_off)
         self._pending = (fut, res.rows, tag)
+
+    def _local_day(self, cols: dict, res, row_off: int, tag):
+        gids, rendered = render_local(self.source, cols, res, row_off)
+        full = gather_rendered(res.rows, gids, rendered, None)
+        if self.write is not None:
+            self.write(full) if tag is None else self.write(full, tag)
+        return full
 
     def _finish(self):
         if self._pending is None:
             return None
         fut, rows, tag = self._pending
         self._pending = None
+        if tag == "__done__":
+            return fut.result()
         gids, rendered = fut.result()
         full = gather_rendered(rows, gids, rendered, self.comm)
         if self.write is not None:
