@@ -74,25 +74,41 @@ __global__ __launch_bounds__(kTailBlock) void k_tail_partials(const int32_t* __r
   }
 }
 
-__global__ void k_tail_final(const double* __restrict__ part, int nblocks, double* __restrict__ out) {
-  if (threadIdx.x < kTailVals) {
-    double v = 0.0;
-    for (int b = 0; b < nblocks; ++b) v += part[(int64_t)b * kTailVals + threadIdx.x];
-    out[threadIdx.x] = v;
-  }
+// wave j reduces value j over the blocks: lane-strided sums, then the butterfly (a fixed order:
+// deterministic)
+__global__ __launch_bounds__(kTailVals * 64) void k_tail_final(const double* __restrict__ part, int nblocks,
+                                                              double* __restrict__ out) {
+  const int j = threadIdx.x / oni::kWave, lane = threadIdx.x % oni::kWave;
+  double v = 0.0;
+  for (int b = lane; b < nblocks; b += oni::kWave) v += part[(int64_t)b * kTailVals + j];
+  v = wave_sum_d(v);
+  if (lane == 0) out[j] = v;
 }
 
-// one thread per row: n_d is a sum of integer counts (exact in f32 below 2^24, any order)
+// 256 rows per block: thread t sums row t's counts (n_d is a sum of integer counts, exact in f32
+// below 2^24 in any order) into LDS, then the block reads and writes its rows' KS columns
+// coalesced (a row per thread touched KS scattered words per lane).
 __global__ __launch_bounds__(256) void k_theta_rows(const int32_t* __restrict__ n, int64_t D, int K, int KS, float add,
                                                     float den_add, float* __restrict__ th) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; d < D; d += stride) {
-    const int32_t* r = n + d * KS;
-    float nd = 0.f;
-    for (int k = 0; k < K; ++k) nd += (float)r[k];
-    const float den = nd + den_add;
-    float* o = th + d * KS;
-    for (int k = 0; k < KS; ++k) o[k] = k < K ? ((float)r[k] + add) / den : 0.f;
+  __shared__ float den[256];
+  for (int64_t r0 = (int64_t)blockIdx.x * 256; r0 < D; r0 += (int64_t)gridDim.x * 256) {
+    const int64_t d = r0 + threadIdx.x;
+    if (d < D) {
+      const int32_t* r = n + d * KS;
+      float nd = 0.f;
+      for (int k = 0; k < K; ++k) nd += (float)r[k];
+      den[threadIdx.x] = nd + den_add;
+    }
+    __syncthreads();
+    const int64_t rows = D - r0 < 256 ? D - r0 : 256;
+    const int64_t cells = rows * KS;
+    const int32_t* src = n + r0 * KS;
+    float* dst = th + r0 * KS;
+    for (int64_t i = threadIdx.x; i < cells; i += 256) {
+      const int k = (int)(i % KS);
+      dst[i] = k < K ? ((float)src[i] + add) / den[i / KS] : 0.f;
+    }
+    __syncthreads();
   }
 }
 
@@ -121,7 +137,7 @@ ONI_API int oni_tail_sums(const int32_t* nwk, const float* q, const int32_t* nk,
   if (K < 1 || K > KS || KS > 256) return (int)hipErrorInvalidValue;
   const int grid = 512;
   k_tail_partials<<<grid, kTailBlock, 0, s>>>(nwk, q, nk, ndk, V, D, K, KS, alpha, beta, vbeta, kalpha, part);
-  k_tail_final<<<1, 64, 0, s>>>(part, grid, out);
+  k_tail_final<<<1, kTailVals * 64, 0, s>>>(part, grid, out);
   return (int)hipGetLastError();
 }
 
@@ -129,7 +145,7 @@ ONI_API int oni_theta_rows(const int32_t* n, int64_t D, int K, int KS, float add
                            hipStream_t s) {
   if (K < 1 || K > KS) return (int)hipErrorInvalidValue;
   if (D <= 0) return 0;
-  k_theta_rows<<<oni::grid_for(D, 256, 4096), 256, 0, s>>>(n, D, K, KS, add, den_add, th);
+  k_theta_rows<<<oni::grid_for(D, 256, 2048), 256, 0, s>>>(n, D, K, KS, add, den_add, th);
   return (int)hipGetLastError();
 }
 

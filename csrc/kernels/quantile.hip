@@ -67,31 +67,55 @@ __global__ void k_bin_keys(const uint32_t* __restrict__ keys, int64_t n, const u
   }
 }
 
-// Device-side radix-select step (no host round trip between passes): thread q scans its query's
+// Device-side radix-select step (no host round trip between passes): wave q scans query q's
 // histogram (pass 1: the feature's single histogram, all prefixes being 0) for the first digit
 // whose cumulative count exceeds the query's remaining rank -- searchsorted(cumsum, rank, right)
-// capped at B-1, exactly the host step it replaces -- and narrows the prefix / rank.
-__global__ void k_quantile_pick(const uint32_t* __restrict__ hist, const int32_t* __restrict__ base, int nq, int B,
-                                int shift, uint32_t* __restrict__ prefix, int64_t* __restrict__ rank) {
-  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+// capped at B-1, exactly the host step it replaces -- and narrows the prefix / rank. Each lane
+// owns B/64 consecutive bins: lane sums, one wave prefix scan, then the owning lane walks its bins.
+__global__ __launch_bounds__(64) void k_quantile_pick(const uint32_t* __restrict__ hist,
+                                                      const int32_t* __restrict__ base, int nq, int B, int shift,
+                                                      uint32_t* __restrict__ prefix, int64_t* __restrict__ rank) {
+  const int q = blockIdx.x;
+  const int lane = threadIdx.x;
   if (q >= nq) return;
   const uint32_t* h = hist + base[q];
+  const int per = B / oni::kWave;
   const int64_t r = rank[q];
-  int64_t cum = 0;
-  int digit = B - 1;
-  int64_t below = 0;
-  for (int b = 0; b < B; ++b) {
-    const int64_t nxt = cum + (int64_t)h[b];
-    if (nxt > r) {
-      digit = b;
-      below = cum;
-      break;
-    }
-    if (b == B - 2) below = nxt;
-    cum = nxt;
+  int64_t mine = 0;
+  for (int j = 0; j < per; ++j) mine += h[lane * per + j];
+  int64_t incl = mine;  // inclusive scan over lanes
+#pragma unroll
+  for (int d = 1; d < oni::kWave; d <<= 1) {
+    const int64_t y = __shfl_up(incl, d);
+    if (lane >= d) incl += y;
   }
-  if (digit > 0) rank[q] = r - below;
-  prefix[q] |= (uint32_t)digit << shift;
+  const int64_t excl = incl - mine;
+  // the lane whose bins hold the first cumulative count > r (none: digit B-1)
+  const uint64_t hit = __ballot(incl > r);
+  if (hit) {
+    const int owner = __ffsll((unsigned long long)hit) - 1;
+    if (lane == owner) {
+      int64_t cum = excl;
+      int digit = lane * per + per - 1;
+      int64_t below = cum;
+      for (int j = 0; j < per; ++j) {
+        const int64_t nxt = cum + h[lane * per + j];
+        if (nxt > r) {
+          digit = lane * per + j;
+          below = cum;
+          break;
+        }
+        cum = nxt;
+      }
+      if (digit > 0) rank[q] = r - below;
+      prefix[q] |= (uint32_t)digit << shift;
+    }
+  } else if (lane == oni::kWave - 1) {
+    // every count ≤ r: digit B-1, rank -= cumsum[B-2]
+    const int64_t below = incl - h[B - 1];
+    rank[q] = r - below;
+    prefix[q] |= (uint32_t)(B - 1) << shift;
+  }
 }
 
 }  // namespace
@@ -99,7 +123,8 @@ __global__ void k_quantile_pick(const uint32_t* __restrict__ hist, const int32_t
 ONI_API int oni_quantile_pick(const uint32_t* hist, const int32_t* base, int nq, int nbits, int shift, uint32_t* prefix,
                               int64_t* rank, hipStream_t s) {
   if (nq < 1 || nbits < 1 || nbits > 16) return (int)hipErrorInvalidValue;
-  k_quantile_pick<<<(nq + 63) / 64, 64, 0, s>>>(hist, base, nq, 1 << nbits, shift, prefix, rank);
+  if ((1 << nbits) % 64) return (int)hipErrorInvalidValue;
+  k_quantile_pick<<<nq, 64, 0, s>>>(hist, base, nq, 1 << nbits, shift, prefix, rank);
   return (int)hipGetLastError();
 }
 

@@ -253,18 +253,24 @@ def gather_rendered(all_rows: np.ndarray, gids: np.ndarray, rendered: Rendered, 
     t = torch.from_numpy(payload)
     if comm.device.type == "cuda":
         t = t.to(comm.device)
-    by_gid = {}
+    gl, st, en, texts, base = [], [], [], [], 0
     for part in comm.allgather_var(t):
         b = part.cpu().numpy()
         n, nb = (int(x) for x in b[:16].view(np.int64))
-        pg = b[16:16 + 8 * n].view(np.int64)
         pe = b[16 + 8 * n:16 + 16 * n].view(np.int64)
-        text = b[16 + 16 * n:16 + 16 * n + nb].tobytes()
-        for gid, line in zip(pg.tolist(), Rendered(text, pe).lines()):
-            by_gid[gid] = line
-    lines = [by_gid[int(x)] for x in np.asarray(all_rows).tolist()]
-    ends = np.cumsum([len(x) for x in lines]).astype(np.int64) if lines else np.zeros(0, np.int64)
-    return Rendered(b"".join(lines), ends)
+        gl.append(b[16:16 + 8 * n].view(np.int64))
+        st.append(base + np.concatenate([[0], pe[:-1]]) if n else np.zeros(0, np.int64))
+        en.append(base + pe)
+        texts.append(b[16 + 16 * n:16 + 16 * n + nb].tobytes())
+        base += nb
+    g_all, s_all, e_all = np.concatenate(gl), np.concatenate(st), np.concatenate(en)
+    blob = b"".join(texts)
+    o = np.argsort(g_all, kind="stable")
+    pos = o[np.searchsorted(g_all[o], np.asarray(all_rows, dtype=np.int64))]
+    mv = memoryview(blob)
+    out = b"".join(mv[a:b_] for a, b_ in zip(s_all[pos].tolist(), e_all[pos].tolist()))
+    ends = np.cumsum(e_all[pos] - s_all[pos]).astype(np.int64)
+    return Rendered(out, ends)
 
 
 def render_result(source: str, cols: dict, res, row_off: int, comm=None) -> Rendered:
@@ -292,6 +298,9 @@ class ResultPipe:
         self.write = write
         self._pool = ThreadPoolExecutor(1, thread_name_prefix="oni-results")
         self._pending = None  # (future of (gids, Rendered), all result rows)
+        # data parallel: the rendered-row gather runs on the worker thread too, over a gloo group
+        # of its own (host bytes; never interleaves with the main thread's device collectives)
+        self._hcomm = comm.side_group("results") if comm is not None and comm.dist else None
 
     def submit(self, cols: dict, res, row_off: int, tag=None) -> None:
         """Queue this day's formatting; finishes the previous day first. ``ONI_RESULT_PIPE=0``
@@ -305,8 +314,9 @@ class ResultPipe:
             self._pending = (fut, res.rows, tag)
             self._finish()
             return
-        if self.comm is None or not self.comm.dist:
-            # no collective to keep in program order: the worker formats AND writes the day
+        if os.environ.get("ONI_RESULT_GATHER_WORKER", "1") == "1" or self.comm is None or not self.comm.dist:
+            # the worker formats, gathers (data parallel: on its own gloo group, days in program
+            # order on every rank) AND writes the day
             self._pending = (self._pool.submit(self._local_day, cols, res, row_off, tag), None, "__done__")
             return
         fut = self._pool.submit(render_local, self.source, cols, res, row_off)
@@ -314,7 +324,7 @@ class ResultPipe:
 
     def _local_day(self, cols: dict, res, row_off: int, tag):
         gids, rendered = render_local(self.source, cols, res, row_off)
-        full = gather_rendered(res.rows, gids, rendered, None)
+        full = gather_rendered(res.rows, gids, rendered, self._hcomm)
         if self.write is not None:
             self.write(full) if tag is None else self.write(full, tag)
         return full

@@ -165,6 +165,20 @@ class Comm:
                 self._host_side = Comm(self.rank, self.world, torch.device("cpu"), g, forced=True, backend="gloo")
         return self._host_side
 
+    def side_group(self, name: str) -> "Comm":
+        """A further CPU (gloo) communicator of its own, for one more worker thread's host-side
+        collectives (e.g. the result pipe's rendered-row gather) -- like :meth:`host_side`, each
+        thread owns its group so no two threads' collectives interleave on one channel.
+        Collective call: every rank creates it in the same order."""
+        groups = self.__dict__.setdefault("_side_groups", {})
+        if name not in groups:
+            if not self.dist:
+                groups[name] = Comm(self.rank, self.world, torch.device("cpu"), backend="gloo")
+            else:
+                g = dist.new_group(backend="gloo")
+                groups[name] = Comm(self.rank, self.world, torch.device("cpu"), g, forced=True, backend="gloo")
+        return groups[name]
+
     def _host_view(self) -> "Comm":
         return Comm(self.rank, self.world, torch.device("cpu"), self.group, forced=self.dist, backend="gloo")
 

@@ -727,6 +727,7 @@ SCORE_TILES = False
 # score events in first-endpoint pair order (one monotone + one random gather per flow instead of
 # two random ones; DNS/proxy events become a pure stream); results map back through plan.order
 SCORE_SORT_EVENTS = True
+SCORE_SORT_PAIRS = os.environ.get("ONI_SCORE_SORT_PAIRS", "0") == "1"
 
 
 @traced("oni:score_plan")
@@ -765,7 +766,10 @@ def plan_from_pairs(ps, n: int, n_sides: int, doc_rows: torch.Tensor | None = No
     pdoc = ps.pair_doc if doc_rows is None else doc_rows[ps.pair_doc.long()].to(torch.int32)
     invs = [ps.tok_pair[i * n:(i + 1) * n] for i in range(n_sides)]
     plan = ScorePlan(pdoc.contiguous(), ps.pair_word, invs)
-    if SCORE_SORT_EVENTS and ps.order0 is not None:
+    # the pair-ordered event view costs two 12.5M-element random gathers (inv[order0]) inside the
+    # day now that the plan is built per day (0.44 ms), more than the random pair-score reads it
+    # saves in k_event_min: off by default here (ONI_SCORE_SORT_PAIRS=1 restores it)
+    if SCORE_SORT_PAIRS and ps.order0 is not None:
         plan.order = ps.order0
         plan.inv_sorted = [x[ps.order0].contiguous() for x in invs]
     return plan
