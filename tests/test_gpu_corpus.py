@@ -59,7 +59,7 @@ def test_dict_encode_equals_unique(gpu, n, bits):
     assert torch.equal(u, nu.cpu()) and torch.equal(inv.to(torch.int32), ni.cpu())
 
 
-def test_pair_plan_equals_score_plan(gpu):
+def test_pair_plan_equals_score_plan(gpu, monkeypatch):
     r = np.random.default_rng(5)
     n, D, V = 50_000, 900, 700
     dkeys = torch.from_numpy(np.sort(r.choice(2**32, D, replace=False)).astype(np.int64))
@@ -76,6 +76,10 @@ def test_pair_plan_equals_score_plan(gpu):
     assert torch.equal(ref.pdoc, plan.pdoc) and torch.equal(ref.pword, plan.pword)
     for a, b in zip(ref.inv, plan.inv):
         assert torch.equal(a, b)
+    assert plan.order is None  # the per-day plan scores events in event order by default
+    # the pair-ordered event view (ONI_SCORE_SORT_PAIRS=1) equals score_plan's
+    monkeypatch.setattr(common, "SCORE_SORT_PAIRS", True)
+    plan = common.plan_from_pairs(ps, n, 2, doc_rows=common.lookup(dkeys.to(gpu), ud))
     assert torch.equal(ref.order, plan.order) and torch.equal(ref.rank, plan.rank)
 
 
