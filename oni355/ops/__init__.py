@@ -217,6 +217,8 @@ def quantile_cuts_dev(keys_list: list, fracs_list: list, allreduce_=None, n_glob
     n = keys_list[0].numel() if n_global is None else int(n_global)
     nq = [len(f) for f in fracs_list]
     NQ = int(sum(nq))
+    if n == 0:  # an empty day: all-zero cuts, as quantile_cuts_multi
+        return torch.zeros(NQ, dtype=torch.int32, device=dev)
     ranks = np.concatenate([spec.quantile_ranks(n, f).astype(np.int64) for f in fracs_list])
     qoff = np.concatenate([[0], np.cumsum(nq)]).astype(np.int64)
     B = 1 << 11
