@@ -215,3 +215,68 @@ ONI_API int oni_set_probe(const uint64_t* h, int64_t n, const uint64_t* tab, uin
   k_set_probe<<<oni::grid_for(n), 256, 0, s>>>(h, n, tab, mask, out);
   return (int)hipGetLastError();
 }
+
+// ---- categorical codes by pattern table (proxy method / content type) -------------------------
+// code(s) for a string s, after trimming ASCII whitespace and folding case (fold: 1 = upper,
+// 2 = lower): the code of the LONGEST pattern p that matches -- exactly (mode 0) or as a prefix
+// (mode 1) -- else `dflt`. The patterns of one table (≤ 32, ≤ 32 bytes each) live in LDS; one
+// thread per row. The same rule as proxy.method_code / proxy.ctype_class on the host, without
+// the round trip of "distinct values → host labels → table".
+namespace {
+constexpr int kCatMax = 32, kCatLen = 32;
+
+__device__ __forceinline__ uint8_t fold_char(uint8_t c, int fold) {
+  if (fold == 1 && c >= 'a' && c <= 'z') return (uint8_t)(c - 32);
+  if (fold == 2 && c >= 'A' && c <= 'Z') return (uint8_t)(c + 32);
+  return c;
+}
+
+__device__ __forceinline__ bool is_space(uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r' ||
+                                                             c == '\v' || c == '\f'; }
+
+__global__ __launch_bounds__(256) void k_category_codes(const int64_t* __restrict__ off,
+                                                        const uint8_t* __restrict__ chars, int64_t n,
+                                                        const uint8_t* __restrict__ pat, const int32_t* __restrict__ plen,
+                                                        const int32_t* __restrict__ pmode,
+                                                        const int32_t* __restrict__ pcode, int np, int fold, int dflt,
+                                                        int32_t* __restrict__ out) {
+  __shared__ uint8_t sp[kCatMax * kCatLen];
+  __shared__ int32_t sl[kCatMax], sm[kCatMax], sc[kCatMax];
+  for (int i = threadIdx.x; i < np * kCatLen; i += blockDim.x) sp[i] = pat[i];
+  for (int i = threadIdx.x; i < np; i += blockDim.x) {
+    sl[i] = plen[i];
+    sm[i] = pmode[i];
+    sc[i] = pcode[i];
+  }
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += stride) {
+    int64_t a = off[r], b = off[r + 1];
+    while (a < b && is_space(chars[a])) ++a;
+    while (b > a && is_space(chars[b - 1])) --b;
+    const int64_t len = b - a;
+    int best = dflt, blen = -1;
+    for (int p = 0; p < np; ++p) {
+      const int pl = sl[p];
+      if (pl <= blen || (sm[p] == 0 ? len != pl : len < pl)) continue;
+      bool ok = true;
+      for (int j = 0; j < pl && ok; ++j) ok = fold_char(chars[a + j], fold) == sp[p * kCatLen + j];
+      if (ok) {
+        best = sc[p];
+        blen = pl;
+      }
+    }
+    out[r] = best;
+  }
+}
+}  // namespace
+
+ONI_API int oni_category_codes(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t* pat,
+                               const int32_t* plen, const int32_t* pmode, const int32_t* pcode, int np, int fold,
+                               int dflt, int32_t* out, hipStream_t s) {
+  if (np < 0 || np > kCatMax) return (int)hipErrorInvalidValue;
+  if (n <= 0) return 0;
+  k_category_codes<<<oni::grid_for(n, 256, 4096), 256, 0, s>>>(off, chars, n, pat, plen, pmode, pcode, np, fold, dflt,
+                                                                out);
+  return (int)hipGetLastError();
+}

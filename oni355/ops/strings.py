@@ -29,6 +29,7 @@ _lib.register_optional("oni_domain_features", [vp, vp, i64, vp, C.c_uint64, C.c_
 _lib.register_optional("oni_string_features", [vp, vp, i64, vp, vp, vp, vp, vp, vp])
 _lib.register_optional("oni_set_probe", [vp, i64, vp, C.c_uint64, vp, vp])
 _lib.register_optional("oni_pack_words", [C.POINTER(OniPack), vp])
+_lib.register_optional("oni_category_codes", [vp, vp, i64, vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, vp, vp])
 _lib.register_optional("oni_pack_sizeof", [])
 
 _tables: dict = {}
@@ -160,4 +161,38 @@ def pack_words(keys: list, cuts: list, kshift: list, raws: list, rmask: list, rs
     if L.oni_pack_sizeof() != C.sizeof(OniPack):
         raise RuntimeError("OniPack ABI mismatch; rebuild")
     _lib.check(L.oni_pack_words(C.byref(a), _lib.stream()), "oni_pack_words")
+    return out
+
+
+def _category_table(patterns: tuple, device):
+    """Device pattern table of :func:`category_codes` (cached per pattern tuple and device)."""
+    key = (patterns, str(device))
+    if key not in _tables:
+        if len(patterns) > 32 or any(len(p.encode()) > 32 for p, _, _ in patterns):
+            raise ValueError("category patterns: at most 32, of at most 32 bytes")
+        pat = np.zeros((max(len(patterns), 1), 32), np.uint8)
+        for i, (p, _, _) in enumerate(patterns):
+            b = p.encode()
+            pat[i, :len(b)] = np.frombuffer(b, np.uint8)
+        cols = [np.array([len(p.encode()) for p, _, _ in patterns] or [0], np.int32),
+                np.array([m for _, m, _ in patterns] or [0], np.int32),
+                np.array([c for _, _, c in patterns] or [0], np.int32)]
+        _tables[key] = (torch.from_numpy(pat.reshape(-1)).to(device), *(torch.from_numpy(c).to(device) for c in cols))
+    return _tables[key]
+
+
+def category_codes(offsets: torch.Tensor, chars: torch.Tensor, patterns: tuple, fold: int, default: int) -> torch.Tensor:
+    """int32 code per string (k_category_codes): trim ASCII whitespace, fold case (1 upper, 2 lower),
+    then the code of the longest matching pattern ((text, mode 0 exact / 1 prefix, code), first
+    of equal length wins), else ``default``. GPU only (the CPU path labels distinct values)."""
+    n = offsets.numel() - 1
+    dev = offsets.device
+    out = torch.empty(max(n, 0), dtype=torch.int32, device=dev)
+    if n <= 0:
+        return out
+    pat, plen, pmode, pcode = _category_table(tuple(patterns), dev)
+    ch = chars if chars.numel() else torch.zeros(1, dtype=torch.uint8, device=dev)
+    _lib.check(_lib.lib().oni_category_codes(_lib.ptr(offsets), _lib.ptr(ch), n, _lib.ptr(pat), _lib.ptr(plen),
+                                             _lib.ptr(pmode), _lib.ptr(pcode), len(patterns), int(fold), int(default),
+                                             _lib.ptr(out), _lib.stream()), "oni_category_codes")
     return out

@@ -97,6 +97,11 @@ def _unique_first(h: torch.Tensor):
     return uniq, first.cpu(), inv
 
 
+# the same rules as method_code / ctype_class as device pattern tables (ops.strings.category_codes)
+METHOD_PATTERNS = tuple((m, 0, i) for i, m in enumerate(METHODS))
+CTYPE_PATTERNS = tuple((p, 0 if p in ("", "-") else 1, c) for p, c in CTYPE_CLASSES)
+
+
 def method_code(s: str) -> int:
     s = s.strip().upper()
     return METHODS.index(s) if s in METHODS else 0
@@ -180,8 +185,14 @@ def featurize(cols: dict, device, comm: Comm | None, topset, allreduce_counts: b
         if comm is not None and comm.dist:
             n_glob = int(comm.allreduce_np(np.array([n], np.int64))[0])
         cuts, dev_cuts = common.binned_cuts(keys, BINNED, comm, n_glob)
-    raws = {"method": _codes_by_hash(cols["reqmethod"], *strcol("reqmethod"), method_code),
-            "ctype": _codes_by_hash(cols["resconttype"], *strcol("resconttype"), ctype_class),
+    if dev.type == "cuda":
+        # per-row pattern match on the device: no distinct-value round trip through the host
+        meth = sops.category_codes(*strcol("reqmethod"), METHOD_PATTERNS, 1, 0)
+        ctyp = sops.category_codes(*strcol("resconttype"), CTYPE_PATTERNS, 2, 10)
+    else:
+        meth = _codes_by_hash(cols["reqmethod"], *strcol("reqmethod"), method_code)
+        ctyp = _codes_by_hash(cols["resconttype"], *strcol("resconttype"), ctype_class)
+    raws = {"method": meth, "ctype": ctyp,
             "respcode": d["respcode"]}
     words = sops.pack_words([keys[nm] for nm, _, _ in BINNED],
                             [range(len(fr)) if dev_cuts is not None else cuts[nm] for nm, fr, _ in BINNED],

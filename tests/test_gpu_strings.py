@@ -84,3 +84,20 @@ def test_domain_features_public_suffix_table_bitwise(gpu, tmp_path):
                                    rules)
         for w, g in zip(want, got):
             assert np.array_equal(np.asarray(w).view(np.uint8), g.cpu().numpy().view(np.uint8))
+
+
+def test_category_codes_match_host_rules(gpu):
+    """k_category_codes == proxy.method_code / ctype_class (trim, case fold, longest pattern)."""
+    from oni355.pipeline import proxy as px
+    meths = ["GET", " get ", "Post", "PUT\t", "head", "CONNECT", "options", "DELETE", "trace", "PATCH", "GETX", "",
+             "-", "OTHER", "g e t", "pOsT "]
+    ctypes = ["text/html", "TEXT/HTML; charset=utf-8", " text/plain", "image/png", "application/javascript",
+              "application/json", "application/octet-stream", "application/x-foo", "video/mp4", "audio/ogg",
+              "multipart/form-data", "", "-", " - ", "weird/type", "textual", "application", "IMAGE/"]
+    for vals, pats, fold, dflt, fn in ((meths, px.METHOD_PATTERNS, 1, 0, px.method_code),
+                                       (ctypes, px.CTYPE_PATTERNS, 2, 10, px.ctype_class)):
+        col = StringColumn.from_list(vals * 50)
+        off = torch.from_numpy(col.offsets.astype(np.int64)).to(gpu)
+        ch = torch.from_numpy(col.chars).to(gpu)
+        got = sops.category_codes(off, ch, pats, fold, dflt).cpu().numpy()
+        assert got.tolist() == [fn(v) for v in vals * 50]
