@@ -41,6 +41,7 @@ struct OniWsTabs {
   const float* la;      // [V][KS] a_wk = n_wk / (n_k + Vβ), same order
   const float* b;       // [KS] b_k = β / (n_k + Vβ); 0 for k ≥ K
   unsigned long long* stats;  // optional [5]: tokens, smoothing-bucket draws, slow-path lists, Σ wave-step list max, wave steps
+  const uint32_t* lofs;       // [V] for G-lane units (k_gibbs_wsg): byte g = first list entry of lane g's topics
 };
 
 namespace {
@@ -321,13 +322,264 @@ __global__ __launch_bounds__(64) void k_gibbs_ws(const OniGibbs a, const OniWsTa
   }
 }
 
+// ---- word-sparse sampler on G-lane units (K > 32) --------------------------------------------
+// k_gibbs_ws holds a whole doc row per lane in LDS (26 KB per 64 chains at K = 100: 6 waves per
+// CU, and the measured kernel was slower than the dense one). Here the layout is the dense LDS
+// sampler's (k_gibbs_ldsg): unit = G lanes, lane g owns topics [g·KP, (g+1)·KP) in its LDS row
+// (20 waves per CU at K = 100), and the word bucket is split the same way -- lane g walks only the
+// word's list entries in its topic range (contiguous in the ascending list; the per-word lane
+// offsets come from k_ws_tables). Per lane: W_g over its entries, R_g its smoothing bucket (fma
+// chain over its topics at chunk start, ± b on count changes), T_g = W_g + R_g combined by the
+// same DPP Hillis-Steele scan as ldsg; the first lane with incl > thr draws inside its range.
+// Numerics: oni355/ref/spec.py gibbs_pass_wsg (bitwise).
+template <int G, int KP, int MODE, bool AIR>
+__global__ __launch_bounds__(kBlock) void k_gibbs_wsg(const OniGibbs a, const OniWsTabs t) {
+  static_assert(G > 1, "one-lane units use k_gibbs_ws");
+  constexpr int S = oni::kWave / G;
+  constexpr int KS = G * KP;
+  constexpr int kSlots = LdsRow<KP>::kSlots;
+  constexpr int E = 8;  // register capacity of a lane's share of the word's list
+  __shared__ float4 sa[kBlock * kSlots];
+  __shared__ float bt[KS];
+  __shared__ int32_t red[kWavesPerBlock][KS];
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int c = lane / G;
+  const int g = lane % G;
+  const int K = a.K;
+  const int64_t slice = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  const bool valid = slice < a.n_slices;
+  const int64_t chunk = slice * S + c;
+  const int doc = valid ? a.chunk_doc[chunk] : -1;
+  const bool live = doc >= 0;
+  const int kbase = g * KP;
+  const float alpha = a.alpha;
+  float4* row = sa + threadIdx.x * kSlots;
+  float* rowf = reinterpret_cast<float*>(row);
+  for (int k = threadIdx.x; k < KS; k += kBlock) bt[k] = t.b[k];
+  {
+    int32_t n0[KP];
+#pragma unroll
+    for (int j = 0; j < KP; ++j) n0[j] = 0;
+    if (live) load_row_i<KP>(a.ndk_src + (int64_t)doc * KS + kbase, n0);
+    const float a0 = AIR ? alpha : 0.f;
+#pragma unroll
+    for (int j = 0; j < KP / 4; ++j)
+      row[j] = make_float4((float)n0[4 * j] + a0, (float)n0[4 * j + 1] + a0, (float)n0[4 * j + 2] + a0,
+                           (float)n0[4 * j + 3] + a0);
+  }
+  __syncthreads();
+  float R = 0.f;
+#pragma unroll
+  for (int j = 0; j < KP; ++j) R = fmaf(AIR ? rowf[j] : rowf[j] + alpha, bt[kbase + j], R);
+
+  const int len = valid ? a.slice_len[slice] : 0;
+  const int64_t off = valid ? a.slice_off[slice] : 0;
+  const uint32_t key = live ? a.chunk_key[chunk] : 0u;
+  const uint32_t pos0 = live ? (uint32_t)a.chunk_pos0[chunk] : 0u;
+  const uint32_t sweep = *a.sweep_ctr;
+  uint32_t gbase = pos0 >> 2;
+  oni::U4 r = oni::philox10(oni::U4{gbase + (uint32_t)g, key, sweep, 1u}, a.seed0, a.seed1);
+  uint32_t wcur = oni::kPadWord;
+  int jb = 0, nb = 0;
+  float la_r[E];
+  int lk_r[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    la_r[j] = 0.f;
+    lk_r[j] = 0;
+  }
+  int nchg = 0;
+  uint32_t w_nx = len > 0 ? a.tok_word[off + c] : oni::kPadWord;
+  int z_nx = len > 0 ? (int)a.tok_z[off + c] : 0;
+  for (int s = 0; s < len; ++s) {
+    const int64_t idx = off + (int64_t)s * S + c;
+    const uint32_t w = w_nx;
+    const int zo = z_nx;
+    if (s + 1 < len) {
+      w_nx = a.tok_word[idx + S];
+      z_nx = a.tok_z[idx + S];
+    }
+    if (w == oni::kPadWord) continue;  // uniform across the G lanes of a unit
+    const uint32_t pos = pos0 + (uint32_t)s;
+    const uint32_t gi = pos >> 2;
+    if (gi - gbase >= (uint32_t)G) {  // uniform within the unit
+      gbase = gi;
+      r = oni::philox10(oni::U4{gbase + (uint32_t)g, key, sweep, 1u}, a.seed0, a.seed1);
+    }
+    const uint32_t rr = (uint32_t)__shfl((int)oni::pick4(r, pos & 3u), (int)(gi - gbase), G);
+    const float* lap = t.la + (int64_t)w * KS;
+    const uint8_t* lkp = t.lk + (int64_t)w * KS;
+    if (w != wcur) {  // this lane's share of the word's list: entries [jb, jb + nb)
+      const uint32_t lo = t.lofs[w];
+      const int L = t.llen[w];
+      jb = (int)((lo >> (8 * g)) & 0xFFu);
+      const int je = g + 1 < G ? (int)((lo >> (8 * (g + 1))) & 0xFFu) : L;
+      nb = je - jb;
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        if (j < nb) {
+          la_r[j] = lap[jb + j];
+          lk_r[j] = (int)lkp[jb + j] - kbase;
+        }
+      }
+      wcur = w;
+    }
+    const unsigned zlo = (unsigned)(zo - kbase);
+    if (zlo < (unsigned)KP) {
+      atomicAdd(&rowf[zlo], -1.0f);
+      R = R - bt[zo];
+    }
+    const int nr = nb < E ? nb : E;
+    float v[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) v[j] = j < nr ? rowf[lk_r[j]] : 0.f;
+    float cum[E];
+    float W = 0.f;
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      if (j < nr) W = fmaf(AIR ? v[j] : v[j] + alpha, la_r[j], W);
+      cum[j] = W;
+    }
+    for (int j = E; j < nb; ++j) {  // slow path: a longer share than the register capacity
+      const float rv = rowf[(int)lkp[jb + j] - kbase];
+      W = fmaf(AIR ? rv : rv + alpha, lap[jb + j], W);
+    }
+    const float T = W + R;
+    const float incl = group_scan_dpp<G>(T, g);
+    float excl = dpp_row_shr<1>(incl);
+    if (g == 0) excl = 0.f;
+    const float total = __shfl(incl, G - 1, G);
+    const float thr = oni::u01(rr) * total;
+    int gs = group_sum_dpp<G>(incl <= thr ? 1 : 0);
+    gs = gs < G - 1 ? gs : G - 1;
+    int z = 0;
+    if (g == gs) {
+      const float tt = thr - excl;
+      if (tt < W) {
+        int pick = -1;
+#pragma unroll
+        for (int j = 0; j < E; ++j)
+          if (pick < 0 && j < nr && cum[j] > tt) pick = j;
+        if (pick < 0) {
+          float W2 = nr > 0 ? cum[nr - 1] : 0.f;
+          for (int j = E; j < nb; ++j) {
+            const float rv = rowf[(int)lkp[jb + j] - kbase];
+            W2 = fmaf(AIR ? rv : rv + alpha, lap[jb + j], W2);
+            if (W2 > tt) {
+              pick = j;
+              break;
+            }
+          }
+          if (pick < 0) pick = nb - 1;  // unreachable in exact arithmetic: W2 ends at W > tt
+        }
+        z = kbase + (pick < E ? lk_r[pick] : (int)lkp[jb + pick] - kbase);
+      } else {
+        const float t2 = tt - W;
+        const int kend = K - kbase < KP ? K - kbase : KP;
+        float acc = 0.f;
+        z = kbase + kend - 1;
+        for (int j = 0; j < kend; ++j) {
+          acc = fmaf(AIR ? rowf[j] : rowf[j] + alpha, bt[kbase + j], acc);
+          if (acc > t2) {
+            z = kbase + j;
+            break;
+          }
+        }
+      }
+    }
+    const int zn = __shfl(z, gs, G);
+    const unsigned znl = (unsigned)(zn - kbase);
+    if (znl < (unsigned)KP) {
+      atomicAdd(&rowf[znl], 1.0f);
+      R = R + bt[zn];
+    }
+    const bool changed = zn != zo && g == 0;
+    if (changed) {
+      ++nchg;
+      a.tok_z[idx] = (uint8_t)zn;
+      if constexpr (MODE == 3) a.z_w[a.wpos[idx]] = (uint8_t)zn;
+      if constexpr (MODE == 4) mark_changed_w(a, a.wpos[idx], zo, zn);
+      if constexpr (MODE == 1) {
+        atomicAdd(&a.dnwk[(int64_t)w * KS + zo], -1);
+        atomicAdd(&a.dnwk[(int64_t)w * KS + zn], 1);
+      }
+    }
+    if constexpr (MODE == 2) {
+      const uint64_t m = __ballot(changed);
+      if (lane == 0) a.chg_mask[(off + (int64_t)s * S) / S] = m;
+    }
+  }
+  if (a.chg_count) add_wave_count(a.chg_count, nchg);
+  // ---- epilogue (as k_gibbs_ldsg): doc rows + per-topic totals --------------------------------
+  int32_t d[KP], n[KP];
+#pragma unroll
+  for (int j = 0; j < KP; ++j) {
+    n[j] = (int32_t)(AIR ? rowf[j] - alpha : rowf[j]);
+    d[j] = 0;
+  }
+  if (live) {
+    int32_t* dst = a.ndk_dst + (int64_t)doc * KS + kbase;
+    int32_t n0[KP];
+    load_row_i<KP>(a.ndk_src + (int64_t)doc * KS + kbase, n0);
+#pragma unroll
+    for (int j = 0; j < KP; ++j) d[j] = n[j] - n0[j];
+    if (!a.chunk_multi[chunk]) {
+#pragma unroll
+      for (int j = 0; j < KP; j += 4) *reinterpret_cast<int4*>(dst + j) = make_int4(n[j], n[j + 1], n[j + 2], n[j + 3]);
+    }
+  }
+  {
+    const bool multi = live && a.chunk_multi[chunk];
+    if (__ballot(multi)) flush_multi_rows<G, KP>(a.ndk_dst, KS, doc, multi, kbase, d);
+  }
+#pragma unroll
+  for (int j = 0; j < KP; ++j) {
+    int vv = d[j];
+#pragma unroll
+    for (int m = G; m < oni::kWave; m <<= 1) vv += __shfl_xor(vv, m);
+    d[j] = vv;
+  }
+  if (c == 0) {
+#pragma unroll
+    for (int j = 0; j < KP; ++j) red[wave][kbase + j] = d[j];
+  }
+  __syncthreads();
+  if (threadIdx.x < KS) {
+    int vv = 0;
+#pragma unroll
+    for (int w2 = 0; w2 < kWavesPerBlock; ++w2) vv += red[w2][threadIdx.x];
+    if (vv) atomicAdd(&a.dnk[(int)(blockIdx.x & (unsigned)(a.nk_rep - 1)) * KS + threadIdx.x], vv);
+  }
+}
+
+template <int G, int KP>
+int launch_wsg(const OniGibbs& a, const OniWsTabs& t, int mode, hipStream_t s) {
+  const unsigned grid = (unsigned)((a.n_slices + kWavesPerBlock - 1) / kWavesPerBlock);
+  if (grid == 0) return 0;
+  const bool air = (a.flags & 1) != 0;
+#define ONI_WSG(m_)                                                          \
+  if (air) k_gibbs_wsg<G, KP, m_, true><<<grid, kBlock, 0, s>>>(a, t);       \
+  else k_gibbs_wsg<G, KP, m_, false><<<grid, kBlock, 0, s>>>(a, t);
+  switch (mode) {
+    case 0: ONI_WSG(0) break;
+    case 1: ONI_WSG(1) break;
+    case 2: ONI_WSG(2) break;
+    case 3: ONI_WSG(3) break;
+    default: ONI_WSG(4) break;
+  }
+#undef ONI_WSG
+  return (int)hipGetLastError();
+}
+
 // Per-sweep tables of k_gibbs_ws from the refreshed counts: one wave per word compacts the
 // topics with n_wk > 0 (ballot + prefix popcount, ascending k) with a_wk = n_wk / (n_k + Vβ);
 // block 0 writes b_k = β / (n_k + Vβ). den_k is the same f32 expression as k_apply's.
 __global__ __launch_bounds__(256) void k_ws_tables(const int32_t* __restrict__ nwk, const int32_t* __restrict__ nk,
                                                    int64_t V, int K, int KS, float beta, float vbeta,
                                                    int32_t* __restrict__ llen, uint8_t* __restrict__ lk,
-                                                   float* __restrict__ la, float* __restrict__ b) {
+                                                   float* __restrict__ la, float* __restrict__ b,
+                                                   uint32_t* __restrict__ lofs, int G, int KP) {
   const int lane = threadIdx.x & 63;
   const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -335,6 +587,7 @@ __global__ __launch_bounds__(256) void k_ws_tables(const int32_t* __restrict__ n
     for (int k = threadIdx.x; k < KS; k += blockDim.x) b[k] = k < K ? beta / ((float)nk[k] + vbeta) : 0.f;
   for (int64_t w = wave0; w < V; w += nwaves) {
     int base = 0;
+    uint32_t offs = 0;  // byte g: entries with topic < g·KP (lane g's first entry)
     for (int k0 = 0; k0 < K; k0 += oni::kWave) {
       const int k = k0 + lane;
       const int32_t n = k < K ? nwk[w * KS + k] : 0;
@@ -344,9 +597,17 @@ __global__ __launch_bounds__(256) void k_ws_tables(const int32_t* __restrict__ n
         lk[w * KS + p] = (uint8_t)k;
         la[w * KS + p] = (float)n / ((float)nk[k] + vbeta);
       }
+      for (int gg = 1; gg < G; ++gg) {
+        const int lim = gg * KP - k0;  // lanes of this block below the lane boundary
+        const uint64_t below = lim <= 0 ? 0ull : (lim >= 64 ? ~0ull : ((1ull << lim) - 1ull));
+        offs += (uint32_t)__popcll(m & below) << (8 * gg);
+      }
       base += __popcll(m);
     }
-    if (lane == 0) llen[w] = base;
+    if (lane == 0) {
+      llen[w] = base;
+      if (lofs) lofs[w] = offs;
+    }
   }
 }
 
@@ -380,9 +641,26 @@ ONI_API int oni_gibbs_ws_launch(const OniGibbs* a, const OniWsTabs* t, int G, in
 }
 
 ONI_API int oni_ws_tables(const int32_t* nwk, const int32_t* nk, int64_t V, int K, int KS, float beta, float vbeta,
-                          int32_t* llen, uint8_t* lk, float* la, float* b, hipStream_t s) {
+                          int32_t* llen, uint8_t* lk, float* la, float* b, uint32_t* lofs, int G, int KP,
+                          hipStream_t s) {
   if (K < 1 || K > 240 || K > KS || KS % 4) return (int)hipErrorInvalidValue;
+  if (lofs && (G < 1 || G > 4 || G * KP != KS)) return (int)hipErrorInvalidValue;
   const int64_t waves = V > 0 ? V : 1;
-  k_ws_tables<<<oni::grid_for(waves * 64, 256, 4096), 256, 0, s>>>(nwk, nk, V, K, KS, beta, vbeta, llen, lk, la, b);
+  k_ws_tables<<<oni::grid_for(waves * 64, 256, 4096), 256, 0, s>>>(nwk, nk, V, K, KS, beta, vbeta, llen, lk, la, b,
+                                                                    lofs, lofs ? G : 1, KP);
   return (int)hipGetLastError();
+}
+
+ONI_API int oni_gibbs_wsg_launch(const OniGibbs* a, const OniWsTabs* t, int G, int KP, int mode, hipStream_t s) {
+  if (a->K < 1 || a->K > a->KS || a->KS != G * KP || mode < 0 || mode > 4) return (int)hipErrorInvalidValue;
+  if (a->nk_rep < 1 || (a->nk_rep & (a->nk_rep - 1))) return (int)hipErrorInvalidValue;
+  if (mode == 2 && !a->chg_mask) return (int)hipErrorInvalidValue;
+  if (mode == 3 && (!a->wpos || !a->z_w)) return (int)hipErrorInvalidValue;
+  if (mode == 4 && (!a->wpos || !a->zz_w || !a->chg_mask)) return (int)hipErrorInvalidValue;
+  if (!t->llen || !t->lk || !t->la || !t->b || !t->lofs) return (int)hipErrorInvalidValue;
+#define ONI_CASE(g_, kp_) \
+  if (G == g_ && KP == kp_) return launch_wsg<g_, kp_>(*a, *t, mode, s);
+  ONI_CASE(2, 20) ONI_CASE(2, 24) ONI_CASE(2, 28) ONI_CASE(4, 16) ONI_CASE(4, 20) ONI_CASE(4, 24) ONI_CASE(4, 28)
+#undef ONI_CASE
+  return (int)hipErrorInvalidValue;
 }

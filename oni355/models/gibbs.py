@@ -32,7 +32,7 @@ NK_REP = 32
 X01_PACK_MIN_BYTES = 4 << 20
 DZ_MAX_LEN = 128  # kDzMaxLen (csrc/kernels/gibbs_sampler.h)
 SAMPLERS = {"pp": 1, "plain": 0, "lds": 2, "qpf": 4, "ldsq": 5, "q2": 6, "dz": 7, "q2dz": 8, "lds5": 9,
-            "ws": 10, "wsa": 10}  # -> oni_gibbs_launch qpf argument
+            "ws": 10, "wsa": 10, "wsg": 10}  # -> oni_gibbs_launch qpf argument
 
 
 @dataclass
@@ -189,14 +189,17 @@ class GibbsLDA:
                                                                          SAMPLERS["lds"])
         # word-sparse sampler (k_gibbs_ws): "ws" on every sweep; "wsa" only in the sweeps after the
         # auto count mode's switch (the word lists are short once topics have settled; the early
-        # sweeps keep the dense sampler)
+        # sweeps keep the dense sampler); "wsg" the G-lane variant (k_gibbs_wsg: the dense LDS
+        # sampler's layout, each lane walking the word's entries in its topic range)
         self.ws = None
-        if cfg.sampler in ("ws", "wsa"):
+        if cfg.sampler in ("ws", "wsa", "wsg"):
             if cfg.K > 240:
                 raise ValueError("the word-sparse sampler supports K <= 240")
             self.ws = "delta" if (cfg.sampler == "wsa" and self.auto) else "always"
             self.qpf = SAMPLERS["qpf"] if self.G == 1 else SAMPLERS["lds"]
-        self._ws_tabs = ops.ws_alloc(self.V, self.KS, dev) if self.ws else None
+        # (other tilings -- G = 8/16 at K > 112 -- run the one-lane k_gibbs_ws over the same corpus)
+        lanes = (self.G, self.KP) if (cfg.sampler == "wsg" and (self.G, self.KP) in ops.WSG_TILES) else None
+        self._ws_tabs = ops.ws_alloc(self.V, self.KS, dev, lanes) if self.ws else None
         if self.qpf in (5, 9) and self.G == 1:
             self.qpf = 2
         if self.qpf in (7, 8) and (self.G != 1 or corpus.L > DZ_MAX_LEN):

@@ -393,7 +393,10 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
         if not atomic:
             npst["dnwk"] = np.zeros_like(npst["dnwk"])  # discarded: recount rebuilds n_wk
         sweep_no = int(host_sweep if host_sweep is not None else sweep_ctr.item())
-        if ws:
+        if ws and _wsg(ws_tabs, G):
+            spec.gibbs_pass_wsg(npst, G, KP, K, alpha, s0, s1, sweep_no, chunk_len.numpy(),
+                                tuple(ws_tabs[k].numpy() for k in ("llen", "lk", "la", "b")))
+        elif ws:
             spec.gibbs_pass_ws(npst, G, K, alpha, s0, s1, sweep_no, chunk_len.numpy(),
                                tuple(ws_tabs[k].numpy() for k in ("llen", "lk", "la", "b")))
         else:
@@ -443,6 +446,11 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
         t.llen, t.lk, t.la, t.b = (_lib.ptr(ws_tabs[k]) for k in ("llen", "lk", "la", "b"))
         if ws_tabs.get("stats") is not None:  # diagnostics: see tools/ws_probe.py
             t.stats = _lib.ptr(ws_tabs["stats"])
+        if _wsg(ws_tabs, G):
+            t.lofs = _lib.ptr(ws_tabs["lofs"])
+            _lib.check(_lib.lib().oni_gibbs_wsg_launch(C.byref(a), C.byref(t), G, KP, int(mode), _lib.stream()),
+                       "oni_gibbs_wsg_launch")
+            return
         _lib.check(_lib.lib().oni_gibbs_ws_launch(C.byref(a), C.byref(t), G, int(mode), _lib.stream()),
                    "oni_gibbs_ws_launch")
         return
@@ -451,15 +459,26 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
                "oni_gibbs_launch")
 
 
-WS_SAMPLER = 10  # prefetch_q code of the word-sparse sampler (k_gibbs_ws)
+WS_SAMPLER = 10  # prefetch_q code of the word-sparse sampler (k_gibbs_ws / k_gibbs_wsg)
+WSG_TILES = {(2, 20), (2, 24), (2, 28), (4, 16), (4, 20), (4, 24), (4, 28)}  # oni_gibbs_wsg_launch
 
 
-def ws_alloc(V: int, KS: int, device) -> dict:
-    """Device (or CPU) tables of the word-sparse sampler, rebuilt every sweep by :func:`ws_tables`."""
-    return dict(llen=torch.zeros(max(V, 1), dtype=torch.int32, device=device),
-                lk=torch.zeros(max(V, 1), KS, dtype=torch.uint8, device=device),
-                la=torch.zeros(max(V, 1), KS, dtype=torch.float32, device=device),
-                b=torch.zeros(KS, dtype=torch.float32, device=device))
+def _wsg(ws_tabs: dict, G: int) -> bool:
+    """The G-lane word-sparse sampler (k_gibbs_wsg) runs when the tables carry lane offsets."""
+    return G > 1 and ws_tabs.get("lofs") is not None
+
+
+def ws_alloc(V: int, KS: int, device, lanes: tuple | None = None) -> dict:
+    """Device (or CPU) tables of the word-sparse sampler, rebuilt every sweep by :func:`ws_tables`.
+    ``lanes`` = (G, KP) adds the per-word lane offsets of the G-lane sampler (k_gibbs_wsg)."""
+    t = dict(llen=torch.zeros(max(V, 1), dtype=torch.int32, device=device),
+             lk=torch.zeros(max(V, 1), KS, dtype=torch.uint8, device=device),
+             la=torch.zeros(max(V, 1), KS, dtype=torch.float32, device=device),
+             b=torch.zeros(KS, dtype=torch.float32, device=device))
+    if lanes is not None and lanes[0] > 1:
+        t["lofs"] = torch.zeros(max(V, 1), dtype=torch.int32, device=device)
+        t["lanes"] = tuple(lanes)
+    return t
 
 
 def ws_tables(nwk: torch.Tensor, nk: torch.Tensor, K: int, beta: float, vbeta: float, tabs: dict) -> None:
@@ -472,9 +491,14 @@ def ws_tables(nwk: torch.Tensor, nk: torch.Tensor, K: int, beta: float, vbeta: f
         tabs["lk"][:V].copy_(torch.from_numpy(lk))
         tabs["la"][:V].copy_(torch.from_numpy(la))
         tabs["b"].copy_(torch.from_numpy(b))
+        if tabs.get("lofs") is not None:
+            G, KP = tabs["lanes"]
+            tabs["lofs"][:V].copy_(torch.from_numpy(spec.ws_lane_offsets(llen, lk, G, KP).view(np.int32)))
         return
+    G, KP = tabs.get("lanes", (1, KS))
     _lib.check(_lib.lib().oni_ws_tables(_lib.ptr(nwk), _lib.ptr(nk), V, K, KS, float(beta), float(vbeta),
-                                        *(_lib.ptr(tabs[k]) for k in ("llen", "lk", "la", "b")), _lib.stream()),
+                                        *(_lib.ptr(tabs[k]) for k in ("llen", "lk", "la", "b")),
+                                        _lib.ptr(tabs.get("lofs")), G, KP, _lib.stream()),
                "oni_ws_tables")
 
 

@@ -41,7 +41,7 @@ class OniGibbs(C.Structure):
 class OniWsTabs(C.Structure):
     """Mirror of ``struct OniWsTabs`` in csrc/kernels/gibbs_ws.hip (word-sparse sampler tables)."""
 
-    _fields_ = [("llen", vp), ("lk", vp), ("la", vp), ("b", vp), ("stats", vp)]
+    _fields_ = [("llen", vp), ("lk", vp), ("la", vp), ("b", vp), ("stats", vp), ("lofs", vp)]
 
 
 _SIGS = {
@@ -56,7 +56,8 @@ _SIGS = {
     "oni_gibbs_launch": [C.POINTER(OniGibbs), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp],
     "oni_gibbs_sizeof_args": [],
     "oni_gibbs_ws_launch": [C.POINTER(OniGibbs), C.POINTER(OniWsTabs), C.c_int, C.c_int, vp],
-    "oni_ws_tables": [vp, vp, i64, C.c_int, C.c_int, f32, f32, vp, vp, vp, vp, vp],
+    "oni_ws_tables": [vp, vp, i64, C.c_int, C.c_int, f32, f32, vp, vp, vp, vp, vp, C.c_int, C.c_int, vp],
+    "oni_gibbs_wsg_launch": [C.POINTER(OniGibbs), C.POINTER(OniWsTabs), C.c_int, C.c_int, C.c_int, vp],
     "oni_widen_pair": [vp, vp, i64, vp, vp],
     "oni_quantile_pick": [vp, vp, C.c_int, C.c_int, C.c_int, vp, vp, vp],
     "oni_tail_grid": [],

@@ -409,6 +409,118 @@ def gibbs_pass_ws(st: dict, G: int, K: int, alpha: float, seed0: int, seed1: int
     st["dnk"] += d[live].sum(axis=0).astype(np.int32)
 
 
+def ws_lane_offsets(llen: np.ndarray, lk: np.ndarray, G: int, KP: int) -> np.ndarray:
+    """u32 per word: byte g = index of the first list entry whose topic is in lane g's range
+    [g·KP, (g+1)·KP) (entries are ascending, so each lane's entries are contiguous)."""
+    V = llen.shape[0]
+    out = np.zeros(V, dtype=np.uint32)
+    j = np.arange(lk.shape[1])[None, :]
+    for g in range(1, G):
+        first = ((lk < g * KP) & (j < llen[:, None])).sum(axis=1).astype(np.uint32)
+        out |= first << np.uint32(8 * g)
+    return out
+
+
+def gibbs_pass_wsg(st: dict, G: int, KP: int, K: int, alpha: float, seed0: int, seed1: int, sweep: int,
+                   chunk_len: np.ndarray, tabs: tuple):
+    """One sweep of the word-sparse sampler on G-lane units (k_gibbs_wsg, csrc/kernels/gibbs_ws.hip):
+    lane g owns topics [g·KP, (g+1)·KP) of its chunk's doc counts; its part of the weight is
+    T_g = W_g + R_g with W_g = fma chain over the word's list entries in its range, R_g = the lane's
+    smoothing bucket (fma chain over its topics of (n + α)·b at chunk start, ± b per count change).
+    Lanes combine by the Hillis-Steele scan; the draw picks the first lane with incl > thr, then
+    inside it the first entry with cum > thr - excl, or else its smoothing walk."""
+    S = 64 // G
+    KS = G * KP
+    llen, lk, la, b = tabs[:4]
+    slc, lane = _chunk_geometry(st, S)
+    doc = st["chunk_doc"]
+    live = doc >= 0
+    C = doc.shape[0]
+    n = np.zeros((C, KS), dtype=np.int32)
+    n[live] = st["ndk_src"][doc[live]]
+    n_start = n.copy()
+    clen = np.where(live, chunk_len, 0)
+    a32 = F32(alpha)
+    R = np.zeros((C, G), dtype=F32)
+    base = np.arange(G) * KP
+    for j in range(KP):
+        ks = base + j
+        R = fma_f32(n[:, ks].astype(F32) + a32, np.broadcast_to(b[ks], (C, G)), R)
+    for s in range(int(clen.max(initial=0))):
+        act = np.nonzero(clen > s)[0]
+        A = act.size
+        ar = np.arange(A)
+        idx = st["slice_off"][slc[act]] + s * S + lane[act]
+        w = st["tok_word"][idx].astype(np.int64)
+        pos = st["chunk_pos0"][act].astype(U32) + U32(s)
+        rr = token_rand(pos, st["chunk_key"][act], sweep, 1, seed0, seed1)
+        zo = st["tok_z"][idx].astype(np.int64)
+        n[act, zo] -= 1
+        R[act, zo // KP] = R[act, zo // KP] - b[zo]
+        L = llen[w].astype(np.int64)
+        maxL = int(L.max(initial=0))
+        W = np.zeros((A, G), dtype=F32)
+        cum = np.zeros((A, max(maxL, 1)), dtype=F32)
+        for j in range(maxL):
+            m = j < L
+            kj = lk[w, j].astype(np.int64)
+            gj = kj // KP
+            Wn = fma_f32(n[act, kj].astype(F32) + a32, la[w, j], W[ar, gj])
+            W[ar[m], gj[m]] = Wn[m]
+            cum[:, j] = np.where(m, Wn, 0)
+        T = W + R[act]
+        incl = T.copy()
+        d = 1
+        while d < G:
+            prev = incl.copy()
+            incl[:, d:] = prev[:, d:] + prev[:, :-d]
+            d <<= 1
+        excl = np.zeros_like(incl)
+        excl[:, 1:] = incl[:, :-1]
+        thr = u01(rr) * incl[:, -1]
+        gs = np.minimum((incl <= thr[:, None]).sum(axis=1), G - 1)
+        t = thr - excl[ar, gs]
+        Ws = W[ar, gs]
+        zn = np.zeros(A, dtype=np.int64)
+        inw = t < Ws
+        jj = np.arange(cum.shape[1])[None, :]
+        in_lane = (jj < L[:, None]) & ((lk[w, :cum.shape[1]].astype(np.int64) // KP) == gs[:, None])
+        hit = in_lane & (cum > t[:, None])
+        first = np.argmax(hit, axis=1)
+        last = cum.shape[1] - 1 - np.argmax(in_lane[:, ::-1], axis=1)
+        jsel = np.where(hit.any(axis=1), first, last)
+        zn[inw] = lk[w[inw], jsel[inw]]
+        sm = np.nonzero(~inw)[0]
+        if sm.size:
+            rows = act[sm]
+            t2 = t[sm] - Ws[sm]
+            acc = np.zeros(sm.size, dtype=F32)
+            found = np.zeros(sm.size, dtype=bool)
+            g_ = gs[sm]
+            zs = np.minimum(g_ * KP + KP, K) - 1
+            for j in range(KP):
+                k = g_ * KP + j
+                real = k < K
+                acc = np.where(real, fma_f32(n[rows, np.minimum(k, KS - 1)].astype(F32) + a32, b[np.minimum(k, KS - 1)],
+                                             acc), acc)
+                h = real & ~found & (acc > t2)
+                zs[h] = k[h]
+                found |= h
+            zn[sm] = zs
+        n[act, zn] += 1
+        R[act, zn // KP] = R[act, zn // KP] + b[zn]
+        ch = zn != zo
+        st["tok_z"][idx[ch]] = zn[ch].astype(np.uint8)
+        np.add.at(st["dnwk"], (w[ch], zo[ch]), -1)
+        np.add.at(st["dnwk"], (w[ch], zn[ch]), 1)
+    d = n - n_start
+    multi = live & (st["chunk_multi"] != 0)
+    single = live & ~multi
+    st["ndk_dst"][doc[single]] = n[single]
+    np.add.at(st["ndk_dst"], doc[multi], d[multi])
+    st["dnk"] += d[live].sum(axis=0).astype(np.int32)
+
+
 def gibbs_apply(nwk, dcur, dnk_cur, nk_cur, K, beta, vbeta):
     """Returns (nwk', nk', q) exactly as k_apply computes them."""
     nwk = nwk + dcur

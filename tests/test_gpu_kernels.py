@@ -99,7 +99,11 @@ def _toy_tokens(n_docs, V, seed, heavy=True):
                                     (100, "recount+lds5"), (50, "recount+lds5"), (50, "wdelta+lds5"),
                                     (100, "dual+lds5"), (100, "wdelta+ws"), (100, "recount+ws"), (100, "atomic+ws"),
                                     (100, "dual+ws"), (100, "delta+ws"), (50, "wdelta+ws"), (20, "wdelta+ws"),
-                                    (20, "recount+ws"), (7, "atomic+ws"), (200, "wdelta+ws"), (32, "delta+ws")])
+                                    (20, "recount+ws"), (7, "atomic+ws"), (200, "wdelta+ws"), (32, "delta+ws"),
+                                    (100, "wdelta+wsg"), (100, "recount+wsg"), (100, "atomic+wsg"),
+                                    (100, "dual+wsg"), (100, "delta+wsg"), (50, "wdelta+wsg"), (64, "recount+wsg"),
+                                    (80, "wdelta+wsg"), (40, "atomic+wsg"), (48, "wdelta+wsg"), (200, "wdelta+wsg"),
+                                    (20, "recount+wsg")])
 def test_gibbs_bitwise_vs_oracle(gpu, K, mode):
     tdoc, tword, keys = _toy_tokens(300, 400, K)
     G, KP = ops.choose_tiling(K)
@@ -110,10 +114,13 @@ def test_gibbs_bitwise_vs_oracle(gpu, K, mode):
     sampler = mode.split("+")[1] if "+" in mode else "auto"
     mg = GibbsLDA(cg, GibbsConfig(K=K, seed=1234, use_graph=False, count_mode=mode.split("+")[0], sampler=sampler))
     if sampler != "auto":
-        assert (mg.qpf in (2, 5, 9)) == (sampler in ("lds", "ldsq", "lds5")) or sampler == "ws"
+        assert (mg.qpf in (2, 5, 9)) == (sampler in ("lds", "ldsq", "lds5")) or sampler in ("ws", "wsg")
+    if sampler == "wsg":  # the G-lane word-sparse kernel wherever its tiling is compiled
+        assert ("lofs" in mg._ws_tabs) == ((G, KP) in ops.WSG_TILES)
     # the oracle replays the numerics the device sampler uses (fma chain for the LDS samplers)
     mc = GibbsLDA(cc, GibbsConfig(K=K, seed=1234, use_graph=False, count_mode="atomic",
-                                  sampler="ws" if sampler == "ws" else ("lds" if mg.qpf in (2, 5, 9) else "plain")))
+                                  sampler=sampler if sampler in ("ws", "wsg") else
+                                  ("lds" if mg.qpf in (2, 5, 9) else "plain")))
     if mode.startswith("wdelta"):
         assert mg.mode == 4
     mc.initialize()
@@ -129,6 +136,14 @@ def test_gibbs_bitwise_vs_oracle(gpu, K, mode):
         assert torch.equal(mc.nwk, mg.nwk.cpu())
         assert torch.equal(mc.nk_cur, mg.nk_cur.cpu())
         assert torch.equal(mc.q, mg.q.cpu())
+    if mg._ws_tabs is not None:
+        tc, tg = mc._ws_tabs, {k: v.cpu() for k, v in mg._ws_tabs.items() if isinstance(v, torch.Tensor)}
+        for k in ("llen", "b", "lofs"):
+            if k in tg:
+                assert torch.equal(tc[k], tg[k]), k
+        live = torch.arange(tc["lk"].shape[1])[None, :] < tc["llen"][:, None]  # entries past llen: stale
+        for k in ("lk", "la"):
+            assert torch.equal(tc[k][live], tg[k][live]), k
     # invariants
     T = cg.T
     assert int(mg.nwk[:, :K].sum()) == T == int(mg.ndk_cur[:, :K].sum()) == int(mg.nk_cur[:K].sum())
