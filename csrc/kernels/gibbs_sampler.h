@@ -1040,8 +1040,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OCC, 8))
   // Philox blocks are shared by the unit: lane g holds the block of 4-token group gbase + g, so
   // the unit computes one block per G·4 tokens instead of every lane computing one per 4 tokens
   // (the 36 quarter-rate integer multiplies of a block were ≈30 % of the sampler's issue slots)
+  //
+  // The refresh is wave-uniform: every kRefresh = 4G - 3 steps each unit recomputes the G blocks
+  // that cover its next kRefresh tokens (any alignment of pos0 fits in G groups). A per-unit
+  // refresh (when the token leaves the unit's G groups) is taken by SOME unit of the wave on most
+  // steps -- 64 % of them at G = 4, 99 % at G = 2 -- and a block costs 36 quarter-rate multiplies
+  // whoever is masked off; the same blocks at a uniform cadence give the same draws bitwise.
+  constexpr int kRefresh = 4 * G - 3;
   uint32_t gbase = pos0 >> 2;
   oni::U4 r = oni::philox10(oni::U4{gbase + (uint32_t)g, key, sweep, 1u}, a.seed0, a.seed1);
+  int next_refresh = kRefresh;
   uint32_t wprev = oni::kPadWord;
   float qv[KP], qn[KP];
 #pragma unroll
@@ -1051,10 +1059,43 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OCC, 8))
   int z_nx = len > 0 ? (int)a.tok_z[off + c] : 0;
   uint32_t w_nx2 = (QP && len > 1) ? a.tok_word[off + S + c] : oni::kPadWord;
   if (QP && w_nx != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)w_nx * KS + kbase, qn);
+  // Deferred bookkeeping: a changed token's stores/atomics are issued in the NEXT step, right
+  // after that step's token-stream loads. Every vector-memory op retires through the wave's in-order vmcnt
+  // counter, so a store issued at the end of a step made the step's closing wait (for the next
+  // token's word/topic) wait out a full store round trip as well; issued a step later, it drains
+  // behind the step's math. MODE 3/4 stream the word-sorted slot with the token (WPF) instead
+  // of loading it after the draw. Nothing in the kernel reads these locations: same results.
+  constexpr bool WPF = MODE == 3 || MODE == 4;
+  int32_t p_nx = (WPF && len > 0) ? a.wpos[off + c] : 0;
+  bool pend = false;
+  int64_t p_idx = 0;
+  int p_zo = 0, p_zn = 0;
+  int32_t p_pw = 0;
+  uint32_t p_w = 0;
+  uint64_t p_m = 0;
+  int64_t p_mi = -1;
+  auto flush = [&]() {
+    if (pend) {
+      a.tok_z[p_idx] = (uint8_t)p_zn;
+      if constexpr (MODE == 3) a.z_w[p_pw] = (uint8_t)p_zn;
+      if constexpr (MODE == 4) mark_changed_w(a, p_pw, p_zo, p_zn);
+      if constexpr (MODE == 1) {
+        atomicAdd(&a.dnwk[(int64_t)p_w * KS + p_zo], -1);
+        atomicAdd(&a.dnwk[(int64_t)p_w * KS + p_zn], 1);
+      }
+      pend = false;
+    }
+    if constexpr (MODE == 2) {
+      if (p_mi >= 0) a.chg_mask[p_mi] = p_m;
+      p_mi = -1;
+    }
+  };
   for (int s = 0; s < len; ++s) {
     const int64_t idx = off + (int64_t)s * S + c;
     const uint32_t w = w_nx;
     const int zo = z_nx;
+    const int32_t pw = p_nx;
+    if (WPF && s + 1 < len) p_nx = a.wpos[idx + S];
     if constexpr (QP) {
       w_nx = w_nx2;
       if (s + 1 < len) z_nx = a.tok_z[idx + S];
@@ -1069,13 +1110,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OCC, 8))
       w_nx = a.tok_word[idx + S];
       z_nx = a.tok_z[idx + S];
     }
+    flush();  // after the token-stream loads: their wait at the step's end covers a store that had the whole step
+    if (s == next_refresh) {  // wave-uniform (before the pad test: every lane takes it together)
+      next_refresh += kRefresh;
+      gbase = (pos0 + (uint32_t)s) >> 2;
+      r = oni::philox10(oni::U4{gbase + (uint32_t)g, key, sweep, 1u}, a.seed0, a.seed1);
+    }
     if (w == oni::kPadWord) continue;  // uniform across the G lanes of a unit
     const uint32_t pos = pos0 + (uint32_t)s;
     const uint32_t gi = pos >> 2;
-    if (gi - gbase >= (uint32_t)G) {  // uniform within the unit
-      gbase = gi;
-      r = oni::philox10(oni::U4{gbase + (uint32_t)g, key, sweep, 1u}, a.seed0, a.seed1);
-    }
     const uint32_t rr = (uint32_t)__shfl((int)oni::pick4(r, pos & 3u), (int)(gi - gbase), G);
     const unsigned zlo = (unsigned)(zo - kbase);
     if (zlo < (unsigned)KP) rowf[zlo] -= 1.0f;
@@ -1109,20 +1152,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OCC, 8))
     const bool changed = zn != zo && g == 0;
     if (changed) {
       ++nchg;
-      a.tok_z[idx] = (uint8_t)zn;
-      if constexpr (MODE == 3) a.z_w[a.wpos[idx]] = (uint8_t)zn;
-      if constexpr (MODE == 4) mark_changed_w(a, a.wpos[idx], zo, zn);
-      if constexpr (MODE == 1) {
-        atomicAdd(&a.dnwk[(int64_t)w * KS + zo], -1);
-        atomicAdd(&a.dnwk[(int64_t)w * KS + zn], 1);
-      }
+      pend = true;
+      p_idx = idx;
+      p_zo = zo;
+      p_zn = zn;
+      p_pw = pw;
+      p_w = w;
     }
     if constexpr (MODE == 2) {
       // lane 0 (c = 0) owns the slice's longest chunk, so it is active at every step
       const uint64_t m = __ballot(changed);
-      if (lane == 0) a.chg_mask[(off + (int64_t)s * S) / S] = m;
+      if (lane == 0) {
+        p_m = m;
+        p_mi = (off + (int64_t)s * S) / S;
+      }
     }
   }
+  flush();
   if (a.chg_count) add_wave_count(a.chg_count, nchg);
   // ---- epilogue (as k_gibbs): doc rows + per-topic totals ----------------------------------------
   int32_t d[KP], n[KP];

@@ -378,8 +378,10 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_wsg(const OniGibbs a, const On
   const uint32_t key = live ? a.chunk_key[chunk] : 0u;
   const uint32_t pos0 = live ? (uint32_t)a.chunk_pos0[chunk] : 0u;
   const uint32_t sweep = *a.sweep_ctr;
+  constexpr int kRefresh = 4 * G - 3;  // wave-uniform Philox refresh, as k_gibbs_ldsg
   uint32_t gbase = pos0 >> 2;
   oni::U4 r = oni::philox10(oni::U4{gbase + (uint32_t)g, key, sweep, 1u}, a.seed0, a.seed1);
+  int next_refresh = kRefresh;
   uint32_t wcur = oni::kPadWord;
   int jb = 0, nb = 0;
   float la_r[E];
@@ -400,13 +402,14 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_wsg(const OniGibbs a, const On
       w_nx = a.tok_word[idx + S];
       z_nx = a.tok_z[idx + S];
     }
+    if (s == next_refresh) {
+      next_refresh += kRefresh;
+      gbase = (pos0 + (uint32_t)s) >> 2;
+      r = oni::philox10(oni::U4{gbase + (uint32_t)g, key, sweep, 1u}, a.seed0, a.seed1);
+    }
     if (w == oni::kPadWord) continue;  // uniform across the G lanes of a unit
     const uint32_t pos = pos0 + (uint32_t)s;
     const uint32_t gi = pos >> 2;
-    if (gi - gbase >= (uint32_t)G) {  // uniform within the unit
-      gbase = gi;
-      r = oni::philox10(oni::U4{gbase + (uint32_t)g, key, sweep, 1u}, a.seed0, a.seed1);
-    }
     const uint32_t rr = (uint32_t)__shfl((int)oni::pick4(r, pos & 3u), (int)(gi - gbase), G);
     const float* lap = t.la + (int64_t)w * KS;
     const uint8_t* lkp = t.lk + (int64_t)w * KS;
