@@ -453,6 +453,34 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) 
 
   oni::U4 r{0, 0, 0, 0};
   int nchg = 0;
+  // deferred bookkeeping (as k_gibbs_ldsg): a changed token's stores are issued in the next step,
+  // after its q-row and token-stream loads, so the wait for those loads at the top of the step
+  // after does not also wait out the stores (vmcnt retires in issue order)
+  bool pend = false;
+  int64_t p_idx = 0;
+  int p_zo = 0, p_zn = 0;
+  int32_t p_pw = 0;
+  uint32_t p_w = 0;
+  uint64_t p_m = 0;
+  int64_t p_mi = -1;
+  auto flush = [&]() {
+    if constexpr (!DZ) {
+      if (pend) {
+        a.tok_z[p_idx] = (uint8_t)p_zn;
+        if constexpr (MODE == 3) a.z_w[p_pw] = (uint8_t)p_zn;
+        if constexpr (MODE == 4) mark_changed_w(a, p_pw, p_zo, p_zn);
+        if (ATOMIC) {
+          atomicAdd(&a.dnwk[(int64_t)p_w * KS + p_zo], -1);
+          atomicAdd(&a.dnwk[(int64_t)p_w * KS + p_zn], 1);
+        }
+        pend = false;
+      }
+      if constexpr (MODE == 2) {
+        if (p_mi >= 0) a.chg_mask[p_mi] = p_m;
+        p_mi = -1;
+      }
+    }
+  };
   for (int s = 0; s < len; ++s) {
     const int64_t idx = off + (int64_t)s * S + c;
     const uint32_t w = w0;
@@ -472,6 +500,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) 
     } else {
       w1 = oni::kPadWord;
     }
+    flush();
     if (w != oni::kPadWord) {
       const uint32_t pos = pos0 + (uint32_t)s;
       if (s == 0 || (pos & 3u) == 0u) r = oni::philox10(oni::U4{pos >> 2, key, sweep, 1u}, a.seed0, a.seed1);
@@ -497,17 +526,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) 
         if (zn != zo) zb[s * S + c] = (uint8_t)zn;
       } else if (zn != zo) {
         ++nchg;
-        a.tok_z[idx] = (uint8_t)zn;
-        if constexpr (MODE == 3) a.z_w[pw] = (uint8_t)zn;
-        if constexpr (MODE == 4) mark_changed_w(a, pw, zo, zn);
-        if (ATOMIC) {
-          atomicAdd(&a.dnwk[(int64_t)w * KS + zo], -1);
-          atomicAdd(&a.dnwk[(int64_t)w * KS + zn], 1);
-        }
+        pend = true;
+        p_idx = idx;
+        p_zo = zo;
+        p_zn = zn;
+        p_pw = pw;
+        p_w = w;
       }
       if constexpr (MODE == 2 && !DZ) {
         const uint64_t m = __ballot(zn != zo);
-        if (lane == 0) a.chg_mask[(off + (int64_t)s * S) / S] = m;
+        if (lane == 0) {
+          p_m = m;
+          p_mi = (off + (int64_t)s * S) / S;
+        }
       }
     }
     if (fetch) {
@@ -515,6 +546,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) 
       for (int j = 0; j < KP; ++j) qv[j] = qn[j];
     }
   }
+  flush();
 
   // ---- epilogue: doc rows + per-topic totals (as k_gibbs, G = 1) --------------------------------
   if (a.chg_count) add_wave_count(a.chg_count, nchg);

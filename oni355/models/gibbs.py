@@ -212,6 +212,12 @@ class GibbsLDA:
                 self.ws, self._ws_tabs = None, None
             else:
                 self._air = _alpha_in_row_exact(self.alpha, max_len)
+        # auto sampler, one-lane units: the wdelta sweeps (after the auto switch) run the two-deep
+        # token stream k_gibbs_q2, whose loads now wait only for stores a step old (deferred
+        # bookkeeping): 0.2565 -> 0.2438 ms per K = 20 sweep; recount sweeps keep the one-step
+        # prefetch k_gibbs (q2 1-2 % slower there; profiles/r3/ab_q2_deferred_k20_burn*.json).
+        # Same draws bitwise either way.
+        self.qpf_wdelta = SAMPLERS["q2"] if (cfg.sampler == "auto" and self.G == 1) else self.qpf
         self.a = 0  # ndk parity
         self.b = 0  # delta-buffer parity
         self.cn = 0  # nk parity
@@ -431,7 +437,7 @@ class GibbsLDA:
             ops.ws_tables(self.nwk, self.nk[self.cn], self.K, self.beta, self.vbeta, self._ws_tabs)
         ops.gibbs_pass(self._state(False), self.G, self.KP, self.K, self.alpha, self.cfg.seed, False,
                        self.sweep_ctr, c.chunk_len, host_sweep=self.sweeps_done + 1, mode=mode,
-                       prefetch_q=ops.WS_SAMPLER if use_ws else self.qpf,
+                       prefetch_q=ops.WS_SAMPLER if use_ws else (self.qpf_wdelta if mode == 4 else self.qpf),
                        chg_mask=self.wbits if mode == 4 else getattr(self, "chg_mask", None), wpos=c.wpos,
                        z_w=getattr(self, "z_w", None), zz_w=getattr(self, "zz_w", None), alpha_in_row=self._air,
                        ws_tabs=self._ws_tabs if use_ws else None)
