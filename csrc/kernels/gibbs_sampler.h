@@ -190,6 +190,39 @@ __device__ __forceinline__ void dz_flush(const OniGibbs& a, const uint32_t* __re
   }
 }
 
+// Philox blocks at a wave-uniform cadence for samplers with one chain per lane. A lane needs a
+// new block whenever its token position enters a new 4-token group; with 64 chunks at random
+// phases some lane does so on every step, so the wave issued a whole block (36 quarter-rate
+// multiplies) per step for a quarter of its lanes. Here every lane refreshes together every 4
+// steps and computes only the block of the group AFTER its current one (within a 4-step window a
+// position lies in one of two consecutive groups, and the current group's block is the previous
+// refresh's "next"): one block per lane per 4 steps, the same values, the same draws bitwise.
+struct PhiloxPair {
+  oni::U4 cur, nxt;
+  uint32_t pos0, key, sweep, stream;
+  __device__ __forceinline__ void init(uint32_t p0, uint32_t k, uint32_t sw, uint32_t st, const OniGibbs& a) {
+    pos0 = p0;
+    key = k;
+    sweep = sw;
+    stream = st;
+    nxt = oni::philox10(oni::U4{pos0 >> 2, key, sweep, stream}, a.seed0, a.seed1);
+    cur = nxt;
+  }
+  // call with every s, before any lane-divergent exit (the refresh is wave-uniform)
+  __device__ __forceinline__ void step(int s, const OniGibbs& a) {
+    if ((s & 3) == 0) {
+      cur = nxt;
+      nxt = oni::philox10(oni::U4{((pos0 + (uint32_t)s) >> 2) + 1u, key, sweep, stream}, a.seed0, a.seed1);
+    }
+  }
+  __device__ __forceinline__ uint32_t pick(int s) const {
+    const uint32_t pos = pos0 + (uint32_t)s;
+    const bool second = (pos >> 2) != ((pos0 + (uint32_t)(s & ~3)) >> 2);
+    const uint32_t i = pos & 3u;
+    return second ? oni::pick4(nxt, i) : oni::pick4(cur, i);  // value selects: no addressed copy
+  }
+};
+
 // MODE: 0 = no n_wk bookkeeping (full recount afterwards), 1 = per-token Δ atomics,
 //       2 = changed-slot ballot mask per step (delta recount afterwards),
 //       3 = changed topics also scattered into the word-sorted copy z_w (streaming recount afterwards)
@@ -227,7 +260,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) 
   const uint32_t sweep = INIT ? 0u : *a.sweep_ctr;
   const uint32_t stream = INIT ? 0u : 1u;
 
-  oni::U4 r{0, 0, 0, 0};
+  PhiloxPair rng;
+  rng.init(pos0, key, sweep, stream, a);
   uint32_t wprev = oni::kPadWord;
   // QPF: qn always holds the q row of the current token's word (it is refilled at the end of a
   // step only when the next word differs, so a repeated word finds its row still there) and the
@@ -268,10 +302,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) 
       if (!INIT) z_nx = DZ ? (int)zb[(s + 1) * S + c] : (int)a.tok_z[idx + S];
       if (WPF) p_nx = a.wpos[idx + S];
     }
+    rng.step(s, a);
     if (w == oni::kPadWord) continue;  // uniform across the G lanes of a unit
-    const uint32_t pos = pos0 + (uint32_t)s;
-    if (s == 0 || (pos & 3u) == 0u) r = oni::philox10(oni::U4{pos >> 2, key, sweep, stream}, a.seed0, a.seed1);
-    const uint32_t rr = oni::pick4(r, pos & 3u);
+    const uint32_t rr = rng.pick(s);
     if constexpr (INIT) {
       const int z = (int)__umulhi(rr, (uint32_t)a.K);
 #pragma unroll
@@ -451,7 +484,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) 
   for (int j = 0; j < KP; ++j) qv[j] = qn[j] = 0.f;
   if (w0 != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)w0 * KS, qv);
 
-  oni::U4 r{0, 0, 0, 0};
+  PhiloxPair rng;
+  rng.init(pos0, key, sweep, 1u, a);
   int nchg = 0;
   // deferred bookkeeping (as k_gibbs_ldsg): a changed token's stores are issued in the next step,
   // after its q-row and token-stream loads, so the wait for those loads at the top of the step
@@ -501,10 +535,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) 
       w1 = oni::kPadWord;
     }
     flush();
+    rng.step(s, a);
     if (w != oni::kPadWord) {
-      const uint32_t pos = pos0 + (uint32_t)s;
-      if (s == 0 || (pos & 3u) == 0u) r = oni::philox10(oni::U4{pos >> 2, key, sweep, 1u}, a.seed0, a.seed1);
-      const uint32_t rr = oni::pick4(r, pos & 3u);
+      const uint32_t rr = rng.pick(s);
 #pragma unroll
       for (int j = 0; j < KP; ++j) n[j] -= (j == zo);
       float loc[KP];
