@@ -223,6 +223,35 @@ struct PhiloxPair {
   }
 };
 
+// A changed token's bookkeeping, held back one step (see k_gibbs_ldsg "Deferred bookkeeping").
+struct PendZ {
+  bool on = false;
+  int64_t idx = 0;
+  int zo = 0, zn = 0;
+  int32_t pw = 0;
+  uint32_t w = 0;
+  uint64_t m = 0;       // MODE 2: the step's change ballot ...
+  uint64_t* mdst = nullptr;  // ... and where lane 0 stores it
+};
+
+template <int MODE>
+__device__ __forceinline__ void flush_pend(const OniGibbs& a, PendZ& p, int KS) {
+  if (p.on) {
+    a.tok_z[p.idx] = (uint8_t)p.zn;
+    if constexpr (MODE == 3) a.z_w[p.pw] = (uint8_t)p.zn;
+    if constexpr (MODE == 4) mark_changed_w(a, p.pw, p.zo, p.zn);
+    if constexpr (MODE == 1) {
+      atomicAdd(&a.dnwk[(int64_t)p.w * KS + p.zo], -1);
+      atomicAdd(&a.dnwk[(int64_t)p.w * KS + p.zn], 1);
+    }
+    p.on = false;
+  }
+  if constexpr (MODE == 2) {
+    if (p.mdst) *p.mdst = p.m;
+    p.mdst = nullptr;
+  }
+}
+
 // MODE: 0 = no n_wk bookkeeping (full recount afterwards), 1 = per-token Δ atomics,
 //       2 = changed-slot ballot mask per step (delta recount afterwards),
 //       3 = changed topics also scattered into the word-sorted copy z_w (streaming recount afterwards)
@@ -812,8 +841,8 @@ template <int KP>
 __device__ __forceinline__ int count_le(const float (&P)[KP], float excl, float thr);
 
 template <int KP, int MODE, int P, bool AIR>
-__device__ __forceinline__ void lds_step(const OniGibbs& a, int s, int len, int64_t off, int lane, uint32_t key,
-                                         uint32_t pos0, uint32_t sweep, float4* __restrict__ row, oni::U4& r,
+__device__ __forceinline__ void lds_step(const OniGibbs& a, int s, int len, int64_t off, int lane,
+                                         float4* __restrict__ row, PhiloxPair& rng, PendZ& pend,
                                          uint32_t (&wq)[2], int (&zq)[2], int32_t (&pq)[2], const float (&qc)[KP],
                                          float (&qn)[KP], uint64_t* chg_word, int& nchg) {
   constexpr int KS = KP;
@@ -828,11 +857,11 @@ __device__ __forceinline__ void lds_step(const OniGibbs& a, int s, int len, int6
     if constexpr (MODE == 3 || MODE == 4) pq[P] = a.wpos[idx + 128];
   }
   if (s + 1 < len && wq[1 - P] != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)wq[1 - P] * KS, qn);
-  const uint32_t pos = pos0 + (uint32_t)s;
-  if (s == 0 || (pos & 3u) == 0u) r = oni::philox10(oni::U4{pos >> 2, key, sweep, 1u}, a.seed0, a.seed1);
+  flush_pend<MODE>(a, pend, KS);  // the previous step's stores, behind this step's loads
+  rng.step(s, a);
   bool changed = false;
   if (w != oni::kPadWord) {
-    const uint32_t rr = oni::pick4(r, pos & 3u);
+    const uint32_t rr = rng.pick(s);
     rowf[zo] = rowf[zo] - 1.0f;
     float Pc[KP];
     float run = 0.f;
@@ -855,18 +884,20 @@ __device__ __forceinline__ void lds_step(const OniGibbs& a, int s, int len, int6
     changed = zn != zo;
     nchg += changed;
     if (changed) {
-      a.tok_z[idx] = (uint8_t)zn;
-      if constexpr (MODE == 3) a.z_w[wp] = (uint8_t)zn;
-      if constexpr (MODE == 4) mark_changed_w(a, wp, zo, zn);
-      if constexpr (MODE == 1) {
-        atomicAdd(&a.dnwk[(int64_t)w * KS + zo], -1);
-        atomicAdd(&a.dnwk[(int64_t)w * KS + zn], 1);
-      }
+      pend.on = true;
+      pend.idx = idx;
+      pend.zo = zo;
+      pend.zn = zn;
+      pend.pw = wp;
+      pend.w = w;
     }
   }
   if constexpr (MODE == 2) {
     const uint64_t m = __ballot(changed);
-    if (lane == 0) chg_word[s] = m;
+    if (lane == 0) {
+      pend.m = m;
+      pend.mdst = chg_word + s;
+    }
   }
 }
 
@@ -901,7 +932,9 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_lds(const OniGibbs a) {
   const uint32_t pos0 = live ? (uint32_t)a.chunk_pos0[chunk] : 0u;
   const uint32_t sweep = *a.sweep_ctr;
   uint64_t* chg_word = MODE == 2 ? a.chg_mask + off / 64 : nullptr;
-  oni::U4 r{0, 0, 0, 0};
+  PhiloxPair rng;
+  rng.init(pos0, key, sweep, 1u, a);
+  PendZ pend;
   float qa[KP], qb[KP];
 #pragma unroll
   for (int j = 0; j < KP; ++j) qa[j] = qb[j] = 0.f;
@@ -918,10 +951,11 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_lds(const OniGibbs a) {
   }
   if (wq[0] != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)wq[0] * KS, qa);
   for (int s = 0; s < len; s += 2) {
-    lds_step<KP, MODE, 0, AIR>(a, s, len, off, lane, key, pos0, sweep, row, r, wq, zq, pq, qa, qb, chg_word, nchg);
+    lds_step<KP, MODE, 0, AIR>(a, s, len, off, lane, row, rng, pend, wq, zq, pq, qa, qb, chg_word, nchg);
     if (s + 1 < len)
-      lds_step<KP, MODE, 1, AIR>(a, s + 1, len, off, lane, key, pos0, sweep, row, r, wq, zq, pq, qb, qa, chg_word, nchg);
+      lds_step<KP, MODE, 1, AIR>(a, s + 1, len, off, lane, row, rng, pend, wq, zq, pq, qb, qa, chg_word, nchg);
   }
+  flush_pend<MODE>(a, pend, KS);
   if (a.chg_count) add_wave_count(a.chg_count, nchg);
   // epilogue: counts back to ints, doc rows, per-topic totals (n0 re-read: keeps it out of VGPRs)
   const float* rowf = reinterpret_cast<const float*>(row);
