@@ -89,7 +89,7 @@ def main() -> int:
                 head = m.dn[m.b][: m.V * m.KS].view(m.V, m.KS)
                 if stage == 0:
                     ops.gibbs_pass(m._state(False), m.G, m.KP, m.K, m.alpha, m.cfg.seed, False, m.sweep_ctr,
-                                   c.chunk_len, mode=md, prefetch_q=m.qpf,
+                                   c.chunk_len, mode=md, sampler=m.qpf, alpha_in_row=m._air,
                                    chg_mask=m.wbits if md == 4 else getattr(m, "chg_mask", None), wpos=c.wpos,
                                    z_w=getattr(m, "z_w", None), zz_w=getattr(m, "zz_w", None))
                 elif stage == 1 and md == 0:
@@ -106,7 +106,7 @@ def main() -> int:
                     ops.recount(c.wsorted, None, m.z_w, head, m.KS)
                     ops.STREAM_RECOUNT = not ops.STREAM_RECOUNT
                 elif stage == 2:
-                    ops.gibbs_apply(m.nwk, m.dn[m.b], m.dn[1 - m.b], m.nk[m.cn], m.nk[1 - m.cn], m.q, m.V, m.K, m.KS,
+                    ops.gibbs_apply(m.nwk, m.dn[m.b], m.dn[1 - m.b], m.nk[m.cn], m.nk[1 - m.cn], m.q, m.qfix, m.V, m.K, m.KS,
                                     m.beta, m.vbeta, m.sweep_ctr, bump=False, absolute=md in (0, 3))
                 ev[1].record()
                 torch.cuda.synchronize()

@@ -408,8 +408,9 @@ void decode(const uint8_t* base, const Pkt& p, int64_t pkt, Rows* r) {
 // proto) into OPEN datagrams; a datagram closes as soon as its pieces cover [0, end of the last
 // (MF = 0) fragment) without a hole, and the row takes the frame time / length / index of the
 // fragment that completed it (tshark's view). The 16-bit IP id wraps within a day-long capture, so
-// a group is also closed (as incomplete) when a fragment offset it already holds shows up again --
-// that is the next datagram with the same id -- or when the new fragment arrives more than
+// a group is also closed (as incomplete) when a fragment offset it already holds shows up again with
+// different bytes -- that is the next datagram with the same id (an exact duplicate of a held piece
+// is dropped) -- or when the new fragment arrives more than
 // kFragTimeoutNs of frame time after the group's first one (the kernel's ipfrag_time is 30 s).
 constexpr int64_t kFragTimeoutNs = 30ll * 1000000000ll;
 
@@ -458,7 +459,16 @@ void reassemble(std::vector<Frag>& fr, Rows* r) {
     auto it = open.find(key);
     if (it != open.end()) {
       bool restart = f.ts_ns - it->second.first_ts > kFragTimeoutNs;
-      for (const Frag* p : it->second.parts) restart |= p->off == f.off;
+      bool duplicate = false;
+      for (const Frag* p : it->second.parts) {
+        if (p->off != f.off) continue;
+        // an exact copy of a piece the group holds (mirror / SPAN captures duplicate packets) is
+        // dropped, as tshark's reassembly does; a different payload at a held offset is the next
+        // datagram reusing the id
+        if (p->more == f.more && p->data == f.data) duplicate = true;
+        else restart = true;
+      }
+      if (duplicate && !restart) continue;
       if (restart) {
         ++r->frag_incomplete;
         open.erase(it);

@@ -85,8 +85,9 @@ __global__ __launch_bounds__(kTailVals * 64) void k_tail_final(const double* __r
   if (lane == 0) out[j] = v;
 }
 
-// 256 rows per block: thread t sums row t's counts (n_d is a sum of integer counts, exact in f32
-// below 2^24 in any order) into LDS, then the block reads and writes its rows' KS columns
+// 256 rows per block: thread t sums row t's counts in int64 (exact for any document: averaged
+// posterior counts are S times a document's length and pass 2^24 for heavy IPs) and rounds the
+// sum to f32 once, into LDS, then the block reads and writes its rows' KS columns
 // coalesced (a row per thread touched KS scattered words per lane).
 __global__ __launch_bounds__(256) void k_theta_rows(const int32_t* __restrict__ n, int64_t D, int K, int KS, float add,
                                                     float den_add, float* __restrict__ th) {
@@ -95,9 +96,9 @@ __global__ __launch_bounds__(256) void k_theta_rows(const int32_t* __restrict__ 
     const int64_t d = r0 + threadIdx.x;
     if (d < D) {
       const int32_t* r = n + d * KS;
-      float nd = 0.f;
-      for (int k = 0; k < K; ++k) nd += (float)r[k];
-      den[threadIdx.x] = nd + den_add;
+      int64_t nd = 0;
+      for (int k = 0; k < K; ++k) nd += r[k];
+      den[threadIdx.x] = (float)nd + den_add;
     }
     __syncthreads();
     const int64_t rows = D - r0 < 256 ? D - r0 : 256;

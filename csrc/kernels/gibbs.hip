@@ -25,15 +25,18 @@
 
 namespace {
 
-// Delta apply + q refresh: n_wk += Δ; n_k' = n_k + Δn_k; q = (n_wk+β)/(n_k'+Vβ); zero the other
-// delta buffer for the next sweep; bump the device sweep counter. nk/dnwk are ping-ponged by the
+// Delta apply + q refresh: n_wk += Δ; n_k' = n_k + Δn_k; q = (n_wk+β)/(n_k'+Vβ); the token-exclusion
+// constants qfix = (A, B) with D = n_k' + Vβ, A = D/(D−1), B = 1/(D−1) (A = 1, B = 0 for empty
+// topics; see gibbs_sampler.h); zero the other delta buffer for the next sweep; bump the device
+// sweep counter. nk/dnwk are ping-ponged by the
 // host so no block ever reads what another block of this launch writes.
 // With n_rows > 0 the same launch also seeds the NEXT sweep's long-document rows (rdst[r] :=
 // rsrc[r]: chunked documents add their Δn_dk atomically into a copy of the current counts), which
 // saves the separate k_copy_rows launch per sweep.
 __global__ __launch_bounds__(256) void k_apply(int32_t* __restrict__ nwk, const int32_t* __restrict__ dcur,
                                                 int32_t* __restrict__ dother, const int32_t* __restrict__ nk_cur,
-                                                int32_t* __restrict__ nk_next, float* __restrict__ q, int64_t V,
+                                                int32_t* __restrict__ nk_next, float* __restrict__ q,
+                                                float* __restrict__ qfix, int64_t V,
                                                 int K, int KS, float beta, float vbeta, uint32_t* sweep_ctr,
                                                 int bump, int absolute, int nk_rep, const int32_t* __restrict__ rsrc,
                                                 int32_t* __restrict__ rdst, const int32_t* __restrict__ rows,
@@ -62,7 +65,13 @@ __global__ __launch_bounds__(256) void k_apply(int32_t* __restrict__ nwk, const 
   }
   __syncthreads();
   if (blockIdx.x == 0) {
-    for (int k = threadIdx.x; k < KS; k += blockDim.x) nk_next[k] = nkn[k];
+    for (int k = threadIdx.x; k < KS; k += blockDim.x) {
+      nk_next[k] = nkn[k];
+      const float dm1 = den[k] - 1.0f;
+      const bool ok = k < K && nkn[k] >= 1;
+      qfix[k] = ok ? den[k] / dm1 : 1.0f;
+      qfix[KS + k] = ok ? 1.0f / dm1 : 0.0f;
+    }
     for (int k = threadIdx.x; k < nk_rep * KS + kDnAux; k += blockDim.x) dother[V * KS + k] = 0;
     if (threadIdx.x == 0 && bump) *sweep_ctr += 1u;
   }
@@ -406,14 +415,15 @@ ONI_API int oni_gibbs_sizeof_args() { return (int)sizeof(OniGibbs); }
 
 // rsrc/rdst/rows/n_rows: optional fused long-row copy for the next sweep (n_rows = 0: none).
 ONI_API int oni_gibbs_apply(int32_t* nwk, const int32_t* dcur, int32_t* dother, const int32_t* nk_cur,
-                            int32_t* nk_next, float* q, int64_t V, int K, int KS, float beta, float vbeta,
+                            int32_t* nk_next, float* q, float* qfix, int64_t V, int K, int KS, float beta, float vbeta,
                             uint32_t* sweep_ctr, int bump, int absolute, int nk_rep, const int32_t* rsrc,
                             int32_t* rdst, const int32_t* rows, int64_t n_rows, hipStream_t s) {
-  if (KS % 4 != 0 || KS > 256 || nk_rep < 1 || (nk_rep & (nk_rep - 1))) return (int)hipErrorInvalidValue;
+  if (KS % 4 != 0 || KS > 256 || nk_rep < 1 || (nk_rep & (nk_rep - 1)) || qfix == nullptr)
+    return (int)hipErrorInvalidValue;
   if (n_rows < 0 || (n_rows > 0 && (rsrc == nullptr || rdst == nullptr || rows == nullptr)))
     return (int)hipErrorInvalidValue;
   const int64_t work = V * KS / 4 > n_rows * KS ? V * KS / 4 : n_rows * KS;
-  k_apply<<<oni::grid_for(work, 256, 2048), 256, 0, s>>>(nwk, dcur, dother, nk_cur, nk_next, q, V, K, KS, beta,
+  k_apply<<<oni::grid_for(work, 256, 2048), 256, 0, s>>>(nwk, dcur, dother, nk_cur, nk_next, q, qfix, V, K, KS, beta,
                                                           vbeta, sweep_ctr, bump, absolute, nk_rep, rsrc, rdst, rows,
                                                           n_rows);
   return (int)hipGetLastError();

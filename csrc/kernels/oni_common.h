@@ -24,8 +24,10 @@ struct U4 { uint32_t x, y, z, w; };
 __device__ __forceinline__ U4 philox10(U4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
-    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    // one 32x32->64 multiply per product (v_mad_u64_u32) instead of separate lo / hi halves
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+    const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
     c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;

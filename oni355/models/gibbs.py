@@ -30,9 +30,8 @@ from .corpus import Corpus, canonical_tokens
 NK_REP = 32
 # X01 payload packing pays only once the all-reduce is bandwidth-bound (see GibbsLDA._x01_wanted)
 X01_PACK_MIN_BYTES = 4 << 20
-DZ_MAX_LEN = 128  # kDzMaxLen (csrc/kernels/gibbs_sampler.h)
-SAMPLERS = {"pp": 1, "plain": 0, "lds": 2, "qpf": 4, "ldsq": 5, "q2": 6, "dz": 7, "q2dz": 8, "lds5": 9,
-            "ws": 10, "wsa": 10, "wsg": 10}  # -> oni_gibbs_launch qpf argument
+# sweep kernels (-> oni_gibbs_launch variant argument): every one draws the same topics bit for bit
+SAMPLERS = {"generic": 0, "lds": 2, "x1": 3}
 
 
 @dataclass
@@ -63,12 +62,10 @@ class GibbsConfig:
     check_invariants: bool = field(default_factory=lambda: os.environ.get("ONI_CHECK_INVARIANTS", "0") == "1")
     # cheap numerical health check after every sweep() call (ONI_HEALTH_CHECK=0 disables)
     health_check: bool = field(default_factory=lambda: os.environ.get("ONI_HEALTH_CHECK", "1") != "0")
-    # sweep kernel: "auto" (default: "qpf" for K ≤ 32, "lds" above — the measured winners),
-    # "qpf" one-step q-row prefetch, "plain" q-row load on each word change, "pp" ping-pong
-    # registers + 2-step token prefetch, "lds" LDS-staged doc counts (fma numerics; for K > 32 the
-    # multi-lane k_gibbs_ldsg: 1.59 → 1.06 ms per 25M-token sweep at K = 100, 0.80 → 0.57 at K = 50).
-    # ONI_SAMPLER overrides the default. All but "lds" are bitwise identical to each other; "lds"
-    # is bitwise identical to the oracle's fma numerics.
+    # sweep kernel: "auto" (default: "x1" for K ≤ 32, "lds" above), "x1" the one-lane register
+    # sampler k_gibbs_x1, "lds" the multi-lane LDS-count sampler k_gibbs_ldsg, "generic" k_gibbs
+    # (any unit width; the fallback when n + α is not exact in f32). ONI_SAMPLER overrides the
+    # default. All are bitwise identical to each other and to the NumPy oracle (spec.gibbs_pass).
     sampler: str = field(default_factory=lambda: os.environ.get("ONI_SAMPLER", "auto"))
     # posterior averaging: θ and φ are estimated from the counts of the last ``post_samples``
     # samples taken every ``post_every`` sweeps (ending at the last sweep) instead of the final
@@ -148,6 +145,8 @@ class GibbsLDA:
         n_split = self._split["n"] if self._split is not None else 0
         self.dn = [torch.empty(self._split_off + n_split * KS, dtype=i32, device=dev) for _ in range(2)]
         self.q = torch.zeros(V, KS, dtype=torch.float32, device=dev)
+        # token-exclusion constants of the word side (A, B per topic; written with q by k_apply)
+        self.qfix = torch.zeros(2, KS, dtype=torch.float32, device=dev)
         self.sweep_ctr = torch.zeros(1, dtype=i32, device=dev)
         if cfg.count_mode not in ("auto", "dual", "delta", "recount", "atomic", "wdelta"):
             raise ValueError(f"unknown count_mode {cfg.count_mode}")
@@ -182,42 +181,21 @@ class GibbsLDA:
         if self.mode == 2:
             self.tok_zprev = torch.zeros_like(self.tok_z)
             self.chg_mask = torch.zeros(max(corpus.sell_slots // corpus.S, 1), dtype=torch.int64, device=dev)
-        # the LDS sampler keeps counts as f32 integers: exact below 2^24 tokens per document
         if cfg.sampler not in SAMPLERS and cfg.sampler != "auto":
             raise ValueError(f"unknown sampler {cfg.sampler}")
-        self.qpf = SAMPLERS[cfg.sampler] if cfg.sampler != "auto" else (SAMPLERS["qpf"] if self.G == 1 else
-                                                                         SAMPLERS["lds"])
-        # word-sparse sampler (k_gibbs_ws): "ws" on every sweep; "wsa" only in the sweeps after the
-        # auto count mode's switch (the word lists are short once topics have settled; the early
-        # sweeps keep the dense sampler); "wsg" the G-lane variant (k_gibbs_wsg: the dense LDS
-        # sampler's layout, each lane walking the word's entries in its topic range)
-        self.ws = None
-        if cfg.sampler in ("ws", "wsa", "wsg"):
-            if cfg.K > 240:
-                raise ValueError("the word-sparse sampler supports K <= 240")
-            self.ws = "delta" if (cfg.sampler == "wsa" and self.auto) else "always"
-            self.qpf = SAMPLERS["qpf"] if self.G == 1 else SAMPLERS["lds"]
-        # (other tilings -- G = 8/16 at K > 112 -- run the one-lane k_gibbs_ws over the same corpus)
-        lanes = (self.G, self.KP) if (cfg.sampler == "wsg" and (self.G, self.KP) in ops.WSG_TILES) else None
-        self._ws_tabs = ops.ws_alloc(self.V, self.KS, dev, lanes) if self.ws else None
-        if self.qpf in (5, 9) and self.G == 1:
-            self.qpf = 2
-        if self.qpf in (7, 8) and (self.G != 1 or corpus.L > DZ_MAX_LEN):
-            self.qpf = 4  # "dz" stages one slice's topics in LDS: one-lane units, chunks ≤ 128 tokens  # "ldsq" (LDS counts + q-row prefetch) is the multi-lane variant; G = 1 has "lds"
-        self._air = False  # n + α LDS rows (LDS samplers only)
-        if self.qpf in (2, 5, 9) or self.ws:
-            max_len = corpus.max_doc_len()  # one device read, only the LDS samplers need it
-            if max_len >= (1 << 24):
-                self.qpf = 1  # LDS rows hold counts as f32: exact below 2^24
-                self.ws, self._ws_tabs = None, None
-            else:
-                self._air = _alpha_in_row_exact(self.alpha, max_len)
-        # auto sampler, one-lane units: the wdelta sweeps (after the auto switch) run the two-deep
-        # token stream k_gibbs_q2, whose loads now wait only for stores a step old (deferred
-        # bookkeeping): 0.2565 -> 0.2438 ms per K = 20 sweep; recount sweeps keep the one-step
-        # prefetch k_gibbs (q2 1-2 % slower there; profiles/r3/ab_q2_deferred_k20_burn*.json).
-        # Same draws bitwise either way.
-        self.qpf_wdelta = SAMPLERS["q2"] if (cfg.sampler == "auto" and self.G == 1) else self.qpf
+        if cfg.sampler == "auto":
+            self.qpf = SAMPLERS["x1"] if self.G == 1 else SAMPLERS["lds"]
+        else:
+            self.qpf = SAMPLERS[cfg.sampler]
+            if (self.qpf == SAMPLERS["x1"]) != (self.G == 1) and self.qpf != SAMPLERS["generic"]:
+                raise ValueError(f"sampler {cfg.sampler} does not run {self.G}-lane units (K = {cfg.K})")
+        # the specialised kernels keep n + α as f32 in their count rows: exact only when every
+        # n + α of this corpus is (one device read of the longest document); else generic
+        self._air = False
+        if self.qpf != SAMPLERS["generic"]:
+            self._air = _alpha_in_row_exact(self.alpha, corpus.max_doc_len())
+            if not self._air:
+                self.qpf = SAMPLERS["generic"]
         self.a = 0  # ndk parity
         self.b = 0  # delta-buffer parity
         self.cn = 0  # nk parity
@@ -281,7 +259,7 @@ class GibbsLDA:
         # the sampler reads chunk_pos0 only as the Philox position: split pieces use global ones
         st = dict(tok_word=c.tok_word, tok_z=self.tok_z, slice_off=c.slice_off, slice_len=c.slice_len,
                   chunk_doc=c.chunk_doc, chunk_pos0=c.chunk_rng0 if c.chunk_rng0 is not None else c.chunk_pos0,
-                  chunk_key=c.chunk_key, chunk_multi=c.chunk_multi, q=self.q)
+                  chunk_key=c.chunk_key, chunk_multi=c.chunk_multi, q=self.q, qfix=self.qfix)
         VK = self.V * self.KS
         if init:
             st.update(ndk_src=self.ndk[0], ndk_dst=self.ndk[0], dnwk=self.nwk, dnk=self.nk[0])
@@ -413,7 +391,8 @@ class GibbsLDA:
         VK = self.V * self.KS
         self.dn[0].zero_()
         so = self._split_off
-        ops.gibbs_apply(self.nwk, self.dn[0][:so], self.dn[1][:so], self.nk[self.cn], self.nk[1 - self.cn], self.q, self.V,
+        ops.gibbs_apply(self.nwk, self.dn[0][:so], self.dn[1][:so], self.nk[self.cn], self.nk[1 - self.cn], self.q,
+                        self.qfix, self.V,
                         self.K, self.KS, self.beta, self.vbeta, self.sweep_ctr, bump=False,
                         rows_copy=(self.ndk[self.a], self.ndk[1 - self.a], self.c.long_rows))
         self.cn = 1 - self.cn
@@ -431,16 +410,10 @@ class GibbsLDA:
             self._ensure_zw()
         # long (chunked) documents add their Δn_dk into ndk[1-a] rows that hold a copy of ndk[a]:
         # every apply -- the previous sweep's, or _prime()'s after init / resume -- seeds that copy
-        use_ws = self.ws == "always" or (self.ws == "delta" and mode == self.mode)
-        if use_ws:
-            # the word side is the sweep-start snapshot: its sparse tables are built once per sweep
-            ops.ws_tables(self.nwk, self.nk[self.cn], self.K, self.beta, self.vbeta, self._ws_tabs)
         ops.gibbs_pass(self._state(False), self.G, self.KP, self.K, self.alpha, self.cfg.seed, False,
-                       self.sweep_ctr, c.chunk_len, host_sweep=self.sweeps_done + 1, mode=mode,
-                       prefetch_q=ops.WS_SAMPLER if use_ws else (self.qpf_wdelta if mode == 4 else self.qpf),
+                       self.sweep_ctr, c.chunk_len, host_sweep=self.sweeps_done + 1, mode=mode, sampler=self.qpf,
                        chg_mask=self.wbits if mode == 4 else getattr(self, "chg_mask", None), wpos=c.wpos,
-                       z_w=getattr(self, "z_w", None), zz_w=getattr(self, "zz_w", None), alpha_in_row=self._air,
-                       ws_tabs=self._ws_tabs if use_ws else None)
+                       z_w=getattr(self, "z_w", None), zz_w=getattr(self, "zz_w", None), alpha_in_row=self._air)
         head = self.dn[self.b][: self.V * self.KS].view(self.V, self.KS)
         if mode == 4:
             # dn[b] head := Δn_wk of the tokens marked in the word-sorted change bitmap
@@ -463,7 +436,7 @@ class GibbsLDA:
             self._split_apply(self.dn[self.b], self.ndk[self.a], self.ndk[1 - self.a])
         so = self._split_off
         ops.gibbs_apply(self.nwk, self.dn[self.b][:so], self.dn[1 - self.b][:so], self.nk[self.cn], self.nk[1 - self.cn],
-                        self.q, self.V, self.K, self.KS, self.beta, self.vbeta, self.sweep_ctr, bump=True,
+                        self.q, self.qfix, self.V, self.K, self.KS, self.beta, self.vbeta, self.sweep_ctr, bump=True,
                         absolute=mode in (0, 3), rows_copy=(self.ndk[1 - self.a], self.ndk[self.a], c.long_rows))
         self.a, self.b, self.cn = 1 - self.a, 1 - self.b, 1 - self.cn
         self.sweeps_done += 1
@@ -750,7 +723,7 @@ class GibbsLDA:
         if self._avg_cache is None:
             S, K = float(a["n"]), self.K
             n = a["dk"].to(torch.float32)
-            nd = n[:, :K].sum(1, keepdim=True)
+            nd = a["dk"][:, :K].to(torch.int64).sum(1, keepdim=True).to(torch.float32)  # as k_theta_rows
             th = (n + S * self.alpha) / (nd + S * K * self.alpha)
             th[:, K:] = 0
             den = a["k"].to(torch.float32) + np.float32(S) * self.vbeta
@@ -777,7 +750,7 @@ class GibbsLDA:
         if self.device.type == "cuda":
             return ops.theta_rows(self.ndk_cur, self.K, self.alpha, self.K * self.alpha)
         n = self.ndk_cur.to(torch.float32)
-        nd = n[:, : self.K].sum(1, keepdim=True)
+        nd = self.ndk_cur[:, : self.K].to(torch.int64).sum(1, keepdim=True).to(torch.float32)
         th = (n + self.alpha) / (nd + self.K * self.alpha)
         th[:, self.K:] = 0
         return th.contiguous()

@@ -354,31 +354,28 @@ def sell_perm_z(chunk_doc, chunk_pos0, chunk_len, S, slice_off, doc_tok_ptr, tok
 # ------------------------------------------------------------------------------------------------
 def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init: bool, sweep_ctr: torch.Tensor,
                chunk_len: torch.Tensor, host_sweep: int | None = None, mode: int = 1,
-               prefetch_q: bool | int = False, chg_mask: torch.Tensor | None = None, wpos: torch.Tensor | None = None,
+               sampler: int = 0, chg_mask: torch.Tensor | None = None, wpos: torch.Tensor | None = None,
                z_w: torch.Tensor | None = None, zz_w: torch.Tensor | None = None,
-               alpha_in_row: bool = False, ws_tabs: dict | None = None) -> None:
-    """Launch one init/sweep pass. ``st`` holds the OniGibbs tensors (see csrc/kernels/gibbs.hip).
+               alpha_in_row: bool = False) -> None:
+    """Launch one init/sweep pass. ``st`` holds the OniGibbs tensors (csrc/kernels/gibbs_sampler.h);
+    sweeps also need ``st["qfix"]`` ([2, KS] f32, from :func:`gibbs_apply`).
 
     ``mode`` 1: accumulate Δn_wk with per-token atomics; 0: the caller rebuilds n_wk with
     :func:`recount`; 2: record changed slots in ``chg_mask`` for :func:`delta_recount`; 3: also
     write changed topics into the word-sorted copy ``z_w`` (via ``wpos``) for a streaming recount;
     4: changed tokens set their word-sorted bit in ``chg_mask`` (int32 bitmap) and record
     old | new << 8 in ``zz_w`` (int16, word-sorted) for :func:`wdelta_recount`.
-    ``prefetch_q`` (sampler variant) 0: register sampler, q row loaded on a word change; 1: ping-pong
-    register sampler; 4: one-step q prefetch; 2: LDS-staged doc counts with fma numerics (k_gibbs_lds
-    for G = 1, k_gibbs_ldsg for G > 1); 5: as 2 with a one-step q-row prefetch (G > 1); 9: as 2 with a
-    5-wave register budget (G > 1); 10: the word-sparse sampler k_gibbs_ws (sweeps only; ``ws_tabs``
-    from :func:`ws_tables` of the sweep-start counts; any corpus unit width G).
+    ``sampler`` (kernel variant; every variant draws the same topics bit for bit): 0 = generic
+    k_gibbs, 2 = k_gibbs_ldsg (G > 1), 3 = k_gibbs_x1 (G = 1); the specialised kernels need
+    ``alpha_in_row`` (n + α exact in f32 for every count of the corpus), else the generic one runs.
     """
-    ws = int(prefetch_q) == WS_SAMPLER and not init
-    if ws and ws_tabs is None:
-        raise ValueError("the word-sparse sampler needs its per-sweep tables (ws_tables)")
-    atomic = mode == 1
     s0, s1 = spec.split_seed(seed)
     KS = G * KP
     nk_rep = st["dnk"].numel() // KS
     if nk_rep < 1 or nk_rep * KS != st["dnk"].numel() or nk_rep & (nk_rep - 1):
         raise ValueError("dnk must hold a power-of-two number of [KS] replicas")
+    if not init and (st.get("qfix") is None or st["qfix"].numel() != 2 * KS):
+        raise ValueError("a sweep needs the [2, KS] token-exclusion table qfix")
     if mode == 4:
         T = int(zz_w.numel()) if zz_w is not None else 0
         if (wpos is None or zz_w is None or chg_mask is None or wpos.numel() != st["tok_word"].numel()
@@ -390,18 +387,12 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
         npst = {k: (v.numpy().view(np.uint32) if k in ("tok_word", "chunk_key") else v.numpy())
                 for k, v in st.items() if v is not None}
         npst["dnk"] = npst["dnk"][:KS]  # replica 0 (the sum over replicas is what counts)
-        if not atomic:
+        if mode != 1:
             npst["dnwk"] = np.zeros_like(npst["dnwk"])  # discarded: recount rebuilds n_wk
+        if not init:
+            npst["qfix"] = npst["qfix"].reshape(2, KS)
         sweep_no = int(host_sweep if host_sweep is not None else sweep_ctr.item())
-        if ws and _wsg(ws_tabs, G):
-            spec.gibbs_pass_wsg(npst, G, KP, K, alpha, s0, s1, sweep_no, chunk_len.numpy(),
-                                tuple(ws_tabs[k].numpy() for k in ("llen", "lk", "la", "b")))
-        elif ws:
-            spec.gibbs_pass_ws(npst, G, K, alpha, s0, s1, sweep_no, chunk_len.numpy(),
-                               tuple(ws_tabs[k].numpy() for k in ("llen", "lk", "la", "b")))
-        else:
-            spec.gibbs_pass(npst, G, KP, K, alpha, s0, s1, init, sweep_no, chunk_len.numpy(),
-                            fma=(int(prefetch_q) in (2, 5, 9) and not init))
+        spec.gibbs_pass(npst, G, KP, K, alpha, s0, s1, init, sweep_no, chunk_len.numpy())
         if mode == 3:
             valid = wpos >= 0
             z_w[wpos[valid].long()] = st["tok_z"][valid]
@@ -424,6 +415,8 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
     for name in ("tok_word", "tok_z", "slice_off", "slice_len", "chunk_doc", "chunk_pos0", "chunk_key",
                  "chunk_multi", "ndk_src", "ndk_dst", "q", "dnwk", "dnk"):
         setattr(a, name, _lib.ptr(st[name]))
+    if not init:
+        a.qfix = _lib.ptr(st["qfix"])
     a.sweep_ctr = _lib.ptr(sweep_ctr)
     if mode == 2:
         if chg_mask is None or chg_mask.numel() * (64 // G) < st["tok_word"].numel():
@@ -441,65 +434,8 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
     a.nk_rep = nk_rep
     # the caller vouches that n + α is exact in f32 for every doc-topic count of this corpus
     a.flags = 1 if alpha_in_row else 0
-    if ws:
-        t = _lib.OniWsTabs()
-        t.llen, t.lk, t.la, t.b = (_lib.ptr(ws_tabs[k]) for k in ("llen", "lk", "la", "b"))
-        if ws_tabs.get("stats") is not None:  # diagnostics: see tools/ws_probe.py
-            t.stats = _lib.ptr(ws_tabs["stats"])
-        if _wsg(ws_tabs, G):
-            t.lofs = _lib.ptr(ws_tabs["lofs"])
-            _lib.check(_lib.lib().oni_gibbs_wsg_launch(C.byref(a), C.byref(t), G, KP, int(mode), _lib.stream()),
-                       "oni_gibbs_wsg_launch")
-            return
-        _lib.check(_lib.lib().oni_gibbs_ws_launch(C.byref(a), C.byref(t), G, int(mode), _lib.stream()),
-                   "oni_gibbs_ws_launch")
-        return
-    _lib.check(_lib.lib().oni_gibbs_launch(C.byref(a), G, KP, 1 if init else 0, int(mode),
-                                           int(prefetch_q), _lib.stream()),
-               "oni_gibbs_launch")
-
-
-WS_SAMPLER = 10  # prefetch_q code of the word-sparse sampler (k_gibbs_ws / k_gibbs_wsg)
-WSG_TILES = {(2, 20), (2, 24), (2, 28), (4, 16), (4, 20), (4, 24), (4, 28)}  # oni_gibbs_wsg_launch
-
-
-def _wsg(ws_tabs: dict, G: int) -> bool:
-    """The G-lane word-sparse sampler (k_gibbs_wsg) runs when the tables carry lane offsets."""
-    return G > 1 and ws_tabs.get("lofs") is not None
-
-
-def ws_alloc(V: int, KS: int, device, lanes: tuple | None = None) -> dict:
-    """Device (or CPU) tables of the word-sparse sampler, rebuilt every sweep by :func:`ws_tables`.
-    ``lanes`` = (G, KP) adds the per-word lane offsets of the G-lane sampler (k_gibbs_wsg)."""
-    t = dict(llen=torch.zeros(max(V, 1), dtype=torch.int32, device=device),
-             lk=torch.zeros(max(V, 1), KS, dtype=torch.uint8, device=device),
-             la=torch.zeros(max(V, 1), KS, dtype=torch.float32, device=device),
-             b=torch.zeros(KS, dtype=torch.float32, device=device))
-    if lanes is not None and lanes[0] > 1:
-        t["lofs"] = torch.zeros(max(V, 1), dtype=torch.int32, device=device)
-        t["lanes"] = tuple(lanes)
-    return t
-
-
-def ws_tables(nwk: torch.Tensor, nk: torch.Tensor, K: int, beta: float, vbeta: float, tabs: dict) -> None:
-    """Word-sparse sampler tables from the sweep-start n_wk / n_k (k_ws_tables): per word the topics
-    with n_wk > 0 (ascending) and a_wk = n_wk/(n_k + Vβ); b_k = β/(n_k + Vβ)."""
-    V, KS = nwk.shape
-    if not _is_dev(nwk):
-        llen, lk, la, b = spec.ws_tables(nwk.numpy(), nk.numpy(), K, beta, vbeta)
-        tabs["llen"][:V].copy_(torch.from_numpy(llen))
-        tabs["lk"][:V].copy_(torch.from_numpy(lk))
-        tabs["la"][:V].copy_(torch.from_numpy(la))
-        tabs["b"].copy_(torch.from_numpy(b))
-        if tabs.get("lofs") is not None:
-            G, KP = tabs["lanes"]
-            tabs["lofs"][:V].copy_(torch.from_numpy(spec.ws_lane_offsets(llen, lk, G, KP).view(np.int32)))
-        return
-    G, KP = tabs.get("lanes", (1, KS))
-    _lib.check(_lib.lib().oni_ws_tables(_lib.ptr(nwk), _lib.ptr(nk), V, K, KS, float(beta), float(vbeta),
-                                        *(_lib.ptr(tabs[k]) for k in ("llen", "lk", "la", "b")),
-                                        _lib.ptr(tabs.get("lofs")), G, KP, _lib.stream()),
-               "oni_ws_tables")
+    _lib.check(_lib.lib().oni_gibbs_launch(C.byref(a), G, KP, 1 if init else 0, int(mode), int(sampler),
+                                           _lib.stream()), "oni_gibbs_launch")
 
 
 def delta_recount(wslot, tile_wlo, tile_whi, chg_mask, tok_word, tok_z, tok_zprev, dnwk_out, KS: int, G: int) -> None:
@@ -578,9 +514,10 @@ def recount(wsorted, wslot, tok_z, nwk_out, KS: int) -> None:
 STREAM_RECOUNT = True  # k_recount_reg (register runs) 0.065 ms vs k_recount (LDS) 0.093 ms, both at 8 KB LDS
 
 
-def gibbs_apply(nwk, dcur, dother, nk_cur, nk_next, q, V, K, KS, beta, vbeta, sweep_ctr, bump=True, absolute=False,
-                rows_copy=None):
-    """n_wk ← Δ (or absolute), n_k ← n_k + Σ_replicas Δn_k, q refresh; zeroes ``dother``.
+def gibbs_apply(nwk, dcur, dother, nk_cur, nk_next, q, qfix, V, K, KS, beta, vbeta, sweep_ctr, bump=True,
+                absolute=False, rows_copy=None):
+    """n_wk ← Δ (or absolute), n_k ← n_k + Σ_replicas Δn_k, q refresh (+ the token-exclusion
+    table ``qfix`` [2, KS]); zeroes ``dother``.
 
     ``dcur``/``dother`` are [V·KS + R·KS + DN_AUX]: the Δn_wk table, R replicas of Δn_k, then
     DN_AUX auxiliary words ([0] = tokens that changed topic; all-reduced with the rest).
@@ -588,14 +525,17 @@ def gibbs_apply(nwk, dcur, dother, nk_cur, nk_next, q, V, K, KS, beta, vbeta, sw
     nk_rep = (dcur.numel() - V * KS - DN_AUX) // KS
     if nk_rep < 1 or V * KS + nk_rep * KS + DN_AUX != dcur.numel():
         raise ValueError("Δ buffer must be [V*KS + nk_rep*KS + DN_AUX]")
+    if qfix.numel() != 2 * KS or qfix.dtype != torch.float32:
+        raise ValueError("qfix must be a [2, KS] float32 table")
     if not _is_dev(nwk):
         base = np.zeros_like(nwk.numpy()) if absolute else nwk.numpy()
-        n2, nk2, q2 = spec.gibbs_apply(base, dcur[: V * KS].view(V, KS).numpy(),
-                                       dcur[V * KS: V * KS + nk_rep * KS].view(-1, KS).sum(0, dtype=torch.int32).numpy(),
-                                       nk_cur.numpy(), K, beta, vbeta)
+        n2, nk2, q2, qf = spec.gibbs_apply(base, dcur[: V * KS].view(V, KS).numpy(),
+                                           dcur[V * KS: V * KS + nk_rep * KS].view(-1, KS).sum(0, dtype=torch.int32).numpy(),
+                                           nk_cur.numpy(), K, beta, vbeta)
         nwk.copy_(torch.from_numpy(n2))
         nk_next.copy_(torch.from_numpy(nk2))
         q.copy_(torch.from_numpy(q2))
+        qfix.copy_(torch.from_numpy(qf).view_as(qfix))
         dother.zero_()
         if bump:
             sweep_ctr += 1
@@ -603,7 +543,7 @@ def gibbs_apply(nwk, dcur, dother, nk_cur, nk_next, q, V, K, KS, beta, vbeta, sw
             copy_rows(*rows_copy, KS)
         return
     rs, rd, rr = rows_copy if rows_copy is not None and rows_copy[2].numel() else (None, None, None)
-    _lib.check(_lib.lib().oni_gibbs_apply(*map(_lib.ptr, (nwk, dcur, dother, nk_cur, nk_next, q)), V, K, KS,
+    _lib.check(_lib.lib().oni_gibbs_apply(*map(_lib.ptr, (nwk, dcur, dother, nk_cur, nk_next, q, qfix)), V, K, KS,
                                           float(beta), float(vbeta), _lib.ptr(sweep_ctr), 1 if bump else 0,
                                           1 if absolute else 0, nk_rep, _lib.ptr(rs) if rs is not None else None,
                                           _lib.ptr(rd) if rd is not None else None,

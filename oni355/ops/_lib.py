@@ -26,22 +26,16 @@ vp, i32, i64, f32, u32 = C.c_void_p, C.c_int32, C.c_int64, C.c_float, C.c_uint32
 
 
 class OniGibbs(C.Structure):
-    """Mirror of ``struct OniGibbs`` in csrc/kernels/gibbs.hip (size checked at load)."""
+    """Mirror of ``struct OniGibbs`` in csrc/kernels/gibbs_sampler.h (size checked at load)."""
 
     _fields_ = [
         ("tok_word", vp), ("tok_z", vp), ("slice_off", vp), ("slice_len", vp),
         ("chunk_doc", vp), ("chunk_pos0", vp), ("chunk_key", vp), ("chunk_multi", vp),
-        ("ndk_src", vp), ("ndk_dst", vp), ("q", vp), ("dnwk", vp), ("dnk", vp), ("sweep_ctr", vp), ("chg_mask", vp),
+        ("ndk_src", vp), ("ndk_dst", vp), ("q", vp), ("qfix", vp), ("dnwk", vp), ("dnk", vp), ("sweep_ctr", vp), ("chg_mask", vp),
         ("wpos", vp), ("z_w", vp), ("zz_w", vp), ("chg_count", vp),
         ("n_slices", i64), ("K", i32), ("KS", i32), ("alpha", f32), ("seed0", u32), ("seed1", u32),
         ("nk_rep", i32), ("flags", i32),
     ]
-
-
-class OniWsTabs(C.Structure):
-    """Mirror of ``struct OniWsTabs`` in csrc/kernels/gibbs_ws.hip (word-sparse sampler tables)."""
-
-    _fields_ = [("llen", vp), ("lk", vp), ("la", vp), ("b", vp), ("stats", vp), ("lofs", vp)]
 
 
 _SIGS = {
@@ -55,9 +49,6 @@ _SIGS = {
     "oni_sell_perm_z": [vp, vp, vp, i64, C.c_int, vp, vp, vp, vp, C.c_int, vp],
     "oni_gibbs_launch": [C.POINTER(OniGibbs), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp],
     "oni_gibbs_sizeof_args": [],
-    "oni_gibbs_ws_launch": [C.POINTER(OniGibbs), C.POINTER(OniWsTabs), C.c_int, C.c_int, vp],
-    "oni_ws_tables": [vp, vp, i64, C.c_int, C.c_int, f32, f32, vp, vp, vp, vp, vp, C.c_int, C.c_int, vp],
-    "oni_gibbs_wsg_launch": [C.POINTER(OniGibbs), C.POINTER(OniWsTabs), C.c_int, C.c_int, C.c_int, vp],
     "oni_widen_pair": [vp, vp, i64, vp, vp],
     "oni_quantile_pick": [vp, vp, C.c_int, C.c_int, C.c_int, vp, vp, vp],
     "oni_tail_grid": [],
@@ -65,7 +56,7 @@ _SIGS = {
                       vp, vp, vp],
     "oni_theta_rows": [vp, i64, C.c_int, C.c_int, f32, f32, vp, vp],
     "oni_phi_rows": [vp, vp, i64, C.c_int, C.c_int, f32, f32, vp, vp],
-    "oni_gibbs_apply": [vp, vp, vp, vp, vp, vp, i64, C.c_int, C.c_int, f32, f32, vp, C.c_int, C.c_int, C.c_int,
+    "oni_gibbs_apply": [vp, vp, vp, vp, vp, vp, vp, i64, C.c_int, C.c_int, f32, f32, vp, C.c_int, C.c_int, C.c_int,
                         vp, vp, vp, i64, vp],
     "oni_recount": [vp, vp, vp, i64, vp, C.c_int, C.c_int, C.c_int, vp],
     "oni_recount_stream": [vp, vp, i64, vp, C.c_int, C.c_int, C.c_int, vp],

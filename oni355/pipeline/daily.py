@@ -193,13 +193,17 @@ def run_days(source: str, dates: list[str], root: str, lpath: str, comm, kw: dic
             if got is None:
                 if not follow or (max_days and len(records) >= max_days):
                     break
-                new = _next_days(root, source, last, comm)
+                # rank 0 alone decides both the new days and the idle exit (from its own clock) and
+                # shares them: a rank leaving on its local clock while the others block in the next
+                # broadcast would hang the group
+                new, stop = _next_days(root, source, last, comm,
+                                       idle=time.perf_counter() - idle_since > idle_exit_s)
                 if new:
                     last = new[-1]
                     pipe.extend(new)
                     idle_since = time.perf_counter()
                     continue
-                if time.perf_counter() - idle_since > idle_exit_s:
+                if stop:
                     break
                 time.sleep(poll_s)
                 continue
@@ -231,16 +235,18 @@ def run_days(source: str, dates: list[str], root: str, lpath: str, comm, kw: dic
     return records
 
 
-def _next_days(root: str, source: str, after: str | None, comm) -> list[str]:
-    """Complete stored days after ``after`` -- decided by rank 0 and shared, so every rank walks
-    the same days in the same order."""
+def _next_days(root: str, source: str, after: str | None, comm, idle: bool = False) -> tuple[list[str], bool]:
+    """(complete stored days after ``after``, stop) -- both decided by rank 0 and shared, so every
+    rank walks the same days in the same order and leaves the ``--follow`` loop in the same pass.
+    ``stop`` is rank 0's ``idle`` when it found no new day."""
     days = [d for d in columnar.days(root, source) if after is None or d > after] if comm.rank == 0 else []
+    stop = bool(idle) and not days
     if comm.dist:
         import torch.distributed as dist
-        box = [days]
+        box = [(days, stop)]
         dist.broadcast_object_list(box, src=0, group=comm.host_side().group)
-        days = box[0]
-    return days
+        days, stop = box[0]
+    return days, stop
 
 
 def parse_dates(spec: str) -> list[str]:

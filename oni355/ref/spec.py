@@ -233,18 +233,56 @@ def fma_f32(a: np.ndarray, b: np.ndarray, c: np.ndarray) -> np.ndarray:
     return r.astype(F32)
 
 
+def gibbs_qfix(nk_next: np.ndarray, K: int, vbeta: float) -> np.ndarray:
+    """Per-topic constants of the token exclusion on the word side (k_apply writes them with q).
+
+    With D_k = n_k + Vβ (the sweep-start denominator of q) the word factor of a token's own topic
+    with the token removed is (n_wk − 1 + β)/(D_k − 1) = q_wk·A_k − B_k, A_k = D_k/(D_k − 1),
+    B_k = 1/(D_k − 1). Returned as [2, KS] f32 (row 0 = A, row 1 = B); topics with n_k = 0 (never a
+    token's own topic) get A = 1, B = 0."""
+    KS = nk_next.shape[0]
+    out = np.zeros((2, KS), dtype=F32)
+    out[0] = F32(1)
+    den = nk_next.astype(F32) + F32(vbeta)
+    dm1 = den - F32(1)
+    ok = (np.arange(KS) < K) & (nk_next >= 1)
+    out[0, ok] = (den[ok] / dm1[ok]).astype(F32)
+    out[1, ok] = (F32(1) / dm1[ok]).astype(F32)
+    return out
+
+
+def excluded_q(qz: np.ndarray, zo: np.ndarray, qfix: np.ndarray) -> np.ndarray:
+    """q'_{w,zo} = fma(q_{w,zo}, A_zo, −B_zo): the word factor of the token's own topic without
+    the token (the sweep-start snapshot counts every token at its sweep-start topic)."""
+    return fma_f32(qz.astype(F32), qfix[0][zo], -qfix[1][zo])
+
+
 def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed0: int, seed1: int, init: bool,
-               sweep: int, chunk_len: np.ndarray, fma: bool = False):
+               sweep: int, chunk_len: np.ndarray):
     """One init (init=True) or sweep pass over numpy state arrays, in place.
 
-    ``fma`` selects the numerics of the LDS-count samplers (k_gibbs_lds for G = 1, k_gibbs_ldsg
-    for G > 1): inside each lane's KP topics the running weight sum is
-    P_j = fma(n_j + α, q_j, P_{j-1}) instead of P_j = P_{j-1} + (n_j + α)·q_j; lanes are then
-    combined by the same Hillis-Steele scan.
+    A sweep draws every token from the collapsed conditional with the token removed from BOTH
+    sides (SURVEY.md §2.6 K10 "remove its old z"):
+
+        p_k ∝ (n_dk^¬t + α) · (n_wk^¬t + β)/(n_k^¬t + Vβ)
+
+    The doc side n_dk is exact within a chunk (sequential updates); the word side is the
+    sweep-start snapshot q (AD-LDA staleness), which counts the token itself at its sweep-start
+    topic zo, so the factor of topic zo is replaced by q' = fma(q_zo, A_zo, −B_zo)
+    (:func:`excluded_q`, st["qfix"] from :func:`gibbs_qfix`). Weight numerics (the kernels replay
+    them bit for bit):
+
+    * G = 1 (k_gibbs_x1 / k_gibbs): P_j = fma(a_j, q_j, P_{j−1}) with q_zo := q', a_j = n_j + α.
+    * G > 1 (k_gibbs_ldsg / k_gibbs): lane g chains its KP topics, P_j = fma(e_j, q_j, P_{j−1}) with
+      e_j = a_j except e_zo = a_zo · f, f = q' / q_zo (the LDS row of the owning lane is scaled for
+      the one step, the q row stays in registers); lanes are combined by a Hillis-Steele scan.
+
+    The draw is the first topic whose running weight exceeds u·total (count of P_j ≤ thr, capped
+    at K − 1).
 
     st keys: tok_word u32, tok_z u8, slice_off i64, slice_len i32, chunk_doc i32, chunk_pos0 i32,
     chunk_key u32, chunk_multi u8, ndk_src i32 [D,KS], ndk_dst i32 [D,KS], q f32 [V,KS],
-    dnwk i32 [V,KS], dnk i32 [KS].
+    qfix f32 [2,KS] (sweeps), dnwk i32 [V,KS], dnk i32 [KS].
     """
     S = 64 // G
     KS = G * KP
@@ -255,6 +293,7 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed0: int, seed
     n = np.zeros((C, KS), dtype=np.int32)
     if not init:
         n[live] = st["ndk_src"][doc[live]]
+        qfix = st["qfix"]
     n_start = n.copy()
     clen = np.where(live, chunk_len, 0)
     alpha32 = F32(alpha)
@@ -262,6 +301,8 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed0: int, seed
     sw = 0 if init else sweep
     for s in range(int(clen.max(initial=0))):
         act = np.nonzero(clen > s)[0]
+        A = act.size
+        ar = np.arange(A)
         idx = st["slice_off"][slc[act]] + s * S + lane[act]
         w = st["tok_word"][idx].astype(np.int64)
         pos = st["chunk_pos0"][act].astype(U32) + U32(s)
@@ -274,24 +315,26 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed0: int, seed
             continue
         zo = st["tok_z"][idx].astype(np.int64)
         n[act, zo] -= 1
-        qv = st["q"][w]
-        if fma:
-            # per-lane fma chains over each lane's KP topics (k_gibbs_lds / k_gibbs_ldsg)
-            av = (n[act].astype(F32) + alpha32).reshape(-1, G, KP)
-            qg = qv.reshape(-1, G, KP)
-            loc = np.empty_like(av)
-            run = np.zeros(av.shape[:2], dtype=F32)
-            for j in range(KP):
-                run = fma_f32(av[:, :, j], qg[:, :, j], run)
-                loc[:, :, j] = run
-        else:
-            p = (n[act].astype(F32) + alpha32) * qv
+        qv = st["q"][w].copy()
+        qz = qv[ar, zo]
+        qe = excluded_q(qz, zo, qfix)
+        av = n[act].astype(F32) + alpha32
         if G == 1:
-            cum = loc.reshape(-1, KS) if fma else np.cumsum(p, axis=1, dtype=F32)
+            qv[ar, zo] = qe
+        else:
+            f = (qe / qz).astype(F32)
+            av[ar, zo] = (av[ar, zo] * f).astype(F32)
+        avg = av.reshape(-1, G, KP)
+        qg = qv.reshape(-1, G, KP)
+        loc = np.empty_like(avg)
+        run = np.zeros(avg.shape[:2], dtype=F32)
+        for j in range(KP):
+            run = fma_f32(avg[:, :, j], qg[:, :, j], run)
+            loc[:, :, j] = run
+        if G == 1:
+            cum = loc.reshape(-1, KS)
             total = cum[:, -1]
         else:
-            if not fma:
-                loc = np.cumsum(p.reshape(-1, G, KP), axis=2, dtype=F32)
             incl = loc[:, :, -1].copy()
             d = 1
             while d < G:
@@ -318,217 +361,14 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed0: int, seed
     st["dnk"] += d[live].sum(axis=0).astype(np.int32)
 
 
-def ws_tables(nwk: np.ndarray, nk: np.ndarray, K: int, beta: float, vbeta: float):
-    """Per-sweep tables of the word-sparse sampler (k_ws_tables): for every word the topics with
-    n_wk > 0 (ascending) and a_wk = n_wk / (n_k + Vβ), plus b_k = β / (n_k + Vβ)."""
-    V, KS = nwk.shape
-    den = nk.astype(F32) + F32(vbeta)
-    b = np.zeros(KS, dtype=F32)
-    b[:K] = F32(beta) / den[:K]
-    m = nwk[:, :K] > 0
-    llen = m.sum(axis=1).astype(np.int32)
-    lk = np.zeros((V, KS), dtype=np.uint8)
-    la = np.zeros((V, KS), dtype=F32)
-    wi, ki = np.nonzero(m)
-    pos = (np.cumsum(m, axis=1) - 1)[wi, ki]
-    lk[wi, pos] = ki
-    la[wi, pos] = nwk[wi, ki].astype(F32) / den[ki]
-    return llen, lk, la, b
-
-
-def gibbs_pass_ws(st: dict, G: int, K: int, alpha: float, seed0: int, seed1: int, sweep: int,
-                  chunk_len: np.ndarray, tabs: tuple):
-    """One sweep of the word-sparse sampler (k_gibbs_ws, csrc/kernels/gibbs_ws.hip) over numpy
-    state arrays, in place. ``tabs`` = :func:`ws_tables` of the sweep-start counts. The corpus may
-    be laid out for any unit width G (one chain per chunk either way)."""
-    S = 64 // G
-    KS = st["ndk_src"].shape[1]
-    llen, lk, la, b = tabs
-    slc, lane = _chunk_geometry(st, S)
-    doc = st["chunk_doc"]
-    live = doc >= 0
-    C = doc.shape[0]
-    n = np.zeros((C, KS), dtype=np.int32)
-    n[live] = st["ndk_src"][doc[live]]
-    n_start = n.copy()
-    clen = np.where(live, chunk_len, 0)
-    a32 = F32(alpha)
-    R = np.zeros(C, dtype=F32)
-    for k in range(K):
-        R = fma_f32(n[:, k].astype(F32) + a32, b[k], R)
-    for s in range(int(clen.max(initial=0))):
-        act = np.nonzero(clen > s)[0]
-        idx = st["slice_off"][slc[act]] + s * S + lane[act]
-        w = st["tok_word"][idx].astype(np.int64)
-        pos = st["chunk_pos0"][act].astype(U32) + U32(s)
-        rr = token_rand(pos, st["chunk_key"][act], sweep, 1, seed0, seed1)
-        zo = st["tok_z"][idx].astype(np.int64)
-        n[act, zo] -= 1
-        R[act] = R[act] - b[zo]
-        L = llen[w].astype(np.int64)
-        maxL = int(L.max(initial=0))
-        W = np.zeros(act.size, dtype=F32)
-        cum = np.zeros((act.size, max(maxL, 1)), dtype=F32)
-        for j in range(maxL):
-            m = j < L
-            kj = lk[w, j].astype(np.int64)
-            Wn = fma_f32(n[act, kj].astype(F32) + a32, la[w, j], W)
-            W = np.where(m, Wn, W)
-            cum[:, j] = W
-        thr = u01(rr) * (W + R[act])
-        zn = np.full(act.size, K - 1, dtype=np.int64)
-        inw = thr < W
-        if inw.any():
-            gt = (cum > thr[:, None]) & (np.arange(cum.shape[1])[None, :] < L[:, None])
-            jf = np.argmax(gt, axis=1)
-            zn[inw] = lk[w[inw], jf[inw]]
-        sm = np.nonzero(~inw)[0]
-        if sm.size:
-            tt = thr[sm] - W[sm]
-            acc = np.zeros(sm.size, dtype=F32)
-            found = np.zeros(sm.size, dtype=bool)
-            zs = np.full(sm.size, K - 1, dtype=np.int64)
-            rows = act[sm]
-            for k in range(K):
-                acc = fma_f32(n[rows, k].astype(F32) + a32, b[k], acc)
-                hit = ~found & (acc > tt)
-                zs[hit] = k
-                found |= hit
-            zn[sm] = zs
-        n[act, zn] += 1
-        R[act] = R[act] + b[zn]
-        ch = zn != zo
-        st["tok_z"][idx[ch]] = zn[ch].astype(np.uint8)
-        np.add.at(st["dnwk"], (w[ch], zo[ch]), -1)
-        np.add.at(st["dnwk"], (w[ch], zn[ch]), 1)
-    d = n - n_start
-    multi = live & (st["chunk_multi"] != 0)
-    single = live & ~multi
-    st["ndk_dst"][doc[single]] = n[single]
-    np.add.at(st["ndk_dst"], doc[multi], d[multi])
-    st["dnk"] += d[live].sum(axis=0).astype(np.int32)
-
-
-def ws_lane_offsets(llen: np.ndarray, lk: np.ndarray, G: int, KP: int) -> np.ndarray:
-    """u32 per word: byte g = index of the first list entry whose topic is in lane g's range
-    [g·KP, (g+1)·KP) (entries are ascending, so each lane's entries are contiguous)."""
-    V = llen.shape[0]
-    out = np.zeros(V, dtype=np.uint32)
-    j = np.arange(lk.shape[1])[None, :]
-    for g in range(1, G):
-        first = ((lk < g * KP) & (j < llen[:, None])).sum(axis=1).astype(np.uint32)
-        out |= first << np.uint32(8 * g)
-    return out
-
-
-def gibbs_pass_wsg(st: dict, G: int, KP: int, K: int, alpha: float, seed0: int, seed1: int, sweep: int,
-                   chunk_len: np.ndarray, tabs: tuple):
-    """One sweep of the word-sparse sampler on G-lane units (k_gibbs_wsg, csrc/kernels/gibbs_ws.hip):
-    lane g owns topics [g·KP, (g+1)·KP) of its chunk's doc counts; its part of the weight is
-    T_g = W_g + R_g with W_g = fma chain over the word's list entries in its range, R_g = the lane's
-    smoothing bucket (fma chain over its topics of (n + α)·b at chunk start, ± b per count change).
-    Lanes combine by the Hillis-Steele scan; the draw picks the first lane with incl > thr, then
-    inside it the first entry with cum > thr - excl, or else its smoothing walk."""
-    S = 64 // G
-    KS = G * KP
-    llen, lk, la, b = tabs[:4]
-    slc, lane = _chunk_geometry(st, S)
-    doc = st["chunk_doc"]
-    live = doc >= 0
-    C = doc.shape[0]
-    n = np.zeros((C, KS), dtype=np.int32)
-    n[live] = st["ndk_src"][doc[live]]
-    n_start = n.copy()
-    clen = np.where(live, chunk_len, 0)
-    a32 = F32(alpha)
-    R = np.zeros((C, G), dtype=F32)
-    base = np.arange(G) * KP
-    for j in range(KP):
-        ks = base + j
-        R = fma_f32(n[:, ks].astype(F32) + a32, np.broadcast_to(b[ks], (C, G)), R)
-    for s in range(int(clen.max(initial=0))):
-        act = np.nonzero(clen > s)[0]
-        A = act.size
-        ar = np.arange(A)
-        idx = st["slice_off"][slc[act]] + s * S + lane[act]
-        w = st["tok_word"][idx].astype(np.int64)
-        pos = st["chunk_pos0"][act].astype(U32) + U32(s)
-        rr = token_rand(pos, st["chunk_key"][act], sweep, 1, seed0, seed1)
-        zo = st["tok_z"][idx].astype(np.int64)
-        n[act, zo] -= 1
-        R[act, zo // KP] = R[act, zo // KP] - b[zo]
-        L = llen[w].astype(np.int64)
-        maxL = int(L.max(initial=0))
-        W = np.zeros((A, G), dtype=F32)
-        cum = np.zeros((A, max(maxL, 1)), dtype=F32)
-        for j in range(maxL):
-            m = j < L
-            kj = lk[w, j].astype(np.int64)
-            gj = kj // KP
-            Wn = fma_f32(n[act, kj].astype(F32) + a32, la[w, j], W[ar, gj])
-            W[ar[m], gj[m]] = Wn[m]
-            cum[:, j] = np.where(m, Wn, 0)
-        T = W + R[act]
-        incl = T.copy()
-        d = 1
-        while d < G:
-            prev = incl.copy()
-            incl[:, d:] = prev[:, d:] + prev[:, :-d]
-            d <<= 1
-        excl = np.zeros_like(incl)
-        excl[:, 1:] = incl[:, :-1]
-        thr = u01(rr) * incl[:, -1]
-        gs = np.minimum((incl <= thr[:, None]).sum(axis=1), G - 1)
-        t = thr - excl[ar, gs]
-        Ws = W[ar, gs]
-        zn = np.zeros(A, dtype=np.int64)
-        inw = t < Ws
-        jj = np.arange(cum.shape[1])[None, :]
-        in_lane = (jj < L[:, None]) & ((lk[w, :cum.shape[1]].astype(np.int64) // KP) == gs[:, None])
-        hit = in_lane & (cum > t[:, None])
-        first = np.argmax(hit, axis=1)
-        last = cum.shape[1] - 1 - np.argmax(in_lane[:, ::-1], axis=1)
-        jsel = np.where(hit.any(axis=1), first, last)
-        zn[inw] = lk[w[inw], jsel[inw]]
-        sm = np.nonzero(~inw)[0]
-        if sm.size:
-            rows = act[sm]
-            t2 = t[sm] - Ws[sm]
-            acc = np.zeros(sm.size, dtype=F32)
-            found = np.zeros(sm.size, dtype=bool)
-            g_ = gs[sm]
-            zs = np.minimum(g_ * KP + KP, K) - 1
-            for j in range(KP):
-                k = g_ * KP + j
-                real = k < K
-                acc = np.where(real, fma_f32(n[rows, np.minimum(k, KS - 1)].astype(F32) + a32, b[np.minimum(k, KS - 1)],
-                                             acc), acc)
-                h = real & ~found & (acc > t2)
-                zs[h] = k[h]
-                found |= h
-            zn[sm] = zs
-        n[act, zn] += 1
-        R[act, zn // KP] = R[act, zn // KP] + b[zn]
-        ch = zn != zo
-        st["tok_z"][idx[ch]] = zn[ch].astype(np.uint8)
-        np.add.at(st["dnwk"], (w[ch], zo[ch]), -1)
-        np.add.at(st["dnwk"], (w[ch], zn[ch]), 1)
-    d = n - n_start
-    multi = live & (st["chunk_multi"] != 0)
-    single = live & ~multi
-    st["ndk_dst"][doc[single]] = n[single]
-    np.add.at(st["ndk_dst"], doc[multi], d[multi])
-    st["dnk"] += d[live].sum(axis=0).astype(np.int32)
-
-
 def gibbs_apply(nwk, dcur, dnk_cur, nk_cur, K, beta, vbeta):
-    """Returns (nwk', nk', q) exactly as k_apply computes them."""
+    """Returns (nwk', nk', q, qfix) exactly as k_apply computes them."""
     nwk = nwk + dcur
     nk = nk_cur + dnk_cur
     den = nk.astype(F32) + F32(vbeta)
     q = (nwk.astype(F32) + F32(beta)) / den[None, :]
     q[:, K:] = 0
-    return nwk, nk, q.astype(F32)
+    return nwk, nk, q.astype(F32), gibbs_qfix(nk, K, vbeta)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -560,9 +400,14 @@ def score(theta, phi, d1, w1, d2=None, w2=None):
 # ------------------------------------------------------------------------------------------------
 # slow textbook collapsed Gibbs (statistical cross-check only; not bitwise)
 # ------------------------------------------------------------------------------------------------
-def textbook_cgs(docs: list[np.ndarray], V: int, K: int, alpha: float, beta: float, sweeps: int, seed: int):
+def textbook_cgs(docs: list[np.ndarray], V: int, K: int, alpha: float, beta: float, sweeps: int, seed: int,
+                 z0: list[np.ndarray] | None = None, on_sweep=None):
+    """Slow, exact sequential collapsed Gibbs (Griffiths & Steyvers 2004): every count excludes
+    the token being resampled, and every update is visible to the next token. ``z0`` is the
+    initial assignment (default: uniform from ``seed``); ``on_sweep(sweep, z)`` is called after
+    each sweep with the per-document topic arrays. Returns (z, n_dk, n_wk)."""
     rng = np.random.default_rng(seed)
-    z = [rng.integers(0, K, size=len(d)) for d in docs]
+    z = [np.array(a, dtype=np.int64) for a in z0] if z0 is not None else [rng.integers(0, K, size=len(d)) for d in docs]
     ndk = np.zeros((len(docs), K))
     nwk = np.zeros((V, K))
     for d, (ws, zs) in enumerate(zip(docs, z)):
@@ -570,13 +415,16 @@ def textbook_cgs(docs: list[np.ndarray], V: int, K: int, alpha: float, beta: flo
             ndk[d, t] += 1
             nwk[w, t] += 1
     nk = nwk.sum(0)
-    for _ in range(sweeps):
+    for sw in range(sweeps):
         for d, ws in enumerate(docs):
             for i, w in enumerate(ws):
                 t = z[d][i]
                 ndk[d, t] -= 1; nwk[w, t] -= 1; nk[t] -= 1
                 p = (ndk[d] + alpha) * (nwk[w] + beta) / (nk + V * beta)
-                t = rng.choice(K, p=p / p.sum())
+                c = np.cumsum(p)
+                t = min(int(np.searchsorted(c, rng.random() * c[-1], side="right")), K - 1)
                 z[d][i] = t
                 ndk[d, t] += 1; nwk[w, t] += 1; nk[t] += 1
+        if on_sweep is not None:
+            on_sweep(sw + 1, z)
     return z, ndk, nwk

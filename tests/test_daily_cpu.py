@@ -78,3 +78,43 @@ def test_mmap_read_day_is_zero_copy_and_equal(tmp_path):
             assert v.to_list() == b[k].to_list()
         else:
             assert np.array_equal(v, b[k])
+
+
+def _follow_worker(rank, world, port, root, out_q):
+    import os as _os
+    _os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                       LOCAL_RANK=str(rank))
+    from oni355.parallel import comm as pc
+    from oni355.pipeline.daily import _next_days
+    comm = pc.init_from_env("cpu")
+    # rank 1's clock says "idle" at once, rank 0's only on the second pass: every rank must leave
+    # on rank 0's decision, in the same pass
+    passes = 0
+    while True:
+        passes += 1
+        _, stop = _next_days(root, "flow", "99999999", comm, idle=(rank == 1) or passes >= 2)
+        if stop:
+            break
+    out_q.put((rank, passes))
+    comm.barrier()
+    pc.shutdown()
+
+
+def test_follow_idle_exit_is_decided_by_rank0(tmp_path):
+    """the --follow idle exit comes from rank 0 with the day list, not each rank's clock."""
+    import socket
+
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_follow_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == [(0, 2), (1, 2)]

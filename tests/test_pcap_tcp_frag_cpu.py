@@ -129,3 +129,26 @@ def test_fragments_reusing_an_ip_id_are_separate_datagrams(tmp_path):
         assert c["dns_a"].to_list() == ["1.1.1.1", "2.2.2.2", "1.1.1.1"]
         assert c["unix_tstamp"].tolist() == [t0 + 1, t0 + 3, t0 + 47]
         assert c["_frag_incomplete"] == 3
+
+
+def test_duplicate_fragment_is_dropped_not_a_new_datagram(tmp_path):
+    """Mirror / SPAN captures repeat packets: an exact copy of a fragment the open datagram already
+    holds (f0, f1, f1', f2) is dropped, as tshark's reassembly does; the datagram still completes."""
+    srv, cli = "10.0.0.53", "10.1.2.3"
+    big = _udp(53, 5555, _dns_response(9, "dup.example.com", answers=["5.6.7.8"], pad=900))
+    f0, f1, f2 = big[:400], big[400:800], big[800:]
+    t0 = 1467936000
+    frames = [
+        (t0, _eth(_ipv4(srv, cli, 17, f0, ident=31, frag_off=0, more=True))),
+        (t0, _eth(_ipv4(srv, cli, 17, f1, ident=31, frag_off=400, more=True))),
+        (t0 + 1, _eth(_ipv4(srv, cli, 17, f1, ident=31, frag_off=400, more=True))),  # duplicate
+        (t0 + 2, _eth(_ipv4(srv, cli, 17, f2, ident=31, frag_off=800))),
+    ]
+    p = str(tmp_path / "dup.pcap")
+    _write_ts(p, frames)
+    for threads in (1, 2):
+        c = read_pcap_dns(p, threads=threads)
+        assert c["dns_qry_name"].to_list() == ["dup.example.com"]
+        assert c["dns_a"].to_list() == ["5.6.7.8"]
+        assert c["unix_tstamp"].tolist() == [t0 + 2]
+        assert c["_frag_incomplete"] == 0

@@ -181,8 +181,8 @@ def test_lds_sampler_oracle_keeps_counts_consistent():
     tword = torch.from_numpy(r.integers(0, 50, int(lens.sum())))
     keys = torch.arange(80, dtype=torch.int32) * 7 + 1
     c = build_corpus(tdoc, tword, 80, 50, keys, 1, L=64)
-    m = GibbsLDA(c, GibbsConfig(K=20, seed=5, sampler="lds"))
-    assert m.qpf == 2
+    m = GibbsLDA(c, GibbsConfig(K=20, seed=5, sampler="x1"))
+    assert m.qpf == 3
     m.initialize()
     m.sweep(3)
     T = c.T
