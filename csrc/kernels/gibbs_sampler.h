@@ -711,86 +711,64 @@ __device__ __forceinline__ float group_scan_dpp(float x, int g) {
   return x;
 }
 
+// Per-step state of k_gibbs_ldsg. As in k_gibbs_x1 the q rows of consecutive tokens ping-pong
+// between two register sets with static roles (loop unrolled by two): the next token's row and its
+// own-topic value q_{w,zo} are issued a full step before they are used, so neither the word-change
+// row fetch nor the exclusion's gather is a dependent round trip inside the step.
 template <int G, int KP, int MODE>
-__global__ __launch_bounds__(kBlock) void k_gibbs_ldsg(const OniGibbs a) {
-  static_assert(G > 1, "G = 1 uses k_gibbs_x1");
-  constexpr int S = oni::kWave / G;
-  constexpr int KS = G * KP;
-  constexpr int kSlots = LdsRow<KP>::kSlots;
-  __shared__ float4 sa[kBlock * kSlots];
-  __shared__ int32_t red[kWavesPerBlock][KS];
-  __shared__ float2 qfx[KS];
-  for (int k = threadIdx.x; k < KS; k += kBlock) qfx[k] = make_float2(a.qfix[k], a.qfix[KS + k]);
-  const int wave = threadIdx.x >> 6;
-  const int lane = threadIdx.x & 63;
-  const int c = lane / G;
-  const int g = lane % G;
-  const int64_t slice = (int64_t)blockIdx.x * kWavesPerBlock + wave;
-  const bool valid = slice < a.n_slices;
-  const int64_t chunk = slice * S + c;
-  const int doc = valid ? a.chunk_doc[chunk] : -1;
-  const bool live = doc >= 0;
-  const int kbase = g * KP;
-  float4* row = sa + threadIdx.x * kSlots;
-  float* rowf = reinterpret_cast<float*>(row);
-  {
-    int32_t n0[KP];
-#pragma unroll
-    for (int j = 0; j < KP; ++j) n0[j] = 0;
-    if (live) load_row_i<KP>(a.ndk_src + (int64_t)doc * KS + kbase, n0);
-#pragma unroll
-    for (int j = 0; j < KP / 4; ++j)
-      row[j] = make_float4((float)n0[4 * j] + a.alpha, (float)n0[4 * j + 1] + a.alpha,
-                           (float)n0[4 * j + 2] + a.alpha, (float)n0[4 * j + 3] + a.alpha);
-  }
-  __syncthreads();  // qfx
-  const int len = valid ? a.slice_len[slice] : 0;
-  const int64_t off = valid ? a.slice_off[slice] : 0;
-  const uint32_t key = live ? a.chunk_key[chunk] : 0u;
-  const uint32_t pos0 = live ? (uint32_t)a.chunk_pos0[chunk] : 0u;
-  const uint32_t sweep = *a.sweep_ctr;
-  // Philox blocks are shared by the unit: lane g holds the block of 4-token group gbase + g, so
-  // the unit computes one block per G·4 tokens; the refresh is wave-uniform: every
-  // kRefresh = 4G - 3 steps each unit recomputes the G blocks that cover its next kRefresh tokens.
-  constexpr int kRefresh = 4 * G - 3;
-  uint32_t gbase = pos0 >> 2;
-  oni::U4 r = oni::philox10(oni::U4{gbase + (uint32_t)g, key, sweep, 1u}, a.seed0, a.seed1);
-  int next_refresh = kRefresh;
-  uint32_t wprev = oni::kPadWord;
-  float qv[KP];
-#pragma unroll
-  for (int j = 0; j < KP; ++j) qv[j] = 0.f;
-  int nchg = 0;
-  uint32_t w_nx = len > 0 ? a.tok_word[off + c] : oni::kPadWord;
-  int z_nx = len > 0 ? (int)a.tok_z[off + c] : 0;
-  constexpr bool WPF = MODE == 3 || MODE == 4;
-  int32_t p_nx = (WPF && len > 0) ? a.wpos[off + c] : 0;
+struct LG {
+  static constexpr int S = oni::kWave / G;
+  static constexpr int KS = G * KP;
+  static constexpr int kRefresh = 4 * G - 3;
+  static constexpr bool WPF = MODE == 3 || MODE == 4;
+  const OniGibbs& a;
+  const float2* qfx;
+  float4* row;
+  int lane, c, g, kbase;
+  int64_t off;
+  int len;
+  uint32_t w0, w1;
+  int z0, z1;
+  int32_t p0, p1;
+  float qz0;
+  uint32_t pos0, key, sweep, gbase;
+  oni::U4 r;
+  int next_refresh;
+  int nchg;
   Pend<MODE> pend;
-  for (int s = 0; s < len; ++s) {
+
+  __device__ __forceinline__ LG(const OniGibbs& a_, const float2* q_) : a(a_), qfx(q_) {}
+
+  template <int PAR>
+  __device__ __forceinline__ void step(int s, const float (&qc)[KP], float (&qn)[KP]) {
+    float* rowf = reinterpret_cast<float*>(row);
     const int64_t idx = off + (int64_t)s * S + c;
-    const uint32_t w = w_nx;
-    const int zo = z_nx;
-    const int32_t pw = p_nx;
-    if (s + 1 < len) {
-      w_nx = a.tok_word[idx + S];
-      z_nx = a.tok_z[idx + S];
-      if (WPF) p_nx = a.wpos[idx + S];
+    const uint32_t w = w0;
+    const int zo = z0;
+    const int32_t pw = p0;
+    const float qz = qz0;
+    if (w1 != oni::kPadWord) {
+      const float* qr = a.q + (int64_t)w1 * KS;
+      load_row_f<KP>(qr + kbase, qn);
+      qz0 = qr[z1];
     }
-    float qz = 0.f;
-    if (w != oni::kPadWord) {
-      if (w != wprev) {
-        load_row_f<KP>(a.q + (int64_t)w * KS + kbase, qv);
-        wprev = w;
-      }
-      qz = a.q[(int64_t)w * KS + zo];
+    w0 = w1;
+    z0 = z1;
+    p0 = p1;
+    if (s + 2 < len) {
+      w1 = a.tok_word[idx + 2 * S];
+      z1 = (int)a.tok_z[idx + 2 * S];
+      if constexpr (WPF) p1 = a.wpos[idx + 2 * S];
+    } else {
+      w1 = oni::kPadWord;
     }
-    pend.flush(a, KS);  // after the token-stream loads
+    pend.flush(a, KS);  // after this step's loads
     if (s == next_refresh) {  // wave-uniform (before the pad test: every lane takes it together)
       next_refresh += kRefresh;
       gbase = (pos0 + (uint32_t)s) >> 2;
       r = oni::philox10(oni::U4{gbase + (uint32_t)g, key, sweep, 1u}, a.seed0, a.seed1);
     }
-    if (w == oni::kPadWord) continue;  // uniform across the G lanes of a unit
+    if (w == oni::kPadWord) return;  // uniform across the G lanes of a unit
     const uint32_t pos = pos0 + (uint32_t)s;
     const uint32_t gi = pos >> 2;
     const uint32_t rr = (uint32_t)__shfl((int)oni::pick4(r, pos & 3u), (int)(gi - gbase), G);
@@ -808,13 +786,13 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_ldsg(const OniGibbs a) {
 #pragma unroll
     for (int j = 0; j < KP / 4; ++j) {
       const float4 av = row[j];
-      run = fmaf(av.x, qv[4 * j + 0], run);
+      run = fmaf(av.x, qc[4 * j + 0], run);
       P[4 * j + 0] = run;
-      run = fmaf(av.y, qv[4 * j + 1], run);
+      run = fmaf(av.y, qc[4 * j + 1], run);
       P[4 * j + 1] = run;
-      run = fmaf(av.z, qv[4 * j + 2], run);
+      run = fmaf(av.z, qc[4 * j + 2], run);
       P[4 * j + 2] = run;
-      run = fmaf(av.w, qv[4 * j + 3], run);
+      run = fmaf(av.w, qc[4 * j + 3], run);
       P[4 * j + 3] = run;
     }
     if (zlo < (unsigned)KP) rowf[zlo] = tz;
@@ -840,8 +818,80 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_ldsg(const OniGibbs a) {
       }
     }
   }
-  pend.flush(a, KS);
-  if (a.chg_count) add_wave_count(a.chg_count, nchg);
+};
+
+template <int G, int KP, int MODE>
+__global__ __launch_bounds__(kBlock) void k_gibbs_ldsg(const OniGibbs a) {
+  static_assert(G > 1, "G = 1 uses k_gibbs_x1");
+  constexpr int S = oni::kWave / G;
+  constexpr int KS = G * KP;
+  constexpr int kSlots = LdsRow<KP>::kSlots;
+  __shared__ float4 sa[kBlock * kSlots];
+  __shared__ int32_t red[kWavesPerBlock][KS];
+  __shared__ float2 qfx[KS];
+  for (int k = threadIdx.x; k < KS; k += kBlock) qfx[k] = make_float2(a.qfix[k], a.qfix[KS + k]);
+  LG<G, KP, MODE> x(a, qfx);
+  const int wave = threadIdx.x >> 6;
+  x.lane = threadIdx.x & 63;
+  x.c = x.lane / G;
+  x.g = x.lane % G;
+  const int c = x.c, g = x.g;
+  const int64_t slice = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  const bool valid = slice < a.n_slices;
+  const int64_t chunk = slice * S + c;
+  const int doc = valid ? a.chunk_doc[chunk] : -1;
+  const bool live = doc >= 0;
+  x.kbase = g * KP;
+  const int kbase = x.kbase;
+  x.row = sa + threadIdx.x * kSlots;
+  {
+    int32_t n0[KP];
+#pragma unroll
+    for (int j = 0; j < KP; ++j) n0[j] = 0;
+    if (live) load_row_i<KP>(a.ndk_src + (int64_t)doc * KS + kbase, n0);
+#pragma unroll
+    for (int j = 0; j < KP / 4; ++j)
+      x.row[j] = make_float4((float)n0[4 * j] + a.alpha, (float)n0[4 * j + 1] + a.alpha,
+                             (float)n0[4 * j + 2] + a.alpha, (float)n0[4 * j + 3] + a.alpha);
+  }
+  __syncthreads();  // qfx
+  x.len = valid ? a.slice_len[slice] : 0;
+  x.off = valid ? a.slice_off[slice] : 0;
+  const int len = x.len;
+  const int64_t off = x.off;
+  x.key = live ? a.chunk_key[chunk] : 0u;
+  x.pos0 = live ? (uint32_t)a.chunk_pos0[chunk] : 0u;
+  x.sweep = *a.sweep_ctr;
+  // Philox blocks are shared by the unit: lane g holds the block of 4-token group gbase + g, so
+  // the unit computes one block per G·4 tokens; the refresh is wave-uniform: every
+  // kRefresh = 4G - 3 steps each unit recomputes the G blocks that cover its next kRefresh tokens.
+  x.gbase = x.pos0 >> 2;
+  x.r = oni::philox10(oni::U4{x.gbase + (uint32_t)g, x.key, x.sweep, 1u}, a.seed0, a.seed1);
+  x.next_refresh = LG<G, KP, MODE>::kRefresh;
+  x.nchg = 0;
+  constexpr bool WPF = LG<G, KP, MODE>::WPF;
+  x.w0 = len > 0 ? a.tok_word[off + c] : oni::kPadWord;
+  x.z0 = len > 0 ? (int)a.tok_z[off + c] : 0;
+  x.p0 = (WPF && len > 0) ? a.wpos[off + c] : 0;
+  x.w1 = len > 1 ? a.tok_word[off + S + c] : oni::kPadWord;
+  x.z1 = len > 1 ? (int)a.tok_z[off + S + c] : 0;
+  x.p1 = (WPF && len > 1) ? a.wpos[off + S + c] : 0;
+  float qa[KP], qb[KP];
+#pragma unroll
+  for (int j = 0; j < KP; ++j) qa[j] = qb[j] = 0.f;
+  x.qz0 = 0.f;
+  if (x.w0 != oni::kPadWord) {
+    const float* qr = a.q + (int64_t)x.w0 * KS;
+    load_row_f<KP>(qr + kbase, qa);
+    x.qz0 = qr[x.z0];
+  }
+  for (int s = 0; s < len; s += 2) {
+    x.template step<0>(s, qa, qb);
+    if (s + 1 < len) x.template step<1>(s + 1, qb, qa);
+  }
+  x.pend.flush(a, KS);
+  if (a.chg_count) add_wave_count(a.chg_count, x.nchg);
+  const float* rowf = reinterpret_cast<const float*>(x.row);
   int32_t n[KP];
 #pragma unroll
   for (int j = 0; j < KP; ++j) n[j] = (int32_t)(rowf[j] - a.alpha);

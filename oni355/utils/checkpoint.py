@@ -64,7 +64,8 @@ class Checkpointer:
         }
         avg = model.average_state() if hasattr(model, "average_state") else None
         if avg is not None:
-            # inside the posterior-averaging window: the samples so far (this rank's layout)
+            # inside the posterior-averaging window: the samples so far; the doc-topic sums are
+            # rows aligned with doc_keys, so a resume on another world size re-keys them
             payload["avg"] = avg
         name = f"ckpt_s{model.sweeps_done}_r{self.rank}of{self.world}.pt"
         path = os.path.join(self.dir, name)
@@ -182,18 +183,41 @@ class Checkpointer:
         model.load_canonical_z(z, sweep)
         win = model.average_window if hasattr(model, "average_window") else None
         if win is not None and sweep >= win[0]:
-            # resumed inside the posterior-averaging window: the samples taken before the
-            # checkpoint are in this rank's own shard, valid for the same corpus layout only
-            own = os.path.join(self.dir, f"ckpt_s{sweep}_r{self.rank}of{man['world']}.pt")
-            d = torch.load(own, weights_only=True) if os.path.exists(own) else {}
-            if man["world"] != self.world or "avg" not in d or not torch.equal(
-                    d["doc_keys"].to(torch.int64), c.doc_keys.cpu().to(torch.int64)):
-                raise ValueError(f"checkpoint at sweep {sweep} is inside the posterior-averaging window "
-                                 f"{win}: resume it with the world size it was written with "
-                                 f"({man['world']}), or set ONI_POST_SAMPLES=1")
-            model.load_average_state(d["avg"])
+            self._restore_average(model, sweep, man, win)
         return sweep
 
+
+    def _restore_average(self, model, sweep: int, man: dict, win) -> None:
+        """Resume inside the posterior-averaging window on ANY world size: the word-topic and topic
+        sums are global (every shard holds the same), the doc-topic sums are matched to this
+        rank's rows by document key (every row of a document cut into pieces carries the whole
+        document's counts, so any of them serves)."""
+        keys_all, dk_all, glob_avg = [], [], None
+        for p in sorted(glob.glob(os.path.join(self.dir, f"ckpt_s{sweep}_r*of{man['world']}.pt"))):
+            d = torch.load(p, weights_only=True)
+            if "avg" not in d:
+                raise ValueError(f"checkpoint shard {os.path.basename(p)} at sweep {sweep} lacks the posterior "
+                                 f"samples of the averaging window {win}")
+            if glob_avg is None:
+                glob_avg = d["avg"]
+            keys_all.append(d["doc_keys"].to(torch.int64) & 0xFFFFFFFF)
+            dk_all.append(d["avg"]["dk"][: d["doc_keys"].numel()])
+        if glob_avg is None:
+            raise ValueError(f"no checkpoint shards at sweep {sweep}")
+        keys = torch.cat(keys_all)
+        dk = torch.cat(dk_all)
+        my_keys = model.c.doc_keys.cpu().to(torch.int64) & 0xFFFFFFFF
+        out = torch.zeros((max(my_keys.numel(), 1), dk.shape[1]), dtype=dk.dtype)
+        if my_keys.numel():
+            order = torch.argsort(keys, stable=True)
+            sk = keys[order]
+            pos = torch.searchsorted(sk, my_keys).clamp_(max=max(sk.numel() - 1, 0))
+            hit = sk[pos] == my_keys if sk.numel() else torch.zeros_like(my_keys, dtype=torch.bool)
+            if not bool(hit.all()):
+                miss = int(my_keys[torch.nonzero(~hit).flatten()[0]])
+                raise ValueError(f"averaging samples do not match the corpus (doc key {miss} missing)")
+            out[: my_keys.numel()] = dk[order[pos]]
+        model.load_average_state({"n": glob_avg["n"], "wk": glob_avg["wk"], "k": glob_avg["k"], "dk": out})
 
 def _pos0(c) -> torch.Tensor:
     """Canonical position of each corpus row's first token (0 unless the row is a piece)."""

@@ -182,3 +182,18 @@ def test_split_checkpoint_resumes_on_another_world(tmp_path, w_save, w_resume):
     resumed = _run(w_resume, dict(base, sweeps=4, ckpt=ck, ckpt_every=0))
     assert resumed["sweeps"] == 4
     _same(ref, resumed)
+
+
+@pytest.mark.parametrize("w_save,w_resume", [(3, 1), (1, 2)])
+def test_checkpoint_inside_averaging_window_resumes_on_another_world(tmp_path, w_save, w_resume):
+    """A checkpoint taken inside the posterior-averaging window (16 sweeps: samples at 14 and 16)
+    on w_save ranks resumes on w_resume ranks; the averaged θ/φ -- hence the scored rows -- equal
+    an uninterrupted single-rank run bit for bit."""
+    ck = str(tmp_path / "ck")
+    base = dict(source="flow", n=8000, heavy=0.30, sweeps=16)
+    ref = _run(1, base)
+    first = _run(w_save, dict(base, ckpt=ck, ckpt_every=14))
+    assert first["sweeps"] == 16
+    resumed = _run(w_resume, dict(base, ckpt=ck, ckpt_every=0))
+    assert resumed["sweeps"] == 16
+    _same(ref, resumed)
