@@ -278,7 +278,7 @@ struct Pend {
 // α = 50/7). Numerics are the spec's: G = 1 replaces q_zo by q'; G > 1 scales the owner lane's
 // weight of zo by f = q'/q_zo.
 template <int G, int KP, bool INIT, int MODE>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_gibbs(const OniGibbs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 8))) void k_gibbs(const OniGibbs a) {
   constexpr int S = oni::kWave / G;
   constexpr int KS = G * KP;
   __shared__ int32_t red[kWavesPerBlock][KS];
@@ -408,40 +408,43 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) 
 }
 
 // ---- one-lane sweep kernel (K ≤ 32): k_gibbs_x1 ----------------------------------------------------
-// Written for VALU issue, which bounds the one-lane sweep (SQ counters, docs/performance.md). Per
-// token and topic slot j the loop body is
+// Per token and topic slot j the loop body is
 //   * 3 ops of count update: the row r_j = n_dj + α is f32 (exact: the host checks, `flags`
 //     bit 0) and ONE fused update per step applies +1 at the previous token's new topic and −1 at
 //     this token's old topic (the doc-side exclusion) from a 2-bit-field mask M:
-//     r_j += (float)bfe_i32(M, 2j, 2) -- no per-slot compare / select chains;
-//   * 2 ops to put q' in place of q_zo (compare + select), 1 fma for the weight chain;
-//   * 1 compare per slot for the draw: the compares of all lanes form nested ballot masks (the
-//     prefix is monotone), so the count #{j : P_j ≤ thr} is assembled from their bit planes with
-//     scalar XORs (bit b of the count is the XOR of the masks j ≡ 2^b − 1 mod 2^(b+1)) and a
-//     5-step carry-in Horner on the vector side.
-// The q rows of consecutive tokens ping-pong between two register sets with static roles (the
-// loop is unrolled by two; the next token's row is always loaded, an L1 hit when the word
-// repeats), so no row copies; token words / topics / word-sorted slots stream two steps ahead.
-template <int KP, int MODE, bool AIR>
+//     r_j += (float)bfe_i32(M, 2j, 2) -- no per-slot compare / select chains on the row;
+//   * compare + fma + select to put q' = fma(q_j, A, −B) in place of q_zo (no gather of q_{w,zo}:
+//     the row is already in registers), 1 fma for the weight chain, compare + add-with-carry count.
+// ≈ 240 vector instructions per step at K = 20 (the r3 register sampler: ≈ 380).
+// The q row of the next token is fetched a full step ahead into the other register set (static
+// roles: the loop is unrolled by two) when its word differs, else copied; token words / topics
+// stream two steps ahead in parity slots. Measured (profiles/r4/ab_x1_variants_k20.json): loading
+// the next row unconditionally (+0.055 ms/sweep: every lane's 80 B row through the TA each step),
+// a ballot-bit-plane count on the scalar unit (+0.013 ms), the q_{w,zo} gather (+0.025 ms) and a
+// 3-wave register budget (+0.011 ms) all lost.
+// WPD (off: measured 0.255 vs 0.248 ms/sweep): MODE 3/4 changed tokens load their word-sorted
+// slot when they change (exec-masked, ~10 % of lanes) instead of streaming it with every token.
+template <int KP, int MODE, bool AIR, bool WPD>
 struct X1 {
   static constexpr int KS = KP;
+  static constexpr bool WPF = (MODE == 3 || MODE == 4) && !WPD;
   const OniGibbs& a;
   const float2* qfx;  // LDS: (A, B) per topic
   int lane;
   int64_t off;
   int len;
   float r[KP];
-  uint32_t w0, w1;
-  int z0, z1;
-  int32_t p0, p1;
-  float qz0;
+  // token stream in parity slots with static roles (the loop is unrolled by two): slot s & 1
+  // holds token s, the other slot token s + 1. Shifting one register set into another while its
+  // loads are in flight made the loop latch wait for every outstanding memory op (vmcnt(0)).
+  uint32_t ws[2];
+  int zs[2];
+  int32_t ps[2];
   PhiloxPair rng;
   uint32_t pinc_lo, pinc_hi;  // 2-bit field +1 at the previous token's new topic (pending)
   int znp;                    // that topic (-1: none pending)
   int nchg;
   Pend<MODE> pend;
-
-  static constexpr bool WPF = MODE == 3 || MODE == 4;
 
   __device__ __forceinline__ X1(const OniGibbs& a_, const float2* q_) : a(a_), qfx(q_) {}
 
@@ -454,60 +457,29 @@ struct X1 {
     }
   }
 
-  // the draw: #{j : P_j ≤ thr} from nested ballot masks (see above), capped at K − 1. Padding
-  // slots j ≥ K have q = 0, so P_j = P_{K−1}: the lanes of the last mask (every slot counted) are
-  // exactly those whose count reaches K, and they take topic K − 1.
-  __device__ __forceinline__ int draw(const float (&P)[KP], float thr) const {
-    uint64_t b0 = 0, b1 = 0, b2 = 0, b3 = 0, b4 = 0, mlast = 0;
-#pragma unroll
-    for (int j = 0; j < KP; ++j) {
-      const uint64_t m = __ballot(P[j] <= thr);
-      mlast = m;
-      b0 ^= m;
-      if ((j & 1) == 1) b1 ^= m;
-      if ((j & 3) == 3) b2 ^= m;
-      if ((j & 7) == 7) b3 ^= m;
-      if ((j & 15) == 15) b4 ^= m;
-    }
-    const uint32_t km1 = (uint32_t)(a.K - 1);
-    b0 = (b0 & ~mlast) | ((km1 & 1u) ? mlast : 0ull);
-    b1 = (b1 & ~mlast) | ((km1 & 2u) ? mlast : 0ull);
-    b2 = (b2 & ~mlast) | ((km1 & 4u) ? mlast : 0ull);
-    b3 = (b3 & ~mlast) | ((km1 & 8u) ? mlast : 0ull);
-    b4 = (b4 & ~mlast) | ((km1 & 16u) ? mlast : 0ull);
-    // per-lane value: Horner with the bit planes as carry-in, v = 2v + bit (v_addc_co_u32)
-    int v = 0;
-    uint64_t co;
-    asm volatile("v_addc_co_u32_e64 %0, %1, %0, %0, %2" : "+v"(v), "=s"(co) : "s"(b4));
-    asm volatile("v_addc_co_u32_e64 %0, %1, %0, %0, %2" : "+v"(v), "=s"(co) : "s"(b3));
-    asm volatile("v_addc_co_u32_e64 %0, %1, %0, %0, %2" : "+v"(v), "=s"(co) : "s"(b2));
-    asm volatile("v_addc_co_u32_e64 %0, %1, %0, %0, %2" : "+v"(v), "=s"(co) : "s"(b1));
-    asm volatile("v_addc_co_u32_e64 %0, %1, %0, %0, %2" : "+v"(v), "=s"(co) : "s"(b0));
-    return v;
-  }
-
-  template <int PAR>
+  template <int PAR, bool LOAD>
   __device__ __forceinline__ void step(int s, const float (&qc)[KP], float (&qn)[KP]) {
+    constexpr int NX = 1 - PAR;
     const int64_t idx = off + (int64_t)s * 64 + lane;
-    const uint32_t w = w0;
-    const int zo = z0;
-    const int32_t pw = p0;
-    const float qz = qz0;
-    // token s+1: its q row into the other register set, its own-topic q value
-    if (w1 != oni::kPadWord) {
-      const float* qr = a.q + (int64_t)w1 * KS;
-      load_row_f<KP>(qr, qn);
-      qz0 = qr[z1];
+    const uint32_t w = ws[PAR];
+    const int zo = zs[PAR];
+    const int32_t pw = ps[PAR];
+    // token s+1: its q row into the other register set (copied when the word repeats)
+    if (ws[NX] != oni::kPadWord) {
+      if (ws[NX] != w) {
+        load_row_f<KP>(a.q + (int64_t)ws[NX] * KS, qn);
+      } else {
+#pragma unroll
+        for (int j = 0; j < KP; ++j) qn[j] = qc[j];
+      }
     }
-    w0 = w1;
-    z0 = z1;
-    p0 = p1;
-    if (s + 2 < len) {
-      w1 = a.tok_word[idx + 128];
-      z1 = (int)a.tok_z[idx + 128];
-      if constexpr (WPF) p1 = a.wpos[idx + 128];
+    // token s+2 into this step's slot (LOAD: s + 2 < len, known statically in the main loop)
+    if constexpr (LOAD) {
+      ws[PAR] = a.tok_word[idx + 128];
+      zs[PAR] = (int)a.tok_z[idx + 128];
+      if constexpr (WPF) ps[PAR] = a.wpos[idx + 128];
     } else {
-      w1 = oni::kPadWord;
+      ws[PAR] = oni::kPadWord;
     }
     pend.flush(a, KS);
     rng.step(s, a);
@@ -523,17 +495,19 @@ struct X1 {
       add_fields(mlo, mhi);
     }
     const float2 ab = qfx[zo];
-    const float qe = fmaf(qz, ab.x, -ab.y);
     float P[KP];
     float run = 0.f;
 #pragma unroll
     for (int j = 0; j < KP; ++j) {
-      const float qj = j == zo ? qe : qc[j];
+      const float qj = j == zo ? fmaf(qc[j], ab.x, -ab.y) : qc[j];
       run = fmaf(AIR ? r[j] : r[j] + a.alpha, qj, run);
       P[j] = run;
     }
     const float thr = oni::u01(rr) * run;
-    const int zn = draw(P, thr);
+    int cnt = 0;
+#pragma unroll
+    for (int j = 0; j < KP; ++j) cnt += (P[j] <= thr);
+    const int zn = cnt < a.K - 1 ? cnt : a.K - 1;
     {
       const uint32_t sh = 2u * (uint32_t)zn;
       pinc_lo = sh < 32u ? (1u << sh) : 0u;
@@ -543,7 +517,9 @@ struct X1 {
     const bool changed = zn != zo;
     if (changed) {
       ++nchg;
-      pend.note(idx, zo, zn, pw, w);
+      int32_t p = pw;
+      if constexpr (WPD && (MODE == 3 || MODE == 4)) p = a.wpos[idx];  // used by the next step's flush
+      pend.note(idx, zo, zn, p, w);
     }
     if constexpr (MODE == 2) {
       const uint64_t m = __ballot(changed);
@@ -555,15 +531,19 @@ struct X1 {
   }
 };
 
-template <int KP, int MODE, bool AIR>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_gibbs_x1(const OniGibbs a) {
+// 4 waves per SIMD up to KP = 24 (≤ 128 VGPRs: 3 rows of KP plus the weights); wider rows take
+// what they need (a forced 4-wave budget spills at KP = 32)
+template <int KP, int MODE, bool AIR, bool WPD = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KP <= 24 ? 4 : 1, 8))) void k_gibbs_x1(
+    const OniGibbs a) {
   static_assert(KP <= 32 && KP % 4 == 0, "one-lane units hold at most 32 topics");
   __shared__ float2 qfx[KP];
   __shared__ int32_t red[kWavesPerBlock][KP];
   if (threadIdx.x < KP) qfx[threadIdx.x] = make_float2(a.qfix[threadIdx.x], a.qfix[KP + threadIdx.x]);
   __syncthreads();
 
-  X1<KP, MODE, AIR> x(a, qfx);
+  using XT = X1<KP, MODE, AIR, WPD>;
+  XT x(a, qfx);
   const int wave = threadIdx.x >> 6;
   x.lane = threadIdx.x & 63;
   const int64_t slice = (int64_t)blockIdx.x * kWavesPerBlock + wave;
@@ -590,24 +570,27 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) 
   const int len = x.len;
   const int64_t off = x.off;
   const int c = x.lane;
-  x.w0 = len > 0 ? a.tok_word[off + c] : oni::kPadWord;
-  x.z0 = len > 0 ? (int)a.tok_z[off + c] : 0;
-  x.p0 = (X1<KP, MODE, AIR>::WPF && len > 0) ? a.wpos[off + c] : 0;
-  x.w1 = len > 1 ? a.tok_word[off + 64 + c] : oni::kPadWord;
-  x.z1 = len > 1 ? (int)a.tok_z[off + 64 + c] : 0;
-  x.p1 = (X1<KP, MODE, AIR>::WPF && len > 1) ? a.wpos[off + 64 + c] : 0;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    x.ws[t] = len > t ? a.tok_word[off + t * 64 + c] : oni::kPadWord;
+    x.zs[t] = len > t ? (int)a.tok_z[off + t * 64 + c] : 0;
+    x.ps[t] = (XT::WPF && len > t) ? a.wpos[off + t * 64 + c] : 0;
+  }
   float qa[KP], qb[KP];
 #pragma unroll
   for (int j = 0; j < KP; ++j) qa[j] = qb[j] = 0.f;
-  x.qz0 = 0.f;
-  if (x.w0 != oni::kPadWord) {
-    const float* qr = a.q + (int64_t)x.w0 * KP;
-    load_row_f<KP>(qr, qa);
-    x.qz0 = qr[x.z0];
+  if (x.ws[0] != oni::kPadWord) load_row_f<KP>(a.q + (int64_t)x.ws[0] * KP, qa);
+  // main loop: every step's look-ahead load is in range, so no value of the token stream is a
+  // merge of a load and a constant (such a merge made the latch wait for all memory ops)
+  int s = 0;
+  for (; s + 3 < len; s += 2) {
+    x.template step<0, true>(s, qa, qb);
+    x.template step<1, true>(s + 1, qb, qa);
   }
-  for (int s = 0; s < len; s += 2) {
-    x.template step<0>(s, qa, qb);
-    if (s + 1 < len) x.template step<1>(s + 1, qb, qa);
+  for (; s < len; s += 2) {  // the last ≤ 3 steps
+    if (s + 2 < len) x.template step<0, true>(s, qa, qb);
+    else x.template step<0, false>(s, qa, qb);
+    if (s + 1 < len) x.template step<1, false>(s + 1, qb, qa);
   }
   x.pend.flush(a, KP);
   x.add_fields(x.pinc_lo, x.pinc_hi);  // the last token's +1
@@ -727,10 +710,10 @@ struct LG {
   int lane, c, g, kbase;
   int64_t off;
   int len;
-  uint32_t w0, w1;
-  int z0, z1;
-  int32_t p0, p1;
-  float qz0;
+  uint32_t ws[2];  // parity slots with static roles, as in X1
+  int zs[2];
+  int32_t ps[2];
+  float qzs[2];
   uint32_t pos0, key, sweep, gbase;
   oni::U4 r;
   int next_refresh;
@@ -739,28 +722,26 @@ struct LG {
 
   __device__ __forceinline__ LG(const OniGibbs& a_, const float2* q_) : a(a_), qfx(q_) {}
 
-  template <int PAR>
+  template <int PAR, bool LOAD>
   __device__ __forceinline__ void step(int s, const float (&qc)[KP], float (&qn)[KP]) {
+    constexpr int NX = 1 - PAR;
     float* rowf = reinterpret_cast<float*>(row);
     const int64_t idx = off + (int64_t)s * S + c;
-    const uint32_t w = w0;
-    const int zo = z0;
-    const int32_t pw = p0;
-    const float qz = qz0;
-    if (w1 != oni::kPadWord) {
-      const float* qr = a.q + (int64_t)w1 * KS;
+    const uint32_t w = ws[PAR];
+    const int zo = zs[PAR];
+    const int32_t pw = ps[PAR];
+    const float qz = qzs[PAR];
+    if (ws[NX] != oni::kPadWord) {
+      const float* qr = a.q + (int64_t)ws[NX] * KS;
       load_row_f<KP>(qr + kbase, qn);
-      qz0 = qr[z1];
+      qzs[NX] = qr[zs[NX]];
     }
-    w0 = w1;
-    z0 = z1;
-    p0 = p1;
-    if (s + 2 < len) {
-      w1 = a.tok_word[idx + 2 * S];
-      z1 = (int)a.tok_z[idx + 2 * S];
-      if constexpr (WPF) p1 = a.wpos[idx + 2 * S];
+    if constexpr (LOAD) {
+      ws[PAR] = a.tok_word[idx + 2 * S];
+      zs[PAR] = (int)a.tok_z[idx + 2 * S];
+      if constexpr (WPF) ps[PAR] = a.wpos[idx + 2 * S];
     } else {
-      w1 = oni::kPadWord;
+      ws[PAR] = oni::kPadWord;
     }
     pend.flush(a, KS);  // after this step's loads
     if (s == next_refresh) {  // wave-uniform (before the pad test: every lane takes it together)
@@ -820,8 +801,8 @@ struct LG {
   }
 };
 
-template <int G, int KP, int MODE>
-__global__ __launch_bounds__(kBlock) void k_gibbs_ldsg(const OniGibbs a) {
+template <int G, int KP, int MODE, int OCC = 1>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void k_gibbs_ldsg(const OniGibbs a) {
   static_assert(G > 1, "G = 1 uses k_gibbs_x1");
   constexpr int S = oni::kWave / G;
   constexpr int KS = G * KP;
@@ -870,24 +851,30 @@ __global__ __launch_bounds__(kBlock) void k_gibbs_ldsg(const OniGibbs a) {
   x.next_refresh = LG<G, KP, MODE>::kRefresh;
   x.nchg = 0;
   constexpr bool WPF = LG<G, KP, MODE>::WPF;
-  x.w0 = len > 0 ? a.tok_word[off + c] : oni::kPadWord;
-  x.z0 = len > 0 ? (int)a.tok_z[off + c] : 0;
-  x.p0 = (WPF && len > 0) ? a.wpos[off + c] : 0;
-  x.w1 = len > 1 ? a.tok_word[off + S + c] : oni::kPadWord;
-  x.z1 = len > 1 ? (int)a.tok_z[off + S + c] : 0;
-  x.p1 = (WPF && len > 1) ? a.wpos[off + S + c] : 0;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    x.ws[t] = len > t ? a.tok_word[off + t * S + c] : oni::kPadWord;
+    x.zs[t] = len > t ? (int)a.tok_z[off + t * S + c] : 0;
+    x.ps[t] = (WPF && len > t) ? a.wpos[off + t * S + c] : 0;
+    x.qzs[t] = 0.f;
+  }
   float qa[KP], qb[KP];
 #pragma unroll
   for (int j = 0; j < KP; ++j) qa[j] = qb[j] = 0.f;
-  x.qz0 = 0.f;
-  if (x.w0 != oni::kPadWord) {
-    const float* qr = a.q + (int64_t)x.w0 * KS;
+  if (x.ws[0] != oni::kPadWord) {
+    const float* qr = a.q + (int64_t)x.ws[0] * KS;
     load_row_f<KP>(qr + kbase, qa);
-    x.qz0 = qr[x.z0];
+    x.qzs[0] = qr[x.zs[0]];
   }
-  for (int s = 0; s < len; s += 2) {
-    x.template step<0>(s, qa, qb);
-    if (s + 1 < len) x.template step<1>(s + 1, qb, qa);
+  int s = 0;
+  for (; s + 3 < len; s += 2) {
+    x.template step<0, true>(s, qa, qb);
+    x.template step<1, true>(s + 1, qb, qa);
+  }
+  for (; s < len; s += 2) {  // the last ≤ 3 steps
+    if (s + 2 < len) x.template step<0, true>(s, qa, qb);
+    else x.template step<0, false>(s, qa, qb);
+    if (s + 1 < len) x.template step<1, false>(s + 1, qb, qa);
   }
   x.pend.flush(a, KS);
   if (a.chg_count) add_wave_count(a.chg_count, x.nchg);
@@ -917,6 +904,13 @@ int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s)
   const bool air = (a.flags & 1) != 0;
   if constexpr (G == 1) {
     if (qpf == 3 && KP <= 32) {
+      if ((a.flags & 2) && (mode == 3 || mode == 4)) {  // A/B: word-sorted slots loaded on change
+        if (air && mode == 4) k_gibbs_x1<KP, 4, true, true><<<grid, kBlock, 0, s>>>(a);
+        else if (air) k_gibbs_x1<KP, 3, true, true><<<grid, kBlock, 0, s>>>(a);
+        else if (mode == 4) k_gibbs_x1<KP, 4, false, true><<<grid, kBlock, 0, s>>>(a);
+        else k_gibbs_x1<KP, 3, false, true><<<grid, kBlock, 0, s>>>(a);
+        return (int)hipGetLastError();
+      }
       if (air) {
         switch (mode) {
           case 0: k_gibbs_x1<KP, 0, true><<<grid, kBlock, 0, s>>>(a); break;
@@ -937,6 +931,11 @@ int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s)
       return (int)hipGetLastError();
     }
   } else {
+    if (qpf == 2 && air && (a.flags & 4) && (mode == 0 || mode == 4)) {  // A/B: 4-wave register budget
+      if (mode == 0) k_gibbs_ldsg<G, KP, 0, 4><<<grid, kBlock, 0, s>>>(a);
+      else k_gibbs_ldsg<G, KP, 4, 4><<<grid, kBlock, 0, s>>>(a);
+      return (int)hipGetLastError();
+    }
     if (qpf == 2 && air) {
       switch (mode) {
         case 0: k_gibbs_ldsg<G, KP, 0><<<grid, kBlock, 0, s>>>(a); break;

@@ -73,8 +73,11 @@ class GibbsConfig:
     # the score of its event -- follows that one draw: a rare word sampled into a minor topic of
     # its document scores as if it were an anomaly. The averaged counts give it its posterior
     # topic mix, as lda-c's variational β / γ do. 1 = the final sample only.
-    post_samples: int = field(default_factory=lambda: int(os.environ.get("ONI_POST_SAMPLES", "8")))
-    post_every: int = 2
+    # Default: every sweep of the last quarter of the chain, at most 50 (sweeps 151-200 of a
+    # 200-sweep day). With post_every = 1 the sample sums are added inside the captured sweep
+    # graphs (three integer adds per sweep), so the averaging costs no eager launches.
+    post_samples: int = field(default_factory=lambda: int(os.environ.get("ONI_POST_SAMPLES", "50")))
+    post_every: int = field(default_factory=lambda: int(os.environ.get("ONI_POST_EVERY", "1")))
 
     def resolved_alpha(self) -> float:
         return float(self.alpha) if self.alpha is not None else 50.0 / self.K
@@ -213,6 +216,7 @@ class GibbsLDA:
         if comm is not None and comm.dist and self.KS % 2 == 0 and self._x01_wanted():
             self._setup_x01()
         self._avg = None          # posterior-averaging accumulators (plan_average)
+        self._acc = False         # sweeps add their counts to the accumulators (inside graphs too)
         self._avg_at: list = []   # sweep counts at which a sample is added
         self._avg_cache = None    # (θ, φ) of the completed average
 
@@ -441,6 +445,8 @@ class GibbsLDA:
         self.a, self.b, self.cn = 1 - self.a, 1 - self.b, 1 - self.cn
         self.sweeps_done += 1
         self._tail_cache = None
+        if self._acc:
+            self._accumulate()
         if not self._capturing:
             self._zw_synced = mode == 3
 
@@ -536,7 +542,7 @@ class GibbsLDA:
         self.a, self.b, self.cn, self.sweeps_done, self._aux_synced = saved
         self._force_mode = None
         entry = (g, (self.a, self.b, self.cn))
-        self._graphs[mode] = entry
+        self._graphs[(mode, self._acc)] = entry
         return entry
 
     @traced("oni:lda.sweeps")
@@ -550,10 +556,26 @@ class GibbsLDA:
         try:
             while n > 0:
                 nxt = [p for p in self._avg_at if p > self.sweeps_done]
-                seg = min(n, nxt[0] - self.sweeps_done) if nxt else n
+                contiguous = self._avg is not None and int(self.cfg.post_every) == 1
+                if nxt and contiguous and self.sweeps_done + 1 >= nxt[0]:
+                    # inside a contiguous window: every sweep adds its sample, in the graph
+                    seg = min(n, self._avg_at[-1] - self.sweeps_done)
+                    self._acc = True
+                    try:
+                        self._sweep_n(seg)
+                    finally:
+                        self._acc = False
+                    self._avg["n"] += seg
+                    self._avg_cache = None
+                    n -= seg
+                    continue
+                if nxt and contiguous:
+                    seg = min(n, nxt[0] - 1 - self.sweeps_done)
+                else:
+                    seg = min(n, nxt[0] - self.sweeps_done) if nxt else n
                 self._sweep_n(seg)
                 n -= seg
-                if self._avg is not None and self.sweeps_done in self._avg_at:
+                if not contiguous and self._avg is not None and self.sweeps_done in self._avg_at:
                     self._add_sample()
         finally:
             if self._watchdog is not None:
@@ -639,7 +661,7 @@ class GibbsLDA:
                 self._sync_aux_z()
             if m1 == 3:
                 self._ensure_zw()
-            entry = self._graphs.get(m1)
+            entry = self._graphs.get((m1, self._acc))
             if entry is not None and entry[1] != (self.a, self.b, self.cn):
                 self._one_sweep()  # realign parities with the captured pair
                 self._note_changes()
@@ -647,7 +669,8 @@ class GibbsLDA:
                 continue
             if entry is None:
                 entry = self._capture(m1)
-                if self.auto and self.cfg.auto_switch == 0 and m1 == self.early and self.mode not in self._graphs:
+                if (self.auto and self.cfg.auto_switch == 0 and m1 == self.early
+                        and (self.mode, self._acc) not in self._graphs):
                     self._capture(self.mode)  # capture the delta pair now: no capture stall at the switch
             self._graph = entry[0]
             entry[0].replay()
@@ -664,8 +687,8 @@ class GibbsLDA:
         """Average the counts of the samples at sweeps total, total - e, …, total - (S-1)·e
         (e = cfg.post_every, S = cfg.post_samples capped at total / 4e)."""
         S, e = max(1, int(self.cfg.post_samples)), max(1, int(self.cfg.post_every))
-        # at most the last quarter of the chain (burn-in first): a 200-sweep day averages 8
-        # samples over sweeps 186-200, a 30-sweep run 3, a run of < 8 sweeps none
+        # at most the last quarter of the chain (burn-in first): a 200-sweep day averages the 50
+        # samples of sweeps 151-200, a 30-sweep run 7, a run of < 8 sweeps none
         S = min(S, int(total_sweeps) // (4 * e))
         at = [total_sweeps - j * e for j in range(S) if total_sweeps - j * e > 0]
         self._avg_at = sorted(at) if S > 1 else []
@@ -702,12 +725,16 @@ class GibbsLDA:
         a["n"] = int(st["n"])
         self._avg_cache = None
 
-    def _add_sample(self) -> None:
+    def _accumulate(self) -> None:
+        """Add the current counts to the sample sums (device ops only: capturable)."""
         a = self._avg
         a["wk"] += self.nwk
         a["k"] += self.nk_cur
         a["dk"] += self.ndk_cur
-        a["n"] += 1
+
+    def _add_sample(self) -> None:
+        self._accumulate()
+        self._avg["n"] += 1
         self._avg_cache = None
 
     def _averaged(self):

@@ -433,7 +433,9 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
     a.n_slices, a.K, a.KS, a.alpha, a.seed0, a.seed1 = n_slices, K, KS, float(alpha), s0, s1
     a.nk_rep = nk_rep
     # the caller vouches that n + α is exact in f32 for every doc-topic count of this corpus
-    a.flags = 1 if alpha_in_row else 0
+    # ONI_SAMPLER_AB (kernel A/B, bench/sampler_ab.py): bit 0 = word-sorted slots loaded on change
+    # (k_gibbs_x1), bit 1 = 4-wave register budget (k_gibbs_ldsg)
+    a.flags = (1 if alpha_in_row else 0) | (int(os.environ.get("ONI_SAMPLER_AB", "0")) & 3) << 1
     _lib.check(_lib.lib().oni_gibbs_launch(C.byref(a), G, KP, 1 if init else 0, int(mode), int(sampler),
                                            _lib.stream()), "oni_gibbs_launch")
 
