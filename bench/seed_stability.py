@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""Seed stability of the top-N (verdict r3 item 4): the suspicious rows an analyst reviews should be
+a property of the data, not of the sampler's seed. Runs the bench day (12.5M flows, K = 20, 200
+sweeps, top-3000) with several LDA seeds on one GPU and reports the mean pairwise overlap of the
+top-N row sets, planted recall per seed, and day time; the same for the realistic-vocabulary day.
+
+  python bench/seed_stability.py --seeds 3
+"""
+from __future__ import annotations
+
+import argparse
+import itertools
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--flows", type=int, default=12_500_000)
+    ap.add_argument("--seeds", type=int, default=3)
+    ap.add_argument("--maxresults", type=int, default=3000)
+    ap.add_argument("--sweeps", type=int, default=200)
+    ap.add_argument("--days", default="default,realistic")
+    ap.add_argument("--deep", type=int, default=4, help="also rank each seed's rows this many times deeper")
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+
+    from oni355.pipeline.flow import run_flow
+    from oni355.synth.flow import generate_flows
+
+    out = {"flows": a.flows, "maxresults": a.maxresults, "sweeps": a.sweeps, "post_samples":
+           os.environ.get("ONI_POST_SAMPLES", "default"), "days": {}}
+    for kind in a.days.split(","):
+        day = generate_flows(a.flows, seed=7, wide_vocab=kind == "realistic")
+        planted = set(np.asarray(day.anomaly_rows).tolist())
+        tops, rec, times = [], [], []
+        run_flow(day.cols, K=20, sweeps=4, maxresults=10, device="cuda:0")  # warm-up (code objects, pools)
+        for i in range(a.seeds):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            res = run_flow(day.cols, K=20, sweeps=a.sweeps, maxresults=a.maxresults * a.deep, device="cuda:0",
+                           seed=0x0D15EA5E + 7919 * i)
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - t0)
+            deep = np.asarray(res.rows)
+            tops.append((set(deep[: a.maxresults].tolist()), set(deep.tolist()), np.asarray(res.scores)))
+            rows = tops[-1][0]
+            rec.append(len(rows & planted) / max(len(planted), 1))
+        ov = [len(x[0] & y[0]) / a.maxresults for x, y in itertools.combinations(tops, 2)]
+        # boundary jitter: how much of one seed's top-N is inside another seed's top-(deep·N)
+        ovd = [len(x[0] & y[1]) / a.maxresults for x, y in itertools.permutations(tops, 2)]
+        sc = tops[0][2]
+        margin = {"score_at_N": float(sc[a.maxresults - 1]), "score_at_N_over_2": float(sc[a.maxresults // 2]),
+                  "score_at_deep": float(sc[-1]), "rows_within_1pct_of_score_at_N":
+                  int(((sc >= sc[a.maxresults - 1] * 0.99) & (sc <= sc[a.maxresults - 1] * 1.01)).sum())}
+        out["days"][kind] = {"topN_overlap_mean": round(float(np.mean(ov)), 4), "topN_overlap_pairs": [round(v, 4) for v in ov],
+                             f"topN_within_top{a.deep}N_mean": round(float(np.mean(ovd)), 4), "margin_seed0": margin,
+                             "recall": [round(r, 4) for r in rec], "day_s": [round(t, 4) for t in times],
+                             "vocab": int(res.stats.get("V", 0)), "loglik": float(res.stats["loglik"])}
+        print(json.dumps({kind: out["days"][kind]}), file=sys.stderr, flush=True)
+    print(json.dumps(out))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
