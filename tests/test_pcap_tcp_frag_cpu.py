@@ -152,3 +152,43 @@ def test_duplicate_fragment_is_dropped_not_a_new_datagram(tmp_path):
         assert c["dns_a"].to_list() == ["5.6.7.8"]
         assert c["unix_tstamp"].tolist() == [t0 + 2]
         assert c["_frag_incomplete"] == 0
+
+
+def test_parallel_index_equals_sequential_walk(tmp_path):
+    """The classic-pcap index runs in parallel byte ranges with speculated record starts, stitched
+    exactly: any thread count gives the sequential walk's packets -- including payloads that
+    imitate record headers (a UDP payload carrying copies of pcap record headers) and a truncated
+    final record."""
+    import numpy as np
+    from oni355.synth.dns import generate_dns, write_pcap
+    day = generate_dns(3000, seed=9)
+    p = str(tmp_path / "d.pcap")
+    write_pcap(day, p)
+    ref = read_pcap_dns(p, threads=1)
+    for th in (2, 3, 7, 16, 64):
+        got = read_pcap_dns(p, threads=th)
+        for k in ("unix_tstamp", "frame_len", "ip_src", "ip_dst", "dns_qry_type", "dns_qry_rcode"):
+            assert np.array_equal(ref[k], got[k]), (th, k)
+        assert ref["dns_qry_name"].to_list() == got["dns_qry_name"].to_list()
+        assert got["_packets"] == ref["_packets"]
+    # decoys: payloads full of plausible record headers, then a truncated tail record
+    srv, cli = "10.0.0.53", "10.1.2.3"
+    decoy = struct.pack("<IIII", 1467936000, 0, 40, 40) * 24
+    frames = []
+    for i in range(400):
+        if i % 3 == 0:
+            frames.append((1467936000 + i, _eth(_ipv4(srv, cli, 17, _udp(9999, 9999, decoy)))))
+        else:
+            frames.append((1467936000 + i, _eth(_ipv4(srv, cli, 17, _udp(53, 4000 + i, _dns_response(
+                i, f"h{i}.example.com", answers=["9.9.9.9"]))))))
+    q = str(tmp_path / "decoy.pcap")
+    _write_ts(q, frames)
+    with open(q, "ab") as f:
+        f.write(struct.pack("<IIII", 1467937000, 0, 500, 500) + b"\x00" * 100)  # truncated record
+    ref = read_pcap_dns(q, threads=1)
+    assert ref["_packets"] == 400
+    for th in (2, 5, 13, 32):
+        got = read_pcap_dns(q, threads=th)
+        assert got["_packets"] == 400
+        assert got["dns_qry_name"].to_list() == ref["dns_qry_name"].to_list()
+        assert np.array_equal(got["unix_tstamp"], ref["unix_tstamp"])
