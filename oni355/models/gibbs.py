@@ -232,14 +232,20 @@ class GibbsLDA:
         return self.dn[0].numel() * self.dn[0].element_size() >= min_bytes
 
     def _setup_x01(self) -> None:
-        """Packed X01 payload (csrc/kernels/x01.hip): words whose local token count is at most
-        O = ⌊32767 / W⌋ on every rank travel as two offset 16-bit halves per int32 word. Their
-        per-rank value (an absolute local count in recount sweeps, a delta otherwise) is bounded by
-        that local count, so the packed ring sum is exact; everything else stays int32."""
+        """Packed X01 payload (csrc/kernels/x01.hip). A word's per-rank value (an absolute local
+        count in recount sweeps, a delta otherwise) is bounded by its local token count c_{w,r}, so
+        words with max_r c_{w,r} ≤ O8 = ⌊127 / W⌋ travel as four offset bytes per int32 word, words
+        up to O = ⌊32767 / W⌋ as two offset 16-bit halves, and the ring sum stays exact; the rest
+        stays int32. A realistic vocabulary is mostly rare words: 13.6 MB → ~3.4 MB per sweep at
+        V = 170k, K = 20 (dense → 8-bit)."""
         W = self.comm.world
         O = 32767 // W
-        if os.environ.get("ONI_X01_LIGHT_MAX"):  # tests: force a light/heavy mix on small days
+        O8 = 127 // W
+        if os.environ.get("ONI_X01_LIGHT_MAX"):  # tests: force a tiny/light/heavy mix on small days
             O = min(O, int(os.environ["ONI_X01_LIGHT_MAX"]))
+        if os.environ.get("ONI_X01_TINY_MAX"):
+            O8 = min(O8, int(os.environ["ONI_X01_TINY_MAX"]))
+        O8 = min(O8, O)
         V, KS = self.V, self.KS
         dev = self.device
         cnt = torch.zeros(V, dtype=torch.int64, device=dev)
@@ -248,14 +254,18 @@ class GibbsLDA:
             edges = torch.searchsorted(ws, torch.arange(V + 1, dtype=torch.int64, device=dev))
             cnt += edges[1:] - edges[:-1]
         self.comm.allreduce_(cnt, op="max")
-        light = torch.nonzero(cnt <= O).flatten().to(torch.int32)
+        if KS % 4:
+            O8 = -1  # four counts per word need KS % 4 == 0 (always true for choose_tiling)
+        tiny = torch.nonzero(cnt <= O8).flatten().to(torch.int32)
+        light = torch.nonzero((cnt > O8) & (cnt <= O)).flatten().to(torch.int32)
         heavy = torch.nonzero(cnt > O).flatten().to(torch.int32)
         tail_off, tail_len = V * KS, self.dn[0].numel() - V * KS
-        n = ops.x01_packed_len(light.numel(), heavy.numel(), KS, tail_len)
+        n = ops.x01_packed_len(tiny.numel(), light.numel(), heavy.numel(), KS, tail_len)
         if n >= self.dn[0].numel():
             return
-        self._x01 = dict(light=light.contiguous(), heavy=heavy.contiguous(), O=O, WO=W * O, tail_off=tail_off,
-                         tail_len=tail_len, buf=torch.zeros(n, dtype=torch.int32, device=dev))
+        self._x01 = dict(tiny=tiny.contiguous(), light=light.contiguous(), heavy=heavy.contiguous(), O8=max(O8, 0),
+                         O=O, WO8=W * max(O8, 0), WO=W * O, tail_off=tail_off, tail_len=tail_len,
+                         buf=torch.zeros(n, dtype=torch.int32, device=dev))
 
     # ---------------------------------------------------------------------------------------------
     def _state(self, init: bool) -> dict:
@@ -463,9 +473,11 @@ class GibbsLDA:
             e0.record()
         x = self._x01
         if x is not None:
-            ops.x01_pack(buf, x["light"], x["heavy"], self.KS, x["tail_off"], x["tail_len"], x["O"], x["buf"])
+            ops.x01_pack(buf, x["tiny"], x["light"], x["heavy"], self.KS, x["tail_off"], x["tail_len"], x["O8"], x["O"],
+                         x["buf"])
             self.comm.allreduce_(x["buf"])
-            ops.x01_unpack(x["buf"], x["light"], x["heavy"], self.KS, x["tail_off"], x["tail_len"], x["WO"], buf)
+            ops.x01_unpack(x["buf"], x["tiny"], x["light"], x["heavy"], self.KS, x["tail_off"], x["tail_len"], x["WO8"],
+                           x["WO"], buf)
         else:
             self.comm.allreduce_(buf)
         if timed:

@@ -567,44 +567,59 @@ def copy_rows(src, dst, rows, KS):
 # ------------------------------------------------------------------------------------------------
 # X01 payload packing (csrc/kernels/x01.hip)
 # ------------------------------------------------------------------------------------------------
-def x01_packed_len(L: int, H: int, KS: int, tail_len: int) -> int:
-    return L * (KS // 2) + H * KS + tail_len
+def x01_packed_len(T: int, L: int, H: int, KS: int, tail_len: int) -> int:
+    return T * (KS // 4) + L * (KS // 2) + H * KS + tail_len
 
 
-def x01_pack(dn, light, heavy, KS: int, tail_off: int, tail_len: int, O: int, out) -> None:
-    """Light rows as two offset 16-bit halves per int32 word, heavy rows + tail as int32."""
-    L, H = light.numel(), heavy.numel()
+def x01_pack(dn, tiny, light, heavy, KS: int, tail_off: int, tail_len: int, O8: int, O: int, out) -> None:
+    """Tiny rows as four offset bytes per int32 word, light rows as two offset 16-bit halves,
+    heavy rows + tail as int32 (csrc/kernels/x01.hip)."""
+    T, L, H = tiny.numel(), light.numel(), heavy.numel()
     if not _is_dev(dn):
-        half = KS // 2
+        q, half = KS // 4, KS // 2
         rows = dn[: tail_off].view(-1, KS)
-        lv = (rows[light.long()].to(torch.int64) + O).view(L, half, 2)
-        nl = L * half
-        out[:nl] = (lv[..., 0] | (lv[..., 1] << 16)).reshape(-1).to(torch.int32) if L else out[:0]
-        out[nl:nl + H * KS] = rows[heavy.long()].reshape(-1)
-        out[nl + H * KS:nl + H * KS + tail_len] = dn[tail_off:tail_off + tail_len]
-        return
-    _lib.check(_lib.lib().oni_x01_pack(_lib.ptr(dn), _lib.ptr(light), L, _lib.ptr(heavy), H, KS, tail_off, tail_len,
-                                       O, _lib.ptr(out), _lib.stream()), "oni_x01_pack")
-
-
-def x01_unpack(packed, light, heavy, KS: int, tail_off: int, tail_len: int, WO: int, dn) -> None:
-    """Inverse of :func:`x01_pack` after the sum over W ranks (``WO`` = W·O)."""
-    L, H = light.numel(), heavy.numel()
-    if not _is_dev(dn):
-        half = KS // 2
-        nl = L * half
-        v = packed[:nl].to(torch.int64) & 0xFFFFFFFF
-        rows = dn[: tail_off].view(-1, KS)
+        nt, nl = T * q, L * half
+        if T:
+            tv = (rows[tiny.long()].to(torch.int64) + O8).view(T, q, 4)
+            out[:nt] = _u32_to_i32(tv[..., 0] | (tv[..., 1] << 8) | (tv[..., 2] << 16) | (tv[..., 3] << 24)).reshape(-1)
         if L:
+            lv = (rows[light.long()].to(torch.int64) + O).view(L, half, 2)
+            out[nt:nt + nl] = _u32_to_i32(lv[..., 0] | (lv[..., 1] << 16)).reshape(-1)
+        out[nt + nl:nt + nl + H * KS] = rows[heavy.long()].reshape(-1)
+        out[nt + nl + H * KS:nt + nl + H * KS + tail_len] = dn[tail_off:tail_off + tail_len]
+        return
+    _lib.check(_lib.lib().oni_x01_pack(_lib.ptr(dn), _lib.ptr(tiny), T, _lib.ptr(light), L, _lib.ptr(heavy), H, KS,
+                                       tail_off, tail_len, O8, O, _lib.ptr(out), _lib.stream()), "oni_x01_pack")
+
+
+def _u32_to_i32(v: torch.Tensor) -> torch.Tensor:
+    """int64 tensor of u32 bit patterns → the int32 tensor holding the same bits."""
+    return torch.where(v >= 2**31, v - 2**32, v).to(torch.int32)
+
+
+def x01_unpack(packed, tiny, light, heavy, KS: int, tail_off: int, tail_len: int, WO8: int, WO: int, dn) -> None:
+    """Inverse of :func:`x01_pack` after the sum over W ranks (``WO8`` = W·O8, ``WO`` = W·O)."""
+    T, L, H = tiny.numel(), light.numel(), heavy.numel()
+    if not _is_dev(dn):
+        q, half = KS // 4, KS // 2
+        nt, nl = T * q, L * half
+        rows = dn[: tail_off].view(-1, KS)
+        if T:
+            v = packed[:nt].to(torch.int64) & 0xFFFFFFFF
+            parts = [((v >> (8 * b)) & 0xFF) - WO8 for b in range(4)]
+            rows[tiny.long()] = torch.stack(parts, 1).view(T, KS).to(torch.int32)
+        if L:
+            v = packed[nt:nt + nl].to(torch.int64) & 0xFFFFFFFF
             lo = ((v & 0xFFFF) - WO).to(torch.int32).view(L, half)
             hi = ((v >> 16) - WO).to(torch.int32).view(L, half)
             rows[light.long()] = torch.stack([lo, hi], 2).view(L, KS)
         if H:
-            rows[heavy.long()] = packed[nl:nl + H * KS].view(H, KS)
-        dn[tail_off:tail_off + tail_len] = packed[nl + H * KS:nl + H * KS + tail_len]
+            rows[heavy.long()] = packed[nt + nl:nt + nl + H * KS].view(H, KS)
+        dn[tail_off:tail_off + tail_len] = packed[nt + nl + H * KS:nt + nl + H * KS + tail_len]
         return
-    _lib.check(_lib.lib().oni_x01_unpack(_lib.ptr(packed), _lib.ptr(light), L, _lib.ptr(heavy), H, KS, tail_off,
-                                         tail_len, WO, _lib.ptr(dn), _lib.stream()), "oni_x01_unpack")
+    _lib.check(_lib.lib().oni_x01_unpack(_lib.ptr(packed), _lib.ptr(tiny), T, _lib.ptr(light), L, _lib.ptr(heavy), H,
+                                         KS, tail_off, tail_len, WO8, WO, _lib.ptr(dn), _lib.stream()),
+               "oni_x01_unpack")
 
 
 # ------------------------------------------------------------------------------------------------

@@ -62,8 +62,8 @@ _SIGS = {
     "oni_recount_stream": [vp, vp, i64, vp, C.c_int, C.c_int, C.c_int, vp],
     "oni_delta_recount": [vp, vp, vp, vp, vp, vp, vp, i64, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp],
     "oni_copy_rows": [vp, vp, vp, i64, C.c_int, vp],
-    "oni_x01_pack": [vp, vp, i64, vp, i64, C.c_int, i64, i64, C.c_int, vp, vp],
-    "oni_x01_unpack": [vp, vp, i64, vp, i64, C.c_int, i64, i64, C.c_int, vp, vp],
+    "oni_x01_pack": [vp, vp, i64, vp, i64, vp, i64, C.c_int, i64, i64, C.c_int, C.c_int, vp, vp],
+    "oni_x01_unpack": [vp, vp, i64, vp, i64, vp, i64, C.c_int, i64, i64, C.c_int, C.c_int, vp, vp],
     "oni_score": [vp, vp, C.c_int, vp, vp, vp, vp, i64, f32, vp, vp, vp, vp, vp],
     "oni_select_below": [vp, i64, f32, u32, vp, vp, vp, i64, vp],
     "oni_pair_score": [vp, vp, C.c_int, vp, vp, i64, vp, vp],

@@ -56,6 +56,7 @@ def _run_world(world, n_total, env=None):
 
 @pytest.mark.parametrize("world,env", [(2, None), (3, None), (2, {"ONI_X01_PACK": "1"}),
                                        (3, {"ONI_X01_PACK": "1", "ONI_X01_LIGHT_MAX": "40"}),
+                                       (3, {"ONI_X01_PACK": "1", "ONI_X01_LIGHT_MAX": "40", "ONI_X01_TINY_MAX": "6"}),
                                        (2, {"ONI_X01_PACK": "auto", "ONI_X01_PACK_MIN_BYTES": "0"})])
 def test_dp_matches_single_process(world, env):
     """Also with the packed X01 payload forced into a light/heavy word mix, and unpacked."""
@@ -117,27 +118,31 @@ def test_lpt_place_native_matches_numpy_reference():
 @pytest.mark.parametrize("W", [1, 2, 3, 8])
 def test_x01_packed_sum_is_exact(W):
     """Σ over W ranks of packed buffers (int32 wrap-around, as RCCL sums) unpacks to the exact
-    per-entry sum whenever every light value is within ±O."""
+    per-entry sum whenever every tiny value is within ±O8 and every light value within ±O."""
     from oni355 import ops
     r = np.random.default_rng(W)
     V, KS, tail = 300, 20, 37
-    O = 32767 // W
-    heavy = torch.from_numpy(np.sort(r.choice(V, 40, replace=False)).astype(np.int32))
-    light = torch.from_numpy(np.setdiff1d(np.arange(V), heavy.numpy()).astype(np.int32))
-    n = ops.x01_packed_len(light.numel(), heavy.numel(), KS, tail)
+    O, O8 = 32767 // W, 127 // W
+    perm = r.permutation(V)
+    heavy = torch.from_numpy(np.sort(perm[:40]).astype(np.int32))
+    tiny = torch.from_numpy(np.sort(perm[40:200]).astype(np.int32))
+    light = torch.from_numpy(np.sort(perm[200:]).astype(np.int32))
+    n = ops.x01_packed_len(tiny.numel(), light.numel(), heavy.numel(), KS, tail)
+    assert n == 160 * KS // 4 + 100 * KS // 2 + 40 * KS + tail
     total = torch.zeros(V * KS + tail, dtype=torch.int64)
     acc = torch.zeros(n, dtype=torch.int64)
     for _ in range(W):
         dn = torch.from_numpy(r.integers(-O, O + 1, V * KS + tail).astype(np.int32))
-        dn.view(-1)[: V * KS].view(V, KS)[heavy.long()] = torch.from_numpy(
-            r.integers(-2**24, 2**24, (heavy.numel(), KS)).astype(np.int32))
+        rows = dn.view(-1)[: V * KS].view(V, KS)
+        rows[heavy.long()] = torch.from_numpy(r.integers(-2**24, 2**24, (heavy.numel(), KS)).astype(np.int32))
+        rows[tiny.long()] = torch.from_numpy(r.integers(-O8, O8 + 1, (tiny.numel(), KS)).astype(np.int32))
         total += dn.to(torch.int64)
         out = torch.zeros(n, dtype=torch.int32)
-        ops.x01_pack(dn, light, heavy, KS, V * KS, tail, O, out)
+        ops.x01_pack(dn, tiny, light, heavy, KS, V * KS, tail, O8, O, out)
         acc += out.to(torch.int64) & 0xFFFFFFFF
     summed = ((acc + 2**31) % 2**32 - 2**31).to(torch.int32)  # int32 wrap-around sum
     back = torch.zeros(V * KS + tail, dtype=torch.int32)
-    ops.x01_unpack(summed, light, heavy, KS, V * KS, tail, W * O, back)
+    ops.x01_unpack(summed, tiny, light, heavy, KS, V * KS, tail, W * O8, W * O, back)
     assert torch.equal(back.to(torch.int64), total)
 
 

@@ -26,10 +26,10 @@ def _slice_cols(cols, lo, hi):
             if not k.startswith("_")}
 
 
-def _day(source, n, heavy):
+def _day(source, n, heavy, wide=False):
     if source == "flow":
         from oni355.synth.flow import generate_flows
-        day = generate_flows(n, seed=11)
+        day = generate_flows(n, seed=11, wide_vocab=wide)
         cols = dict(day.cols)
         if heavy:
             r = np.random.default_rng(5)
@@ -52,7 +52,7 @@ def _worker(rank, world, port, job, out_q):
     from oni355.parallel import comm as pc
     comm = pc.init_from_env("cpu") if world > 1 else None
     source, n = job["source"], job["n"]
-    cols = _day(source, n, job.get("heavy", 0.0))
+    cols = _day(source, n, job.get("heavy", 0.0), job.get("wide", False))
     per = n // world
     lo = rank * per
     hi = n if rank == world - 1 else lo + per
@@ -81,9 +81,14 @@ def _worker(rank, world, port, job, out_q):
     n_split = int(c.split["n_split"]) if c.split is not None else 0
     if comm is not None:
         loads = [int(x) for x in torch.cat(comm.allgather_var(torch.tensor([c.T]))).tolist()]
+    m = res.lda.model
+    x = m._x01
+    x01 = None if x is None else dict(tiny=int(x["tiny"].numel()), light=int(x["light"].numel()),
+                                      heavy=int(x["heavy"].numel()), bytes=m.allreduce_bytes_per_sweep(),
+                                      dense_bytes=int(m.dn[0].numel() * 4))
     if rank == 0:
         out_q.put(dict(rows=res.rows, scores=res.scores, loglik=res.stats["loglik"], loads=loads, n_split=n_split,
-                       sweeps=res.lda.model.sweeps_done))
+                       sweeps=m.sweeps_done, x01=x01))
     if comm is not None:
         comm.barrier()
         pc.shutdown()
@@ -197,3 +202,16 @@ def test_checkpoint_inside_averaging_window_resumes_on_another_world(tmp_path, w
     resumed = _run(w_resume, dict(base, ckpt=ck, ckpt_every=0))
     assert resumed["sweeps"] == 16
     _same(ref, resumed)
+
+
+def test_realistic_vocab_world8_packed_x01_bitwise():
+    """A realistic-vocabulary flow day on 8 ranks with the packed X01 payload (8-bit tiny words,
+    16-bit light words, int32 heavy words): bit for bit the single-rank run, at a fraction of the
+    dense payload."""
+    job = dict(source="flow", n=12000, wide=True, env={"ONI_X01_PACK": "1"})
+    one = _run(1, job)
+    eight = _run(8, job)
+    _same(one, eight)
+    x = eight["x01"]
+    assert x is not None and x["tiny"] > 0
+    assert x["bytes"] < 0.4 * x["dense_bytes"], x
