@@ -63,6 +63,9 @@ def build_parser() -> argparse.ArgumentParser:
                     help="--follow: stop after this many seconds without a new complete day")
     ap.add_argument("--max-days", type=int, default=0, help="stop after N days (0: no limit)")
     ap.add_argument("--quiet", action="store_true")
+    ap.add_argument("--service", metavar="SOCKET",
+                    help="forward this run to a warm oni-mld service on SOCKET (env ONI_MLD_SOCKET); runs locally "
+                         "when none answers")
     return ap
 
 
@@ -198,8 +201,31 @@ def load_events(a, cfg, source: str, rank: int, world: int) -> tuple[dict, int, 
     return columnar.read_day(root, source, a.date, row_range=(lo, hi)), lo, n
 
 
+def _service_socket(argv: list[str]) -> tuple[str | None, list[str]]:
+    """``--service PATH`` / ``ONI_MLD_SOCKET``: the resident service (oni355.cli.service) to forward
+    to; returns (path or None, argv without the option)."""
+    path = os.environ.get("ONI_MLD_SOCKET") or None
+    out, it = [], iter(range(len(argv)))
+    for i in it:
+        if argv[i] == "--service" and i + 1 < len(argv):
+            path = argv[i + 1]
+            next(it, None)
+        elif argv[i].startswith("--service="):
+            path = argv[i].split("=", 1)[1]
+        else:
+            out.append(argv[i])
+    return path, out
+
+
 def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
+    svc, argv = _service_socket(argv)
+    if svc and os.environ.get("ONI_MLD_INSIDE") != "1":
+        # a warm service answers: the day runs there (nothing here has imported torch yet)
+        from .service import forward
+        rc = forward(svc, argv)
+        if rc is not None:
+            return rc
     a = build_parser().parse_args(argv)
     from ..config import load_config
     cfg = load_config(a.config if a.config and os.path.exists(a.config) else None,
