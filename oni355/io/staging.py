@@ -22,6 +22,7 @@ import atexit
 import ctypes as C
 import os
 import threading
+import warnings
 
 import numpy as np
 import torch
@@ -100,7 +101,18 @@ def upload_tensor(t: torch.Tensor, device) -> torch.Tensor:
 
 def upload(a, device, dtype: torch.dtype | None = None) -> torch.Tensor:
     """NumPy array (or CPU tensor) → device tensor; ``dtype`` converts on the host first."""
-    t = a if isinstance(a, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(a))
+    if isinstance(a, torch.Tensor):
+        t = a
+    else:
+        a = np.ascontiguousarray(a)
+        if a.flags.writeable:
+            t = torch.from_numpy(a)
+        else:
+            # a read-only store memmap: wrapped without a copy, and this tensor is only ever the
+            # source of the device copy (or of a dtype conversion, which allocates), never written
+            with warnings.catch_warnings():
+                warnings.filterwarnings("ignore", message="The given NumPy array is not writable")
+                t = torch.from_numpy(a)
     if dtype is not None and t.dtype != dtype:
         t = t.to(dtype)
     return upload_tensor(t, device)
