@@ -1,0 +1,560 @@
+// K10-MH -- Metropolis-Hastings LDA sweep with sweep-static alias proposals (k_gibbs_mh), its
+// proposal-table builder (k_mh_alias) and the one-lane init pass for K > 32 (k_gibbs_mh_init).
+//
+// Why: the dense samplers spend K multiply-adds (plus a scan and a search) on every token; at
+// K = 100 k_gibbs_ldsg runs 0.89 ms per 25M-token sweep, bound by the per-token q-row round trip
+// and its 4-lane scans (docs/performance.md). An MH step costs O(1) per token whatever K is: the
+// proposals come from alias tables built once per sweep from the sweep-start snapshot (the word
+// factor q of every word; the sweep-start row of every document spread over several chunks), and
+// the acceptance test needs a handful of counts. Semantics and numerics: oni355/ref/spec.py
+// gibbs_pass_mh / mh_moves / alias_table, replayed bit for bit (tests/test_gpu_mh.py); the moves
+// leave the collapsed conditional invariant (tests/test_mh_conditional.py).
+//
+// Execution model (MI355X-first):
+//  * One lane per chunk (S = 64 chunks per SELL slice, one wave per block): the lane walks its
+//    chunk sequentially. Its doc counts live in LDS as u8 cells, interleaved by lane
+//    (cell k of lane l at byte k*64 + l: any per-lane topic index hits a distinct dword column);
+//    a one-chunk document keeps n_dk (≤ 127), a multi-chunk one keeps n − n_src + 128 (chunks are
+//    ≤ 127 tokens), so 100 topics cost 6.4 KB per wave instead of 25.6 KB of f32 rows. The
+//    chunk's current topics (the one-chunk doc proposal picks a random other token) sit next to
+//    them, also u8 and interleaved.
+//  * Loads are software-pipelined by token: the token word two steps ahead; the next token's
+//    Philox block, q[w, zo], the word table's row sum, its alias entry (and a multi-chunk doc's
+//    alias entry and n_src[zo]) one step ahead -- all independent of the chain state -- so a
+//    step waits only for the gathers that depend on its proposals (q[w, t], n_src[t]).
+//  * Every draw is Philox4x32-10 on (pos, doc key, sweep, 2 + move): a pure function of the data
+//    and the seed, so the chain is bitwise identical for any GPU count or chunk placement.
+#include "gibbs_sampler.h"
+
+struct OniMH {
+  OniGibbs g;
+  const uint32_t* walias;      // [V][K] alias entries (thr24 << 8 | alias) of the word proposal
+  const float* wsum;           // [V] Σ_k q[w, k] (the word table's weight)
+  const uint32_t* dalias;      // [n_long][K] alias entries of the multi-chunk docs' n_src + α
+  const float* mh_g;           // [KS] 1 / (n_k + Vβ + 1)
+  const int32_t* chunk_dslot;  // [C] row of dalias (multi-chunk doc) or -1
+  const int32_t* chunk_len;    // [C] tokens of the chunk
+  float kalpha;                // f32(K) · α
+  float inv_alpha;             // f32(1/α)
+  int32_t lmax;                // longest chunk (LDS topic slice rows)
+  int32_t doc_moves;           // 1 or 2
+};
+
+namespace {
+
+constexpr int kMHBias = 128;
+
+// j = ⌊r·K / 2^32⌋ and the coin (top 24 bits of the low word) of an alias draw
+__device__ __forceinline__ void alias_index(uint32_t r, int K, int& j, uint32_t& coin) {
+  const uint64_t p = (uint64_t)r * (uint32_t)K;
+  j = (int)(p >> 32);
+  coin = (uint32_t)p >> 8;
+}
+__device__ __forceinline__ int alias_resolve(int j, uint32_t coin, uint32_t e) {
+  return coin < (e >> 8) ? j : (int)(e & 0xFFu);
+}
+
+// ---- proposal tables ---------------------------------------------------------------------------
+// One lane per row (rows [0, V): word rows of q; rows [V, V + n_long): sweep-start rows of the
+// multi-chunk docs + α). Sequential f32 per lane, exactly spec.alias_table: sum, scale, classify
+// into the small / large stacks (one u8 array: small grows up from 0, large down from K − 1),
+// pair off, leftovers keep their own index. p and the stack live in LDS, interleaved by lane.
+__global__ __launch_bounds__(64) void k_mh_alias(const float* __restrict__ q, int64_t V, int K, int KS,
+                                                  const int32_t* __restrict__ ndk, const int32_t* __restrict__ rows,
+                                                  int64_t n_long, float alpha, uint32_t* __restrict__ walias,
+                                                  float* __restrict__ wsum, uint32_t* __restrict__ dalias,
+                                                  const int32_t* __restrict__ nk, float vbeta, float* __restrict__ g) {
+  extern __shared__ __align__(16) unsigned char smem_alias[];
+  float* p = reinterpret_cast<float*>(smem_alias);           // [K][64]
+  uint8_t* stk = smem_alias + (size_t)K * 64 * sizeof(float);  // [K][64]
+  const int lane = threadIdx.x;
+  if (blockIdx.x == 0) {
+    for (int k = lane; k < KS; k += 64) g[k] = 1.0f / (((float)nk[k] + vbeta) + 1.0f);
+  }
+  const int64_t row = (int64_t)blockIdx.x * 64 + lane;
+  if (row >= V + n_long) return;
+  const bool word = row < V;
+  const float* qr = q + (word ? row : 0) * KS;
+  const int32_t* br = ndk + (word ? 0 : (int64_t)rows[row - V]) * KS;
+  uint32_t* out = word ? walias + row * K : dalias + (row - V) * K;
+  float tot = 0.f;
+  for (int k = 0; k < K; ++k) {
+    const float w = word ? qr[k] : (float)br[k] + alpha;
+    p[k * 64 + lane] = w;
+    tot = tot + w;
+  }
+  const float scale = (float)K / tot;
+  int ns = 0, nl = 0;
+  for (int k = 0; k < K; ++k) {
+    const float v = p[k * 64 + lane] * scale;
+    p[k * 64 + lane] = v;
+    if (v < 1.0f) stk[(ns++) * 64 + lane] = (uint8_t)k;
+    else stk[(K - 1 - nl++) * 64 + lane] = (uint8_t)k;
+  }
+  while (ns > 0 && nl > 0) {
+    const int s = stk[(--ns) * 64 + lane];
+    const int l = stk[(K - nl) * 64 + lane];
+    --nl;
+    const float ps = p[s * 64 + lane];
+    uint32_t thr = (uint32_t)(ps * 16777216.0f);
+    thr = thr < 0xFFFFFFu ? thr : 0xFFFFFFu;
+    out[s] = (thr << 8) | (uint32_t)l;
+    const float pl = (p[l * 64 + lane] + ps) - 1.0f;
+    p[l * 64 + lane] = pl;
+    if (pl < 1.0f) stk[(ns++) * 64 + lane] = (uint8_t)l;
+    else stk[(K - 1 - nl++) * 64 + lane] = (uint8_t)l;
+  }
+  for (int i = 0; i < ns; ++i) {
+    const int k = stk[i * 64 + lane];
+    out[k] = 0xFFFFFF00u | (uint32_t)k;
+  }
+  for (int i = 0; i < nl; ++i) {
+    const int k = stk[(K - 1 - i) * 64 + lane];
+    out[k] = 0xFFFFFF00u | (uint32_t)k;
+  }
+  if (word) wsum[row] = tot;
+}
+
+// ---- the sweep -----------------------------------------------------------------------------------
+// LDS per block (one wave): (A, B) token-exclusion pairs and g per topic, then the u8 count cells
+// [KS][64] and the chunk topics [lmax][64].
+struct MHLds {
+  float2* qfx;
+  float* gk;
+  uint8_t* cnt;
+  uint8_t* zsl;
+};
+
+// stage-B data of one token (issued one step ahead; none of it depends on the chain state)
+struct MHB {
+  oni::U4 r;     // Philox block (pos, key, sweep, 2)
+  int zo;        // sweep-start topic
+  float qz;      // q[w, zo]
+  float zw;      // Σ_k q[w, k]
+  uint32_t ew;   // word alias entry at j(r.x)
+  uint32_t ed;   // doc alias entry at j(r.z) (multi-chunk docs)
+  int32_t bzo;   // n_src[doc, zo] (multi-chunk docs)
+};
+
+template <int MODE, int DM>
+struct MHLane {
+  const OniMH& m;
+  const OniGibbs& a;
+  MHLds L;
+  int lane;
+  int64_t off;
+  int K, KS;
+  int doc;
+  bool multi;
+  int dslot;
+  int lc;            // chunk length
+  uint32_t pos0, key, sweep;
+  const int32_t* brow;  // n_src row of the doc
+  uint32_t wa[2];       // stage A: token words (parity slots)
+  int32_t pa[2];        // stage A: word-sorted slots (MODE 3/4)
+  MHB b[2];             // stage B (parity slots)
+  int nchg;
+  Pend<MODE> pend;
+
+  __device__ __forceinline__ MHLane(const OniMH& m_) : m(m_), a(m_.g) {}
+
+  __device__ __forceinline__ int cell(int k) const { return (int)L.cnt[k * 64 + lane]; }
+  __device__ __forceinline__ void cell_add(int k, int d) {
+    L.cnt[k * 64 + lane] = (uint8_t)((int)L.cnt[k * 64 + lane] + d);
+  }
+  // n_dk^¬ + α of topic k given its sweep-start count bk (multi-chunk docs)
+  __device__ __forceinline__ float aw(int k, int32_t bk) const {
+    const int v = multi ? bk + cell(k) - kMHBias : cell(k);
+    return (float)v + a.alpha;
+  }
+
+  // stage B of the token at step s (word w): Philox block, then the state-free gathers
+  __device__ __forceinline__ void issue_b(int P, int s, uint32_t w) {
+    MHB& x = b[P];
+    if (w == oni::kPadWord) return;
+    x.r = oni::philox10(oni::U4{pos0 + (uint32_t)s, key, sweep, 2u}, a.seed0, a.seed1);
+    x.zo = (int)L.zsl[s * 64 + lane];
+    const int64_t qrow = (int64_t)w * KS;
+    x.qz = a.q[qrow + x.zo];
+    x.zw = m.wsum[w];
+    int j;
+    uint32_t coin;
+    alias_index(x.r.x, K, j, coin);
+    x.ew = m.walias[(int64_t)w * K + j];
+    if (multi) {
+      alias_index(x.r.z, K, j, coin);
+      x.ed = m.dalias[(int64_t)dslot * K + j];
+      x.bzo = brow[x.zo];
+    }
+  }
+
+  // one token: word move, doc move(s), bookkeeping. Loads of later tokens are issued first.
+  template <int P, bool LOAD_A, bool LOAD_B>
+  __device__ __forceinline__ void step(int s) {
+    constexpr int NX = 1 - P;
+    const int64_t idx = off + (int64_t)s * 64 + lane;
+    const uint32_t w = wa[P];
+    const int32_t pw = pa[P];
+    const MHB x = b[P];
+    const bool act = w != oni::kPadWord;
+    // ---- stage C: the gathers of this token's proposals
+    int tw = 0, td = 0;
+    float qtw = 0.f, qtd = 0.f;
+    int32_t btw = 0, btd = 0;
+    const int64_t qrow = (int64_t)(act ? w : 0u) * KS;
+    if (act) {
+      cell_add(x.zo, -1);  // the token leaves its topic: every count below is n^¬
+      int j;
+      uint32_t coin;
+      alias_index(x.r.x, K, j, coin);
+      tw = alias_resolve(j, coin, x.ew);
+      if (multi) {
+        alias_index(x.r.z, K, j, coin);
+        td = alias_resolve(j, coin, x.ed);
+      } else {
+        const float nd = (float)(lc - 1);
+        const float y = oni::u01(x.r.z) * (nd + m.kalpha);
+        if (y < nd) {
+          int pp = (int)y;
+          pp += pp >= s ? 1 : 0;
+          td = (int)L.zsl[pp * 64 + lane];
+        } else {
+          const int tu = (int)((y - nd) * m.inv_alpha);
+          td = tu < K - 1 ? tu : K - 1;
+        }
+      }
+      qtw = a.q[qrow + tw];
+      qtd = a.q[qrow + td];
+      if (multi) {
+        btw = brow[tw];
+        btd = brow[td];
+      }
+    }
+    // ---- stage B of the next token, stage A of the one after
+    if constexpr (LOAD_B) issue_b(NX, s + 1, wa[NX]);
+    if constexpr (LOAD_A) {
+      wa[P] = a.tok_word[idx + 128];
+      if constexpr (MODE == 3 || MODE == 4) pa[P] = a.wpos[idx + 128];
+    } else {
+      wa[P] = oni::kPadWord;
+    }
+    pend.flush(a, KS);
+    bool changed = false;
+    if (act) {
+      const int zo = x.zo;
+      const float2 ab = L.qfx[zo];
+      const float qe = fmaf(x.qz, ab.x, -ab.y);
+      // word move (from zo): ratio a_t Z_zo / (a_zo Z_t), Z_t = (Z_zo − (q_zo − q'_zo)) + (1 − q_t) g_t
+      const float azo = aw(zo, x.bzo);
+      const float atw = aw(tw, btw);
+      const float d = x.qz - qe;
+      const float zt = (x.zw - d) + ((1.0f - qtw) * L.gk[tw]);
+      int sc = zo;
+      float qs = qe, as = azo;
+      int32_t bs = x.bzo;
+      {
+        const float num = atw * x.zw;
+        const float den = azo * zt;
+        if (tw != zo && oni::u01(x.r.y) * den < num) {
+          sc = tw;
+          qs = qtw;
+          as = atw;
+          bs = btw;
+        }
+      }
+      // doc moves: one-chunk docs ratio q'_t / q'_s; multi-chunk docs
+      // (a_t q'_t bn_s) / (a_s q'_s bn_t), bn = n_src without the token + α
+#pragma unroll
+      for (int c = 0; c < DM; ++c) {
+        uint32_t r3 = x.r.w;
+        int t = td;
+        float qt = td == zo ? qe : qtd;
+        int32_t bt = btd;
+        if (c > 0) {
+          const oni::U4 r2 = oni::philox10(oni::U4{pos0 + (uint32_t)s, key, sweep, 2u + (uint32_t)c}, a.seed0, a.seed1);
+          r3 = r2.w;
+          if (multi) {
+            int j;
+            uint32_t coin;
+            alias_index(r2.z, K, j, coin);
+            t = alias_resolve(j, coin, m.dalias[(int64_t)dslot * K + j]);
+          } else {
+            const float nd = (float)(lc - 1);
+            const float y = oni::u01(r2.z) * (nd + m.kalpha);
+            if (y < nd) {
+              int pp = (int)y;
+              pp += pp >= s ? 1 : 0;
+              t = (int)L.zsl[pp * 64 + lane];
+            } else {
+              const int tu = (int)((y - nd) * m.inv_alpha);
+              t = tu < K - 1 ? tu : K - 1;
+            }
+          }
+          qt = t == zo ? qe : a.q[qrow + t];
+          if (multi) bt = brow[t];
+        }
+        const float u = oni::u01(r3);
+        bool ok;
+        float at = 0.f;
+        if (multi) {
+          at = aw(t, bt);
+          const float bnt = (float)(bt - (t == zo ? 1 : 0)) + a.alpha;
+          const float bns = (float)(bs - (sc == zo ? 1 : 0)) + a.alpha;
+          const float num = (at * qt) * bns;
+          const float den = (as * qs) * bnt;
+          if (t == zo && sc != zo) {
+            // the table holds the token at zo: from sc ≠ zo a draw of zo is a no-op with
+            // probability 1/(b_zo + α)
+            const float bz = (float)bt + a.alpha;
+            ok = (u * bz < bnt) && ((u * den) * bz < num * bnt);
+          } else {
+            ok = u * den < num;
+          }
+        } else {
+          ok = u * qs < qt;
+        }
+        if (ok && t != sc) {
+          sc = t;
+          qs = qt;
+          as = at;
+          bs = bt;
+        }
+      }
+      cell_add(sc, 1);
+      L.zsl[s * 64 + lane] = (uint8_t)sc;
+      changed = sc != zo;
+      if (changed) {
+        ++nchg;
+        pend.note(idx, zo, sc, pw, w);
+      }
+    }
+    if constexpr (MODE == 2) {
+      const uint64_t msk = __ballot(changed);
+      if (lane == 0) {
+        pend.m = msk;
+        pend.mi = (off + (int64_t)s * 64) / 64;
+      }
+    }
+  }
+};
+
+// segmented (same doc, consecutive lanes) suffix sum: the run's first lane gets the run total
+__device__ __forceinline__ int run_sum(int v, int c, int next) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_down(v, o);
+    if (c + o < next) v += t;
+  }
+  return v;
+}
+
+// Epilogue: one-chunk docs store their row; multi-chunk docs add their deltas (summed over the
+// wave's consecutive chunks of the same doc first); the per-topic deltas go to one dnk replica.
+__device__ __forceinline__ void mh_epilogue(const OniMH& m, const MHLds& L, int KS, int lane, int doc, bool live,
+                                            bool multi, bool init, int32_t* red) {
+  const OniGibbs& a = m.g;
+  const int prev_doc = __shfl_up(doc, 1);
+  const bool head = lane == 0 || prev_doc != doc;
+  const uint64_t heads = __ballot(head);
+  const uint64_t above = lane < 63 ? heads & (~0ull << (lane + 1)) : 0ull;
+  const int next = above ? __ffsll((unsigned long long)above) - 1 : 64;
+  const bool any_multi = __ballot(live && multi) != 0ull;
+  int32_t* dst = a.ndk_dst + (int64_t)(live ? doc : 0) * KS;
+  const int32_t* src = a.ndk_src + (int64_t)(live ? doc : 0) * KS;
+  for (int k0 = 0; k0 < KS; k0 += 4) {
+    int d[4];
+    int n[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int v = live ? (int)L.cnt[(k0 + i) * 64 + lane] : 0;
+      n[i] = v;
+      d[i] = 0;
+      if (live) d[i] = multi ? v - kMHBias : v;
+    }
+    if (live && !multi) {
+      if (!init) {
+        const int4 o = *reinterpret_cast<const int4*>(src + k0);
+        d[0] -= o.x; d[1] -= o.y; d[2] -= o.z; d[3] -= o.w;
+      }
+      *reinterpret_cast<int4*>(dst + k0) = make_int4(n[0], n[1], n[2], n[3]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (any_multi && __ballot(live && multi && d[i] != 0)) {
+        const int sm = run_sum(live && multi ? d[i] : 0, lane, next);
+        if (live && multi && head && sm) atomicAdd(dst + k0 + i, sm);
+      }
+      int v = d[i];
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) v += __shfl_xor(v, o);
+      if (lane == 0) red[k0 + i] = v;
+    }
+  }
+  __syncthreads();
+  for (int k = lane; k < KS; k += 64) {
+    const int v = red[k];
+    if (v) atomicAdd(&a.dnk[(int)(blockIdx.x & (unsigned)(a.nk_rep - 1)) * KS + k], v);
+  }
+}
+
+__device__ __forceinline__ MHLds mh_lds(unsigned char* smem, int KS) {
+  MHLds L;
+  L.qfx = reinterpret_cast<float2*>(smem);
+  L.gk = reinterpret_cast<float*>(smem + (size_t)KS * sizeof(float2));
+  L.cnt = smem + (size_t)KS * (sizeof(float2) + sizeof(float) + sizeof(int32_t));
+  L.zsl = L.cnt + (size_t)KS * 64;
+  return L;
+}
+
+template <int MODE, int DM>
+__global__ __launch_bounds__(64) void k_gibbs_mh(const OniMH m) {
+  extern __shared__ __align__(16) unsigned char smem_mh[];
+  const OniGibbs& a = m.g;
+  const int KS = a.KS;
+  MHLane<MODE, DM> x(m);
+  x.L = mh_lds(smem_mh, KS);
+  int32_t* red = reinterpret_cast<int32_t*>(smem_mh + (size_t)KS * (sizeof(float2) + sizeof(float)));
+  const int lane = threadIdx.x;
+  x.lane = lane;
+  x.K = a.K;
+  x.KS = KS;
+  for (int k = lane; k < KS; k += 64) {
+    x.L.qfx[k] = make_float2(a.qfix[k], a.qfix[KS + k]);
+    x.L.gk[k] = m.mh_g[k];
+  }
+  const int64_t slice = blockIdx.x;
+  const int64_t chunk = slice * 64 + lane;
+  const int doc = a.chunk_doc[chunk];
+  const bool live = doc >= 0;
+  x.doc = doc;
+  x.multi = live && a.chunk_multi[chunk] != 0;
+  x.dslot = x.multi ? m.chunk_dslot[chunk] : 0;
+  x.lc = live ? m.chunk_len[chunk] : 0;
+  x.pos0 = live ? (uint32_t)a.chunk_pos0[chunk] : 0u;
+  x.key = live ? a.chunk_key[chunk] : 0u;
+  x.sweep = *a.sweep_ctr;
+  x.brow = a.ndk_src + (int64_t)(live ? doc : 0) * KS;
+  x.nchg = 0;
+  const int len = a.slice_len[slice];
+  x.off = a.slice_off[slice];
+  // count cells: n (one-chunk docs, ≤ 127) or the bias (multi-chunk docs); chunk topics
+  for (int k = 0; k < KS; ++k) {
+    int v = 0;
+    if (live) v = x.multi ? kMHBias : x.brow[k];
+    x.L.cnt[k * 64 + lane] = (uint8_t)v;
+  }
+  for (int s = 0; s < len; ++s) x.L.zsl[s * 64 + lane] = s < x.lc ? a.tok_z[x.off + (int64_t)s * 64 + lane] : 0;
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    x.wa[t] = len > t ? a.tok_word[x.off + t * 64 + lane] : oni::kPadWord;
+    x.pa[t] = ((MODE == 3 || MODE == 4) && len > t) ? a.wpos[x.off + t * 64 + lane] : 0;
+  }
+  x.issue_b(0, 0, x.wa[0]);
+  int s = 0;
+  for (; s + 3 < len; s += 2) {
+    x.template step<0, true, true>(s);
+    x.template step<1, true, true>(s + 1);
+  }
+  for (; s < len; s += 2) {  // the last ≤ 3 steps
+    if (s + 2 < len) x.template step<0, true, true>(s);
+    else if (s + 1 < len) x.template step<0, false, true>(s);
+    else x.template step<0, false, false>(s);
+    if (s + 2 < len) x.template step<1, false, true>(s + 1);
+    else if (s + 1 < len) x.template step<1, false, false>(s + 1);
+  }
+  x.pend.flush(a, KS);
+  if (a.chg_count) add_wave_count(a.chg_count, x.nchg);
+  __syncthreads();
+  mh_epilogue(m, x.L, KS, lane, doc, live, x.multi, false, red);
+}
+
+// init pass (one-lane units, any K): z = ⌊r·K / 2^32⌋ with r the generic init's draw (stream 0,
+// one Philox block per 4 positions) -- the same topics as spec.gibbs_pass(init=True)
+__global__ __launch_bounds__(64) void k_gibbs_mh_init(const OniMH m) {
+  extern __shared__ __align__(16) unsigned char smem_mh[];
+  const OniGibbs& a = m.g;
+  const int KS = a.KS;
+  MHLds L = mh_lds(smem_mh, KS);
+  int32_t* red = reinterpret_cast<int32_t*>(smem_mh + (size_t)KS * (sizeof(float2) + sizeof(float)));
+  const int lane = threadIdx.x;
+  const int64_t slice = blockIdx.x;
+  const int64_t chunk = slice * 64 + lane;
+  const int doc = a.chunk_doc[chunk];
+  const bool live = doc >= 0;
+  const bool multi = live && a.chunk_multi[chunk] != 0;
+  const int lc = live ? m.chunk_len[chunk] : 0;
+  const uint32_t pos0 = live ? (uint32_t)a.chunk_pos0[chunk] : 0u;
+  const uint32_t key = live ? a.chunk_key[chunk] : 0u;
+  const int64_t off = a.slice_off[slice];
+  for (int k = 0; k < KS; ++k) L.cnt[k * 64 + lane] = (uint8_t)(live && multi ? kMHBias : 0);
+  __syncthreads();
+  for (int s = 0; s < lc; ++s) {
+    const uint32_t pos = pos0 + (uint32_t)s;
+    const oni::U4 r = oni::philox10(oni::U4{pos >> 2, key, 0u, 0u}, a.seed0, a.seed1);
+    const uint32_t rr = oni::pick4(r, pos & 3u);
+    const int z = (int)(((uint64_t)rr * (uint32_t)a.K) >> 32);
+    L.cnt[z * 64 + lane] = (uint8_t)((int)L.cnt[z * 64 + lane] + 1);
+    a.tok_z[off + (int64_t)s * 64 + lane] = (uint8_t)z;
+  }
+  __syncthreads();
+  mh_epilogue(m, L, KS, lane, doc, live, multi, true, red);
+}
+
+}  // namespace
+
+static size_t mh_lds_bytes(int KS, int lmax) {
+  return (size_t)KS * (sizeof(float2) + sizeof(float) + sizeof(int32_t)) + (size_t)KS * 64 + (size_t)lmax * 64;
+}
+
+ONI_API int oni_mh_tables(const float* q, int64_t V, int K, int KS, const int32_t* ndk, const int32_t* rows,
+                          int64_t n_long, float alpha, uint32_t* walias, float* wsum, uint32_t* dalias,
+                          const int32_t* nk, float vbeta, float* g, hipStream_t s) {
+  if (K < 1 || K > 255 || K > KS || KS % 4 || V < 0 || n_long < 0) return (int)hipErrorInvalidValue;
+  const int64_t nrows = V + n_long;
+  const unsigned grid = (unsigned)((nrows + 63) / 64 > 0 ? (nrows + 63) / 64 : 1);
+  const size_t lds = (size_t)K * 64 * (sizeof(float) + 1);
+  k_mh_alias<<<grid, 64, lds, s>>>(q, V, K, KS, ndk, rows, n_long, alpha, walias, wsum, dalias, nk, vbeta, g);
+  return (int)hipGetLastError();
+}
+
+ONI_API int oni_gibbs_mh_launch(const OniMH* m, int init, int mode, hipStream_t s) {
+  const OniGibbs& a = m->g;
+  if (a.K < 1 || a.K > 255 || a.K > a.KS || a.KS % 4 || a.KS > 256 || mode < 0 || mode > 4) return (int)hipErrorInvalidValue;
+  if (a.nk_rep < 1 || (a.nk_rep & (a.nk_rep - 1))) return (int)hipErrorInvalidValue;
+  if (m->lmax < 1 || m->lmax > 127 || !m->chunk_len) return (int)hipErrorInvalidValue;
+  if (a.n_slices < 1) return 0;
+  const unsigned grid = (unsigned)a.n_slices;
+  const size_t lds = mh_lds_bytes(a.KS, m->lmax);
+  if (init) {
+    k_gibbs_mh_init<<<grid, 64, lds, s>>>(*m);
+    return (int)hipGetLastError();
+  }
+  if (!a.qfix || !m->walias || !m->wsum || !m->mh_g || !m->chunk_dslot) return (int)hipErrorInvalidValue;
+  if (m->doc_moves < 1 || m->doc_moves > 2) return (int)hipErrorInvalidValue;
+  if (mode == 2 && !a.chg_mask) return (int)hipErrorInvalidValue;
+  if (mode == 3 && (!a.wpos || !a.z_w)) return (int)hipErrorInvalidValue;
+  if (mode == 4 && (!a.wpos || !a.zz_w || !a.chg_mask)) return (int)hipErrorInvalidValue;
+#define ONI_MH(md, dm) k_gibbs_mh<md, dm><<<grid, 64, lds, s>>>(*m)
+  if (m->doc_moves == 1) {
+    switch (mode) {
+      case 0: ONI_MH(0, 1); break;
+      case 1: ONI_MH(1, 1); break;
+      case 2: ONI_MH(2, 1); break;
+      case 3: ONI_MH(3, 1); break;
+      default: ONI_MH(4, 1); break;
+    }
+  } else {
+    switch (mode) {
+      case 0: ONI_MH(0, 2); break;
+      case 1: ONI_MH(1, 2); break;
+      case 2: ONI_MH(2, 2); break;
+      case 3: ONI_MH(3, 2); break;
+      default: ONI_MH(4, 2); break;
+    }
+  }
+#undef ONI_MH
+  return (int)hipGetLastError();
+}
+
+ONI_API int oni_mh_sizeof_args() { return (int)sizeof(OniMH); }

@@ -22,6 +22,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from ..ref import spec
 from ..utils.obs import traced
 from ..utils import fault
 from .corpus import Corpus, canonical_tokens
@@ -31,7 +32,18 @@ NK_REP = 32
 # X01 payload packing pays only once the all-reduce is bandwidth-bound (see GibbsLDA._x01_wanted)
 X01_PACK_MIN_BYTES = 4 << 20
 # sweep kernels (-> oni_gibbs_launch variant argument): every one draws the same topics bit for bit
-SAMPLERS = {"generic": 0, "lds": 2, "x1": 3}
+SAMPLERS = {"generic": 0, "lds": 2, "x1": 3, "mh": ops.SAMPLER_MH}
+
+
+def sampler_for(K: int, sampler: str | None = None) -> str:
+    """The sweep kernel a K-topic model runs (``sampler`` or ONI_SAMPLER, default "auto"); the
+    corpus must be built for its tiling (ops.choose_tiling(K, "mh") for the MH sampler)."""
+    s = sampler if sampler is not None else os.environ.get("ONI_SAMPLER", "auto")
+    return s
+
+
+def tiling_for(K: int, sampler: str | None = None) -> tuple[int, int]:
+    return ops.choose_tiling(K, "mh" if sampler_for(K, sampler) == "mh" else None)
 
 
 @dataclass
@@ -115,7 +127,7 @@ class GibbsLDA:
         self.cfg = cfg
         self.comm = comm
         self.K = cfg.K
-        self.G, self.KP = ops.choose_tiling(cfg.K)
+        self.G, self.KP = tiling_for(cfg.K, cfg.sampler)
         if corpus.G != self.G:
             raise ValueError(f"corpus built for G={corpus.G}, K={cfg.K} needs G={self.G}")
         self.KS = self.G * self.KP
@@ -186,8 +198,12 @@ class GibbsLDA:
             self.chg_mask = torch.zeros(max(corpus.sell_slots // corpus.S, 1), dtype=torch.int64, device=dev)
         if cfg.sampler not in SAMPLERS and cfg.sampler != "auto":
             raise ValueError(f"unknown sampler {cfg.sampler}")
+        self.mh = cfg.sampler == "mh"
         if cfg.sampler == "auto":
             self.qpf = SAMPLERS["x1"] if self.G == 1 else SAMPLERS["lds"]
+        elif self.mh:
+            self.qpf = SAMPLERS["mh"]
+            self._setup_mh()
         else:
             self.qpf = SAMPLERS[cfg.sampler]
             if (self.qpf == SAMPLERS["x1"]) != (self.G == 1) and self.qpf != SAMPLERS["generic"]:
@@ -195,7 +211,7 @@ class GibbsLDA:
         # the specialised kernels keep n + α as f32 in their count rows: exact only when every
         # n + α of this corpus is (one device read of the longest document); else generic
         self._air = False
-        if self.qpf != SAMPLERS["generic"]:
+        if self.qpf not in (SAMPLERS["generic"], SAMPLERS["mh"]):
             self._air = _alpha_in_row_exact(self.alpha, corpus.max_doc_len())
             if not self._air:
                 self.qpf = SAMPLERS["generic"]
@@ -219,6 +235,28 @@ class GibbsLDA:
         self._acc = False         # sweeps add their counts to the accumulators (inside graphs too)
         self._avg_at: list = []   # sweep counts at which a sample is added
         self._avg_cache = None    # (θ, φ) of the completed average
+
+    def _setup_mh(self) -> None:
+        """MH sampler state: per-sweep alias tables (words; documents spread over several chunks,
+        which propose from their sweep-start row) and every chunk's row in the doc table."""
+        c = self.c
+        if c.L > spec.MH_MAX_CHUNK or (c.chunk_len.numel() and int(c.chunk_len.max()) > spec.MH_MAX_CHUNK):
+            raise ValueError(f"the MH sampler needs chunks of at most {spec.MH_MAX_CHUNK} tokens (corpus L = {c.L})")
+        dev = self.device
+        live = c.chunk_doc >= 0
+        multi = live & (c.chunk_multi != 0)
+        rows = torch.unique(c.chunk_doc[multi].to(torch.int64))
+        self.mh_rows = rows.to(torch.int32)
+        dslot = torch.full_like(c.chunk_doc, -1)
+        if rows.numel():
+            dslot[multi] = torch.searchsorted(rows, c.chunk_doc[multi].to(torch.int64)).to(torch.int32)
+        self.chunk_dslot = dslot
+        self.walias = torch.zeros(self.V, self.K, dtype=torch.int32, device=dev)
+        self.wsum = torch.zeros(self.V, dtype=torch.float32, device=dev)
+        self.dalias = torch.zeros(max(int(rows.numel()), 1), self.K, dtype=torch.int32, device=dev)
+        self.mh_g = torch.zeros(self.KS, dtype=torch.float32, device=dev)
+        self.mh_doc_moves = int(os.environ.get("ONI_MH_DOC_MOVES", "1"))
+        self.mh_lmax = max(1, min(int(c.L), spec.MH_MAX_CHUNK))
 
     def _x01_wanted(self) -> bool:
         """``ONI_X01_PACK``: "1" always packs, "0" never, "auto" (default) packs when the dense Δ
@@ -293,8 +331,12 @@ class GibbsLDA:
         self.cn = 0
         # topics drawn without n_wk atomics, then n_wk rebuilt by the word-sorted recount (integer
         # counts: identical to the atomic build, without its same-address contention)
-        ops.gibbs_pass(self._state(True), self.G, self.KP, self.K, self.alpha, self.cfg.seed, True,
-                       self.sweep_ctr, self.c.chunk_len, host_sweep=0, mode=0)
+        st = self._state(True)
+        if self.mh:
+            st["mh_lmax"] = self.mh_lmax
+        ops.gibbs_pass(st, self.G, self.KP, self.K, self.alpha, self.cfg.seed, True,
+                       self.sweep_ctr, self.c.chunk_len, host_sweep=0, mode=0,
+                       sampler=SAMPLERS["mh"] if self.mh else 0)
         ops.recount(self.c.wsorted, self.c.wslot, self.tok_z, self.nwk, self.KS)
         self._split_sync_absolute(self.ndk[0])
         if self.comm is not None and self.comm.dist:
@@ -424,10 +466,18 @@ class GibbsLDA:
             self._ensure_zw()
         # long (chunked) documents add their Δn_dk into ndk[1-a] rows that hold a copy of ndk[a]:
         # every apply -- the previous sweep's, or _prime()'s after init / resume -- seeds that copy
-        ops.gibbs_pass(self._state(False), self.G, self.KP, self.K, self.alpha, self.cfg.seed, False,
+        st = self._state(False)
+        if self.mh:
+            # the snapshot's topic totals: the last apply wrote q from nk[cn]
+            ops.mh_tables(self.q, self.nk[self.cn], self.ndk[self.a], self.mh_rows, self.K, self.alpha, self.vbeta,
+                          self.walias, self.wsum, self.dalias, self.mh_g)
+            st.update(walias=self.walias, wsum=self.wsum, dalias=self.dalias, mh_g=self.mh_g,
+                      chunk_dslot=self.chunk_dslot, mh_lmax=self.mh_lmax)
+        ops.gibbs_pass(st, self.G, self.KP, self.K, self.alpha, self.cfg.seed, False,
                        self.sweep_ctr, c.chunk_len, host_sweep=self.sweeps_done + 1, mode=mode, sampler=self.qpf,
                        chg_mask=self.wbits if mode == 4 else getattr(self, "chg_mask", None), wpos=c.wpos,
-                       z_w=getattr(self, "z_w", None), zz_w=getattr(self, "zz_w", None), alpha_in_row=self._air)
+                       z_w=getattr(self, "z_w", None), zz_w=getattr(self, "zz_w", None), alpha_in_row=self._air,
+                       mh_doc_moves=getattr(self, "mh_doc_moves", 1))
         head = self.dn[self.b][: self.V * self.KS].view(self.V, self.KS)
         if mode == 4:
             # dn[b] head := Δn_wk of the tokens marked in the word-sorted change bitmap

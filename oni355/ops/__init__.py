@@ -21,7 +21,7 @@ from . import _lib
 
 __all__ = [
     "f32_keys", "i64_keys", "quantile_cuts", "bin_keys", "flow_keys", "flow_wordify", "sell_fill",
-    "sell_perm_z", "gibbs_pass", "gibbs_apply", "copy_rows", "score", "select_below", "choose_tiling",
+    "sell_perm_z", "gibbs_pass", "gibbs_apply", "mh_tables", "SAMPLER_MH", "copy_rows", "score", "select_below", "choose_tiling",
 ]
 
 
@@ -49,10 +49,14 @@ def _need(t: torch.Tensor, dtype: torch.dtype, name: str, n: int | None = None) 
 # ------------------------------------------------------------------------------------------------
 # tiling choice for the sampler: (G lanes per unit, KP topics per lane)
 # ------------------------------------------------------------------------------------------------
-def choose_tiling(K: int) -> tuple[int, int]:
+def choose_tiling(K: int, sampler: str | None = None) -> tuple[int, int]:
+    """(G, KP): lanes per sampler unit and topic slots per lane (KS = G·KP ≥ K). ``sampler`` "mh"
+    (k_gibbs_mh) always runs one-lane units (S = 64 chunks a slice) with KS = K rounded up to 4."""
     if K < 1 or K > 255:
         raise ValueError("K must be in [1, 255]")
     r4 = lambda x: (x + 3) // 4 * 4  # noqa: E731
+    if sampler == "mh":
+        return 1, r4(K)
     if K <= 32:
         return 1, r4(K)
     wide = os.environ.get("ONI_TILING", "wide") == "wide"
@@ -352,11 +356,14 @@ def sell_perm_z(chunk_doc, chunk_pos0, chunk_len, S, slice_off, doc_tok_ptr, tok
 # ------------------------------------------------------------------------------------------------
 # sampler
 # ------------------------------------------------------------------------------------------------
+SAMPLER_MH = 4
+
+
 def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init: bool, sweep_ctr: torch.Tensor,
                chunk_len: torch.Tensor, host_sweep: int | None = None, mode: int = 1,
                sampler: int = 0, chg_mask: torch.Tensor | None = None, wpos: torch.Tensor | None = None,
                z_w: torch.Tensor | None = None, zz_w: torch.Tensor | None = None,
-               alpha_in_row: bool = False) -> None:
+               alpha_in_row: bool = False, mh_doc_moves: int = 1) -> None:
     """Launch one init/sweep pass. ``st`` holds the OniGibbs tensors (csrc/kernels/gibbs_sampler.h);
     sweeps also need ``st["qfix"]`` ([2, KS] f32, from :func:`gibbs_apply`).
 
@@ -368,6 +375,10 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
     ``sampler`` (kernel variant; every variant draws the same topics bit for bit): 0 = generic
     k_gibbs, 2 = k_gibbs_ldsg (G > 1), 3 = k_gibbs_x1 (G = 1); the specialised kernels need
     ``alpha_in_row`` (n + α exact in f32 for every count of the corpus), else the generic one runs.
+    4 = k_gibbs_mh, the Metropolis-Hastings sampler (one-lane units, chunks ≤ 127 tokens; NOT the
+    same draws: its own oracle spec.gibbs_pass_mh) which also needs ``st["walias"]``,
+    ``st["wsum"]``, ``st["dalias"]``, ``st["mh_g"]`` (:func:`mh_tables`) and ``st["chunk_dslot"]``;
+    ``mh_doc_moves`` doc moves after each token's word move.
     """
     s0, s1 = spec.split_seed(seed)
     KS = G * KP
@@ -384,15 +395,20 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
     if not _is_dev(st["tok_word"]):
         chg = st.get("chg_count")
         z_before = st["tok_z"].clone() if (chg is not None or mode == 4) else None
-        npst = {k: (v.numpy().view(np.uint32) if k in ("tok_word", "chunk_key") else v.numpy())
-                for k, v in st.items() if v is not None}
+        npst = {k: (v.numpy().view(np.uint32) if k in ("tok_word", "chunk_key", "walias", "dalias") else v.numpy())
+                for k, v in st.items() if isinstance(v, torch.Tensor)}
         npst["dnk"] = npst["dnk"][:KS]  # replica 0 (the sum over replicas is what counts)
         if mode != 1:
             npst["dnwk"] = np.zeros_like(npst["dnwk"])  # discarded: recount rebuilds n_wk
         if not init:
             npst["qfix"] = npst["qfix"].reshape(2, KS)
         sweep_no = int(host_sweep if host_sweep is not None else sweep_ctr.item())
-        spec.gibbs_pass(npst, G, KP, K, alpha, s0, s1, init, sweep_no, chunk_len.numpy())
+        if sampler == SAMPLER_MH and not init:
+            if G != 1:
+                raise ValueError("the MH sampler runs one-lane units")
+            spec.gibbs_pass_mh(npst, KS, K, alpha, s0, s1, sweep_no, chunk_len.numpy(), doc_moves=mh_doc_moves)
+        else:
+            spec.gibbs_pass(npst, G, KP, K, alpha, s0, s1, init, sweep_no, chunk_len.numpy())
         if mode == 3:
             valid = wpos >= 0
             z_w[wpos[valid].long()] = st["tok_z"][valid]
@@ -436,8 +452,48 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
     # ONI_SAMPLER_AB (kernel A/B, bench/sampler_ab.py): bit 0 = word-sorted slots loaded on change
     # (k_gibbs_x1), bit 1 = 4-wave register budget (k_gibbs_ldsg)
     a.flags = (1 if alpha_in_row else 0) | (int(os.environ.get("ONI_SAMPLER_AB", "0")) & 3) << 1
+    if sampler == SAMPLER_MH:
+        if G != 1:
+            raise ValueError("the MH sampler runs one-lane units")
+        m = _lib.OniMH()
+        m.g = a
+        m.chunk_len = _lib.ptr(chunk_len)
+        m.lmax = int(st["mh_lmax"])
+        m.kalpha = float(np.float32(K) * np.float32(alpha))
+        m.inv_alpha = float(np.float32(1.0 / alpha))
+        m.doc_moves = int(mh_doc_moves)
+        if not init:
+            for name in ("walias", "wsum", "dalias", "chunk_dslot"):
+                setattr(m, name, _lib.ptr(st[name]))
+            m.mh_g = _lib.ptr(st["mh_g"])
+        _lib.check(_lib.lib().oni_gibbs_mh_launch(C.byref(m), 1 if init else 0, int(mode), _lib.stream()),
+                   "oni_gibbs_mh_launch")
+        return
     _lib.check(_lib.lib().oni_gibbs_launch(C.byref(a), G, KP, 1 if init else 0, int(mode), int(sampler),
                                            _lib.stream()), "oni_gibbs_launch")
+
+
+def mh_tables(q: torch.Tensor, nk: torch.Tensor, ndk_src: torch.Tensor, long_rows: torch.Tensor, K: int,
+              alpha: float, vbeta: float, walias: torch.Tensor, wsum: torch.Tensor, dalias: torch.Tensor,
+              g: torch.Tensor) -> None:
+    """Per-sweep tables of the MH sampler (k_mh_alias, spec.mh_tables): ``walias`` [V, K] := the
+    alias table of every word's q row and ``wsum`` [V] its sum, ``dalias`` [n_long, K] := that of
+    n_dk + α for every document over several chunks (rows ``long_rows`` of ``ndk_src``),
+    ``g`` [KS] := 1/(n_k + Vβ + 1) of the snapshot's topic totals ``nk``. int32 tensors hold the u32
+    entries."""
+    if not _is_dev(q):
+        wa, ws, da, gg = spec.mh_tables(q.numpy(), nk.numpy(), ndk_src.numpy(), long_rows.numpy(), K, alpha, vbeta)
+        walias.copy_(torch.from_numpy(wa.view(np.int32)))
+        wsum.copy_(torch.from_numpy(ws))
+        if da.shape[0]:
+            dalias.copy_(torch.from_numpy(da.view(np.int32)))
+        g.copy_(torch.from_numpy(gg))
+        return
+    V, KS = q.shape
+    _lib.check(_lib.lib().oni_mh_tables(_lib.ptr(q), V, K, KS, _lib.ptr(ndk_src), _lib.ptr(long_rows),
+                                        long_rows.numel(), float(alpha), _lib.ptr(walias), _lib.ptr(wsum),
+                                        _lib.ptr(dalias), _lib.ptr(nk), float(vbeta), _lib.ptr(g), _lib.stream()),
+               "oni_mh_tables")
 
 
 def delta_recount(wslot, tile_wlo, tile_whi, chg_mask, tok_word, tok_z, tok_zprev, dnwk_out, KS: int, G: int) -> None:

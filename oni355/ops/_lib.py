@@ -38,6 +38,15 @@ class OniGibbs(C.Structure):
     ]
 
 
+class OniMH(C.Structure):
+    """Mirror of ``struct OniMH`` in csrc/kernels/gibbs_mh.hip (size checked at load)."""
+
+    _fields_ = [
+        ("g", OniGibbs), ("walias", vp), ("wsum", vp), ("dalias", vp), ("mh_g", vp), ("chunk_dslot", vp),
+        ("chunk_len", vp), ("kalpha", f32), ("inv_alpha", f32), ("lmax", i32), ("doc_moves", i32),
+    ]
+
+
 _SIGS = {
     "oni_radix_hist": [vp, i64, C.c_int, C.c_int, vp, C.c_int, u32, vp, vp],
     "oni_f32_keys": [vp, i64, vp, vp],
@@ -49,6 +58,9 @@ _SIGS = {
     "oni_sell_perm_z": [vp, vp, vp, i64, C.c_int, vp, vp, vp, vp, C.c_int, vp],
     "oni_gibbs_launch": [C.POINTER(OniGibbs), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp],
     "oni_gibbs_sizeof_args": [],
+    "oni_gibbs_mh_launch": [C.POINTER(OniMH), C.c_int, C.c_int, vp],
+    "oni_mh_sizeof_args": [],
+    "oni_mh_tables": [vp, i64, C.c_int, C.c_int, vp, vp, i64, f32, vp, vp, vp, vp, f32, vp, vp],
     "oni_widen_pair": [vp, vp, i64, vp, vp],
     "oni_quantile_pick": [vp, vp, C.c_int, C.c_int, C.c_int, vp, vp, vp],
     "oni_tail_grid": [],
@@ -109,6 +121,8 @@ def lib() -> C.CDLL:
         for name, args in _OPTIONAL_SIGS.items():
             if hasattr(h, name):
                 _bind(h, name, args)
+        if h.oni_mh_sizeof_args() != C.sizeof(OniMH):
+            raise RuntimeError("OniMH layout mismatch between liboni_hip.so and oni355/ops/_lib.py")
         if h.oni_gibbs_sizeof_args() != C.sizeof(OniGibbs):
             raise RuntimeError("OniGibbs ABI mismatch between Python and liboni_hip.so; rebuild")
         from ..utils import provenance

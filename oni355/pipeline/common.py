@@ -484,14 +484,17 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
         if word_ids is None:
             word_ids = torch.searchsorted(vocab, word_keys64).to(torch.int32)
         use_w = weights is not None
-        G, _ = ops.choose_tiling(K)
+        from ..models.gibbs import sampler_for, tiling_for
+        G, _ = tiling_for(K)
+        mh = sampler_for(K) == "mh"
         if chunk_len <= 0:
             # the global (weighted) token count picks L -- before routing: the placement cuts
             # heavy documents at multiples of L
             T_glob = float(weights.sum()) if use_w else float(doc_keys64.numel())
             if dist_on:
                 T_glob = comm.allreduce_scalar(T_glob, "sum")
-            chunk_len = auto_chunk_len(int(T_glob), G)
+            # the MH sampler's u8 LDS cells hold a chunk's count deltas: chunks ≤ 64 tokens
+            chunk_len = auto_chunk_len(int(T_glob), G, hi=64 if mh else 128)
         udoc, inv, wi, wt, route = route_to_owners(doc_keys64, word_ids, weights, comm,
                                                    split_L=chunk_len if dist_on else 0)
         D, V = int(udoc.numel()), int(vocab.numel())

@@ -372,6 +372,222 @@ def gibbs_apply(nwk, dcur, dnk_cur, nk_cur, K, beta, vbeta):
 
 
 # ------------------------------------------------------------------------------------------------
+# Metropolis-Hastings sampler with sweep-static alias proposals (k_mh_alias / k_gibbs_mh)
+# ------------------------------------------------------------------------------------------------
+MH_BIAS = 128     # multi-chunk docs keep n_view - n_src + MH_BIAS in the kernel's u8 LDS cells
+MH_MAX_CHUNK = 127
+
+
+def alias_table(wts: np.ndarray):
+    """Vose alias tables of the rows of ``wts`` ([R, K] f32, positive), exactly as k_mh_alias builds
+    them (one lane per row, sequential f32): tot = Σ_k w_k in order, p_k = w_k · (K / tot); indices
+    with p < 1 are pushed on the small stack, the others on the large one (both in k order); then
+    while both are non-empty: s = pop small, l = pop large, bucket s := (p_s, alias l),
+    p_l := (p_l + p_s) − 1, l pushed back on small if p_l < 1 else on large. Buckets left over
+    keep their own index. Entry = thr24 << 8 | alias with thr24 = min(⌊p · 2^24⌋, 2^24 − 1)
+    (2^24 − 1 and alias = itself for p ≥ 1): a draw takes j = ⌊r·K / 2^32⌋ and keeps j when the
+    low word's top 24 bits are below thr24, else its alias (:func:`alias_draw`).
+    Returns (tables [R, K] u32, tot [R] f32)."""
+    wts = np.ascontiguousarray(wts, dtype=F32)
+    R, K = wts.shape
+    tot = np.zeros(R, dtype=F32)
+    for k in range(K):
+        tot = (tot + wts[:, k]).astype(F32)
+    scale = (F32(K) / tot).astype(F32)
+    p = (wts * scale[:, None]).astype(F32)
+    stk = np.zeros((R, K), dtype=np.int64)
+    ns = np.zeros(R, dtype=np.int64)
+    nl = np.zeros(R, dtype=np.int64)
+    rows = np.arange(R)
+    for k in range(K):
+        sm = p[:, k] < F32(1)
+        stk[rows[sm], ns[sm]] = k
+        stk[rows[~sm], K - 1 - nl[~sm]] = k
+        ns += sm
+        nl += ~sm
+    prob = np.ones((R, K), dtype=F32)
+    alias = np.tile(np.arange(K, dtype=np.int64), (R, 1))
+    for _ in range(K):
+        r = np.nonzero((ns > 0) & (nl > 0))[0]
+        if r.size == 0:
+            break
+        s_ = stk[r, ns[r] - 1]
+        ns[r] -= 1
+        l_ = stk[r, K - nl[r]]
+        nl[r] -= 1
+        prob[r, s_] = p[r, s_]
+        alias[r, s_] = l_
+        pl = ((p[r, l_] + p[r, s_]).astype(F32) - F32(1)).astype(F32)
+        p[r, l_] = pl
+        sm = pl < F32(1)
+        stk[r[sm], ns[r[sm]]] = l_[sm]
+        ns[r[sm]] += 1
+        stk[r[~sm], K - 1 - nl[r[~sm]]] = l_[~sm]
+        nl[r[~sm]] += 1
+    full = prob >= F32(1)
+    thr = np.minimum((prob * F32(16777216.0)).astype(np.int64), 0xFFFFFF)
+    thr = np.where(full, 0xFFFFFF, thr)
+    alias = np.where(full, np.arange(K)[None, :], alias)
+    return ((thr << 8) | alias).astype(U32), tot
+
+
+def alias_draw(tab_rows: np.ndarray, r: np.ndarray, K: int) -> np.ndarray:
+    """Topic drawn from alias rows ``tab_rows`` ([A, K] u32) with u32 randoms ``r`` ([A])."""
+    prod = np.asarray(r, dtype=U32).astype(U64) * U64(K)
+    j = (prod >> U64(32)).astype(np.int64)
+    coin = ((prod & MASK32) >> U64(8)).astype(np.int64)
+    e = tab_rows[np.arange(j.size), j].astype(np.int64)
+    return np.where(coin < (e >> 8), j, e & 0xFF)
+
+
+def mh_tables(q: np.ndarray, nk: np.ndarray, ndk_src: np.ndarray, long_rows: np.ndarray, K: int, alpha: float,
+              vbeta: float):
+    """Per-sweep tables of the MH sampler (k_mh_alias): the word proposal ∝ q[w, k] (sweep-start
+    word factor) of every word with its row sum, the doc proposal ∝ n_dk + α (sweep-start row) of
+    every document over several chunks, and g_k = 1/(n_k + Vβ + 1) (the word factor a token adds
+    to a topic it moves into). Returns (walias [V, K] u32, wsum [V] f32, dalias [n_long, K] u32,
+    g [KS] f32)."""
+    walias, wsum = alias_table(q[:, :K])
+    b = ndk_src[np.asarray(long_rows, dtype=np.int64), :K].astype(F32) + F32(alpha)
+    dalias = alias_table(b)[0] if b.shape[0] else np.zeros((0, K), dtype=U32)
+    g = (F32(1) / ((nk.astype(F32) + F32(vbeta)).astype(F32) + F32(1))).astype(F32)
+    return walias, wsum, dalias, g
+
+
+def mh_moves(nn, bb, qrow, zo, qe, multi, Nd, s, zslice, drows, wrows, wsum, g, pos, key, sweep, seed0, seed1,
+             K, alpha, doc_moves=1):
+    """The MH moves of one token per row (see :func:`gibbs_pass_mh`). ``nn`` doc counts without the
+    token (the chunk's view), ``bb`` sweep-start doc rows (with the token), ``qrow`` sweep-start q
+    rows (with the token), ``qe`` the word factor of ``zo`` without it, ``Nd`` other tokens in the
+    chunk, ``s`` the token's position, ``zslice`` current topics of the chunk's positions,
+    ``drows`` / ``wrows`` alias rows of the doc (multi-chunk docs) / word, ``wsum`` the word
+    rows' sums, ``g`` [KS] = 1/(D + 1). Returns the new topics."""
+    A = zo.shape[0]
+    ar = np.arange(A)
+    a32 = F32(alpha)
+    kalpha = (F32(K) * a32).astype(F32)
+    inv_a = F32(1.0 / alpha)
+    one = F32(1)
+    Ndf = np.asarray(Nd).astype(F32)
+    tot = (Ndf + kalpha).astype(F32)
+
+    def aw(k):
+        return (nn[ar, k].astype(F32) + a32).astype(F32)
+
+    def qx(k):  # q' (word factor without the token)
+        return np.where(k == zo, qe, qrow[ar, k]).astype(F32)
+
+    def bn(k):  # sweep-start doc row without the token, + α
+        return ((bb[ar, k] - (k == zo)).astype(F32) + a32).astype(F32)
+    # word move (from zo; proposal = the word's table, built with the token at zo)
+    r0, r1, r2, r3 = philox10(pos, key, U32(sweep), U32(2), seed0, seed1)
+    t = alias_draw(wrows, r0, K)
+    d = (qrow[ar, zo] - qe).astype(F32)
+    zt = ((wsum - d).astype(F32) + ((one - qrow[ar, t]).astype(F32) * g[t]).astype(F32)).astype(F32)
+    num = (aw(t) * wsum).astype(F32)
+    den = (aw(zo) * zt).astype(F32)
+    acc = (t != zo) & ((u01(r1) * den).astype(F32) < num)
+    sc = np.where(acc, t, zo)
+    for c in range(doc_moves):
+        if c:
+            _, _, r2, r3 = philox10(pos, key, U32(sweep), U32(2 + c), seed0, seed1)
+        y = (u01(r2) * tot).astype(F32)
+        pick = y < Ndf
+        pp = y.astype(np.int64)
+        pp = np.where(pp >= s, pp + 1, pp)
+        tz = zslice[ar, np.where(pick, pp, 0)]
+        tu = np.minimum(((y - Ndf).astype(F32) * inv_a).astype(F32).astype(np.int64), K - 1)
+        t = np.where(pick, tz, tu)
+        if drows is not None and multi.any():
+            t = np.where(multi, alias_draw(drows, r2, K), t)
+        qt, qs = qx(t), qx(sc)
+        u = u01(r3)
+        num = np.where(multi, ((aw(t) * qt).astype(F32) * bn(sc)).astype(F32), qt)
+        den = np.where(multi, ((aw(sc) * qs).astype(F32) * bn(t)).astype(F32), qs)
+        ok = (u * den).astype(F32) < num
+        # a multi-chunk doc's table holds the token at zo; from sc ≠ zo a draw of zo stands for
+        # sc with probability 1/(b_zo + α) (a no-op), so zo is proposed with (b_zo^¬ + α)/N
+        sw = multi & (t == zo) & (sc != zo)
+        bz = (bb[ar, zo].astype(F32) + a32).astype(F32)
+        wn = bn(zo)
+        ok_sw = ((u * bz).astype(F32) < wn) & (((u * den).astype(F32) * bz).astype(F32) < (num * wn).astype(F32))
+        ok = np.where(sw, ok_sw, ok) & (t != sc)
+        sc = np.where(ok, t, sc)
+    return sc
+
+
+def gibbs_pass_mh(st: dict, KS: int, K: int, alpha: float, seed0: int, seed1: int, sweep: int,
+                  chunk_len: np.ndarray, doc_moves: int = 1):
+    """One Metropolis-Hastings sweep (k_gibbs_mh), in place; one-lane units (S = 64 chunks a slice).
+
+    Target per token (zo = its topic, counts without it, AD-LDA word side as in :func:`gibbs_pass`):
+        π(k) ∝ (n_dk^¬ + α) · q'_k,   q'_k = q[w, k] (k ≠ zo), q'_zo = fma(q_zo, A_zo, −B_zo).
+    π does not depend on zo, but the sweep's proposal tables do (they count the token at zo). Every
+    move is therefore an MH step with the proposal the tables WOULD give with the token at the
+    current state x -- a kernel reversible w.r.t. π, so their composition leaves π invariant
+    (tests/test_mh_conditional.py). Philox blocks (pos, doc key, sweep, 2 + c) → r0..r3:
+
+    * word move, from zo only (r0 proposes t from the word's alias table ∝ q[w, ·], r1 accepts):
+      ratio (n_t^¬+α)·Z_zo / ((n_zo^¬+α)·Z_t) with Z_zo = Σ_k q[w, k] (the table's sum) and
+      Z_t = (Z_zo − (q_zo − q'_zo)) + (1 − q_t)·g_t, the sum the table would have with the token
+      at t (g_t = 1/(D_t + 1)).
+    * ``doc_moves`` doc moves (r2 proposes, r3 accepts; move c > 0 uses block 2 + c). One-chunk
+      documents propose ∝ n_dk^¬ + α -- with y = u(r2)·(L − 1 + Kα), y < L − 1 picks the current
+      topic of another token of the chunk (position ⌊y⌋, skipping its own), else topic
+      ⌊(y − (L − 1))/α⌋ -- a state-free proposal: ratio q'_t / q'_x. Documents over several chunks
+      propose from the alias table of their sweep-start row b + α: ratio
+      (n_t^¬+α)·q'_t·(b_x^¬+α) / ((n_x^¬+α)·q'_x·(b_t^¬+α)), b^¬ = b without the token; a draw of
+      zo from x ≠ zo is kept with probability (b_zo^¬ + α)/(b_zo + α) first.
+
+    A move is taken when u(r)·den < num (f32). st as for :func:`gibbs_pass` plus ``walias``
+    [V, K] u32, ``wsum`` [V] f32, ``dalias`` [n_long, K] u32, ``mh_g`` [KS] f32 (:func:`mh_tables`)
+    and ``chunk_dslot`` [C] i32 (row of dalias of a multi-chunk doc's chunk, −1 otherwise)."""
+    S = 64
+    slc, lane = _chunk_geometry(st, S)
+    doc = st["chunk_doc"]
+    live = doc >= 0
+    C = doc.shape[0]
+    n = np.zeros((C, KS), dtype=np.int32)
+    n[live] = st["ndk_src"][doc[live]]
+    b = n.copy()
+    n_start = n.copy()
+    multi_c = live & (st["chunk_multi"] != 0)
+    clen = np.where(live, chunk_len, 0).astype(np.int64)
+    if clen.max(initial=0) > MH_MAX_CHUNK:
+        raise ValueError("the MH sampler needs chunks of at most 127 tokens")
+    qfix = st["qfix"]
+    walias, dalias = st["walias"], st["dalias"]
+    dslot = st["chunk_dslot"].astype(np.int64)
+    base = st["slice_off"][slc].astype(np.int64) + lane
+    for s in range(int(clen.max(initial=0))):
+        act = np.nonzero(clen > s)[0]
+        ar = np.arange(act.size)
+        idx = base[act] + s * S
+        w = st["tok_word"][idx].astype(np.int64)
+        zo = st["tok_z"][idx].astype(np.int64)
+        pos = st["chunk_pos0"][act].astype(U32) + U32(s)
+        n[act, zo] -= 1
+        qrow = st["q"][w]
+        qe = excluded_q(qrow[ar, zo], zo, qfix)
+        zp = np.minimum(np.arange(int(clen[act].max()))[None, :], clen[act][:, None] - 1)
+        zslice = st["tok_z"][base[act][:, None] + zp * S].astype(np.int64)
+        zn = mh_moves(n[act], b[act], qrow, zo, qe, multi_c[act], clen[act] - 1, s, zslice,
+                      dalias[np.where(multi_c[act], dslot[act], 0)] if dalias.shape[0] else None, walias[w],
+                      st["wsum"][w], st["mh_g"], pos, st["chunk_key"][act], sweep, seed0, seed1, K, alpha,
+                      doc_moves)
+        n[act, zn] += 1
+        ch = zn != zo
+        st["tok_z"][idx[ch]] = zn[ch].astype(np.uint8)
+        np.add.at(st["dnwk"], (w[ch], zo[ch]), -1)
+        np.add.at(st["dnwk"], (w[ch], zn[ch]), 1)
+    d = n - n_start
+    single = live & ~multi_c
+    st["ndk_dst"][doc[single]] = n[single]
+    np.add.at(st["ndk_dst"], doc[multi_c], d[multi_c])
+    st["dnk"] += d[live].sum(axis=0).astype(np.int32)
+
+
+# ------------------------------------------------------------------------------------------------
 # scoring (K15)
 # ------------------------------------------------------------------------------------------------
 def dot_rows(theta_rows, phi_rows):

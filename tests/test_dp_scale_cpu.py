@@ -88,7 +88,7 @@ def _worker(rank, world, port, job, out_q):
                                       dense_bytes=int(m.dn[0].numel() * 4))
     if rank == 0:
         out_q.put(dict(rows=res.rows, scores=res.scores, loglik=res.stats["loglik"], loads=loads, n_split=n_split,
-                       sweeps=m.sweeps_done, x01=x01))
+                       sweeps=m.sweeps_done, x01=x01, qpf=m.qpf))
     if comm is not None:
         comm.barrier()
         pc.shutdown()
@@ -157,6 +157,16 @@ def test_flow_world8_heavy_ip_bitwise_and_balanced():
     assert eight["n_split"] >= 1
     loads = np.asarray(eight["loads"], np.float64)
     assert loads.max() / loads.mean() < 1.10, loads
+
+
+def test_mh_sampler_world4_heavy_ip_bitwise():
+    """The MH sampler (one-lane units, alias proposals; heavy IP cut across ranks) gives the
+    world-1 chain on 4 gloo ranks."""
+    job = dict(source="flow", n=12000, heavy=0.30, K=40, sweeps=5, env={"ONI_SAMPLER": "mh"})
+    one = _run(1, job)
+    four = _run(4, job)
+    _same(one, four)
+    assert four["n_split"] >= 1 and one["qpf"] == four["qpf"] == 4
 
 
 @pytest.mark.parametrize("source", ["dns", "proxy"])

@@ -1,0 +1,97 @@
+"""k_mh_alias / k_gibbs_mh / k_gibbs_mh_init (csrc/kernels/gibbs_mh.hip) against their NumPy oracle
+(spec.mh_tables, spec.gibbs_pass_mh, spec.gibbs_pass init), bit for bit, in every count mode,
+with one and two doc moves, one-chunk and multi-chunk documents, eager and graph-captured."""
+import numpy as np
+import pytest
+import torch
+
+from oni355 import ops
+from oni355.models.corpus import build_corpus
+from oni355.models.gibbs import GibbsConfig, GibbsLDA
+from oni355.ref import spec
+
+pytestmark = pytest.mark.gpu
+
+
+def _toy(n_docs, V, seed):
+    r = np.random.default_rng(seed)
+    lens = r.zipf(1.6, n_docs).clip(1, 3000)
+    lens[0] = 5000  # a heavy doc: many chunks, several waves
+    tdoc = np.repeat(np.arange(n_docs), lens)
+    tword = (r.zipf(1.3, tdoc.size) - 1) % V
+    keys = ((np.arange(n_docs, dtype=np.int64) * 2654435761 + seed) % (2**31 - 1)).astype(np.int32)
+    return torch.from_numpy(tdoc), torch.from_numpy(tword), keys
+
+
+@pytest.mark.parametrize("K", [7, 40, 100, 255])
+def test_alias_tables_bitwise(gpu, K):
+    r = np.random.default_rng(K)
+    V, KS = 1000, (K + 3) // 4 * 4
+    q = np.zeros((V, KS), np.float32)
+    q[:, :K] = (r.random((V, K)) ** 6 * 0.3 + 1e-6).astype(np.float32)
+    q[3, :K] = 0.01  # a flat row
+    ndk = r.integers(0, 50, (200, KS)).astype(np.int32) * (r.random((200, KS)) < 0.2)
+    ndk[:, K:] = 0
+    rows = np.array([0, 5, 7, 199], np.int32)
+    nk = r.integers(0, 10**6, KS).astype(np.int32)
+    wa, ws, da, g = spec.mh_tables(q, nk, ndk, rows, K, 0.37, 17.5)
+    dev = torch.device(gpu)
+    out = [torch.zeros(V, K, dtype=torch.int32, device=dev), torch.zeros(V, device=dev),
+           torch.zeros(len(rows), K, dtype=torch.int32, device=dev), torch.zeros(KS, device=dev)]
+    ops.mh_tables(torch.from_numpy(q).to(dev), torch.from_numpy(nk).to(dev), torch.from_numpy(ndk).to(dev),
+                  torch.from_numpy(rows).to(dev), K, 0.37, 17.5, *out)
+    assert np.array_equal(out[0].cpu().numpy().view(np.uint32), wa)
+    assert np.array_equal(out[1].cpu().numpy(), ws)
+    assert np.array_equal(out[2].cpu().numpy().view(np.uint32), da)
+    assert np.array_equal(out[3].cpu().numpy(), g)
+
+
+_CASES = [(100, "recount", 1, 64), (100, "wdelta", 1, 64), (100, "atomic", 1, 64), (100, "dual", 1, 64),
+          (100, "delta", 1, 64), (100, "recount", 2, 64), (100, "wdelta", 2, 32), (40, "wdelta", 1, 32),
+          (7, "recount", 1, 64), (255, "wdelta", 2, 64), (64, "dual", 2, 127)]
+
+
+@pytest.mark.parametrize("K,mode,dm,L", _CASES)
+def test_mh_sweep_bitwise_vs_oracle(gpu, K, mode, dm, L, monkeypatch):
+    monkeypatch.setenv("ONI_MH_DOC_MOVES", str(dm))
+    tdoc, tword, keys = _toy(300, 400, K + dm)
+    G, KP = ops.choose_tiling(K, "mh")
+    cc = build_corpus(tdoc, tword, 300, 400, torch.from_numpy(keys), G, L=L)
+    cg = build_corpus(tdoc.to(gpu), tword.to(gpu), 300, 400, torch.from_numpy(keys).to(gpu), G, L=L)
+    assert torch.equal(cc.chunk_doc, cg.chunk_doc.cpu())
+    mc = GibbsLDA(cc, GibbsConfig(K=K, seed=4321, use_graph=False, count_mode="atomic", sampler="mh"))
+    mg = GibbsLDA(cg, GibbsConfig(K=K, seed=4321, use_graph=False, count_mode=mode, sampler="mh"))
+    assert mg.qpf == ops.SAMPLER_MH and mg.mh_doc_moves == dm
+    mc.initialize()
+    mg.initialize()
+    assert torch.equal(mc.tok_z, mg.tok_z.cpu())
+    assert torch.equal(mc.ndk_cur, mg.ndk_cur.cpu())
+    assert torch.equal(mc.nwk, mg.nwk.cpu())
+    for _ in range(3):
+        mc.sweep(1)
+        mg.sweep(1)
+        assert torch.equal(mc.walias, mg.walias.cpu()) and torch.equal(mc.wsum, mg.wsum.cpu())
+        assert torch.equal(mc.dalias, mg.dalias.cpu()) and torch.equal(mc.mh_g, mg.mh_g.cpu())
+        assert torch.equal(mc.tok_z, mg.tok_z.cpu())
+        assert torch.equal(mc.ndk_cur, mg.ndk_cur.cpu())
+        assert torch.equal(mc.nwk, mg.nwk.cpu())
+        assert torch.equal(mc.nk_cur, mg.nk_cur.cpu())
+    T = cg.T
+    assert int(mg.nwk[:, :K].sum()) == T == int(mg.ndk_cur[:, :K].sum()) == int(mg.nk_cur[:K].sum())
+    assert int(mg.nwk.min()) >= 0 and int(mg.ndk_cur.min()) >= 0
+
+
+def test_mh_graph_auto_matches_eager(gpu):
+    """Graph-captured sweeps (the auto count mode's recount → wdelta switch) equal eager ones."""
+    tdoc, tword, keys = _toy(2000, 700, 3)
+    c = build_corpus(tdoc.to(gpu), tword.to(gpu), 2000, 700, torch.from_numpy(keys).to(gpu), 1, L=64)
+    runs = []
+    for graph in (False, True):
+        m = GibbsLDA(c, GibbsConfig(K=100, seed=5, count_mode="auto", auto_switch=5, sampler="mh", use_graph=graph))
+        m.initialize()
+        m.sweep(2)
+        m.sweep(10)
+        runs.append(m)
+    a, b = runs
+    assert b._graph is not None or b._graphs
+    assert torch.equal(a.tok_z, b.tok_z) and torch.equal(a.nwk, b.nwk) and torch.equal(a.ndk_cur, b.ndk_cur)
