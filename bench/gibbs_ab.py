@@ -79,8 +79,10 @@ def main() -> int:
     for name, m in models.items():
         st = {}
         md = m._sweep_mode(m.sweeps_done + 1)
-        for stage in range(4):
+        for stage in range(5):
             if stage == 3 and md != 3:
+                continue
+            if stage == 4 and not m.mh:
                 continue
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
             ts = []
@@ -88,8 +90,12 @@ def main() -> int:
                 ev[0].record()
                 head = m.dn[m.b][: m.V * m.KS].view(m.V, m.KS)
                 if stage == 0:
-                    ops.gibbs_pass(m._state(False), m.G, m.KP, m.K, m.alpha, m.cfg.seed, False, m.sweep_ctr,
+                    st0 = m._state(False)
+                    if m.mh:
+                        st0.update(m.mh_state())
+                    ops.gibbs_pass(st0, m.G, m.KP, m.K, m.alpha, m.cfg.seed, False, m.sweep_ctr,
                                    c.chunk_len, mode=md, sampler=m.qpf, alpha_in_row=m._air,
+                                   mh_doc_moves=getattr(m, "mh_doc_moves", 1),
                                    chg_mask=m.wbits if md == 4 else getattr(m, "chg_mask", None), wpos=c.wpos,
                                    z_w=getattr(m, "z_w", None), zz_w=getattr(m, "zz_w", None))
                 elif stage == 1 and md == 0:
@@ -105,13 +111,15 @@ def main() -> int:
                     ops.STREAM_RECOUNT = not ops.STREAM_RECOUNT
                     ops.recount(c.wsorted, None, m.z_w, head, m.KS)
                     ops.STREAM_RECOUNT = not ops.STREAM_RECOUNT
+                elif stage == 4:
+                    m.mh_build_tables()
                 elif stage == 2:
                     ops.gibbs_apply(m.nwk, m.dn[m.b], m.dn[1 - m.b], m.nk[m.cn], m.nk[1 - m.cn], m.q, m.qfix, m.V, m.K, m.KS,
                                     m.beta, m.vbeta, m.sweep_ctr, bump=False, absolute=md in (0, 3))
                 ev[1].record()
                 torch.cuda.synchronize()
                 ts.append(ev[0].elapsed_time(ev[1]))
-            st[["sample", "recount", "apply", "recount_alt"][stage]] = float(np.median(ts))
+            st[["sample", "recount", "apply", "recount_alt", "mh_tables"][stage]] = float(np.median(ts))
         out[name]["stages_ms"] = st
     print(json.dumps(out), flush=True)
     # chunk-length sweep (the sampler's serial critical path is L steps per lane)

@@ -438,10 +438,13 @@ __global__ __launch_bounds__(64) void k_gibbs_mh(const OniMH m) {
   const int len = a.slice_len[slice];
   x.off = a.slice_off[slice];
   // count cells: n (one-chunk docs, ≤ 127) or the bias (multi-chunk docs); chunk topics
-  for (int k = 0; k < KS; ++k) {
-    int v = 0;
-    if (live) v = x.multi ? kMHBias : x.brow[k];
-    x.L.cnt[k * 64 + lane] = (uint8_t)v;
+  for (int k = 0; k < KS; k += 4) {
+    int4 v = make_int4(0, 0, 0, 0);
+    if (live) v = x.multi ? make_int4(kMHBias, kMHBias, kMHBias, kMHBias) : *reinterpret_cast<const int4*>(x.brow + k);
+    x.L.cnt[k * 64 + lane] = (uint8_t)v.x;
+    x.L.cnt[(k + 1) * 64 + lane] = (uint8_t)v.y;
+    x.L.cnt[(k + 2) * 64 + lane] = (uint8_t)v.z;
+    x.L.cnt[(k + 3) * 64 + lane] = (uint8_t)v.w;
   }
   for (int s = 0; s < len; ++s) x.L.zsl[s * 64 + lane] = s < x.lc ? a.tok_z[x.off + (int64_t)s * 64 + lane] : 0;
   __syncthreads();

@@ -258,6 +258,16 @@ class GibbsLDA:
         self.mh_doc_moves = int(os.environ.get("ONI_MH_DOC_MOVES", "1"))
         self.mh_lmax = max(1, min(int(c.L), spec.MH_MAX_CHUNK))
 
+    def mh_build_tables(self) -> None:
+        """The sweep's MH proposal tables from the snapshot (q and the topic totals nk[cn] the last
+        apply wrote, the sweep-start doc rows ndk[a])."""
+        ops.mh_tables(self.q, self.nk[self.cn], self.ndk[self.a], self.mh_rows, self.K, self.alpha, self.vbeta,
+                      self.walias, self.wsum, self.dalias, self.mh_g)
+
+    def mh_state(self) -> dict:
+        return dict(walias=self.walias, wsum=self.wsum, dalias=self.dalias, mh_g=self.mh_g,
+                    chunk_dslot=self.chunk_dslot, mh_lmax=self.mh_lmax)
+
     def _x01_wanted(self) -> bool:
         """``ONI_X01_PACK``: "1" always packs, "0" never, "auto" (default) packs when the dense Δ
         buffer is at least ``ONI_X01_PACK_MIN_BYTES`` (default 4 MiB). Below that the all-reduce
@@ -468,11 +478,8 @@ class GibbsLDA:
         # every apply -- the previous sweep's, or _prime()'s after init / resume -- seeds that copy
         st = self._state(False)
         if self.mh:
-            # the snapshot's topic totals: the last apply wrote q from nk[cn]
-            ops.mh_tables(self.q, self.nk[self.cn], self.ndk[self.a], self.mh_rows, self.K, self.alpha, self.vbeta,
-                          self.walias, self.wsum, self.dalias, self.mh_g)
-            st.update(walias=self.walias, wsum=self.wsum, dalias=self.dalias, mh_g=self.mh_g,
-                      chunk_dslot=self.chunk_dslot, mh_lmax=self.mh_lmax)
+            self.mh_build_tables()
+            st.update(self.mh_state())
         ops.gibbs_pass(st, self.G, self.KP, self.K, self.alpha, self.cfg.seed, False,
                        self.sweep_ctr, c.chunk_len, host_sweep=self.sweeps_done + 1, mode=mode, sampler=self.qpf,
                        chg_mask=self.wbits if mode == 4 else getattr(self, "chg_mask", None), wpos=c.wpos,
