@@ -28,7 +28,7 @@
 
 struct OniMH {
   OniGibbs g;
-  const uint32_t* walias;      // [V][K] alias entries (thr24 << 8 | alias) of the word proposal
+  const uint4* walias;         // [V][K] word proposal records {thr24 << 8 | alias, q_j, q_alias, Σ q}
   const float* wsum;           // [V] Σ_k q[w, k] (the word table's weight)
   const uint32_t* dalias;      // [n_long][K] alias entries of the multi-chunk docs' n_src + α
   const float* mh_g;           // [KS] 1 / (n_k + Vβ + 1)
@@ -59,14 +59,18 @@ __device__ __forceinline__ int alias_resolve(int j, uint32_t coin, uint32_t e) {
 // multi-chunk docs + α). Sequential f32 per lane, exactly spec.alias_table: sum, scale, classify
 // into the small / large stacks (one u8 array: small grows up from 0, large down from K − 1),
 // pair off, leftovers keep their own index. p and the stack live in LDS, interleaved by lane.
+// Word rows are written as 16-B records {entry, q_j, q_alias(j), Σ_k q_k}: the sampler's one
+// gather of a word proposal then also brings q_t and the row sum (the word move's ratio), so a token
+// costs three scattered loads (record, q[w, zo], q[w, t_doc]) instead of five.
 __global__ __launch_bounds__(64) void k_mh_alias(const float* __restrict__ q, int64_t V, int K, int KS,
                                                   const int32_t* __restrict__ ndk, const int32_t* __restrict__ rows,
-                                                  int64_t n_long, float alpha, uint32_t* __restrict__ walias,
+                                                  int64_t n_long, float alpha, uint4* __restrict__ wrec,
                                                   float* __restrict__ wsum, uint32_t* __restrict__ dalias,
                                                   const int32_t* __restrict__ nk, float vbeta, float* __restrict__ g) {
   extern __shared__ __align__(16) unsigned char smem_alias[];
-  float* p = reinterpret_cast<float*>(smem_alias);           // [K][64]
-  uint8_t* stk = smem_alias + (size_t)K * 64 * sizeof(float);  // [K][64]
+  float* p = reinterpret_cast<float*>(smem_alias);                          // [K][64]
+  uint32_t* ent = reinterpret_cast<uint32_t*>(smem_alias + (size_t)K * 64 * sizeof(float));  // [K][64]
+  uint8_t* stk = smem_alias + (size_t)K * 64 * 2 * sizeof(float);           // [K][64]
   const int lane = threadIdx.x;
   if (blockIdx.x == 0) {
     for (int k = lane; k < KS; k += 64) g[k] = 1.0f / (((float)nk[k] + vbeta) + 1.0f);
@@ -76,7 +80,7 @@ __global__ __launch_bounds__(64) void k_mh_alias(const float* __restrict__ q, in
   const bool word = row < V;
   const float* qr = q + (word ? row : 0) * KS;
   const int32_t* br = ndk + (word ? 0 : (int64_t)rows[row - V]) * KS;
-  uint32_t* out = word ? walias + row * K : dalias + (row - V) * K;
+  uint32_t* dout = dalias + (word ? 0 : (row - V) * K);
   float tot = 0.f;
   for (int k = 0; k < K; ++k) {
     const float w = word ? qr[k] : (float)br[k] + alpha;
@@ -98,7 +102,9 @@ __global__ __launch_bounds__(64) void k_mh_alias(const float* __restrict__ q, in
     const float ps = p[s * 64 + lane];
     uint32_t thr = (uint32_t)(ps * 16777216.0f);
     thr = thr < 0xFFFFFFu ? thr : 0xFFFFFFu;
-    out[s] = (thr << 8) | (uint32_t)l;
+    const uint32_t e = (thr << 8) | (uint32_t)l;
+    if (word) ent[s * 64 + lane] = e;
+    else dout[s] = e;
     const float pl = (p[l * 64 + lane] + ps) - 1.0f;
     p[l * 64 + lane] = pl;
     if (pl < 1.0f) stk[(ns++) * 64 + lane] = (uint8_t)l;
@@ -106,13 +112,22 @@ __global__ __launch_bounds__(64) void k_mh_alias(const float* __restrict__ q, in
   }
   for (int i = 0; i < ns; ++i) {
     const int k = stk[i * 64 + lane];
-    out[k] = 0xFFFFFF00u | (uint32_t)k;
+    if (word) ent[k * 64 + lane] = 0xFFFFFF00u | (uint32_t)k;
+    else dout[k] = 0xFFFFFF00u | (uint32_t)k;
   }
   for (int i = 0; i < nl; ++i) {
     const int k = stk[(K - 1 - i) * 64 + lane];
-    out[k] = 0xFFFFFF00u | (uint32_t)k;
+    if (word) ent[k * 64 + lane] = 0xFFFFFF00u | (uint32_t)k;
+    else dout[k] = 0xFFFFFF00u | (uint32_t)k;
   }
-  if (word) wsum[row] = tot;
+  if (word) {
+    wsum[row] = tot;
+    uint4* out = wrec + row * K;
+    for (int k = 0; k < K; ++k) {
+      const uint32_t e = ent[k * 64 + lane];
+      out[k] = make_uint4(e, __float_as_uint(qr[k]), __float_as_uint(qr[e & 0xFFu]), __float_as_uint(tot));
+    }
+  }
 }
 
 // ---- the sweep -----------------------------------------------------------------------------------
@@ -130,12 +145,19 @@ struct MHB {
   oni::U4 r;     // Philox block (pos, key, sweep, 2)
   int zo;        // sweep-start topic
   float qz;      // q[w, zo]
-  float zw;      // Σ_k q[w, k]
-  uint32_t ew;   // word alias entry at j(r.x)
-  uint32_t ed;   // doc alias entry at j(r.z) (multi-chunk docs)
-  int32_t bzo;   // n_src[doc, zo] (multi-chunk docs)
+  uint4 rw;      // word proposal record at j(r.x): {entry, q_j, q_alias, Σ_k q_k}
+  uint32_t ed;   // doc alias entry at j(r.z) (read for every chunk; used by multi-chunk docs)
+  int32_t bzo;   // n_src[doc, zo]
+  // stage C (issued at the end of the previous step, once that token has moved)
+  int tw, td;    // word / doc proposals
+  float qtd;     // q[w, td]
+  int32_t btw, btd;  // n_src[doc, tw / td] (multi-chunk docs)
 };
 
+// Straight-line step: every lane issues the same loads (padding lanes on word 0, one-chunk docs
+// on one common address for the doc tables) and every decision is a select, so no loaded value is
+// merged at a control-flow join -- a merge there makes the compiler wait for every outstanding
+// memory op (vmcnt(0)), which serialised the token pipeline.
 template <int MODE, int DM>
 struct MHLane {
   const OniMH& m;
@@ -144,189 +166,161 @@ struct MHLane {
   int lane;
   int64_t off;
   int K, KS;
-  int doc;
   bool multi;
-  int dslot;
-  int lc;            // chunk length
+  int lc;               // chunk length
   uint32_t pos0, key, sweep;
   const int32_t* brow;  // n_src row of the doc
+  const uint32_t* drow; // dalias row of the doc (row 0 for one-chunk docs)
   uint32_t wa[2];       // stage A: token words (parity slots)
   int32_t pa[2];        // stage A: word-sorted slots (MODE 3/4)
   MHB b[2];             // stage B (parity slots)
+  int32_t* red;         // LDS: per-topic count deltas of the wave
   int nchg;
   Pend<MODE> pend;
 
   __device__ __forceinline__ MHLane(const OniMH& m_) : m(m_), a(m_.g) {}
 
   __device__ __forceinline__ int cell(int k) const { return (int)L.cnt[k * 64 + lane]; }
-  __device__ __forceinline__ void cell_add(int k, int d) {
-    L.cnt[k * 64 + lane] = (uint8_t)((int)L.cnt[k * 64 + lane] + d);
+  __device__ __forceinline__ void cell_set(int k, int v) { L.cnt[k * 64 + lane] = (uint8_t)v; }
+  // n_dk^¬ + α from a count cell c and the sweep-start count bk
+  __device__ __forceinline__ float aw(int c, int32_t bk) const {
+    return (float)(multi ? bk + c - kMHBias : c) + a.alpha;
   }
-  // n_dk^¬ + α of topic k given its sweep-start count bk (multi-chunk docs)
-  __device__ __forceinline__ float aw(int k, int32_t bk) const {
-    const int v = multi ? bk + cell(k) - kMHBias : cell(k);
-    return (float)v + a.alpha;
+  __device__ __forceinline__ bool alias_keeps(uint32_t r, uint32_t e) const {
+    return ((r * (uint32_t)K) >> 8) < (e >> 8);
+  }
+  __device__ __forceinline__ int alias_draw(uint32_t r, uint32_t e) const {
+    const int j = (int)__umulhi(r, (uint32_t)K);
+    return alias_resolve(j, (r * (uint32_t)K) >> 8, e);
+  }
+  // one-chunk documents: a random other token's current topic, or a uniform topic
+  __device__ __forceinline__ int single_pick(uint32_t r, int s) const {
+    const float nd = (float)(lc - 1);
+    const float y = oni::u01(r) * (nd + m.kalpha);
+    int pp = (int)y;
+    pp += pp >= s ? 1 : 0;
+    pp = pp < lc ? pp : 0;
+    const int tz = (int)L.zsl[pp * 64 + lane];
+    int tu = (int)((y - nd) * m.inv_alpha);
+    tu = tu < K - 1 ? tu : K - 1;
+    return y < nd ? tz : tu;
   }
 
   // stage B of the token at step s (word w): Philox block, then the state-free gathers
   __device__ __forceinline__ void issue_b(int P, int s, uint32_t w) {
     MHB& x = b[P];
-    if (w == oni::kPadWord) return;
+    const uint32_t wc = w == oni::kPadWord ? 0u : w;
     x.r = oni::philox10(oni::U4{pos0 + (uint32_t)s, key, sweep, 2u}, a.seed0, a.seed1);
-    x.zo = (int)L.zsl[s * 64 + lane];
-    const int64_t qrow = (int64_t)w * KS;
-    x.qz = a.q[qrow + x.zo];
-    x.zw = m.wsum[w];
-    int j;
-    uint32_t coin;
-    alias_index(x.r.x, K, j, coin);
-    x.ew = m.walias[(int64_t)w * K + j];
-    if (multi) {
-      alias_index(x.r.z, K, j, coin);
-      x.ed = m.dalias[(int64_t)dslot * K + j];
-      x.bzo = brow[x.zo];
-    }
+    const int z0 = (int)L.zsl[s * 64 + lane];
+    x.zo = z0 < K - 1 ? z0 : K - 1;  // padding slots hold 0; clamp anyway: an LDS index
+    x.qz = a.q[wc * (uint32_t)KS + (uint32_t)x.zo];
+    x.rw = m.walias[wc * (uint32_t)K + __umulhi(x.r.x, (uint32_t)K)];
+    // one-chunk docs read one common address (they use neither value): no scattered lines
+    x.ed = drow[multi ? __umulhi(x.r.z, (uint32_t)K) : 0u];
+    x.bzo = brow[multi ? x.zo : 0];
   }
 
-  // one token: word move, doc move(s), bookkeeping. Loads of later tokens are issued first.
+  // stage C of the token at step s: its proposals (the one-chunk doc proposal reads the chunk's
+  // current topics, so this runs after the previous token has moved) and their gathers
+  __device__ __forceinline__ void issue_c(int P, int s, uint32_t w) {
+    MHB& x = b[P];
+    const uint32_t qo = (w == oni::kPadWord ? 0u : w) * (uint32_t)KS;
+    x.tw = alias_draw(x.r.x, x.rw.x);
+    const int tdm = alias_draw(x.r.z, x.ed);
+    const int tds = single_pick(x.r.z, s);
+    x.td = multi ? tdm : tds;
+    x.qtd = a.q[qo + (uint32_t)x.td];
+    x.btw = brow[multi ? x.tw : 0];
+    x.btd = brow[multi ? x.td : 0];
+  }
+
+  // one token: word move, doc move(s), bookkeeping. The next token's prefetches are issued before
+  // this token's math, its stage C after it (the issue order is the wait order: one in-order vmcnt;
+  // pinned by compiler fences).
   template <int P, bool LOAD_A, bool LOAD_B>
   __device__ __forceinline__ void step(int s) {
     constexpr int NX = 1 - P;
     const int64_t idx = off + (int64_t)s * 64 + lane;
     const uint32_t w = wa[P];
     const int32_t pw = pa[P];
-    const MHB x = b[P];
     const bool act = w != oni::kPadWord;
-    // ---- stage C: the gathers of this token's proposals
-    int tw = 0, td = 0;
-    float qtw = 0.f, qtd = 0.f;
-    int32_t btw = 0, btd = 0;
-    const int64_t qrow = (int64_t)(act ? w : 0u) * KS;
-    if (act) {
-      cell_add(x.zo, -1);  // the token leaves its topic: every count below is n^¬
-      int j;
-      uint32_t coin;
-      alias_index(x.r.x, K, j, coin);
-      tw = alias_resolve(j, coin, x.ew);
-      if (multi) {
-        alias_index(x.r.z, K, j, coin);
-        td = alias_resolve(j, coin, x.ed);
-      } else {
-        const float nd = (float)(lc - 1);
-        const float y = oni::u01(x.r.z) * (nd + m.kalpha);
-        if (y < nd) {
-          int pp = (int)y;
-          pp += pp >= s ? 1 : 0;
-          td = (int)L.zsl[pp * 64 + lane];
-        } else {
-          const int tu = (int)((y - nd) * m.inv_alpha);
-          td = tu < K - 1 ? tu : K - 1;
-        }
-      }
-      qtw = a.q[qrow + tw];
-      qtd = a.q[qrow + td];
-      if (multi) {
-        btw = brow[tw];
-        btd = brow[td];
-      }
-    }
-    // ---- stage B of the next token, stage A of the one after
+    const uint32_t qo = (act ? w : 0u) * (uint32_t)KS;
+    const MHB& x = b[P];
+    const int zo = x.zo;
+    cell_set(zo, cell(zo) - (act ? 1 : 0));  // the token leaves its topic: every count below is n^¬
+    asm volatile("" ::: "memory");
     if constexpr (LOAD_B) issue_b(NX, s + 1, wa[NX]);
+    asm volatile("" ::: "memory");
     if constexpr (LOAD_A) {
       wa[P] = a.tok_word[idx + 128];
       if constexpr (MODE == 3 || MODE == 4) pa[P] = a.wpos[idx + 128];
     } else {
       wa[P] = oni::kPadWord;
     }
+    asm volatile("" ::: "memory");
     pend.flush(a, KS);
-    bool changed = false;
-    if (act) {
-      const int zo = x.zo;
-      const float2 ab = L.qfx[zo];
-      const float qe = fmaf(x.qz, ab.x, -ab.y);
-      // word move (from zo): ratio a_t Z_zo / (a_zo Z_t), Z_t = (Z_zo − (q_zo − q'_zo)) + (1 − q_t) g_t
-      const float azo = aw(zo, x.bzo);
-      const float atw = aw(tw, btw);
-      const float d = x.qz - qe;
-      const float zt = (x.zw - d) + ((1.0f - qtw) * L.gk[tw]);
-      int sc = zo;
-      float qs = qe, as = azo;
-      int32_t bs = x.bzo;
-      {
-        const float num = atw * x.zw;
-        const float den = azo * zt;
-        if (tw != zo && oni::u01(x.r.y) * den < num) {
-          sc = tw;
-          qs = qtw;
-          as = atw;
-          bs = btw;
-        }
-      }
-      // doc moves: one-chunk docs ratio q'_t / q'_s; multi-chunk docs
-      // (a_t q'_t bn_s) / (a_s q'_s bn_t), bn = n_src without the token + α
+    asm volatile("" ::: "memory");
+    const int tw = x.tw, td = x.td;
+    const float qtw = __uint_as_float(alias_keeps(x.r.x, x.rw.x) ? x.rw.y : x.rw.z);
+    const float zw = __uint_as_float(x.rw.w);
+    const float qtd = x.qtd;
+    const int32_t btw = x.btw, btd = x.btd;
+    const float2 ab = L.qfx[zo];
+    const float qe = fmaf(x.qz, ab.x, -ab.y);
+    const float azo = aw(cell(zo), x.bzo);
+    const float atw = aw(cell(tw), btw);
+    const float atd = aw(cell(td), btd);
+    // word move (from zo): ratio a_t Z_zo / (a_zo Z_t), Z_t = (Z_zo − (q_zo − q'_zo)) + (1 − q_t) g_t
+    const float d = x.qz - qe;
+    const float zt = (zw - d) + ((1.0f - qtw) * L.gk[tw]);
+    const bool accw = (tw != zo) & (oni::u01(x.r.y) * (azo * zt) < atw * zw);
+    int sc = accw ? tw : zo;
+    float qs = accw ? qtw : qe;
+    float as = accw ? atw : azo;
+    int32_t bs = accw ? btw : x.bzo;
+    // doc moves: one-chunk docs ratio q'_t / q'_s; multi-chunk docs (a_t q'_t bn_s) / (a_s q'_s bn_t),
+    // bn = n_src without the token + α; from s ≠ zo a draw of zo is a no-op w.p. 1/(b_zo + α)
 #pragma unroll
-      for (int c = 0; c < DM; ++c) {
-        uint32_t r3 = x.r.w;
-        int t = td;
-        float qt = td == zo ? qe : qtd;
-        int32_t bt = btd;
-        if (c > 0) {
-          const oni::U4 r2 = oni::philox10(oni::U4{pos0 + (uint32_t)s, key, sweep, 2u + (uint32_t)c}, a.seed0, a.seed1);
-          r3 = r2.w;
-          if (multi) {
-            int j;
-            uint32_t coin;
-            alias_index(r2.z, K, j, coin);
-            t = alias_resolve(j, coin, m.dalias[(int64_t)dslot * K + j]);
-          } else {
-            const float nd = (float)(lc - 1);
-            const float y = oni::u01(r2.z) * (nd + m.kalpha);
-            if (y < nd) {
-              int pp = (int)y;
-              pp += pp >= s ? 1 : 0;
-              t = (int)L.zsl[pp * 64 + lane];
-            } else {
-              const int tu = (int)((y - nd) * m.inv_alpha);
-              t = tu < K - 1 ? tu : K - 1;
-            }
-          }
-          qt = t == zo ? qe : a.q[qrow + t];
-          if (multi) bt = brow[t];
-        }
-        const float u = oni::u01(r3);
-        bool ok;
-        float at = 0.f;
-        if (multi) {
-          at = aw(t, bt);
-          const float bnt = (float)(bt - (t == zo ? 1 : 0)) + a.alpha;
-          const float bns = (float)(bs - (sc == zo ? 1 : 0)) + a.alpha;
-          const float num = (at * qt) * bns;
-          const float den = (as * qs) * bnt;
-          if (t == zo && sc != zo) {
-            // the table holds the token at zo: from sc ≠ zo a draw of zo is a no-op with
-            // probability 1/(b_zo + α)
-            const float bz = (float)bt + a.alpha;
-            ok = (u * bz < bnt) && ((u * den) * bz < num * bnt);
-          } else {
-            ok = u * den < num;
-          }
-        } else {
-          ok = u * qs < qt;
-        }
-        if (ok && t != sc) {
-          sc = t;
-          qs = qt;
-          as = at;
-          bs = bt;
-        }
+    for (int c = 0; c < DM; ++c) {
+      uint32_t r3 = x.r.w;
+      int t = td;
+      float qt = td == zo ? qe : qtd;
+      int32_t bt = btd;
+      float at = atd;
+      if (c > 0) {
+        const oni::U4 r2 = oni::philox10(oni::U4{pos0 + (uint32_t)s, key, sweep, 2u + (uint32_t)c}, a.seed0, a.seed1);
+        r3 = r2.w;
+        t = multi ? alias_draw(r2.z, drow[multi ? __umulhi(r2.z, (uint32_t)K) : 0u]) : single_pick(r2.z, s);
+        const float qg = a.q[qo + (uint32_t)t];
+        qt = t == zo ? qe : qg;
+        bt = brow[multi ? t : 0];
+        at = aw(cell(t), bt);
       }
-      cell_add(sc, 1);
-      L.zsl[s * 64 + lane] = (uint8_t)sc;
-      changed = sc != zo;
-      if (changed) {
-        ++nchg;
-        pend.note(idx, zo, sc, pw, w);
-      }
+      const float u = oni::u01(r3);
+      const float bnt = (float)(bt - (t == zo ? 1 : 0)) + a.alpha;
+      const float bns = (float)(bs - (sc == zo ? 1 : 0)) + a.alpha;
+      const float num = (at * qt) * bns;
+      const float den = (as * qs) * bnt;
+      const float bz = (float)bt + a.alpha;
+      const bool sw = t == zo && sc != zo;
+      const bool ok_sw = (u * bz < bnt) & ((u * den) * bz < num * bnt);
+      const bool ok_m = sw ? ok_sw : (u * den < num);
+      const bool ok_s = u * qs < qt;
+      const bool ok = (multi ? ok_m : ok_s) & (t != sc);
+      sc = ok ? t : sc;
+      qs = ok ? qt : qs;
+      as = ok ? at : as;
+      bs = ok ? bt : bs;
+    }
+    const bool changed = act & (sc != zo);
+    cell_set(sc, cell(sc) + (act ? 1 : 0));
+    L.zsl[s * 64 + lane] = (uint8_t)sc;
+    nchg += changed ? 1 : 0;
+    pend.note(idx, zo, sc, pw, w);
+    pend.on = changed;
+    if (changed) {
+      atomicAdd(&red[zo], -1);
+      atomicAdd(&red[sc], 1);
     }
     if constexpr (MODE == 2) {
       const uint64_t msk = __ballot(changed);
@@ -335,6 +329,8 @@ struct MHLane {
         pend.mi = (off + (int64_t)s * 64) / 64;
       }
     }
+    asm volatile("" ::: "memory");
+    if constexpr (LOAD_B) issue_c(NX, s + 1, wa[NX]);
   }
 };
 
@@ -349,9 +345,10 @@ __device__ __forceinline__ int run_sum(int v, int c, int next) {
 }
 
 // Epilogue: one-chunk docs store their row; multi-chunk docs add their deltas (summed over the
-// wave's consecutive chunks of the same doc first); the per-topic deltas go to one dnk replica.
+// wave's consecutive chunks of the same doc first). The per-topic deltas were counted in LDS
+// (`red`, one ds_add per move) and go to one dnk replica.
 __device__ __forceinline__ void mh_epilogue(const OniMH& m, const MHLds& L, int KS, int lane, int doc, bool live,
-                                            bool multi, bool init, int32_t* red) {
+                                            bool multi, const int32_t* red) {
   const OniGibbs& a = m.g;
   const int prev_doc = __shfl_up(doc, 1);
   const bool head = lane == 0 || prev_doc != doc;
@@ -360,34 +357,21 @@ __device__ __forceinline__ void mh_epilogue(const OniMH& m, const MHLds& L, int 
   const int next = above ? __ffsll((unsigned long long)above) - 1 : 64;
   const bool any_multi = __ballot(live && multi) != 0ull;
   int32_t* dst = a.ndk_dst + (int64_t)(live ? doc : 0) * KS;
-  const int32_t* src = a.ndk_src + (int64_t)(live ? doc : 0) * KS;
+#pragma unroll 2
   for (int k0 = 0; k0 < KS; k0 += 4) {
-    int d[4];
-    int n[4];
+    int c[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int v = live ? (int)L.cnt[(k0 + i) * 64 + lane] : 0;
-      n[i] = v;
-      d[i] = 0;
-      if (live) d[i] = multi ? v - kMHBias : v;
-    }
-    if (live && !multi) {
-      if (!init) {
-        const int4 o = *reinterpret_cast<const int4*>(src + k0);
-        d[0] -= o.x; d[1] -= o.y; d[2] -= o.z; d[3] -= o.w;
+    for (int i = 0; i < 4; ++i) c[i] = (int)L.cnt[(k0 + i) * 64 + lane];
+    if (live && !multi) *reinterpret_cast<int4*>(dst + k0) = make_int4(c[0], c[1], c[2], c[3]);
+    if (any_multi) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int d = live && multi ? c[i] - kMHBias : 0;
+        if (__ballot(d != 0)) {
+          const int sm = run_sum(d, lane, next);
+          if (live && multi && head && sm) atomicAdd(dst + k0 + i, sm);
+        }
       }
-      *reinterpret_cast<int4*>(dst + k0) = make_int4(n[0], n[1], n[2], n[3]);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (any_multi && __ballot(live && multi && d[i] != 0)) {
-        const int sm = run_sum(live && multi ? d[i] : 0, lane, next);
-        if (live && multi && head && sm) atomicAdd(dst + k0 + i, sm);
-      }
-      int v = d[i];
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) v += __shfl_xor(v, o);
-      if (lane == 0) red[k0 + i] = v;
     }
   }
   __syncthreads();
@@ -395,6 +379,13 @@ __device__ __forceinline__ void mh_epilogue(const OniMH& m, const MHLds& L, int 
     const int v = red[k];
     if (v) atomicAdd(&a.dnk[(int)(blockIdx.x & (unsigned)(a.nk_rep - 1)) * KS + k], v);
   }
+}
+
+// the slice's topics into LDS: the SELL slice is len rows of 64 bytes, exactly the [s][lane] layout
+__device__ __forceinline__ void load_slice_topics(const OniGibbs& a, uint8_t* zsl, int64_t off, int len) {
+  const uint4* src = reinterpret_cast<const uint4*>(a.tok_z + off);
+  uint4* dst = reinterpret_cast<uint4*>(zsl);
+  for (int i = threadIdx.x; i < len * 4; i += 64) dst[i] = src[i];
 }
 
 __device__ __forceinline__ MHLds mh_lds(unsigned char* smem, int KS) {
@@ -414,6 +405,7 @@ __global__ __launch_bounds__(64) void k_gibbs_mh(const OniMH m) {
   MHLane<MODE, DM> x(m);
   x.L = mh_lds(smem_mh, KS);
   int32_t* red = reinterpret_cast<int32_t*>(smem_mh + (size_t)KS * (sizeof(float2) + sizeof(float)));
+  x.red = red;
   const int lane = threadIdx.x;
   x.lane = lane;
   x.K = a.K;
@@ -421,32 +413,36 @@ __global__ __launch_bounds__(64) void k_gibbs_mh(const OniMH m) {
   for (int k = lane; k < KS; k += 64) {
     x.L.qfx[k] = make_float2(a.qfix[k], a.qfix[KS + k]);
     x.L.gk[k] = m.mh_g[k];
+    red[k] = 0;
   }
   const int64_t slice = blockIdx.x;
   const int64_t chunk = slice * 64 + lane;
   const int doc = a.chunk_doc[chunk];
   const bool live = doc >= 0;
-  x.doc = doc;
   x.multi = live && a.chunk_multi[chunk] != 0;
-  x.dslot = x.multi ? m.chunk_dslot[chunk] : 0;
+  x.drow = m.dalias + (int64_t)(x.multi ? m.chunk_dslot[chunk] : 0) * a.K;
   x.lc = live ? m.chunk_len[chunk] : 0;
   x.pos0 = live ? (uint32_t)a.chunk_pos0[chunk] : 0u;
   x.key = live ? a.chunk_key[chunk] : 0u;
   x.sweep = *a.sweep_ctr;
-  x.brow = a.ndk_src + (int64_t)(live ? doc : 0) * KS;
+  const int32_t* own = a.ndk_src + (int64_t)(live ? doc : 0) * KS;
+  // multi-chunk docs read their sweep-start row; one-chunk docs never use it and read one common
+  // address instead (row 0, index 0), so their lanes add no scattered lines to the gathers
+  x.brow = x.multi ? own : a.ndk_src;
   x.nchg = 0;
   const int len = a.slice_len[slice];
   x.off = a.slice_off[slice];
   // count cells: n (one-chunk docs, ≤ 127) or the bias (multi-chunk docs); chunk topics
+  load_slice_topics(a, x.L.zsl, x.off, len);
+#pragma unroll 5
   for (int k = 0; k < KS; k += 4) {
     int4 v = make_int4(0, 0, 0, 0);
-    if (live) v = x.multi ? make_int4(kMHBias, kMHBias, kMHBias, kMHBias) : *reinterpret_cast<const int4*>(x.brow + k);
+    if (live) v = x.multi ? make_int4(kMHBias, kMHBias, kMHBias, kMHBias) : *reinterpret_cast<const int4*>(own + k);
     x.L.cnt[k * 64 + lane] = (uint8_t)v.x;
     x.L.cnt[(k + 1) * 64 + lane] = (uint8_t)v.y;
     x.L.cnt[(k + 2) * 64 + lane] = (uint8_t)v.z;
     x.L.cnt[(k + 3) * 64 + lane] = (uint8_t)v.w;
   }
-  for (int s = 0; s < len; ++s) x.L.zsl[s * 64 + lane] = s < x.lc ? a.tok_z[x.off + (int64_t)s * 64 + lane] : 0;
   __syncthreads();
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -454,6 +450,7 @@ __global__ __launch_bounds__(64) void k_gibbs_mh(const OniMH m) {
     x.pa[t] = ((MODE == 3 || MODE == 4) && len > t) ? a.wpos[x.off + t * 64 + lane] : 0;
   }
   x.issue_b(0, 0, x.wa[0]);
+  x.issue_c(0, 0, x.wa[0]);
   int s = 0;
   for (; s + 3 < len; s += 2) {
     x.template step<0, true, true>(s);
@@ -469,7 +466,7 @@ __global__ __launch_bounds__(64) void k_gibbs_mh(const OniMH m) {
   x.pend.flush(a, KS);
   if (a.chg_count) add_wave_count(a.chg_count, x.nchg);
   __syncthreads();
-  mh_epilogue(m, x.L, KS, lane, doc, live, x.multi, false, red);
+  mh_epilogue(m, x.L, KS, lane, doc, live, x.multi, red);
 }
 
 // init pass (one-lane units, any K): z = ⌊r·K / 2^32⌋ with r the generic init's draw (stream 0,
@@ -491,6 +488,7 @@ __global__ __launch_bounds__(64) void k_gibbs_mh_init(const OniMH m) {
   const uint32_t key = live ? a.chunk_key[chunk] : 0u;
   const int64_t off = a.slice_off[slice];
   for (int k = 0; k < KS; ++k) L.cnt[k * 64 + lane] = (uint8_t)(live && multi ? kMHBias : 0);
+  for (int k = lane; k < KS; k += 64) red[k] = 0;
   __syncthreads();
   for (int s = 0; s < lc; ++s) {
     const uint32_t pos = pos0 + (uint32_t)s;
@@ -498,10 +496,11 @@ __global__ __launch_bounds__(64) void k_gibbs_mh_init(const OniMH m) {
     const uint32_t rr = oni::pick4(r, pos & 3u);
     const int z = (int)(((uint64_t)rr * (uint32_t)a.K) >> 32);
     L.cnt[z * 64 + lane] = (uint8_t)((int)L.cnt[z * 64 + lane] + 1);
+    atomicAdd(&red[z], 1);
     a.tok_z[off + (int64_t)s * 64 + lane] = (uint8_t)z;
   }
   __syncthreads();
-  mh_epilogue(m, L, KS, lane, doc, live, multi, true, red);
+  mh_epilogue(m, L, KS, lane, doc, live, multi, red);
 }
 
 }  // namespace
@@ -511,12 +510,12 @@ static size_t mh_lds_bytes(int KS, int lmax) {
 }
 
 ONI_API int oni_mh_tables(const float* q, int64_t V, int K, int KS, const int32_t* ndk, const int32_t* rows,
-                          int64_t n_long, float alpha, uint32_t* walias, float* wsum, uint32_t* dalias,
+                          int64_t n_long, float alpha, uint4* walias, float* wsum, uint32_t* dalias,
                           const int32_t* nk, float vbeta, float* g, hipStream_t s) {
   if (K < 1 || K > 255 || K > KS || KS % 4 || V < 0 || n_long < 0) return (int)hipErrorInvalidValue;
   const int64_t nrows = V + n_long;
   const unsigned grid = (unsigned)((nrows + 63) / 64 > 0 ? (nrows + 63) / 64 : 1);
-  const size_t lds = (size_t)K * 64 * (sizeof(float) + 1);
+  const size_t lds = (size_t)K * 64 * (2 * sizeof(float) + 1);
   k_mh_alias<<<grid, 64, lds, s>>>(q, V, K, KS, ndk, rows, n_long, alpha, walias, wsum, dalias, nk, vbeta, g);
   return (int)hipGetLastError();
 }

@@ -251,7 +251,7 @@ class GibbsLDA:
         if rows.numel():
             dslot[multi] = torch.searchsorted(rows, c.chunk_doc[multi].to(torch.int64)).to(torch.int32)
         self.chunk_dslot = dslot
-        self.walias = torch.zeros(self.V, self.K, dtype=torch.int32, device=dev)
+        self.walias = torch.zeros(self.V, self.K, 4, dtype=torch.int32, device=dev)  # 16-B records
         self.wsum = torch.zeros(self.V, dtype=torch.float32, device=dev)
         self.dalias = torch.zeros(max(int(rows.numel()), 1), self.K, dtype=torch.int32, device=dev)
         self.mh_g = torch.zeros(self.KS, dtype=torch.float32, device=dev)

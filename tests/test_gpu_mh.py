@@ -36,7 +36,7 @@ def test_alias_tables_bitwise(gpu, K):
     nk = r.integers(0, 10**6, KS).astype(np.int32)
     wa, ws, da, g = spec.mh_tables(q, nk, ndk, rows, K, 0.37, 17.5)
     dev = torch.device(gpu)
-    out = [torch.zeros(V, K, dtype=torch.int32, device=dev), torch.zeros(V, device=dev),
+    out = [torch.zeros(V, K, 4, dtype=torch.int32, device=dev), torch.zeros(V, device=dev),
            torch.zeros(len(rows), K, dtype=torch.int32, device=dev), torch.zeros(KS, device=dev)]
     ops.mh_tables(torch.from_numpy(q).to(dev), torch.from_numpy(nk).to(dev), torch.from_numpy(ndk).to(dev),
                   torch.from_numpy(rows).to(dev), K, 0.37, 17.5, *out)
