@@ -43,6 +43,7 @@ struct OniMH {
 namespace {
 
 constexpr int kMHBias = 128;
+constexpr int kAS = 65;  // k_mh_alias LDS row stride (dwords)
 
 // j = ⌊r·K / 2^32⌋ and the coin (top 24 bits of the low word) of an alias draw
 __device__ __forceinline__ void alias_index(uint32_t r, int K, int& j, uint32_t& coin) {
@@ -58,7 +59,9 @@ __device__ __forceinline__ int alias_resolve(int j, uint32_t coin, uint32_t e) {
 // One lane per row (rows [0, V): word rows of q; rows [V, V + n_long): sweep-start rows of the
 // multi-chunk docs + α). Sequential f32 per lane, exactly spec.alias_table: sum, scale, classify
 // into the small / large stacks (one u8 array: small grows up from 0, large down from K − 1),
-// pair off, leftovers keep their own index. p and the stack live in LDS, interleaved by lane.
+// pair off, leftovers keep their own index. The rows are read and written cooperatively (the wave
+// walks its 64 rows, lanes along k: coalesced), p / entries / stack live in LDS transposed to
+// [k][row] for the per-lane sequential part.
 // Word rows are written as 16-B records {entry, q_j, q_alias(j), Σ_k q_k}: the sampler's one
 // gather of a word proposal then also brings q_t and the row sum (the word move's ratio), so a token
 // costs three scattered loads (record, q[w, zo], q[w, t_doc]) instead of five.
@@ -68,64 +71,96 @@ __global__ __launch_bounds__(64) void k_mh_alias(const float* __restrict__ q, in
                                                   float* __restrict__ wsum, uint32_t* __restrict__ dalias,
                                                   const int32_t* __restrict__ nk, float vbeta, float* __restrict__ g) {
   extern __shared__ __align__(16) unsigned char smem_alias[];
-  float* p = reinterpret_cast<float*>(smem_alias);                          // [K][64]
-  uint32_t* ent = reinterpret_cast<uint32_t*>(smem_alias + (size_t)K * 64 * sizeof(float));  // [K][64]
-  uint8_t* stk = smem_alias + (size_t)K * 64 * 2 * sizeof(float);           // [K][64]
+  // p and the entries are [K][65] (a padded row: the cooperative passes walk k across lanes)
+  float* p = reinterpret_cast<float*>(smem_alias);
+  uint32_t* ent = reinterpret_cast<uint32_t*>(smem_alias + (size_t)K * kAS * sizeof(float));
+  float* tots = reinterpret_cast<float*>(smem_alias + (size_t)K * kAS * 2 * sizeof(float));   // [64]
+  uint8_t* stk = smem_alias + (size_t)K * kAS * 2 * sizeof(float) + 64 * sizeof(float);      // [K][64]
   const int lane = threadIdx.x;
   if (blockIdx.x == 0) {
     for (int k = lane; k < KS; k += 64) g[k] = 1.0f / (((float)nk[k] + vbeta) + 1.0f);
   }
-  const int64_t row = (int64_t)blockIdx.x * 64 + lane;
-  if (row >= V + n_long) return;
-  const bool word = row < V;
+  const int64_t r0 = (int64_t)blockIdx.x * 64;
+  const int nrows = (int)((V + n_long - r0) < 64 ? (V + n_long - r0) : 64);
+  // each lane loads its own row (16-B vectors; K rows of q are KS-strided, KS % 4 == 0)
+  const int64_t row = r0 + lane;
+  const bool has = lane < nrows;
+  const bool word = has && row < V;
   const float* qr = q + (word ? row : 0) * KS;
-  const int32_t* br = ndk + (word ? 0 : (int64_t)rows[row - V]) * KS;
-  uint32_t* dout = dalias + (word ? 0 : (row - V) * K);
-  float tot = 0.f;
-  for (int k = 0; k < K; ++k) {
-    const float w = word ? qr[k] : (float)br[k] + alpha;
-    p[k * 64 + lane] = w;
-    tot = tot + w;
+  const int32_t* br = ndk + (has && !word ? (int64_t)rows[row - V] : 0) * KS;
+  if (has) {
+#pragma unroll 4
+    for (int k = 0; k < K; k += 4) {
+      float4 v;
+      if (word) {
+        v = *reinterpret_cast<const float4*>(qr + k);
+      } else {
+        const int4 c = *reinterpret_cast<const int4*>(br + k);
+        v = make_float4((float)c.x + alpha, (float)c.y + alpha, (float)c.z + alpha, (float)c.w + alpha);
+      }
+      p[k * kAS + lane] = v.x;
+      if (k + 1 < K) p[(k + 1) * kAS + lane] = v.y;
+      if (k + 2 < K) p[(k + 2) * kAS + lane] = v.z;
+      if (k + 3 < K) p[(k + 3) * kAS + lane] = v.w;
+    }
   }
-  const float scale = (float)K / tot;
-  int ns = 0, nl = 0;
-  for (int k = 0; k < K; ++k) {
-    const float v = p[k * 64 + lane] * scale;
-    p[k * 64 + lane] = v;
-    if (v < 1.0f) stk[(ns++) * 64 + lane] = (uint8_t)k;
-    else stk[(K - 1 - nl++) * 64 + lane] = (uint8_t)k;
-  }
-  while (ns > 0 && nl > 0) {
-    const int s = stk[(--ns) * 64 + lane];
-    const int l = stk[(K - nl) * 64 + lane];
-    --nl;
-    const float ps = p[s * 64 + lane];
-    uint32_t thr = (uint32_t)(ps * 16777216.0f);
-    thr = thr < 0xFFFFFFu ? thr : 0xFFFFFFu;
-    const uint32_t e = (thr << 8) | (uint32_t)l;
-    if (word) ent[s * 64 + lane] = e;
-    else dout[s] = e;
-    const float pl = (p[l * 64 + lane] + ps) - 1.0f;
-    p[l * 64 + lane] = pl;
-    if (pl < 1.0f) stk[(ns++) * 64 + lane] = (uint8_t)l;
-    else stk[(K - 1 - nl++) * 64 + lane] = (uint8_t)l;
-  }
-  for (int i = 0; i < ns; ++i) {
-    const int k = stk[i * 64 + lane];
-    if (word) ent[k * 64 + lane] = 0xFFFFFF00u | (uint32_t)k;
-    else dout[k] = 0xFFFFFF00u | (uint32_t)k;
-  }
-  for (int i = 0; i < nl; ++i) {
-    const int k = stk[(K - 1 - i) * 64 + lane];
-    if (word) ent[k * 64 + lane] = 0xFFFFFF00u | (uint32_t)k;
-    else dout[k] = 0xFFFFFF00u | (uint32_t)k;
-  }
-  if (word) {
-    wsum[row] = tot;
-    uint4* out = wrec + row * K;
+  __syncthreads();
+  if (lane < nrows) {
+    float tot = 0.f;
+    for (int k = 0; k < K; ++k) tot = tot + p[k * kAS + lane];
+    tots[lane] = tot;
+    const float scale = (float)K / tot;
+    int ns = 0, nl = 0;
     for (int k = 0; k < K; ++k) {
-      const uint32_t e = ent[k * 64 + lane];
-      out[k] = make_uint4(e, __float_as_uint(qr[k]), __float_as_uint(qr[e & 0xFFu]), __float_as_uint(tot));
+      const float v = p[k * kAS + lane] * scale;
+      p[k * kAS + lane] = v;
+      ent[k * kAS + lane] = 0xFFFFFF00u | (uint32_t)k;  // leftovers keep their own index
+      if (v < 1.0f) stk[(ns++) * 64 + lane] = (uint8_t)k;
+      else stk[(K - 1 - nl++) * 64 + lane] = (uint8_t)k;
+    }
+    // Vose pairing. The large index l of a pair is pushed back and popped again by the very next
+    // pair (onto the small stack if its weight fell below 1, else onto the large one), so it is
+    // carried in registers with its weight: one stack read and one weight read per pair.
+    if (ns > 0 && nl > 0) {
+      int s = stk[(--ns) * 64 + lane];
+      float ps = p[s * kAS + lane];
+      int l = stk[(K - nl) * 64 + lane];
+      --nl;
+      float pl = p[l * kAS + lane];
+      // branch-free: lanes pair at their own pace without splitting the wave's paths
+      for (;;) {
+        uint32_t thr = (uint32_t)(ps * 16777216.0f);
+        thr = thr < 0xFFFFFFu ? thr : 0xFFFFFFu;
+        ent[s * kAS + lane] = (thr << 8) | (uint32_t)l;
+        const float rest = (pl + ps) - 1.0f;
+        const bool small = rest < 1.0f;  // l joins the small stack: pair it with a new large
+        if (small ? nl == 0 : ns == 0) break;
+        const int at = small ? K - nl : ns - 1;
+        nl -= small ? 1 : 0;
+        ns -= small ? 0 : 1;
+        const int x = stk[at * 64 + lane];
+        const float px = p[x * kAS + lane];
+        s = small ? l : x;
+        ps = small ? rest : px;
+        l = small ? x : l;
+        pl = small ? px : rest;
+      }
+    }
+  }
+  if (has) {
+    if (word) {
+      const uint32_t tb = __float_as_uint(tots[lane]);
+      uint4* out = wrec + row * K;
+#pragma unroll 4
+      for (int k = 0; k < K; ++k) {
+        const uint32_t e = ent[k * kAS + lane];
+        out[k] = make_uint4(e, __float_as_uint(qr[k]), __float_as_uint(qr[e & 0xFFu]), tb);
+      }
+      wsum[row] = tots[lane];
+    } else {
+      uint32_t* out = dalias + (row - V) * K;
+#pragma unroll 4
+      for (int k = 0; k < K; ++k) out[k] = ent[k * kAS + lane];
     }
   }
 }
@@ -152,6 +187,11 @@ struct MHB {
   int tw, td;    // word / doc proposals
   float qtd;     // q[w, td]
   int32_t btw, btd;  // n_src[doc, tw / td] (multi-chunk docs)
+  // second doc move (DM = 2): Philox block (pos, key, sweep, 3) words z / w, its proposal and gathers
+  uint32_t r2z, r2w, ed2;
+  int td2;
+  float qtd2;
+  int32_t btd2;
 };
 
 // Straight-line step: every lane issues the same loads (padding lanes on word 0, one-chunk docs
@@ -218,6 +258,12 @@ struct MHLane {
     // one-chunk docs read one common address (they use neither value): no scattered lines
     x.ed = drow[multi ? __umulhi(x.r.z, (uint32_t)K) : 0u];
     x.bzo = brow[multi ? x.zo : 0];
+    if constexpr (DM > 1) {
+      const oni::U4 r2 = oni::philox10(oni::U4{pos0 + (uint32_t)s, key, sweep, 3u}, a.seed0, a.seed1);
+      x.r2z = r2.z;
+      x.r2w = r2.w;
+      x.ed2 = drow[multi ? __umulhi(r2.z, (uint32_t)K) : 0u];
+    }
   }
 
   // stage C of the token at step s: its proposals (the one-chunk doc proposal reads the chunk's
@@ -232,6 +278,15 @@ struct MHLane {
     x.qtd = a.q[qo + (uint32_t)x.td];
     x.btw = brow[multi ? x.tw : 0];
     x.btd = brow[multi ? x.td : 0];
+    if constexpr (DM > 1) {
+      // the second doc move's proposal is state-free too (the chunk's other topics do not move
+      // while this token does): prefetched with the first
+      const int t2m = alias_draw(x.r2z, x.ed2);
+      const int t2s = single_pick(x.r2z, s);
+      x.td2 = multi ? t2m : t2s;
+      x.qtd2 = a.q[qo + (uint32_t)x.td2];
+      x.btd2 = brow[multi ? x.td2 : 0];
+    }
   }
 
   // one token: word move, doc move(s), bookkeeping. The next token's prefetches are issued before
@@ -244,7 +299,6 @@ struct MHLane {
     const uint32_t w = wa[P];
     const int32_t pw = pa[P];
     const bool act = w != oni::kPadWord;
-    const uint32_t qo = (act ? w : 0u) * (uint32_t)KS;
     const MHB& x = b[P];
     const int zo = x.zo;
     cell_set(zo, cell(zo) - (act ? 1 : 0));  // the token leaves its topic: every count below is n^¬
@@ -287,14 +341,14 @@ struct MHLane {
       float qt = td == zo ? qe : qtd;
       int32_t bt = btd;
       float at = atd;
-      if (c > 0) {
-        const oni::U4 r2 = oni::philox10(oni::U4{pos0 + (uint32_t)s, key, sweep, 2u + (uint32_t)c}, a.seed0, a.seed1);
-        r3 = r2.w;
-        t = multi ? alias_draw(r2.z, drow[multi ? __umulhi(r2.z, (uint32_t)K) : 0u]) : single_pick(r2.z, s);
-        const float qg = a.q[qo + (uint32_t)t];
-        qt = t == zo ? qe : qg;
-        bt = brow[multi ? t : 0];
-        at = aw(cell(t), bt);
+      if constexpr (DM > 1) {
+        if (c > 0) {
+          r3 = x.r2w;
+          t = x.td2;
+          qt = t == zo ? qe : x.qtd2;
+          bt = x.btd2;
+          at = aw(cell(t), bt);
+        }
       }
       const float u = oni::u01(r3);
       const float bnt = (float)(bt - (t == zo ? 1 : 0)) + a.alpha;
@@ -515,7 +569,7 @@ ONI_API int oni_mh_tables(const float* q, int64_t V, int K, int KS, const int32_
   if (K < 1 || K > 255 || K > KS || KS % 4 || V < 0 || n_long < 0) return (int)hipErrorInvalidValue;
   const int64_t nrows = V + n_long;
   const unsigned grid = (unsigned)((nrows + 63) / 64 > 0 ? (nrows + 63) / 64 : 1);
-  const size_t lds = (size_t)K * 64 * (2 * sizeof(float) + 1);
+  const size_t lds = (size_t)K * kAS * 2 * sizeof(float) + 64 * sizeof(float) + (size_t)K * 64;
   k_mh_alias<<<grid, 64, lds, s>>>(q, V, K, KS, ndk, rows, n_long, alpha, walias, wsum, dalias, nk, vbeta, g);
   return (int)hipGetLastError();
 }

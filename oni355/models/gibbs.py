@@ -255,7 +255,11 @@ class GibbsLDA:
         self.wsum = torch.zeros(self.V, dtype=torch.float32, device=dev)
         self.dalias = torch.zeros(max(int(rows.numel()), 1), self.K, dtype=torch.int32, device=dev)
         self.mh_g = torch.zeros(self.KS, dtype=torch.float32, device=dev)
-        self.mh_doc_moves = int(os.environ.get("ONI_MH_DOC_MOVES", "1"))
+        # one word move + two doc moves per token: with one doc move the chain plateaus 2.6 % lower
+        # in log-likelihood on the 12.5M-flow day (rare words' word tables mostly propose the
+        # token's own topic); two match the dense chain at the same chunk length
+        # (profiles/r4/mh_quality_gpu_*.json)
+        self.mh_doc_moves = int(os.environ.get("ONI_MH_DOC_MOVES", "2"))
         self.mh_lmax = max(1, min(int(c.L), spec.MH_MAX_CHUNK))
 
     def mh_build_tables(self) -> None:

@@ -16,6 +16,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from ..ref import spec
 from ..utils.obs import StageTimer, traced
 from ..models.corpus import Corpus, auto_chunk_len, build_corpus
 from ..models.gibbs import GibbsConfig, GibbsLDA
@@ -493,8 +494,8 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
             T_glob = float(weights.sum()) if use_w else float(doc_keys64.numel())
             if dist_on:
                 T_glob = comm.allreduce_scalar(T_glob, "sum")
-            # the MH sampler's u8 LDS cells hold a chunk's count deltas: chunks ≤ 64 tokens
-            chunk_len = auto_chunk_len(int(T_glob), G, hi=64 if mh else 128)
+            # the MH sampler's u8 LDS cells hold a chunk's count deltas: chunks ≤ 127 tokens
+            chunk_len = auto_chunk_len(int(T_glob), G, hi=spec.MH_MAX_CHUNK if mh else 128)
         udoc, inv, wi, wt, route = route_to_owners(doc_keys64, word_ids, weights, comm,
                                                    split_L=chunk_len if dist_on else 0)
         D, V = int(udoc.numel()), int(vocab.numel())
