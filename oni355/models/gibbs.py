@@ -35,10 +35,19 @@ X01_PACK_MIN_BYTES = 4 << 20
 SAMPLERS = {"generic": 0, "lds": 2, "x1": 3, "mh": ops.SAMPLER_MH}
 
 
+# "auto" runs the MH sampler above this many topics: at K = 100 its sweep is 0.84 vs 1.02 ms on the
+# 12.5M-flow day and 3.2 vs 6.6 ms on the config-5 flow model, at equal chain quality
+# (profiles/r4/mh_*); the dense samplers below
+MH_AUTO_MIN_K = 65
+
+
 def sampler_for(K: int, sampler: str | None = None) -> str:
-    """The sweep kernel a K-topic model runs (``sampler`` or ONI_SAMPLER, default "auto"); the
-    corpus must be built for its tiling (ops.choose_tiling(K, "mh") for the MH sampler)."""
+    """The sweep kernel family a K-topic model runs: ``sampler`` or ONI_SAMPLER (default "auto");
+    "auto" resolves to "mh" for K ≥ MH_AUTO_MIN_K and to "dense" (k_gibbs_x1 / k_gibbs_ldsg) below.
+    The corpus must be built for its tiling (:func:`tiling_for`)."""
     s = sampler if sampler is not None else os.environ.get("ONI_SAMPLER", "auto")
+    if s == "auto":
+        return "mh" if K >= MH_AUTO_MIN_K else "dense"
     return s
 
 
@@ -74,10 +83,12 @@ class GibbsConfig:
     check_invariants: bool = field(default_factory=lambda: os.environ.get("ONI_CHECK_INVARIANTS", "0") == "1")
     # cheap numerical health check after every sweep() call (ONI_HEALTH_CHECK=0 disables)
     health_check: bool = field(default_factory=lambda: os.environ.get("ONI_HEALTH_CHECK", "1") != "0")
-    # sweep kernel: "auto" (default: "x1" for K ≤ 32, "lds" above), "x1" the one-lane register
-    # sampler k_gibbs_x1, "lds" the multi-lane LDS-count sampler k_gibbs_ldsg, "generic" k_gibbs
-    # (any unit width; the fallback when n + α is not exact in f32). ONI_SAMPLER overrides the
-    # default. All are bitwise identical to each other and to the NumPy oracle (spec.gibbs_pass).
+    # sweep kernel: "auto" (default: "mh" for K ≥ MH_AUTO_MIN_K, else "dense"), "dense" ("x1" for
+    # K ≤ 32, "lds" above), "x1" the one-lane register sampler k_gibbs_x1, "lds" the multi-lane
+    # LDS-count sampler k_gibbs_ldsg, "generic" k_gibbs (any unit width; the fallback when n + α is
+    # not exact in f32) -- these are bitwise identical to each other and to spec.gibbs_pass --
+    # and "mh" the Metropolis-Hastings sampler k_gibbs_mh (its own chain, spec.gibbs_pass_mh).
+    # ONI_SAMPLER overrides the default.
     sampler: str = field(default_factory=lambda: os.environ.get("ONI_SAMPLER", "auto"))
     # posterior averaging: θ and φ are estimated from the counts of the last ``post_samples``
     # samples taken every ``post_every`` sweeps (ending at the last sweep) instead of the final
@@ -196,16 +207,17 @@ class GibbsLDA:
         if self.mode == 2:
             self.tok_zprev = torch.zeros_like(self.tok_z)
             self.chg_mask = torch.zeros(max(corpus.sell_slots // corpus.S, 1), dtype=torch.int64, device=dev)
-        if cfg.sampler not in SAMPLERS and cfg.sampler != "auto":
+        if cfg.sampler not in SAMPLERS and cfg.sampler not in ("auto", "dense"):
             raise ValueError(f"unknown sampler {cfg.sampler}")
-        self.mh = cfg.sampler == "mh"
-        if cfg.sampler == "auto":
+        samp = sampler_for(cfg.K, cfg.sampler)
+        self.mh = samp == "mh"
+        if samp == "dense":
             self.qpf = SAMPLERS["x1"] if self.G == 1 else SAMPLERS["lds"]
         elif self.mh:
             self.qpf = SAMPLERS["mh"]
             self._setup_mh()
         else:
-            self.qpf = SAMPLERS[cfg.sampler]
+            self.qpf = SAMPLERS[samp]
             if (self.qpf == SAMPLERS["x1"]) != (self.G == 1) and self.qpf != SAMPLERS["generic"]:
                 raise ValueError(f"sampler {cfg.sampler} does not run {self.G}-lane units (K = {cfg.K})")
         # the specialised kernels keep n + α as f32 in their count rows: exact only when every

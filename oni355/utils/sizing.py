@@ -25,8 +25,8 @@ TOKENS_PER_EVENT = {"flow": 2, "dns": 1, "proxy": 1}
 
 
 def ks_of(K: int) -> int:
-    from ..ops import choose_tiling
-    G, KP = choose_tiling(K)
+    from ..models.gibbs import tiling_for
+    G, KP = tiling_for(K)
     return G * KP
 
 

@@ -127,7 +127,8 @@ def test_stay_rates_match_textbook_collapsed_gibbs():
     K, alpha, beta = 20, 2.5, 0.01
     keys = torch.arange(D, dtype=torch.int32) * 13 + 5
     c = build_corpus(torch.from_numpy(tdoc), torch.from_numpy(tword), D, V, keys, 1, L=128)
-    m = GibbsLDA(c, GibbsConfig(K=K, alpha=alpha, beta=beta, seed=9, count_mode="atomic", post_samples=1))
+    m = GibbsLDA(c, GibbsConfig(K=K, alpha=alpha, beta=beta, seed=9, count_mode="atomic", post_samples=1,
+                                sampler="dense"))
     m.initialize()
     cdoc, cword = (t.numpy() for t in canonical_tokens(c))
     wc = np.bincount(cword, minlength=V)

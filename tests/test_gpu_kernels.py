@@ -97,12 +97,12 @@ def test_gibbs_bitwise_vs_oracle(gpu, K, mode):
     cg = build_corpus(tdoc.to(gpu), tword.to(gpu), 300, 400, torch.from_numpy(keys).to(gpu), G, L=64)
     assert torch.equal(cc.tok_word, cg.tok_word.cpu())
     assert torch.equal(cc.chunk_doc, cg.chunk_doc.cpu())
-    sampler = mode.split("+")[1] if "+" in mode else "auto"
+    sampler = mode.split("+")[1] if "+" in mode else "dense"
     mg = GibbsLDA(cg, GibbsConfig(K=K, seed=1234, use_graph=False, count_mode=mode.split("+")[0], sampler=sampler))
     exact = K not in (7, 12)  # α = 50/K exact in f32 (and below 2^24 documents) selects the fast kernels
-    if sampler == "auto":
+    if sampler == "dense":
         assert mg.qpf == ((3 if G == 1 else 2) if exact else 0), (K, mg.qpf)
-    mc = GibbsLDA(cc, GibbsConfig(K=K, seed=1234, use_graph=False, count_mode="atomic"))
+    mc = GibbsLDA(cc, GibbsConfig(K=K, seed=1234, use_graph=False, count_mode="atomic", sampler="dense"))
     if mode.startswith("wdelta"):
         assert mg.mode == 4
     mc.initialize()

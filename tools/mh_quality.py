@@ -35,7 +35,7 @@ def chain(a, sampler: str, cycles: int):
     udoc, inv = torch.unique(dk, return_inverse=True)
     wi = torch.searchsorted(vocab, wk).to(torch.int32)
     G, _ = tiling_for(a.topics, sampler)
-    L = a.chunk_len or auto_chunk_len(int(dk.numel()), G, hi=64 if sampler == "mh" else 128)
+    L = a.chunk_len or auto_chunk_len(int(dk.numel()), G, hi=127 if sampler == "mh" else 128)
     c = build_corpus(inv.to(torch.int32), wi, int(udoc.numel()), int(vocab.numel()), common.i64_to_u32bits(udoc), G, L)
     m = GibbsLDA(c, GibbsConfig(K=a.topics, sampler=sampler, post_samples=1, use_graph=a.device != "cpu"))
     m.initialize()
@@ -64,7 +64,7 @@ def main() -> int:
     ap.add_argument("--wide", action="store_true")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
-    res = {"flows": a.flows, "topics": a.topics, "gibbs": chain(a, "auto", 1)}
+    res = {"flows": a.flows, "topics": a.topics, "gibbs": chain(a, "dense", 1)}
     for cy in [int(x) for x in a.doc_moves.split(",") if x]:
         res[f"mh{cy}"] = chain(a, "mh", cy)
     g = res["gibbs"]["traj"][-1][1]
