@@ -546,8 +546,13 @@ __global__ __launch_bounds__(64) void k_gibbs_mh_init(const OniMH m) {
   __syncthreads();
   for (int s = 0; s < lc; ++s) {
     const uint32_t pos = pos0 + (uint32_t)s;
-    const oni::U4 r = oni::philox10(oni::U4{pos >> 2, key, 0u, 0u}, a.seed0, a.seed1);
-    const uint32_t rr = oni::pick4(r, pos & 3u);
+    uint32_t rr;
+    if (a.flags & 8) {
+      rr = oni::mix32(a.tok_word[off + (int64_t)s * 64 + lane]);
+    } else {
+      const oni::U4 r = oni::philox10(oni::U4{pos >> 2, key, 0u, 0u}, a.seed0, a.seed1);
+      rr = oni::pick4(r, pos & 3u);
+    }
     const int z = (int)(((uint64_t)rr * (uint32_t)a.K) >> 32);
     L.cnt[z * 64 + lane] = (uint8_t)((int)L.cnt[z * 64 + lane] + 1);
     atomicAdd(&red[z], 1);

@@ -62,7 +62,9 @@ struct OniGibbs {
   float alpha;
   uint32_t seed0, seed1;
   int32_t nk_rep;              // dnk holds nk_rep replicas of [KS] (power of 2): block b adds into b % nk_rep
-  int32_t flags;               // bit 0: n + α is exact in f32 for every count of this corpus (rows may hold it)
+  int32_t flags;               // bit 0: n + α is exact in f32 for every count of this corpus (rows may hold it);
+                               // bits 1-2: kernel A/B variants; bit 3: init pass puts every token of a word
+                               // in topic ⌊mix32(w)·K / 2^32⌋ (seed-free start)
 };
 
 namespace {
@@ -333,7 +335,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 8))) 
     if (w == oni::kPadWord) continue;  // uniform across the G lanes of a unit
     const uint32_t rr = rng.pick(s);
     if constexpr (INIT) {
-      const int z = (int)__umulhi(rr, (uint32_t)a.K);
+      // flags bit 3: seed-free start, every token of a word in the word's hashed topic
+      const int z = (int)__umulhi((a.flags & 8) ? oni::mix32(w) : rr, (uint32_t)a.K);
 #pragma unroll
       for (int j = 0; j < KP; ++j) n[j] += (kbase + j == z);
       if (g == 0) {

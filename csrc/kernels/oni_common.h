@@ -39,6 +39,16 @@ __device__ __forceinline__ uint32_t pick4(const U4& r, uint32_t i) {
   return i == 0 ? r.x : (i == 1 ? r.y : (i == 2 ? r.z : r.w));
 }
 
+// 32-bit integer mixer (lowbias32, C. Wellons): the seed-free initial topic of a word.
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
 // 24-bit uniform in [0,1): exact in f32 on both sides (GPU and NumPy oracle).
 __device__ __forceinline__ float u01(uint32_t r) { return (float)(r >> 8) * 5.9604644775390625e-08f; }
 

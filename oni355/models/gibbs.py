@@ -101,6 +101,9 @@ class GibbsConfig:
     # graphs (three integer adds per sweep), so the averaging costs no eager launches.
     post_samples: int = field(default_factory=lambda: int(os.environ.get("ONI_POST_SAMPLES", "50")))
     post_every: int = field(default_factory=lambda: int(os.environ.get("ONI_POST_EVERY", "1")))
+    # initial topics: "random" (Philox stream 0 per token) or "word" (every token of a word in the
+    # word's hashed topic, independent of the seed: chains of different seeds start together)
+    init: str = field(default_factory=lambda: os.environ.get("ONI_INIT", "random"))
 
     def resolved_alpha(self) -> float:
         return float(self.alpha) if self.alpha is not None else 50.0 / self.K
@@ -362,7 +365,7 @@ class GibbsLDA:
             st["mh_lmax"] = self.mh_lmax
         ops.gibbs_pass(st, self.G, self.KP, self.K, self.alpha, self.cfg.seed, True,
                        self.sweep_ctr, self.c.chunk_len, host_sweep=0, mode=0,
-                       sampler=SAMPLERS["mh"] if self.mh else 0)
+                       sampler=SAMPLERS["mh"] if self.mh else 0, word_init=self.cfg.init == "word")
         ops.recount(self.c.wsorted, self.c.wslot, self.tok_z, self.nwk, self.KS)
         self._split_sync_absolute(self.ndk[0])
         if self.comm is not None and self.comm.dist:

@@ -57,6 +57,17 @@ def token_rand(pos, key, sweep, stream, seed0, seed1):
     return np.select([sel == 0, sel == 1, sel == 2], [r[0], r[1], r[2]], r[3]).astype(U32)
 
 
+def mix32(x):
+    """lowbias32 integer mixer (oni_common.h mix32): the seed-free initial topic of a word."""
+    x = np.asarray(x, dtype=U64) & MASK32
+    x ^= x >> U64(16)
+    x = (x * U64(0x7FEB352D)) & MASK32
+    x ^= x >> U64(15)
+    x = (x * U64(0x846CA68B)) & MASK32
+    x ^= x >> U64(16)
+    return x.astype(U32)
+
+
 def u01(r):
     return (np.asarray(r, dtype=U32) >> U32(8)).astype(F32) * F32(5.9604644775390625e-08)
 
@@ -258,7 +269,7 @@ def excluded_q(qz: np.ndarray, zo: np.ndarray, qfix: np.ndarray) -> np.ndarray:
 
 
 def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed0: int, seed1: int, init: bool,
-               sweep: int, chunk_len: np.ndarray):
+               sweep: int, chunk_len: np.ndarray, word_init: bool = False):
     """One init (init=True) or sweep pass over numpy state arrays, in place.
 
     A sweep draws every token from the collapsed conditional with the token removed from BOTH
@@ -308,6 +319,8 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed0: int, seed
         pos = st["chunk_pos0"][act].astype(U32) + U32(s)
         rr = token_rand(pos, st["chunk_key"][act], sw, stream, seed0, seed1)
         if init:
+            if word_init:  # seed-free start: every token of a word in the word's hashed topic
+                rr = mix32(w)
             z = ((rr.astype(U64) * U64(K)) >> U64(32)).astype(np.int64)
             n[act, z] += 1
             st["tok_z"][idx] = z.astype(np.uint8)

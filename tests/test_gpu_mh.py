@@ -95,3 +95,24 @@ def test_mh_graph_auto_matches_eager(gpu):
     a, b = runs
     assert b._graph is not None or b._graphs
     assert torch.equal(a.tok_z, b.tok_z) and torch.equal(a.nwk, b.nwk) and torch.equal(a.ndk_cur, b.ndk_cur)
+
+
+@pytest.mark.parametrize("K,sampler", [(20, "dense"), (50, "dense"), (100, "mh")])
+def test_word_init_bitwise_and_seed_free(gpu, K, sampler):
+    """ONI_INIT=word: every token of a word starts in the word's hashed topic, on the GPU as in the
+    oracle, whatever the seed."""
+    tdoc, tword, keys = _toy(300, 400, 9)
+    G, KP = ops.choose_tiling(K, "mh" if sampler == "mh" else None)
+    cc = build_corpus(tdoc, tword, 300, 400, torch.from_numpy(keys), G, L=64)
+    cg = build_corpus(tdoc.to(gpu), tword.to(gpu), 300, 400, torch.from_numpy(keys).to(gpu), G, L=64)
+    zs = []
+    for seed, c in ((1, cc), (1, cg), (77, cg)):
+        m = GibbsLDA(c, GibbsConfig(K=K, seed=seed, use_graph=False, sampler=sampler, init="word"))
+        m.initialize()
+        zs.append((m.tok_z.cpu(), m.ndk_cur.cpu(), m.nwk.cpu()))
+    for i in range(3):
+        assert torch.equal(zs[0][i], zs[1][i]) and torch.equal(zs[1][i], zs[2][i])
+    w = cc.tok_word.numpy().view(np.uint32)
+    real = w != 0xFFFFFFFF
+    want = ((spec.mix32(w[real]).astype(np.uint64) * np.uint64(K)) >> np.uint64(32)).astype(np.uint8)
+    assert np.array_equal(zs[0][0].numpy()[real], want)
