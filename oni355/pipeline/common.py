@@ -104,11 +104,13 @@ def encode_words(word_keys64: torch.Tensor, comm: Comm | None, key_bits: int = 6
     return vocab, remap[lids.long()]
 
 
+@traced("oni:global_vocab")
 def global_vocab(keys64: torch.Tensor, comm: Comm | None) -> torch.Tensor:
     """Sorted unique int64 word keys over all ranks (collective X02)."""
     return encode_words(keys64, comm)[0]
 
 
+@traced("oni:encode_docs")
 def encode_docs(doc_keys64: torch.Tensor, key_bits: int = 32):
     """(sorted unique doc keys int64, int32 doc id of every token)."""
     if doc_keys64.is_cuda:
@@ -196,6 +198,7 @@ def lpt_place(counts: np.ndarray, load: np.ndarray) -> np.ndarray:
     return owner
 
 
+@traced("oni:place_docs")
 def place_docs(doc_keys64: torch.Tensor, weights: torch.Tensor | None, comm: Comm, per_doc: bool = False,
                split_L: int | None = None):
     """Owner rank of each token's document, balanced by global token counts.
@@ -355,6 +358,7 @@ def route_to_owners(doc_keys64: torch.Tensor, word_ids: torch.Tensor, weights: t
     return udoc, inv, wi, wt, Route(order, counts.tolist(), rc, plan)
 
 
+@traced("oni:return_to_origin")
 def return_to_origin(x: torch.Tensor, route: Route, comm: Comm) -> torch.Tensor:
     """Inverse of :func:`route_to_owners` for a per-received-token value ``x`` (owner layout):
     returns the value of every token this rank sent, in its original token order."""
@@ -779,7 +783,7 @@ def plan_from_pairs(ps, n: int, n_sides: int, doc_rows: torch.Tensor | None = No
     return plan
 
 
-@traced("oni:score_plan")
+@traced("oni:event_score_plan")
 def event_score_plan(run: LdaRun, dkeys: torch.Tensor, vocab: torch.Tensor, doc_sides: list, word_ids_ev: torch.Tensor,
                      word_sides: list, comm: Comm | None) -> ScorePlan:
     """Score plan of this rank's events (``doc_sides``: doc keys per endpoint, ``word_ids_ev``: the

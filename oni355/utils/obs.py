@@ -19,7 +19,9 @@ def _load_roctx():
     global _roctx
     with _roctx_lock:
         if _roctx is None:
-            for name in ("libroctx64.so", "/opt/rocm/lib/libroctx64.so"):
+            # the rocprofiler-sdk roctx first: rocprofv3 --marker-trace intercepts that one
+            for name in ("librocprofiler-sdk-roctx.so.1", "/opt/rocm/lib/librocprofiler-sdk-roctx.so.1",
+                         "libroctx64.so", "/opt/rocm/lib/libroctx64.so"):
                 try:
                     lib = ctypes.CDLL(name)
                     lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
