@@ -116,3 +116,23 @@ def test_word_init_bitwise_and_seed_free(gpu, K, sampler):
     real = w != 0xFFFFFFFF
     want = ((spec.mix32(w[real]).astype(np.uint64) * np.uint64(K)) >> np.uint64(32)).astype(np.uint8)
     assert np.array_equal(zs[0][0].numpy()[real], want)
+
+
+def test_mh_resume_bitwise(gpu):
+    """An MH chain restored from its canonical z continues bit for bit (the tables are rebuilt
+    from the restored counts every sweep)."""
+    tdoc, tword, keys = _toy(400, 300, 13)
+    c = build_corpus(tdoc.to(gpu), tword.to(gpu), 400, 300, torch.from_numpy(keys).to(gpu), 1, L=127)
+    cfg = dict(K=100, seed=3, sampler="mh")
+    a = GibbsLDA(c, GibbsConfig(**cfg))
+    a.initialize()
+    a.sweep(7)
+    b = GibbsLDA(c, GibbsConfig(**cfg))
+    b.initialize()
+    b.sweep(3)
+    z = b.canonical_z().cpu()
+    r = GibbsLDA(c, GibbsConfig(**cfg))
+    r.load_canonical_z(z, 3)
+    r.sweep(4)
+    assert torch.equal(a.canonical_z(), r.canonical_z())
+    assert torch.equal(a.nwk, r.nwk) and torch.equal(a.ndk_cur, r.ndk_cur)
