@@ -209,6 +209,7 @@ struct MHLane {
   bool multi;
   int lc;               // chunk length
   uint32_t pos0, key, sweep;
+  uint32_t key2;        // per-sweep key of the second doc move's Philox2x32 stream
   const int32_t* brow;  // n_src row of the doc
   const uint32_t* drow; // dalias row of the doc (row 0 for one-chunk docs)
   uint32_t wa[2];       // stage A: token words (parity slots)
@@ -259,10 +260,11 @@ struct MHLane {
     x.ed = drow[multi ? __umulhi(x.r.z, (uint32_t)K) : 0u];
     x.bzo = brow[multi ? x.zo : 0];
     if constexpr (DM > 1) {
-      const oni::U4 r2 = oni::philox10(oni::U4{pos0 + (uint32_t)s, key, sweep, 3u}, a.seed0, a.seed1);
-      x.r2z = r2.z;
-      x.r2w = r2.w;
-      x.ed2 = drow[multi ? __umulhi(r2.z, (uint32_t)K) : 0u];
+      uint32_t c0 = pos0 + (uint32_t)s, c1 = key;
+      oni::philox2x32_10(c0, c1, key2);
+      x.r2z = c0;
+      x.r2w = c1;
+      x.ed2 = drow[multi ? __umulhi(c0, (uint32_t)K) : 0u];
     }
   }
 
@@ -479,6 +481,7 @@ __global__ __launch_bounds__(64) void k_gibbs_mh(const OniMH m) {
   x.pos0 = live ? (uint32_t)a.chunk_pos0[chunk] : 0u;
   x.key = live ? a.chunk_key[chunk] : 0u;
   x.sweep = *a.sweep_ctr;
+  x.key2 = oni::philox10(oni::U4{x.sweep, 3u, 0x4D48u, 0u}, a.seed0, a.seed1).x;
   const int32_t* own = a.ndk_src + (int64_t)(live ? doc : 0) * KS;
   // multi-chunk docs read their sweep-start row; one-chunk docs never use it and read one common
   // address instead (row 0, index 0), so their lanes add no scattered lines to the gathers

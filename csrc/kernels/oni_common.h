@@ -35,6 +35,19 @@ __device__ __forceinline__ U4 philox10(U4 c, uint32_t k0, uint32_t k1) {
   return c;
 }
 
+// Philox2x32-10: two words per counter (pos, doc key) under key k -- half the multiplies of the
+// 4x32 generator where a draw needs two words.
+__device__ __forceinline__ void philox2x32_10(uint32_t& c0, uint32_t& c1, uint32_t k) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p = (uint64_t)0xD256D193u * c0;
+    const uint32_t hi = (uint32_t)(p >> 32), lo = (uint32_t)p;
+    c0 = hi ^ k ^ c1;
+    c1 = lo;
+    k += 0x9E3779B9u;
+  }
+}
+
 __device__ __forceinline__ uint32_t pick4(const U4& r, uint32_t i) {
   return i == 0 ? r.x : (i == 1 ? r.y : (i == 2 ? r.z : r.w));
 }

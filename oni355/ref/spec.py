@@ -49,6 +49,28 @@ def philox10(c0, c1, c2, c3, k0, k1):
     return c0, c1, c2, c3
 
 
+def philox2x32_10(c0, c1, k):
+    """Philox2x32-10 (multiplier 0xD256D193, key bump 0x9E3779B9): half the work of the 4x32
+    generator where a draw needs two words (the MH sampler's extra doc moves)."""
+    c0 = np.asarray(c0, dtype=U32).copy()
+    c1 = np.asarray(c1, dtype=U32).copy()
+    c0, c1 = np.broadcast_arrays(c0, c1)
+    c0, c1 = c0.copy(), c1.copy()
+    k = int(k) & 0xFFFFFFFF
+    for _ in range(10):
+        p = c0.astype(U64) * U64(0xD256D193)
+        hi, lo = (p >> U64(32)).astype(U32), (p & MASK32).astype(U32)
+        c0, c1 = hi ^ U32(k) ^ c1, lo
+        k = (k + 0x9E3779B9) & 0xFFFFFFFF
+    return c0, c1
+
+
+def mh_move_key(sweep, move, seed0, seed1):
+    """Per-sweep key of the Philox2x32 stream of MH doc move ``move`` ≥ 1 (counter = (pos, doc
+    key)); one Philox4x32 block of (sweep, 2 + move, 'MH', 0) under the run seed."""
+    return int(philox10(U32(sweep), U32(2 + move), U32(0x4D48), U32(0), seed0, seed1)[0])
+
+
 def token_rand(pos, key, sweep, stream, seed0, seed1):
     """The u32 draw of token (doc key, pos) in (sweep, stream): mirrors the kernel's pick4."""
     pos = np.asarray(pos, dtype=U32)
@@ -508,7 +530,7 @@ def mh_moves(nn, bb, qrow, zo, qe, multi, Nd, s, zslice, drows, wrows, wsum, g, 
     sc = np.where(acc, t, zo)
     for c in range(doc_moves):
         if c:
-            _, _, r2, r3 = philox10(pos, key, U32(sweep), U32(2 + c), seed0, seed1)
+            r2, r3 = philox2x32_10(pos, key, mh_move_key(sweep, c, seed0, seed1))
         y = (u01(r2) * tot).astype(F32)
         pick = y < Ndf
         pp = y.astype(np.int64)
@@ -549,7 +571,8 @@ def gibbs_pass_mh(st: dict, KS: int, K: int, alpha: float, seed0: int, seed1: in
       ratio (n_t^¬+α)·Z_zo / ((n_zo^¬+α)·Z_t) with Z_zo = Σ_k q[w, k] (the table's sum) and
       Z_t = (Z_zo − (q_zo − q'_zo)) + (1 − q_t)·g_t, the sum the table would have with the token
       at t (g_t = 1/(D_t + 1)).
-    * ``doc_moves`` doc moves (r2 proposes, r3 accepts; move c > 0 uses block 2 + c). One-chunk
+    * ``doc_moves`` doc moves (r2 proposes, r3 accepts; move c > 0 draws (r2, r3) from
+      Philox2x32-10 on (pos, doc key) under the per-sweep key :func:`mh_move_key`). One-chunk
       documents propose ∝ n_dk^¬ + α -- with y = u(r2)·(L − 1 + Kα), y < L − 1 picks the current
       topic of another token of the chunk (position ⌊y⌋, skipping its own), else topic
       ⌊(y − (L − 1))/α⌋ -- a state-free proposal: ratio q'_t / q'_x. Documents over several chunks
