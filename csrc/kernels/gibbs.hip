@@ -343,20 +343,32 @@ __global__ __launch_bounds__(256) void k_wdelta_recount(uint32_t* __restrict__ w
     m = wbits[word];
     if (m) wbits[word] = 0u;
   }
+  // four set bits per round: their word / topic loads are issued together (one latency, not four)
   while (m) {
-    const int b = __ffs(m) - 1;
-    m &= m - 1u;
-    const int64_t i = word * 32 + b;
-    const int w = wsorted[i];
-    const uint32_t zz = zz_w[i];
-    const int zo = (int)(zz & 0xFFu), zn = (int)(zz >> 8);
-    const int r = w - w_lo;
-    if (r < rows) {
-      atomicAdd(&hst[r * KS + zn], 1);
-      atomicAdd(&hst[r * KS + zo], -1);
-    } else {
-      atomicAdd(&dnwk[(int64_t)w * KS + zn], 1);
-      atomicAdd(&dnwk[(int64_t)w * KS + zo], -1);
+    int w[4];
+    uint32_t zz[4];
+    bool v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] = m != 0u;
+      const int b = v[j] ? __ffs(m) - 1 : 0;
+      m &= v[j] ? m - 1u : m;
+      const int64_t i = word * 32 + b;
+      w[j] = wsorted[i];
+      zz[j] = zz_w[i];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!v[j]) continue;
+      const int zo = (int)(zz[j] & 0xFFu), zn = (int)(zz[j] >> 8);
+      const int r = w[j] - w_lo;
+      if (r < rows) {
+        atomicAdd(&hst[r * KS + zn], 1);
+        atomicAdd(&hst[r * KS + zo], -1);
+      } else {
+        atomicAdd(&dnwk[(int64_t)w[j] * KS + zn], 1);
+        atomicAdd(&dnwk[(int64_t)w[j] * KS + zo], -1);
+      }
     }
   }
   __syncthreads();
