@@ -35,10 +35,13 @@ X01_PACK_MIN_BYTES = 4 << 20
 SAMPLERS = {"generic": 0, "lds": 2, "x1": 3, "mh": ops.SAMPLER_MH}
 
 
-# "auto" runs the MH sampler above this many topics: at K = 100 its sweep is 0.84 vs 1.02 ms on the
-# 12.5M-flow day and 3.2 vs 6.6 ms on the config-5 flow model, at equal chain quality
-# (profiles/r4/mh_*); the dense samplers below
-MH_AUTO_MIN_K = 65
+# "auto" would run the MH sampler from this many topics (env ONI_MH_AUTO_MIN_K). Off by default:
+# at K = 100 it is 0.83 vs 1.02 ms per sweep on the 12.5M-flow day and 3.2 vs 6.6 ms on the
+# config-5 flow model, but on the 125M-token model its chain is still climbing at sweep 400
+# (−2.7 % log-likelihood against the dense chain, flat from sweep 50) and the config-5 proxy
+# recall drops 0.845 → 0.72 (profiles/r4/mh_quality_gpu_62.5M_k100_400sweeps.json,
+# combined_day_config5_share_125M_{mh,dense}.json). ONI_SAMPLER=mh selects it.
+MH_AUTO_MIN_K = int(os.environ.get("ONI_MH_AUTO_MIN_K", "256"))
 
 
 def sampler_for(K: int, sampler: str | None = None) -> str:
@@ -83,7 +86,7 @@ class GibbsConfig:
     check_invariants: bool = field(default_factory=lambda: os.environ.get("ONI_CHECK_INVARIANTS", "0") == "1")
     # cheap numerical health check after every sweep() call (ONI_HEALTH_CHECK=0 disables)
     health_check: bool = field(default_factory=lambda: os.environ.get("ONI_HEALTH_CHECK", "1") != "0")
-    # sweep kernel: "auto" (default: "mh" for K ≥ MH_AUTO_MIN_K, else "dense"), "dense" ("x1" for
+    # sweep kernel: "auto" (default: "dense"; "mh" for K ≥ MH_AUTO_MIN_K when that is set), "dense" ("x1" for
     # K ≤ 32, "lds" above), "x1" the one-lane register sampler k_gibbs_x1, "lds" the multi-lane
     # LDS-count sampler k_gibbs_ldsg, "generic" k_gibbs (any unit width; the fallback when n + α is
     # not exact in f32) -- these are bitwise identical to each other and to spec.gibbs_pass --
