@@ -176,6 +176,7 @@ struct MHLds {
 };
 
 // stage-B data of one token (issued one step ahead; none of it depends on the chain state)
+template <int DM>
 struct MHB {
   oni::U4 r;     // Philox block (pos, key, sweep, 2)
   int zo;        // sweep-start topic
@@ -188,10 +189,11 @@ struct MHB {
   float qtd;     // q[w, td]
   int32_t btw, btd;  // n_src[doc, tw / td] (multi-chunk docs)
   // second doc move (DM = 2): Philox block (pos, key, sweep, 3) words z / w, its proposal and gathers
-  uint32_t r2z, r2w, ed2;
-  int td2;
-  float qtd2;
-  int32_t btd2;
+  // doc moves 2..DM: Philox2x32 words (proposal, acceptance), doc alias entry, proposal, gathers
+  uint32_t r2z[DM > 1 ? DM - 1 : 1], r2w[DM > 1 ? DM - 1 : 1], ed2[DM > 1 ? DM - 1 : 1];
+  int td2[DM > 1 ? DM - 1 : 1];
+  float qtd2[DM > 1 ? DM - 1 : 1];
+  int32_t btd2[DM > 1 ? DM - 1 : 1];
 };
 
 // Straight-line step: every lane issues the same loads (padding lanes on word 0, one-chunk docs
@@ -209,12 +211,12 @@ struct MHLane {
   bool multi;
   int lc;               // chunk length
   uint32_t pos0, key, sweep;
-  uint32_t key2;        // per-sweep key of the second doc move's Philox2x32 stream
+  uint32_t key2[DM > 1 ? DM - 1 : 1];  // per-sweep keys of doc moves 2..DM (Philox2x32 streams)
   const int32_t* brow;  // n_src row of the doc
   const uint32_t* drow; // dalias row of the doc (row 0 for one-chunk docs)
   uint32_t wa[2];       // stage A: token words (parity slots)
   int32_t pa[2];        // stage A: word-sorted slots (MODE 3/4)
-  MHB b[2];             // stage B (parity slots)
+  MHB<DM> b[2];             // stage B (parity slots)
   int32_t* red;         // LDS: per-topic count deltas of the wave
   int nchg;
   Pend<MODE> pend;
@@ -249,7 +251,7 @@ struct MHLane {
 
   // stage B of the token at step s (word w): Philox block, then the state-free gathers
   __device__ __forceinline__ void issue_b(int P, int s, uint32_t w) {
-    MHB& x = b[P];
+    MHB<DM>& x = b[P];
     const uint32_t wc = w == oni::kPadWord ? 0u : w;
     x.r = oni::philox10(oni::U4{pos0 + (uint32_t)s, key, sweep, 2u}, a.seed0, a.seed1);
     const int z0 = (int)L.zsl[s * 64 + lane];
@@ -259,19 +261,20 @@ struct MHLane {
     // one-chunk docs read one common address (they use neither value): no scattered lines
     x.ed = drow[multi ? __umulhi(x.r.z, (uint32_t)K) : 0u];
     x.bzo = brow[multi ? x.zo : 0];
-    if constexpr (DM > 1) {
+#pragma unroll
+    for (int c = 0; c < DM - 1; ++c) {
       uint32_t c0 = pos0 + (uint32_t)s, c1 = key;
-      oni::philox2x32_10(c0, c1, key2);
-      x.r2z = c0;
-      x.r2w = c1;
-      x.ed2 = drow[multi ? __umulhi(c0, (uint32_t)K) : 0u];
+      oni::philox2x32_10(c0, c1, key2[c]);
+      x.r2z[c] = c0;
+      x.r2w[c] = c1;
+      x.ed2[c] = drow[multi ? __umulhi(c0, (uint32_t)K) : 0u];
     }
   }
 
   // stage C of the token at step s: its proposals (the one-chunk doc proposal reads the chunk's
   // current topics, so this runs after the previous token has moved) and their gathers
   __device__ __forceinline__ void issue_c(int P, int s, uint32_t w) {
-    MHB& x = b[P];
+    MHB<DM>& x = b[P];
     const uint32_t qo = (w == oni::kPadWord ? 0u : w) * (uint32_t)KS;
     x.tw = alias_draw(x.r.x, x.rw.x);
     const int tdm = alias_draw(x.r.z, x.ed);
@@ -280,14 +283,15 @@ struct MHLane {
     x.qtd = a.q[qo + (uint32_t)x.td];
     x.btw = brow[multi ? x.tw : 0];
     x.btd = brow[multi ? x.td : 0];
-    if constexpr (DM > 1) {
-      // the second doc move's proposal is state-free too (the chunk's other topics do not move
-      // while this token does): prefetched with the first
-      const int t2m = alias_draw(x.r2z, x.ed2);
-      const int t2s = single_pick(x.r2z, s);
-      x.td2 = multi ? t2m : t2s;
-      x.qtd2 = a.q[qo + (uint32_t)x.td2];
-      x.btd2 = brow[multi ? x.td2 : 0];
+    // the later doc moves' proposals are state-free too (the chunk's other topics do not move
+    // while this token does): prefetched with the first
+#pragma unroll
+    for (int c = 0; c < DM - 1; ++c) {
+      const int t2m = alias_draw(x.r2z[c], x.ed2[c]);
+      const int t2s = single_pick(x.r2z[c], s);
+      x.td2[c] = multi ? t2m : t2s;
+      x.qtd2[c] = a.q[qo + (uint32_t)x.td2[c]];
+      x.btd2[c] = brow[multi ? x.td2[c] : 0];
     }
   }
 
@@ -301,7 +305,7 @@ struct MHLane {
     const uint32_t w = wa[P];
     const int32_t pw = pa[P];
     const bool act = w != oni::kPadWord;
-    const MHB& x = b[P];
+    const MHB<DM>& x = b[P];
     const int zo = x.zo;
     cell_set(zo, cell(zo) - (act ? 1 : 0));  // the token leaves its topic: every count below is n^¬
     asm volatile("" ::: "memory");
@@ -345,10 +349,10 @@ struct MHLane {
       float at = atd;
       if constexpr (DM > 1) {
         if (c > 0) {
-          r3 = x.r2w;
-          t = x.td2;
-          qt = t == zo ? qe : x.qtd2;
-          bt = x.btd2;
+          r3 = x.r2w[c - 1];
+          t = x.td2[c - 1];
+          qt = t == zo ? qe : x.qtd2[c - 1];
+          bt = x.btd2[c - 1];
           at = aw(cell(t), bt);
         }
       }
@@ -481,7 +485,9 @@ __global__ __launch_bounds__(64) void k_gibbs_mh(const OniMH m) {
   x.pos0 = live ? (uint32_t)a.chunk_pos0[chunk] : 0u;
   x.key = live ? a.chunk_key[chunk] : 0u;
   x.sweep = *a.sweep_ctr;
-  x.key2 = oni::philox10(oni::U4{x.sweep, 3u, 0x4D48u, 0u}, a.seed0, a.seed1).x;
+#pragma unroll
+  for (int c = 0; c < DM - 1; ++c)
+    x.key2[c] = oni::philox10(oni::U4{x.sweep, 3u + (uint32_t)c, 0x4D48u, 0u}, a.seed0, a.seed1).x;
   const int32_t* own = a.ndk_src + (int64_t)(live ? doc : 0) * KS;
   // multi-chunk docs read their sweep-start row; one-chunk docs never use it and read one common
   // address instead (row 0, index 0), so their lanes add no scattered lines to the gathers
@@ -595,27 +601,21 @@ ONI_API int oni_gibbs_mh_launch(const OniMH* m, int init, int mode, hipStream_t 
     return (int)hipGetLastError();
   }
   if (!a.qfix || !m->walias || !m->wsum || !m->mh_g || !m->chunk_dslot) return (int)hipErrorInvalidValue;
-  if (m->doc_moves < 1 || m->doc_moves > 2) return (int)hipErrorInvalidValue;
+  if (m->doc_moves < 1 || m->doc_moves > 4) return (int)hipErrorInvalidValue;
   if (mode == 2 && !a.chg_mask) return (int)hipErrorInvalidValue;
   if (mode == 3 && (!a.wpos || !a.z_w)) return (int)hipErrorInvalidValue;
   if (mode == 4 && (!a.wpos || !a.zz_w || !a.chg_mask)) return (int)hipErrorInvalidValue;
 #define ONI_MH(md, dm) k_gibbs_mh<md, dm><<<grid, 64, lds, s>>>(*m)
-  if (m->doc_moves == 1) {
-    switch (mode) {
-      case 0: ONI_MH(0, 1); break;
-      case 1: ONI_MH(1, 1); break;
-      case 2: ONI_MH(2, 1); break;
-      case 3: ONI_MH(3, 1); break;
-      default: ONI_MH(4, 1); break;
-    }
-  } else {
-    switch (mode) {
-      case 0: ONI_MH(0, 2); break;
-      case 1: ONI_MH(1, 2); break;
-      case 2: ONI_MH(2, 2); break;
-      case 3: ONI_MH(3, 2); break;
-      default: ONI_MH(4, 2); break;
-    }
+  switch (m->doc_moves * 8 + mode) {
+#define ONI_MH_CASES(dm) \
+    case dm * 8 + 0: ONI_MH(0, dm); break; \
+    case dm * 8 + 1: ONI_MH(1, dm); break; \
+    case dm * 8 + 2: ONI_MH(2, dm); break; \
+    case dm * 8 + 3: ONI_MH(3, dm); break; \
+    case dm * 8 + 4: ONI_MH(4, dm); break;
+    ONI_MH_CASES(1) ONI_MH_CASES(2) ONI_MH_CASES(3) ONI_MH_CASES(4)
+#undef ONI_MH_CASES
+    default: return (int)hipErrorInvalidValue;
   }
 #undef ONI_MH
   return (int)hipGetLastError();

@@ -48,7 +48,8 @@ def test_alias_tables_bitwise(gpu, K):
 
 _CASES = [(100, "recount", 1, 64), (100, "wdelta", 1, 64), (100, "atomic", 1, 64), (100, "dual", 1, 64),
           (100, "delta", 1, 64), (100, "recount", 2, 64), (100, "wdelta", 2, 32), (40, "wdelta", 1, 32),
-          (7, "recount", 1, 64), (255, "wdelta", 2, 64), (64, "dual", 2, 127)]
+          (7, "recount", 1, 64), (255, "wdelta", 2, 64), (64, "dual", 2, 127), (100, "wdelta", 3, 64),
+          (100, "recount", 4, 127), (40, "dual", 4, 32)]
 
 
 @pytest.mark.parametrize("K,mode,dm,L", _CASES)

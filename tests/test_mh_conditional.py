@@ -69,7 +69,7 @@ def _case(K, alpha, multi, R=120_000, Ld=7, s=2, seed=5, beta=0.01, V=50, stale=
 
 @pytest.mark.parametrize("K,alpha", [(7, 0.5), (20, 2.5), (9, 50 / 9)])
 @pytest.mark.parametrize("multi", [False, True, "sparse"])
-@pytest.mark.parametrize("doc_moves", [1, 2])
+@pytest.mark.parametrize("doc_moves", [1, 2, 4])
 def test_mh_moves_leave_the_conditional_invariant(K, alpha, multi, doc_moves):
     # "sparse": a multi-chunk doc whose sweep-start row holds just its chunk (b_zo = 1 is common, so
     # the table's copy of the token at zo matters most)

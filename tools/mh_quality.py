@@ -15,7 +15,7 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def chain(a, sampler: str, cycles: int):
+def chain(a, sampler: str, cycles: int, burn: int = 0):
     import torch
 
     from oni355.models.corpus import auto_chunk_len, build_corpus
@@ -37,16 +37,25 @@ def chain(a, sampler: str, cycles: int):
     G, _ = tiling_for(a.topics, sampler)
     L = a.chunk_len or auto_chunk_len(int(dk.numel()), G, hi=127 if sampler == "mh" else 128)
     c = build_corpus(inv.to(torch.int32), wi, int(udoc.numel()), int(vocab.numel()), common.i64_to_u32bits(udoc), G, L)
-    m = GibbsLDA(c, GibbsConfig(K=a.topics, sampler=sampler, post_samples=1, use_graph=a.device != "cpu"))
+    # burn > 0: the exact generic Gibbs kernel on the MH corpus for ``burn`` sweeps, then MH from
+    # that state (does the MH chain hold the dense chain's equilibrium, or drift off it?)
+    m = GibbsLDA(c, GibbsConfig(K=a.topics, sampler="generic" if burn else sampler, post_samples=1,
+                                use_graph=a.device != "cpu"))
     m.initialize()
+    if burn:
+        from oni355.models.gibbs import SAMPLERS
+        m.sweep(burn)
+        print(json.dumps({"sampler": "generic", "sweep": burn, "loglik": round(m.log_likelihood(), 2)}), flush=True)
+        m.mh, m.qpf, m._graph, m._graphs = True, SAMPLERS["mh"], None, {}
+        m._setup_mh()
     traj = []
     t0 = time.time()
     done = 0
     for stop in range(a.every, a.sweeps + 1, a.every):
         m.sweep(stop - done)
         done = stop
-        traj.append((done, round(m.log_likelihood(), 2)))
-        print(json.dumps({"sampler": sampler, "cycles": cycles, "sweep": done, "loglik": traj[-1][1],
+        traj.append((burn + done, round(m.log_likelihood(), 2)))
+        print(json.dumps({"sampler": sampler, "burn": burn, "cycles": cycles, "sweep": done, "loglik": traj[-1][1],
                           "change": m.change_log[-1][1] if m.change_log else None,
                           "s": round(time.time() - t0, 1)}), flush=True)
     return {"L": L, "G": G, "T": int(c.T), "traj": traj}
@@ -62,11 +71,14 @@ def main() -> int:
     ap.add_argument("--chunk-len", type=int, default=0)
     ap.add_argument("--doc-moves", default="1,2")
     ap.add_argument("--wide", action="store_true")
+    ap.add_argument("--burn", type=int, default=0, help="also run MH after this many exact generic sweeps")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     res = {"flows": a.flows, "topics": a.topics, "gibbs": chain(a, "dense", 1)}
     for cy in [int(x) for x in a.doc_moves.split(",") if x]:
         res[f"mh{cy}"] = chain(a, "mh", cy)
+        if a.burn:
+            res[f"mh{cy}_after_burn{a.burn}"] = chain(a, "mh", cy, a.burn)
     g = res["gibbs"]["traj"][-1][1]
     for k in list(res):
         if k.startswith("mh"):
