@@ -54,6 +54,17 @@ def sampler_for(K: int, sampler: str | None = None) -> str:
     return s
 
 
+def mh_burn_for(sweeps: int) -> int:
+    """Dense sweeps an MH model runs before its own (env ONI_MH_BURN, default 20): the pipeline
+    samples them with the exact dense kernel on a second corpus of the dense tiling and hands the
+    chain over through its canonical z (:meth:`GibbsLDA.load_canonical_z`). From a random start
+    the MH chain burns in slowly on large models (−3 % log-likelihood at sweep 200 on the
+    125M-token flow model); started from the dense chain's state it holds the dense chain's
+    equilibrium (+0.01 % after 40 dense sweeps, +0.1 % after 20, −0.45 % after 10:
+    profiles/r4/mh_quality_gpu_62.5M_k100_burn*.json)."""
+    return max(0, min(int(os.environ.get("ONI_MH_BURN", "20")), int(sweeps)))
+
+
 def tiling_for(K: int, sampler: str | None = None) -> tuple[int, int]:
     return ops.choose_tiling(K, "mh" if sampler_for(K, sampler) == "mh" else None)
 

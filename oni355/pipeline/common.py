@@ -489,9 +489,12 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
         if word_ids is None:
             word_ids = torch.searchsorted(vocab, word_keys64).to(torch.int32)
         use_w = weights is not None
-        from ..models.gibbs import sampler_for, tiling_for
+        from ..models.gibbs import mh_burn_for, sampler_for, tiling_for
         G, _ = tiling_for(K)
         mh = sampler_for(K) == "mh"
+        # an MH model's first sweeps run the dense kernel on a corpus of the dense tiling
+        burn_mh = mh_burn_for(sweeps) if mh and train else 0
+        Gd = tiling_for(K, "dense")[0] if burn_mh else G
         if chunk_len <= 0:
             # the global (weighted) token count picks L -- before routing: the placement cuts
             # heavy documents at multiples of L
@@ -516,12 +519,17 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
             # heavy documents cut across ranks: the corpus holds this rank's pieces (pairs clipped
             # to their canonical ranges) instead of the tokens the primary received for scoring
             tdoc, tword, twt, dkeys, meta = split_corpus_tokens(plan, udoc, inv, wi, wt, V, comm)
-            corpus = build_corpus(tdoc, tword, int(dkeys.numel()), V, i64_to_u32bits(dkeys), G, chunk_len,
-                                  weight=twt)
-            apply_split(corpus, meta)
+
+            def corpus_for(g):
+                c = build_corpus(tdoc, tword, int(dkeys.numel()), V, i64_to_u32bits(dkeys), g, chunk_len, weight=twt)
+                apply_split(c, meta)
+                return c
         else:
-            corpus = build_corpus(inv, wi, D, V, i64_to_u32bits(udoc), G, chunk_len,
-                                  weight=wt if use_w else None, pairs=pairs if dev.type == "cuda" else None)
+            def corpus_for(g):
+                return build_corpus(inv, wi, D, V, i64_to_u32bits(udoc), g, chunk_len,
+                                    weight=wt if use_w else None, pairs=pairs if dev.type == "cuda" else None)
+        corpus = corpus_for(G)
+        dcorpus = corpus_for(Gd) if Gd != G else None
     with timer.stage("init"):
         model = GibbsLDA(corpus, GibbsConfig(K=K, alpha=alpha, beta=beta, seed=seed), comm=comm,
                          V_global=int(vocab.numel()))
@@ -529,35 +537,54 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
         if not train:
             return run
         model.plan_average(sweeps)
+        win = model.average_window
+        if win is not None and dcorpus is not None:
+            burn_mh = min(burn_mh, win[0] - 1)  # the MH model takes every posterior sample
+        burner = None  # the dense model of an MH model's first burn_mh sweeps
+        if burn_mh <= 0:
+            dcorpus = None
+        if dcorpus is not None and not (ckpt is not None and ckpt.exists() and ckpt.manifest()["sweep"] >= burn_mh):
+            burner = GibbsLDA(dcorpus, GibbsConfig(K=K, alpha=alpha, beta=beta, seed=seed, sampler="dense"),
+                              comm=comm, V_global=int(vocab.numel()))
+        first = burner or model
         if ckpt is not None and ckpt.exists():
-            ckpt.restore(model)
+            ckpt.restore(first)
         else:
-            model.initialize()
+            first.initialize()
     with timer.stage("train"):
         if on_train is not None:
             on_train()
-        remaining = sweeps - model.sweeps_done
+        remaining = sweeps - first.sweeps_done
         step = eval_every if eval_every > 0 else remaining
         ck_every = ckpt.every if ckpt is not None and ckpt.every > 0 else 0
         lag = int(ldac_lag) if ldac_dir else 0
         while remaining > 0:
+            cur = burner or model
             n = min(step, remaining)
+            if burner is not None:
+                n = min(n, burn_mh - burner.sweeps_done)
             if ck_every:
-                n = min(n, ck_every - (model.sweeps_done % ck_every))
+                n = min(n, ck_every - (cur.sweeps_done % ck_every))
             if lag:
-                n = min(n, lag - (model.sweeps_done % lag))
-            model.sweep(n)
+                n = min(n, lag - (cur.sweeps_done % lag))
+            cur.sweep(n)
             remaining -= n
-            mixed = model.sweeps_done > burnin
-            if eval_every > 0 and model.sweeps_done % eval_every == 0 and mixed:
-                ll = model.record_likelihood()
+            mixed = cur.sweeps_done > burnin
+            if eval_every > 0 and cur.sweeps_done % eval_every == 0 and mixed:
+                ll = cur.record_likelihood()
                 if log:
-                    log(f"sweep {model.sweeps_done} loglik {ll:.6e}")
-            if ck_every and model.sweeps_done % ck_every == 0:
-                ckpt.save(model)
-            if lag and model.sweeps_done % lag == 0 and remaining > 0 and mixed:
+                    log(f"sweep {cur.sweeps_done} loglik {ll:.6e}")
+            if ck_every and cur.sweeps_done % ck_every == 0:
+                ckpt.save(cur)
+            if lag and cur.sweeps_done % lag == 0 and remaining > 0 and mixed:
                 from ..io import ldac
-                ldac.export_gibbs(ldac_dir, model, prefix=f"{model.sweeps_done:03d}")
+                ldac.export_gibbs(ldac_dir, cur, prefix=f"{cur.sweeps_done:03d}")
+            if burner is not None and burner.sweeps_done >= burn_mh:
+                # hand the chain to the MH model: same documents and tokens, another tiling
+                model.load_canonical_z(burner.canonical_z(), burner.sweeps_done)
+                model.likelihoods = list(burner.likelihoods)
+                burner.close()
+                burner = dcorpus = None
     model.close()
     if not model.likelihoods or model.likelihoods[-1][0] != model.sweeps_done:
         model.record_likelihood()

@@ -169,6 +169,33 @@ def test_mh_sampler_world4_heavy_ip_bitwise():
     assert four["n_split"] >= 1 and one["qpf"] == four["qpf"] == 4
 
 
+def test_mh_after_dense_burn_world4_bitwise():
+    """An MH model's first sweeps run the dense kernel on a corpus of the dense tiling, then the
+    chain moves to the MH corpus through its canonical z (pipeline.common.build_and_train): the
+    same chain on 1 and 4 ranks (heavy IP cut across ranks), and different from pure MH."""
+    job = dict(source="flow", n=12000, heavy=0.30, K=40, sweeps=6, env={"ONI_SAMPLER": "mh", "ONI_MH_BURN": "3"})
+    one = _run(1, job)
+    four = _run(4, job)
+    _same(one, four)
+    assert four["n_split"] >= 1 and one["qpf"] == four["qpf"] == 4 and four["sweeps"] == 6
+    pure = _run(1, dict(job, env={"ONI_SAMPLER": "mh", "ONI_MH_BURN": "0"}))
+    assert pure["qpf"] == 4 and pure["loglik"] != one["loglik"]
+
+
+@pytest.mark.parametrize("w_save,w_resume,at", [(3, 1, 2), (1, 2, 4)])
+def test_mh_burn_checkpoint_resumes_on_another_world(tmp_path, w_save, w_resume, at):
+    """A checkpoint inside the dense burn-in (sweep 2 of 3) or after the hand-over (sweep 4) on
+    w_save ranks resumes on w_resume ranks, equal to an uninterrupted single-rank run."""
+    ck = str(tmp_path / "ck")
+    base = dict(source="flow", n=8000, heavy=0.30, K=40, env={"ONI_SAMPLER": "mh", "ONI_MH_BURN": "3"})
+    ref = _run(1, dict(base, sweeps=6))
+    first = _run(w_save, dict(base, sweeps=at, ckpt=ck, ckpt_every=at))
+    assert first["sweeps"] == at
+    resumed = _run(w_resume, dict(base, sweeps=6, ckpt=ck, ckpt_every=0))
+    assert resumed["sweeps"] == 6
+    _same(ref, resumed)
+
+
 @pytest.mark.parametrize("source", ["dns", "proxy"])
 def test_dns_proxy_world8_bitwise(source):
     job = dict(source=source, n=6000, K=10 if source == "dns" else 20)

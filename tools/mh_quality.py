@@ -15,7 +15,9 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def chain(a, sampler: str, cycles: int, burn: int = 0):
+def chain(a, sampler: str, cycles: int, z0=None, burn: int = 0, sweeps: int | None = None):
+    """One chain; ``z0`` (canonical z after ``burn`` sweeps of another chain) starts it from that
+    state: does the MH chain hold the dense chain's equilibrium, or drift off it?"""
     import torch
 
     from oni355.models.corpus import auto_chunk_len, build_corpus
@@ -37,28 +39,23 @@ def chain(a, sampler: str, cycles: int, burn: int = 0):
     G, _ = tiling_for(a.topics, sampler)
     L = a.chunk_len or auto_chunk_len(int(dk.numel()), G, hi=127 if sampler == "mh" else 128)
     c = build_corpus(inv.to(torch.int32), wi, int(udoc.numel()), int(vocab.numel()), common.i64_to_u32bits(udoc), G, L)
-    # burn > 0: the exact generic Gibbs kernel on the MH corpus for ``burn`` sweeps, then MH from
-    # that state (does the MH chain hold the dense chain's equilibrium, or drift off it?)
-    m = GibbsLDA(c, GibbsConfig(K=a.topics, sampler="generic" if burn else sampler, post_samples=1,
-                                use_graph=a.device != "cpu"))
-    m.initialize()
-    if burn:
-        from oni355.models.gibbs import SAMPLERS
-        m.sweep(burn)
-        print(json.dumps({"sampler": "generic", "sweep": burn, "loglik": round(m.log_likelihood(), 2)}), flush=True)
-        m.mh, m.qpf, m._graph, m._graphs = True, SAMPLERS["mh"], None, {}
-        m._setup_mh()
+    m = GibbsLDA(c, GibbsConfig(K=a.topics, sampler=sampler, post_samples=1, use_graph=a.device != "cpu"))
+    if z0 is None:
+        m.initialize()
+    else:
+        m.load_canonical_z(z0, burn)
+        print(json.dumps({"sampler": sampler, "start": burn, "loglik": round(m.log_likelihood(), 2)}), flush=True)
     traj = []
     t0 = time.time()
     done = 0
-    for stop in range(a.every, a.sweeps + 1, a.every):
+    for stop in range(a.every, (sweeps or a.sweeps) + 1, a.every):
         m.sweep(stop - done)
         done = stop
         traj.append((burn + done, round(m.log_likelihood(), 2)))
-        print(json.dumps({"sampler": sampler, "burn": burn, "cycles": cycles, "sweep": done, "loglik": traj[-1][1],
-                          "change": m.change_log[-1][1] if m.change_log else None,
+        print(json.dumps({"sampler": sampler, "burn": burn, "cycles": cycles, "sweep": burn + done,
+                          "loglik": traj[-1][1], "change": m.change_log[-1][1] if m.change_log else None,
                           "s": round(time.time() - t0, 1)}), flush=True)
-    return {"L": L, "G": G, "T": int(c.T), "traj": traj}
+    return {"L": L, "G": G, "T": int(c.T), "traj": traj}, m.canonical_z().cpu()
 
 
 def main() -> int:
@@ -71,14 +68,19 @@ def main() -> int:
     ap.add_argument("--chunk-len", type=int, default=0)
     ap.add_argument("--doc-moves", default="1,2")
     ap.add_argument("--wide", action="store_true")
-    ap.add_argument("--burn", type=int, default=0, help="also run MH after this many exact generic sweeps")
+    ap.add_argument("--skip-plain", action="store_true", help="no MH chain from the random start")
+    ap.add_argument("--burn", default="", help="comma list: also run MH from the dense chain's state after this many sweeps")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
-    res = {"flows": a.flows, "topics": a.topics, "gibbs": chain(a, "dense", 1)}
+    res = {"flows": a.flows, "topics": a.topics}
+    res["gibbs"], _ = chain(a, "dense", 1)
+    burns = [int(x) for x in a.burn.split(",") if x]
+    zb = {b: chain(a, "dense", 1, sweeps=b)[1] for b in burns}
     for cy in [int(x) for x in a.doc_moves.split(",") if x]:
-        res[f"mh{cy}"] = chain(a, "mh", cy)
-        if a.burn:
-            res[f"mh{cy}_after_burn{a.burn}"] = chain(a, "mh", cy, a.burn)
+        if not a.skip_plain:
+            res[f"mh{cy}"], _ = chain(a, "mh", cy)
+        for b in burns:
+            res[f"mh{cy}_after_burn{b}"], _ = chain(a, "mh", cy, zb[b], b, a.sweeps - b)
     g = res["gibbs"]["traj"][-1][1]
     for k in list(res):
         if k.startswith("mh"):
