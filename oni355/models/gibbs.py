@@ -35,13 +35,13 @@ X01_PACK_MIN_BYTES = 4 << 20
 SAMPLERS = {"generic": 0, "lds": 2, "x1": 3, "mh": ops.SAMPLER_MH}
 
 
-# "auto" would run the MH sampler from this many topics (env ONI_MH_AUTO_MIN_K). Off by default:
-# at K = 100 it is 0.83 vs 1.02 ms per sweep on the 12.5M-flow day and 3.2 vs 6.6 ms on the
-# config-5 flow model, but on the 125M-token model its chain is still climbing at sweep 400
-# (−2.7 % log-likelihood against the dense chain, flat from sweep 50) and the config-5 proxy
-# recall drops 0.845 → 0.72 (profiles/r4/mh_quality_gpu_62.5M_k100_400sweeps.json,
-# combined_day_config5_share_125M_{mh,dense}.json). ONI_SAMPLER=mh selects it.
-MH_AUTO_MIN_K = int(os.environ.get("ONI_MH_AUTO_MIN_K", "256"))
+# "auto" runs the MH sampler from this many topics (env ONI_MH_AUTO_MIN_K), after the dense burn-in
+# of mh_burn_for(): at K = 100 its sweep is 3.2 vs 6.6 ms on the config-5 flow model, and started
+# from 20 dense sweeps its chain holds the dense chain's log-likelihood (+0.1 % at sweep 200; from a
+# random start it burns in slowly, −3 %). Config-5 day 2.110 → 1.444 s at recall 0.99 / 1.0 / 0.865
+# (dense 0.995 / 1.0 / 0.845; profiles/r4/combined_day_config5_share_125M_{dense,mh_burn20}.json).
+# At K = 50 the dense kernel is the faster one.
+MH_AUTO_MIN_K = int(os.environ.get("ONI_MH_AUTO_MIN_K", "100"))
 
 
 def sampler_for(K: int, sampler: str | None = None) -> str:
@@ -97,7 +97,7 @@ class GibbsConfig:
     check_invariants: bool = field(default_factory=lambda: os.environ.get("ONI_CHECK_INVARIANTS", "0") == "1")
     # cheap numerical health check after every sweep() call (ONI_HEALTH_CHECK=0 disables)
     health_check: bool = field(default_factory=lambda: os.environ.get("ONI_HEALTH_CHECK", "1") != "0")
-    # sweep kernel: "auto" (default: "dense"; "mh" for K ≥ MH_AUTO_MIN_K when that is set), "dense" ("x1" for
+    # sweep kernel: "auto" (default: "dense"; "mh" for K ≥ MH_AUTO_MIN_K = 100), "dense" ("x1" for
     # K ≤ 32, "lds" above), "x1" the one-lane register sampler k_gibbs_x1, "lds" the multi-lane
     # LDS-count sampler k_gibbs_ldsg, "generic" k_gibbs (any unit width; the fallback when n + α is
     # not exact in f32) -- these are bitwise identical to each other and to spec.gibbs_pass --
@@ -942,26 +942,37 @@ class GibbsLDA:
                         True)
         return out[: c.T]
 
-    def load_canonical_z(self, z: torch.Tensor, sweeps_done: int) -> None:
-        """Resume: scatter z into SELL, recount every table from z, refresh q (bitwise resume)."""
+    def load_canonical_z(self, z: torch.Tensor, sweeps_done: int, counts_from: "GibbsLDA | None" = None) -> None:
+        """Resume: scatter z into SELL, recount every table from z, refresh q (bitwise resume).
+
+        ``counts_from``: a model of another tiling over the same documents and tokens whose chain
+        ``z`` is (the MH model's dense burn-in, pipeline.common.build_and_train): its count tables
+        -- current at the end of every sweep -- are copied instead of recounted (125M index adds
+        and two all-reduces less)."""
         c = self.c
         zc = torch.zeros(max(c.T, 1), dtype=torch.uint8, device=self.device)
         zc[: c.T] = z.to(self.device)
         self.tok_z.zero_()
         ops.sell_perm_z(c.chunk_doc, c.chunk_pos0, c.chunk_len, c.S, c.slice_off, c.doc_tok_ptr, self.tok_z, zc,
                         False)
-        tdoc, tword = canonical_tokens(c)
-        zz = zc[: c.T].to(torch.int64)
         for t in (*self.ndk, self.nwk, *self.nk, *self.dn):
             t.zero_()
-        KS = self.KS
-        self.ndk[0].view(-1).index_add_(0, tdoc * KS + zz, torch.ones_like(zz, dtype=torch.int32))
-        self.nwk.view(-1).index_add_(0, tword * KS + zz, torch.ones_like(zz, dtype=torch.int32))
-        self.nk[0].index_add_(0, zz, torch.ones_like(zz, dtype=torch.int32))
-        self._split_sync_absolute(self.ndk[0])
-        if self.comm is not None and self.comm.dist:
-            self.comm.allreduce_(self.nwk)
-            self.comm.allreduce_(self.nk[0])
+        K, KS = self.K, self.KS
+        o = counts_from
+        if o is not None and o.K == K and o.nwk.shape[0] == self.nwk.shape[0] and o.ndk_cur.shape[0] == self.ndk[0].shape[0]:
+            self.ndk[0][:, :K].copy_(o.ndk_cur[:, :K])
+            self.nwk[:, :K].copy_(o.nwk[:, :K])
+            self.nk[0][:K].copy_(o.nk_cur[:K])
+        else:
+            tdoc, tword = canonical_tokens(c)
+            zz = zc[: c.T].to(torch.int64)
+            self.ndk[0].view(-1).index_add_(0, tdoc * KS + zz, torch.ones_like(zz, dtype=torch.int32))
+            self.nwk.view(-1).index_add_(0, tword * KS + zz, torch.ones_like(zz, dtype=torch.int32))
+            self.nk[0].index_add_(0, zz, torch.ones_like(zz, dtype=torch.int32))
+            self._split_sync_absolute(self.ndk[0])
+            if self.comm is not None and self.comm.dist:
+                self.comm.allreduce_(self.nwk)
+                self.comm.allreduce_(self.nk[0])
         self._sync_aux_z()
         self.a = self.b = self.cn = 0
         self.sweeps_done = sweeps_done

@@ -581,7 +581,7 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
                 ldac.export_gibbs(ldac_dir, cur, prefix=f"{cur.sweeps_done:03d}")
             if burner is not None and burner.sweeps_done >= burn_mh:
                 # hand the chain to the MH model: same documents and tokens, another tiling
-                model.load_canonical_z(burner.canonical_z(), burner.sweeps_done)
+                model.load_canonical_z(burner.canonical_z(), burner.sweeps_done, counts_from=burner)
                 model.likelihoods = list(burner.likelihoods)
                 burner.close()
                 burner = dcorpus = None
