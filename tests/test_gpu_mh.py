@@ -23,10 +23,11 @@ def _toy(n_docs, V, seed):
     return torch.from_numpy(tdoc), torch.from_numpy(tword), keys
 
 
-@pytest.mark.parametrize("K", [7, 40, 100, 255])
-def test_alias_tables_bitwise(gpu, K):
+@pytest.mark.parametrize("K,V", [(7, 1000), (40, 1000), (100, 1000), (255, 1000), (40, 70001)])
+def test_alias_tables_bitwise(gpu, K, V):
+    """V ≥ 65536: the word records go out row by row, lanes along k (the large-vocabulary path)."""
     r = np.random.default_rng(K)
-    V, KS = 1000, (K + 3) // 4 * 4
+    KS = (K + 3) // 4 * 4
     q = np.zeros((V, KS), np.float32)
     q[:, :K] = (r.random((V, K)) ** 6 * 0.3 + 1e-6).astype(np.float32)
     q[3, :K] = 0.01  # a flat row
