@@ -376,6 +376,10 @@ def run_pipeline_mode(a, comm) -> dict:
         "setup_s": round(setup_s, 2),
         "allreduce_ms_per_sweep": model.allreduce_ms_per_sweep(),
         "allreduce_bytes_per_sweep": model.allreduce_bytes_per_sweep(),
+        # count magnitudes (the int32 tables' headroom) and the device memory high-water mark
+        "max_topic_share": round(float(model.nk_cur[:K].max()) / max(model.T_global, 1), 4),
+        "min_score_topN": float(res.scores[0]) if len(res.scores) else None,
+        "hbm_peak_gb": (round(torch.cuda.max_memory_allocated(dev) / 2**30, 2) if dev.type == "cuda" else None),
     }
 
 

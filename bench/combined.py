@@ -39,6 +39,13 @@ def main(argv=None) -> int:
     ap.add_argument("--mode", choices=["day", "sweep"], default="day")
     ap.add_argument("--sweeps", type=int, default=200, help="day mode: Gibbs sweeps per model per day")
     ap.add_argument("--maxresults", type=int, default=3000)
+    ap.add_argument("--flow-shards", type=int, default=1,
+                    help="day mode: build the flow day from this many weak-scaling shards generated in parallel "
+                         "processes (a 500M-flow / 1B-token flow model on one GPU)")
+    ap.add_argument("--gen-procs", type=int, default=8, help="worker processes of --flow-shards generation")
+    ap.add_argument("--realistic-vocab", action="store_true",
+                    help="day mode: long-tail vocabularies on every source (flow V ~ 1.7e5 per 12.5M flows; dns / "
+                         "proxy: half the rows from the long tail), as bench.py --realistic-vocab")
     a = ap.parse_args(argv)
     if a.mode == "day" and a.steps == 20 and a.warmup == 10:
         a.steps, a.warmup = 2, 1
@@ -161,15 +168,23 @@ def run_day_mode(a, comm, sync) -> dict:
         if per <= 0:
             continue
         n_total = per * world
-        if src == "flow":
+        wide = 0.5 if a.realistic_vocab else 0.0
+        if src == "flow" and a.flow_shards > 1:
+            from oni355.synth.flow import generate_flows_sharded
+            if world > 1 or per % a.flow_shards:
+                raise SystemExit("--flow-shards: one rank, flows divisible by the shard count")
+            day = generate_flows_sharded(per // a.flow_shards, a.flow_shards, seed=a.seed, n_hosts=max(64, n_total // 25),
+                                         procs=a.gen_procs, wide_vocab=a.realistic_vocab)
+        elif src == "flow":
             from oni355.synth.flow import generate_flows
-            day = generate_flows(per, seed=a.seed, rank=rank, n_hosts=max(64, n_total // 25))
+            day = generate_flows(per, seed=a.seed, rank=rank, n_hosts=max(64, n_total // 25),
+                                 wide_vocab=a.realistic_vocab)
         elif src == "dns":
             from oni355.synth.dns import generate_dns
-            day = generate_dns(per, seed=a.seed, rank=rank, n_clients=max(32, n_total // 40))
+            day = generate_dns(per, seed=a.seed, rank=rank, n_clients=max(32, n_total // 40), wide_vocab=wide)
         else:
             from oni355.synth.proxy import generate_proxy
-            day = generate_proxy(per, seed=a.seed, rank=rank, n_clients=max(32, n_total // 40))
+            day = generate_proxy(per, seed=a.seed, rank=rank, n_clients=max(32, n_total // 40), wide_vocab=wide)
         days.append((src, per, n_total, day))
         print(f"[combined] {src}: {per} events/rank generated at {time.perf_counter() - t0:.1f} s", file=sys.stderr,
               flush=True)
@@ -196,8 +211,16 @@ def run_day_mode(a, comm, sync) -> dict:
                 rio.write_rendered(os.path.join(tmp, f"{src}_results.csv"), schema.result_columns(src), rendered)
             sync()
             times[src] = time.perf_counter() - ts
+            m = res.lda.model
             stats[src] = {"train_dev_s": res.timings.get("train_dev_s", res.timings.get("train_s")),
                           "tokens": res.lda.corpus.T, "vocab": int(res.lda.vocab.numel()),
+                          "sampler": m.chain["sampler"], "mh_burn": m.chain["mh_burn"],
+                          "max_topic_share": round(float(m.nk_cur[: m.K].max()) / max(m.T_global, 1), 4),
+                          "max_word_tokens": int(m.nwk[:, : m.K].sum(1, dtype=torch.int64).max()),
+                          "posterior_sum_dtypes": ({k: str(m._avg[k].dtype) for k in ("wk", "k", "dk")}
+                                                   if m._avg is not None and m._avg["wk"] is not None else None),
+                          "min_score_topN": float(res.scores[0]) if len(res.scores) else None,
+                          "n_scores_nonpositive": int((np.asarray(res.scores) <= 0).sum()),
                           "rows": len(rendered), "loglik": res.stats.get("loglik"),
                           "planted_recall_topN": float(np.isin(day.anomaly_rows + rank * per,
                                                                res.rows[: a.maxresults]).mean())}
@@ -232,6 +255,7 @@ def run_day_mode(a, comm, sync) -> dict:
                    "events_per_gpu": {src: per for src, per, _, _ in days}, "parallelism": f"dp{world}",
                    "sweeps_per_model": a.sweeps, "maxresults": a.maxresults,
                    "baseline_config": "Combined flow+DNS+proxy 1B events, 100 topics, 8xMI355X (one GPU's share)"},
+        "realistic_vocab": a.realistic_vocab,
         "step": f"each source's whole day (H2D -> featurize -> corpus -> {a.sweeps} sweeps -> score -> "
                 f"top-{a.maxresults} -> CSV rows), source after source",
         "day_s_by_model": {k: round(v, 4) for k, v in times.items()},

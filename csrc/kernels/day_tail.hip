@@ -89,13 +89,16 @@ __global__ __launch_bounds__(kTailVals * 64) void k_tail_final(const double* __r
 // posterior counts are S times a document's length and pass 2^24 for heavy IPs) and rounds the
 // sum to f32 once, into LDS, then the block reads and writes its rows' KS columns
 // coalesced (a row per thread touched KS scattered words per lane).
-__global__ __launch_bounds__(256) void k_theta_rows(const int32_t* __restrict__ n, int64_t D, int K, int KS, float add,
+// Count type C: int32 for one sample's counts, int64 for the posterior-average sums (S samples of
+// counts up to 2^31 each: an int32 sum wraps once a count passes 2^31 / S).
+template <typename C>
+__global__ __launch_bounds__(256) void k_theta_rows(const C* __restrict__ n, int64_t D, int K, int KS, float add,
                                                     float den_add, float* __restrict__ th) {
   __shared__ float den[256];
   for (int64_t r0 = (int64_t)blockIdx.x * 256; r0 < D; r0 += (int64_t)gridDim.x * 256) {
     const int64_t d = r0 + threadIdx.x;
     if (d < D) {
-      const int32_t* r = n + d * KS;
+      const C* r = n + d * KS;
       int64_t nd = 0;
       for (int k = 0; k < K; ++k) nd += r[k];
       den[threadIdx.x] = (float)nd + den_add;
@@ -103,7 +106,7 @@ __global__ __launch_bounds__(256) void k_theta_rows(const int32_t* __restrict__ 
     __syncthreads();
     const int64_t rows = D - r0 < 256 ? D - r0 : 256;
     const int64_t cells = rows * KS;
-    const int32_t* src = n + r0 * KS;
+    const C* src = n + r0 * KS;
     float* dst = th + r0 * KS;
     for (int64_t i = threadIdx.x; i < cells; i += 256) {
       const int k = (int)(i % KS);
@@ -113,7 +116,8 @@ __global__ __launch_bounds__(256) void k_theta_rows(const int32_t* __restrict__ 
   }
 }
 
-__global__ __launch_bounds__(256) void k_phi_rows(const int32_t* __restrict__ nw, const int32_t* __restrict__ nk,
+template <typename C, typename CK>
+__global__ __launch_bounds__(256) void k_phi_rows(const C* __restrict__ nw, const CK* __restrict__ nk,
                                                   int64_t V, int K, int KS, float add, float vb,
                                                   float* __restrict__ ph) {
   __shared__ float den[256];
@@ -142,18 +146,33 @@ ONI_API int oni_tail_sums(const int32_t* nwk, const float* q, const int32_t* nk,
   return (int)hipGetLastError();
 }
 
-ONI_API int oni_theta_rows(const int32_t* n, int64_t D, int K, int KS, float add, float den_add, float* th,
+// csize: bytes per count (4: int32 tables, 8: int64 posterior-average sums)
+ONI_API int oni_theta_rows(const void* n, int64_t D, int K, int KS, float add, float den_add, float* th, int csize,
                            hipStream_t s) {
-  if (K < 1 || K > KS) return (int)hipErrorInvalidValue;
+  if (K < 1 || K > KS || (csize != 4 && csize != 8)) return (int)hipErrorInvalidValue;
   if (D <= 0) return 0;
-  k_theta_rows<<<oni::grid_for(D, 256, 2048), 256, 0, s>>>(n, D, K, KS, add, den_add, th);
+  const unsigned grid = oni::grid_for(D, 256, 2048);
+  if (csize == 8)
+    k_theta_rows<int64_t><<<grid, 256, 0, s>>>(static_cast<const int64_t*>(n), D, K, KS, add, den_add, th);
+  else
+    k_theta_rows<int32_t><<<grid, 256, 0, s>>>(static_cast<const int32_t*>(n), D, K, KS, add, den_add, th);
   return (int)hipGetLastError();
 }
 
-ONI_API int oni_phi_rows(const int32_t* nw, const int32_t* nk, int64_t V, int K, int KS, float add, float vb, float* ph,
-                         hipStream_t s) {
-  if (K < 1 || K > KS || KS > 256) return (int)hipErrorInvalidValue;
+// csize / ksize: bytes per count of nw / nk (4 or 8)
+ONI_API int oni_phi_rows(const void* nw, const void* nk, int64_t V, int K, int KS, float add, float vb, float* ph,
+                         int csize, int ksize, hipStream_t s) {
+  if (K < 1 || K > KS || KS > 256 || (csize != 4 && csize != 8) || (ksize != 4 && ksize != 8))
+    return (int)hipErrorInvalidValue;
   if (V <= 0) return 0;
-  k_phi_rows<<<oni::grid_for(V * KS, 256, 4096), 256, 0, s>>>(nw, nk, V, K, KS, add, vb, ph);
+  const unsigned grid = oni::grid_for(V * KS, 256, 4096);
+#define ONI_PHI(C, CK)                                                                                      \
+  k_phi_rows<C, CK><<<grid, 256, 0, s>>>(static_cast<const C*>(nw), static_cast<const CK*>(nk), V, K, KS, add, \
+                                         vb, ph)
+  if (csize == 8 && ksize == 8) ONI_PHI(int64_t, int64_t);
+  else if (csize == 8) ONI_PHI(int64_t, int32_t);
+  else if (ksize == 8) ONI_PHI(int32_t, int64_t);
+  else ONI_PHI(int32_t, int32_t);
+#undef ONI_PHI
   return (int)hipGetLastError();
 }

@@ -25,6 +25,23 @@
 
 namespace {
 
+// Posterior-average sums += four int32 counts at vector i: int64 sums where S samples of the
+// table's largest count could pass 2^31 (the host decides per table), else int32 (half the bytes).
+__device__ __forceinline__ void add_counts(void* __restrict__ base, int64_t i, const int4 v, int wide) {
+  if (wide) {
+    longlong2* q = reinterpret_cast<longlong2*>(static_cast<int64_t*>(base) + i * 4);
+    longlong2 a = q[0], b = q[1];
+    a.x += v.x; a.y += v.y; b.x += v.z; b.y += v.w;
+    q[0] = a;
+    q[1] = b;
+  } else {
+    int4* q = static_cast<int4*>(base) + i;
+    int4 a = *q;
+    a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    *q = a;
+  }
+}
+
 // Delta apply + q refresh: n_wk += Δ; n_k' = n_k + Δn_k; q = (n_wk+β)/(n_k'+Vβ); the token-exclusion
 // constants qfix = (A, B) with D = n_k' + Vβ, A = D/(D−1), B = 1/(D−1) (A = 1, B = 0 for empty
 // topics; see gibbs_sampler.h); zero the other delta buffer for the next sweep; bump the device
@@ -40,7 +57,9 @@ __global__ __launch_bounds__(256) void k_apply(int32_t* __restrict__ nwk, const 
                                                 int K, int KS, float beta, float vbeta, uint32_t* sweep_ctr,
                                                 int bump, int absolute, int nk_rep, const int32_t* __restrict__ rsrc,
                                                 int32_t* __restrict__ rdst, const int32_t* __restrict__ rows,
-                                                int64_t n_rows) {
+                                                int64_t n_rows, void* __restrict__ acc_wk, void* __restrict__ acc_k,
+                                                void* __restrict__ acc_dk, int acc_wide,
+                                                const int32_t* __restrict__ ndk_fin, int64_t D) {
   __shared__ float den[256];
   __shared__ int32_t nkn[256];
   __shared__ int32_t part[256];
@@ -74,6 +93,11 @@ __global__ __launch_bounds__(256) void k_apply(int32_t* __restrict__ nwk, const 
     }
     for (int k = threadIdx.x; k < nk_rep * KS + kDnAux; k += blockDim.x) dother[V * KS + k] = 0;
     if (threadIdx.x == 0 && bump) *sweep_ctr += 1u;
+    if (acc_k)
+      for (int k = threadIdx.x; k < KS; k += blockDim.x) {
+        if (acc_wide & 2) static_cast<int64_t*>(acc_k)[k] += nkn[k];
+        else static_cast<int32_t*>(acc_k)[k] += nkn[k];
+      }
   }
   const int64_t nvec = V * KS / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -86,6 +110,7 @@ __global__ __launch_bounds__(256) void k_apply(int32_t* __restrict__ nwk, const 
     }
     reinterpret_cast<int4*>(nwk)[i] = nv;
     reinterpret_cast<int4*>(dother)[i] = make_int4(0, 0, 0, 0);
+    if (acc_wk) add_counts(acc_wk, i, nv, acc_wide & 1);
     const int k0 = (int)((i * 4) % KS);
     float4 qo;
     qo.x = k0 + 0 < K ? ((float)nv.x + beta) / den[k0 + 0] : 0.f;
@@ -99,6 +124,11 @@ __global__ __launch_bounds__(256) void k_apply(int32_t* __restrict__ nwk, const 
     const int64_t r = rows[i / KS];
     const int k = (int)(i % KS);
     rdst[r * KS + k] = rsrc[r * KS + k];
+  }
+  if (acc_dk) {
+    const int64_t dvec = D * KS / 4;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < dvec; i += stride)
+      add_counts(acc_dk, i, reinterpret_cast<const int4*>(ndk_fin)[i], acc_wide & 4);
   }
 }
 
@@ -426,18 +456,27 @@ ONI_API int oni_gibbs_launch(const OniGibbs* a, int G, int KP, int init, int mod
 ONI_API int oni_gibbs_sizeof_args() { return (int)sizeof(OniGibbs); }
 
 // rsrc/rdst/rows/n_rows: optional fused long-row copy for the next sweep (n_rows = 0: none).
+// acc_wk/acc_k/acc_dk (all or none): the posterior-average sums ([V, KS], [KS], [D, KS]; int64 where
+// bit 0 / 1 / 2 of acc_wide is set, else int32) gain this sweep's n_wk, n_k and doc rows ndk_fin
+// [D, KS] -- the sample add in the same pass.
 ONI_API int oni_gibbs_apply(int32_t* nwk, const int32_t* dcur, int32_t* dother, const int32_t* nk_cur,
                             int32_t* nk_next, float* q, float* qfix, int64_t V, int K, int KS, float beta, float vbeta,
                             uint32_t* sweep_ctr, int bump, int absolute, int nk_rep, const int32_t* rsrc,
-                            int32_t* rdst, const int32_t* rows, int64_t n_rows, hipStream_t s) {
+                            int32_t* rdst, const int32_t* rows, int64_t n_rows, void* acc_wk, void* acc_k,
+                            void* acc_dk, int acc_wide, const int32_t* ndk_fin, int64_t D, hipStream_t s) {
   if (KS % 4 != 0 || KS > 256 || nk_rep < 1 || (nk_rep & (nk_rep - 1)) || qfix == nullptr)
     return (int)hipErrorInvalidValue;
   if (n_rows < 0 || (n_rows > 0 && (rsrc == nullptr || rdst == nullptr || rows == nullptr)))
     return (int)hipErrorInvalidValue;
-  const int64_t work = V * KS / 4 > n_rows * KS ? V * KS / 4 : n_rows * KS;
+  const bool acc = acc_wk != nullptr;
+  if (acc != (acc_k != nullptr) || acc != (acc_dk != nullptr) || (acc && (ndk_fin == nullptr || D < 0)))
+    return (int)hipErrorInvalidValue;
+  int64_t work = V * KS / 4 > n_rows * KS ? V * KS / 4 : n_rows * KS;
+  if (acc && D * KS / 4 > work) work = D * KS / 4;
   k_apply<<<oni::grid_for(work, 256, 2048), 256, 0, s>>>(nwk, dcur, dother, nk_cur, nk_next, q, qfix, V, K, KS, beta,
                                                           vbeta, sweep_ctr, bump, absolute, nk_rep, rsrc, rdst, rows,
-                                                          n_rows);
+                                                          n_rows, acc_wk, acc_k, acc ? acc_dk : nullptr, acc_wide,
+                                                          ndk_fin, acc ? D : 0);
   return (int)hipGetLastError();
 }
 

@@ -29,6 +29,9 @@ from .corpus import Corpus, canonical_tokens
 
 
 NK_REP = 32
+# largest global token count a model takes: every int32 count (n_wk, n_k, n_dk, Δ) is ≤ the token
+# count, and the Δn_k replicas hold partial sums of it
+INT32_COUNT_MAX = 2**31 - 1
 # X01 payload packing pays only once the all-reduce is bandwidth-bound (see GibbsLDA._x01_wanted)
 X01_PACK_MIN_BYTES = 4 << 20
 # sweep kernels (-> oni_gibbs_launch variant argument): every one draws the same topics bit for bit
@@ -244,6 +247,9 @@ class GibbsLDA:
             self._air = _alpha_in_row_exact(self.alpha, corpus.max_doc_len())
             if not self._air:
                 self.qpf = SAMPLERS["generic"]
+        # the Markov chain this model runs (checkpoint identity): the dense kernels are bitwise
+        # one chain; MH is another, and its pipeline sets the dense burn-in it starts from
+        self.chain = {"sampler": "mh" if self.mh else "dense", "mh_burn": 0}
         self.a = 0  # ndk parity
         self.b = 0  # delta-buffer parity
         self.cn = 0  # nk parity
@@ -388,12 +394,21 @@ class GibbsLDA:
         # world 1: every token holds one topic, so Σ n_k = T (no device read); DP: the global sum
         self.T_global = (int(self.nk[0][: self.K].sum()) if self.comm is not None and self.comm.dist
                          else int(self.c.T))
+        self._check_magnitude()
         self._delta_on = False
         self._chg_q = []
         self._sync_aux_z()
         self.sweeps_done = 0
         self._graph = None
         self._prime()
+
+    def _check_magnitude(self) -> None:
+        """Every count table (n_wk, n_k, n_dk, the Δ buffers) is int32 and bounded by the global
+        token count: refuse a model whose tokens (feedback duplicates included) could wrap one,
+        instead of sampling from garbage. The posterior-average sums are int64."""
+        if self.T_global > INT32_COUNT_MAX or self.c.T > INT32_COUNT_MAX:
+            raise ValueError(f"{self.T_global} global tokens: int32 count tables hold at most {INT32_COUNT_MAX} "
+                             "(split the day or the source into several models)")
 
     # ---- split documents: one n_dk row per document across its pieces ---------------------------
     def _split_sync_absolute(self, ndk: torch.Tensor) -> None:
@@ -539,14 +554,16 @@ class GibbsLDA:
         if self._split is not None:
             self._split_apply(self.dn[self.b], self.ndk[self.a], self.ndk[1 - self.a])
         so = self._split_off
+        # inside a contiguous averaging window the sample sums gain this sweep's counts in the
+        # same launch (int64: no extra pass over n_wk, no separate adds)
+        acc = ((self._avg["wk"], self._avg["k"], self._avg["dk"], self.ndk[1 - self.a]) if self._acc else None)
         ops.gibbs_apply(self.nwk, self.dn[self.b][:so], self.dn[1 - self.b][:so], self.nk[self.cn], self.nk[1 - self.cn],
                         self.q, self.qfix, self.V, self.K, self.KS, self.beta, self.vbeta, self.sweep_ctr, bump=True,
-                        absolute=mode in (0, 3), rows_copy=(self.ndk[1 - self.a], self.ndk[self.a], c.long_rows))
+                        absolute=mode in (0, 3), rows_copy=(self.ndk[1 - self.a], self.ndk[self.a], c.long_rows),
+                        acc=acc)
         self.a, self.b, self.cn = 1 - self.a, 1 - self.b, 1 - self.cn
         self.sweeps_done += 1
         self._tail_cache = None
-        if self._acc:
-            self._accumulate()
         if not self._capturing:
             self._zw_synced = mode == 3
 
@@ -661,6 +678,7 @@ class GibbsLDA:
                 contiguous = self._avg is not None and int(self.cfg.post_every) == 1
                 if nxt and contiguous and self.sweeps_done + 1 >= nxt[0]:
                     # inside a contiguous window: every sweep adds its sample, in the graph
+                    self._ensure_avg()
                     seg = min(n, self._avg_at[-1] - self.sweeps_done)
                     self._acc = True
                     try:
@@ -796,12 +814,30 @@ class GibbsLDA:
         self._avg_at = sorted(at) if S > 1 else []
         self._avg_cache = None
         dev = self.device
-        if self._avg_at:
-            self._avg = dict(n=0, wk=torch.zeros_like(self.nwk), k=torch.zeros_like(self.nk[0]),
-                             dk=torch.zeros_like(self.ndk[0]))
-        else:
-            self._avg = None
+        # the sums are allocated at the first sample (_ensure_avg), when the counts they bound exist
+        self._avg = dict(n=0, wk=None, k=None, dk=None) if self._avg_at else None
         _ = dev
+
+    def _ensure_avg(self) -> None:
+        """Allocate the sample sums. S samples of an int32 count wrap an int32 sum once the count
+        passes 2^31 / S (43M at S = 50: one topic's share of a config-4/5 corpus), so each table is
+        int64 when S times its largest possible entry could pass 2^31 -- n_k: the global token
+        count; n_wk: the largest global word count; n_dk: the longest document row -- and int32
+        otherwise (the default day: half the bytes in k_apply's fused add). ONI_POST_WIDE=1 forces
+        int64."""
+        a = self._avg
+        if a is None or a["wk"] is not None:
+            return
+        S, K, dev = len(self._avg_at), self.K, self.device
+        force = os.environ.get("ONI_POST_WIDE", "0") == "1"
+        wk_max = int(self.nwk[:, :K].sum(1, dtype=torch.int64).max()) if self.nwk.shape[0] else 0
+        dk_max = int(self.ndk_cur[:, :K].sum(1, dtype=torch.int64).max()) if self.c.D else 0
+
+        def dt(bound: int):
+            return torch.int64 if force or bound * S > INT32_COUNT_MAX else torch.int32
+        a["wk"] = torch.zeros(self.nwk.shape, dtype=dt(wk_max), device=dev)
+        a["k"] = torch.zeros(self.nk[0].shape, dtype=dt(max(self.T_global, int(self.nk_cur[:K].max()))), device=dev)
+        a["dk"] = torch.zeros(self.ndk[0].shape, dtype=dt(dk_max), device=dev)
 
     @property
     def average_window(self) -> tuple[int, int] | None:
@@ -809,26 +845,36 @@ class GibbsLDA:
         return (self._avg_at[0], self._avg_at[-1]) if self._avg_at else None
 
     def average_state(self) -> dict | None:
-        """The accumulated samples (for a checkpoint), or None outside an averaging window."""
+        """The accumulated samples (for a checkpoint; the K real topics only, so the state does
+        not depend on the kernel tiling's padding), or None outside an averaging window."""
         a = self._avg
         if a is None or a["n"] == 0:
             return None
-        return {"n": int(a["n"]), "wk": a["wk"].cpu(), "k": a["k"].cpu(), "dk": a["dk"].cpu()}
+        K = self.K
+        return {"n": int(a["n"]), "wk": a["wk"][:, :K].cpu().to(torch.int64), "k": a["k"][:K].cpu().to(torch.int64),
+                "dk": a["dk"][:, :K].cpu().to(torch.int64)}
 
     def load_average_state(self, st: dict) -> None:
-        """Restore :meth:`average_state` (same corpus layout) after a resume inside the window."""
+        """Restore :meth:`average_state` (same documents and vocabulary) after a resume inside the
+        window."""
         a = self._avg
         if a is None:
             raise ValueError("checkpoint holds posterior-averaging samples but no average is planned")
+        self._ensure_avg()
+        K = self.K
         for k in ("wk", "k", "dk"):
-            if tuple(st[k].shape) != tuple(a[k].shape):
-                raise ValueError(f"averaging state {k} shape {tuple(st[k].shape)} != {tuple(a[k].shape)}")
-            a[k].copy_(st[k].to(a[k].device))
+            want = (a[k].shape[0], K) if a[k].dim() == 2 else (K,)
+            if tuple(st[k].shape) != want:
+                raise ValueError(f"averaging state {k} shape {tuple(st[k].shape)} != {want}")
+            a[k].zero_()
+            a[k][..., :K].copy_(st[k].to(a[k].device))
         a["n"] = int(st["n"])
         self._avg_cache = None
 
     def _accumulate(self) -> None:
-        """Add the current counts to the sample sums (device ops only: capturable)."""
+        """Add the current counts to the (int64) sample sums: samples taken every post_every > 1
+        sweeps, outside the graphs (contiguous windows add inside k_apply)."""
+        self._ensure_avg()
         a = self._avg
         a["wk"] += self.nwk
         a["k"] += self.nk_cur
@@ -977,6 +1023,7 @@ class GibbsLDA:
         self.a = self.b = self.cn = 0
         self.sweeps_done = sweeps_done
         self.T_global = int(self.nk[0][: self.K].sum())
+        self._check_magnitude()
         self._delta_on = False
         self._chg_q = []
         self._graph = None

@@ -574,13 +574,21 @@ STREAM_RECOUNT = True  # k_recount_reg (register runs) 0.065 ms vs k_recount (LD
 
 
 def gibbs_apply(nwk, dcur, dother, nk_cur, nk_next, q, qfix, V, K, KS, beta, vbeta, sweep_ctr, bump=True,
-                absolute=False, rows_copy=None):
+                absolute=False, rows_copy=None, acc=None):
     """n_wk ← Δ (or absolute), n_k ← n_k + Σ_replicas Δn_k, q refresh (+ the token-exclusion
     table ``qfix`` [2, KS]); zeroes ``dother``.
 
     ``dcur``/``dother`` are [V·KS + R·KS + DN_AUX]: the Δn_wk table, R replicas of Δn_k, then
     DN_AUX auxiliary words ([0] = tokens that changed topic; all-reduced with the rest).
-    ``rows_copy = (src, dst, rows)``: also :func:`copy_rows` in the same launch."""
+    ``rows_copy = (src, dst, rows)``: also :func:`copy_rows` in the same launch.
+    ``acc = (wk, k, dk, ndk)``: the posterior-average sums [V, KS], [KS], [D, KS] (each int32 or
+    int64) also gain the new n_wk, n_k and the doc rows ``ndk`` [D, KS] (int32) in the same launch."""
+    if acc is not None:
+        wk, kk, dk, ndk = acc
+        if (any(t.dtype not in (torch.int32, torch.int64) for t in (wk, kk, dk))
+                or tuple(wk.shape) != (V, KS) or kk.numel() != KS or tuple(dk.shape) != tuple(ndk.shape)
+                or ndk.dtype != torch.int32 or ndk.shape[-1] != KS):
+            raise ValueError("posterior sums must be int32/int64 [V, KS], [KS], [D, KS] over int32 [D, KS] doc rows")
     nk_rep = (dcur.numel() - V * KS - DN_AUX) // KS
     if nk_rep < 1 or V * KS + nk_rep * KS + DN_AUX != dcur.numel():
         raise ValueError("Δ buffer must be [V*KS + nk_rep*KS + DN_AUX]")
@@ -600,13 +608,23 @@ def gibbs_apply(nwk, dcur, dother, nk_cur, nk_next, q, qfix, V, K, KS, beta, vbe
             sweep_ctr += 1
         if rows_copy is not None:
             copy_rows(*rows_copy, KS)
+        if acc is not None:
+            wk += nwk
+            kk += nk_next
+            dk += ndk
         return
     rs, rd, rr = rows_copy if rows_copy is not None and rows_copy[2].numel() else (None, None, None)
+    aw = ak = ad = an = None
+    wide = 0
+    if acc is not None:
+        aw, ak, ad, an = (_lib.ptr(t) for t in acc)
+        wide = sum(b for b, t in ((1, acc[0]), (2, acc[1]), (4, acc[2])) if t.dtype == torch.int64)
     _lib.check(_lib.lib().oni_gibbs_apply(*map(_lib.ptr, (nwk, dcur, dother, nk_cur, nk_next, q, qfix)), V, K, KS,
                                           float(beta), float(vbeta), _lib.ptr(sweep_ctr), 1 if bump else 0,
                                           1 if absolute else 0, nk_rep, _lib.ptr(rs) if rs is not None else None,
                                           _lib.ptr(rd) if rd is not None else None,
                                           _lib.ptr(rr) if rr is not None else None, rr.numel() if rr is not None else 0,
+                                          aw, ak, ad, wide, an, acc[3].shape[0] if acc is not None else 0,
                                           _lib.stream()), "oni_gibbs_apply")
 
 
@@ -810,19 +828,28 @@ def tail_sums(nwk: torch.Tensor, q: torch.Tensor, nk: torch.Tensor, ndk: torch.T
     return out
 
 
+def _count_size(t: torch.Tensor) -> int:
+    if t.dtype not in (torch.int32, torch.int64):
+        raise ValueError("count tables must be int32 or int64")
+    return t.element_size()
+
+
 def theta_rows(n: torch.Tensor, K: int, add: float, den_add: float) -> torch.Tensor:
-    """θ = (n + add) / (n_d + den_add) in f32 per row (k_theta_rows), zero past K."""
+    """θ = (n + add) / (n_d + den_add) in f32 per row (k_theta_rows), zero past K. ``n`` is an
+    int32 count table or the int64 posterior-average sums."""
     D, KS = n.shape
     out = torch.empty(D, KS, dtype=torch.float32, device=n.device)
     _lib.check(_lib.lib().oni_theta_rows(_lib.ptr(n), D, int(K), KS, float(np.float32(add)), float(np.float32(den_add)),
-                                         _lib.ptr(out), _lib.stream()), "oni_theta_rows")
+                                         _lib.ptr(out), _count_size(n), _lib.stream()), "oni_theta_rows")
     return out
 
 
 def phi_rows(nw: torch.Tensor, nk: torch.Tensor, K: int, add: float, vb: float) -> torch.Tensor:
-    """φ = (n_wk + add) / (n_k + vb) in f32 (k_phi_rows), zero past K."""
+    """φ = (n_wk + add) / (n_k + vb) in f32 (k_phi_rows), zero past K; int32 or int64 counts."""
     V, KS = nw.shape
     out = torch.empty(V, KS, dtype=torch.float32, device=nw.device)
     _lib.check(_lib.lib().oni_phi_rows(_lib.ptr(nw), _lib.ptr(nk), V, int(K), KS, float(np.float32(add)),
-                                       float(np.float32(vb)), _lib.ptr(out), _lib.stream()), "oni_phi_rows")
+                                       float(np.float32(vb)), _lib.ptr(out), _count_size(nw), _count_size(nk),
+                                       _lib.stream()),
+               "oni_phi_rows")
     return out

@@ -66,10 +66,10 @@ _SIGS = {
     "oni_tail_grid": [],
     "oni_tail_sums": [vp, vp, vp, vp, i64, i64, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double, C.c_double,
                       vp, vp, vp],
-    "oni_theta_rows": [vp, i64, C.c_int, C.c_int, f32, f32, vp, vp],
-    "oni_phi_rows": [vp, vp, i64, C.c_int, C.c_int, f32, f32, vp, vp],
+    "oni_theta_rows": [vp, i64, C.c_int, C.c_int, f32, f32, vp, C.c_int, vp],
+    "oni_phi_rows": [vp, vp, i64, C.c_int, C.c_int, f32, f32, vp, C.c_int, C.c_int, vp],
     "oni_gibbs_apply": [vp, vp, vp, vp, vp, vp, vp, i64, C.c_int, C.c_int, f32, f32, vp, C.c_int, C.c_int, C.c_int,
-                        vp, vp, vp, i64, vp],
+                        vp, vp, vp, i64, vp, vp, vp, C.c_int, vp, i64, vp],
     "oni_recount": [vp, vp, vp, i64, vp, C.c_int, C.c_int, C.c_int, vp],
     "oni_recount_stream": [vp, vp, i64, vp, C.c_int, C.c_int, C.c_int, vp],
     "oni_delta_recount": [vp, vp, vp, vp, vp, vp, vp, i64, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp],

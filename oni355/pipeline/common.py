@@ -503,6 +503,13 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
                 T_glob = comm.allreduce_scalar(T_glob, "sum")
             # the MH sampler's u8 LDS cells hold a chunk's count deltas: chunks ≤ 127 tokens
             chunk_len = auto_chunk_len(int(T_glob), G, hi=spec.MH_MAX_CHUNK if mh else 128)
+        elif mh and chunk_len > spec.MH_MAX_CHUNK:
+            # an explicit CHUNK_LEN (valid up to 128 for the dense kernels) above the MH sampler's
+            # limit: clamp rather than fail the day
+            if log:
+                log(f"chunk_len {chunk_len} -> {spec.MH_MAX_CHUNK}: the MH sampler's chunks hold at most "
+                    f"{spec.MH_MAX_CHUNK} tokens")
+            chunk_len = spec.MH_MAX_CHUNK
         udoc, inv, wi, wt, route = route_to_owners(doc_keys64, word_ids, weights, comm,
                                                    split_L=chunk_len if dist_on else 0)
         D, V = int(udoc.numel()), int(vocab.numel())
@@ -543,9 +550,12 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
         burner = None  # the dense model of an MH model's first burn_mh sweeps
         if burn_mh <= 0:
             dcorpus = None
+        if mh:
+            model.chain["mh_burn"] = burn_mh if dcorpus is not None else 0
         if dcorpus is not None and not (ckpt is not None and ckpt.exists() and ckpt.manifest()["sweep"] >= burn_mh):
             burner = GibbsLDA(dcorpus, GibbsConfig(K=K, alpha=alpha, beta=beta, seed=seed, sampler="dense"),
                               comm=comm, V_global=int(vocab.numel()))
+            burner.chain = model.chain  # its checkpoints belong to the MH run
         first = burner or model
         if ckpt is not None and ckpt.exists():
             ckpt.restore(first)

@@ -314,3 +314,60 @@ def generate_flows(n: int, seed: int = 7, n_hosts: int | None = None, n_profiles
             cols[k6] = StringColumn.from_list(txt)
             cols[k4] = np.where(v6_rows, 0, cols[k4]).astype(np.uint32)
     return FlowDay(cols=cols, theta_true=theta, host_ips=host_ips, anomaly_rows=anomaly_rows)
+
+
+def generate_flows_sharded(per: int, parts: int, seed: int = 7, n_hosts: int | None = None, procs: int = 8,
+                           **kw) -> FlowDay:
+    """The ``parts`` weak-scaling shards (rank 0..parts-1, ``per`` flows each, one host population)
+    of a ``per·parts``-flow day concatenated into ONE day -- e.g. all of a 1B-token day on one GPU
+    -- generated by ``procs`` forked workers writing straight into shared-memory columns (a 500M-flow
+    day is ~68 GB of columns and ~10 min of single-process generation). Row ids of the planted
+    anomalies are offset by their shard's position."""
+    import multiprocessing as mp
+    from multiprocessing import shared_memory
+
+    if n_hosts is None:
+        n_hosts = max(64, per * parts // 25)
+    probe = generate_flows(min(per, 1000), seed=seed, n_hosts=n_hosts, rank=0, **kw)
+    if any(not isinstance(v, np.ndarray) for v in probe.cols.values()):
+        raise ValueError("sharded generation supports numeric columns only (no IPv6 text columns)")
+    n = per * parts
+    shm = {k: shared_memory.SharedMemory(create=True, size=max(1, n * v.dtype.itemsize))
+           for k, v in probe.cols.items()}
+    spec_ = {k: (s.name, probe.cols[k].dtype.str) for k, s in shm.items()}
+    ctx = mp.get_context("fork")
+
+    def work(r: int, q) -> None:
+        d = generate_flows(per, seed=seed, n_hosts=n_hosts, rank=r, **kw)
+        for k, (name, dt) in spec_.items():
+            s = shared_memory.SharedMemory(name=name)
+            np.ndarray((n,), dtype=np.dtype(dt), buffer=s.buf)[r * per:(r + 1) * per] = d.cols[k]
+            s.close()
+        q.put((r, d.anomaly_rows + r * per))
+
+    q = ctx.Queue()
+    anomalies = {}
+    pending = list(range(parts))
+    running: dict = {}
+    try:
+        while pending or running:
+            while pending and len(running) < max(1, procs):
+                r = pending.pop(0)
+                running[r] = ctx.Process(target=work, args=(r, q))
+                running[r].start()
+            r, rows = q.get(timeout=3600)
+            anomalies[r] = rows
+            running.pop(r).join()
+    finally:
+        for p in running.values():
+            p.terminate()
+            p.join()
+    cols = {}
+    for k, s in shm.items():
+        # own copy in this process's memory (plain numpy: pinning and the columnar store expect it),
+        # then release the shared segment
+        cols[k] = np.ndarray((n,), dtype=np.dtype(spec_[k][1]), buffer=s.buf).copy()
+        s.close()
+        s.unlink()
+    return FlowDay(cols=cols, theta_true=probe.theta_true, host_ips=probe.host_ips,
+                   anomaly_rows=np.concatenate([anomalies[r] for r in range(parts)]))

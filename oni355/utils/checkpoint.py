@@ -36,7 +36,14 @@ class Checkpointer:
         return self.comm.world if self.comm else 1
 
     def _ident(self, model) -> dict:
-        return {"K": model.K, "alpha": model.alpha, "beta": model.beta, "seed": int(model.cfg.seed), "V": model.V}
+        """What the chain is a function of: a checkpoint resumes only a run of the same identity.
+        ``chain`` names the sampler family and, for MH runs, the dense burn-in length (the MH
+        chain and the dense chain are different Markov chains over the same z)."""
+        ident = {"K": model.K, "alpha": model.alpha, "beta": model.beta, "seed": int(model.cfg.seed), "V": model.V}
+        chain = getattr(model, "chain", None)
+        if chain is not None:
+            ident["chain"] = dict(chain)
+        return ident
 
     def manifest(self) -> dict | None:
         p = os.path.join(self.dir, "manifest.json")
@@ -103,7 +110,8 @@ class Checkpointer:
         if man is None:
             raise FileNotFoundError(f"no checkpoint manifest in {self.dir}")
         if man["ident"] != self._ident(model):
-            raise ValueError(f"checkpoint identity {man['ident']} != run {self._ident(model)}")
+            raise ValueError(f"checkpoint identity {man['ident']} != run {self._ident(model)} (a checkpoint resumes "
+                             "only the chain that wrote it: same K, α, β, seed, vocabulary, sampler and MH burn-in)")
         sweep = int(man["sweep"])
         c = model.c
         mask = 0xFFFFFFFF

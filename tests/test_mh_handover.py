@@ -51,3 +51,19 @@ def test_handover_copy_equals_recount(K):
 def test_handover_copy_equals_recount_gpu(gpu, K):
     # 12 dense sweeps: the auto count mode has left "recount" for a delta mode by then
     _handover(gpu, K, 12, 3)
+
+
+def test_explicit_chunk_len_128_clamped_for_mh():
+    """CHUNK_LEN = 128 is valid for the dense kernels; a K = 100 (MH) day clamps it to the MH limit
+    instead of failing."""
+    from oni355.pipeline.common import build_and_train
+    from oni355.ref import spec
+    tdoc, tword, keys = _toy(120, 90, 3)
+    doc_keys = keys.to(torch.int64)[tdoc.long()]
+    vocab = torch.arange(90, dtype=torch.int64)
+    msgs = []
+    run = build_and_train(doc_keys, vocab[tword.long()], None, vocab, 100, None, 0.01, 5, 6, 128, None,
+                          log=msgs.append)
+    assert run.corpus.L <= spec.MH_MAX_CHUNK and run.model.mh
+    assert any("MH sampler" in m for m in msgs)
+    assert run.model.chain == {"sampler": "mh", "mh_burn": 6}
