@@ -43,6 +43,9 @@ def main(argv=None) -> int:
                     help="day mode: build the flow day from this many weak-scaling shards generated in parallel "
                          "processes (a 500M-flow / 1B-token flow model on one GPU)")
     ap.add_argument("--gen-procs", type=int, default=8, help="worker processes of --flow-shards generation")
+    ap.add_argument("--recall-at", default="",
+                    help="day mode: also report planted recall in the top N for these N (comma-separated, each "
+                         "≤ --maxresults; e.g. the 1B-token day plants 200 anomalies per 62.5M-flow shard)")
     ap.add_argument("--realistic-vocab", action="store_true",
                     help="day mode: long-tail vocabularies on every source (flow V ~ 1.7e5 per 12.5M flows; dns / "
                          "proxy: half the rows from the long tail), as bench.py --realistic-vocab")
@@ -224,6 +227,11 @@ def run_day_mode(a, comm, sync) -> dict:
                           "rows": len(rendered), "loglik": res.stats.get("loglik"),
                           "planted_recall_topN": float(np.isin(day.anomaly_rows + rank * per,
                                                                res.rows[: a.maxresults]).mean())}
+            if a.recall_at:
+                pl = day.anomaly_rows + rank * per
+                stats[src]["planted_recall_at"] = {n: round(float(np.isin(pl, res.rows[:int(n)]).mean()), 4)
+                                                   for n in a.recall_at.split(",")}
+                stats[src]["planted"] = int(pl.size)
             del res
             print(f"[combined] {src} day {times[src]:.3f} s", file=sys.stderr, flush=True)
         return times, stats

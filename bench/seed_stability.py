@@ -48,18 +48,42 @@ def main() -> int:
             torch.cuda.synchronize()
             times.append(time.perf_counter() - t0)
             deep = np.asarray(res.rows)
-            tops.append((set(deep[: a.maxresults].tolist()), set(deep.tolist()), np.asarray(res.scores)))
+            tops.append((set(deep[: a.maxresults].tolist()), set(deep.tolist()), np.asarray(res.scores), deep))
             rows = tops[-1][0]
             rec.append(len(rows & planted) / max(len(planted), 1))
         ov = [len(x[0] & y[0]) / a.maxresults for x, y in itertools.combinations(tops, 2)]
         # boundary jitter: how much of one seed's top-N is inside another seed's top-(deep·N)
         ovd = [len(x[0] & y[1]) / a.maxresults for x, y in itertools.permutations(tops, 2)]
+        # where do the rows that leave the top-N go, and how much does one row's score move between
+        # seeds? (the cut falls in a smooth score density: rows near it trade places with the
+        # posterior estimate's seed-to-seed noise, not with exact ties)
+        anat = []
+        for x, y in itertools.permutations(tops, 2):
+            ry = {int(r): i for i, r in enumerate(y[3])}
+            sy = y[2]
+            lost = [int(r) for r in x[3][: a.maxresults] if int(r) not in y[0]]
+            lost_rank = np.array([ry.get(r, len(y[3])) for r in lost]) + 1
+            both = [(i, ry[int(r)]) for i, r in enumerate(x[3]) if int(r) in ry]
+            lr = np.abs(np.log(np.array([x[2][i] / sy[j] for i, j in both])))
+            near = [i for i, j in both if i < a.maxresults]
+            lr_top = np.abs(np.log(np.array([x[2][i] / sy[ry[int(x[3][i])]] for i in near])))
+            anat.append({"lost": len(lost), "lost_rank_in_other_median": int(np.median(lost_rank)) if lost else None,
+                         "lost_rank_in_other_p90": int(np.percentile(lost_rank, 90)) if lost else None,
+                         "lost_beyond_deep": int((lost_rank > len(y[3])).sum()),
+                         "score_abs_log_ratio_median_topN": round(float(np.median(lr_top)), 4),
+                         "score_abs_log_ratio_median_deep": round(float(np.median(lr)), 4)})
         sc = tops[0][2]
+        # rank distance that the median seed-to-seed score change spans at the cut
+        med = float(np.median([v["score_abs_log_ratio_median_topN"] for v in anat]))
+        cut = sc[a.maxresults - 1]
+        lo, hi = np.searchsorted(sc, cut * np.exp(-med)), np.searchsorted(sc, cut * np.exp(med))
         margin = {"score_at_N": float(sc[a.maxresults - 1]), "score_at_N_over_2": float(sc[a.maxresults // 2]),
                   "score_at_deep": float(sc[-1]), "rows_within_1pct_of_score_at_N":
                   int(((sc >= sc[a.maxresults - 1] * 0.99) & (sc <= sc[a.maxresults - 1] * 1.01)).sum())}
         out["days"][kind] = {"topN_overlap_mean": round(float(np.mean(ov)), 4), "topN_overlap_pairs": [round(v, 4) for v in ov],
                              f"topN_within_top{a.deep}N_mean": round(float(np.mean(ovd)), 4), "margin_seed0": margin,
+                             "boundary_anatomy": anat,
+                             "ranks_spanned_by_median_score_noise_at_N": [int(lo) + 1, int(hi) + 1],
                              "recall": [round(r, 4) for r in rec], "day_s": [round(t, 4) for t in times],
                              "vocab": int(res.stats.get("V", 0)), "loglik": float(res.stats["loglik"])}
         print(json.dumps({kind: out["days"][kind]}), file=sys.stderr, flush=True)

@@ -286,7 +286,7 @@ class GibbsLDA:
         if rows.numel():
             dslot[multi] = torch.searchsorted(rows, c.chunk_doc[multi].to(torch.int64)).to(torch.int32)
         self.chunk_dslot = dslot
-        self.walias = torch.zeros(self.V, self.K, 4, dtype=torch.int32, device=dev)  # 16-B records
+        self.walias = torch.zeros(self.V, self.K, dtype=torch.int32, device=dev)  # u32 alias entries
         self.wsum = torch.zeros(self.V, dtype=torch.float32, device=dev)
         self.dalias = torch.zeros(max(int(rows.numel()), 1), self.K, dtype=torch.int32, device=dev)
         self.mh_g = torch.zeros(self.KS, dtype=torch.float32, device=dev)
@@ -579,13 +579,18 @@ class GibbsLDA:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record()
         x = self._x01
+        # a forced 1-rank group (ONI_FORCE_DIST=1: every data-parallel code path on one GPU) keeps
+        # the pack / unpack but drops the collective itself -- the sum over one rank is the identity,
+        # and the RCCL node would be the only difference to world 1 in the captured sweep
+        reduce = self.comm.world > 1
         if x is not None:
             ops.x01_pack(buf, x["tiny"], x["light"], x["heavy"], self.KS, x["tail_off"], x["tail_len"], x["O8"], x["O"],
                          x["buf"])
-            self.comm.allreduce_(x["buf"])
+            if reduce:
+                self.comm.allreduce_(x["buf"])
             ops.x01_unpack(x["buf"], x["tiny"], x["light"], x["heavy"], self.KS, x["tail_off"], x["tail_len"], x["WO8"],
                            x["WO"], buf)
-        else:
+        elif reduce:
             self.comm.allreduce_(buf)
         if timed:
             e1 = torch.cuda.Event(enable_timing=True)

@@ -477,8 +477,8 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
 def mh_tables(q: torch.Tensor, nk: torch.Tensor, ndk_src: torch.Tensor, long_rows: torch.Tensor, K: int,
               alpha: float, vbeta: float, walias: torch.Tensor, wsum: torch.Tensor, dalias: torch.Tensor,
               g: torch.Tensor) -> None:
-    """Per-sweep tables of the MH sampler (k_mh_alias, spec.mh_tables): ``walias`` [V, K, 4] := the
-    alias records {entry, q_j, q_alias, Σ q} of every word's q row and ``wsum`` [V] its sum, ``dalias`` [n_long, K] := that of
+    """Per-sweep tables of the MH sampler (k_mh_alias, spec.mh_tables): ``walias`` [V, K] := the
+    alias entries of every word's q row and ``wsum`` [V] its sum, ``dalias`` [n_long, K] := that of
     n_dk + α for every document over several chunks (rows ``long_rows`` of ``ndk_src``),
     ``g`` [KS] := 1/(n_k + Vβ + 1) of the snapshot's topic totals ``nk``. int32 tensors hold the u32
     entries."""

@@ -480,14 +480,9 @@ def mh_tables(q: np.ndarray, nk: np.ndarray, ndk_src: np.ndarray, long_rows: np.
     """Per-sweep tables of the MH sampler (k_mh_alias): the word proposal ∝ q[w, k] (sweep-start
     word factor) of every word with its row sum, the doc proposal ∝ n_dk + α (sweep-start row) of
     every document over several chunks, and g_k = 1/(n_k + Vβ + 1) (the word factor a token adds
-    to a topic it moves into). Word rows are records {entry, q_j, q_alias(j), Σ_k q_k} (the
-    kernel's 16-B gather). Returns (walias [V, K, 4] u32, wsum [V] f32, dalias [n_long, K] u32,
+    to a topic it moves into). Returns (walias [V, K] u32 entries, wsum [V] f32, dalias [n_long, K] u32,
     g [KS] f32)."""
-    ent, wsum = alias_table(q[:, :K])
-    q32 = np.ascontiguousarray(q[:, :K], dtype=F32)
-    al = (ent & U32(0xFF)).astype(np.int64)
-    walias = np.stack([ent, q32.view(U32), np.take_along_axis(q32, al, axis=1).view(U32),
-                       np.repeat(wsum[:, None], K, axis=1).astype(F32).view(U32)], axis=2).astype(U32)
+    walias, wsum = alias_table(q[:, :K])
     b = ndk_src[np.asarray(long_rows, dtype=np.int64), :K].astype(F32) + F32(alpha)
     dalias = alias_table(b)[0] if b.shape[0] else np.zeros((0, K), dtype=U32)
     g = (F32(1) / ((nk.astype(F32) + F32(vbeta)).astype(F32) + F32(1))).astype(F32)
@@ -581,7 +576,7 @@ def gibbs_pass_mh(st: dict, KS: int, K: int, alpha: float, seed0: int, seed1: in
       zo from x ≠ zo is kept with probability (b_zo^¬ + α)/(b_zo + α) first.
 
     A move is taken when u(r)·den < num (f32). st as for :func:`gibbs_pass` plus ``walias``
-    [V, K, 4] u32 records, ``wsum`` [V] f32, ``dalias`` [n_long, K] u32, ``mh_g`` [KS] f32 (:func:`mh_tables`)
+    [V, K] u32 alias entries, ``wsum`` [V] f32, ``dalias`` [n_long, K] u32, ``mh_g`` [KS] f32 (:func:`mh_tables`)
     and ``chunk_dslot`` [C] i32 (row of dalias of a multi-chunk doc's chunk, −1 otherwise)."""
     S = 64
     slc, lane = _chunk_geometry(st, S)
@@ -613,7 +608,7 @@ def gibbs_pass_mh(st: dict, KS: int, K: int, alpha: float, seed0: int, seed1: in
         zp = np.minimum(np.arange(int(clen[act].max()))[None, :], clen[act][:, None] - 1)
         zslice = st["tok_z"][base[act][:, None] + zp * S].astype(np.int64)
         zn = mh_moves(n[act], b[act], qrow, zo, qe, multi_c[act], clen[act] - 1, s, zslice,
-                      dalias[np.where(multi_c[act], dslot[act], 0)] if dalias.shape[0] else None, walias[w, :, 0],
+                      dalias[np.where(multi_c[act], dslot[act], 0)] if dalias.shape[0] else None, walias[w],
                       st["wsum"][w], st["mh_g"], pos, st["chunk_key"][act], sweep, seed0, seed1, K, alpha,
                       doc_moves)
         n[act, zn] += 1

@@ -109,7 +109,7 @@ class Checkpointer:
         man = self.manifest()
         if man is None:
             raise FileNotFoundError(f"no checkpoint manifest in {self.dir}")
-        if man["ident"] != self._ident(model):
+        if not _same_chain(man["ident"], self._ident(model), int(man["sweep"])):
             raise ValueError(f"checkpoint identity {man['ident']} != run {self._ident(model)} (a checkpoint resumes "
                              "only the chain that wrote it: same K, α, β, seed, vocabulary, sampler and MH burn-in)")
         sweep = int(man["sweep"])
@@ -226,6 +226,19 @@ class Checkpointer:
                 raise ValueError(f"averaging samples do not match the corpus (doc key {miss} missing)")
             out[: my_keys.numel()] = dk[order[pos]]
         model.load_average_state({"n": glob_avg["n"], "wk": glob_avg["wk"], "k": glob_avg["k"], "dk": out})
+
+def _same_chain(saved: dict, run: dict, sweep: int) -> bool:
+    """Does a checkpoint of identity ``saved`` at ``sweep`` lie on the chain ``run`` samples? Equal
+    identities do; an MH run's state inside its dense burn-in is also a prefix of any MH run whose
+    burn-in reaches that sweep (a 2-sweep run capped the same ONI_MH_BURN = 3 at 2)."""
+    s, r = dict(saved), dict(run)
+    sc, rc = s.pop("chain", None), r.pop("chain", None)
+    if s != r or (sc is None) != (rc is None):
+        return False
+    if sc is None or sc == rc:
+        return True
+    return sc.get("sampler") == rc.get("sampler") and sweep <= min(sc.get("mh_burn", 0), rc.get("mh_burn", 0))
+
 
 def _pos0(c) -> torch.Tensor:
     """Canonical position of each corpus row's first token (0 unless the row is a piece)."""

@@ -25,7 +25,7 @@ def _toy(n_docs, V, seed):
 
 @pytest.mark.parametrize("K,V", [(7, 1000), (40, 1000), (100, 1000), (255, 1000), (40, 70001)])
 def test_alias_tables_bitwise(gpu, K, V):
-    """V ≥ 65536: the word records go out row by row, lanes along k (the large-vocabulary path)."""
+    """V ≥ 65536: the word entries go out row by row, lanes along k (the large-vocabulary path)."""
     r = np.random.default_rng(K)
     KS = (K + 3) // 4 * 4
     q = np.zeros((V, KS), np.float32)
@@ -37,7 +37,7 @@ def test_alias_tables_bitwise(gpu, K, V):
     nk = r.integers(0, 10**6, KS).astype(np.int32)
     wa, ws, da, g = spec.mh_tables(q, nk, ndk, rows, K, 0.37, 17.5)
     dev = torch.device(gpu)
-    out = [torch.zeros(V, K, 4, dtype=torch.int32, device=dev), torch.zeros(V, device=dev),
+    out = [torch.zeros(V, K, dtype=torch.int32, device=dev), torch.zeros(V, device=dev),
            torch.zeros(len(rows), K, dtype=torch.int32, device=dev), torch.zeros(KS, device=dev)]
     ops.mh_tables(torch.from_numpy(q).to(dev), torch.from_numpy(nk).to(dev), torch.from_numpy(ndk).to(dev),
                   torch.from_numpy(rows).to(dev), K, 0.37, 17.5, *out)

@@ -187,3 +187,13 @@ def test_small_counts_keep_int32_sums():
         assert m._avg["wk"].dtype == (torch.int64 if wide == "1" else torch.int32)
         out.append((m.theta(), m.phi()))
     assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+
+
+def test_burn_in_prefix_is_the_same_chain():
+    from oni355.utils.checkpoint import _same_chain
+    base = {"K": 100, "alpha": 0.5, "beta": 0.01, "seed": 1, "V": 10}
+    mh = lambda b: {**base, "chain": {"sampler": "mh", "mh_burn": b}}  # noqa: E731
+    assert _same_chain(mh(2), mh(3), 2)        # a 2-sweep run capped the burn-in at 2
+    assert not _same_chain(mh(2), mh(3), 3)    # after its hand-over the chains differ
+    assert _same_chain(mh(20), mh(20), 150)
+    assert not _same_chain({**base, "chain": {"sampler": "dense", "mh_burn": 0}}, mh(20), 0)
