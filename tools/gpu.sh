@@ -14,11 +14,16 @@
 #   py:<script>[:<args>]  python <script> <args>
 #   list                  rocprofv3 --list-avail (PMC counter names of this GPU)
 # TAG env var (default "run") names the output directory.
+# STAGE=1: run the frozen copy in gpurun_stage/ (tools/stage.sh made it while the tree was consistent)
+# so that edits made while the call waits for a box cannot mix into it; output still goes to the
+# top-level gpurun_out/.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TOP="$(cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && pwd)"
+cd "$TOP"
+[[ "${STAGE:-0}" == "1" ]] && cd "$TOP/gpurun_stage"
 export TMPDIR=/tmp
 TAG="${TAG:-run}"
-OUT="gpurun_out/$TAG"
+OUT="$TOP/gpurun_out/$TAG"
 mkdir -p "$OUT"
 log() { echo "$(date +%T) $*" | tee -a "$OUT/progress.log"; }
 n=0

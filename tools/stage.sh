@@ -1,0 +1,11 @@
+#!/bin/bash
+# Freeze the current tree (sources + built libraries) into gpurun_stage/ for `STAGE=1 bash
+# tools/gpu.sh ...`: a gpurun call snapshots the tree only when it gets a box, which can be many
+# minutes after it was started; the stage keeps the call on the tree it was started for.
+set -e
+cd "$(dirname "$0")/.."
+rm -rf gpurun_stage
+mkdir -p gpurun_stage
+tar --exclude=./.git --exclude=./gpurun_out --exclude=./gpurun_stage --exclude=./profiles \
+  --exclude='__pycache__' --exclude=./build --exclude='*_asan*' --exclude='*.log' --exclude=./gpurun_out -cf - . | tar -xf - -C gpurun_stage
+echo "staged $(du -sh gpurun_stage | cut -f1)"
