@@ -59,7 +59,7 @@ __global__ __launch_bounds__(256) void k_apply(int32_t* __restrict__ nwk, const 
                                                 int32_t* __restrict__ rdst, const int32_t* __restrict__ rows,
                                                 int64_t n_rows, void* __restrict__ acc_wk, void* __restrict__ acc_k,
                                                 void* __restrict__ acc_dk, int acc_wide,
-                                                const int32_t* __restrict__ ndk_fin, int64_t D) {
+                                                const int32_t* __restrict__ ndk_fin, int64_t D, int inplace) {
   __shared__ float den[256];
   __shared__ int32_t nkn[256];
   __shared__ int32_t part[256];
@@ -102,14 +102,21 @@ __global__ __launch_bounds__(256) void k_apply(int32_t* __restrict__ nwk, const 
   const int64_t nvec = V * KS / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
-    const int4 dv = reinterpret_cast<const int4*>(dcur)[i];
-    int4 nv = dv;
-    if (!absolute) {
-      nv = reinterpret_cast<int4*>(nwk)[i];
-      nv.x += dv.x; nv.y += dv.y; nv.z += dv.z; nv.w += dv.w;
+    int4 nv;
+    if (inplace) {
+      // the count pass already added this sweep's Δn_wk into n_wk (one process, no X01): the Δ
+      // heads are never written, so neither read nor zeroed -- 2 of the 5 table passes
+      nv = reinterpret_cast<const int4*>(nwk)[i];
+    } else {
+      const int4 dv = reinterpret_cast<const int4*>(dcur)[i];
+      nv = dv;
+      if (!absolute) {
+        nv = reinterpret_cast<int4*>(nwk)[i];
+        nv.x += dv.x; nv.y += dv.y; nv.z += dv.z; nv.w += dv.w;
+      }
+      reinterpret_cast<int4*>(nwk)[i] = nv;
+      reinterpret_cast<int4*>(dother)[i] = make_int4(0, 0, 0, 0);
     }
-    reinterpret_cast<int4*>(nwk)[i] = nv;
-    reinterpret_cast<int4*>(dother)[i] = make_int4(0, 0, 0, 0);
     if (acc_wk) add_counts(acc_wk, i, nv, acc_wide & 1);
     const int k0 = (int)((i * 4) % KS);
     float4 qo;
@@ -456,6 +463,8 @@ ONI_API int oni_gibbs_launch(const OniGibbs* a, int G, int KP, int init, int mod
 ONI_API int oni_gibbs_sizeof_args() { return (int)sizeof(OniGibbs); }
 
 // rsrc/rdst/rows/n_rows: optional fused long-row copy for the next sweep (n_rows = 0: none).
+// inplace: Δn_wk was added straight into nwk by the count pass (world 1); only q, n_k, the Δn_k
+// replicas and the aux words are handled here.
 // acc_wk/acc_k/acc_dk (all or none): the posterior-average sums ([V, KS], [KS], [D, KS]; int64 where
 // bit 0 / 1 / 2 of acc_wide is set, else int32) gain this sweep's n_wk, n_k and doc rows ndk_fin
 // [D, KS] -- the sample add in the same pass.
@@ -463,7 +472,9 @@ ONI_API int oni_gibbs_apply(int32_t* nwk, const int32_t* dcur, int32_t* dother, 
                             int32_t* nk_next, float* q, float* qfix, int64_t V, int K, int KS, float beta, float vbeta,
                             uint32_t* sweep_ctr, int bump, int absolute, int nk_rep, const int32_t* rsrc,
                             int32_t* rdst, const int32_t* rows, int64_t n_rows, void* acc_wk, void* acc_k,
-                            void* acc_dk, int acc_wide, const int32_t* ndk_fin, int64_t D, hipStream_t s) {
+                            void* acc_dk, int acc_wide, const int32_t* ndk_fin, int64_t D, int inplace,
+                            hipStream_t s) {
+  if (inplace && absolute) return (int)hipErrorInvalidValue;
   if (KS % 4 != 0 || KS > 256 || nk_rep < 1 || (nk_rep & (nk_rep - 1)) || qfix == nullptr)
     return (int)hipErrorInvalidValue;
   if (n_rows < 0 || (n_rows > 0 && (rsrc == nullptr || rdst == nullptr || rows == nullptr)))
@@ -476,7 +487,7 @@ ONI_API int oni_gibbs_apply(int32_t* nwk, const int32_t* dcur, int32_t* dother, 
   k_apply<<<oni::grid_for(work, 256, 2048), 256, 0, s>>>(nwk, dcur, dother, nk_cur, nk_next, q, qfix, V, K, KS, beta,
                                                           vbeta, sweep_ctr, bump, absolute, nk_rep, rsrc, rdst, rows,
                                                           n_rows, acc_wk, acc_k, acc ? acc_dk : nullptr, acc_wide,
-                                                          ndk_fin, acc ? D : 0);
+                                                          ndk_fin, acc ? D : 0, inplace);
   return (int)hipGetLastError();
 }
 

@@ -4,9 +4,12 @@
 // Why: the dense samplers spend K multiply-adds (plus a scan and a search) on every token; at
 // K = 100 k_gibbs_ldsg runs 0.89 ms per 25M-token sweep, bound by the per-token q-row round trip
 // and its 4-lane scans (docs/performance.md). An MH step costs O(1) per token whatever K is: the
-// proposals come from alias tables built once per sweep from the sweep-start snapshot (the word
-// factor q of every word; the sweep-start row of every document spread over several chunks), and
-// the acceptance test needs a handful of counts. Semantics and numerics: oni355/ref/spec.py
+// word proposal ∝ q[w, ·] is a two-level inverse CDF -- a 64-B row of bucket prefix sums built once
+// per sweep (k_mh_cdf: a streaming pass over q, V·64 B written), then the bucket's own 8-16 q values
+// -- and the doc proposal an alias table of the sweep-start row of every document spread over
+// several chunks; the acceptance test needs a handful of counts. (Round 4 built a Vose alias table
+// of every word's q row per sweep: V·K·16 B of records, 0.24 ms at V = 180k, K = 100, sequential
+// per-lane construction bound by LDS latency.) Semantics and numerics: oni355/ref/spec.py
 // gibbs_pass_mh / mh_moves / alias_table, replayed bit for bit (tests/test_gpu_mh.py); the moves
 // leave the collapsed conditional invariant (tests/test_mh_conditional.py).
 //
@@ -28,8 +31,7 @@
 
 struct OniMH {
   OniGibbs g;
-  const uint4* walias;         // [V][K] word proposal records {thr24 << 8 | alias, q_j, q_alias, Σ q}
-  const float* wsum;           // [V] Σ_k q[w, k] (the word table's weight)
+  const float* wcdf;           // [V][16] level-1 CDF of the word proposal ∝ q[w, ·] (k_mh_cdf)
   const uint32_t* dalias;      // [n_long][K] alias entries of the multi-chunk docs' n_src + α
   const float* mh_g;           // [KS] 1 / (n_k + Vβ + 1)
   const int32_t* chunk_dslot;  // [C] row of dalias (multi-chunk doc) or -1
@@ -55,64 +57,47 @@ __device__ __forceinline__ int alias_resolve(int j, uint32_t coin, uint32_t e) {
   return coin < (e >> 8) ? j : (int)(e & 0xFFu);
 }
 
-// ---- proposal tables ---------------------------------------------------------------------------
-// One lane per row (rows [0, V): word rows of q; rows [V, V + n_long): sweep-start rows of the
-// multi-chunk docs + α). Sequential f32 per lane, exactly spec.alias_table: sum, scale, classify
-// into the small / large stacks (one u8 array: small grows up from 0, large down from K − 1),
-// pair off, leftovers keep their own index. The rows are read and written cooperatively (the wave
-// walks its 64 rows, lanes along k: coalesced), p / entries / stack live in LDS transposed to
-// [k][row] for the per-lane sequential part.
-// Word rows are written as 16-B records {entry, q_j, q_alias(j), Σ_k q_k}: the sampler's one
-// gather of a word proposal then also brings q_t and the row sum (the word move's ratio), so a token
-// costs three scattered loads (record, q[w, zo], q[w, t_doc]) instead of five.
-__global__ __launch_bounds__(64) void k_mh_alias(const float* __restrict__ q, int64_t V, int K, int KS,
-                                                  const int32_t* __restrict__ ndk, const int32_t* __restrict__ rows,
-                                                  int64_t n_long, float alpha, uint4* __restrict__ wrec,
-                                                  float* __restrict__ wsum, uint32_t* __restrict__ dalias,
-                                                  const int32_t* __restrict__ nk, float vbeta, float* __restrict__ g,
-                                                  bool coal) {
+// ---- doc proposal tables ------------------------------------------------------------------------
+// One lane per multi-chunk document: its sweep-start row + α. Sequential f32 per lane, exactly
+// spec.alias_table: sum, scale, classify into the small / large stacks (one u8 array: small grows up
+// from 0, large down from K − 1), pair off, leftovers keep their own index; p / entries / stack live
+// in LDS transposed to [k][row] for the per-lane sequential part. Block 0 also writes
+// g_k = 1/(n_k + Vβ + 1).
+__global__ __launch_bounds__(64) void k_mh_alias(int K, int KS, const int32_t* __restrict__ ndk,
+                                                  const int32_t* __restrict__ rows, int64_t n_long, float alpha,
+                                                  uint32_t* __restrict__ dalias, const int32_t* __restrict__ nk,
+                                                  float vbeta, float* __restrict__ g) {
   extern __shared__ __align__(16) unsigned char smem_alias[];
   // p is [K][65], one column per lane. The entries share its storage: Vose writes entry s once
   // p[s] is spent (s is the popped small, whose weight is already in a register, or the carried
   // large, whose weight lives in a register), and the leftovers get their own index after the
-  // pairing; 32 instead of 58 KB per wave at K = 100 (4 waves per CU instead of 2)
+  // pairing (32 instead of 58 KB per wave at K = 100)
   float* p = reinterpret_cast<float*>(smem_alias);
   uint32_t* ent = reinterpret_cast<uint32_t*>(smem_alias);
-  float* tots = reinterpret_cast<float*>(smem_alias + (size_t)K * kAS * sizeof(float));   // [64]
-  uint8_t* stk = smem_alias + (size_t)K * kAS * sizeof(float) + 64 * sizeof(float);      // [K][64]
+  uint8_t* stk = smem_alias + (size_t)K * kAS * sizeof(float);  // [K][64]
   const int lane = threadIdx.x;
   if (blockIdx.x == 0) {
     for (int k = lane; k < KS; k += 64) g[k] = 1.0f / (((float)nk[k] + vbeta) + 1.0f);
   }
   const int64_t r0 = (int64_t)blockIdx.x * 64;
-  const int nrows = (int)((V + n_long - r0) < 64 ? (V + n_long - r0) : 64);
-  // each lane loads its own row (16-B vectors; K rows of q are KS-strided, KS % 4 == 0)
+  const int nrows = (int)((n_long - r0) < 64 ? (n_long - r0) : 64);
   const int64_t row = r0 + lane;
   const bool has = lane < nrows;
-  const bool word = has && row < V;
-  const float* qr = q + (word ? row : 0) * KS;
-  const int32_t* br = ndk + (has && !word ? (int64_t)rows[row - V] : 0) * KS;
+  const int32_t* br = ndk + (has ? (int64_t)rows[row] : 0) * KS;
   if (has) {
 #pragma unroll 4
     for (int k = 0; k < K; k += 4) {
-      float4 v;
-      if (word) {
-        v = *reinterpret_cast<const float4*>(qr + k);
-      } else {
-        const int4 c = *reinterpret_cast<const int4*>(br + k);
-        v = make_float4((float)c.x + alpha, (float)c.y + alpha, (float)c.z + alpha, (float)c.w + alpha);
-      }
-      p[k * kAS + lane] = v.x;
-      if (k + 1 < K) p[(k + 1) * kAS + lane] = v.y;
-      if (k + 2 < K) p[(k + 2) * kAS + lane] = v.z;
-      if (k + 3 < K) p[(k + 3) * kAS + lane] = v.w;
+      const int4 c = *reinterpret_cast<const int4*>(br + k);
+      p[k * kAS + lane] = (float)c.x + alpha;
+      if (k + 1 < K) p[(k + 1) * kAS + lane] = (float)c.y + alpha;
+      if (k + 2 < K) p[(k + 2) * kAS + lane] = (float)c.z + alpha;
+      if (k + 3 < K) p[(k + 3) * kAS + lane] = (float)c.w + alpha;
     }
   }
   __syncthreads();
-  if (lane < nrows) {
+  if (has) {
     float tot = 0.f;
     for (int k = 0; k < K; ++k) tot = tot + p[k * kAS + lane];
-    tots[lane] = tot;
     const float scale = (float)K / tot;
     int ns = 0, nl = 0;
     for (int k = 0; k < K; ++k) {
@@ -161,38 +146,51 @@ __global__ __launch_bounds__(64) void k_mh_alias(const float* __restrict__ q, in
     }
   }
   __syncthreads();
-  // large vocabularies (many waves: store-throughput bound): word rows go out one row at a time,
-  // lanes along k, so each store instruction writes 64 consecutive 16-B records (a lane per row
-  // touches 64 rows K·16 B apart per store): 0.288 -> 0.244 ms at V = 180k, K = 100. Small ones
-  // (few waves: latency bound) keep a lane per row: 0.049 vs 0.058 ms at V = 6.5k.
-  const int nw = coal ? (int)(V - r0 < (int64_t)nrows ? (V - r0 > 0 ? V - r0 : 0) : nrows) : 0;
-  if (!coal && word) {
-    const uint32_t tb = __float_as_uint(tots[lane]);
-    uint4* out = wrec + row * K;
-#pragma unroll 4
-    for (int k = 0; k < K; ++k) {
-      const uint32_t e = ent[k * kAS + lane];
-      out[k] = make_uint4(e, __float_as_uint(qr[k]), __float_as_uint(qr[e & 0xFFu]), tb);
-    }
-  }
-#pragma unroll 2
-  for (int r = 0; r < nw; ++r) {
-    const float* qq = q + (r0 + r) * KS;
-    const uint32_t tb = __float_as_uint(tots[r]);
-    uint4* out = wrec + (r0 + r) * K;
-    for (int k = lane; k < K; k += 64) {
-      const uint32_t e = ent[k * kAS + r];
-      out[k] = make_uint4(e, __float_as_uint(qq[k]), __float_as_uint(qq[e & 0xFFu]), tb);
-    }
-  }
   if (has) {
-    if (word) {
-      wsum[row] = tots[lane];
-    } else {
-      uint32_t* out = dalias + (row - V) * K;
+    uint32_t* out = dalias + row * K;
 #pragma unroll 4
-      for (int k = 0; k < K; ++k) out[k] = ent[k * kAS + lane];
+    for (int k = 0; k < K; ++k) out[k] = ent[k * kAS + lane];
+  }
+}
+
+// ---- word proposal: level-1 CDF rows ----------------------------------------------------------------
+// 16 lanes per word (4 words per wave): lane b sums bucket b's q values sequentially (the bucket's
+// W = 8 or 16 topics, two or four 16-B loads of the q row: lanes along the row, coalesced), then
+// takes C[b] = S_0 + … + S_b in order from its group's lanes and writes it: one 64-B row per word.
+// Exactly spec.word_cdf.
+template <int WB>
+__global__ __launch_bounds__(256) void k_mh_cdf(const float* __restrict__ q, int64_t V, int K, int KS,
+                                                float* __restrict__ wcdf) {
+  const int lane = threadIdx.x & 63;
+  const int bk = lane & 15;
+  const int nb = (K + WB - 1) / WB;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t r0 = wave * 4; r0 < V; r0 += nwaves * 4) {
+    const int64_t row = r0 + (lane >> 4);
+    const bool live = row < V;
+    float sb = 0.f;
+    if (live && bk < nb) {
+      const float* qr = q + row * KS + bk * WB;
+#pragma unroll
+      for (int j4 = 0; j4 < WB / 4; ++j4) {
+        const int k0 = bk * WB + 4 * j4;
+        if (k0 < KS) {
+          const float4 v = *reinterpret_cast<const float4*>(qr + 4 * j4);
+          if (k0 + 0 < K) sb = sb + v.x;
+          if (k0 + 1 < K) sb = sb + v.y;
+          if (k0 + 2 < K) sb = sb + v.z;
+          if (k0 + 3 < K) sb = sb + v.w;
+        }
+      }
     }
+    float c = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float si = __shfl(sb, (lane & ~15) + i);
+      if (i <= bk && i < nb) c = c + si;
+    }
+    if (live) wcdf[row * 16 + bk] = c;
   }
 }
 
@@ -212,7 +210,8 @@ struct MHB {
   oni::U4 r;     // Philox block (pos, key, sweep, 2)
   int zo;        // sweep-start topic
   float qz;      // q[w, zo]
-  uint4 rw;      // word proposal record at j(r.x): {entry, q_j, q_alias, Σ_k q_k}
+  float zw;      // Σ_k q[w, k] as the word CDF's total Z
+  float qtw;     // q[w, tw] (stage C, from the bucket's q values)
   uint32_t ed;   // doc alias entry at j(r.z) (read for every chunk; used by multi-chunk docs)
   int32_t bzo;   // n_src[doc, zo]
   // stage C (issued at the end of the previous step, once that token has moved)
@@ -231,7 +230,7 @@ struct MHB {
 // on one common address for the doc tables) and every decision is a select, so no loaded value is
 // merged at a control-flow join -- a merge there makes the compiler wait for every outstanding
 // memory op (vmcnt(0)), which serialised the token pipeline.
-template <int MODE, int DM>
+template <int MODE, int DM, int WB>
 struct MHLane {
   const OniMH& m;
   const OniGibbs& a;
@@ -248,6 +247,11 @@ struct MHLane {
   uint32_t wa[2];       // stage A: token words (parity slots)
   int32_t pa[2];        // stage A: word-sorted slots (MODE 3/4)
   MHB<DM> b[2];             // stage B (parity slots)
+  float c1[16];         // level-1 word CDF row of the token after next (gathered a step ahead of its stage B)
+  float qb[WB];         // the proposed bucket's q values (stage B → stage C of one token)
+  float ywd;            // the word draw's y = u·Z
+  float base;           // C[bucket − 1] (gathered)
+  int bk;               // the bucket
   int32_t* red;         // LDS: per-topic count deltas of the wave
   int nchg;
   Pend<MODE> pend;
@@ -259,9 +263,6 @@ struct MHLane {
   // n_dk^¬ + α from a count cell c and the sweep-start count bk
   __device__ __forceinline__ float aw(int c, int32_t bk) const {
     return (float)(multi ? bk + c - kMHBias : c) + a.alpha;
-  }
-  __device__ __forceinline__ bool alias_keeps(uint32_t r, uint32_t e) const {
-    return ((r * (uint32_t)K) >> 8) < (e >> 8);
   }
   __device__ __forceinline__ int alias_draw(uint32_t r, uint32_t e) const {
     const int j = (int)__umulhi(r, (uint32_t)K);
@@ -280,6 +281,19 @@ struct MHLane {
     return y < nd ? tz : tu;
   }
 
+  // level-1 word CDF row of word w (a stage ahead of its stage B: its bucket gather depends on it)
+  __device__ __forceinline__ void load_c1(uint32_t w) {
+    const float4* r = reinterpret_cast<const float4*>(m.wcdf) + (int64_t)(w == oni::kPadWord ? 0u : w) * 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float4 v = r[i];
+      c1[4 * i] = v.x;
+      c1[4 * i + 1] = v.y;
+      c1[4 * i + 2] = v.z;
+      c1[4 * i + 3] = v.w;
+    }
+  }
+
   // stage B of the token at step s (word w): Philox block, then the state-free gathers
   __device__ __forceinline__ void issue_b(int P, int s, uint32_t w) {
     MHB<DM>& x = b[P];
@@ -288,7 +302,28 @@ struct MHLane {
     const int z0 = (int)L.zsl[s * 64 + lane];
     x.zo = z0 < K - 1 ? z0 : K - 1;  // padding slots hold 0; clamp anyway: an LDS index
     x.qz = a.q[wc * (uint32_t)KS + (uint32_t)x.zo];
-    x.rw = m.walias[wc * (uint32_t)K + __umulhi(x.r.x, (uint32_t)K)];
+    // word proposal, level 1: y = u·Z, bucket = #{i : C[i] ≤ y} (capped; a branch-free binary search
+    // over the monotone row), residual y − C[b − 1] (C[b − 1] gathered from the row's cache line,
+    // not selected out of 16 registers)
+    {
+      const int nb = (K + WB - 1) / WB;
+      x.zw = c1[15];
+      ywd = oni::u01(x.r.x) * c1[15];
+      const int nbk = count_le<16>(c1, 0.f, ywd);
+      bk = nbk < nb - 1 ? nbk : nb - 1;
+      base = m.wcdf[(int64_t)wc * 16 + (bk > 0 ? bk - 1 : 0)];
+      // level 2: the bucket's q values (a float4 past the row's KS padding is not read)
+      const float* qr = a.q + (int64_t)wc * KS + bk * WB;
+#pragma unroll
+      for (int j4 = 0; j4 < WB / 4; ++j4) {
+        const bool in = bk * WB + 4 * j4 < KS;
+        const float4 v = *reinterpret_cast<const float4*>(in ? qr + 4 * j4 : a.q);
+        qb[4 * j4] = in ? v.x : 0.f;
+        qb[4 * j4 + 1] = in ? v.y : 0.f;
+        qb[4 * j4 + 2] = in ? v.z : 0.f;
+        qb[4 * j4 + 3] = in ? v.w : 0.f;
+      }
+    }
     // one-chunk docs read one common address (they use neither value): no scattered lines
     x.ed = drow[multi ? __umulhi(x.r.z, (uint32_t)K) : 0u];
     x.bzo = brow[multi ? x.zo : 0];
@@ -307,7 +342,24 @@ struct MHLane {
   __device__ __forceinline__ void issue_c(int P, int s, uint32_t w) {
     MHB<DM>& x = b[P];
     const uint32_t qo = (w == oni::kPadWord ? 0u : w) * (uint32_t)KS;
-    x.tw = alias_draw(x.r.x, x.rw.x);
+    {
+      // word proposal, level 2: running f32 sum of the bucket's q values from 0 (spec.word_cdf_draw).
+      // Topics past K hold q = 0 (k_apply) and the loads past KS were zeroed: their running sums
+      // repeat the last real one, so counting them changes nothing after the cap.
+      const float y2 = ywd - (bk > 0 ? base : 0.f);
+      float cum[WB];
+      float run = 0.f;
+#pragma unroll
+      for (int j = 0; j < WB; ++j) {
+        run = run + qb[j];
+        cum[j] = run;
+      }
+      const int cnt = count_le<WB>(cum, 0.f, y2);
+      const int rem = K - bk * WB;
+      const int last = (rem < WB ? rem : WB) - 1;
+      x.tw = bk * WB + (cnt < last ? cnt : last);
+      x.qtw = a.q[qo + (uint32_t)x.tw];
+    }
     const int tdm = alias_draw(x.r.z, x.ed);
     const int tds = single_pick(x.r.z, s);
     x.td = multi ? tdm : tds;
@@ -352,8 +404,8 @@ struct MHLane {
     pend.flush(a, KS);
     asm volatile("" ::: "memory");
     const int tw = x.tw, td = x.td;
-    const float qtw = __uint_as_float(alias_keeps(x.r.x, x.rw.x) ? x.rw.y : x.rw.z);
-    const float zw = __uint_as_float(x.rw.w);
+    const float qtw = x.qtw;
+    const float zw = x.zw;
     const float qtd = x.qtd;
     const int32_t btw = x.btw, btd = x.btd;
     const float2 ab = L.qfx[zo];
@@ -421,7 +473,11 @@ struct MHLane {
       }
     }
     asm volatile("" ::: "memory");
-    if constexpr (LOAD_B) issue_c(NX, s + 1, wa[NX]);
+    if constexpr (LOAD_B) {
+      load_c1(wa[P]);  // the token after next (issued before stage C: its wait must not cover C)
+      asm volatile("" ::: "memory");
+      issue_c(NX, s + 1, wa[NX]);
+    }
   }
 };
 
@@ -488,12 +544,12 @@ __device__ __forceinline__ MHLds mh_lds(unsigned char* smem, int KS) {
   return L;
 }
 
-template <int MODE, int DM>
+template <int MODE, int DM, int WB>
 __global__ __launch_bounds__(64) void k_gibbs_mh(const OniMH m) {
   extern __shared__ __align__(16) unsigned char smem_mh[];
   const OniGibbs& a = m.g;
   const int KS = a.KS;
-  MHLane<MODE, DM> x(m);
+  MHLane<MODE, DM, WB> x(m);
   x.L = mh_lds(smem_mh, KS);
   int32_t* red = reinterpret_cast<int32_t*>(smem_mh + (size_t)KS * (sizeof(float2) + sizeof(float)));
   x.red = red;
@@ -543,7 +599,9 @@ __global__ __launch_bounds__(64) void k_gibbs_mh(const OniMH m) {
     x.wa[t] = len > t ? a.tok_word[x.off + t * 64 + lane] : oni::kPadWord;
     x.pa[t] = ((MODE == 3 || MODE == 4) && len > t) ? a.wpos[x.off + t * 64 + lane] : 0;
   }
+  x.load_c1(x.wa[0]);
   x.issue_b(0, 0, x.wa[0]);
+  x.load_c1(x.wa[1]);
   x.issue_c(0, 0, x.wa[0]);
   int s = 0;
   for (; s + 3 < len; s += 2) {
@@ -608,15 +666,20 @@ static size_t mh_lds_bytes(int KS, int lmax) {
   return (size_t)KS * (sizeof(float2) + sizeof(float) + sizeof(int32_t)) + (size_t)KS * 64 + (size_t)lmax * 64;
 }
 
+// Per-sweep MH tables: the word CDF rows (k_mh_cdf, all V words) and the alias rows of the n_long
+// multi-chunk documents + g (k_mh_alias over the document rows only).
 ONI_API int oni_mh_tables(const float* q, int64_t V, int K, int KS, const int32_t* ndk, const int32_t* rows,
-                          int64_t n_long, float alpha, uint4* walias, float* wsum, uint32_t* dalias,
-                          const int32_t* nk, float vbeta, float* g, hipStream_t s) {
+                          int64_t n_long, float alpha, float* wcdf, uint32_t* dalias, const int32_t* nk, float vbeta,
+                          float* g, hipStream_t s) {
   if (K < 1 || K > 255 || K > KS || KS % 4 || V < 0 || n_long < 0) return (int)hipErrorInvalidValue;
-  const int64_t nrows = V + n_long;
-  const unsigned grid = (unsigned)((nrows + 63) / 64 > 0 ? (nrows + 63) / 64 : 1);
-  const size_t lds = (size_t)K * kAS * sizeof(float) + 64 * sizeof(float) + (size_t)K * 64;
-  k_mh_alias<<<grid, 64, lds, s>>>(q, V, K, KS, ndk, rows, n_long, alpha, walias, wsum, dalias, nk, vbeta, g,
-                                   V >= 65536);
+  if (V > 0) {
+    const unsigned cgrid = oni::grid_for((V + 3) / 4 * 64, 256, 8192);
+    if (K <= 128) k_mh_cdf<8><<<cgrid, 256, 0, s>>>(q, V, K, KS, wcdf);
+    else k_mh_cdf<16><<<cgrid, 256, 0, s>>>(q, V, K, KS, wcdf);
+  }
+  const unsigned grid = (unsigned)((n_long + 63) / 64 > 0 ? (n_long + 63) / 64 : 1);
+  const size_t lds = (size_t)K * kAS * sizeof(float) + (size_t)K * 64;
+  k_mh_alias<<<grid, 64, lds, s>>>(K, KS, ndk, rows, n_long, alpha, dalias, nk, vbeta, g);
   return (int)hipGetLastError();
 }
 
@@ -632,12 +695,16 @@ ONI_API int oni_gibbs_mh_launch(const OniMH* m, int init, int mode, hipStream_t 
     k_gibbs_mh_init<<<grid, 64, lds, s>>>(*m);
     return (int)hipGetLastError();
   }
-  if (!a.qfix || !m->walias || !m->wsum || !m->mh_g || !m->chunk_dslot) return (int)hipErrorInvalidValue;
+  if (!a.qfix || !m->wcdf || !m->mh_g || !m->chunk_dslot) return (int)hipErrorInvalidValue;
   if (m->doc_moves < 1 || m->doc_moves > 4) return (int)hipErrorInvalidValue;
   if (mode == 2 && !a.chg_mask) return (int)hipErrorInvalidValue;
   if (mode == 3 && (!a.wpos || !a.z_w)) return (int)hipErrorInvalidValue;
   if (mode == 4 && (!a.wpos || !a.zz_w || !a.chg_mask)) return (int)hipErrorInvalidValue;
-#define ONI_MH(md, dm) k_gibbs_mh<md, dm><<<grid, 64, lds, s>>>(*m)
+#define ONI_MH(md, dm)                                                  \
+  do {                                                                  \
+    if (a.K <= 128) k_gibbs_mh<md, dm, 8><<<grid, 64, lds, s>>>(*m);    \
+    else k_gibbs_mh<md, dm, 16><<<grid, 64, lds, s>>>(*m);              \
+  } while (0)
   switch (m->doc_moves * 8 + mode) {
 #define ONI_MH_CASES(dm) \
     case dm * 8 + 0: ONI_MH(0, dm); break; \

@@ -266,14 +266,19 @@ class GibbsLDA:
         self._x01 = None
         if comm is not None and comm.dist and self.KS % 2 == 0 and self._x01_wanted():
             self._setup_x01()
+        # one process (no X01): the count passes add Δn_wk straight into n_wk and k_apply refreshes
+        # q from it (2 of its 5 passes over V·KS fewer); ONI_APPLY_INPLACE=0 keeps the Δ buffer
+        self._inplace_ok = ((comm is None or not comm.dist) and self._split is None
+                            and os.environ.get("ONI_APPLY_INPLACE", "1") != "0")
         self._avg = None          # posterior-averaging accumulators (plan_average)
         self._acc = False         # sweeps add their counts to the accumulators (inside graphs too)
         self._avg_at: list = []   # sweep counts at which a sample is added
         self._avg_cache = None    # (θ, φ) of the completed average
 
     def _setup_mh(self) -> None:
-        """MH sampler state: per-sweep alias tables (words; documents spread over several chunks,
-        which propose from their sweep-start row) and every chunk's row in the doc table."""
+        """MH sampler state: per-sweep proposal tables (every word's level-1 CDF row; alias rows of
+        the documents spread over several chunks, which propose from their sweep-start row) and
+        every chunk's row in the doc table."""
         c = self.c
         if c.L > spec.MH_MAX_CHUNK or (c.chunk_len.numel() and int(c.chunk_len.max()) > spec.MH_MAX_CHUNK):
             raise ValueError(f"the MH sampler needs chunks of at most {spec.MH_MAX_CHUNK} tokens (corpus L = {c.L})")
@@ -286,8 +291,8 @@ class GibbsLDA:
         if rows.numel():
             dslot[multi] = torch.searchsorted(rows, c.chunk_doc[multi].to(torch.int64)).to(torch.int32)
         self.chunk_dslot = dslot
-        self.walias = torch.zeros(self.V, self.K, dtype=torch.int32, device=dev)  # u32 alias entries
-        self.wsum = torch.zeros(self.V, dtype=torch.float32, device=dev)
+        # word proposal ∝ q[w, ·]: level-1 CDF rows (bucket prefix sums; level 2 is the q row itself)
+        self.wcdf = torch.zeros(self.V, spec.MH_CDF_BUCKETS, dtype=torch.float32, device=dev)
         self.dalias = torch.zeros(max(int(rows.numel()), 1), self.K, dtype=torch.int32, device=dev)
         self.mh_g = torch.zeros(self.KS, dtype=torch.float32, device=dev)
         # one word move + two doc moves per token: with one doc move the chain plateaus 2.6 % lower
@@ -301,10 +306,10 @@ class GibbsLDA:
         """The sweep's MH proposal tables from the snapshot (q and the topic totals nk[cn] the last
         apply wrote, the sweep-start doc rows ndk[a])."""
         ops.mh_tables(self.q, self.nk[self.cn], self.ndk[self.a], self.mh_rows, self.K, self.alpha, self.vbeta,
-                      self.walias, self.wsum, self.dalias, self.mh_g)
+                      self.wcdf, self.dalias, self.mh_g)
 
     def mh_state(self) -> dict:
-        return dict(walias=self.walias, wsum=self.wsum, dalias=self.dalias, mh_g=self.mh_g,
+        return dict(wcdf=self.wcdf, dalias=self.dalias, mh_g=self.mh_g,
                     chunk_dslot=self.chunk_dslot, mh_lmax=self.mh_lmax)
 
     def _x01_wanted(self) -> bool:
@@ -525,6 +530,9 @@ class GibbsLDA:
         # long (chunked) documents add their Δn_dk into ndk[1-a] rows that hold a copy of ndk[a]:
         # every apply -- the previous sweep's, or _prime()'s after init / resume -- seeds that copy
         st = self._state(False)
+        inplace = self._inplace_ok and mode in (1, 2, 4)
+        if inplace:
+            st["dnwk"] = self.nwk  # MODE 1: the sampler's Δ atomics land in n_wk itself
         if self.mh:
             self.mh_build_tables()
             st.update(self.mh_state())
@@ -533,7 +541,7 @@ class GibbsLDA:
                        chg_mask=self.wbits if mode == 4 else getattr(self, "chg_mask", None), wpos=c.wpos,
                        z_w=getattr(self, "z_w", None), zz_w=getattr(self, "zz_w", None), alpha_in_row=self._air,
                        mh_doc_moves=getattr(self, "mh_doc_moves", 1))
-        head = self.dn[self.b][: self.V * self.KS].view(self.V, self.KS)
+        head = self.nwk if inplace else self.dn[self.b][: self.V * self.KS].view(self.V, self.KS)
         if mode == 4:
             # dn[b] head := Δn_wk of the tokens marked in the word-sorted change bitmap
             ops.wdelta_recount(self.wbits, c.wsorted, self.zz_w, head, self.KS)
@@ -560,7 +568,7 @@ class GibbsLDA:
         ops.gibbs_apply(self.nwk, self.dn[self.b][:so], self.dn[1 - self.b][:so], self.nk[self.cn], self.nk[1 - self.cn],
                         self.q, self.qfix, self.V, self.K, self.KS, self.beta, self.vbeta, self.sweep_ctr, bump=True,
                         absolute=mode in (0, 3), rows_copy=(self.ndk[1 - self.a], self.ndk[self.a], c.long_rows),
-                        acc=acc)
+                        acc=acc, inplace=inplace)
         self.a, self.b, self.cn = 1 - self.a, 1 - self.b, 1 - self.cn
         self.sweeps_done += 1
         self._tail_cache = None

@@ -376,8 +376,8 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
     k_gibbs, 2 = k_gibbs_ldsg (G > 1), 3 = k_gibbs_x1 (G = 1); the specialised kernels need
     ``alpha_in_row`` (n + α exact in f32 for every count of the corpus), else the generic one runs.
     4 = k_gibbs_mh, the Metropolis-Hastings sampler (one-lane units, chunks ≤ 127 tokens; NOT the
-    same draws: its own oracle spec.gibbs_pass_mh) which also needs ``st["walias"]``,
-    ``st["wsum"]``, ``st["dalias"]``, ``st["mh_g"]`` (:func:`mh_tables`) and ``st["chunk_dslot"]``;
+    same draws: its own oracle spec.gibbs_pass_mh) which also needs ``st["wcdf"]``,
+    ``st["dalias"]``, ``st["mh_g"]`` (:func:`mh_tables`) and ``st["chunk_dslot"]``;
     ``mh_doc_moves`` doc moves after each token's word move.
     """
     s0, s1 = spec.split_seed(seed)
@@ -395,7 +395,7 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
     if not _is_dev(st["tok_word"]):
         chg = st.get("chg_count")
         z_before = st["tok_z"].clone() if (chg is not None or mode == 4) else None
-        npst = {k: (v.numpy().view(np.uint32) if k in ("tok_word", "chunk_key", "walias", "dalias") else v.numpy())
+        npst = {k: (v.numpy().view(np.uint32) if k in ("tok_word", "chunk_key", "dalias") else v.numpy())
                 for k, v in st.items() if isinstance(v, torch.Tensor)}
         npst["dnk"] = npst["dnk"][:KS]  # replica 0 (the sum over replicas is what counts)
         if mode != 1:
@@ -464,7 +464,7 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
         m.inv_alpha = float(np.float32(1.0 / alpha))
         m.doc_moves = int(mh_doc_moves)
         if not init:
-            for name in ("walias", "wsum", "dalias", "chunk_dslot"):
+            for name in ("wcdf", "dalias", "chunk_dslot"):
                 setattr(m, name, _lib.ptr(st[name]))
             m.mh_g = _lib.ptr(st["mh_g"])
         _lib.check(_lib.lib().oni_gibbs_mh_launch(C.byref(m), 1 if init else 0, int(mode), _lib.stream()),
@@ -475,24 +475,25 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
 
 
 def mh_tables(q: torch.Tensor, nk: torch.Tensor, ndk_src: torch.Tensor, long_rows: torch.Tensor, K: int,
-              alpha: float, vbeta: float, walias: torch.Tensor, wsum: torch.Tensor, dalias: torch.Tensor,
+              alpha: float, vbeta: float, wcdf: torch.Tensor, dalias: torch.Tensor,
               g: torch.Tensor) -> None:
-    """Per-sweep tables of the MH sampler (k_mh_alias, spec.mh_tables): ``walias`` [V, K] := the
-    alias entries of every word's q row and ``wsum`` [V] its sum, ``dalias`` [n_long, K] := that of
+    """Per-sweep tables of the MH sampler (k_mh_cdf + k_mh_alias, spec.mh_tables): ``wcdf`` [V, 16]
+    f32 := every word's level-1 CDF row of its q row, ``dalias`` [n_long, K] := the alias entries of
     n_dk + α for every document over several chunks (rows ``long_rows`` of ``ndk_src``),
     ``g`` [KS] := 1/(n_k + Vβ + 1) of the snapshot's topic totals ``nk``. int32 tensors hold the u32
     entries."""
+    if wcdf.shape != (q.shape[0], spec.MH_CDF_BUCKETS) or wcdf.dtype != torch.float32:
+        raise ValueError("wcdf must be a [V, 16] float32 table")
     if not _is_dev(q):
-        wa, ws, da, gg = spec.mh_tables(q.numpy(), nk.numpy(), ndk_src.numpy(), long_rows.numpy(), K, alpha, vbeta)
-        walias.copy_(torch.from_numpy(wa.view(np.int32)))
-        wsum.copy_(torch.from_numpy(ws))
+        wc, da, gg = spec.mh_tables(q.numpy(), nk.numpy(), ndk_src.numpy(), long_rows.numpy(), K, alpha, vbeta)
+        wcdf.copy_(torch.from_numpy(wc))
         if da.shape[0]:
             dalias.copy_(torch.from_numpy(da.view(np.int32)))
         g.copy_(torch.from_numpy(gg))
         return
     V, KS = q.shape
     _lib.check(_lib.lib().oni_mh_tables(_lib.ptr(q), V, K, KS, _lib.ptr(ndk_src), _lib.ptr(long_rows),
-                                        long_rows.numel(), float(alpha), _lib.ptr(walias), _lib.ptr(wsum),
+                                        long_rows.numel(), float(alpha), _lib.ptr(wcdf),
                                         _lib.ptr(dalias), _lib.ptr(nk), float(vbeta), _lib.ptr(g), _lib.stream()),
                "oni_mh_tables")
 
@@ -574,7 +575,7 @@ STREAM_RECOUNT = True  # k_recount_reg (register runs) 0.065 ms vs k_recount (LD
 
 
 def gibbs_apply(nwk, dcur, dother, nk_cur, nk_next, q, qfix, V, K, KS, beta, vbeta, sweep_ctr, bump=True,
-                absolute=False, rows_copy=None, acc=None):
+                absolute=False, rows_copy=None, acc=None, inplace=False):
     """n_wk ← Δ (or absolute), n_k ← n_k + Σ_replicas Δn_k, q refresh (+ the token-exclusion
     table ``qfix`` [2, KS]); zeroes ``dother``.
 
@@ -582,7 +583,11 @@ def gibbs_apply(nwk, dcur, dother, nk_cur, nk_next, q, qfix, V, K, KS, beta, vbe
     DN_AUX auxiliary words ([0] = tokens that changed topic; all-reduced with the rest).
     ``rows_copy = (src, dst, rows)``: also :func:`copy_rows` in the same launch.
     ``acc = (wk, k, dk, ndk)``: the posterior-average sums [V, KS], [KS], [D, KS] (each int32 or
-    int64) also gain the new n_wk, n_k and the doc rows ``ndk`` [D, KS] (int32) in the same launch."""
+    int64) also gain the new n_wk, n_k and the doc rows ``ndk`` [D, KS] (int32) in the same launch.
+    ``inplace``: this sweep's Δn_wk is already in ``nwk`` (the count pass wrote it there: one process,
+    no X01); the Δ heads of ``dcur`` / ``dother`` are neither read nor zeroed."""
+    if inplace and absolute:
+        raise ValueError("an absolute (recount) sweep cannot apply in place")
     if acc is not None:
         wk, kk, dk, ndk = acc
         if (any(t.dtype not in (torch.int32, torch.int64) for t in (wk, kk, dk))
@@ -596,14 +601,18 @@ def gibbs_apply(nwk, dcur, dother, nk_cur, nk_next, q, qfix, V, K, KS, beta, vbe
         raise ValueError("qfix must be a [2, KS] float32 table")
     if not _is_dev(nwk):
         base = np.zeros_like(nwk.numpy()) if absolute else nwk.numpy()
-        n2, nk2, q2, qf = spec.gibbs_apply(base, dcur[: V * KS].view(V, KS).numpy(),
+        head = torch.zeros(V, KS, dtype=torch.int32) if inplace else dcur[: V * KS].view(V, KS)
+        n2, nk2, q2, qf = spec.gibbs_apply(base, head.numpy(),
                                            dcur[V * KS: V * KS + nk_rep * KS].view(-1, KS).sum(0, dtype=torch.int32).numpy(),
                                            nk_cur.numpy(), K, beta, vbeta)
         nwk.copy_(torch.from_numpy(n2))
         nk_next.copy_(torch.from_numpy(nk2))
         q.copy_(torch.from_numpy(q2))
         qfix.copy_(torch.from_numpy(qf).view_as(qfix))
-        dother.zero_()
+        if inplace:
+            dother[V * KS:].zero_()
+        else:
+            dother.zero_()
         if bump:
             sweep_ctr += 1
         if rows_copy is not None:
@@ -625,7 +634,7 @@ def gibbs_apply(nwk, dcur, dother, nk_cur, nk_next, q, qfix, V, K, KS, beta, vbe
                                           _lib.ptr(rd) if rd is not None else None,
                                           _lib.ptr(rr) if rr is not None else None, rr.numel() if rr is not None else 0,
                                           aw, ak, ad, wide, an, acc[3].shape[0] if acc is not None else 0,
-                                          _lib.stream()), "oni_gibbs_apply")
+                                          1 if inplace else 0, _lib.stream()), "oni_gibbs_apply")
 
 
 def copy_rows(src, dst, rows, KS):

@@ -42,7 +42,7 @@ class OniMH(C.Structure):
     """Mirror of ``struct OniMH`` in csrc/kernels/gibbs_mh.hip (size checked at load)."""
 
     _fields_ = [
-        ("g", OniGibbs), ("walias", vp), ("wsum", vp), ("dalias", vp), ("mh_g", vp), ("chunk_dslot", vp),
+        ("g", OniGibbs), ("wcdf", vp), ("dalias", vp), ("mh_g", vp), ("chunk_dslot", vp),
         ("chunk_len", vp), ("kalpha", f32), ("inv_alpha", f32), ("lmax", i32), ("doc_moves", i32),
     ]
 
@@ -60,7 +60,7 @@ _SIGS = {
     "oni_gibbs_sizeof_args": [],
     "oni_gibbs_mh_launch": [C.POINTER(OniMH), C.c_int, C.c_int, vp],
     "oni_mh_sizeof_args": [],
-    "oni_mh_tables": [vp, i64, C.c_int, C.c_int, vp, vp, i64, f32, vp, vp, vp, vp, f32, vp, vp],
+    "oni_mh_tables": [vp, i64, C.c_int, C.c_int, vp, vp, i64, f32, vp, vp, vp, f32, vp, vp],
     "oni_widen_pair": [vp, vp, i64, vp, vp],
     "oni_quantile_pick": [vp, vp, C.c_int, C.c_int, C.c_int, vp, vp, vp],
     "oni_tail_grid": [],
@@ -69,7 +69,7 @@ _SIGS = {
     "oni_theta_rows": [vp, i64, C.c_int, C.c_int, f32, f32, vp, C.c_int, vp],
     "oni_phi_rows": [vp, vp, i64, C.c_int, C.c_int, f32, f32, vp, C.c_int, C.c_int, vp],
     "oni_gibbs_apply": [vp, vp, vp, vp, vp, vp, vp, i64, C.c_int, C.c_int, f32, f32, vp, C.c_int, C.c_int, C.c_int,
-                        vp, vp, vp, i64, vp, vp, vp, C.c_int, vp, i64, vp],
+                        vp, vp, vp, i64, vp, vp, vp, C.c_int, vp, i64, C.c_int, vp],
     "oni_recount": [vp, vp, vp, i64, vp, C.c_int, C.c_int, C.c_int, vp],
     "oni_recount_stream": [vp, vp, i64, vp, C.c_int, C.c_int, C.c_int, vp],
     "oni_delta_recount": [vp, vp, vp, vp, vp, vp, vp, i64, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp],

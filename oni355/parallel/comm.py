@@ -114,8 +114,9 @@ class Comm:
     # -- variable-size gathers / exchanges ------------------------------------------------------
     def allgather_var(self, t: torch.Tensor) -> list[torch.Tensor]:
         """All-gather tensors whose first dim differs per rank."""
-        if not self.dist:
-            return [t]
+        if not self.dist or self.world == 1:
+            # a 1-rank group (ONI_FORCE_DIST=1) gathers its own tensor: no copy, no collective
+            return [t.to(self.device) if self.dist else t]
         if self._via_host and t.is_cuda:
             return [o.to(self.device) for o in self._host_view().allgather_var(t.cpu())]
         n = torch.full((1,), t.shape[0], dtype=torch.int64, device=self.device)
@@ -134,7 +135,10 @@ class Comm:
 
         ``recv_counts`` (when the caller already knows them, e.g. the way back of a routed
         exchange) skips the count exchange. ``return_recv_counts`` also returns them (list)."""
-        if not self.dist:
+        if not self.dist or self.world == 1:
+            # 1-rank group: the exchange is the identity (every row stays) -- no copy, no collective
+            if self.dist:
+                t = t.to(self.device)
             return (t, [int(t.shape[0])]) if return_recv_counts else t
         sc = [int(x) for x in (send_counts.tolist() if torch.is_tensor(send_counts) else send_counts)]
         if self._via_host and t.is_cuda:

@@ -333,28 +333,13 @@ def route_to_owners(doc_keys64: torch.Tensor, word_ids: torch.Tensor, weights: t
         ksend = i64_to_u32bits(ukeys[kperm]).to(torch.int32).contiguous()
         send, order, counts = oc.route_pack_ids(uown, ids, pos, word_ids.to(torch.int32).contiguous(),
                                                 weights, comm.world)
-        # both count vectors travel in one small exchange, then ONE payload alltoallv: destination
-        # r's segment is [its key list | its packed token rows] (int32 words)
+        # both count vectors travel in one small exchange, then the two payload alltoallvs
         sc = torch.stack([counts.to(torch.int64), kcounts.to(torch.int64)], 1).reshape(-1).contiguous()
         rcm = comm.alltoallv(sc.view(comm.world, 2), [1] * comm.world, recv_counts=[1] * comm.world).reshape(-1).tolist()
         rc, krc = rcm[0::2], rcm[1::2]
         scl, kcl = counts.tolist(), kcounts.tolist()
-        C = int(send.shape[1]) if send.dim() == 2 else 1
-        flat = send.reshape(-1)
-        parts, ko, so = [], 0, 0
-        for r in range(comm.world):
-            parts += [ksend[ko:ko + kcl[r]], flat[so * C:(so + scl[r]) * C]]
-            ko += kcl[r]
-            so += scl[r]
-        seg = [kcl[r] + C * scl[r] for r in range(comm.world)]
-        got = comm.alltoallv(torch.cat(parts), seg, recv_counts=[krc[r] + C * rc[r] for r in range(comm.world)])
-        kparts, tparts, off = [], [], 0
-        for r in range(comm.world):
-            kparts.append(got[off:off + krc[r]])
-            tparts.append(got[off + krc[r]:off + krc[r] + C * rc[r]])
-            off += krc[r] + C * rc[r]
-        rkeys = torch.cat(kparts)
-        recv = torch.cat(tparts).view(-1, C) if send.dim() == 2 else torch.cat(tparts)
+        rkeys = comm.alltoallv(ksend, kcl, recv_counts=krc)
+        recv = comm.alltoallv(send, scl, recv_counts=rc)
         udoc, kid = encode_docs(u32_to_i64(rkeys.view(-1)).contiguous())
         inv, wi, wt = oc.route_unpack(recv.contiguous(), rc, krc, kid, weights is not None)
         return udoc, inv, wi, wt, Route(order, scl, rc, plan)

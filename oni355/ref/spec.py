@@ -475,28 +475,82 @@ def alias_draw(tab_rows: np.ndarray, r: np.ndarray, K: int) -> np.ndarray:
     return np.where(coin < (e >> 8), j, e & 0xFF)
 
 
+MH_CDF_BUCKETS = 16  # level-1 entries per word (one 64-B row)
+
+
+def mh_bucket_width(K: int) -> int:
+    """Topics per level-1 bucket of the word proposal: 8 up to K = 128, 16 above (≤ 16 buckets)."""
+    return 8 if K <= 128 else 16
+
+
+def word_cdf(q: np.ndarray, K: int) -> np.ndarray:
+    """Level-1 table of the word proposal ∝ q[w, ·] (k_mh_cdf): topics in buckets of
+    :func:`mh_bucket_width` consecutive topics; S_b = Σ_k q_k over the bucket (sequential f32 in k),
+    C[b] = Σ_{b' ≤ b} S_b' (sequential f32), entries past the last bucket repeat the total.
+    Returns [V, 16] f32; C[:, 15] is the proposal's normaliser Z."""
+    q = np.asarray(q, dtype=F32)
+    V = q.shape[0]
+    Wb = mh_bucket_width(K)
+    nb = (K + Wb - 1) // Wb
+    C = np.zeros((V, MH_CDF_BUCKETS), dtype=F32)
+    c = np.zeros(V, dtype=F32)
+    for b in range(MH_CDF_BUCKETS):
+        if b < nb:
+            sb = np.zeros(V, dtype=F32)
+            for j in range(Wb):
+                k = b * Wb + j
+                if k < K:
+                    sb = (sb + q[:, k]).astype(F32)
+            c = (c + sb).astype(F32)
+        C[:, b] = c
+    return C
+
+
+def word_cdf_draw(C: np.ndarray, qrow: np.ndarray, r: np.ndarray, K: int) -> np.ndarray:
+    """Topic of the word proposal (inverse CDF, two levels): y = u(r)·Z; bucket b = #{i : C[i] ≤ y}
+    (capped at the last bucket); y' = y − C[b − 1] (C[−1] = 0); inside the bucket the running f32
+    sum of q from 0, topic = b·W + #{j : cum_j ≤ y'} capped at the bucket's last topic."""
+    A = C.shape[0]
+    ar = np.arange(A)
+    Wb = mh_bucket_width(K)
+    nb = (K + Wb - 1) // Wb
+    y = (u01(r) * C[:, MH_CDF_BUCKETS - 1]).astype(F32)
+    b = np.minimum((C <= y[:, None]).sum(axis=1), nb - 1)
+    base = np.where(b > 0, C[ar, np.maximum(b - 1, 0)], F32(0)).astype(F32)
+    y2 = (y - base).astype(F32)
+    cum = np.zeros(A, dtype=F32)
+    cnt = np.zeros(A, dtype=np.int64)
+    for j in range(Wb):
+        k = b * Wb + j
+        ok = k < K
+        cum = (cum + np.where(ok, qrow[ar, np.minimum(k, K - 1)], F32(0))).astype(F32)
+        cnt += (ok & (cum <= y2)).astype(np.int64)
+    last = np.minimum(Wb, K - b * Wb) - 1
+    return b * Wb + np.minimum(cnt, last)
+
+
 def mh_tables(q: np.ndarray, nk: np.ndarray, ndk_src: np.ndarray, long_rows: np.ndarray, K: int, alpha: float,
               vbeta: float):
-    """Per-sweep tables of the MH sampler (k_mh_alias): the word proposal ∝ q[w, k] (sweep-start
-    word factor) of every word with its row sum, the doc proposal ∝ n_dk + α (sweep-start row) of
-    every document over several chunks, and g_k = 1/(n_k + Vβ + 1) (the word factor a token adds
-    to a topic it moves into). Returns (walias [V, K] u32 entries, wsum [V] f32, dalias [n_long, K] u32,
-    g [KS] f32)."""
-    walias, wsum = alias_table(q[:, :K])
+    """Per-sweep tables of the MH sampler (k_mh_cdf / k_mh_alias): the word proposal ∝ q[w, k]
+    (sweep-start word factor) as every word's level-1 CDF row (:func:`word_cdf`; the second level
+    is the q row itself), the doc proposal ∝ n_dk + α (sweep-start row) of every document over
+    several chunks as alias rows, and g_k = 1/(n_k + Vβ + 1) (the word factor a token adds to a
+    topic it moves into). Returns (wcdf [V, 16] f32, dalias [n_long, K] u32, g [KS] f32)."""
+    wcdf = word_cdf(q[:, :K], K)
     b = ndk_src[np.asarray(long_rows, dtype=np.int64), :K].astype(F32) + F32(alpha)
     dalias = alias_table(b)[0] if b.shape[0] else np.zeros((0, K), dtype=U32)
     g = (F32(1) / ((nk.astype(F32) + F32(vbeta)).astype(F32) + F32(1))).astype(F32)
-    return walias, wsum, dalias, g
+    return wcdf, dalias, g
 
 
-def mh_moves(nn, bb, qrow, zo, qe, multi, Nd, s, zslice, drows, wrows, wsum, g, pos, key, sweep, seed0, seed1,
+def mh_moves(nn, bb, qrow, zo, qe, multi, Nd, s, zslice, drows, wcdf, g, pos, key, sweep, seed0, seed1,
              K, alpha, doc_moves=1):
     """The MH moves of one token per row (see :func:`gibbs_pass_mh`). ``nn`` doc counts without the
     token (the chunk's view), ``bb`` sweep-start doc rows (with the token), ``qrow`` sweep-start q
     rows (with the token), ``qe`` the word factor of ``zo`` without it, ``Nd`` other tokens in the
     chunk, ``s`` the token's position, ``zslice`` current topics of the chunk's positions,
-    ``drows`` / ``wrows`` alias rows of the doc (multi-chunk docs) / word, ``wsum`` the word
-    rows' sums, ``g`` [KS] = 1/(D + 1). Returns the new topics."""
+    ``drows`` alias rows of the doc (multi-chunk docs), ``wcdf`` the word's level-1 CDF rows
+    (:func:`word_cdf`; Z = wcdf[:, 15]), ``g`` [KS] = 1/(D + 1). Returns the new topics."""
     A = zo.shape[0]
     ar = np.arange(A)
     a32 = F32(alpha)
@@ -514,9 +568,10 @@ def mh_moves(nn, bb, qrow, zo, qe, multi, Nd, s, zslice, drows, wrows, wsum, g, 
 
     def bn(k):  # sweep-start doc row without the token, + α
         return ((bb[ar, k] - (k == zo)).astype(F32) + a32).astype(F32)
-    # word move (from zo; proposal = the word's table, built with the token at zo)
+    # word move (from zo; proposal = the word's CDF over the snapshot q, which holds the token at zo)
     r0, r1, r2, r3 = philox10(pos, key, U32(sweep), U32(2), seed0, seed1)
-    t = alias_draw(wrows, r0, K)
+    t = word_cdf_draw(wcdf, qrow, r0, K)
+    wsum = wcdf[:, MH_CDF_BUCKETS - 1]
     d = (qrow[ar, zo] - qe).astype(F32)
     zt = ((wsum - d).astype(F32) + ((one - qrow[ar, t]).astype(F32) * g[t]).astype(F32)).astype(F32)
     num = (aw(t) * wsum).astype(F32)
@@ -562,8 +617,9 @@ def gibbs_pass_mh(st: dict, KS: int, K: int, alpha: float, seed0: int, seed1: in
     current state x -- a kernel reversible w.r.t. π, so their composition leaves π invariant
     (tests/test_mh_conditional.py). Philox blocks (pos, doc key, sweep, 2 + c) → r0..r3:
 
-    * word move, from zo only (r0 proposes t from the word's alias table ∝ q[w, ·], r1 accepts):
-      ratio (n_t^¬+α)·Z_zo / ((n_zo^¬+α)·Z_t) with Z_zo = Σ_k q[w, k] (the table's sum) and
+    * word move, from zo only (r0 proposes t ∝ q[w, ·] by the two-level inverse CDF
+      :func:`word_cdf_draw` -- level 1 the per-sweep bucket sums, level 2 the q row itself -- r1
+      accepts): ratio (n_t^¬+α)·Z_zo / ((n_zo^¬+α)·Z_t) with Z_zo = the CDF's total and
       Z_t = (Z_zo − (q_zo − q'_zo)) + (1 − q_t)·g_t, the sum the table would have with the token
       at t (g_t = 1/(D_t + 1)).
     * ``doc_moves`` doc moves (r2 proposes, r3 accepts; move c > 0 draws (r2, r3) from
@@ -575,8 +631,8 @@ def gibbs_pass_mh(st: dict, KS: int, K: int, alpha: float, seed0: int, seed1: in
       (n_t^¬+α)·q'_t·(b_x^¬+α) / ((n_x^¬+α)·q'_x·(b_t^¬+α)), b^¬ = b without the token; a draw of
       zo from x ≠ zo is kept with probability (b_zo^¬ + α)/(b_zo + α) first.
 
-    A move is taken when u(r)·den < num (f32). st as for :func:`gibbs_pass` plus ``walias``
-    [V, K] u32 alias entries, ``wsum`` [V] f32, ``dalias`` [n_long, K] u32, ``mh_g`` [KS] f32 (:func:`mh_tables`)
+    A move is taken when u(r)·den < num (f32). st as for :func:`gibbs_pass` plus ``wcdf``
+    [V, 16] f32 (the word proposal's level-1 CDF rows), ``dalias`` [n_long, K] u32, ``mh_g`` [KS] f32 (:func:`mh_tables`)
     and ``chunk_dslot`` [C] i32 (row of dalias of a multi-chunk doc's chunk, −1 otherwise)."""
     S = 64
     slc, lane = _chunk_geometry(st, S)
@@ -592,7 +648,7 @@ def gibbs_pass_mh(st: dict, KS: int, K: int, alpha: float, seed0: int, seed1: in
     if clen.max(initial=0) > MH_MAX_CHUNK:
         raise ValueError("the MH sampler needs chunks of at most 127 tokens")
     qfix = st["qfix"]
-    walias, dalias = st["walias"], st["dalias"]
+    wcdf, dalias = st["wcdf"], st["dalias"]
     dslot = st["chunk_dslot"].astype(np.int64)
     base = st["slice_off"][slc].astype(np.int64) + lane
     for s in range(int(clen.max(initial=0))):
@@ -608,8 +664,8 @@ def gibbs_pass_mh(st: dict, KS: int, K: int, alpha: float, seed0: int, seed1: in
         zp = np.minimum(np.arange(int(clen[act].max()))[None, :], clen[act][:, None] - 1)
         zslice = st["tok_z"][base[act][:, None] + zp * S].astype(np.int64)
         zn = mh_moves(n[act], b[act], qrow, zo, qe, multi_c[act], clen[act] - 1, s, zslice,
-                      dalias[np.where(multi_c[act], dslot[act], 0)] if dalias.shape[0] else None, walias[w],
-                      st["wsum"][w], st["mh_g"], pos, st["chunk_key"][act], sweep, seed0, seed1, K, alpha,
+                      dalias[np.where(multi_c[act], dslot[act], 0)] if dalias.shape[0] else None, wcdf[w],
+                      st["mh_g"], pos, st["chunk_key"][act], sweep, seed0, seed1, K, alpha,
                       doc_moves)
         n[act, zn] += 1
         ch = zn != zo

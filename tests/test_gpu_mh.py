@@ -25,7 +25,8 @@ def _toy(n_docs, V, seed):
 
 @pytest.mark.parametrize("K,V", [(7, 1000), (40, 1000), (100, 1000), (255, 1000), (40, 70001)])
 def test_alias_tables_bitwise(gpu, K, V):
-    """V ≥ 65536: the word entries go out row by row, lanes along k (the large-vocabulary path)."""
+    """Word CDF rows (k_mh_cdf: buckets of 8 topics up to K = 128, 16 above) and the multi-chunk
+    documents' alias rows (k_mh_alias), bit for bit."""
     r = np.random.default_rng(K)
     KS = (K + 3) // 4 * 4
     q = np.zeros((V, KS), np.float32)
@@ -35,16 +36,15 @@ def test_alias_tables_bitwise(gpu, K, V):
     ndk[:, K:] = 0
     rows = np.array([0, 5, 7, 199], np.int32)
     nk = r.integers(0, 10**6, KS).astype(np.int32)
-    wa, ws, da, g = spec.mh_tables(q, nk, ndk, rows, K, 0.37, 17.5)
+    wc, da, g = spec.mh_tables(q, nk, ndk, rows, K, 0.37, 17.5)
     dev = torch.device(gpu)
-    out = [torch.zeros(V, K, dtype=torch.int32, device=dev), torch.zeros(V, device=dev),
-           torch.zeros(len(rows), K, dtype=torch.int32, device=dev), torch.zeros(KS, device=dev)]
+    out = [torch.zeros(V, 16, device=dev), torch.zeros(len(rows), K, dtype=torch.int32, device=dev),
+           torch.zeros(KS, device=dev)]
     ops.mh_tables(torch.from_numpy(q).to(dev), torch.from_numpy(nk).to(dev), torch.from_numpy(ndk).to(dev),
                   torch.from_numpy(rows).to(dev), K, 0.37, 17.5, *out)
-    assert np.array_equal(out[0].cpu().numpy().view(np.uint32), wa)
-    assert np.array_equal(out[1].cpu().numpy(), ws)
-    assert np.array_equal(out[2].cpu().numpy().view(np.uint32), da)
-    assert np.array_equal(out[3].cpu().numpy(), g)
+    assert np.array_equal(out[0].cpu().numpy(), wc)
+    assert np.array_equal(out[1].cpu().numpy().view(np.uint32), da)
+    assert np.array_equal(out[2].cpu().numpy(), g)
 
 
 _CASES = [(100, "recount", 1, 64), (100, "wdelta", 1, 64), (100, "atomic", 1, 64), (100, "dual", 1, 64),
@@ -72,7 +72,7 @@ def test_mh_sweep_bitwise_vs_oracle(gpu, K, mode, dm, L, monkeypatch):
     for _ in range(3):
         mc.sweep(1)
         mg.sweep(1)
-        assert torch.equal(mc.walias, mg.walias.cpu()) and torch.equal(mc.wsum, mg.wsum.cpu())
+        assert torch.equal(mc.wcdf, mg.wcdf.cpu())
         assert torch.equal(mc.dalias, mg.dalias.cpu()) and torch.equal(mc.mh_g, mg.mh_g.cpu())
         assert torch.equal(mc.tok_z, mg.tok_z.cpu())
         assert torch.equal(mc.ndk_cur, mg.ndk_cur.cpu())

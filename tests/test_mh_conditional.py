@@ -4,11 +4,12 @@ conditional invariant (verdict r3 next-round item 2: "exact-stationary under MH"
 Stationarity check of the oracle's token moves (spec.mh_moves): for a token with fixed other
 counts, π(k) ∝ (n_dk^¬ + α)·q'_k does not depend on the token's own topic zo. Each replica draws zo
 from π, builds the sweep-start state that CONTAINS the token at zo (doc row b, q row with q_zo such
-that fma(q_zo, A_zo, −B_zo) = q'_zo, the word's alias table of that q row) and runs the MH moves
+that fma(q_zo, A_zo, −B_zo) = q'_zo, the word's level-1 CDF of that q row) and runs the MH moves
 from zo with its own Philox stream. If every move is a correct MH step, the output topics are again
 distributed as π (chi-square), for one-chunk documents (proposals from the chunk's other tokens)
 and documents over several chunks (proposals from the sweep-start row's alias table), one and two
-cycles. Plus: the alias tables reproduce their weights, and the MH chain runs through GibbsLDA.
+cycles. Plus: the alias tables and the two-level word CDF reproduce their weights, and the MH chain
+runs through GibbsLDA.
 """
 from __future__ import annotations
 
@@ -39,8 +40,8 @@ def _case(K, alpha, multi, R=120_000, Ld=7, s=2, seed=5, beta=0.01, V=50, stale=
     pi = (nn + alpha) * qrest
     pi /= pi.sum()
     zo = r.choice(K, size=R, p=pi)
-    # snapshot with the token at z (k_apply's numerics): q rows, qfix, g and the word's alias table
-    qrows, qfixes, gs, wal, wsums = [], [], [], [], []
+    # snapshot with the token at z (k_apply's numerics): q rows, qfix, g and the word's CDF
+    qrows, qfixes, gs, wcd = [], [], [], []
     for z in range(K):
         nw = nw_rest.copy(); nw[z] += 1
         nk = nk_rest.copy(); nk[z] += 1
@@ -48,10 +49,9 @@ def _case(K, alpha, multi, R=120_000, Ld=7, s=2, seed=5, beta=0.01, V=50, stale=
         q = ((nw.astype(F32) + F32(beta)) / den).astype(F32)
         qrows.append(q)
         qfixes.append(spec.gibbs_qfix(nk.astype(np.int32), K, float(vbeta)))
-        t, tot = spec.alias_table(q[None, :])
-        wal.append(t[0]); wsums.append(tot[0])
+        wcd.append(spec.word_cdf(q[None, :], K)[0])
         gs.append((F32(1) / (den + F32(1))).astype(F32))
-    qrows, wal, wsums, gs = map(np.array, (qrows, wal, wsums, gs))
+    qrows, wcd, gs = map(np.array, (qrows, wcd, gs))
     qrow = qrows[zo]
     qe = np.array([spec.excluded_q(qrows[z][z:z + 1], np.array([z]), qfixes[z])[0] for z in range(K)])[zo]
     # sweep-start doc row: the chunk's view without the token + stale counts of other chunks + the token
@@ -64,7 +64,7 @@ def _case(K, alpha, multi, R=120_000, Ld=7, s=2, seed=5, beta=0.01, V=50, stale=
     zslice[:, s] = zo
     return pi, zo, dict(nn=np.tile(nn, (R, 1)).astype(np.int32), bb=bb, qrow=qrow, zo=zo, qe=qe,
                         multi=np.full(R, multi), Nd=np.full(R, Ld - 1), s=s, zslice=zslice, drows=drows,
-                        wrows=wal[zo], wsum=wsums[zo], gs=gs)
+                        wcdf=wcd[zo], gs=gs)
 
 
 @pytest.mark.parametrize("K,alpha", [(7, 0.5), (20, 2.5), (9, 50 / 9)])
@@ -86,7 +86,7 @@ def test_mh_moves_leave_the_conditional_invariant(K, alpha, multi, doc_moves):
         g = a["gs"][(z + 1) % K].copy()
         sub = {k: (v[m] if isinstance(v, np.ndarray) and v.shape[:1] == (R,) else v) for k, v in a.items()}
         zn[m] = spec.mh_moves(sub["nn"], sub["bb"], sub["qrow"], sub["zo"], sub["qe"], sub["multi"], sub["Nd"],
-                              a["s"], sub["zslice"], sub["drows"], sub["wrows"], sub["wsum"], g, pos[m], key[m], 11,
+                              a["s"], sub["zslice"], sub["drows"], sub["wcdf"], g, pos[m], key[m], 11,
                               0x1234, 0x5678, K, alpha, doc_moves)
     moved = float((zn != zo).mean())
     assert moved > 0.05, moved  # the moves are not all rejected
@@ -118,6 +118,24 @@ def test_alias_tables_reproduce_their_weights():
         got = spec.alias_draw(np.repeat(t[:1], rr.size, 0), rr, K)
         h = np.bincount(got, minlength=K) / rr.size
         assert np.abs(h - ref[0]).max() < 0.01
+
+
+@pytest.mark.parametrize("K", [3, 7, 20, 100, 129, 255])
+def test_word_cdf_draw_reproduces_q(K):
+    """The two-level inverse CDF draws topic k with probability q_k / Σq (buckets of 8 topics up to
+    K = 128, 16 above; padding and empty topics never drawn)."""
+    r = np.random.default_rng(K)
+    q = (r.random((1, K)) ** 5 * 0.2).astype(F32)
+    q[0, r.integers(0, K, max(1, K // 5))] = 0  # empty topics
+    C = spec.word_cdf(q, K)
+    assert np.isclose(C[0, -1], q.sum(), rtol=1e-5)
+    n = 400_000
+    rr = r.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    got = spec.word_cdf_draw(np.repeat(C, n, 0), np.repeat(q, n, 0), rr, K)
+    h = np.bincount(got, minlength=K) / n
+    ref = q[0] / q[0].sum(dtype=np.float64)
+    assert got.max() < K and not h[ref == 0].any()
+    assert np.abs(h - ref).max() < 0.006, np.abs(h - ref).max()
 
 
 def test_mh_chain_through_the_model_cpu():

@@ -41,6 +41,9 @@ def main() -> int:
     ap.add_argument("--tiny", type=int, default=6, help="flows in the day of a 'tiny' host")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--lt-codebook", type=float, default=0.01)
+    ap.add_argument("--rounds", type=int, default=2,
+                    help="feedback rounds: each reviews the latest top-N, marks its new false positives and "
+                         "reruns the day with every verdict so far")
     a = ap.parse_args()
     import torch
 
@@ -75,33 +78,46 @@ def main() -> int:
         rows = np.asarray(res.rows[: a.maxresults], dtype=np.int64)
         return res, rows, el
 
-    res1, rows1, t1 = one_run(None)
-    res_csv = os.path.join(lp, "flow", date, "flow_results.csv")
-    rio.write_rendered(res_csv, schema.result_columns("flow"), rio.render_result("flow", day.cols, res1, 0))
-    assert oa.main(["-d", date, "-t", "flow", "--lpath", lp, "--config", os.path.join(lp, "none.conf")]) == 0
-    review = rows1 if a.review <= 0 else rows1[: a.review]
-    fp_idx = [i for i, r in enumerate(review) if r not in set(planted.tolist())]
-    fp_rows = review[fp_idx]
-    assert oa.main(["score", "-d", date, "-t", "flow", "--lpath", lp, "--config", os.path.join(lp, "none.conf"),
-                    "--rows", ",".join(map(str, fp_idx)), "--sev", "3"]) == 0
-    assert oa.main(["publish", "-d", date, "-t", "flow", "--lpath", lp, "--config", os.path.join(lp, "none.conf")]) == 0
-    fb = fbm.load_feedback(rio.scores_path(lp, "flow"), "flow")
-    n_fb = len(fb["sip"]) if fb else 0
-    res2, rows2, t2 = one_run(fb)
-    pos2 = {int(r): i for i, r in enumerate(rows2)}
-    still = [pos2[int(r)] for r in fp_rows if int(r) in pos2]
-    tiny = np.minimum(flows_of(sip[fp_rows]), flows_of(dip[fp_rows])) <= a.tiny
+    cfgp = os.path.join(lp, "none.conf")
+    planted_set = set(planted.tolist())
+
+    def review(res, rows, rnd):
+        """The analyst's pass over one day's results: enrich, mark the unplanted rows benign, publish."""
+        res_csv = os.path.join(lp, "flow", date, "flow_results.csv")
+        rio.write_rendered(res_csv, schema.result_columns("flow"), rio.render_result("flow", day.cols, res, 0))
+        assert oa.main(["-d", date, "-t", "flow", "--lpath", lp, "--config", cfgp]) == 0
+        seen = rows if a.review <= 0 else rows[: a.review]
+        idx = [i for i, r in enumerate(seen) if int(r) not in planted_set]
+        if idx:
+            assert oa.main(["score", "-d", date, "-t", "flow", "--lpath", lp, "--config", cfgp,
+                            "--rows", ",".join(map(str, idx)), "--sev", "3"]) == 0
+        assert oa.main(["publish", "-d", date, "-t", "flow", "--lpath", lp, "--config", cfgp]) == 0
+        return seen[idx], fbm.load_feedback(rio.scores_path(lp, "flow"), "flow")
+
+    res, rows, t = one_run(None)
+    rounds = [{"recall": round(float(np.isin(planted, rows).mean()), 4), "day_s": round(t, 3)}]
+    fb_all, marked_all = None, np.zeros(0, np.int64)
+    for rnd in range(a.rounds):
+        marked, fb = review(res, rows, rnd)
+        marked_all = np.concatenate([marked_all, marked])
+        if fb is not None:
+            # the analyst's verdicts accumulate over the rounds (each publish holds one day's review)
+            fb_all = fb if fb_all is None else {k: (np.concatenate([fb_all[k], fb[k]]) if isinstance(fb[k], np.ndarray)
+                                                    else fb[k]) for k in fb}
+        res, rows, t = one_run(fb_all)
+        pos = {int(r): i for i, r in enumerate(rows)}
+        still = [pos[int(r)] for r in marked_all if int(r) in pos]
+        tiny = np.minimum(flows_of(sip[marked]), flows_of(dip[marked])) <= a.tiny if marked.size else np.zeros(0, bool)
+        rounds.append({"recall": round(float(np.isin(planted, rows).mean()), 4), "day_s": round(t, 3),
+                       "marked_this_round": int(marked.size), "marked_tiny_host_rows": int(tiny.sum()),
+                       "feedback_rows_total": int(len(fb_all["sip"])) if fb_all else 0,
+                       "marked_still_in_topN": len(still),
+                       "marked_still_in_topN_median_rank": (int(np.median(still)) + 1) if still else None})
     out = {
-        "flows": a.flows, "vocab": int(res1.lda.vocab.numel()), "maxresults": a.maxresults,
-        "planted": int(planted.size),
-        "recall_before": round(float(np.isin(planted, rows1).mean()), 4),
-        "recall_after": round(float(np.isin(planted, rows2).mean()), 4),
-        "reviewed_rows": int(review.size), "marked_sev3": int(fp_rows.size), "feedback_rows_loaded": n_fb,
-        "marked_tiny_host_rows": int(tiny.sum()),
-        "marked_still_in_topN": len(still),
-        "marked_still_in_topN_median_rank": (int(np.median(still)) + 1) if still else None,
-        "day_s": [round(t1, 3), round(t2, 3)], "dupfactor": a.dupfactor, "sweeps": a.sweeps,
-        "total_s": round(time.perf_counter() - t0, 1),
+        "flows": a.flows, "vocab": int(res.lda.vocab.numel()), "maxresults": a.maxresults,
+        "planted": int(planted.size), "recall_before": rounds[0]["recall"], "recall_after": rounds[-1]["recall"],
+        "rounds": rounds, "reviewed_rows_per_round": a.review or a.maxresults, "dupfactor": a.dupfactor,
+        "sweeps": a.sweeps, "total_s": round(time.perf_counter() - t0, 1),
         "path": "results CSV -> oni-oa enrich -> oni-oa score --sev 3 -> oni-oa publish -> oni-ml feedback",
     }
     print(json.dumps(out), flush=True)

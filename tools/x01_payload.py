@@ -32,8 +32,8 @@ def main() -> int:
     from oni355.synth.flow import generate_flows
 
     dev = torch.device("cuda:0")
-    _, KP = ops.choose_tiling(a.K)
-    G, _ = ops.choose_tiling(a.K)
+    from oni355.models.gibbs import tiling_for
+    G, KP = tiling_for(a.K)  # the tiling the model of K topics samples with (K ≥ 100: MH, KS = K)
     KS = G * KP
     Wmax = max(int(w) for w in a.worlds.split(","))
     shard_words, cuts = [], None
