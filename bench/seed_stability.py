@@ -34,7 +34,7 @@ def main() -> int:
     from oni355.synth.flow import generate_flows
 
     out = {"flows": a.flows, "maxresults": a.maxresults, "sweeps": a.sweeps, "post_samples":
-           os.environ.get("ONI_POST_SAMPLES", "default"), "days": {}}
+           os.environ.get("ONI_POST_SAMPLES", "default"), "chains": int(os.environ.get("ONI_CHAINS", "1")), "days": {}}
     for kind in a.days.split(","):
         day = generate_flows(a.flows, seed=7, wide_vocab=kind == "realistic")
         planted = set(np.asarray(day.anomaly_rows).tolist())

@@ -31,7 +31,9 @@
 
 struct OniMH {
   OniGibbs g;
-  const float* wcdf;           // [V][16] level-1 CDF of the word proposal ∝ q[w, ·] (k_mh_cdf)
+  const uint4* walias;         // [V][K] alias word proposal records {thr24 << 8 | alias, q_j, q_alias, Σ q} (wp 0)
+  const float* wsum;           // [V] Σ_k q[w, k] (wp 0)
+  const float* wcdf;           // [V][16] level-1 CDF rows of the word proposal ∝ q[w, ·] (wp 8 / 16, k_mh_cdf)
   const uint32_t* dalias;      // [n_long][K] alias entries of the multi-chunk docs' n_src + α
   const float* mh_g;           // [KS] 1 / (n_k + Vβ + 1)
   const int32_t* chunk_dslot;  // [C] row of dalias (multi-chunk doc) or -1
@@ -40,6 +42,7 @@ struct OniMH {
   float inv_alpha;             // f32(1/α)
   int32_t lmax;                // longest chunk (LDS topic slice rows)
   int32_t doc_moves;           // 1 or 2
+  int32_t wp;                  // word proposal: 0 alias records, 8 / 16 two-level CDF (bucket width)
 };
 
 namespace {
@@ -57,47 +60,65 @@ __device__ __forceinline__ int alias_resolve(int j, uint32_t coin, uint32_t e) {
   return coin < (e >> 8) ? j : (int)(e & 0xFFu);
 }
 
-// ---- doc proposal tables ------------------------------------------------------------------------
-// One lane per multi-chunk document: its sweep-start row + α. Sequential f32 per lane, exactly
-// spec.alias_table: sum, scale, classify into the small / large stacks (one u8 array: small grows up
-// from 0, large down from K − 1), pair off, leftovers keep their own index; p / entries / stack live
-// in LDS transposed to [k][row] for the per-lane sequential part. Block 0 also writes
-// g_k = 1/(n_k + Vβ + 1).
-__global__ __launch_bounds__(64) void k_mh_alias(int K, int KS, const int32_t* __restrict__ ndk,
-                                                  const int32_t* __restrict__ rows, int64_t n_long, float alpha,
-                                                  uint32_t* __restrict__ dalias, const int32_t* __restrict__ nk,
-                                                  float vbeta, float* __restrict__ g) {
+// ---- proposal tables ---------------------------------------------------------------------------
+// One lane per row (rows [0, V): word rows of q; rows [V, V + n_long): sweep-start rows of the
+// multi-chunk docs + α). Sequential f32 per lane, exactly spec.alias_table: sum, scale, classify
+// into the small / large stacks (one u8 array: small grows up from 0, large down from K − 1),
+// pair off, leftovers keep their own index. The rows are read and written cooperatively (the wave
+// walks its 64 rows, lanes along k: coalesced), p / entries / stack live in LDS transposed to
+// [k][row] for the per-lane sequential part.
+// Word rows (the alias word proposal, small vocabularies) are written as 16-B records {entry, q_j,
+// q_alias(j), Σ_k q_k}: the sampler's one gather of a word proposal then also brings q_t and the row
+// sum (the word move's ratio), so a token costs three scattered loads (record, q[w, zo], q[w, t_doc])
+// instead of five. With V = 0 only the documents' rows (and g) are built (the CDF word proposal).
+__global__ __launch_bounds__(64) void k_mh_alias(const float* __restrict__ q, int64_t V, int K, int KS,
+                                                  const int32_t* __restrict__ ndk, const int32_t* __restrict__ rows,
+                                                  int64_t n_long, float alpha, uint4* __restrict__ wrec,
+                                                  float* __restrict__ wsum, uint32_t* __restrict__ dalias,
+                                                  const int32_t* __restrict__ nk, float vbeta, float* __restrict__ g,
+                                                  bool coal) {
   extern __shared__ __align__(16) unsigned char smem_alias[];
   // p is [K][65], one column per lane. The entries share its storage: Vose writes entry s once
   // p[s] is spent (s is the popped small, whose weight is already in a register, or the carried
   // large, whose weight lives in a register), and the leftovers get their own index after the
-  // pairing (32 instead of 58 KB per wave at K = 100)
+  // pairing; 32 instead of 58 KB per wave at K = 100 (4 waves per CU instead of 2)
   float* p = reinterpret_cast<float*>(smem_alias);
   uint32_t* ent = reinterpret_cast<uint32_t*>(smem_alias);
-  uint8_t* stk = smem_alias + (size_t)K * kAS * sizeof(float);  // [K][64]
+  float* tots = reinterpret_cast<float*>(smem_alias + (size_t)K * kAS * sizeof(float));   // [64]
+  uint8_t* stk = smem_alias + (size_t)K * kAS * sizeof(float) + 64 * sizeof(float);      // [K][64]
   const int lane = threadIdx.x;
   if (blockIdx.x == 0) {
     for (int k = lane; k < KS; k += 64) g[k] = 1.0f / (((float)nk[k] + vbeta) + 1.0f);
   }
   const int64_t r0 = (int64_t)blockIdx.x * 64;
-  const int nrows = (int)((n_long - r0) < 64 ? (n_long - r0) : 64);
+  const int nrows = (int)((V + n_long - r0) < 64 ? (V + n_long - r0) : 64);
+  // each lane loads its own row (16-B vectors; K rows of q are KS-strided, KS % 4 == 0)
   const int64_t row = r0 + lane;
   const bool has = lane < nrows;
-  const int32_t* br = ndk + (has ? (int64_t)rows[row] : 0) * KS;
+  const bool word = has && row < V;
+  const float* qr = q + (word ? row : 0) * KS;
+  const int32_t* br = ndk + (has && !word ? (int64_t)rows[row - V] : 0) * KS;
   if (has) {
 #pragma unroll 4
     for (int k = 0; k < K; k += 4) {
-      const int4 c = *reinterpret_cast<const int4*>(br + k);
-      p[k * kAS + lane] = (float)c.x + alpha;
-      if (k + 1 < K) p[(k + 1) * kAS + lane] = (float)c.y + alpha;
-      if (k + 2 < K) p[(k + 2) * kAS + lane] = (float)c.z + alpha;
-      if (k + 3 < K) p[(k + 3) * kAS + lane] = (float)c.w + alpha;
+      float4 v;
+      if (word) {
+        v = *reinterpret_cast<const float4*>(qr + k);
+      } else {
+        const int4 c = *reinterpret_cast<const int4*>(br + k);
+        v = make_float4((float)c.x + alpha, (float)c.y + alpha, (float)c.z + alpha, (float)c.w + alpha);
+      }
+      p[k * kAS + lane] = v.x;
+      if (k + 1 < K) p[(k + 1) * kAS + lane] = v.y;
+      if (k + 2 < K) p[(k + 2) * kAS + lane] = v.z;
+      if (k + 3 < K) p[(k + 3) * kAS + lane] = v.w;
     }
   }
   __syncthreads();
-  if (has) {
+  if (lane < nrows) {
     float tot = 0.f;
     for (int k = 0; k < K; ++k) tot = tot + p[k * kAS + lane];
+    tots[lane] = tot;
     const float scale = (float)K / tot;
     int ns = 0, nl = 0;
     for (int k = 0; k < K; ++k) {
@@ -146,10 +167,38 @@ __global__ __launch_bounds__(64) void k_mh_alias(int K, int KS, const int32_t* _
     }
   }
   __syncthreads();
-  if (has) {
-    uint32_t* out = dalias + row * K;
+  // large vocabularies (many waves: store-throughput bound): word rows go out one row at a time,
+  // lanes along k, so each store instruction writes 64 consecutive 16-B records (a lane per row
+  // touches 64 rows K·16 B apart per store): 0.288 -> 0.244 ms at V = 180k, K = 100. Small ones
+  // (few waves: latency bound) keep a lane per row: 0.049 vs 0.058 ms at V = 6.5k.
+  const int nw = coal ? (int)(V - r0 < (int64_t)nrows ? (V - r0 > 0 ? V - r0 : 0) : nrows) : 0;
+  if (!coal && word) {
+    const uint32_t tb = __float_as_uint(tots[lane]);
+    uint4* out = wrec + row * K;
 #pragma unroll 4
-    for (int k = 0; k < K; ++k) out[k] = ent[k * kAS + lane];
+    for (int k = 0; k < K; ++k) {
+      const uint32_t e = ent[k * kAS + lane];
+      out[k] = make_uint4(e, __float_as_uint(qr[k]), __float_as_uint(qr[e & 0xFFu]), tb);
+    }
+  }
+#pragma unroll 2
+  for (int r = 0; r < nw; ++r) {
+    const float* qq = q + (r0 + r) * KS;
+    const uint32_t tb = __float_as_uint(tots[r]);
+    uint4* out = wrec + (r0 + r) * K;
+    for (int k = lane; k < K; k += 64) {
+      const uint32_t e = ent[k * kAS + r];
+      out[k] = make_uint4(e, __float_as_uint(qq[k]), __float_as_uint(qq[e & 0xFFu]), tb);
+    }
+  }
+  if (has) {
+    if (word) {
+      wsum[row] = tots[lane];
+    } else {
+      uint32_t* out = dalias + (row - V) * K;
+#pragma unroll 4
+      for (int k = 0; k < K; ++k) out[k] = ent[k * kAS + lane];
+    }
   }
 }
 
@@ -210,8 +259,9 @@ struct MHB {
   oni::U4 r;     // Philox block (pos, key, sweep, 2)
   int zo;        // sweep-start topic
   float qz;      // q[w, zo]
-  float zw;      // Σ_k q[w, k] as the word CDF's total Z
-  float qtw;     // q[w, tw] (stage C, from the bucket's q values)
+  uint4 rw;      // wp 0: word proposal record at j(r.x): {entry, q_j, q_alias, Σ_k q_k}
+  float zw;      // wp > 0: Σ_k q[w, k] as the word CDF's total Z
+  float qtw;     // wp > 0: q[w, tw] (stage C, from the bucket's q values)
   uint32_t ed;   // doc alias entry at j(r.z) (read for every chunk; used by multi-chunk docs)
   int32_t bzo;   // n_src[doc, zo]
   // stage C (issued at the end of the previous step, once that token has moved)
@@ -230,8 +280,9 @@ struct MHB {
 // on one common address for the doc tables) and every decision is a select, so no loaded value is
 // merged at a control-flow join -- a merge there makes the compiler wait for every outstanding
 // memory op (vmcnt(0)), which serialised the token pipeline.
-template <int MODE, int DM, int WB>
+template <int MODE, int DM, int WP>
 struct MHLane {
+  static constexpr int WB = WP > 0 ? WP : 1;
   const OniMH& m;
   const OniGibbs& a;
   MHLds L;
@@ -264,6 +315,9 @@ struct MHLane {
   __device__ __forceinline__ float aw(int c, int32_t bk) const {
     return (float)(multi ? bk + c - kMHBias : c) + a.alpha;
   }
+  __device__ __forceinline__ bool alias_keeps(uint32_t r, uint32_t e) const {
+    return ((r * (uint32_t)K) >> 8) < (e >> 8);
+  }
   __device__ __forceinline__ int alias_draw(uint32_t r, uint32_t e) const {
     const int j = (int)__umulhi(r, (uint32_t)K);
     return alias_resolve(j, (r * (uint32_t)K) >> 8, e);
@@ -283,6 +337,7 @@ struct MHLane {
 
   // level-1 word CDF row of word w (a stage ahead of its stage B: its bucket gather depends on it)
   __device__ __forceinline__ void load_c1(uint32_t w) {
+    if constexpr (WP == 0) return;
     const float4* r = reinterpret_cast<const float4*>(m.wcdf) + (int64_t)(w == oni::kPadWord ? 0u : w) * 4;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -302,16 +357,21 @@ struct MHLane {
     const int z0 = (int)L.zsl[s * 64 + lane];
     x.zo = z0 < K - 1 ? z0 : K - 1;  // padding slots hold 0; clamp anyway: an LDS index
     x.qz = a.q[wc * (uint32_t)KS + (uint32_t)x.zo];
+    if constexpr (WP == 0) {
+      x.rw = m.walias[wc * (uint32_t)K + __umulhi(x.r.x, (uint32_t)K)];
+    } else {
     // word proposal, level 1: y = u·Z, bucket = #{i : C[i] ≤ y} (capped; a branch-free binary search
-    // over the monotone row), residual y − C[b − 1] (C[b − 1] gathered from the row's cache line,
-    // not selected out of 16 registers)
-    {
+    // over the monotone row), residual y − C[b − 1]
       const int nb = (K + WB - 1) / WB;
       x.zw = c1[15];
       ywd = oni::u01(x.r.x) * c1[15];
       const int nbk = count_le<16>(c1, 0.f, ywd);
       bk = nbk < nb - 1 ? nbk : nb - 1;
-      base = m.wcdf[(int64_t)wc * 16 + (bk > 0 ? bk - 1 : 0)];
+      // C[b − 1] selected from the registers (a gather here measured 14 % slower: one more load in
+      // the token pipeline's in-order vmcnt)
+      base = 0.f;
+#pragma unroll
+      for (int i = 0; i < 15; ++i) base = i == bk - 1 ? c1[i] : base;
       // level 2: the bucket's q values (a float4 past the row's KS padding is not read)
       const float* qr = a.q + (int64_t)wc * KS + bk * WB;
 #pragma unroll
@@ -342,7 +402,9 @@ struct MHLane {
   __device__ __forceinline__ void issue_c(int P, int s, uint32_t w) {
     MHB<DM>& x = b[P];
     const uint32_t qo = (w == oni::kPadWord ? 0u : w) * (uint32_t)KS;
-    {
+    if constexpr (WP == 0) {
+      x.tw = alias_draw(x.r.x, x.rw.x);
+    } else {
       // word proposal, level 2: running f32 sum of the bucket's q values from 0 (spec.word_cdf_draw).
       // Topics past K hold q = 0 (k_apply) and the loads past KS were zeroed: their running sums
       // repeat the last real one, so counting them changes nothing after the cap.
@@ -357,8 +419,12 @@ struct MHLane {
       const int cnt = count_le<WB>(cum, 0.f, y2);
       const int rem = K - bk * WB;
       const int last = (rem < WB ? rem : WB) - 1;
-      x.tw = bk * WB + (cnt < last ? cnt : last);
-      x.qtw = a.q[qo + (uint32_t)x.tw];
+      const int tin = cnt < last ? cnt : last;
+      float qt = qb[0];
+#pragma unroll
+      for (int j = 1; j < WB; ++j) qt = j == tin ? qb[j] : qt;
+      x.tw = bk * WB + tin;
+      x.qtw = qt;
     }
     const int tdm = alias_draw(x.r.z, x.ed);
     const int tds = single_pick(x.r.z, s);
@@ -404,8 +470,14 @@ struct MHLane {
     pend.flush(a, KS);
     asm volatile("" ::: "memory");
     const int tw = x.tw, td = x.td;
-    const float qtw = x.qtw;
-    const float zw = x.zw;
+    float qtw, zw;
+    if constexpr (WP == 0) {
+      qtw = __uint_as_float(alias_keeps(x.r.x, x.rw.x) ? x.rw.y : x.rw.z);
+      zw = __uint_as_float(x.rw.w);
+    } else {
+      qtw = x.qtw;
+      zw = x.zw;
+    }
     const float qtd = x.qtd;
     const int32_t btw = x.btw, btd = x.btd;
     const float2 ab = L.qfx[zo];
@@ -544,12 +616,12 @@ __device__ __forceinline__ MHLds mh_lds(unsigned char* smem, int KS) {
   return L;
 }
 
-template <int MODE, int DM, int WB>
+template <int MODE, int DM, int WP>
 __global__ __launch_bounds__(64) void k_gibbs_mh(const OniMH m) {
   extern __shared__ __align__(16) unsigned char smem_mh[];
   const OniGibbs& a = m.g;
   const int KS = a.KS;
-  MHLane<MODE, DM, WB> x(m);
+  MHLane<MODE, DM, WP> x(m);
   x.L = mh_lds(smem_mh, KS);
   int32_t* red = reinterpret_cast<int32_t*>(smem_mh + (size_t)KS * (sizeof(float2) + sizeof(float)));
   x.red = red;
@@ -666,20 +738,29 @@ static size_t mh_lds_bytes(int KS, int lmax) {
   return (size_t)KS * (sizeof(float2) + sizeof(float) + sizeof(int32_t)) + (size_t)KS * 64 + (size_t)lmax * 64;
 }
 
-// Per-sweep MH tables: the word CDF rows (k_mh_cdf, all V words) and the alias rows of the n_long
-// multi-chunk documents + g (k_mh_alias over the document rows only).
+// Per-sweep MH tables. Word proposal: alias records (walias + wsum, k_mh_alias over the V word rows)
+// or the level-1 CDF rows (wcdf, k_mh_cdf); exactly one of the two. Then the alias rows of the n_long
+// multi-chunk documents and g (k_mh_alias, document rows).
 ONI_API int oni_mh_tables(const float* q, int64_t V, int K, int KS, const int32_t* ndk, const int32_t* rows,
-                          int64_t n_long, float alpha, float* wcdf, uint32_t* dalias, const int32_t* nk, float vbeta,
-                          float* g, hipStream_t s) {
+                          int64_t n_long, float alpha, uint4* walias, float* wsum, float* wcdf, uint32_t* dalias,
+                          const int32_t* nk, float vbeta, float* g, hipStream_t s) {
   if (K < 1 || K > 255 || K > KS || KS % 4 || V < 0 || n_long < 0) return (int)hipErrorInvalidValue;
-  if (V > 0) {
-    const unsigned cgrid = oni::grid_for((V + 3) / 4 * 64, 256, 8192);
-    if (K <= 128) k_mh_cdf<8><<<cgrid, 256, 0, s>>>(q, V, K, KS, wcdf);
-    else k_mh_cdf<16><<<cgrid, 256, 0, s>>>(q, V, K, KS, wcdf);
+  if ((walias == nullptr) == (wcdf == nullptr) || (walias != nullptr && wsum == nullptr))
+    return (int)hipErrorInvalidValue;
+  int64_t Vw = V;
+  if (wcdf != nullptr) {
+    if (V > 0) {
+      const unsigned cgrid = oni::grid_for((V + 3) / 4 * 64, 256, 8192);
+      if (K <= 128) k_mh_cdf<8><<<cgrid, 256, 0, s>>>(q, V, K, KS, wcdf);
+      else k_mh_cdf<16><<<cgrid, 256, 0, s>>>(q, V, K, KS, wcdf);
+    }
+    Vw = 0;
   }
-  const unsigned grid = (unsigned)((n_long + 63) / 64 > 0 ? (n_long + 63) / 64 : 1);
-  const size_t lds = (size_t)K * kAS * sizeof(float) + (size_t)K * 64;
-  k_mh_alias<<<grid, 64, lds, s>>>(K, KS, ndk, rows, n_long, alpha, dalias, nk, vbeta, g);
+  const int64_t nrows = Vw + n_long;
+  const unsigned grid = (unsigned)((nrows + 63) / 64 > 0 ? (nrows + 63) / 64 : 1);
+  const size_t lds = (size_t)K * kAS * sizeof(float) + 64 * sizeof(float) + (size_t)K * 64;
+  k_mh_alias<<<grid, 64, lds, s>>>(q, Vw, K, KS, ndk, rows, n_long, alpha, walias, wsum, dalias, nk, vbeta, g,
+                                   Vw >= 65536);
   return (int)hipGetLastError();
 }
 
@@ -695,14 +776,17 @@ ONI_API int oni_gibbs_mh_launch(const OniMH* m, int init, int mode, hipStream_t 
     k_gibbs_mh_init<<<grid, 64, lds, s>>>(*m);
     return (int)hipGetLastError();
   }
-  if (!a.qfix || !m->wcdf || !m->mh_g || !m->chunk_dslot) return (int)hipErrorInvalidValue;
+  if (!a.qfix || !m->mh_g || !m->chunk_dslot) return (int)hipErrorInvalidValue;
+  if (m->wp == 0 ? (!m->walias || !m->wsum) : (!m->wcdf || m->wp != (a.K <= 128 ? 8 : 16)))
+    return (int)hipErrorInvalidValue;
   if (m->doc_moves < 1 || m->doc_moves > 4) return (int)hipErrorInvalidValue;
   if (mode == 2 && !a.chg_mask) return (int)hipErrorInvalidValue;
   if (mode == 3 && (!a.wpos || !a.z_w)) return (int)hipErrorInvalidValue;
   if (mode == 4 && (!a.wpos || !a.zz_w || !a.chg_mask)) return (int)hipErrorInvalidValue;
 #define ONI_MH(md, dm)                                                  \
   do {                                                                  \
-    if (a.K <= 128) k_gibbs_mh<md, dm, 8><<<grid, 64, lds, s>>>(*m);    \
+    if (m->wp == 0) k_gibbs_mh<md, dm, 0><<<grid, 64, lds, s>>>(*m);    \
+    else if (m->wp == 8) k_gibbs_mh<md, dm, 8><<<grid, 64, lds, s>>>(*m); \
     else k_gibbs_mh<md, dm, 16><<<grid, 64, lds, s>>>(*m);              \
   } while (0)
   switch (m->doc_moves * 8 + mode) {

@@ -233,12 +233,20 @@ def main(argv=None) -> int:
                       DUPFACTOR=a.dupfactor, USER_DOMAIN=a.user_domain, LPATH=a.lpath, EVAL_EVERY=a.eval_every,
                       CKPT_EVERY=a.ckpt_every, TOP_DOMAINS=a.top_domains, TOL=a.tol, MAXRESULTS=a.maxresults,
                       ALPHA=a.alpha, BURNIN=a.burnin)
+    inside = os.environ.get("ONI_MLD_INSIDE") == "1"
     if a.max_restarts > 0 and os.environ.get("ONI_SUPERVISED") != "1":
+        if inside:
+            # the supervisor's children would write to the service's stdout, not the client's
+            from .service import RunLocally
+            raise RunLocally("a supervised run (--max-restarts) starts child processes")
         return supervise(a, argv, cfg)
     if cfg.PUBLIC_SUFFIX:
         os.environ["ONI_PUBLIC_SUFFIX"] = cfg.PUBLIC_SUFFIX  # read by oni355.ref.psl.default_rules
     gpus = a.gpus if a.gpus is not None else cfg.PROCESS_COUNT
     if gpus > 1 and "WORLD_SIZE" not in os.environ:
+        if inside:
+            from .service import RunLocally
+            raise RunLocally(f"{gpus} GPUs: one process per GPU")
         return _relaunch(gpus, argv)
 
     import torch

@@ -50,10 +50,30 @@ def _recv(sock: socket.socket):
 
 # environment variables a request may set for its run (the service's own stay otherwise)
 _PASS_ENV = ("ONI_", "HSA_", "OMP_NUM_THREADS")
+# knobs the package reads once, at import: the warm service cannot honour a request that sets them
+# differently from its own environment, so such a request runs in the client's own process
+IMPORT_TIME_KNOBS = ("ONI_SPLIT_DEN", "ONI_SPLIT_MIN_WORLD", "ONI_SCORE_SORT_PAIRS", "ONI_MH_AUTO_MIN_K",
+                     "ONI_PREFETCH_COPY", "ONI_PULL_BLOCKS", "ONI_STAGE_CHUNK_MB", "ONI_STAGE_THREADS")
+
+
+class RunLocally(Exception):
+    """Raised inside the service for a request it must not run (several GPUs, a supervised run):
+    the client then runs the day in its own process."""
+
+
+def _local_reason(req: dict) -> str | None:
+    env = req.get("env") or {}
+    for k in IMPORT_TIME_KNOBS:
+        if env.get(k) != os.environ.get(k):
+            return f"{k} is read at import time ({env.get(k)!r} here, {os.environ.get(k)!r} in the service)"
+    return None
 
 
 def _run_one(req: dict) -> dict:
     from . import ml
+    why = _local_reason(req)
+    if why:
+        return {"local": True, "rc": None, "stdout": "", "stderr": f"[oni-mld] running locally: {why}\n"}
     out, err = io.StringIO(), io.StringIO()
     saved_env = dict(os.environ)
     cwd = os.getcwd()
@@ -67,6 +87,8 @@ def _run_one(req: dict) -> dict:
         with contextlib.redirect_stdout(out), contextlib.redirect_stderr(err):
             try:
                 rc = int(ml.main(list(req["argv"])) or 0)
+            except RunLocally as e:
+                return {"local": True, "rc": None, "stdout": "", "stderr": f"[oni-mld] running locally: {e}\n"}
             except SystemExit as e:
                 rc = e.code if isinstance(e.code, int) else (0 if e.code is None else 1)
             except Exception:  # noqa: BLE001 -- reported to the client, the service keeps running
@@ -136,6 +158,8 @@ def forward(path: str, argv: list[str]) -> int | None:
     sys.stderr.write(rep.get("stderr", ""))
     sys.stdout.flush()
     sys.stderr.flush()
+    if rep.get("local"):
+        return None  # the service declined: the caller runs the day itself
     return int(rep.get("rc", 1))
 
 

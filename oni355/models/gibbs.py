@@ -250,6 +250,8 @@ class GibbsLDA:
         # the Markov chain this model runs (checkpoint identity): the dense kernels are bitwise
         # one chain; MH is another, and its pipeline sets the dense burn-in it starts from
         self.chain = {"sampler": "mh" if self.mh else "dense", "mh_burn": 0}
+        if self.mh:
+            self.chain["mh_word"] = self.mh_word
         self.a = 0  # ndk parity
         self.b = 0  # delta-buffer parity
         self.cn = 0  # nk parity
@@ -291,8 +293,27 @@ class GibbsLDA:
         if rows.numel():
             dslot[multi] = torch.searchsorted(rows, c.chunk_doc[multi].to(torch.int64)).to(torch.int32)
         self.chunk_dslot = dslot
-        # word proposal ∝ q[w, ·]: level-1 CDF rows (bucket prefix sums; level 2 is the q row itself)
-        self.wcdf = torch.zeros(self.V, spec.MH_CDF_BUCKETS, dtype=torch.float32, device=dev)
+        # word proposal ∝ q[w, ·] (ONI_MH_WORD, default "auto"): "alias" -- every word's alias row as
+        # 16-B records built per sweep (one gather per proposal; the build writes V·K·16 B), or "cdf"
+        # -- a 64-B row of bucket prefix sums per word (a streaming pass over q) with the bucket's q
+        # values as the second level (two gathers and ~60 more VALU per token). "auto" takes the CDF
+        # when 3·V·K > 2·T (global tokens): measured at K = 100 the record build costs ~10 ps per
+        # cell and the CDF draw ~6 ps per token more (profiles/r5/).
+        T_all = torch.tensor([float(c.T)], dtype=torch.float64)
+        if self.comm is not None and self.comm.dist:
+            T_all = self.comm.allreduce_(T_all.to(self.comm.device)).cpu()
+        kind = os.environ.get("ONI_MH_WORD", "auto")
+        if kind == "auto":
+            kind = "cdf" if 3.0 * self.V * self.K > 2.0 * float(T_all[0]) else "alias"
+        if kind not in ("alias", "cdf"):
+            raise ValueError(f"unknown ONI_MH_WORD {kind}")
+        self.mh_word = kind
+        self.walias = self.wsum = self.wcdf = None
+        if kind == "cdf":
+            self.wcdf = torch.zeros(self.V, spec.MH_CDF_BUCKETS, dtype=torch.float32, device=dev)
+        else:
+            self.walias = torch.zeros(self.V, self.K, 4, dtype=torch.int32, device=dev)  # 16-B records
+            self.wsum = torch.zeros(self.V, dtype=torch.float32, device=dev)
         self.dalias = torch.zeros(max(int(rows.numel()), 1), self.K, dtype=torch.int32, device=dev)
         self.mh_g = torch.zeros(self.KS, dtype=torch.float32, device=dev)
         # one word move + two doc moves per token: with one doc move the chain plateaus 2.6 % lower
@@ -306,10 +327,10 @@ class GibbsLDA:
         """The sweep's MH proposal tables from the snapshot (q and the topic totals nk[cn] the last
         apply wrote, the sweep-start doc rows ndk[a])."""
         ops.mh_tables(self.q, self.nk[self.cn], self.ndk[self.a], self.mh_rows, self.K, self.alpha, self.vbeta,
-                      self.wcdf, self.dalias, self.mh_g)
+                      self.dalias, self.mh_g, walias=self.walias, wsum=self.wsum, wcdf=self.wcdf)
 
     def mh_state(self) -> dict:
-        return dict(wcdf=self.wcdf, dalias=self.dalias, mh_g=self.mh_g,
+        return dict(walias=self.walias, wsum=self.wsum, wcdf=self.wcdf, dalias=self.dalias, mh_g=self.mh_g,
                     chunk_dslot=self.chunk_dslot, mh_lmax=self.mh_lmax)
 
     def _x01_wanted(self) -> bool:

@@ -376,8 +376,9 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
     k_gibbs, 2 = k_gibbs_ldsg (G > 1), 3 = k_gibbs_x1 (G = 1); the specialised kernels need
     ``alpha_in_row`` (n + α exact in f32 for every count of the corpus), else the generic one runs.
     4 = k_gibbs_mh, the Metropolis-Hastings sampler (one-lane units, chunks ≤ 127 tokens; NOT the
-    same draws: its own oracle spec.gibbs_pass_mh) which also needs ``st["wcdf"]``,
-    ``st["dalias"]``, ``st["mh_g"]`` (:func:`mh_tables`) and ``st["chunk_dslot"]``;
+    same draws: its own oracle spec.gibbs_pass_mh) which also needs the word proposal
+    (``st["walias"]`` + ``st["wsum"]``, or ``st["wcdf"]``), ``st["dalias"]``, ``st["mh_g"]``
+    (:func:`mh_tables`) and ``st["chunk_dslot"]``;
     ``mh_doc_moves`` doc moves after each token's word move.
     """
     s0, s1 = spec.split_seed(seed)
@@ -395,7 +396,7 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
     if not _is_dev(st["tok_word"]):
         chg = st.get("chg_count")
         z_before = st["tok_z"].clone() if (chg is not None or mode == 4) else None
-        npst = {k: (v.numpy().view(np.uint32) if k in ("tok_word", "chunk_key", "dalias") else v.numpy())
+        npst = {k: (v.numpy().view(np.uint32) if k in ("tok_word", "chunk_key", "walias", "dalias") else v.numpy())
                 for k, v in st.items() if isinstance(v, torch.Tensor)}
         npst["dnk"] = npst["dnk"][:KS]  # replica 0 (the sum over replicas is what counts)
         if mode != 1:
@@ -464,8 +465,12 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
         m.inv_alpha = float(np.float32(1.0 / alpha))
         m.doc_moves = int(mh_doc_moves)
         if not init:
-            for name in ("wcdf", "dalias", "chunk_dslot"):
+            for name in ("dalias", "chunk_dslot"):
                 setattr(m, name, _lib.ptr(st[name]))
+            if st.get("wcdf") is not None:
+                m.wcdf, m.wp = _lib.ptr(st["wcdf"]), (8 if K <= 128 else 16)
+            else:
+                m.walias, m.wsum, m.wp = _lib.ptr(st["walias"]), _lib.ptr(st["wsum"]), 0
             m.mh_g = _lib.ptr(st["mh_g"])
         _lib.check(_lib.lib().oni_gibbs_mh_launch(C.byref(m), 1 if init else 0, int(mode), _lib.stream()),
                    "oni_gibbs_mh_launch")
@@ -475,25 +480,35 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
 
 
 def mh_tables(q: torch.Tensor, nk: torch.Tensor, ndk_src: torch.Tensor, long_rows: torch.Tensor, K: int,
-              alpha: float, vbeta: float, wcdf: torch.Tensor, dalias: torch.Tensor,
-              g: torch.Tensor) -> None:
-    """Per-sweep tables of the MH sampler (k_mh_cdf + k_mh_alias, spec.mh_tables): ``wcdf`` [V, 16]
-    f32 := every word's level-1 CDF row of its q row, ``dalias`` [n_long, K] := the alias entries of
-    n_dk + α for every document over several chunks (rows ``long_rows`` of ``ndk_src``),
-    ``g`` [KS] := 1/(n_k + Vβ + 1) of the snapshot's topic totals ``nk``. int32 tensors hold the u32
-    entries."""
-    if wcdf.shape != (q.shape[0], spec.MH_CDF_BUCKETS) or wcdf.dtype != torch.float32:
+              alpha: float, vbeta: float, dalias: torch.Tensor, g: torch.Tensor, walias: torch.Tensor | None = None,
+              wsum: torch.Tensor | None = None, wcdf: torch.Tensor | None = None) -> None:
+    """Per-sweep tables of the MH sampler (spec.mh_tables). Word proposal ∝ q[w, ·], one of:
+    ``walias`` [V, K, 4] := every word's alias records {entry, q_j, q_alias, Σ q} and ``wsum`` [V]
+    its sums (k_mh_alias), or ``wcdf`` [V, 16] f32 := its level-1 CDF row (k_mh_cdf). ``dalias``
+    [n_long, K] := the alias entries of n_dk + α for every document over several chunks (rows
+    ``long_rows`` of ``ndk_src``), ``g`` [KS] := 1/(n_k + Vβ + 1) of the snapshot's topic totals
+    ``nk``. int32 tensors hold the u32 entries."""
+    cdf = wcdf is not None
+    if cdf == (walias is not None) or (walias is not None and wsum is None):
+        raise ValueError("one word proposal table: walias + wsum, or wcdf")
+    if cdf and (wcdf.shape != (q.shape[0], spec.MH_CDF_BUCKETS) or wcdf.dtype != torch.float32):
         raise ValueError("wcdf must be a [V, 16] float32 table")
     if not _is_dev(q):
-        wc, da, gg = spec.mh_tables(q.numpy(), nk.numpy(), ndk_src.numpy(), long_rows.numpy(), K, alpha, vbeta)
-        wcdf.copy_(torch.from_numpy(wc))
+        wt, ws, da, gg = spec.mh_tables(q.numpy(), nk.numpy(), ndk_src.numpy(), long_rows.numpy(), K, alpha, vbeta,
+                                        word="cdf" if cdf else "alias")
+        if cdf:
+            wcdf.copy_(torch.from_numpy(wt))
+        else:
+            walias.copy_(torch.from_numpy(wt.view(np.int32)))
+            wsum.copy_(torch.from_numpy(ws))
         if da.shape[0]:
             dalias.copy_(torch.from_numpy(da.view(np.int32)))
         g.copy_(torch.from_numpy(gg))
         return
     V, KS = q.shape
+    p = lambda t: _lib.ptr(t) if t is not None else None  # noqa: E731
     _lib.check(_lib.lib().oni_mh_tables(_lib.ptr(q), V, K, KS, _lib.ptr(ndk_src), _lib.ptr(long_rows),
-                                        long_rows.numel(), float(alpha), _lib.ptr(wcdf),
+                                        long_rows.numel(), float(alpha), p(walias), p(wsum), p(wcdf),
                                         _lib.ptr(dalias), _lib.ptr(nk), float(vbeta), _lib.ptr(g), _lib.stream()),
                "oni_mh_tables")
 

@@ -42,8 +42,8 @@ class OniMH(C.Structure):
     """Mirror of ``struct OniMH`` in csrc/kernels/gibbs_mh.hip (size checked at load)."""
 
     _fields_ = [
-        ("g", OniGibbs), ("wcdf", vp), ("dalias", vp), ("mh_g", vp), ("chunk_dslot", vp),
-        ("chunk_len", vp), ("kalpha", f32), ("inv_alpha", f32), ("lmax", i32), ("doc_moves", i32),
+        ("g", OniGibbs), ("walias", vp), ("wsum", vp), ("wcdf", vp), ("dalias", vp), ("mh_g", vp), ("chunk_dslot", vp),
+        ("chunk_len", vp), ("kalpha", f32), ("inv_alpha", f32), ("lmax", i32), ("doc_moves", i32), ("wp", i32),
     ]
 
 
@@ -60,7 +60,7 @@ _SIGS = {
     "oni_gibbs_sizeof_args": [],
     "oni_gibbs_mh_launch": [C.POINTER(OniMH), C.c_int, C.c_int, vp],
     "oni_mh_sizeof_args": [],
-    "oni_mh_tables": [vp, i64, C.c_int, C.c_int, vp, vp, i64, f32, vp, vp, vp, f32, vp, vp],
+    "oni_mh_tables": [vp, i64, C.c_int, C.c_int, vp, vp, i64, f32, vp, vp, vp, vp, vp, f32, vp, vp],
     "oni_widen_pair": [vp, vp, i64, vp, vp],
     "oni_quantile_pick": [vp, vp, C.c_int, C.c_int, C.c_int, vp, vp, vp],
     "oni_tail_grid": [],

@@ -460,6 +460,20 @@ class LdaRun:
     # its (doc, word) pair for owner-side scoring (owner_token_scores)
     pairs: object = None
     route: Route | None = None  # with a process group: how this rank's tokens went to their owners
+    # independent chains beyond ``model`` (ONI_CHAINS > 1): scores are averaged over all chains
+    extra_models: list = field(default_factory=list)
+
+    def pair_scores(self, theta: torch.Tensor, phi: torch.Tensor, pdoc: torch.Tensor,
+                    pword: torch.Tensor) -> torch.Tensor:
+        """θ·φ of every (doc, word) pair, averaged in score space over the chains (θ / φ of the
+        first chain given; topic labels differ between chains, so only scores can be averaged)."""
+        ps = ops.pair_score(theta, phi, pdoc, pword)
+        if not self.extra_models:
+            return ps
+        D = theta.shape[0]
+        for m in self.extra_models:
+            ps = ps + ops.pair_score(m.theta()[:D], m.phi(), pdoc, pword)
+        return ps * np.float32(1.0 / (1 + len(self.extra_models)))
 
 
 @traced("oni:build_and_train")
@@ -537,6 +551,14 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
                                     weight=wt if use_w else None, pairs=pairs if dev.type == "cuda" else None)
         corpus = corpus_for(G)
         dcorpus = corpus_for(Gd) if Gd != G else None
+    # ONI_CHAINS = C > 1: C independent chains of sweeps // C sweeps each (same total sweep count),
+    # scored by the average of their pair scores (LdaRun.pair_scores): the top-N then depends less
+    # on any one chain's seed. Dense samplers only, no checkpointing.
+    chains = max(1, int(os.environ.get("ONI_CHAINS", "1")))
+    if chains > 1 and (mh or ckpt is not None or not train or sweeps < 2 * chains):
+        chains = 1
+    if chains > 1:
+        sweeps = sweeps // chains
     with timer.stage("init"):
         model = GibbsLDA(corpus, GibbsConfig(K=K, alpha=alpha, beta=beta, seed=seed), comm=comm,
                          V_global=int(vocab.numel()))
@@ -598,7 +620,17 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
     model.close()
     if not model.likelihoods or model.likelihoods[-1][0] != model.sweeps_done:
         model.record_likelihood()
-    run.timings.update({"sweeps": sweeps})
+    if chains > 1:
+        with timer.stage("train"):
+            for c in range(1, chains):
+                mc = GibbsLDA(corpus, GibbsConfig(K=K, alpha=alpha, beta=beta, seed=(seed + c * 0x9E3779B1) & 0xFFFFFFFF),
+                              comm=comm, V_global=int(vocab.numel()))
+                mc.plan_average(sweeps)
+                mc.initialize()
+                mc.sweep(sweeps)
+                mc.close()
+                run.extra_models.append(mc)
+    run.timings.update({"sweeps": sweeps * chains, "chains": chains})
     return run
 
 
@@ -625,7 +657,7 @@ def owner_token_scores(run: LdaRun, comm: Comm) -> torch.Tensor:
     This replaces an all-gather of every θ row to every rank (D_global·K·4 B per rank, 320 MB at
     the 100M-flow day) plus a per-rank pair build over the events: θ never leaves its owner. The
     per-pair dot is the same kernel as world 1 (k_pair_score), so scores stay bitwise equal."""
-    ps = ops.pair_score(run.model.theta(), run.model.phi(), run.pairs.pair_doc, run.pairs.pair_word)
+    ps = run.pair_scores(run.model.theta(), run.model.phi(), run.pairs.pair_doc, run.pairs.pair_word)
     return return_to_origin(ps[run.pairs.tok_pair.long()], run.route, comm)
 
 
@@ -840,10 +872,14 @@ def event_score_plan(run: LdaRun, dkeys: torch.Tensor, vocab: torch.Tensor, doc_
 
 
 @traced("oni:score")
-def plan_score(theta: torch.Tensor, phi: torch.Tensor, plan: ScorePlan, tol: float, hist=None, want_parts=False):
+def plan_score(theta: torch.Tensor, phi: torch.Tensor, plan: ScorePlan, tol: float, hist=None, want_parts=False,
+               run: "LdaRun | None" = None):
     """(score, s1, s2) per event in PLAN order (event order unless plan.order is set; map plan
-    positions back with plan.order / event indices forward with plan.rank)."""
-    if plan.tiles is not None:
+    positions back with plan.order / event indices forward with plan.rank). ``run`` with extra
+    chains: pair scores averaged over the chains (:meth:`LdaRun.pair_scores`)."""
+    if run is not None and run.extra_models:
+        ps = run.pair_scores(theta, phi, plan.pdoc, plan.pword)
+    elif plan.tiles is not None:
         t = plan.tiles
         ps = ops.tile_score(theta, phi, t.item_docs, t.item_words, t.item_p0, t.pair_rc, plan.pdoc, plan.pword)
     else:
@@ -920,7 +956,7 @@ def run_single_doc_events(doc_keys64: torch.Tensor, word_keys64: torch.Tensor, K
             dkeys, theta = gather_theta(run, comm)
             plan = event_score_plan(run, dkeys, vocab, [doc_keys64], wids[:n], [word_keys64], comm)
         with timer.stage("score"):
-            score, _, _ = plan_score(theta, run.model.phi(), plan, tol, hist=hist)
+            score, _, _ = plan_score(theta, run.model.phi(), plan, tol, hist=hist, run=run)
             rows, scs = top_n(score, tol, maxresults, comm, row_offset, hist=hist, order=plan.order)
     t = timer.summary()
     t.update(run.timings)

@@ -283,7 +283,7 @@ def run_flow(cols: dict, K: int = 20, sweeps: int = 200, tol: float = 1.0, maxre
                 plan = common.event_score_plan(run, dkeys, vocab, [doc_keys[:n], doc_keys[n: 2 * n]], wids[: 2 * n],
                                                [word_keys[:n], word_keys[n: 2 * n]], comm)
         with timer.stage("score"):
-            score, s1, s2 = common.plan_score(theta, phi, plan, tol, hist=hist, want_parts=True)
+            score, s1, s2 = common.plan_score(theta, phi, plan, tol, hist=hist, want_parts=True, run=run)
             rows, scs, rpos = common.top_n(score, tol, maxresults, comm, row_offset, hist=hist, order=plan.order,
                                            return_pos=True)
     t = timer.summary()

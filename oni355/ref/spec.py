@@ -530,27 +530,38 @@ def word_cdf_draw(C: np.ndarray, qrow: np.ndarray, r: np.ndarray, K: int) -> np.
 
 
 def mh_tables(q: np.ndarray, nk: np.ndarray, ndk_src: np.ndarray, long_rows: np.ndarray, K: int, alpha: float,
-              vbeta: float):
-    """Per-sweep tables of the MH sampler (k_mh_cdf / k_mh_alias): the word proposal ∝ q[w, k]
-    (sweep-start word factor) as every word's level-1 CDF row (:func:`word_cdf`; the second level
-    is the q row itself), the doc proposal ∝ n_dk + α (sweep-start row) of every document over
+              vbeta: float, word: str = "alias"):
+    """Per-sweep tables of the MH sampler (k_mh_alias / k_mh_cdf): the word proposal ∝ q[w, k]
+    (sweep-start word factor), the doc proposal ∝ n_dk + α (sweep-start row) of every document over
     several chunks as alias rows, and g_k = 1/(n_k + Vβ + 1) (the word factor a token adds to a
-    topic it moves into). Returns (wcdf [V, 16] f32, dalias [n_long, K] u32, g [KS] f32)."""
-    wcdf = word_cdf(q[:, :K], K)
+    topic it moves into). ``word`` "alias": every word's alias row as records {entry, q_j,
+    q_alias(j), Σ_k q_k} (the kernel's 16-B gather; small vocabularies); "cdf": every word's
+    level-1 CDF row (:func:`word_cdf`; the second level is the q row itself; large ones).
+    Returns (wtab, wsum, dalias [n_long, K] u32, g [KS] f32) with wtab = walias [V, K, 4] u32 and
+    wsum [V] f32, or wtab = wcdf [V, 16] f32 and wsum None."""
+    if word == "cdf":
+        wtab, wsum = word_cdf(q[:, :K], K), None
+    else:
+        ent, wsum = alias_table(q[:, :K])
+        q32 = np.ascontiguousarray(q[:, :K], dtype=F32)
+        al = (ent & U32(0xFF)).astype(np.int64)
+        wtab = np.stack([ent, q32.view(U32), np.take_along_axis(q32, al, axis=1).view(U32),
+                         np.repeat(wsum[:, None], K, axis=1).astype(F32).view(U32)], axis=2).astype(U32)
     b = ndk_src[np.asarray(long_rows, dtype=np.int64), :K].astype(F32) + F32(alpha)
     dalias = alias_table(b)[0] if b.shape[0] else np.zeros((0, K), dtype=U32)
     g = (F32(1) / ((nk.astype(F32) + F32(vbeta)).astype(F32) + F32(1))).astype(F32)
-    return wcdf, dalias, g
+    return wtab, wsum, dalias, g
 
 
-def mh_moves(nn, bb, qrow, zo, qe, multi, Nd, s, zslice, drows, wcdf, g, pos, key, sweep, seed0, seed1,
+def mh_moves(nn, bb, qrow, zo, qe, multi, Nd, s, zslice, drows, wtab, wsum, g, pos, key, sweep, seed0, seed1,
              K, alpha, doc_moves=1):
     """The MH moves of one token per row (see :func:`gibbs_pass_mh`). ``nn`` doc counts without the
     token (the chunk's view), ``bb`` sweep-start doc rows (with the token), ``qrow`` sweep-start q
     rows (with the token), ``qe`` the word factor of ``zo`` without it, ``Nd`` other tokens in the
     chunk, ``s`` the token's position, ``zslice`` current topics of the chunk's positions,
-    ``drows`` alias rows of the doc (multi-chunk docs), ``wcdf`` the word's level-1 CDF rows
-    (:func:`word_cdf`; Z = wcdf[:, 15]), ``g`` [KS] = 1/(D + 1). Returns the new topics."""
+    ``drows`` alias rows of the doc (multi-chunk docs), ``wtab`` / ``wsum`` the word's alias rows
+    [A, K] u32 and row sums, or (``wsum`` None) its level-1 CDF rows [A, 16] f32 (:func:`word_cdf`,
+    Z = wtab[:, 15]), ``g`` [KS] = 1/(D + 1). Returns the new topics."""
     A = zo.shape[0]
     ar = np.arange(A)
     a32 = F32(alpha)
@@ -570,8 +581,11 @@ def mh_moves(nn, bb, qrow, zo, qe, multi, Nd, s, zslice, drows, wcdf, g, pos, ke
         return ((bb[ar, k] - (k == zo)).astype(F32) + a32).astype(F32)
     # word move (from zo; proposal = the word's CDF over the snapshot q, which holds the token at zo)
     r0, r1, r2, r3 = philox10(pos, key, U32(sweep), U32(2), seed0, seed1)
-    t = word_cdf_draw(wcdf, qrow, r0, K)
-    wsum = wcdf[:, MH_CDF_BUCKETS - 1]
+    if wsum is None:
+        t = word_cdf_draw(wtab, qrow, r0, K)
+        wsum = wtab[:, MH_CDF_BUCKETS - 1]
+    else:
+        t = alias_draw(wtab, r0, K)
     d = (qrow[ar, zo] - qe).astype(F32)
     zt = ((wsum - d).astype(F32) + ((one - qrow[ar, t]).astype(F32) * g[t]).astype(F32)).astype(F32)
     num = (aw(t) * wsum).astype(F32)
@@ -617,9 +631,10 @@ def gibbs_pass_mh(st: dict, KS: int, K: int, alpha: float, seed0: int, seed1: in
     current state x -- a kernel reversible w.r.t. π, so their composition leaves π invariant
     (tests/test_mh_conditional.py). Philox blocks (pos, doc key, sweep, 2 + c) → r0..r3:
 
-    * word move, from zo only (r0 proposes t ∝ q[w, ·] by the two-level inverse CDF
-      :func:`word_cdf_draw` -- level 1 the per-sweep bucket sums, level 2 the q row itself -- r1
-      accepts): ratio (n_t^¬+α)·Z_zo / ((n_zo^¬+α)·Z_t) with Z_zo = the CDF's total and
+    * word move, from zo only (r0 proposes t ∝ q[w, ·] -- from the word's alias row, or by the
+      two-level inverse CDF :func:`word_cdf_draw`: level 1 the per-sweep bucket sums, level 2 the q
+      row itself -- r1 accepts): ratio (n_t^¬+α)·Z_zo / ((n_zo^¬+α)·Z_t) with Z_zo = the proposal's
+      total (alias row sum / CDF total) and
       Z_t = (Z_zo − (q_zo − q'_zo)) + (1 − q_t)·g_t, the sum the table would have with the token
       at t (g_t = 1/(D_t + 1)).
     * ``doc_moves`` doc moves (r2 proposes, r3 accepts; move c > 0 draws (r2, r3) from
@@ -631,8 +646,9 @@ def gibbs_pass_mh(st: dict, KS: int, K: int, alpha: float, seed0: int, seed1: in
       (n_t^¬+α)·q'_t·(b_x^¬+α) / ((n_x^¬+α)·q'_x·(b_t^¬+α)), b^¬ = b without the token; a draw of
       zo from x ≠ zo is kept with probability (b_zo^¬ + α)/(b_zo + α) first.
 
-    A move is taken when u(r)·den < num (f32). st as for :func:`gibbs_pass` plus ``wcdf``
-    [V, 16] f32 (the word proposal's level-1 CDF rows), ``dalias`` [n_long, K] u32, ``mh_g`` [KS] f32 (:func:`mh_tables`)
+    A move is taken when u(r)·den < num (f32). st as for :func:`gibbs_pass` plus the word proposal
+    (``walias`` [V, K, 4] u32 records and ``wsum`` [V] f32, or ``wcdf`` [V, 16] f32 level-1 CDF
+    rows), ``dalias`` [n_long, K] u32, ``mh_g`` [KS] f32 (:func:`mh_tables`)
     and ``chunk_dslot`` [C] i32 (row of dalias of a multi-chunk doc's chunk, −1 otherwise)."""
     S = 64
     slc, lane = _chunk_geometry(st, S)
@@ -648,7 +664,8 @@ def gibbs_pass_mh(st: dict, KS: int, K: int, alpha: float, seed0: int, seed1: in
     if clen.max(initial=0) > MH_MAX_CHUNK:
         raise ValueError("the MH sampler needs chunks of at most 127 tokens")
     qfix = st["qfix"]
-    wcdf, dalias = st["wcdf"], st["dalias"]
+    dalias = st["dalias"]
+    cdf = st.get("wcdf") is not None
     dslot = st["chunk_dslot"].astype(np.int64)
     base = st["slice_off"][slc].astype(np.int64) + lane
     for s in range(int(clen.max(initial=0))):
@@ -664,7 +681,8 @@ def gibbs_pass_mh(st: dict, KS: int, K: int, alpha: float, seed0: int, seed1: in
         zp = np.minimum(np.arange(int(clen[act].max()))[None, :], clen[act][:, None] - 1)
         zslice = st["tok_z"][base[act][:, None] + zp * S].astype(np.int64)
         zn = mh_moves(n[act], b[act], qrow, zo, qe, multi_c[act], clen[act] - 1, s, zslice,
-                      dalias[np.where(multi_c[act], dslot[act], 0)] if dalias.shape[0] else None, wcdf[w],
+                      dalias[np.where(multi_c[act], dslot[act], 0)] if dalias.shape[0] else None,
+                      st["wcdf"][w] if cdf else st["walias"][w, :, 0], None if cdf else st["wsum"][w],
                       st["mh_g"], pos, st["chunk_key"][act], sweep, seed0, seed1, K, alpha,
                       doc_moves)
         n[act, zn] += 1

@@ -8,7 +8,14 @@ Byte counts follow the device layout of this engine:
 * vocabulary (per word): n_wk + q + two Δ buffers, KS × 4 B each  = 16·KS B;
 * raw columns on device while featurizing (per event): flow 9 columns ≈ 44 B, DNS/proxy ≈ 40 B plus
   string bytes;
-* corpus build transient: the (doc, word) pair sort holds ≈ 24 B per token at its peak.
+* corpus build transient: the (doc, word) pair sort holds ≈ 24 B per token at its peak;
+* posterior-average sums (the last quarter of the chain): n_dk / n_wk sums of KS entries per doc /
+  word, int64 when S times the largest count can pass 2^31 (config-4/5 magnitudes), int32 below;
+* scoring: θ (docs × KS f32) and φ (vocab × KS f32);
+* MH models (K ≥ 100): the word proposal tables (alias records V·K·16 B + sums, or 64-B CDF rows
+  when 3·V·K > 2·T) and, during the dense burn-in, a second corpus of the dense tiling with its own
+  document and word tables (the round-4 estimate left these out and projected 68 GB for
+  the 1B-token flow model that measured 154 GB, profiles/r5/combined_flow_1B_tokens_k100_1gpu.json).
 
 ``plan()`` returns the estimate; ``bench/combined.py`` prints it next to torch's measured peak.
 """
@@ -50,13 +57,31 @@ class Plan:
                 "peak_GB": round(self.peak_bytes / 1e9, 3)}
 
 
-def plan(source: str, events: int, K: int, docs: int, vocab: int, string_bytes_per_event: int = 0) -> Plan:
-    """Estimate one GPU's HBM use for ``events`` local events of ``source``."""
+def plan(source: str, events: int, K: int, docs: int, vocab: int, string_bytes_per_event: int = 0,
+         samples: int = 50, mh_burn: int | None = None, tokens_global: int | None = None) -> Plan:
+    """Estimate one GPU's HBM use for ``events`` local events of ``source`` (``samples`` posterior
+    samples; ``mh_burn``: dense burn-in sweeps of an MH model, default ONI_MH_BURN's 20;
+    ``tokens_global``: the model's token count over all GPUs, default the local one)."""
+    from ..models.gibbs import sampler_for, tiling_for
     KS = ks_of(K)
     tokens = events * TOKENS_PER_EVENT[source]
+    T = tokens_global or tokens
     steady = int(tokens * TOKEN_BYTES + docs * (8 * KS + 40) + vocab * 16 * KS)
+    # posterior sums: a doc row / word row / topic total of S samples, int64 past 2^31
+    wide = lambda bound: 8 if bound * samples > 2**31 - 1 else 4  # noqa: E731
+    sums = docs * KS * wide(tokens // max(docs, 1) * 64) + vocab * KS * wide(T // max(vocab, 1) * 64)
+    scoring = (docs + vocab) * KS * 4
+    extra = 0
+    if sampler_for(K) == "mh":
+        cdf = 3 * vocab * K > 2 * T
+        extra += vocab * 64 if cdf else vocab * (K * 16 + 4)
+        burn = 20 if mh_burn is None else mh_burn
+        if burn > 0:
+            Gd, KPd = tiling_for(K, "dense")
+            KSd = Gd * KPd
+            extra += int(tokens * TOKEN_BYTES + docs * (8 * KSd + 40) + vocab * 16 * KSd)
     raw = events * (RAW_BYTES[source] + string_bytes_per_event)
-    peak = steady + raw + tokens * BUILD_BYTES_PER_TOKEN
+    peak = steady + sums + scoring + extra + raw + tokens * BUILD_BYTES_PER_TOKEN
     return Plan(source, events, tokens, docs, vocab, K, steady, int(peak))
 
 

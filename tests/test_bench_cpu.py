@@ -108,3 +108,14 @@ def test_bench_forced_one_rank_process_group_matches_plain():
     for k in ("loglik", "tokens", "vocab", "docs_local", "planted_anomaly_recall_topN"):
         assert forced[k] == plain[k], k
     assert forced["allreduce_bytes_per_sweep"] > 0 and plain["allreduce_bytes_per_sweep"] == 0
+
+
+def test_sizing_counts_mh_burn_in_and_posterior_sums():
+    """The K = 100 projection includes the MH word tables, the dense burn-in's second corpus and
+    model, the posterior sums and θ / φ: the 1B-token flow model on one MI355X measured 154 GB
+    (profiles/r5/combined_flow_1B_tokens_k100_1gpu.json); the round-4 formula said 68 GB."""
+    from oni355.utils import sizing
+    p = sizing.plan("flow", 500_000_000, 100, 20_000_000, 7008)
+    assert 0.75 * 154e9 < p.peak_bytes < 1.25 * 154e9, p.as_dict()
+    nb = sizing.plan("flow", 500_000_000, 100, 20_000_000, 7008, mh_burn=0)
+    assert nb.peak_bytes < p.peak_bytes

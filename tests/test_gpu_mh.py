@@ -25,8 +25,9 @@ def _toy(n_docs, V, seed):
 
 @pytest.mark.parametrize("K,V", [(7, 1000), (40, 1000), (100, 1000), (255, 1000), (40, 70001)])
 def test_alias_tables_bitwise(gpu, K, V):
-    """Word CDF rows (k_mh_cdf: buckets of 8 topics up to K = 128, 16 above) and the multi-chunk
-    documents' alias rows (k_mh_alias), bit for bit."""
+    """Word proposal tables -- alias records (k_mh_alias; V ≥ 65536: rows go out one at a time,
+    lanes along k) and CDF rows (k_mh_cdf: buckets of 8 topics up to K = 128, 16 above) -- and the
+    multi-chunk documents' alias rows, bit for bit."""
     r = np.random.default_rng(K)
     KS = (K + 3) // 4 * 4
     q = np.zeros((V, KS), np.float32)
@@ -36,15 +37,23 @@ def test_alias_tables_bitwise(gpu, K, V):
     ndk[:, K:] = 0
     rows = np.array([0, 5, 7, 199], np.int32)
     nk = r.integers(0, 10**6, KS).astype(np.int32)
-    wc, da, g = spec.mh_tables(q, nk, ndk, rows, K, 0.37, 17.5)
     dev = torch.device(gpu)
-    out = [torch.zeros(V, 16, device=dev), torch.zeros(len(rows), K, dtype=torch.int32, device=dev),
-           torch.zeros(KS, device=dev)]
-    ops.mh_tables(torch.from_numpy(q).to(dev), torch.from_numpy(nk).to(dev), torch.from_numpy(ndk).to(dev),
-                  torch.from_numpy(rows).to(dev), K, 0.37, 17.5, *out)
-    assert np.array_equal(out[0].cpu().numpy(), wc)
-    assert np.array_equal(out[1].cpu().numpy().view(np.uint32), da)
-    assert np.array_equal(out[2].cpu().numpy(), g)
+    args = [torch.from_numpy(x).to(dev) for x in (q, nk, ndk, rows)]
+    for word in ("alias", "cdf"):
+        wt, ws, da, g = spec.mh_tables(q, nk, ndk, rows, K, 0.37, 17.5, word=word)
+        out = [torch.zeros(len(rows), K, dtype=torch.int32, device=dev), torch.zeros(KS, device=dev)]
+        if word == "cdf":
+            tabs = dict(wcdf=torch.zeros(V, 16, device=dev))
+        else:
+            tabs = dict(walias=torch.zeros(V, K, 4, dtype=torch.int32, device=dev), wsum=torch.zeros(V, device=dev))
+        ops.mh_tables(*args[:2], args[2], args[3], K, 0.37, 17.5, *out, **tabs)
+        if word == "cdf":
+            assert np.array_equal(tabs["wcdf"].cpu().numpy(), wt)
+        else:
+            assert np.array_equal(tabs["walias"].cpu().numpy().view(np.uint32), wt)
+            assert np.array_equal(tabs["wsum"].cpu().numpy(), ws)
+        assert np.array_equal(out[0].cpu().numpy().view(np.uint32), da)
+        assert np.array_equal(out[1].cpu().numpy(), g)
 
 
 _CASES = [(100, "recount", 1, 64), (100, "wdelta", 1, 64), (100, "atomic", 1, 64), (100, "dual", 1, 64),
@@ -53,9 +62,11 @@ _CASES = [(100, "recount", 1, 64), (100, "wdelta", 1, 64), (100, "atomic", 1, 64
           (100, "recount", 4, 127), (40, "dual", 4, 32)]
 
 
+@pytest.mark.parametrize("word", ["alias", "cdf"])
 @pytest.mark.parametrize("K,mode,dm,L", _CASES)
-def test_mh_sweep_bitwise_vs_oracle(gpu, K, mode, dm, L, monkeypatch):
+def test_mh_sweep_bitwise_vs_oracle(gpu, K, mode, dm, L, word, monkeypatch):
     monkeypatch.setenv("ONI_MH_DOC_MOVES", str(dm))
+    monkeypatch.setenv("ONI_MH_WORD", word)
     tdoc, tword, keys = _toy(300, 400, K + dm)
     G, KP = ops.choose_tiling(K, "mh")
     cc = build_corpus(tdoc, tword, 300, 400, torch.from_numpy(keys), G, L=L)
@@ -63,7 +74,7 @@ def test_mh_sweep_bitwise_vs_oracle(gpu, K, mode, dm, L, monkeypatch):
     assert torch.equal(cc.chunk_doc, cg.chunk_doc.cpu())
     mc = GibbsLDA(cc, GibbsConfig(K=K, seed=4321, use_graph=False, count_mode="atomic", sampler="mh"))
     mg = GibbsLDA(cg, GibbsConfig(K=K, seed=4321, use_graph=False, count_mode=mode, sampler="mh"))
-    assert mg.qpf == ops.SAMPLER_MH and mg.mh_doc_moves == dm
+    assert mg.qpf == ops.SAMPLER_MH and mg.mh_doc_moves == dm and mg.mh_word == mc.mh_word == word
     mc.initialize()
     mg.initialize()
     assert torch.equal(mc.tok_z, mg.tok_z.cpu())
@@ -72,7 +83,10 @@ def test_mh_sweep_bitwise_vs_oracle(gpu, K, mode, dm, L, monkeypatch):
     for _ in range(3):
         mc.sweep(1)
         mg.sweep(1)
-        assert torch.equal(mc.wcdf, mg.wcdf.cpu())
+        if mg.mh_word == "cdf":
+            assert torch.equal(mc.wcdf, mg.wcdf.cpu())
+        else:
+            assert torch.equal(mc.walias, mg.walias.cpu()) and torch.equal(mc.wsum, mg.wsum.cpu())
         assert torch.equal(mc.dalias, mg.dalias.cpu()) and torch.equal(mc.mh_g, mg.mh_g.cpu())
         assert torch.equal(mc.tok_z, mg.tok_z.cpu())
         assert torch.equal(mc.ndk_cur, mg.ndk_cur.cpu())

@@ -40,8 +40,9 @@ def _case(K, alpha, multi, R=120_000, Ld=7, s=2, seed=5, beta=0.01, V=50, stale=
     pi = (nn + alpha) * qrest
     pi /= pi.sum()
     zo = r.choice(K, size=R, p=pi)
-    # snapshot with the token at z (k_apply's numerics): q rows, qfix, g and the word's CDF
-    qrows, qfixes, gs, wcd = [], [], [], []
+    # snapshot with the token at z (k_apply's numerics): q rows, qfix, g and the word's proposal
+    # tables (alias row + sum, CDF row)
+    qrows, qfixes, gs, wcd, wal, wsums = [], [], [], [], [], []
     for z in range(K):
         nw = nw_rest.copy(); nw[z] += 1
         nk = nk_rest.copy(); nk[z] += 1
@@ -50,8 +51,10 @@ def _case(K, alpha, multi, R=120_000, Ld=7, s=2, seed=5, beta=0.01, V=50, stale=
         qrows.append(q)
         qfixes.append(spec.gibbs_qfix(nk.astype(np.int32), K, float(vbeta)))
         wcd.append(spec.word_cdf(q[None, :], K)[0])
+        t, tot = spec.alias_table(q[None, :])
+        wal.append(t[0]); wsums.append(tot[0])
         gs.append((F32(1) / (den + F32(1))).astype(F32))
-    qrows, wcd, gs = map(np.array, (qrows, wcd, gs))
+    qrows, wcd, gs, wal, wsums = map(np.array, (qrows, wcd, gs, wal, wsums))
     qrow = qrows[zo]
     qe = np.array([spec.excluded_q(qrows[z][z:z + 1], np.array([z]), qfixes[z])[0] for z in range(K)])[zo]
     # sweep-start doc row: the chunk's view without the token + stale counts of other chunks + the token
@@ -64,13 +67,14 @@ def _case(K, alpha, multi, R=120_000, Ld=7, s=2, seed=5, beta=0.01, V=50, stale=
     zslice[:, s] = zo
     return pi, zo, dict(nn=np.tile(nn, (R, 1)).astype(np.int32), bb=bb, qrow=qrow, zo=zo, qe=qe,
                         multi=np.full(R, multi), Nd=np.full(R, Ld - 1), s=s, zslice=zslice, drows=drows,
-                        wcdf=wcd[zo], gs=gs)
+                        wcdf=wcd[zo], wrows=wal[zo], wsum=wsums[zo], gs=gs)
 
 
 @pytest.mark.parametrize("K,alpha", [(7, 0.5), (20, 2.5), (9, 50 / 9)])
 @pytest.mark.parametrize("multi", [False, True, "sparse"])
 @pytest.mark.parametrize("doc_moves", [1, 2, 4])
-def test_mh_moves_leave_the_conditional_invariant(K, alpha, multi, doc_moves):
+@pytest.mark.parametrize("word", ["alias", "cdf"])
+def test_mh_moves_leave_the_conditional_invariant(K, alpha, multi, doc_moves, word):
     # "sparse": a multi-chunk doc whose sweep-start row holds just its chunk (b_zo = 1 is common, so
     # the table's copy of the token at zo matters most)
     pi, zo, a = _case(K, alpha, bool(multi), stale=multi != "sparse")
@@ -86,7 +90,8 @@ def test_mh_moves_leave_the_conditional_invariant(K, alpha, multi, doc_moves):
         g = a["gs"][(z + 1) % K].copy()
         sub = {k: (v[m] if isinstance(v, np.ndarray) and v.shape[:1] == (R,) else v) for k, v in a.items()}
         zn[m] = spec.mh_moves(sub["nn"], sub["bb"], sub["qrow"], sub["zo"], sub["qe"], sub["multi"], sub["Nd"],
-                              a["s"], sub["zslice"], sub["drows"], sub["wcdf"], g, pos[m], key[m], 11,
+                              a["s"], sub["zslice"], sub["drows"], sub["wcdf"] if word == "cdf" else sub["wrows"],
+                              None if word == "cdf" else sub["wsum"], g, pos[m], key[m], 11,
                               0x1234, 0x5678, K, alpha, doc_moves)
     moved = float((zn != zo).mean())
     assert moved > 0.05, moved  # the moves are not all rejected

@@ -66,4 +66,4 @@ def test_explicit_chunk_len_128_clamped_for_mh():
                           log=msgs.append)
     assert run.corpus.L <= spec.MH_MAX_CHUNK and run.model.mh
     assert any("MH sampler" in m for m in msgs)
-    assert run.model.chain == {"sampler": "mh", "mh_burn": 6}
+    assert run.model.chain["sampler"] == "mh" and run.model.chain["mh_burn"] == 6

@@ -62,3 +62,17 @@ def test_no_service_runs_locally(tmp_path):
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     assert os.path.exists(os.path.join(lp, "flow", "20160708", "flow_results.csv"))
+
+
+def test_service_declines_what_it_cannot_run(tmp_path, monkeypatch):
+    """Import-time knobs set differently from the service's, supervised runs and multi-GPU runs come
+    back as "run locally" (the client then runs the day in its own process)."""
+    from oni355.cli import service
+    monkeypatch.delenv("ONI_SPLIT_DEN", raising=False)
+    rep = service._run_one({"argv": _args(str(tmp_path / "a")), "env": {"ONI_SPLIT_DEN": "4"}})
+    assert rep["local"] and "ONI_SPLIT_DEN" in rep["stderr"]
+    rep = service._run_one({"argv": _args(str(tmp_path / "b")) + ["--max-restarts", "1"], "env": {}})
+    assert rep["local"] and "--max-restarts" in rep["stderr"]
+    rep = service._run_one({"argv": _args(str(tmp_path / "c")) + ["--gpus", "2"], "env": {}})
+    assert rep["local"] and "2 GPUs" in rep["stderr"]
+    assert "ONI_MLD_INSIDE" not in os.environ  # the service's environment is restored
