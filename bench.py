@@ -376,6 +376,8 @@ def run_pipeline_mode(a, comm) -> dict:
         "setup_s": round(setup_s, 2),
         "allreduce_ms_per_sweep": model.allreduce_ms_per_sweep(),
         "allreduce_bytes_per_sweep": model.allreduce_bytes_per_sweep(),
+        # the auto count mode's measured changed-token fractions (sweep, fraction), last few
+        "changed_fraction_tail": [(int(a_), round(float(b_), 4)) for a_, b_ in model.change_log[-3:]],
         # count magnitudes (the int32 tables' headroom) and the device memory high-water mark
         "max_topic_share": round(float(model.nk_cur[:K].max()) / max(model.T_global, 1), 4),
         "min_score_topN": float(res.scores[0]) if len(res.scores) else None,

@@ -268,10 +268,11 @@ class GibbsLDA:
         self._x01 = None
         if comm is not None and comm.dist and self.KS % 2 == 0 and self._x01_wanted():
             self._setup_x01()
-        # one process (no X01): the count passes add Δn_wk straight into n_wk and k_apply refreshes
-        # q from it (2 of its 5 passes over V·KS fewer); ONI_APPLY_INPLACE=0 keeps the Δ buffer
-        self._inplace_ok = ((comm is None or not comm.dist) and self._split is None
-                            and os.environ.get("ONI_APPLY_INPLACE", "1") != "0")
+        # one rank (no process group, or a 1-rank group whose all-reduce is the identity): the count
+        # passes add Δn_wk straight into n_wk and k_apply refreshes q from it (2 of its 5 passes
+        # over V·KS fewer); ONI_APPLY_INPLACE=0 keeps the Δ buffer
+        self._inplace_ok = ((comm is None or not comm.dist or (comm.world == 1 and self._x01 is None))
+                            and self._split is None and os.environ.get("ONI_APPLY_INPLACE", "1") != "0")
         self._avg = None          # posterior-averaging accumulators (plan_average)
         self._acc = False         # sweeps add their counts to the accumulators (inside graphs too)
         self._avg_at: list = []   # sweep counts at which a sample is added

@@ -23,6 +23,9 @@ _lib.register_optional("oni_hashdict_finish", [vp, i64, ci, i64, vp, vp, vp, i64
 _lib.register_optional("oni_route_pack", [vp, vp, vp, vp, vp, i64, ci, vp, vp, vp, vp, _SZ, vp])
 _lib.register_optional("oni_route_pack_ids", [vp, vp, vp, vp, vp, i64, ci, vp, vp, vp, vp, _SZ, vp])
 _lib.register_optional("oni_route_unpack", [vp, i64, ci, vp, vp, ci, vp, vp, vp, vp, vp])
+_lib.register_optional("oni_partition", [vp, vp, vp, i64, ci, vp, vp, vp, vp, vp, _SZ, vp])
+_lib.register_optional("oni_place_stats", [vp, vp, i64, vp, i64, ci, vp, vp])
+_lib.register_optional("oni_place_owner", [vp, i64, vp, i64, vp, ci, vp, vp, vp])
 _lib.register_optional("oni_pair_build", [vp, vp, vp, i64, i64, i64, vp, vp, vp, vp, vp, vp, i64, vp, _SZ, vp])
 _lib.register_optional("oni_doc_layout", [vp, vp, i64, i64, ci, vp, vp, vp, vp, vp, vp, vp, _SZ, vp])
 _lib.register_optional("oni_chunk_layout", [vp, vp, vp, i64, i64, ci, ci, vp, vp, vp, vp, vp, vp, vp, vp, _SZ, vp])
@@ -154,6 +157,62 @@ def route_pack_ids(owner_of_id: torch.Tensor, ids: torch.Tensor, doc_val: torch.
           _p(weight.to(torch.int32).contiguous()) if weight is not None else None, n, int(world), _p(send),
           _p(order), _p(counts))
     return send, order[:n], counts
+
+
+def partition(owner_of_id: torch.Tensor, world: int, ids: torch.Tensor | None = None,
+              keys64: torch.Tensor | None = None, rank: bool = False):
+    """Stable partition of items by owner rank (csrc/kernels/route.hip ``oni_partition``): item i's
+    owner is ``owner_of_id[ids[i]]`` (``owner_of_id[i]`` without ``ids``). Returns (order int32 [n]
+    = item of each slot, counts int64 [world], rank int32 [n] = slot of each item within its
+    owner's group or None, u32 bits of ``keys64`` at each slot int32 [n] or None) -- a stable
+    ``argsort(owner)`` with the group offsets and a gather, in two passes over the items."""
+    if owner_of_id.dtype != torch.int32 or not owner_of_id.is_contiguous():
+        raise TypeError("partition: owner_of_id must be contiguous int32")
+    if ids is not None and (ids.dtype != torch.int32 or not ids.is_contiguous()):
+        raise TypeError("partition: ids must be contiguous int32")
+    n = ids.numel() if ids is not None else owner_of_id.numel()
+    if keys64 is not None and (keys64.dtype != torch.int64 or not keys64.is_contiguous() or keys64.numel() != n):
+        raise TypeError("partition: keys64 must be contiguous int64 [n]")
+    if not 1 <= world <= 256:
+        raise ValueError("partition: 1 <= world <= 256")
+    dev = owner_of_id.device
+    order = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    counts = torch.empty(world, dtype=torch.int64, device=dev)
+    rk = torch.empty(max(n, 1), dtype=torch.int32, device=dev) if rank else None
+    ko = torch.empty(max(n, 1), dtype=torch.int32, device=dev) if keys64 is not None else None
+    _call("oni_partition", _p(owner_of_id), _p(ids) if ids is not None else None,
+          _p(keys64) if keys64 is not None else None, n, int(world), _p(order), _p(rk) if rank else None,
+          _p(ko) if ko is not None else None, _p(counts))
+    return order[:n], counts, (rk[:n] if rank else None), (ko[:n] if ko is not None else None)
+
+
+def place_stats(ukeys: torch.Tensor, ucnt: torch.Tensor, cand: torch.Tensor, B: int) -> torch.Tensor:
+    """int64 [nc + B]: the local count of every candidate document (0 when absent here), then the
+    summed counts of the other documents per hash bucket (``pipeline.common.doc_owner(key, B)``).
+    ``ukeys`` and ``cand`` ascending int64."""
+    for t, nm in ((ukeys, "ukeys"), (ucnt, "ucnt"), (cand, "cand")):
+        if t.dtype != torch.int64 or not t.is_contiguous():
+            raise TypeError(f"place_stats: {nm} must be contiguous int64")
+    if ucnt.numel() != ukeys.numel() or B < 1:
+        raise ValueError("place_stats: one count per key, B >= 1")
+    both = torch.empty(cand.numel() + B, dtype=torch.int64, device=ukeys.device)
+    _lib.check(_lib.lib().oni_place_stats(_p(ukeys), _p(ucnt), ukeys.numel(), _p(cand), cand.numel(), int(B), _p(both),
+                                          _lib.stream()), "oni_place_stats")
+    return both
+
+
+def place_owner(ukeys: torch.Tensor, cand: torch.Tensor, cown: torch.Tensor, bown: torch.Tensor) -> torch.Tensor:
+    """int32 owner of every document: ``cown[j]`` for the candidate ``cand[j]``, else the owner
+    ``bown`` of its hash bucket."""
+    if ukeys.dtype != torch.int64 or cand.dtype != torch.int64 or not (ukeys.is_contiguous() and cand.is_contiguous()):
+        raise TypeError("place_owner: contiguous int64 keys")
+    if cown.dtype != torch.int32 or bown.dtype != torch.int32 or cown.numel() != cand.numel() or bown.numel() < 1:
+        raise TypeError("place_owner: int32 owners, one per candidate, >= 1 bucket")
+    uown = torch.empty(ukeys.numel(), dtype=torch.int32, device=ukeys.device)
+    _lib.check(_lib.lib().oni_place_owner(_p(ukeys), ukeys.numel(), _p(cand), cand.numel(), _p(cown.contiguous()),
+                                          int(bown.numel()), _p(bown.contiguous()), _p(uown), _lib.stream()),
+               "oni_place_owner")
+    return uown
 
 
 def route_unpack(recv: torch.Tensor, recv_counts: list, key_counts: list, kid: torch.Tensor, weights: bool):

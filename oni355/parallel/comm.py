@@ -39,8 +39,11 @@ class Comm:
         self.dist = world > 1 or forced
 
     # -- basic ------------------------------------------------------------------------------------
+    # A 1-rank group (ONI_FORCE_DIST=1) reduces, broadcasts and gathers as the identity: the
+    # data-parallel code paths around the collectives run, the collectives themselves (one RCCL
+    # copy kernel each) do not -- as in the sweeps' X01 (models/gibbs.py _allreduce_dn).
     def allreduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
-        if self.dist:
+        if self.dist and self.world > 1:
             rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
             if self._via_host and t.is_cuda:
                 h = t.cpu()
@@ -54,13 +57,13 @@ class Comm:
         """Sum over ranks → host array. ``a``: a host array, or a device tensor (reduced where it
         lives -- no host→device copy; the caller's tensor is left unchanged)."""
         if torch.is_tensor(a):
-            if not self.dist:
+            if not self.dist or self.world == 1:
                 return a.cpu().numpy()
             t = a.to(self._coll_device, copy=True)
             dist.all_reduce(t, group=self.group)
             return t.cpu().numpy()
         a = np.asarray(a)
-        if not self.dist:
+        if not self.dist or self.world == 1:
             return a
         # a private copy: on CPU collectives torch.from_numpy would alias (and reduce into) ``a``
         t = self._small_tensor(a) if a.size == 1 else torch.from_numpy(np.array(a, copy=True)).to(self._coll_device)
@@ -78,7 +81,7 @@ class Comm:
                           device=self._coll_device)
 
     def allreduce_scalar(self, x: float, op: str = "sum") -> float:
-        if not self.dist:
+        if not self.dist or self.world == 1:
             return float(x)
         t = torch.full((1,), float(x), dtype=torch.float64, device=self._coll_device)
         dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
@@ -93,7 +96,7 @@ class Comm:
                 dist.barrier(group=self.group)
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
-        if self.dist:
+        if self.dist and self.world > 1:
             if self._via_host and t.is_cuda:
                 h = t.cpu()
                 dist.broadcast(h, src=src, group=self.group)

@@ -96,8 +96,8 @@ def encode_words(word_keys64: torch.Tensor, comm: Comm | None, key_bits: int = 6
     else:
         luniq, inv = torch.unique(word_keys64, return_inverse=True)
         lids = inv.to(torch.int32)
-    if comm is None or not comm.dist:
-        return luniq, lids
+    if comm is None or not comm.dist or comm.world == 1:
+        return luniq, lids  # one rank: the local dictionary is the global one
     parts = comm.allgather_var(luniq)
     vocab = torch.unique(torch.cat([p.to(luniq.device) for p in parts]))
     remap = torch.searchsorted(vocab, luniq).to(torch.int32)
@@ -205,22 +205,27 @@ def place_docs(doc_keys64: torch.Tensor, weights: torch.Tensor | None, comm: Com
 
     IP documents are power-law sized (one synthetic 100M-flow day puts ~8 % of all tokens on a
     single IP), so a plain hash leaves the busiest rank ~1.5× the mean at 8 ranks and every sweep
-    waits for it. Every rank proposes its ``HEAVY_DOCS_PER_RANK`` locally heaviest documents; the
-    union of the proposals gets exact global counts (one all-reduce over the candidates, not an
-    all-gather of every document); every other document falls into one of
+    waits for it. Every rank proposes the documents holding more than 1/``HEAVY_DOCS_PER_RANK`` of
+    its tokens (at most that many: a threshold, no sort; any document above 1/H of the global
+    tokens is proposed by at least one rank); the union of the proposals gets exact global counts
+    (one all-reduce over the candidates, not an all-gather of every document); every other
+    document falls into one of
     ``PLACEMENT_BUCKETS_PER_RANK × world`` hash buckets, and candidates and buckets together are
     placed by longest-processing-time greedy (:func:`lpt_place`). Collective volume is
     O(candidates · world), independent of the number of documents.
-    Deterministic on every rank (same candidate set and counts; order count desc, key asc; ties →
-    lowest rank); results stay world-size invariant because the sampler's chain never depends on
-    placement. Returns the owner of every token, or with ``per_doc`` (owner of every local
+    The candidate counts and bucket loads come from one kernel (``ops.corpus.place_stats``), the
+    owner of every document from another (``place_owner``); the host only runs the LPT over
+    ≤ H·world + 64·world items. Deterministic on every rank (same candidate set and counts; order
+    count desc, key asc; ties → lowest rank); results stay world-size invariant because the
+    sampler's chain never depends on placement. Returns the owner of every token, or with ``per_doc`` (owner of every local
     document int32, document id of every token int32, sorted unique local doc keys int64).
     ``split_L`` > 0 (the chunk length) also cuts candidates above 1/(SPLIT_DEN · world) of all
     tokens into pieces (:class:`SplitPlan`, appended to the return value; a split document's
     tokens go to its primary)."""
     W = comm.world
     dev = doc_keys64.device
-    if doc_keys64.is_cuda:
+    cuda = doc_keys64.is_cuda
+    if cuda:
         from ..ops import corpus as oc
         ukeys, inv, ucnt = oc.dict_encode(doc_keys64.contiguous(), 32,
                                           weights.to(torch.int32) if weights is not None else None, counts=True)
@@ -228,25 +233,15 @@ def place_docs(doc_keys64: torch.Tensor, weights: torch.Tensor | None, comm: Com
         ukeys, inv = encode_docs(doc_keys64.contiguous())
         w = weights.to(torch.int64) if weights is not None else torch.ones(inv.numel(), dtype=torch.int64)
         ucnt = torch.zeros(ukeys.numel(), dtype=torch.int64).index_add_(0, inv.long(), w)
-    U = int(ukeys.numel())
-    # local proposals: heaviest first, ties by key (ukeys is ascending, the sort is stable)
-    top = torch.argsort(ucnt, descending=True, stable=True)[: min(HEAVY_DOCS_PER_RANK, U)]
-    cand = torch.unique(torch.cat([p.to(dev) for p in comm.allgather_var(ukeys[top].contiguous())]))
-    if U:
-        pos = torch.searchsorted(ukeys, cand).clamp_(max=U - 1)
-        hit = ukeys[pos] == cand
-    else:
-        pos = torch.zeros_like(cand)
-        hit = torch.zeros(cand.numel(), dtype=torch.bool, device=dev)
-    ccnt = torch.where(hit, ucnt[pos] if U else torch.zeros_like(cand), torch.zeros_like(cand))
-    is_cand = torch.zeros(U, dtype=torch.bool, device=dev)
-    is_cand[pos[hit]] = True
+    # local proposals: every document holding more than 1/H of this rank's tokens -- at most H of
+    # them, picked by a threshold instead of a sort; ukeys is ascending, so the proposals are too
+    prop = ukeys[ucnt * HEAVY_DOCS_PER_RANK > ucnt.sum()].contiguous()
+    cand = prop if W == 1 else torch.unique(torch.cat([p.to(dev) for p in comm.allgather_var(prop)]))
     # all other documents are hashed into B buckets that are placed like documents, so the rank
     # that takes a huge IP takes correspondingly fewer light ones
     B = PLACEMENT_BUCKETS_PER_RANK * W
-    hb = doc_owner(ukeys, B)
-    bload = torch.zeros(B, dtype=torch.int64, device=dev).index_add_(0, hb[~is_cand], ucnt[~is_cand])
-    both = torch.cat([ccnt, bload])  # one collective for candidate counts + bucket loads
+    # candidate counts ‖ bucket loads, summed over the ranks in one collective
+    both = oc.place_stats(ukeys, ucnt, cand, B) if cuda else _place_stats_ref(ukeys, ucnt, cand, B)
     comm.allreduce_(both)
     nc = int(cand.numel())
     bc = both.cpu().numpy().astype(np.int64)
@@ -273,18 +268,42 @@ def place_docs(doc_keys64: torch.Tensor, weights: torch.Tensor | None, comm: Com
         first = np.r_[True, pdoc[1:] != pdoc[:-1]]
         primary[:] = piece_owner[first]
         cown[sp_idx] = primary
-    bown = torch.from_numpy(iown[n_ns + n_p:]).to(dev)
-    uown = bown[hb]
-    uown[pos[hit]] = torch.from_numpy(cown).to(dev)[hit]
+    bown = torch.from_numpy(iown[n_ns + n_p:].astype(np.int32)).to(dev)
+    cown_t = torch.from_numpy(cown.astype(np.int32)).to(dev)
+    uown = oc.place_owner(ukeys, cand, cown_t, bown) if cuda else _place_owner_ref(ukeys, cand, cown_t, bown)
     plan = None
     if sp.any():
         plan = SplitPlan(keys=cand[torch.from_numpy(sp_idx).to(dev)].cpu(), count=ccg[sp], piece_doc=pdoc,
                          piece_p0=pp0, piece_p1=pp1, piece_owner=piece_owner, primary=primary, L=int(split_L))
     if per_doc:
-        out = (uown.to(torch.int32), inv, ukeys)
+        out = (uown, inv, ukeys)
     else:
-        out = uown[inv.long()]
+        out = uown.long()[inv.long()]
     return (out, plan) if split_L is not None else out
+
+
+def _place_stats_ref(ukeys: torch.Tensor, ucnt: torch.Tensor, cand: torch.Tensor, B: int) -> torch.Tensor:
+    """Torch twin of ``ops.corpus.place_stats`` (the CPU path): candidate counts ‖ bucket loads."""
+    nc = int(cand.numel())
+    both = torch.zeros(nc + B, dtype=torch.int64, device=ukeys.device)
+    hit = torch.zeros(ukeys.numel(), dtype=torch.bool, device=ukeys.device)
+    if nc and ukeys.numel():
+        pos = torch.searchsorted(cand, ukeys).clamp_(max=nc - 1)
+        hit = cand[pos] == ukeys
+        both[pos[hit]] = ucnt[hit]
+    both[nc:].index_add_(0, doc_owner(ukeys[~hit], B), ucnt[~hit])
+    return both
+
+
+def _place_owner_ref(ukeys: torch.Tensor, cand: torch.Tensor, cown: torch.Tensor, bown: torch.Tensor) -> torch.Tensor:
+    """Torch twin of ``ops.corpus.place_owner``: owner of every document (int32)."""
+    uown = bown[doc_owner(ukeys, int(bown.numel()))]
+    nc = int(cand.numel())
+    if nc and ukeys.numel():
+        pos = torch.searchsorted(cand, ukeys).clamp_(max=nc - 1)
+        hit = cand[pos] == ukeys
+        uown[hit] = cown[pos[hit]]
+    return uown
 
 
 def balanced_owner(doc_keys64: torch.Tensor, weights: torch.Tensor, comm: Comm) -> torch.Tensor:
@@ -322,25 +341,26 @@ def route_to_owners(doc_keys64: torch.Tensor, word_ids: torch.Tensor, weights: t
     if doc_keys64.is_cuda:
         from ..ops import corpus as oc
         (uown, ids, ukeys), plan = place_docs(doc_keys64, weights, comm, per_doc=True, split_L=split_L)
-        U = int(ukeys.numel())
-        # key lists per owner: the local docs grouped by owner, ascending keys inside a group
-        kperm = torch.argsort(uown, stable=True)
-        kcounts = torch.bincount(uown.long(), minlength=comm.world)
-        kstart = _excl_cumsum(kcounts)
-        pos = torch.empty(U, dtype=torch.int32, device=ukeys.device)
-        pos[kperm] = (torch.arange(U, dtype=torch.int64, device=ukeys.device)
-                      - kstart[uown[kperm].long()]).to(torch.int32)
-        ksend = i64_to_u32bits(ukeys[kperm]).to(torch.int32).contiguous()
+        W = comm.world
+        # key lists per owner (the local docs grouped by owner, ascending keys inside a group) and
+        # every doc's position in its owner's list: one stable partition of the documents
+        _, kcounts, pos, ksend = oc.partition(uown, W, keys64=ukeys, rank=True)
         send, order, counts = oc.route_pack_ids(uown, ids, pos, word_ids.to(torch.int32).contiguous(),
-                                                weights, comm.world)
-        # both count vectors travel in one small exchange, then the two payload alltoallvs
-        sc = torch.stack([counts.to(torch.int64), kcounts.to(torch.int64)], 1).reshape(-1).contiguous()
-        rcm = comm.alltoallv(sc.view(comm.world, 2), [1] * comm.world, recv_counts=[1] * comm.world).reshape(-1).tolist()
-        rc, krc = rcm[0::2], rcm[1::2]
-        scl, kcl = counts.tolist(), kcounts.tolist()
+                                                weights, W)
+        # both count vectors travel in one small exchange, then the two payload alltoallvs; one
+        # host read for sent and received counts
+        sc = torch.stack([counts, kcounts], 1).reshape(-1).contiguous()
+        rcm = comm.alltoallv(sc.view(W, 2), [1] * W, recv_counts=[1] * W).reshape(-1)
+        host = torch.cat([sc, rcm.to(sc.device)]).tolist()
+        scl, kcl, rc, krc = host[0:2 * W:2], host[1:2 * W:2], host[2 * W::2], host[2 * W + 1::2]
         rkeys = comm.alltoallv(ksend, kcl, recv_counts=krc)
         recv = comm.alltoallv(send, scl, recv_counts=rc)
-        udoc, kid = encode_docs(u32_to_i64(rkeys.view(-1)).contiguous())
+        if W == 1:
+            # a 1-rank group receives its own ascending key list: it already is the dictionary
+            udoc = ukeys
+            kid = torch.arange(udoc.numel(), dtype=torch.int32, device=udoc.device)
+        else:
+            udoc, kid = encode_docs(u32_to_i64(rkeys.view(-1)).contiguous())
         inv, wi, wt = oc.route_unpack(recv.contiguous(), rc, krc, kid, weights is not None)
         return udoc, inv, wi, wt, Route(order, scl, rc, plan)
     owner, plan = place_docs(doc_keys64, weights, comm, split_L=split_L)
@@ -988,8 +1008,8 @@ def _top_n_from_hist(score, hist, tol, maxresults, comm, row_offset, order=None,
         bmax = 2047 if maxresults > 0 else -1
     else:
         bmax = int(np.searchsorted(cum, min(maxresults, int(cum[-1])), side="left"))
-    if return_pos and comm is not None and comm.dist:
-        raise ValueError("top_n: positions are only defined without a process group")
+    if return_pos and comm is not None and comm.dist and comm.world > 1:
+        raise ValueError("top_n: positions are only defined on one rank")
     if bmax < 0:
         e = torch.zeros(0, dtype=torch.int64, device=score.device)
         out = (e, torch.zeros(0, dtype=torch.float32, device=score.device))
@@ -998,31 +1018,23 @@ def _top_n_from_hist(score, hist, tol, maxresults, comm, row_offset, order=None,
     cap = int(np.cumsum(h_loc)[bmax])
     pos, sc = ops.select_below(score, tol, bmax, cap=max(cap, 1))
     idx = order[pos] if order is not None else pos
-    if comm is None or not comm.dist:
-        # world 1: the ≤ a few thousand candidates come to the host in ONE copy and are ordered
-        # there (a chain of tiny device sorts / gathers was ~2 ms of launch and sync gaps per day);
-        # results are host tensors
-        packed = torch.stack([idx.to(torch.int64), pos.to(torch.int64),
-                              sc.view(torch.int32).to(torch.int64)]).cpu().numpy()
-        gid = packed[0] + int(row_offset)
-        sch = packed[2].astype(np.int32).view(np.float32)
-        o = np.lexsort((gid, sch))[:maxresults]  # by score, ties by global row id
-        out = (torch.from_numpy(gid[o].copy()), torch.from_numpy(sch[o].copy()))
-        return out + (torch.from_numpy(packed[1][o].copy()),) if return_pos else out
-    gid = idx + row_offset
-    # exact order: (score, global id); keep local top-N then merge
-    o1 = torch.argsort(gid, stable=True)
-    o2 = o1[torch.argsort(sc[o1], stable=True)][:maxresults]
-    gid, sc = gid[o2], sc[o2]
+    # the ≤ a few thousand candidates come to the host in ONE copy and are ordered there (a chain
+    # of tiny device sorts / gathers was ~2 ms of launch and sync gaps per day); results are host
+    # tensors
+    packed = torch.stack([idx.to(torch.int64), pos.to(torch.int64),
+                          sc.view(torch.int32).to(torch.int64)]).cpu().numpy()
+    gid = packed[0] + int(row_offset)
+    sch = packed[2].astype(np.int32).view(np.float32)
+    o = np.lexsort((gid, sch))[:maxresults]  # by score, ties by global row id
     if return_pos:
-        return gid, sc, pos[o2]
-    if comm is not None and comm.dist:
-        # one all-gather of (global id, score bits) pairs
-        both = torch.cat(comm.allgather_var(torch.stack([gid.to(torch.int64),
-                                                         sc.view(torch.int32).to(torch.int64)], 1)))
-        gid, sc = both[:, 0].contiguous(), both[:, 1].to(torch.int32).view(torch.float32)
-        o1 = torch.argsort(gid, stable=True)
-        gid, sc = gid[o1], sc[o1]
-        o2 = torch.argsort(sc, stable=True)
-        gid, sc = gid[o2][:maxresults], sc[o2][:maxresults]
-    return gid, sc
+        return (torch.from_numpy(gid[o].copy()), torch.from_numpy(sch[o].copy()),
+                torch.from_numpy(packed[1][o].copy()))
+    gid, bits = gid[o], packed[2][o]
+    if comm is not None and comm.dist and comm.world > 1:
+        # one all-gather of every rank's local top-N (global id, score bits), merged on the host
+        loc = torch.from_numpy(np.stack([gid, bits], 1).astype(np.int64)).to(score.device)
+        both = torch.cat([p.to(score.device) for p in comm.allgather_var(loc)]).cpu().numpy()
+        gid, bits = both[:, 0], both[:, 1]
+        o = np.lexsort((gid, bits.astype(np.int32).view(np.float32)))[:maxresults]
+        gid, bits = gid[o], bits[o]
+    return torch.from_numpy(np.ascontiguousarray(gid)), torch.from_numpy(bits.astype(np.int32).view(np.float32))

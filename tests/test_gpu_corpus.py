@@ -130,6 +130,48 @@ def test_route_pack_is_stable_owner_partition(gpu, n, W, weighted):
     assert torch.equal(send.cpu(), torch.stack(cols, 1))
 
 
+@pytest.mark.parametrize("n,W", [(0, 1), (1, 1), (5000, 2), (2049, 64), (1_234_567, 8), (300_000, 256)])
+def test_partition_is_stable_argsort_with_ranks(gpu, n, W):
+    """oni_partition == stable argsort by owner (order), bincount (counts), slot within the owner
+    group (rank) and the keys' u32 bits in slot order -- with and without an id indirection."""
+    r = np.random.default_rng(n + W)
+    U = max(n // 3, 1)
+    own = torch.from_numpy(r.integers(0, W, U).astype(np.int32))
+    ids = torch.from_numpy(r.integers(0, U, n).astype(np.int32))
+    keys = torch.from_numpy(r.integers(0, 2**32, n, dtype=np.int64))
+    order, counts, rank, kout = oc.partition(own.to(gpu), W, ids=ids.to(gpu), keys64=keys.to(gpu), rank=True)
+    tok = own[ids.long()].long()
+    ref = torch.argsort(tok, stable=True)
+    assert torch.equal(order.cpu().long(), ref)
+    cnt = torch.bincount(tok, minlength=W)
+    assert torch.equal(counts.cpu(), cnt)
+    start = torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(cnt, 0)[:-1]])
+    ref_rank = torch.empty(n, dtype=torch.int64)
+    ref_rank[ref] = torch.arange(n) - start[tok[ref]]
+    assert torch.equal(rank.cpu().long(), ref_rank)
+    assert torch.equal(kout.cpu(), common.i64_to_u32bits(keys[ref]))
+    o2, c2, _, _ = oc.partition(own.to(gpu), W)  # documents themselves
+    assert torch.equal(o2.cpu().long(), torch.argsort(own.long(), stable=True))
+    assert torch.equal(c2.cpu(), torch.bincount(own.long(), minlength=W))
+
+
+@pytest.mark.parametrize("U,B,nc", [(1, 1, 0), (10_000, 64, 37), (500_000, 512, 4096), (200_000, 8192, 100)])
+def test_place_kernels_match_torch_twins(gpu, U, B, nc):
+    """place_stats / place_owner (csrc/kernels/route.hip) == the torch twins place_docs uses on the
+    CPU: candidate counts, hash-bucket loads (LDS and global-atomic bucket paths) and owners."""
+    r = np.random.default_rng(U + B)
+    ukeys = torch.from_numpy(np.unique(r.integers(0, 2**32, U, dtype=np.int64)))
+    ucnt = torch.from_numpy(r.zipf(1.3, ukeys.numel()).clip(max=10**6).astype(np.int64))
+    extra = torch.from_numpy(r.integers(0, 2**32, nc // 2, dtype=np.int64))  # candidates absent here
+    cand = torch.unique(torch.cat([ukeys[torch.from_numpy(r.permutation(ukeys.numel())[: nc - nc // 2])], extra]))
+    both = oc.place_stats(ukeys.to(gpu), ucnt.to(gpu), cand.to(gpu), B)
+    assert torch.equal(both.cpu(), common._place_stats_ref(ukeys, ucnt, cand, B))
+    cown = torch.from_numpy(r.integers(0, 8, cand.numel()).astype(np.int32))
+    bown = torch.from_numpy(r.integers(0, 8, B).astype(np.int32))
+    got = oc.place_owner(ukeys.to(gpu), cand.to(gpu), cown.to(gpu), bown.to(gpu))
+    assert torch.equal(got.cpu(), common._place_owner_ref(ukeys, cand, cown, bown))
+
+
 @pytest.mark.parametrize("W,weighted", [(1, False), (3, True), (8, False)])
 def test_route_ids_unpack_equals_key_routing(gpu, W, weighted):
     """Id routing (route_pack_ids at every source + key lists + route_unpack at the owner) gives

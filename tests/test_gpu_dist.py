@@ -123,9 +123,11 @@ def _forced_rccl_worker(port, n_total, sweeps, out_q, heavy=0.0):
 
 @pytest.mark.parametrize("heavy", [0.0, 0.30])
 def test_forced_rccl_sweeps_replay_from_graphs_bitwise(gpu, heavy):
-    """A 1-rank RCCL process group (ONI_FORCE_DIST=1): the per-sweep Δ all-reduce is captured into
-    the sweep HIP graphs and the run stays bitwise equal to the collective-free world=1 run -- also
-    with a 30 % IP cut into pieces whose Δn_dk rows ride in the captured X01 buffer."""
+    """A 1-rank RCCL process group (ONI_FORCE_DIST=1): every data-parallel code path (placement,
+    routing, split pieces, owner scoring, result merge) runs, the sweeps replay from HIP graphs, and
+    the run stays bitwise equal to the world=1 run -- also with a 30 % IP cut into pieces whose
+    Δn_dk rows travel in the X01 buffer. (A 1-rank group's collectives are the identity: no RCCL
+    kernel runs, comm.Comm.)"""
     n, sweeps = 20_000, 8
     from oni355.pipeline.flow import run_flow
     plain = run_flow(_flow_cols(n, heavy), K=20, sweeps=sweeps, maxresults=200, device="cuda:0")
@@ -141,7 +143,7 @@ def test_forced_rccl_sweeps_replay_from_graphs_bitwise(gpu, heavy):
             p.kill()
     assert p.exitcode == 0
     assert n_graphs >= 1, "DP sweeps were not captured into a HIP graph"
-    assert ar_ms is not None and ar_ms > 0 and ar_bytes > 0
+    assert ar_ms is not None and ar_bytes > 0
     assert np.array_equal(plain.rows, rows) and np.array_equal(plain.scores, scores)
     assert plain.stats["loglik"] == ll
     assert (n_split >= 1) == (heavy > 0)

@@ -10,6 +10,7 @@
 #   smoke                 __graft_entry__.smoke()
 #   bench[:<args>]        python bench.py <args>            (args: comma-separated, e.g. bench:--steps,20)
 #   prof[:<args>]         rocprofv3 --kernel-trace --stats -- python bench.py <args>
+#   mprof[:<args>]        the same plus --marker-trace (the package's roctx ranges)
 #   pmc:<ctrs>[:<args>]   rocprofv3 --pmc <ctrs> --kernel-trace --stats (ctrs comma-separated)
 #   py:<script>[:<args>]  python <script> <args>
 #   list                  rocprofv3 --list-avail (PMC counter names of this GPU)
@@ -47,6 +48,10 @@ for step in "$@"; do
       IFS=',' read -r -a args <<< "$rest"
       timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$n" -o run \
         -- python3 -u bench.py "${args[@]}" > "$OUT/prof_$n.log" 2>&1; rc=$? ;;
+    mprof)
+      IFS=',' read -r -a args <<< "$rest"
+      timeout -k 10 900 rocprofv3 --marker-trace --kernel-trace --stats --output-format csv -d "$OUT/mprof_$n" -o run \
+        -- python3 -u bench.py "${args[@]}" > "$OUT/mprof_$n.log" 2>&1; rc=$? ;;
     pmc)
       ctrs="${rest%%:*}"; bargs=""; [[ "$rest" == *:* ]] && bargs="${rest#*:}"
       IFS=',' read -r -a args <<< "$bargs"

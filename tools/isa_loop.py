@@ -21,7 +21,7 @@ def kernel_lines(path, sym):
             if sym in l.split(":")[0]:
                 start = i
                 continue
-        if start is not None and (l.startswith(".Lfunc_end") or l.strip().startswith("s_endpgm")):
+        if start is not None and l.startswith(".Lfunc_end"):
             return lines[start:i + 1]
     raise SystemExit(f"kernel {sym} not found")
 
@@ -48,7 +48,7 @@ def main():
     labels = {}
     insts = []  # (index, label-or-None, mnemonic, text)
     for l in body:
-        s = l.strip()
+        s = l.split(";")[0].strip()
         if not s or s.startswith((";", ".")) and not s.startswith(".LBB"):
             continue
         if s.startswith(".LBB") and s.endswith(":"):

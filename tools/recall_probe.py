@@ -56,13 +56,30 @@ def main() -> int:
                         top_domains=top_domain_list(), chunk_len=a.chunk_len)
     rank = {int(r): i for i, r in enumerate(res.rows)}
     ranks = np.array(sorted(rank.get(int(x), a.n) for x in day.anomaly_rows))
+    # quiet vs active clients of the planted rows (dns / proxy): a client is "quiet" when it is in
+    # the least active tenth of the day's clients by event count
+    split = {}
+    ccol = {"dns": "ip_dst", "proxy": "clientip"}.get(a.source)
+    if ccol is not None and len(day.anomaly_rows):
+        cli = np.asarray(day.cols[ccol])
+        uc, inv, cnt = np.unique(cli, return_inverse=True, return_counts=True)
+        quiet_max = np.sort(cnt)[max(0, uc.size // 10 - 1)]
+        ar = np.asarray(day.anomaly_rows, dtype=np.int64)
+        ev = cnt[inv[ar]]
+        hit = np.array([rank.get(int(x), a.n) < a.maxresults for x in ar])
+        q = ev <= quiet_max
+        split = {"clients": int(uc.size), "quiet_client_max_events": int(quiet_max),
+                 "planted_on_quiet_clients": int(q.sum()), "planted_on_active_clients": int((~q).sum()),
+                 "recall_quiet": float(hit[q].mean()) if q.any() else None,
+                 "recall_active": float(hit[~q].mean()) if (~q).any() else None,
+                 "planted_client_events_p50": int(np.median(ev))}
     out = {"source": a.source, "n": a.n, "wide": a.wide, "kind": a.anomaly_kind, "K": K, "sweeps": a.sweeps,
            "lt_codebook": a.lt_codebook if a.source == "flow" and a.wide else None,
            "ms_per_sweep": round(res.timings.get("train_dev_s", res.timings.get("train_s", 0)) / a.sweeps * 1e3, 4),
            "vocab": int(res.lda.vocab.numel()), "anomalies": int(ranks.size),
            "recall_topN": float(np.mean(ranks < a.maxresults)), "maxresults": a.maxresults,
            "rank_p50": int(np.median(ranks)), "rank_max": int(ranks.max()), "ranks_head": ranks[:20].tolist(),
-           "loglik": res.stats.get("loglik"), "wall_s": round(time.perf_counter() - t0, 1)}
+           "loglik": res.stats.get("loglik"), "wall_s": round(time.perf_counter() - t0, 1), **split}
     print(json.dumps(out), flush=True)
     return 0
 

@@ -35,6 +35,7 @@ def main() -> int:
     from oni355.models.gibbs import tiling_for
     G, KP = tiling_for(a.K)  # the tiling the model of K topics samples with (K ≥ 100: MH, KS = K)
     KS = G * KP
+    a.worlds = a.worlds.replace("+", ",")  # tools/gpu.sh splits arguments at commas
     Wmax = max(int(w) for w in a.worlds.split(","))
     shard_words, cuts = [], None
     for r in range(Wmax):
