@@ -17,7 +17,7 @@ CONFIGS = [
 ]
 
 if __name__ == "__main__":
-    only = sys.argv[1].split(",") if len(sys.argv) > 1 else None
+    only = sys.argv[1].replace("+", ",").split(",") if len(sys.argv) > 1 else None  # tools/gpu.sh splits at commas
     for src, n, wide, kind in CONFIGS:
         if only and src not in only:
             continue

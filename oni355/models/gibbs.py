@@ -843,8 +843,10 @@ class GibbsLDA:
         (e = cfg.post_every, S = cfg.post_samples capped at total / 4e)."""
         S, e = max(1, int(self.cfg.post_samples)), max(1, int(self.cfg.post_every))
         # at most the last quarter of the chain (burn-in first): a 200-sweep day averages the 50
-        # samples of sweeps 151-200, a 30-sweep run 7, a run of < 8 sweeps none
-        S = min(S, int(total_sweeps) // (4 * e))
+        # samples of sweeps 151-200, a 30-sweep run 7, a run of < 8 sweeps none. ONI_POST_SPAN
+        # (default 0.25) sets that fraction.
+        span = float(os.environ.get("ONI_POST_SPAN", "0.25"))
+        S = min(S, int(int(total_sweeps) * span) // e)
         at = [total_sweeps - j * e for j in range(S) if total_sweeps - j * e > 0]
         self._avg_at = sorted(at) if S > 1 else []
         self._avg_cache = None

@@ -54,9 +54,11 @@ def main() -> int:
     for W in (int(w) for w in a.worlds.split(",")):
         vocab = torch.unique(torch.cat([u for u, _ in shard_words[:W]]))
         mx = torch.zeros(vocab.numel(), dtype=torch.int64, device=dev)
+        cg = torch.zeros(vocab.numel(), dtype=torch.int64, device=dev)
         for u, c in shard_words[:W]:
             idx = torch.searchsorted(vocab, u)
             mx[idx] = torch.maximum(mx[idx], c)
+            cg[idx] += c
         O8, O = 127 // W, 32767 // W
         T = int((mx <= O8).sum())
         L = int(((mx > O8) & (mx <= O)).sum())
@@ -66,8 +68,17 @@ def main() -> int:
         packed = ops.x01_packed_len(T, L, H, KS, tail) * 4
         packed16 = ops.x01_packed_len(0, T + L, H, KS, tail) * 4
         dense = (V * KS + tail) * 4
+        # modular classes (the sum taken mod 2^8 / 2^16 in int8 / int16 collectives): a word's
+        # global value lies in [-c_w, c_w] for its GLOBAL count c_w, so the class depends on c_w
+        # alone -- no per-rank offsets, no 1/W shrink of the ranges
+        mT = int((cg <= 127).sum())
+        mL = int(((cg > 127) & (cg <= 32767)).sum())
+        mH = int((cg > 32767).sum())
+        modular = (mT * KS + 2 * mL * KS + 4 * mH * KS + 4 * tail)
         out["worlds"][W] = dict(V=V, tiny=T, light=L, heavy=H, dense_MB=round(dense / 1e6, 3),
-                                packed16_MB=round(packed16 / 1e6, 3), packed_MB=round(packed / 1e6, 3))
+                                packed16_MB=round(packed16 / 1e6, 3), packed_MB=round(packed / 1e6, 3),
+                                modular_tiny=mT, modular_light=mL, modular_heavy=mH,
+                                modular_MB=round(modular / 1e6, 3))
     print(json.dumps(out))
     return 0
 
