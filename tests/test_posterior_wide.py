@@ -197,3 +197,16 @@ def test_burn_in_prefix_is_the_same_chain():
     assert not _same_chain(mh(2), mh(3), 3)    # after its hand-over the chains differ
     assert _same_chain(mh(20), mh(20), 150)
     assert not _same_chain({**base, "chain": {"sampler": "dense", "mh_burn": 0}}, mh(20), 0)
+
+
+@pytest.mark.parametrize("span,sweeps,want", [(None, 200, 50), ("0.5", 200, 50), ("0.5", 60, 30), (None, 30, 7),
+                                              ("0.75", 400, 50)])
+def test_post_span_caps_the_window(monkeypatch, span, sweeps, want):
+    """ONI_POST_SPAN: the averaging window is at most that fraction of the chain (default the last
+    quarter); ONI_POST_SAMPLES still caps the sample count."""
+    if span is None:
+        monkeypatch.delenv("ONI_POST_SPAN", raising=False)
+    else:
+        monkeypatch.setenv("ONI_POST_SPAN", span)
+    m = _model(torch.device("cpu"), sweeps=sweeps)
+    assert len(m._avg_at) == want and m._avg_at[-1] == sweeps
