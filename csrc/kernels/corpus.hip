@@ -51,7 +51,15 @@ __global__ void k_heads(const K* __restrict__ k, int64_t n, int32_t* __restrict_
   if (i < n) flag[i] = (i == 0 || k[i] != k[i - 1]) ? 1 : 0;
 }
 
-__global__ void k_dict_scatter(const uint64_t* __restrict__ ks, const int32_t* __restrict__ perm,
+// keys of at most 32 significant bits are sorted as u32: a radix pass then moves 8 B per element
+// (key + index) instead of 12
+__global__ void k_narrow(const uint64_t* __restrict__ k, int64_t n, uint32_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
+  if (i < n) out[i] = (uint32_t)k[i];
+}
+
+template <class K>
+__global__ void k_dict_scatter(const K* __restrict__ ks, const int32_t* __restrict__ perm,
                                const int32_t* __restrict__ rank, int64_t n, uint64_t* __restrict__ uniq,
                                int32_t* __restrict__ ids, int64_t* __restrict__ n_uniq, int64_t* __restrict__ head) {
   const int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
@@ -59,7 +67,7 @@ __global__ void k_dict_scatter(const uint64_t* __restrict__ ks, const int32_t* _
   const int32_t r = rank[i] - 1;
   ids[perm[i]] = r;
   if (i == 0 || ks[i] != ks[i - 1]) {
-    uniq[r] = ks[i];
+    uniq[r] = (uint64_t)ks[i];
     if (head) head[r] = i;
   }
   if (i == n - 1) {
@@ -68,13 +76,15 @@ __global__ void k_dict_scatter(const uint64_t* __restrict__ ks, const int32_t* _
   }
 }
 
+template <class K>
 __global__ void k_pair_keys(const int32_t* __restrict__ doc, const int32_t* __restrict__ word, int64_t n, int64_t V,
-                            uint64_t* __restrict__ key) {
+                            K* __restrict__ key) {
   const int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
-  if (i < n) key[i] = (uint64_t)doc[i] * (uint64_t)V + (uint64_t)word[i];
+  if (i < n) key[i] = (K)((uint64_t)doc[i] * (uint64_t)V + (uint64_t)word[i]);
 }
 
-__global__ void k_pair_scatter(const uint64_t* __restrict__ ks, const int32_t* __restrict__ perm,
+template <class K>
+__global__ void k_pair_scatter(const K* __restrict__ ks, const int32_t* __restrict__ perm,
                                const int32_t* __restrict__ run, int64_t n, int64_t V, int32_t* __restrict__ pair_doc,
                                int32_t* __restrict__ pair_word, int64_t* __restrict__ head_pos,
                                int32_t* __restrict__ tok_pair, int64_t* __restrict__ nnz) {
@@ -83,8 +93,8 @@ __global__ void k_pair_scatter(const uint64_t* __restrict__ ks, const int32_t* _
   const int32_t r = run[i] - 1;
   tok_pair[perm[i]] = r;
   if (i == 0 || ks[i] != ks[i - 1]) {
-    pair_doc[r] = (int32_t)(ks[i] / (uint64_t)V);
-    pair_word[r] = (int32_t)(ks[i] % (uint64_t)V);
+    pair_doc[r] = (int32_t)((uint64_t)ks[i] / (uint64_t)V);
+    pair_word[r] = (int32_t)((uint64_t)ks[i] % (uint64_t)V);
     head_pos[r] = i;
   }
   if (i == n - 1) {
@@ -278,12 +288,14 @@ int bits_for(uint64_t maxv) {  // number of bits needed to represent values in [
 // Optional counts[n] (int64): Σ weight (1 per key without ``weight``) of every unique key -- the
 // per-document token counts the data-parallel placement needs, read off the sorted runs instead of
 // a same-address-atomic index_add (power-law documents serialise those: 12 ms at 25M tokens).
-ONI_API int oni_dict_encode(const uint64_t* keys, int64_t n, int key_bits, uint64_t* uniq, int32_t* ids,
+template <class K>
+static int dict_encode_impl(const uint64_t* keys, int64_t n, int key_bits, uint64_t* uniq, int32_t* ids,
                             int64_t* n_uniq, const int32_t* weight, int64_t* counts, void* tmp, size_t* tmp_bytes,
                             hipStream_t s) {
-  if (n >= (int64_t)1 << 31) return (int)hipErrorInvalidValue;
+  constexpr bool kNarrow = sizeof(K) == 4;
   Arena ar{static_cast<char*>(tmp)};
-  uint64_t* ks = ar.take<uint64_t>(n);
+  K* kin = kNarrow ? ar.take<K>(n) : nullptr;
+  K* ks = ar.take<K>(n);
   int32_t* iota = ar.take<int32_t>(n);
   int32_t* perm = ar.take<int32_t>(n);
   int32_t* flag = ar.take<int32_t>(n);
@@ -291,8 +303,9 @@ ONI_API int oni_dict_encode(const uint64_t* keys, int64_t n, int key_bits, uint6
   int64_t* head = counts ? ar.take<int64_t>(n + 1) : nullptr;
   int64_t* ws = counts ? ar.take<int64_t>(n) : nullptr;
   int64_t* psum = counts ? ar.take<int64_t>(n) : nullptr;
+  const K* src = kNarrow ? kin : reinterpret_cast<const K*>(keys);
   size_t sb = 0, cb = 0, wb = 0;
-  ONI_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, sb, keys, ks, iota, perm, (int)n, 0, key_bits, s));
+  ONI_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, sb, src, ks, iota, perm, (int)n, 0, key_bits, s));
   ONI_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, cb, flag, rank, (int)n, s));
   if (counts) ONI_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, wb, ws, psum, (int)n, s));
   size_t cbytes = sb > cb ? sb : cb;
@@ -306,11 +319,12 @@ ONI_API int oni_dict_encode(const uint64_t* keys, int64_t n, int key_bits, uint6
     ONI_TRY(hipMemsetAsync(n_uniq, 0, sizeof(int64_t), s));
     return (int)hipGetLastError();
   }
+  if constexpr (kNarrow) k_narrow<<<nblk(n), kB, 0, s>>>(keys, n, reinterpret_cast<uint32_t*>(kin));
   k_iota<<<nblk(n), kB, 0, s>>>(iota, n);
-  ONI_TRY(hipcub::DeviceRadixSort::SortPairs(cub, cbytes, keys, ks, iota, perm, (int)n, 0, key_bits, s));
-  k_heads<uint64_t><<<nblk(n), kB, 0, s>>>(ks, n, flag);
+  ONI_TRY(hipcub::DeviceRadixSort::SortPairs(cub, cbytes, src, ks, iota, perm, (int)n, 0, key_bits, s));
+  k_heads<K><<<nblk(n), kB, 0, s>>>(ks, n, flag);
   ONI_TRY(hipcub::DeviceScan::InclusiveSum(cub, cbytes, flag, rank, (int)n, s));
-  k_dict_scatter<<<nblk(n), kB, 0, s>>>(ks, perm, rank, n, uniq, ids, n_uniq, head);
+  k_dict_scatter<K><<<nblk(n), kB, 0, s>>>(ks, perm, rank, n, uniq, ids, n_uniq, head);
   if (counts) {
     k_weights_sorted<<<nblk(n), kB, 0, s>>>(weight, perm, n, ws);
     ONI_TRY(hipcub::DeviceScan::InclusiveSum(cub, cbytes, ws, psum, (int)n, s));
@@ -319,18 +333,26 @@ ONI_API int oni_dict_encode(const uint64_t* keys, int64_t n, int key_bits, uint6
   return (int)hipGetLastError();
 }
 
+ONI_API int oni_dict_encode(const uint64_t* keys, int64_t n, int key_bits, uint64_t* uniq, int32_t* ids,
+                            int64_t* n_uniq, const int32_t* weight, int64_t* counts, void* tmp, size_t* tmp_bytes,
+                            hipStream_t s) {
+  if (n >= (int64_t)1 << 31) return (int)hipErrorInvalidValue;
+  if (key_bits <= 32)
+    return dict_encode_impl<uint32_t>(keys, n, key_bits, uniq, ids, n_uniq, weight, counts, tmp, tmp_bytes, s);
+  return dict_encode_impl<uint64_t>(keys, n, key_bits, uniq, ids, n_uniq, weight, counts, tmp, tmp_bytes, s);
+}
+
 // ------------------------------------------------------------------------------------------------
 // pair_build: tokens (doc, word[, weight]) → distinct pairs (doc-major, word-sorted) with counts,
 // tok_pair[n] (pair of every token), nnz on device; order0[n0] = tokens < n0 sorted by pair
 // (stable: the score plan's first-endpoint event order). Outputs sized n (nnz ≤ n).
-ONI_API int oni_pair_build(const int32_t* doc, const int32_t* word, const int32_t* weight, int64_t n, int64_t D,
-                           int64_t V, int32_t* pair_doc, int32_t* pair_word, int32_t* pair_cnt, int32_t* tok_pair,
+template <class K>
+static int pair_build_impl(const int32_t* doc, const int32_t* word, const int32_t* weight, int64_t n, int64_t V,
+                           int bits, int32_t* pair_doc, int32_t* pair_word, int32_t* pair_cnt, int32_t* tok_pair,
                            int64_t* nnz, int32_t* order0, int64_t n0, void* tmp, size_t* tmp_bytes, hipStream_t s) {
-  if (n >= (int64_t)1 << 31) return (int)hipErrorInvalidValue;
-  const int bits = bits_for((uint64_t)(D > 0 ? D : 1) * (uint64_t)(V > 0 ? V : 1));
   Arena ar{static_cast<char*>(tmp)};
-  uint64_t* key = ar.take<uint64_t>(n);
-  uint64_t* ks = ar.take<uint64_t>(n);
+  K* key = ar.take<K>(n);
+  K* ks = ar.take<K>(n);
   int32_t* iota = ar.take<int32_t>(n);
   int32_t* perm = ar.take<int32_t>(n);
   int32_t* flag = ar.take<int32_t>(n);
@@ -357,17 +379,29 @@ ONI_API int oni_pair_build(const int32_t* doc, const int32_t* word, const int32_
     ONI_TRY(hipMemsetAsync(nnz, 0, sizeof(int64_t), s));
     return (int)hipGetLastError();
   }
-  k_pair_keys<<<nblk(n), kB, 0, s>>>(doc, word, n, V, key);
+  k_pair_keys<K><<<nblk(n), kB, 0, s>>>(doc, word, n, V, key);
   k_iota<<<nblk(n), kB, 0, s>>>(iota, n);
   ONI_TRY(hipcub::DeviceRadixSort::SortPairs(cub, cbytes, key, ks, iota, perm, (int)n, 0, bits, s));
-  k_heads<uint64_t><<<nblk(n), kB, 0, s>>>(ks, n, flag);
+  k_heads<K><<<nblk(n), kB, 0, s>>>(ks, n, flag);
   ONI_TRY(hipcub::DeviceScan::InclusiveSum(cub, cbytes, flag, run, (int)n, s));
-  k_pair_scatter<<<nblk(n), kB, 0, s>>>(ks, perm, run, n, V, pair_doc, pair_word, head, tok_pair, nnz);
+  k_pair_scatter<K><<<nblk(n), kB, 0, s>>>(ks, perm, run, n, V, pair_doc, pair_word, head, tok_pair, nnz);
   k_weights_sorted<<<nblk(n), kB, 0, s>>>(weight, perm, n, ws);
   ONI_TRY(hipcub::DeviceScan::InclusiveSum(cub, cbytes, ws, psum, (int)n, s));
   k_pair_counts<<<nblk(n), kB, 0, s>>>(head, psum, nnz, n, pair_cnt);
   if (order0 && n0 > 0) ONI_TRY(hipcub::DeviceSelect::If(cub, cbytes, perm, order0, nsel, (int)n, BelowN{(int32_t)n0}, s));
   return (int)hipGetLastError();
+}
+
+ONI_API int oni_pair_build(const int32_t* doc, const int32_t* word, const int32_t* weight, int64_t n, int64_t D,
+                           int64_t V, int32_t* pair_doc, int32_t* pair_word, int32_t* pair_cnt, int32_t* tok_pair,
+                           int64_t* nnz, int32_t* order0, int64_t n0, void* tmp, size_t* tmp_bytes, hipStream_t s) {
+  if (n >= (int64_t)1 << 31) return (int)hipErrorInvalidValue;
+  const int bits = bits_for((uint64_t)(D > 0 ? D : 1) * (uint64_t)(V > 0 ? V : 1));
+  if (bits <= 32)
+    return pair_build_impl<uint32_t>(doc, word, weight, n, V, bits, pair_doc, pair_word, pair_cnt, tok_pair, nnz,
+                                     order0, n0, tmp, tmp_bytes, s);
+  return pair_build_impl<uint64_t>(doc, word, weight, n, V, bits, pair_doc, pair_word, pair_cnt, tok_pair, nnz,
+                                   order0, n0, tmp, tmp_bytes, s);
 }
 
 // ------------------------------------------------------------------------------------------------
