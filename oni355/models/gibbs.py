@@ -35,6 +35,7 @@ INT32_COUNT_MAX = 2**31 - 1
 # X01 payload packing pays only once the all-reduce is bandwidth-bound (see GibbsLDA._x01_wanted)
 X01_PACK_MIN_BYTES = 4 << 20
 # sweep kernels (-> oni_gibbs_launch variant argument): every one draws the same topics bit for bit
+MH_ALIAS_MAX_BYTES = 128e6  # word alias records above this size (half the MALL) use the CDF proposal
 SAMPLERS = {"generic": 0, "lds": 2, "x1": 3, "mh": ops.SAMPLER_MH}
 
 
@@ -299,13 +300,17 @@ class GibbsLDA:
         # -- a 64-B row of bucket prefix sums per word (a streaming pass over q) with the bucket's q
         # values as the second level (two gathers and ~60 more VALU per token). "auto" takes the CDF
         # when 3·V·K > 2·T (global tokens): measured at K = 100 the record build costs ~10 ps per
-        # cell and the CDF draw ~6 ps per token more (profiles/r5/).
+        # cell and the CDF draw ~6 ps per token more (profiles/r5/) -- or when the records
+        # (V·K·16 B) outgrow half of the 256 MB MALL, where their gathers miss: at V = 349k,
+        # T = 125M the CDF ran 4.38 against the records' 4.62 ms/sweep
+        # (profiles/r5/bench_k100_realistic_62.5M_{alias,cdf}.json).
         T_all = torch.tensor([float(c.T)], dtype=torch.float64)
         if self.comm is not None and self.comm.dist:
             T_all = self.comm.allreduce_(T_all.to(self.comm.device)).cpu()
         kind = os.environ.get("ONI_MH_WORD", "auto")
         if kind == "auto":
-            kind = "cdf" if 3.0 * self.V * self.K > 2.0 * float(T_all[0]) else "alias"
+            kind = ("cdf" if 3.0 * self.V * self.K > 2.0 * float(T_all[0]) or 16.0 * self.V * self.K > MH_ALIAS_MAX_BYTES
+                    else "alias")
         if kind not in ("alias", "cdf"):
             raise ValueError(f"unknown ONI_MH_WORD {kind}")
         self.mh_word = kind

@@ -73,7 +73,7 @@ def plan(source: str, events: int, K: int, docs: int, vocab: int, string_bytes_p
     scoring = (docs + vocab) * KS * 4
     extra = 0
     if sampler_for(K) == "mh":
-        cdf = 3 * vocab * K > 2 * T
+        cdf = 3 * vocab * K > 2 * T or 16 * vocab * K > 128e6  # models/gibbs.py _setup_mh
         extra += vocab * 64 if cdf else vocab * (K * 16 + 4)
         burn = 20 if mh_burn is None else mh_burn
         if burn > 0:
