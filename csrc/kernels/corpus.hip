@@ -248,13 +248,13 @@ __global__ void k_word_keys(const uint32_t* __restrict__ tok_word, int64_t n, ui
   }
 }
 
+// the sort wrote wsorted / wslot in place (their first T entries are the real tokens, padding
+// sorts last under key V): what is left is the inverse map and the recount tile bounds
 __global__ void k_word_index(const uint32_t* __restrict__ ks, const int32_t* __restrict__ slot, int64_t T, int tile,
-                             int32_t* __restrict__ wsorted, int32_t* __restrict__ wslot, int32_t* __restrict__ wpos,
-                             int32_t* __restrict__ tile_wlo, int32_t* __restrict__ tile_whi) {
+                             int32_t* __restrict__ wpos, int32_t* __restrict__ tile_wlo,
+                             int32_t* __restrict__ tile_whi) {
   const int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
   if (i >= T) return;
-  wsorted[i] = (int32_t)ks[i];
-  wslot[i] = slot[i];
   wpos[slot[i]] = (int32_t)i;
   if (i % tile == 0) {
     const int64_t t = i / tile;
@@ -484,17 +484,18 @@ ONI_API int oni_chunk_layout(const int64_t* chunk_first, const int64_t* doc_tok_
 }
 
 // ------------------------------------------------------------------------------------------------
-// word_index: word-sorted view of the SELL tokens (stable by slot): wsorted[T], wslot[T],
-// wpos[slots] (-1 on padding), tile_wlo/tile_whi[ceil(T/tile)] (K11 recount tiles)
+// word_index: word-sorted view of the SELL tokens (stable by slot): wsorted, wslot (sized
+// ``slots``: the first T entries are the tokens, the sort writes them in place), wpos[slots] (-1 on
+// padding), tile_wlo/tile_whi[ceil(T/tile)] (K11 recount tiles)
 ONI_API int oni_word_index(const uint32_t* tok_word, int64_t slots, int64_t T, int64_t V, int tile,
                            int32_t* wsorted, int32_t* wslot, int32_t* wpos, int32_t* tile_wlo, int32_t* tile_whi,
                            void* tmp, size_t* tmp_bytes, hipStream_t s) {
   if (slots >= (int64_t)1 << 31) return (int)hipErrorInvalidValue;
   Arena ar{static_cast<char*>(tmp)};
   uint32_t* key = ar.take<uint32_t>(slots);
-  uint32_t* ks = ar.take<uint32_t>(slots);
+  uint32_t* ks = reinterpret_cast<uint32_t*>(wsorted);
   int32_t* iota = ar.take<int32_t>(slots);
-  int32_t* slot = ar.take<int32_t>(slots);
+  int32_t* slot = wslot;
   const int kbits = bits_for((uint64_t)V);
   size_t b1 = 0;
   ONI_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, b1, key, ks, iota, slot, (int)slots, 0, kbits, s));
@@ -508,6 +509,6 @@ ONI_API int oni_word_index(const uint32_t* tok_word, int64_t slots, int64_t T, i
   k_word_keys<<<nblk(slots), kB, 0, s>>>(tok_word, slots, (uint32_t)V, key);
   k_iota<<<nblk(slots), kB, 0, s>>>(iota, slots);
   ONI_TRY(hipcub::DeviceRadixSort::SortPairs(cub, b1, key, ks, iota, slot, (int)slots, 0, kbits, s));
-  if (T > 0) k_word_index<<<nblk(T), kB, 0, s>>>(ks, slot, T, tile, wsorted, wslot, wpos, tile_wlo, tile_whi);
+  if (T > 0) k_word_index<<<nblk(T), kB, 0, s>>>(ks, slot, T, tile, wpos, tile_wlo, tile_whi);
   return (int)hipGetLastError();
 }

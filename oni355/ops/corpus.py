@@ -322,7 +322,7 @@ def corpus_layout(ps: PairSet, doc_keys: torch.Tensor, G: int, L: int, recount_t
                       pair_tokoff[:nnz].contiguous(), ps.pair_word, ps.pair_cnt, tok_word)
     slots = tok_word.numel()
     n_tiles = (T + recount_tile - 1) // recount_tile
-    wsorted = torch.empty(max(T, 1), dtype=i32t, device=dev)
+    wsorted = torch.empty(max(slots, 1), dtype=i32t, device=dev)  # sorted in place; [:T] are the tokens
     wslot = torch.empty_like(wsorted)
     wpos = torch.empty(slots, dtype=i32t, device=dev)
     tile_wlo = torch.empty(max(n_tiles, 1), dtype=i32t, device=dev)
