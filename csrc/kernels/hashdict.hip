@@ -96,12 +96,23 @@ __global__ __launch_bounds__(kB) void k_hd_insert(const uint64_t* __restrict__ k
 }
 
 // occupied slots → unsorted unique keys
+// one counter atomic per wave (ballot + prefix popcount): a per-slot atomic on the one counter
+// serialised 170k times at a realistic vocabulary (0.69 ms); the order is irrelevant (sorted next)
 __global__ void k_hd_compact(const uint64_t* __restrict__ tab, int64_t m, uint64_t* __restrict__ uniq,
                              uint32_t* __restrict__ cnt, uint32_t cap) {
   const int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
-  if (i < m && tab[i] != kEmpty) {
-    const uint32_t at = atomicAdd(cnt, 1u);
-    if (at < cap) uniq[at] = tab[i];  // beyond cap the caller falls back to the sort path
+  const uint64_t k = i < m ? tab[i] : kEmpty;
+  const bool keep = k != kEmpty;
+  const uint64_t b = __ballot(keep);
+  if (b == 0ull) return;
+  const int lane = oni::lane_id();
+  const int leader = __ffsll((unsigned long long)b) - 1;
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(cnt, (uint32_t)__popcll(b));
+  base = (uint32_t)__shfl((int)base, leader);
+  if (keep) {
+    const uint32_t at = base + (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
+    if (at < cap) uniq[at] = k;  // beyond cap the caller falls back to the sort path
   }
 }
 
