@@ -50,6 +50,9 @@ def main(argv=None) -> int:
                     help="day mode: long-tail vocabularies on every source (flow V ~ 1.7e5 per 12.5M flows; dns / "
                          "proxy: half the rows from the long tail), as bench.py --realistic-vocab")
     a = ap.parse_args(argv)
+    # --recall-at "3000,15000" (or "+"-separated: tools/gpu.sh splits at commas); the day then
+    # selects max(N) result rows so the deeper recalls can be read off the same ranking
+    a.recall_ns = [int(x) for x in a.recall_at.replace("+", ",").split(",") if x] if a.recall_at else []
     if a.mode == "day" and a.steps == 20 and a.warmup == 10:
         a.steps, a.warmup = 2, 1
     # the contract is ONE JSON line on stdout: keep the real stdout for it and send everything else
@@ -197,7 +200,7 @@ def run_day_mode(a, comm, sync) -> dict:
     def one_day():
         times, stats = {}, {}
         for src, per, n_total, day in days:
-            kw = dict(K=a.topics, sweeps=a.sweeps, tol=1.0, maxresults=a.maxresults, device=dev, comm=comm,
+            kw = dict(K=a.topics, sweeps=a.sweeps, tol=1.0, maxresults=max([a.maxresults] + a.recall_ns), device=dev, comm=comm,
                       row_offset=rank * per)
             ts = time.perf_counter()
             if src == "flow":
@@ -229,8 +232,8 @@ def run_day_mode(a, comm, sync) -> dict:
                                                                res.rows[: a.maxresults]).mean())}
             if a.recall_at:
                 pl = day.anomaly_rows + rank * per
-                stats[src]["planted_recall_at"] = {n: round(float(np.isin(pl, res.rows[:int(n)]).mean()), 4)
-                                                   for n in a.recall_at.split(",")}
+                stats[src]["planted_recall_at"] = {str(n): round(float(np.isin(pl, res.rows[:n]).mean()), 4)
+                                                   for n in a.recall_ns}
                 stats[src]["planted"] = int(pl.size)
             del res
             print(f"[combined] {src} day {times[src]:.3f} s", file=sys.stderr, flush=True)
