@@ -410,6 +410,49 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 8))) 
   sweep_epilogue<G, KP>(a, red, doc, live, chunk, kbase, n, INIT);
 }
 
+// #{j : excl + P_j ≤ thr} over a lane's monotone prefix P (branch-free binary search; exact
+// because fl(excl + x) is monotone in x). Shared by k_gibbs_x1 (excl = 0) and k_gibbs_ldsg.
+template <int KP>
+__device__ __forceinline__ int count_le(const float (&P)[KP], float excl, float thr) {
+  if constexpr (KP == 16) {
+    if (excl + P[15] <= thr) return 16;
+    const bool b3 = excl + P[7] <= thr;
+    const bool b2 = excl + (b3 ? P[11] : P[3]) <= thr;
+    const float a1 = b2 ? P[5] : P[1], a2 = b2 ? P[13] : P[9];
+    const bool b1 = excl + (b3 ? a2 : a1) <= thr;
+    const float c0 = b1 ? P[2] : P[0], c1 = b1 ? P[6] : P[4], c2 = b1 ? P[10] : P[8], c3 = b1 ? P[14] : P[12];
+    const float d0 = b2 ? c1 : c0, d1 = b2 ? c3 : c2;
+    const bool b0 = excl + (b3 ? d1 : d0) <= thr;
+    return (b3 ? 8 : 0) + (b2 ? 4 : 0) + (b1 ? 2 : 0) + (b0 ? 1 : 0);
+  } else if constexpr (KP == 8) {
+    if (excl + P[7] <= thr) return 8;
+    const bool b2 = excl + P[3] <= thr;
+    const bool b1 = excl + (b2 ? P[5] : P[1]) <= thr;
+    const float c0 = b1 ? P[2] : P[0], c1 = b1 ? P[6] : P[4];
+    const bool b0 = excl + (b2 ? c1 : c0) <= thr;
+    return (b2 ? 4 : 0) + (b1 ? 2 : 0) + (b0 ? 1 : 0);
+  } else if constexpr (KP > 16 && KP <= 32) {
+    // upper or lower 16 by one compare, then the 16-wide search over the selected half (entries
+    // past KP read +inf: never counted, thr is finite)
+    const bool hi = excl + P[15] <= thr;
+    float Q[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) Q[j] = hi ? (16 + j < KP ? P[(16 + j) % KP] : __builtin_inff()) : P[j];
+    return (hi ? 16 : 0) + count_le<16>(Q, excl, thr);
+  } else if constexpr (KP > 8 && KP < 16) {
+    const bool hi = excl + P[7] <= thr;
+    float Q[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Q[j] = hi ? (8 + j < KP ? P[(8 + j) % KP] : __builtin_inff()) : P[j];
+    return (hi ? 8 : 0) + count_le<8>(Q, excl, thr);
+  } else {
+    int cnt = 0;
+#pragma unroll
+    for (int j = 0; j < KP; ++j) cnt += (excl + P[j] <= thr);
+    return cnt;
+  }
+}
+
 // ---- one-lane sweep kernel (K ≤ 32): k_gibbs_x1 ----------------------------------------------------
 // Per token and topic slot j the loop body is
 //   * 3 ops of count update: the row r_j = n_dj + α is f32 (exact: the host checks, `flags`
@@ -508,8 +551,19 @@ struct X1 {
     }
     const float thr = oni::u01(rr) * run;
     int cnt = 0;
+    if constexpr (KP > 16) {
+      // the first 16 slots by a binary search over the monotone prefix (~20 VALU instead of 32),
+      // the rest linearly: the same count
+      float P16[16];
 #pragma unroll
-    for (int j = 0; j < KP; ++j) cnt += (P[j] <= thr);
+      for (int j = 0; j < 16; ++j) P16[j] = P[j];
+      cnt = count_le<16>(P16, 0.f, thr);
+#pragma unroll
+      for (int j = 16; j < KP; ++j) cnt += (P[j] <= thr);
+    } else {
+#pragma unroll
+      for (int j = 0; j < KP; ++j) cnt += (P[j] <= thr);
+    }
     const int zn = cnt < a.K - 1 ? cnt : a.K - 1;
     {
       const uint32_t sh = 2u * (uint32_t)zn;
@@ -617,47 +671,6 @@ template <int KP>
 struct LdsRow {
   static constexpr int kSlots = ((KP / 4) % 2 == 0) ? KP / 4 + 1 : KP / 4;
 };
-
-template <int KP>
-__device__ __forceinline__ int count_le(const float (&P)[KP], float excl, float thr) {
-  if constexpr (KP == 16) {
-    if (excl + P[15] <= thr) return 16;
-    const bool b3 = excl + P[7] <= thr;
-    const bool b2 = excl + (b3 ? P[11] : P[3]) <= thr;
-    const float a1 = b2 ? P[5] : P[1], a2 = b2 ? P[13] : P[9];
-    const bool b1 = excl + (b3 ? a2 : a1) <= thr;
-    const float c0 = b1 ? P[2] : P[0], c1 = b1 ? P[6] : P[4], c2 = b1 ? P[10] : P[8], c3 = b1 ? P[14] : P[12];
-    const float d0 = b2 ? c1 : c0, d1 = b2 ? c3 : c2;
-    const bool b0 = excl + (b3 ? d1 : d0) <= thr;
-    return (b3 ? 8 : 0) + (b2 ? 4 : 0) + (b1 ? 2 : 0) + (b0 ? 1 : 0);
-  } else if constexpr (KP == 8) {
-    if (excl + P[7] <= thr) return 8;
-    const bool b2 = excl + P[3] <= thr;
-    const bool b1 = excl + (b2 ? P[5] : P[1]) <= thr;
-    const float c0 = b1 ? P[2] : P[0], c1 = b1 ? P[6] : P[4];
-    const bool b0 = excl + (b2 ? c1 : c0) <= thr;
-    return (b2 ? 4 : 0) + (b1 ? 2 : 0) + (b0 ? 1 : 0);
-  } else if constexpr (KP > 16 && KP <= 32) {
-    // upper or lower 16 by one compare, then the 16-wide search over the selected half (entries
-    // past KP read +inf: never counted, thr is finite)
-    const bool hi = excl + P[15] <= thr;
-    float Q[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) Q[j] = hi ? (16 + j < KP ? P[(16 + j) % KP] : __builtin_inff()) : P[j];
-    return (hi ? 16 : 0) + count_le<16>(Q, excl, thr);
-  } else if constexpr (KP > 8 && KP < 16) {
-    const bool hi = excl + P[7] <= thr;
-    float Q[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) Q[j] = hi ? (8 + j < KP ? P[(8 + j) % KP] : __builtin_inff()) : P[j];
-    return (hi ? 8 : 0) + count_le<8>(Q, excl, thr);
-  } else {
-    int cnt = 0;
-#pragma unroll
-    for (int j = 0; j < KP; ++j) cnt += (excl + P[j] <= thr);
-    return cnt;
-  }
-}
 
 // Sum of an int over each aligned group of G ∈ {2, 4, 8, 16} lanes with DPP butterflies.
 template <int G>
