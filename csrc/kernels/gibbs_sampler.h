@@ -220,6 +220,16 @@ struct PhiloxPair {
       nxt = oni::philox10(oni::U4{((pos0 + (uint32_t)s) >> 2) + 1u, key, sweep, stream}, a.seed0, a.seed1);
     }
   }
+  // chunk starts at multiples of 4 (flags bit 4: L % 4 == 0): a token's block is always `cur` and
+  // its word index is s & 3 -- wave-uniform, so the pick is a scalar choice, not four selects
+  __device__ __forceinline__ uint32_t pick_aligned(int s) const {
+    switch (s & 3) {
+      case 0: return cur.x;
+      case 1: return cur.y;
+      case 2: return cur.z;
+      default: return cur.w;
+    }
+  }
   __device__ __forceinline__ uint32_t pick(int s) const {
     const uint32_t pos = pos0 + (uint32_t)s;
     const bool second = (pos >> 2) != ((pos0 + (uint32_t)(s & ~3)) >> 2);
@@ -470,7 +480,7 @@ __device__ __forceinline__ int count_le(const float (&P)[KP], float excl, float 
 // 3-wave register budget (+0.011 ms) all lost.
 // WPD (off: measured 0.255 vs 0.248 ms/sweep): MODE 3/4 changed tokens load their word-sorted
 // slot when they change (exec-masked, ~10 % of lanes) instead of streaming it with every token.
-template <int KP, int MODE, bool AIR, bool WPD>
+template <int KP, int MODE, bool AIR, bool WPD, bool ALN = false>
 struct X1 {
   static constexpr int KS = KP;
   static constexpr bool WPF = (MODE == 3 || MODE == 4) && !WPD;
@@ -530,7 +540,7 @@ struct X1 {
     pend.flush(a, KS);
     rng.step(s, a);
     if (w == oni::kPadWord) return;
-    const uint32_t rr = rng.pick(s);
+    const uint32_t rr = ALN ? rng.pick_aligned(s) : rng.pick(s);
     // fused count update: +1 at the previous token's new topic, −1 at this token's old topic
     {
       const uint32_t sh = 2u * (uint32_t)zo;
@@ -590,7 +600,7 @@ struct X1 {
 
 // 4 waves per SIMD up to KP = 24 (≤ 128 VGPRs: 3 rows of KP plus the weights); wider rows take
 // what they need (a forced 4-wave budget spills at KP = 32)
-template <int KP, int MODE, bool AIR, bool WPD = false>
+template <int KP, int MODE, bool AIR, bool WPD = false, bool ALN = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KP <= 24 ? 4 : 1, 8))) void k_gibbs_x1(
     const OniGibbs a) {
   static_assert(KP <= 32 && KP % 4 == 0, "one-lane units hold at most 32 topics");
@@ -599,7 +609,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KP <= 24
   if (threadIdx.x < KP) qfx[threadIdx.x] = make_float2(a.qfix[threadIdx.x], a.qfix[KP + threadIdx.x]);
   __syncthreads();
 
-  using XT = X1<KP, MODE, AIR, WPD>;
+  using XT = X1<KP, MODE, AIR, WPD, ALN>;
   XT x(a, qfx);
   const int wave = threadIdx.x >> 6;
   x.lane = threadIdx.x & 63;
@@ -919,6 +929,12 @@ int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s)
   if (a.qfix == nullptr) return (int)hipErrorInvalidValue;
   const bool air = (a.flags & 1) != 0;
   if constexpr (G == 1) {
+    if (qpf == 3 && KP <= 32 && air && (a.flags & 16) && !(a.flags & 2) && (mode == 0 || mode == 4)) {
+      // every chunk starts at a multiple of 4 tokens (the default day's path: recount / wdelta)
+      if (mode == 0) k_gibbs_x1<KP, 0, true, false, true><<<grid, kBlock, 0, s>>>(a);
+      else k_gibbs_x1<KP, 4, true, false, true><<<grid, kBlock, 0, s>>>(a);
+      return (int)hipGetLastError();
+    }
     if (qpf == 3 && KP <= 32) {
       if ((a.flags & 2) && (mode == 3 || mode == 4)) {  // A/B: word-sorted slots loaded on change
         if (air && mode == 4) k_gibbs_x1<KP, 4, true, true><<<grid, kBlock, 0, s>>>(a);

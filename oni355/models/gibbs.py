@@ -274,6 +274,9 @@ class GibbsLDA:
         # over V·KS fewer); ONI_APPLY_INPLACE=0 keeps the Δ buffer
         self._inplace_ok = ((comm is None or not comm.dist or (comm.world == 1 and self._x01 is None))
                             and self._split is None and os.environ.get("ONI_APPLY_INPLACE", "1") != "0")
+        # chunk starts (doc-local token positions) are multiples of the chunk length L, pieces of
+        # split documents included: with L % 4 == 0 every chunk starts a Philox 4-token group
+        self._pos_aligned = int(self.c.L) % 4 == 0
         self._avg = None          # posterior-averaging accumulators (plan_average)
         self._acc = False         # sweeps add their counts to the accumulators (inside graphs too)
         self._avg_at: list = []   # sweep counts at which a sample is added
@@ -567,7 +570,7 @@ class GibbsLDA:
                        self.sweep_ctr, c.chunk_len, host_sweep=self.sweeps_done + 1, mode=mode, sampler=self.qpf,
                        chg_mask=self.wbits if mode == 4 else getattr(self, "chg_mask", None), wpos=c.wpos,
                        z_w=getattr(self, "z_w", None), zz_w=getattr(self, "zz_w", None), alpha_in_row=self._air,
-                       mh_doc_moves=getattr(self, "mh_doc_moves", 1))
+                       mh_doc_moves=getattr(self, "mh_doc_moves", 1), pos_aligned=self._pos_aligned)
         head = self.nwk if inplace else self.dn[self.b][: self.V * self.KS].view(self.V, self.KS)
         if mode == 4:
             # dn[b] head := Δn_wk of the tokens marked in the word-sorted change bitmap

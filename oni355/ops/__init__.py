@@ -363,7 +363,8 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
                chunk_len: torch.Tensor, host_sweep: int | None = None, mode: int = 1,
                sampler: int = 0, chg_mask: torch.Tensor | None = None, wpos: torch.Tensor | None = None,
                z_w: torch.Tensor | None = None, zz_w: torch.Tensor | None = None,
-               alpha_in_row: bool = False, mh_doc_moves: int = 1, word_init: bool = False) -> None:
+               alpha_in_row: bool = False, mh_doc_moves: int = 1, word_init: bool = False,
+               pos_aligned: bool = False) -> None:
     """Launch one init/sweep pass. ``st`` holds the OniGibbs tensors (csrc/kernels/gibbs_sampler.h);
     sweeps also need ``st["qfix"]`` ([2, KS] f32, from :func:`gibbs_apply`).
 
@@ -452,8 +453,10 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
     # the caller vouches that n + α is exact in f32 for every doc-topic count of this corpus
     # ONI_SAMPLER_AB (kernel A/B, bench/sampler_ab.py): bit 0 = word-sorted slots loaded on change
     # (k_gibbs_x1), bit 1 = 4-wave register budget (k_gibbs_ldsg)
+    # pos_aligned: every chunk starts at a multiple of 4 tokens (chunk length % 4 == 0), so the
+    # one-lane sampler picks its Philox word by the uniform step index (bit 4)
     a.flags = ((1 if alpha_in_row else 0) | (int(os.environ.get("ONI_SAMPLER_AB", "0")) & 3) << 1
-               | (8 if (init and word_init) else 0))
+               | (8 if (init and word_init) else 0) | (16 if pos_aligned else 0))
     if sampler == SAMPLER_MH:
         if G != 1:
             raise ValueError("the MH sampler runs one-lane units")
