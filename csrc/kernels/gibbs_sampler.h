@@ -724,7 +724,33 @@ __device__ __forceinline__ float group_scan_dpp(float x, int g) {
 // between two register sets with static roles (loop unrolled by two): the next token's row and its
 // own-topic value q_{w,zo} are issued a full step before they are used, so neither the word-change
 // row fetch nor the exclusion's gather is a dependent round trip inside the step.
-template <int G, int KP, int MODE>
+// The Philox word of token s for an aligned unit (every chunk starts at a multiple of 4 tokens):
+// its word index s & 3 and the lane of the unit holding its block, (s >> 2) − (s_ref >> 2), are
+// both wave-uniform, so the pick is a scalar choice and the exchange one DPP quad permute
+// instead of a ds_bpermute (G ∈ {2, 4}: a unit lies inside one quad).
+template <int G>
+__device__ __forceinline__ uint32_t unit_word(const oni::U4& r, int s, int off) {
+  int v;
+  switch (s & 3) {
+    case 0: v = (int)r.x; break;
+    case 1: v = (int)r.y; break;
+    case 2: v = (int)r.z; break;
+    default: v = (int)r.w; break;
+  }
+  if constexpr (G == 2) {
+    return (uint32_t)(off == 0 ? __builtin_amdgcn_update_dpp(0, v, 0xA0, 0xF, 0xF, false)    // [0,0,2,2]
+                               : __builtin_amdgcn_update_dpp(0, v, 0xF5, 0xF, 0xF, false));  // [1,1,3,3]
+  } else {
+    switch (off) {
+      case 0: return (uint32_t)__builtin_amdgcn_update_dpp(0, v, 0x00, 0xF, 0xF, false);
+      case 1: return (uint32_t)__builtin_amdgcn_update_dpp(0, v, 0x55, 0xF, 0xF, false);
+      case 2: return (uint32_t)__builtin_amdgcn_update_dpp(0, v, 0xAA, 0xF, 0xF, false);
+      default: return (uint32_t)__builtin_amdgcn_update_dpp(0, v, 0xFF, 0xF, 0xF, false);
+    }
+  }
+}
+
+template <int G, int KP, int MODE, bool ALN = false>
 struct LG {
   static constexpr int S = oni::kWave / G;
   static constexpr int KS = G * KP;
@@ -776,9 +802,14 @@ struct LG {
       r = oni::philox10(oni::U4{gbase + (uint32_t)g, key, sweep, 1u}, a.seed0, a.seed1);
     }
     if (w == oni::kPadWord) return;  // uniform across the G lanes of a unit
-    const uint32_t pos = pos0 + (uint32_t)s;
-    const uint32_t gi = pos >> 2;
-    const uint32_t rr = (uint32_t)__shfl((int)oni::pick4(r, pos & 3u), (int)(gi - gbase), G);
+    uint32_t rr;
+    if constexpr (ALN && (G == 2 || G == 4)) {
+      rr = unit_word<G>(r, s, (s >> 2) - ((next_refresh - kRefresh) >> 2));
+    } else {
+      const uint32_t pos = pos0 + (uint32_t)s;
+      const uint32_t gi = pos >> 2;
+      rr = (uint32_t)__shfl((int)oni::pick4(r, pos & 3u), (int)(gi - gbase), G);
+    }
     const unsigned zlo = (unsigned)(zo - kbase);
     const float2 ab = qfx[zo];
     const float qe = fmaf(qz, ab.x, -ab.y);
@@ -827,7 +858,7 @@ struct LG {
   }
 };
 
-template <int G, int KP, int MODE, int OCC = 1>
+template <int G, int KP, int MODE, int OCC = 1, bool ALN = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void k_gibbs_ldsg(const OniGibbs a) {
   static_assert(G > 1, "G = 1 uses k_gibbs_x1");
   constexpr int S = oni::kWave / G;
@@ -837,7 +868,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OCC, 8))
   __shared__ int32_t red[kWavesPerBlock][KS];
   __shared__ float2 qfx[KS];
   for (int k = threadIdx.x; k < KS; k += kBlock) qfx[k] = make_float2(a.qfix[k], a.qfix[KS + k]);
-  LG<G, KP, MODE> x(a, qfx);
+  LG<G, KP, MODE, ALN> x(a, qfx);
   const int wave = threadIdx.x >> 6;
   x.lane = threadIdx.x & 63;
   x.c = x.lane / G;
@@ -874,9 +905,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OCC, 8))
   // kRefresh = 4G - 3 steps each unit recomputes the G blocks that cover its next kRefresh tokens.
   x.gbase = x.pos0 >> 2;
   x.r = oni::philox10(oni::U4{x.gbase + (uint32_t)g, x.key, x.sweep, 1u}, a.seed0, a.seed1);
-  x.next_refresh = LG<G, KP, MODE>::kRefresh;
+  x.next_refresh = LG<G, KP, MODE, ALN>::kRefresh;
   x.nchg = 0;
-  constexpr bool WPF = LG<G, KP, MODE>::WPF;
+  constexpr bool WPF = LG<G, KP, MODE, ALN>::WPF;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     x.ws[t] = len > t ? a.tok_word[off + t * S + c] : oni::kPadWord;
@@ -966,6 +997,12 @@ int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s)
     if (qpf == 2 && air && (a.flags & 4) && (mode == 0 || mode == 4)) {  // A/B: 4-wave register budget
       if (mode == 0) k_gibbs_ldsg<G, KP, 0, 4><<<grid, kBlock, 0, s>>>(a);
       else k_gibbs_ldsg<G, KP, 4, 4><<<grid, kBlock, 0, s>>>(a);
+      return (int)hipGetLastError();
+    }
+    if (qpf == 2 && air && (a.flags & 16) && (G == 2 || G == 4) && (mode == 0 || mode == 4)) {
+      // every chunk starts at a multiple of 4 tokens: uniform Philox word, DPP exchange
+      if (mode == 0) k_gibbs_ldsg<G, KP, 0, 1, true><<<grid, kBlock, 0, s>>>(a);
+      else k_gibbs_ldsg<G, KP, 4, 1, true><<<grid, kBlock, 0, s>>>(a);
       return (int)hipGetLastError();
     }
     if (qpf == 2 && air) {

@@ -14,6 +14,7 @@ GPUs, any chunk packing, and across checkpoint/resume (tests/test_gibbs*.py).
 """
 from __future__ import annotations
 
+import gc
 import math
 import os
 from dataclasses import dataclass, field
@@ -686,6 +687,10 @@ class GibbsLDA:
         # capture does not execute: the host-side parities are rewound afterwards
         calls = self.timings["allreduce_calls"]
         self._capturing = True
+        # no garbage collection during the capture: a collected CUDAGraph (another model's) would
+        # be destroyed mid-capture, which HIP refuses (hipErrorStreamCaptureUnsupported)
+        gc_on = gc.isenabled()
+        gc.disable()
         try:
             with torch.cuda.stream(s):
                 # capture_begin/end directly: the torch.cuda.graph() context would synchronize the
@@ -700,6 +705,8 @@ class GibbsLDA:
         finally:
             self._capturing = False
             self.timings["allreduce_calls"] = calls
+            if gc_on:
+                gc.enable()
         torch.cuda.current_stream(self.device).wait_stream(s)
         self.a, self.b, self.cn, self.sweeps_done, self._aux_synced = saved
         self._force_mode = None
@@ -783,10 +790,14 @@ class GibbsLDA:
                                        f"negative counts={flags[1] or flags[2]}")
 
     def close(self) -> None:
-        """Stop the watchdog thread (training finished)."""
+        """Stop the watchdog thread and release the captured sweep graphs (training finished): a
+        graph destroyed later, by the cyclic garbage collector, could land inside the next model's
+        capture, where HIP refuses the destruction. A later sweep() recaptures."""
         if self._watchdog is not None:
             self._watchdog.close()
             self._watchdog = None
+        self._graph = None
+        self._graphs = {}
 
     def check_invariants(self) -> None:
         """Debug-mode count invariants: Σn_wk = Σn_k = global tokens, Σn_dk = local
@@ -837,6 +848,7 @@ class GibbsLDA:
                     self._capture(self.mode)  # capture the delta pair now: no capture stall at the switch
             self._graph = entry[0]
             entry[0].replay()
+            self.timings["graph_replays"] = self.timings.get("graph_replays", 0) + 1
             self.sweeps_done += 2
             self._aux_synced = self._keeps_aux(m1)
             self._zw_synced = m1 == 3

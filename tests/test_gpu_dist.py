@@ -115,7 +115,7 @@ def _forced_rccl_worker(port, n_total, sweeps, out_q, heavy=0.0):
     res = run_flow(_flow_cols(n_total, heavy), K=20, sweeps=sweeps, maxresults=200, device="cuda:0", comm=comm)
     m = res.lda.model
     c = res.lda.corpus
-    out_q.put((res.rows, res.scores, res.stats["loglik"], len(m._graphs), m.allreduce_ms_per_sweep(),
+    out_q.put((res.rows, res.scores, res.stats["loglik"], m.timings.get("graph_replays", 0), m.allreduce_ms_per_sweep(),
                m.allreduce_bytes_per_sweep(), int(c.split["n_split"]) if c.split is not None else 0))
     comm.barrier()
     pc.shutdown()
