@@ -53,7 +53,9 @@ struct OniGibbs {
   uint64_t* chg_mask;          // MODE 2: one u64 per SELL step, bit c*G set if slot c's topic changed
   const int32_t* wpos;         // MODE 3/4: word-sorted position of every SELL slot
   uint8_t* z_w;                // MODE 3: topic array in word-sorted order (kept in sync for changed tokens)
-  uint16_t* zz_w;              // MODE 4: (old | new << 8) topics of each changed token, word-sorted order
+  uint32_t* zz_w;              // MODE 4, word-sorted [T]: bits 0-15 (old | new << 8) topics of a changed
+                                //   token; bits 16-31 its word's row in its k_wdelta_recount block
+                                //   (written once with the corpus, 0xFFFF: read wsorted)
                                // (MODE 4 reuses chg_mask as a u32 bitmap over word-sorted positions)
   int32_t* chg_count;          // optional: += number of tokens whose topic changed (drives the auto mode)
   int64_t n_slices;
@@ -193,7 +195,8 @@ __device__ __forceinline__ void sweep_epilogue(const OniGibbs& a, int32_t (*red)
 // MODE 4: a changed token records (old, new) topic at its word-sorted position p and sets bit p
 // of a word-sorted bitmap; k_wdelta_recount then visits only set bits.
 __device__ __forceinline__ void mark_changed_w(const OniGibbs& a, int32_t p, int zo, int zn) {
-  a.zz_w[p] = (uint16_t)(zo | (zn << 8));  // one 2-B store: only read where the bit below is set
+  // one 2-B store into the low half (the row half stays): only read where the bit below is set
+  reinterpret_cast<uint16_t*>(a.zz_w + p)[0] = (uint16_t)(zo | (zn << 8));
   atomicOr(reinterpret_cast<uint32_t*>(a.chg_mask) + (p >> 5), 1u << (p & 31));
 }
 

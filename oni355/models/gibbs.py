@@ -222,10 +222,11 @@ class GibbsLDA:
         if self.mode == 3 or self.early == 3:
             self.z_w = torch.empty(max(corpus.T, 1), dtype=torch.uint8, device=dev)  # synced before use
         if self.mode == 4:
-            # word-sorted change bitmap (+ slack word) and (old | new << 8) of each changed token;
-            # zz_w is only read where a bit is set, so it never needs a sync with tok_z
+            # word-sorted change bitmap (+ slack word) and per-position records: (old | new << 8) of
+            # each changed token (only read where a bit is set, so never synced with tok_z) next to
+            # the position's word row in its recount block (written once here)
             self.wbits = torch.empty((corpus.T + 31) // 32 + 1, dtype=torch.int32, device=dev)  # _sync_aux_z zeroes
-            self.zz_w = torch.empty(max(corpus.T, 1), dtype=torch.int16, device=dev)
+            self.zz_w = ops.wdelta_records(corpus.wsorted)
         if self.mode == 2:
             self.tok_zprev = torch.zeros_like(self.tok_z)
             self.chg_mask = torch.zeros(max(corpus.sell_slots // corpus.S, 1), dtype=torch.int64, device=dev)

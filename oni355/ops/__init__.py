@@ -372,7 +372,8 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
     :func:`recount`; 2: record changed slots in ``chg_mask`` for :func:`delta_recount`; 3: also
     write changed topics into the word-sorted copy ``z_w`` (via ``wpos``) for a streaming recount;
     4: changed tokens set their word-sorted bit in ``chg_mask`` (int32 bitmap) and record
-    old | new << 8 in ``zz_w`` (int16, word-sorted) for :func:`wdelta_recount`.
+    old | new << 8 in the low half of ``zz_w`` (int32 [T], word-sorted, from :func:`wdelta_records`)
+    for :func:`wdelta_recount`.
     ``sampler`` (kernel variant; every variant draws the same topics bit for bit): 0 = generic
     k_gibbs, 2 = k_gibbs_ldsg (G > 1), 3 = k_gibbs_x1 (G = 1); the specialised kernels need
     ``alpha_in_row`` (n + α exact in f32 for every count of the corpus), else the generic one runs.
@@ -392,8 +393,8 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
     if mode == 4:
         T = int(zz_w.numel()) if zz_w is not None else 0
         if (wpos is None or zz_w is None or chg_mask is None or wpos.numel() != st["tok_word"].numel()
-                or zz_w.dtype != torch.int16 or chg_mask.dtype != torch.int32 or chg_mask.numel() * 32 < T):
-            raise ValueError("wdelta mode needs wpos [SELL slots], int16 zz_w [T] and an int32 bitmap of T bits")
+                or zz_w.dtype != torch.int32 or chg_mask.dtype != torch.int32 or chg_mask.numel() * 32 < T):
+            raise ValueError("wdelta mode needs wpos [SELL slots], int32 zz_w [T] and an int32 bitmap of T bits")
     if not _is_dev(st["tok_word"]):
         chg = st.get("chg_count")
         z_before = st["tok_z"].clone() if (chg is not None or mode == 4) else None
@@ -417,7 +418,8 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
         if mode == 4:
             ch = st["tok_z"] != z_before
             p = wpos[ch].long()
-            zz_w[p] = (z_before[ch].to(torch.int32) | (st["tok_z"][ch].to(torch.int32) << 8)).to(torch.int16)
+            zz16 = (z_before[ch].to(torch.int32) | (st["tok_z"][ch].to(torch.int32) << 8))
+            zz_w.view(torch.int16).view(-1, 2)[p, 0] = torch.where(zz16 >= 0x8000, zz16 - 0x10000, zz16).to(torch.int16)
             upd = np.zeros(chg_mask.numel(), dtype=np.uint32)
             np.bitwise_or.at(upd, (p >> 5).numpy(), (np.uint32(1) << (p & 31).numpy().astype(np.uint32)))
             chg_mask |= torch.from_numpy(upd.view(np.int32))
@@ -539,9 +541,27 @@ def delta_recount(wslot, tile_wlo, tile_whi, chg_mask, tok_word, tok_z, tok_zpre
                "oni_delta_recount")
 
 
+WBITS_BLOCK = 8192  # word-sorted positions per k_wdelta_recount block (matches kWBitsPerBlock)
+
+
+def wdelta_records(wsorted: torch.Tensor) -> torch.Tensor:
+    """The int32 [T] record array of MODE 4: high half = each position's word minus the first word
+    of its k_wdelta_recount block (0xFFFF when that does not fit), low half = the (old | new << 8)
+    topics the sampler writes for a changed token (zero here)."""
+    T = wsorted.numel()
+    out = torch.zeros((max(T, 1), 2), dtype=torch.int16, device=wsorted.device)
+    if T:
+        nb = -(-T // WBITS_BLOCK)
+        w = torch.nn.functional.pad(wsorted.to(torch.int32), (0, nb * WBITS_BLOCK - T)).view(nb, WBITS_BLOCK)
+        rel = (w - w[:, :1]).view(-1)[:T].clamp_(max=0xFFFF)  # word-sorted: ≥ 0
+        out[:T, 1] = torch.where(rel >= 0x8000, rel - 0x10000, rel).to(torch.int16)
+    return out.view(torch.int32).view(-1)
+
+
 def wdelta_recount(wbits, wsorted, zz_w, dnwk_out, KS: int) -> None:
     """Δn_wk of the tokens marked in the word-sorted bitmap ``wbits`` (+1 at (w, new), -1 at
-    (w, old) with zz_w = old | new << 8); clears the bitmap (k_wdelta_recount)."""
+    (w, old) with zz_w's low half = old | new << 8, its high half the row in the block: see
+    :func:`wdelta_records`); clears the bitmap (k_wdelta_recount)."""
     T = wsorted.numel()
     if T == 0:
         return
@@ -556,6 +576,8 @@ def wdelta_recount(wbits, wsorted, zz_w, dnwk_out, KS: int) -> None:
         dnwk_out.view(-1).index_add_(0, w * KS + (zz & 0xFF), -one)
         wbits.zero_()
         return
+    if zz_w.dtype != torch.int32 or zz_w.numel() < T:
+        raise ValueError("zz_w must be the int32 [T] record array of wdelta_records")
     wmax = max(1, RECOUNT_CELLS // KS)
     _lib.check(_lib.lib().oni_wdelta_recount(*map(_lib.ptr, (wbits, wsorted, zz_w)), T, _lib.ptr(dnwk_out), KS,
                                              wmax, _lib.stream()), "oni_wdelta_recount")

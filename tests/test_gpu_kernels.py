@@ -278,3 +278,31 @@ def test_widen_pair_matches_torch_glue(gpu):
     out = ops.widen_pair(a.to(gpu), b.to(gpu))
     assert out.dtype == torch.int64 and torch.equal(out.cpu(), ref)
     assert torch.equal(ops.widen_pair(a, b), ref)
+
+
+def test_wdelta_recount_far_words_matches_cpu(gpu):
+    """k_wdelta_recount on packed records: rows in the LDS table, rows past its cap and words too far
+    from their block's first word for 16 bits (read back from wsorted) all give the CPU deltas."""
+    r = np.random.default_rng(3)
+    KS = 8
+    words = np.sort(r.choice(3_000_000, 900, replace=False)).astype(np.int32)
+    ws = torch.from_numpy(np.repeat(words, r.integers(1, 60, words.size)).astype(np.int32))
+    T = ws.numel()
+    rec = ops.wdelta_records(ws)
+    zz = torch.from_numpy(r.integers(0, KS, (T, 2)).astype(np.int32))
+    chg = torch.from_numpy(r.random(T) < 0.3)
+    low = (zz[:, 0] | zz[:, 1] << 8).to(torch.int16)
+    rec.view(torch.int16).view(-1, 2)[:, 0] = torch.where(chg, low, torch.zeros_like(low))
+    bits = np.zeros((T + 31) // 32 + 1, dtype=np.uint32)
+    pos = np.nonzero(chg.numpy())[0]
+    np.bitwise_or.at(bits, pos >> 5, (np.uint32(1) << (pos & 31).astype(np.uint32)))
+    V = int(words[-1]) + 1
+    out = {}
+    for dev in ("cpu", gpu):
+        wb = torch.from_numpy(bits.view(np.int32).copy()).to(dev)
+        d = torch.zeros(V, KS, dtype=torch.int32, device=dev)
+        ops.wdelta_recount(wb, ws.to(dev), rec.to(dev), d, KS)
+        assert not bool(wb.any())
+        out[dev] = d.cpu()
+    assert torch.equal(out["cpu"], out[gpu])
+    assert int(out["cpu"].abs().sum()) > 0

@@ -245,6 +245,25 @@ def test_wdelta_count_mode_matches_recount():
         m.sweep(5)
     assert torch.equal(a.tok_z, b.tok_z) and torch.equal(a.nwk, b.nwk) and torch.equal(a.nk_cur, b.nk_cur)
     assert not bool(a.wbits.any())  # the recount clears every bit it consumed
+    rec = a.zz_w.view(torch.int16).view(-1, 2)[:, 1].to(torch.int32) & 0xFFFF
+    ws = c.wsorted.to(torch.int32)
+    assert torch.equal(rec[:c.T], ws - ws[0])  # one 8192-position block: rows below its first word
+
+
+def test_wdelta_records_rows_and_far_words():
+    """The MODE-4 record array holds each position's word row in its 8192-position recount block,
+    0xFFFF when the gap does not fit 16 bits, and zero topic halves."""
+    import torch
+
+    from oni355 import ops
+    ws = torch.tensor([3] * 5000 + [70000] * 3192 + [70001] * 10 + [200000] * 5, dtype=torch.int32)
+    rec = ops.wdelta_records(ws)
+    assert rec.dtype == torch.int32 and rec.numel() == ws.numel()
+    halves = rec.view(torch.int16).view(-1, 2).to(torch.int32) & 0xFFFF
+    assert int(halves[:, 0].abs().sum()) == 0
+    hi = halves[:, 1]
+    assert hi[:5000].eq(0).all() and hi[5000:8192].eq(0xFFFF).all()  # 69997 > 0xFFFF: read wsorted
+    assert hi[8192:8202].eq(0).all() and hi[8202:].eq(0xFFFF).all()  # next block starts at 70001
 
 
 def test_auto_with_dual_early_sweeps_matches_recount(monkeypatch):
