@@ -93,9 +93,10 @@ class GibbsConfig:
     # topic in a sweep falls below auto_threshold (measured on device, read two sweeps late so the
     # host never stalls the stream); auto_switch > 0 instead fixes the first delta sweep (tests)
     auto_switch: int = 0
-    # 0.12: the wdelta sweep beats the full recount below ~12-15 % changed tokens (bench A/B on the
-    # 12.5M-flow day: 0.08 → 0.309, 0.12 → 0.304, 0.16 → 0.307 ms/sweep over sweeps 11-60)
-    auto_threshold: float = field(default_factory=lambda: float(os.environ.get("ONI_AUTO_THRESHOLD", "0.12")))
+    # 0.19: the wdelta sweep beats the full recount below ~15-25 % changed tokens since its records
+    # carry the word row (default flow day 58.6 ms at 0.12, 58.0-58.2 at 0.16 / 0.19 / 0.22 / 0.30;
+    # DNS 26.1 ms at 0.30, 25.2-25.3 below; profiles/r5/auto_threshold/)
+    auto_threshold: float = field(default_factory=lambda: float(os.environ.get("ONI_AUTO_THRESHOLD", "0.19")))
     # the delta bookkeeping auto mode switches to: "wdelta" (word-sorted change bitmap) | "delta"
     auto_delta: str = field(default_factory=lambda: os.environ.get("ONI_AUTO_DELTA", "wdelta"))
     # debug: verify count invariants after every sweep() call (ONI_CHECK_INVARIANTS=1)
