@@ -29,7 +29,7 @@ def _tokens(n, D, V, seed, zipf=True):
 
 @pytest.mark.parametrize("n,D,V,G,L,weighted", [(1, 1, 1, 1, 32, False), (65, 63, 64, 1, 32, False),
                                                 (5000, 300, 200, 1, 64, True), (20000, 700, 900, 4, 128, False),
-                                                (200_003, 4000, 3000, 8, 128, True), (2_000_000, 60_000, 6000, 1, 128, False)])
+                                                (200_003, 4000, 3000, 8, 128, True), (2_500_000, 60_000, 6000, 1, 128, False)])
 def test_native_corpus_equals_torch_build(gpu, n, D, V, G, L, weighted):
     tdoc, tword = _tokens(n, D, V, seed=n)
     keys = (torch.arange(D, dtype=torch.int64) * 2654435761 & 0xFFFFFFFF).to(torch.int64)
@@ -49,7 +49,7 @@ def test_native_corpus_equals_torch_build(gpu, n, D, V, G, L, weighted):
         assert torch.equal(a.cpu(), b.cpu()), f
 
 
-@pytest.mark.parametrize("n,bits", [(1, 32), (1000, 32), (3_000_001, 32), (100_000, 40), (77, 64)])
+@pytest.mark.parametrize("n,bits", [(1, 32), (1000, 32), (3_000_001, 32), (100_000, 40), (2_200_000, 40), (77, 64)])
 def test_dict_encode_equals_unique(gpu, n, bits):
     r = np.random.default_rng(n)
     table = r.integers(0, 2 ** min(bits, 62), max(n // 3, 1), dtype=np.int64)
@@ -96,7 +96,7 @@ def test_flow_pipeline_native_equals_torch_corpus(gpu, monkeypatch):
     assert a.stats["loglik"] == b.stats["loglik"]
 
 
-@pytest.mark.parametrize("n,weighted", [(1, False), (5000, True), (2_000_000, False), (1_000_003, True)])
+@pytest.mark.parametrize("n,weighted", [(1, False), (5000, True), (2_200_000, False), (1_000_003, True)])
 def test_dict_encode_counts_equal_weighted_unique(gpu, n, weighted):
     """Per-key token counts (the DP placement's document loads) == torch.unique counts / index_add."""
     r = np.random.default_rng(n + 7)
