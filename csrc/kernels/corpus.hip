@@ -58,14 +58,22 @@ __global__ void k_narrow(const uint64_t* __restrict__ k, int64_t n, uint32_t* __
   if (i < n) out[i] = (uint32_t)k[i];
 }
 
-template <class K>
+// The id of every key in input order is the inverse permutation applied to the sorted ranks. As
+// one scatter (ids[perm[i]] = r) every 4-B store lands on its own line: 25M of them cost ~0.55 ms.
+// Above kSortBackMin keys the ranks are written in sorted order (SEQ), ONE radix pass over perm's
+// top 8 bits groups them into 256 destination windows (~0.4 MB each at 25M), and the scatter then
+// writes inside a window at a time, where the L2 merges the stores into whole lines.
+constexpr int64_t kSortBackMin = int64_t(1) << 21;
+
+template <class K, bool SEQ>
 __global__ void k_dict_scatter(const K* __restrict__ ks, const int32_t* __restrict__ perm,
                                const int32_t* __restrict__ rank, int64_t n, uint64_t* __restrict__ uniq,
                                int32_t* __restrict__ ids, int64_t* __restrict__ n_uniq, int64_t* __restrict__ head) {
   const int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
   if (i >= n) return;
   const int32_t r = rank[i] - 1;
-  ids[perm[i]] = r;
+  if constexpr (SEQ) ids[i] = r;
+  else ids[perm[i]] = r;
   if (i == 0 || ks[i] != ks[i - 1]) {
     uniq[r] = (uint64_t)ks[i];
     if (head) head[r] = i;
@@ -83,7 +91,7 @@ __global__ void k_pair_keys(const int32_t* __restrict__ doc, const int32_t* __re
   if (i < n) key[i] = (K)((uint64_t)doc[i] * (uint64_t)V + (uint64_t)word[i]);
 }
 
-template <class K>
+template <class K, bool SEQ>
 __global__ void k_pair_scatter(const K* __restrict__ ks, const int32_t* __restrict__ perm,
                                const int32_t* __restrict__ run, int64_t n, int64_t V, int32_t* __restrict__ pair_doc,
                                int32_t* __restrict__ pair_word, int64_t* __restrict__ head_pos,
@@ -91,7 +99,8 @@ __global__ void k_pair_scatter(const K* __restrict__ ks, const int32_t* __restri
   const int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
   if (i >= n) return;
   const int32_t r = run[i] - 1;
-  tok_pair[perm[i]] = r;
+  if constexpr (SEQ) tok_pair[i] = r;  // sorted order: scatter_back restores the token order
+  else tok_pair[perm[i]] = r;
   if (i == 0 || ks[i] != ks[i - 1]) {
     pair_doc[r] = (int32_t)((uint64_t)ks[i] / (uint64_t)V);
     pair_word[r] = (int32_t)((uint64_t)ks[i] % (uint64_t)V);
@@ -281,6 +290,29 @@ int bits_for(uint64_t maxv) {  // number of bits needed to represent values in [
   return b;
 }
 
+// one radix pass of (perm, val) over perm's top 8 bits: destination windows of 2^(bits-8) slots
+hipError_t window_pass(void* tmp, size_t& bytes, const int32_t* perm, int32_t* keys_out, const int32_t* val,
+                       int32_t* val_out, int64_t n, hipStream_t s) {
+  const int pbits = bits_for(n > 1 ? (uint64_t)(n - 1) : 1);
+  const int lo = pbits > 8 ? pbits - 8 : 0;
+  return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, reinterpret_cast<const uint32_t*>(perm),
+                                            reinterpret_cast<uint32_t*>(keys_out), val, val_out, (int)n, lo, pbits,
+                                            s);
+}
+
+// XCD-aware: workgroups are dispatched round-robin over the 8 XCDs, so workgroup b takes tile
+// (b % 8) * (grid / 8) + b / 8 -- each XCD walks one contiguous eighth of the window-grouped
+// input, and a destination window's lines fill in ONE L2 instead of eight partial copies.
+__global__ void k_scatter(const int32_t* __restrict__ dst, const int32_t* __restrict__ val, int64_t n,
+                          int32_t* __restrict__ out) {
+  const unsigned per = gridDim.x / 8u;  // grid is a multiple of 8
+  const unsigned t = (blockIdx.x % 8u) * per + blockIdx.x / 8u;
+  const int64_t i = (int64_t)t * kB + threadIdx.x;
+  if (i < n) out[dst[i]] = val[i];
+}
+
+inline unsigned nblk8(int64_t n) { return (nblk(n) + 7u) & ~7u; }
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------------
@@ -304,12 +336,17 @@ static int dict_encode_impl(const uint64_t* keys, int64_t n, int key_bits, uint6
   int64_t* ws = counts ? ar.take<int64_t>(n) : nullptr;
   int64_t* psum = counts ? ar.take<int64_t>(n) : nullptr;
   const K* src = kNarrow ? kin : reinterpret_cast<const K*>(keys);
-  size_t sb = 0, cb = 0, wb = 0;
+  size_t sb = 0, cb = 0, wb = 0, bb = 0;
+  const bool back = n >= kSortBackMin;
+  // window pass scratch: keys into iota (free after the sort), values into a slice of its own
+  int32_t* wval = back ? ar.take<int32_t>(n) : nullptr;
   ONI_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, sb, src, ks, iota, perm, (int)n, 0, key_bits, s));
   ONI_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, cb, flag, rank, (int)n, s));
   if (counts) ONI_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, wb, ws, psum, (int)n, s));
+  if (back) ONI_TRY(window_pass(nullptr, bb, perm, iota, flag, wval, n, s));
   size_t cbytes = sb > cb ? sb : cb;
   if (wb > cbytes) cbytes = wb;
+  if (bb > cbytes) cbytes = bb;
   void* cub = ar.take<char>(cbytes);
   if (!tmp) {
     *tmp_bytes = ar.used + 256;
@@ -324,7 +361,14 @@ static int dict_encode_impl(const uint64_t* keys, int64_t n, int key_bits, uint6
   ONI_TRY(hipcub::DeviceRadixSort::SortPairs(cub, cbytes, src, ks, iota, perm, (int)n, 0, key_bits, s));
   k_heads<K><<<nblk(n), kB, 0, s>>>(ks, n, flag);
   ONI_TRY(hipcub::DeviceScan::InclusiveSum(cub, cbytes, flag, rank, (int)n, s));
-  k_dict_scatter<K><<<nblk(n), kB, 0, s>>>(ks, perm, rank, n, uniq, ids, n_uniq, head);
+  if (back) {
+    // ranks in sorted order into flag (free after the scan), grouped by destination window, placed
+    k_dict_scatter<K, true><<<nblk(n), kB, 0, s>>>(ks, perm, rank, n, uniq, flag, n_uniq, head);
+    ONI_TRY(window_pass(cub, cbytes, perm, iota, flag, wval, n, s));
+    k_scatter<<<nblk8(n), kB, 0, s>>>(iota, wval, n, ids);
+  } else {
+    k_dict_scatter<K, false><<<nblk(n), kB, 0, s>>>(ks, perm, rank, n, uniq, ids, n_uniq, head);
+  }
   if (counts) {
     k_weights_sorted<<<nblk(n), kB, 0, s>>>(weight, perm, n, ws);
     ONI_TRY(hipcub::DeviceScan::InclusiveSum(cub, cbytes, ws, psum, (int)n, s));
@@ -361,7 +405,10 @@ static int pair_build_impl(const int32_t* doc, const int32_t* word, const int32_
   int64_t* ws = ar.take<int64_t>(n);
   int64_t* psum = ar.take<int64_t>(n);
   int64_t* nsel = ar.take<int64_t>(1);
-  size_t b1 = 0, b2 = 0, b3 = 0, b4 = 0;
+  size_t b1 = 0, b2 = 0, b3 = 0, b4 = 0, b5 = 0;
+  const bool back = n >= kSortBackMin;
+  int32_t* wval = back ? ar.take<int32_t>(n) : nullptr;
+  if (back) ONI_TRY(window_pass(nullptr, b5, perm, iota, flag, wval, n, s));
   ONI_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, b1, key, ks, iota, perm, (int)n, 0, bits, s));
   ONI_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b2, flag, run, (int)n, s));
   ONI_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b3, ws, psum, (int)n, s));
@@ -370,6 +417,7 @@ static int pair_build_impl(const int32_t* doc, const int32_t* word, const int32_
   if (b2 > cbytes) cbytes = b2;
   if (b3 > cbytes) cbytes = b3;
   if (b4 > cbytes) cbytes = b4;
+  if (b5 > cbytes) cbytes = b5;
   void* cub = ar.take<char>(cbytes);
   if (!tmp) {
     *tmp_bytes = ar.used + 256;
@@ -384,7 +432,13 @@ static int pair_build_impl(const int32_t* doc, const int32_t* word, const int32_
   ONI_TRY(hipcub::DeviceRadixSort::SortPairs(cub, cbytes, key, ks, iota, perm, (int)n, 0, bits, s));
   k_heads<K><<<nblk(n), kB, 0, s>>>(ks, n, flag);
   ONI_TRY(hipcub::DeviceScan::InclusiveSum(cub, cbytes, flag, run, (int)n, s));
-  k_pair_scatter<K><<<nblk(n), kB, 0, s>>>(ks, perm, run, n, V, pair_doc, pair_word, head, tok_pair, nnz);
+  if (back) {
+    k_pair_scatter<K, true><<<nblk(n), kB, 0, s>>>(ks, perm, run, n, V, pair_doc, pair_word, head, flag, nnz);
+    ONI_TRY(window_pass(cub, cbytes, perm, iota, flag, wval, n, s));
+    k_scatter<<<nblk8(n), kB, 0, s>>>(iota, wval, n, tok_pair);
+  } else {
+    k_pair_scatter<K, false><<<nblk(n), kB, 0, s>>>(ks, perm, run, n, V, pair_doc, pair_word, head, tok_pair, nnz);
+  }
   k_weights_sorted<<<nblk(n), kB, 0, s>>>(weight, perm, n, ws);
   ONI_TRY(hipcub::DeviceScan::InclusiveSum(cub, cbytes, ws, psum, (int)n, s));
   k_pair_counts<<<nblk(n), kB, 0, s>>>(head, psum, nnz, n, pair_cnt);
