@@ -36,10 +36,18 @@ __global__ void k_sell_fill(const int32_t* __restrict__ chunk_doc, const int32_t
   const int64_t pos0 = chunk_pos0[i];
   const int len = chunk_len[i];
   int64_t j = find_pair(pair_tokoff, doc_pair_ptr[d], doc_pair_ptr[d + 1], pos0);
+  // the current pair's end and word stay in registers: a token of the same pair (most of them) is
+  // a store, not two dependent reloads
+  int64_t end = pair_tokoff[j] + pair_cnt[j];
+  uint32_t w = (uint32_t)pair_word[j];
   for (int s = 0; s < len; ++s) {
     const int64_t pos = pos0 + s;
-    while (pair_tokoff[j] + pair_cnt[j] <= pos) ++j;
-    tok_word[off + (int64_t)s * S] = (uint32_t)pair_word[j];
+    while (end <= pos) {
+      ++j;
+      end = pair_tokoff[j] + pair_cnt[j];
+      w = (uint32_t)pair_word[j];
+    }
+    tok_word[off + (int64_t)s * S] = w;
   }
 }
 
