@@ -25,16 +25,46 @@ __global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__
 #pragma unroll
   for (int p = 0; p < kMaxPrefixes; ++p) pre[p] = p < P ? prefixes[p] : 0xFFFFFFFFu;
   __syncthreads();
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const uint32_t k = keys[i];
+  // Skewed columns (most flows of 1 packet, ...) put most lanes of a wave on ONE bin, and
+  // same-address LDS atomics serialise: for the key's first matching prefix, the lanes sharing the
+  // first active lane's bin add their count with one atomic. (The device-only pipeline's prefixes
+  // are not de-duplicated: a key adds to every prefix it matches, the later ones one by one.)
+  auto count = [&](uint32_t k) {
     const uint32_t hi = k & mask;
-    const uint32_t digit = (k >> shift) & (B - 1);
+    const int digit = (int)((k >> shift) & (B - 1));
+    int bin = -1;
 #pragma unroll
     for (int p = 0; p < kMaxPrefixes; ++p) {
-      if (p < P && hi == pre[p]) atomicAdd(&lh[p * B + digit], 1u);
+      if (p < P && hi == pre[p]) {
+        if (bin < 0) bin = p * B + digit;
+        else atomicAdd(&lh[p * B + digit], 1u);
+      }
     }
+    const int b0 = __builtin_amdgcn_readfirstlane(bin);
+    const uint64_t same = __ballot(bin == b0);
+    if (bin == b0) {
+      if (b0 >= 0 && __lane_id() == __ffsll((unsigned long long)same) - 1)
+        atomicAdd(&lh[b0], (uint32_t)__popcll(same));
+    } else if (bin >= 0) {
+      atomicAdd(&lh[bin], 1u);
+    }
+  };
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i0 = 0;
+  if ((reinterpret_cast<uintptr_t>(keys) & 15u) == 0) {
+    // four keys per 16-B load: four independent loads in flight per lane, not one
+    const int64_t n4 = n / 4;
+    const uint4* k4 = reinterpret_cast<const uint4*>(keys);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+      const uint4 v = k4[i];
+      count(v.x);
+      count(v.y);
+      count(v.z);
+      count(v.w);
+    }
+    i0 = n4 * 4;
   }
+  for (int64_t i = i0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) count(keys[i]);
   __syncthreads();
   for (int i = threadIdx.x; i < nb; i += blockDim.x) {
     const uint32_t v = lh[i];
@@ -133,7 +163,8 @@ ONI_API int oni_radix_hist(const uint32_t* keys, int64_t n, int shift, int nbits
   if (P < 1 || P > kMaxPrefixes) return (int)hipErrorInvalidValue;
   const size_t lds = (size_t)P << nbits << 2;
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
-  const unsigned grid = oni::grid_for(n, 256, 512);
+  // 2048 workgroups (8 per CU): the loop is latency-bound, 512 left 8 waves per CU
+  const unsigned grid = oni::grid_for((n + 3) / 4, 256, 2048);
   if (nbits == 11)
     k_radix_hist<11><<<grid, 256, lds, s>>>(keys, n, shift, prefixes, P, mask, hist);
   else if (nbits == 10)
