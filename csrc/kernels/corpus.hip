@@ -124,7 +124,7 @@ __global__ void k_pair_counts(const int64_t* __restrict__ head_pos, const int64_
   const int64_t r = (int64_t)blockIdx.x * kB + threadIdx.x;
   if (r >= *nnz_p) return;
   const int64_t a = head_pos[r], b = head_pos[r + 1];
-  const int64_t s = psum[b - 1] - (a > 0 ? psum[a - 1] : 0);
+  const int64_t s = psum ? psum[b - 1] - (a > 0 ? psum[a - 1] : 0) : b - a;  // no weights: run length
   cnt[r] = (int32_t)(s < 0x7FFFFFFF ? s : 0x7FFFFFFF);
 }
 
@@ -134,7 +134,7 @@ __global__ void k_run_sums(const int64_t* __restrict__ head_pos, const int64_t* 
   const int64_t r = (int64_t)blockIdx.x * kB + threadIdx.x;
   if (r >= *nr_p) return;
   const int64_t a = head_pos[r], b = head_pos[r + 1];
-  sums[r] = psum[b - 1] - (a > 0 ? psum[a - 1] : 0);
+  sums[r] = psum ? psum[b - 1] - (a > 0 ? psum[a - 1] : 0) : b - a;  // no weights: run length
 }
 
 struct BelowN {
@@ -370,9 +370,12 @@ static int dict_encode_impl(const uint64_t* keys, int64_t n, int key_bits, uint6
     k_dict_scatter<K, false><<<nblk(n), kB, 0, s>>>(ks, perm, rank, n, uniq, ids, n_uniq, head);
   }
   if (counts) {
-    k_weights_sorted<<<nblk(n), kB, 0, s>>>(weight, perm, n, ws);
-    ONI_TRY(hipcub::DeviceScan::InclusiveSum(cub, cbytes, ws, psum, (int)n, s));
-    k_run_sums<<<nblk(n), kB, 0, s>>>(head, psum, n_uniq, counts);
+    // unweighted keys count their run lengths: no 8-B-per-key weight stream and scan
+    if (weight) {
+      k_weights_sorted<<<nblk(n), kB, 0, s>>>(weight, perm, n, ws);
+      ONI_TRY(hipcub::DeviceScan::InclusiveSum(cub, cbytes, ws, psum, (int)n, s));
+    }
+    k_run_sums<<<nblk(n), kB, 0, s>>>(head, weight ? psum : nullptr, n_uniq, counts);
   }
   return (int)hipGetLastError();
 }
@@ -439,9 +442,11 @@ static int pair_build_impl(const int32_t* doc, const int32_t* word, const int32_
   } else {
     k_pair_scatter<K, false><<<nblk(n), kB, 0, s>>>(ks, perm, run, n, V, pair_doc, pair_word, head, tok_pair, nnz);
   }
-  k_weights_sorted<<<nblk(n), kB, 0, s>>>(weight, perm, n, ws);
-  ONI_TRY(hipcub::DeviceScan::InclusiveSum(cub, cbytes, ws, psum, (int)n, s));
-  k_pair_counts<<<nblk(n), kB, 0, s>>>(head, psum, nnz, n, pair_cnt);
+  if (weight) {
+    k_weights_sorted<<<nblk(n), kB, 0, s>>>(weight, perm, n, ws);
+    ONI_TRY(hipcub::DeviceScan::InclusiveSum(cub, cbytes, ws, psum, (int)n, s));
+  }
+  k_pair_counts<<<nblk(n), kB, 0, s>>>(head, weight ? psum : nullptr, nnz, n, pair_cnt);
   if (order0 && n0 > 0) ONI_TRY(hipcub::DeviceSelect::If(cub, cbytes, perm, order0, nsel, (int)n, BelowN{(int32_t)n0}, s));
   return (int)hipGetLastError();
 }
