@@ -429,9 +429,10 @@ class GibbsLDA:
         if self.comm is not None and self.comm.dist:
             self.comm.allreduce_(self.nwk)
             self.comm.allreduce_(self.nk[0])
-        # world 1: every token holds one topic, so Σ n_k = T (no device read); DP: the global sum
+        # one rank (a forced 1-rank group too): every token holds one topic, so Σ n_k = T (no device
+        # read, no host sync behind the init kernels); DP: the global sum
         self.T_global = (int(self.nk[0][: self.K].sum()) if self.comm is not None and self.comm.dist
-                         else int(self.c.T))
+                         and self.comm.world > 1 else int(self.c.T))
         self._check_magnitude()
         self._delta_on = False
         self._chg_q = []

@@ -227,6 +227,14 @@ def place_docs(doc_keys64: torch.Tensor, weights: torch.Tensor | None, comm: Com
     cuda = doc_keys64.is_cuda
     if cuda:
         from ..ops import corpus as oc
+    if W == 1 and not (split_L and split_L > 0 and W >= SPLIT_MIN_WORLD and SPLIT_DEN > 0):
+        # a 1-rank group owns every document (LPT puts every item on rank 0; nothing is split):
+        # no counts, candidates, collectives or host round trip
+        ukeys, inv = encode_docs(doc_keys64.contiguous())
+        uown = torch.zeros(ukeys.numel(), dtype=torch.int32, device=dev)
+        out = (uown, inv, ukeys) if per_doc else uown.long()[inv.long()]
+        return (out, None) if split_L is not None else out
+    if cuda:
         ukeys, inv, ucnt = oc.dict_encode(doc_keys64.contiguous(), 32,
                                           weights.to(torch.int32) if weights is not None else None, counts=True)
     else:
