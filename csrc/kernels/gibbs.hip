@@ -216,44 +216,52 @@ __global__ __launch_bounds__(256) void k_delta_recount(const int32_t* __restrict
 constexpr int kRecountTile = 4096;
 constexpr int kRecountCells = 2048;
 
+// E tokens per lane: 16 (4096-token tiles) for large corpora; 4 (1024-token tiles) below 8M
+// tokens, where 4096-token tiles leave fewer workgroups than the chip holds (a 2M-token DNS day:
+// 488 of them on 256 CUs)
+template <int E>
 __global__ __launch_bounds__(256) void k_recount(const int32_t* __restrict__ wsorted, const int32_t* __restrict__ wslot,
                                                   const uint8_t* __restrict__ tok_z, int64_t T, int32_t* __restrict__ nwk,
                                                   int KS) {
+  static_assert(E % 4 == 0, "whole 16-B loads");
+  constexpr int kTile = 256 * E;
   __shared__ int32_t hst[kRecountCells];
-  const int64_t lo = (int64_t)blockIdx.x * kRecountTile;
+  const int64_t lo = (int64_t)blockIdx.x * kTile;
   if (lo >= T) return;
-  const int64_t hi = lo + kRecountTile < T ? lo + kRecountTile : T;
+  const int64_t hi = lo + kTile < T ? lo + kTile : T;
   const int w_lo = wsorted[lo], w_hi = wsorted[hi - 1];
   const int cap_rows = kRecountCells / KS;
   const int rows = (w_hi - w_lo + 1) < cap_rows ? (w_hi - w_lo + 1) : cap_rows;
   const int cells = rows * KS;
   for (int i = threadIdx.x; i < cells; i += blockDim.x) hst[i] = 0;
-  const int64_t base = lo + (int64_t)threadIdx.x * 16;
-  int w[16], z[16];
+  const int64_t base = lo + (int64_t)threadIdx.x * E;
+  int w[E], z[E];
   int nt = 0;
-  if (base + 16 <= hi) {
-    nt = 16;
+  if (base + E <= hi) {
+    nt = E;
     const int4* wp = reinterpret_cast<const int4*>(wsorted + base);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < E / 4; ++q) {
       const int4 v = wp[q];
       w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
     }
     if (wslot) {
       const int4* sp = reinterpret_cast<const int4*>(wslot + base);
-      int sl[16];
+      int sl[E];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < E / 4; ++q) {
         const int4 v = sp[q];
         sl[4 * q] = v.x; sl[4 * q + 1] = v.y; sl[4 * q + 2] = v.z; sl[4 * q + 3] = v.w;
       }
 #pragma unroll
-      for (int t = 0; t < 16; ++t) z[t] = tok_z[sl[t]];
+      for (int t = 0; t < E; ++t) z[t] = tok_z[sl[t]];
     } else {
-      const uint4 zb = *reinterpret_cast<const uint4*>(tok_z + base);
-      const uint32_t zz[4] = {zb.x, zb.y, zb.z, zb.w};
 #pragma unroll
-      for (int t = 0; t < 16; ++t) z[t] = (int)((zz[t >> 2] >> (8 * (t & 3))) & 0xFFu);
+      for (int q = 0; q < E / 4; ++q) {
+        const uint32_t zz = *reinterpret_cast<const uint32_t*>(tok_z + base + 4 * q);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) z[4 * q + t] = (int)((zz >> (8 * t)) & 0xFFu);
+      }
     }
   } else if (base < hi) {
     nt = (int)(hi - base);
@@ -264,7 +272,7 @@ __global__ __launch_bounds__(256) void k_recount(const int32_t* __restrict__ wso
   }
   __syncthreads();
 #pragma unroll
-  for (int t = 0; t < 16; ++t) {
+  for (int t = 0; t < E; ++t) {
     if (t < nt) {
       const int r = w[t] - w_lo;
       if (r < rows) atomicAdd(&hst[r * KS + z[t]], 1);
@@ -501,8 +509,13 @@ ONI_API int oni_recount(const int32_t* wsorted, const int32_t* wslot, const uint
   if (KS < 1 || KS > kRecountCells) return (int)hipErrorInvalidValue;
   (void)tile;
   (void)wmax;
-  const unsigned grid = (unsigned)((T + kRecountTile - 1) / kRecountTile);
-  k_recount<<<grid, 256, 0, s>>>(wsorted, wslot, tok_z, T, nwk, KS);
+  if (T < (int64_t(8) << 20)) {
+    const unsigned grid = (unsigned)((T + 1023) / 1024);
+    k_recount<4><<<grid, 256, 0, s>>>(wsorted, wslot, tok_z, T, nwk, KS);
+  } else {
+    const unsigned grid = (unsigned)((T + kRecountTile - 1) / kRecountTile);
+    k_recount<16><<<grid, 256, 0, s>>>(wsorted, wslot, tok_z, T, nwk, KS);
+  }
   return (int)hipGetLastError();
 }
 
