@@ -30,6 +30,7 @@ from .corpus import Corpus, canonical_tokens
 
 
 NK_REP = 32
+POLL_GIVE_UP_SWEEP = 40  # auto count mode: last sweep that may still start a far-off switch
 # largest global token count a model takes: every int32 count (n_wk, n_k, n_dk, Δ) is ≤ the token
 # count, and the Δn_k replicas hold partial sums of it
 INT32_COUNT_MAX = 2**31 - 1
@@ -208,6 +209,7 @@ class GibbsLDA:
         self._delta_on = False
         self._force_mode = None
         self._chg_q: list = []    # (sweep index, host buffer, event) of pending change-count copies
+        self._poll_off = False
         self.T_global = corpus.T
         self.change_log: list[tuple[int, float]] = []
         # auto's early (high change rate) sweeps: "recount" (0, default) rebuilds n_wk by the
@@ -436,6 +438,7 @@ class GibbsLDA:
         self._check_magnitude()
         self._delta_on = False
         self._chg_q = []
+        self._poll_off = False
         self._sync_aux_z()
         self.sweeps_done = 0
         self._graph = None
@@ -488,7 +491,7 @@ class GibbsLDA:
 
     def _note_changes(self) -> None:
         """Queue an async copy of the last completed sweep's (all-reduced) changed-token count."""
-        if not self.auto or self.cfg.auto_switch > 0 or self._delta_on:
+        if not self.auto or self.cfg.auto_switch > 0 or self._delta_on or self._poll_off:
             return
         src = self.dn[1 - self.b][self._aux_off:self._aux_off + 1]
         if self.device.type == "cuda":
@@ -515,6 +518,12 @@ class GibbsLDA:
             self.change_log.append(latest)
             if latest[1] < self.cfg.auto_threshold:
                 self._delta_on = True
+                self._chg_q.clear()
+            elif latest[0] >= POLL_GIVE_UP_SWEEP and latest[1] > 2 * self.cfg.auto_threshold:
+                # still far above the switch point this late (the DNS day holds at ~67 % changed
+                # tokens): stop the per-pair-of-sweeps count read-back. Count modes all draw the
+                # same chain, so this only trades a possible late switch for 100 fewer polls
+                self._poll_off = True
                 self._chg_q.clear()
 
     def _ensure_zw(self) -> None:
@@ -1086,5 +1095,6 @@ class GibbsLDA:
         self._check_magnitude()
         self._delta_on = False
         self._chg_q = []
+        self._poll_off = False
         self._graph = None
         self._prime()

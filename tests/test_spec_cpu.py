@@ -332,3 +332,25 @@ def test_x01_pack_policy(monkeypatch):
     monkeypatch.setenv("ONI_X01_PACK", "1")
     monkeypatch.setenv("ONI_X01_PACK_MIN_BYTES", str(1 << 40))
     assert m._x01_wanted()
+
+
+def test_auto_mode_stops_polling_far_above_threshold():
+    """A chain still far above the switch point after POLL_GIVE_UP_SWEEP sweeps stops reading back
+    change counts; the chain itself is the recount chain bit for bit."""
+    import torch
+
+    from oni355.models import gibbs as gm
+    from oni355.models.corpus import build_corpus
+    r = np.random.default_rng(12)
+    lens = r.integers(1, 120, 40)
+    tdoc = torch.from_numpy(np.repeat(np.arange(40), lens))
+    tword = torch.from_numpy(r.integers(0, 50, int(lens.sum())))
+    c = build_corpus(tdoc, tword, 40, 50, torch.arange(40, dtype=torch.int32) * 5 + 1, 1, L=64)
+    a = gm.GibbsLDA(c, gm.GibbsConfig(K=20, seed=3, count_mode="auto", auto_threshold=1e-4))
+    b = gm.GibbsLDA(c, gm.GibbsConfig(K=20, seed=3, count_mode="recount"))
+    for m in (a, b):
+        m.initialize()
+        m.sweep(gm.POLL_GIVE_UP_SWEEP + 10)
+    assert a._poll_off and not a._delta_on
+    assert max(sw for sw, _ in a.change_log) < gm.POLL_GIVE_UP_SWEEP + 4
+    assert torch.equal(a.tok_z, b.tok_z) and torch.equal(a.nwk, b.nwk)
