@@ -269,6 +269,7 @@ class GibbsLDA:
         self.timings = {"allreduce_calls": 0}
         self._ar_events: list = []
         self._capturing = False
+        self._last_inplace = False  # the last executed sweep applied in place (Δ heads untouched)
         self._corrupted = False
         self._tail_cache = None  # (sweeps_done, device tail sums, host copy): see _tail()
         self._x01 = None
@@ -277,7 +278,7 @@ class GibbsLDA:
         # one rank (no process group, or a 1-rank group whose all-reduce is the identity): the count
         # passes add Δn_wk straight into n_wk and k_apply refreshes q from it (2 of its 5 passes
         # over V·KS fewer); ONI_APPLY_INPLACE=0 keeps the Δ buffer
-        self._inplace_ok = ((comm is None or not comm.dist or (comm.world == 1 and self._x01 is None))
+        self._inplace_ok = ((comm is None or not comm.live and self._x01 is None)
                             and self._split is None and os.environ.get("ONI_APPLY_INPLACE", "1") != "0")
         # chunk starts (doc-local token positions) are multiples of the chunk length L, pieces of
         # split documents included: with L % 4 == 0 every chunk starts a Philox 4-token group
@@ -433,8 +434,8 @@ class GibbsLDA:
             self.comm.allreduce_(self.nk[0])
         # one rank (a forced 1-rank group too): every token holds one topic, so Σ n_k = T (no device
         # read, no host sync behind the init kernels); DP: the global sum
-        self.T_global = (int(self.nk[0][: self.K].sum()) if self.comm is not None and self.comm.dist
-                         and self.comm.world > 1 else int(self.c.T))
+        self.T_global = (int(self.nk[0][: self.K].sum()) if self.comm is not None and self.comm.live
+                         else int(self.c.T))
         self._check_magnitude()
         self._delta_on = False
         self._chg_q = []
@@ -559,6 +560,7 @@ class GibbsLDA:
                         rows_copy=(self.ndk[self.a], self.ndk[1 - self.a], self.c.long_rows))
         self.cn = 1 - self.cn
         self.sweep_ctr.fill_(self.sweeps_done + 1)
+        self._last_inplace = False  # dn[0] zeroed here, dn[1] by the apply
         _ = VK
 
     # ---------------------------------------------------------------------------------------------
@@ -574,6 +576,8 @@ class GibbsLDA:
         # every apply -- the previous sweep's, or _prime()'s after init / resume -- seeds that copy
         st = self._state(False)
         inplace = self._inplace_ok and mode in (1, 2, 4)
+        if not inplace and self._last_inplace and not self._capturing:
+            self._clean_heads()
         if inplace:
             st["dnwk"] = self.nwk  # MODE 1: the sampler's Δ atomics land in n_wk itself
         if self.mh:
@@ -617,6 +621,19 @@ class GibbsLDA:
         self._tail_cache = None
         if not self._capturing:
             self._zw_synced = mode == 3
+            self._last_inplace = inplace
+
+    def _clean_heads(self) -> None:
+        """Zero both Δ heads before a sweep that writes one after in-place sweeps: an in-place apply
+        neither reads nor zeroes them, so the head a non-in-place sweep left behind is still there
+        (auto mode only switches recount → delta, but a forced or resumed schedule need not)."""
+        VK = self.V * self.KS
+        for d in self.dn:
+            d[:VK].zero_()
+        self._last_inplace = False
+
+    def _pair_inplace(self, mode: int) -> bool:
+        return self._inplace_ok and mode in (1, 2, 4)
 
     def _allreduce_dn(self, buf: torch.Tensor) -> None:
         """X01: all-reduce of the sweep's Δ buffer (Δn_wk ‖ Δn_k replicas ‖ aux words).
@@ -631,9 +648,9 @@ class GibbsLDA:
             e0.record()
         x = self._x01
         # a forced 1-rank group (ONI_FORCE_DIST=1: every data-parallel code path on one GPU) keeps
-        # the pack / unpack but drops the collective itself -- the sum over one rank is the identity,
-        # and the RCCL node would be the only difference to world 1 in the captured sweep
-        reduce = self.comm.world > 1
+        # the pack / unpack but drops the collective itself -- the sum over one rank is the identity
+        # -- unless ONI_COMM_REAL=1 (comm.live), which runs the RCCL all-reduce inside the graph
+        reduce = self.comm.live
         if x is not None:
             ops.x01_pack(buf, x["tiny"], x["light"], x["heavy"], self.KS, x["tail_off"], x["tail_len"], x["O8"], x["O"],
                          x["buf"])
@@ -679,6 +696,8 @@ class GibbsLDA:
         return round(float(np.median(times)), 4)
 
     def _graphable(self) -> bool:
+        if getattr(self, "_graph_off", False):
+            return False  # a capture failed on some rank: eager sweeps for the rest of the model
         if not (self.cfg.use_graph and self.device.type == "cuda" and os.environ.get("ONI_NO_GRAPH", "0") != "1"):
             return False
         if self.comm is None or not self.comm.dist:
@@ -696,7 +715,7 @@ class GibbsLDA:
         s = _capture_stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         g = torch.cuda.CUDAGraph()
-        # capture does not execute: the host-side parities are rewound afterwards
+        # capture does not execute: the host-side parities are rewound afterwards (failed or not)
         calls = self.timings["allreduce_calls"]
         self._capturing = True
         # no garbage collection during the capture: a collected CUDAGraph (another model's) would
@@ -710,6 +729,8 @@ class GibbsLDA:
                 # later allocations then go back to hipMalloc)
                 g.capture_begin()
                 try:
+                    if fault.capture_fails(self.comm.rank if self.comm is not None else 0):
+                        raise fault.InjectedFault("injected sweep-graph capture failure")
                     self._one_sweep()
                     self._one_sweep()
                 finally:
@@ -719,12 +740,43 @@ class GibbsLDA:
             self.timings["allreduce_calls"] = calls
             if gc_on:
                 gc.enable()
-        torch.cuda.current_stream(self.device).wait_stream(s)
-        self.a, self.b, self.cn, self.sweeps_done, self._aux_synced = saved
-        self._force_mode = None
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            self.a, self.b, self.cn, self.sweeps_done, self._aux_synced = saved
+            self._force_mode = None
         entry = (g, (self.a, self.b, self.cn))
         self._graphs[(mode, self._acc)] = entry
         return entry
+
+    def _capture_agreed(self, mode: int, also: int | None = None):
+        """Capture the ``mode`` pair (and the ``also`` pair), then vote: the graphs are used only if
+        every rank captured (comm.Comm.agree, an eager MIN all-reduce -- captures happen at the same
+        sweep on every rank, so the votes line up). Otherwise every rank drops its graphs and runs
+        eager sweeps from here on: the same kernels and collectives in the same order, so the chain
+        is unchanged. Returns the ``mode`` entry, or None after a fallback."""
+        err = None
+        entry = None
+        try:
+            entry = self._capture(mode)
+            if also is not None:
+                self._capture(also)
+        except Exception as e:  # noqa: BLE001 -- any capture error (HIP, RCCL, injected) falls back
+            err = e
+        ok = err is None
+        if self.comm is not None and self.comm.dist:
+            ok = self.comm.agree(ok)
+        if ok:
+            return entry
+        import sys
+        why = repr(err) if err is not None else "another rank's capture failed"
+        sys.stderr.write(f"[oni355] sweep-graph capture failed ({why}): eager sweeps from sweep "
+                         f"{self.sweeps_done + 1}\n")
+        self.timings["graph_fallback"] = why
+        self._graphs = {}
+        self._graph = None
+        self._graph_off = True
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        return None
 
     @traced("oni:lda.sweeps")
     def sweep(self, n: int = 1) -> None:
@@ -854,12 +906,17 @@ class GibbsLDA:
                 done += 1
                 continue
             if entry is None:
-                entry = self._capture(m1)
-                if (self.auto and self.cfg.auto_switch == 0 and m1 == self.early
-                        and (self.mode, self._acc) not in self._graphs):
-                    self._capture(self.mode)  # capture the delta pair now: no capture stall at the switch
+                # capture the delta pair now too: no capture stall at the switch
+                also = (self.mode if (self.auto and self.cfg.auto_switch == 0 and m1 == self.early
+                                      and (self.mode, self._acc) not in self._graphs) else None)
+                entry = self._capture_agreed(m1, also)
+                if entry is None:
+                    continue  # fell back to eager sweeps (every rank)
+            if not self._pair_inplace(m1) and self._last_inplace:
+                self._clean_heads()  # eager, before the replay (see _clean_heads)
             self._graph = entry[0]
             entry[0].replay()
+            self._last_inplace = self._pair_inplace(m1)
             self.timings["graph_replays"] = self.timings.get("graph_replays", 0) + 1
             self.sweeps_done += 2
             self._aux_synced = self._keeps_aux(m1)
@@ -933,10 +990,15 @@ class GibbsLDA:
         K = self.K
         for k in ("wk", "k", "dk"):
             want = (a[k].shape[0], K) if a[k].dim() == 2 else (K,)
-            if tuple(st[k].shape) != want:
+            v = st[k]
+            # states saved before the K-column format hold the KS-wide tiling-padded tables (the
+            # padding topics are never used): their first K columns are the same sums
+            if tuple(v.shape[:-1]) == want[:-1] and v.shape[-1] == self.KS and self.KS != K:
+                v = v[..., :K]
+            if tuple(v.shape) != want:
                 raise ValueError(f"averaging state {k} shape {tuple(st[k].shape)} != {want}")
             a[k].zero_()
-            a[k][..., :K].copy_(st[k].to(a[k].device))
+            a[k][..., :K].copy_(v.to(a[k].device))
         a["n"] = int(st["n"])
         self._avg_cache = None
 

@@ -37,14 +37,25 @@ class Comm:
         # collectives run whenever a process group exists: world > 1, or a forced 1-rank group
         # (ONI_FORCE_DIST=1) that drives the real RCCL / gloo code paths on a single device
         self.dist = world > 1 or forced
+        # ONI_COMM_REAL=1: a forced 1-rank group runs every collective for real (one RCCL kernel
+        # each: X01 inside the captured sweep graph, the routing all-to-all, the vocabulary and
+        # result gathers, the X03 histogram all-reduce) instead of taking the identity shortcut --
+        # the hardware rehearsal of the data-parallel path on one GPU. Off (default): a 1-rank
+        # group's collectives are the identity (no copy, no launch), as in the overhead bench.
+        self.real = self.dist and world == 1 and os.environ.get("ONI_COMM_REAL", "0") == "1"
+        # do collectives move data? (several ranks, or a forced-real 1-rank group)
+        self.live = self.dist and (world > 1 or self.real)
 
     # -- basic ------------------------------------------------------------------------------------
-    # A 1-rank group (ONI_FORCE_DIST=1) reduces, broadcasts and gathers as the identity: the
-    # data-parallel code paths around the collectives run, the collectives themselves (one RCCL
-    # copy kernel each) do not -- as in the sweeps' X01 (models/gibbs.py _allreduce_dn).
+    # A 1-rank group (ONI_FORCE_DIST=1) reduces, broadcasts and gathers as the identity unless
+    # ONI_COMM_REAL=1 (``live``; on RCCL through a self all-to-all, see _one_rank_rccl): the
+    # data-parallel code paths around the collectives run, the collectives themselves do not --
+    # as in the sweeps' X01 (models/gibbs.py _allreduce_dn).
     def allreduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
-        if self.dist and self.world > 1:
-            rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
+        if self.live:
+            if self._one_rank_rccl():
+                return self._reduce_one_rank(t)
+            rop = self._rop(op)
             if self._via_host and t.is_cuda:
                 h = t.cpu()
                 dist.all_reduce(h, op=rop, group=self.group)
@@ -53,21 +64,43 @@ class Comm:
                 dist.all_reduce(t, op=rop, group=self.group)
         return t
 
+    def _rop(self, op: str):
+        return {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
+
+    def _one_rank_rccl(self) -> bool:
+        """A forced-real 1-rank RCCL group (ONI_COMM_REAL=1, one GPU)? RCCL runs an in-place
+        1-rank all-reduce as a no-op -- no kernel, nothing for a graph to hold -- so such a group
+        reduces through a self all-to-all (Σ over one rank = the rank's own buffer), which RCCL
+        executes as a real p2p kernel over the whole payload: the sweep graph then captures and
+        replays an RCCL kernel of the X01 payload's size, joined to the compute stream as a ring
+        all-reduce's would be."""
+        return self.real and self.backend == "nccl" and self.device.type == "cuda" and not self._via_host
+
+    def _reduce_one_rank(self, t: torch.Tensor) -> torch.Tensor:
+        key = (t.numel(), t.dtype)
+        cache = self.__dict__.setdefault("_a2a_scratch", {})
+        if key not in cache:
+            cache[key] = torch.empty(t.numel(), dtype=t.dtype, device=t.device)
+        out = cache[key]
+        dist.all_to_all_single(out, t.reshape(-1), group=self.group)
+        t.copy_(out.view(t.shape))
+        return t
+
     def allreduce_np(self, a) -> np.ndarray:
         """Sum over ranks → host array. ``a``: a host array, or a device tensor (reduced where it
         lives -- no host→device copy; the caller's tensor is left unchanged)."""
         if torch.is_tensor(a):
-            if not self.dist or self.world == 1:
+            if not self.live:
                 return a.cpu().numpy()
             t = a.to(self._coll_device, copy=True)
-            dist.all_reduce(t, group=self.group)
+            self.allreduce_(t)
             return t.cpu().numpy()
         a = np.asarray(a)
-        if not self.dist or self.world == 1:
+        if not self.live:
             return a
         # a private copy: on CPU collectives torch.from_numpy would alias (and reduce into) ``a``
         t = self._small_tensor(a) if a.size == 1 else torch.from_numpy(np.array(a, copy=True)).to(self._coll_device)
-        dist.all_reduce(t, group=self.group)
+        self.allreduce_(t)
         return t.cpu().numpy().reshape(a.shape)
 
     allreduce_np.accepts_tensors = True  # quantile_cuts hands it device histograms
@@ -81,11 +114,10 @@ class Comm:
                           device=self._coll_device)
 
     def allreduce_scalar(self, x: float, op: str = "sum") -> float:
-        if not self.dist or self.world == 1:
+        if not self.live:
             return float(x)
         t = torch.full((1,), float(x), dtype=torch.float64, device=self._coll_device)
-        dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
-                               "min": dist.ReduceOp.MIN}[op], group=self.group)
+        self.allreduce_(t, op)
         return float(t.item())
 
     def barrier(self) -> None:
@@ -96,7 +128,7 @@ class Comm:
                 dist.barrier(group=self.group)
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
-        if self.dist and self.world > 1:
+        if self.live:
             if self._via_host and t.is_cuda:
                 h = t.cpu()
                 dist.broadcast(h, src=src, group=self.group)
@@ -117,7 +149,7 @@ class Comm:
     # -- variable-size gathers / exchanges ------------------------------------------------------
     def allgather_var(self, t: torch.Tensor) -> list[torch.Tensor]:
         """All-gather tensors whose first dim differs per rank."""
-        if not self.dist or self.world == 1:
+        if not self.live:
             # a 1-rank group (ONI_FORCE_DIST=1) gathers its own tensor: no copy, no collective
             return [t.to(self.device) if self.dist else t]
         if self._via_host and t.is_cuda:
@@ -138,7 +170,7 @@ class Comm:
 
         ``recv_counts`` (when the caller already knows them, e.g. the way back of a routed
         exchange) skips the count exchange. ``return_recv_counts`` also returns them (list)."""
-        if not self.dist or self.world == 1:
+        if not self.live:
             # 1-rank group: the exchange is the identity (every row stays) -- no copy, no collective
             if self.dist:
                 t = t.to(self.device)
@@ -187,7 +219,19 @@ class Comm:
         return groups[name]
 
     def _host_view(self) -> "Comm":
-        return Comm(self.rank, self.world, torch.device("cpu"), self.group, forced=self.dist, backend="gloo")
+        v = Comm(self.rank, self.world, torch.device("cpu"), self.group, forced=self.dist, backend="gloo")
+        v.real, v.live = self.real, self.live
+        return v
+
+    def agree(self, ok: bool) -> bool:
+        """Rank-consistent vote: True on every rank iff ``ok`` on every rank (an eager MIN
+        all-reduce; the identity without a process group). Used after a HIP-graph capture of the
+        sweeps (models/gibbs.py): one rank's failed capture sends every rank to eager sweeps."""
+        if not self.live:
+            return bool(ok)
+        t = torch.full((1,), 1 if ok else 0, dtype=torch.int32, device=self._coll_device)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+        return bool(int(t.item()))
 
 
 def init_from_env(device_type: str | None = None, timeout_s: float = 600.0) -> Comm:

@@ -96,7 +96,7 @@ def encode_words(word_keys64: torch.Tensor, comm: Comm | None, key_bits: int = 6
     else:
         luniq, inv = torch.unique(word_keys64, return_inverse=True)
         lids = inv.to(torch.int32)
-    if comm is None or not comm.dist or comm.world == 1:
+    if comm is None or not comm.live:
         return luniq, lids  # one rank: the local dictionary is the global one
     parts = comm.allgather_var(luniq)
     vocab = torch.unique(torch.cat([p.to(luniq.device) for p in parts]))
@@ -424,7 +424,7 @@ def split_corpus_tokens(plan: SplitPlan, udoc: torch.Tensor, inv: torch.Tensor, 
     u, ui = torch.unique(key, return_inverse=True)
     cnt = torch.zeros(u.numel(), dtype=i64, device=dev).index_add_(0, ui, wt[m].to(i64))
     rows = torch.stack([u // V, u % V, cnt], 1).contiguous()
-    allp = torch.cat([p.to(dev) for p in comm.allgather_var(rows)]) if comm.world > 1 else rows
+    allp = torch.cat([p.to(dev) for p in comm.allgather_var(rows)]) if comm.live else rows
     allp = allp[torch.argsort(allp[:, 0] * V + allp[:, 1])]
     mine = np.nonzero(plan.piece_owner == comm.rank)[0]
     pd, pw, pc = [], [], []
@@ -1038,7 +1038,7 @@ def _top_n_from_hist(score, hist, tol, maxresults, comm, row_offset, order=None,
         return (torch.from_numpy(gid[o].copy()), torch.from_numpy(sch[o].copy()),
                 torch.from_numpy(packed[1][o].copy()))
     gid, bits = gid[o], packed[2][o]
-    if comm is not None and comm.dist and comm.world > 1:
+    if comm is not None and comm.live:
         # one all-gather of every rank's local top-N (global id, score bits), merged on the host
         loc = torch.from_numpy(np.stack([gid, bits], 1).astype(np.int64)).to(score.device)
         both = torch.cat([p.to(score.device) for p in comm.allgather_var(loc)]).cpu().numpy()

@@ -44,6 +44,9 @@ class DnsDay:
     top_domains: list[str]
     anomaly_rows: np.ndarray
     theta_true: np.ndarray
+    # generating label per row (tools/oracle_recall.py): profile p, len(profiles) + b for long-tail
+    # behaviour b, -1 for a planted anomaly
+    labels: np.ndarray | None = None
 
     @property
     def n(self) -> int:
@@ -112,6 +115,7 @@ def generate_dns(n: int, seed: int = 5, n_clients: int | None = None, user_domai
     cum[:, -1] = 1
     z = np.clip(np.searchsorted((cum + np.arange(n_clients)[:, None]).ravel(), cli + rng.random(n), side="right")
                 - cli * P, 0, P - 1)
+    labels = z.astype(np.int32)
     pools = {"popular": _POPULAR, "cdn": _CDN, "mail": _MAIL, "telem": _TELEM,
              "user": [f"corp.{user_domain}.com", f"{user_domain}.com", f"eng.{user_domain}.com"]}
     names = [""] * n
@@ -171,6 +175,7 @@ def generate_dns(n: int, seed: int = 5, n_clients: int | None = None, user_domai
         own = np.concatenate([orng.permutation(W) for _ in range(-(-n_sl // W))])[:n_sl]
         own = own[orng.permutation(n_sl)]
         b = own[first[c_w] + (rng.random(m) * slots[c_w]).astype(np.int64)]
+        labels[wide] = P + b
         qtype[wide] = cb_q[b]
         rcode[wide] = cb_r[b]
         hour_f[wide] = cb_h[b]
@@ -179,6 +184,7 @@ def generate_dns(n: int, seed: int = 5, n_clients: int | None = None, user_domai
     hour = np.mod(np.floor(hour_f), 24).astype(np.int64)
     # planted tunnelling / DGA
     anomaly_rows = np.sort(rng.choice(n, size=min(n_anomalies, n), replace=False))
+    labels[anomaly_rows] = -1
     if anomaly_rows.size:
         quiet = np.argsort(w)[: max(1, n_clients // 10)]
         q_draw = quiet[rng.integers(0, quiet.size, size=anomaly_rows.size)]
@@ -230,7 +236,8 @@ def generate_dns(n: int, seed: int = 5, n_clients: int | None = None, user_domai
         "_n_answers": n_ans,
         "_answer_ip": answer,
     }
-    return DnsDay(cols=cols, top_domains=top_domain_list(), anomaly_rows=anomaly_rows, theta_true=theta)
+    return DnsDay(cols=cols, top_domains=top_domain_list(), anomaly_rows=anomaly_rows, theta_true=theta,
+                  labels=labels)
 
 
 def write_pcap(day: DnsDay, path: str) -> int:

@@ -62,6 +62,10 @@ class FlowDay:
     theta_true: np.ndarray  # [n_hosts, n_profiles]
     host_ips: np.ndarray  # uint32 [n_hosts]
     anomaly_rows: np.ndarray  # int64 row ids of planted anomalies
+    # generating label of every row (ground truth for tools/oracle_recall.py): the behaviour
+    # profile p (0..n_profiles-1), n_profiles + b for long-tail behaviour b of the realistic day,
+    # -1 for a planted anomaly
+    labels: np.ndarray | None = None
 
     @property
     def n(self) -> int:
@@ -128,6 +132,7 @@ def generate_flows(n: int, seed: int = 7, n_hosts: int | None = None, n_profiles
     flat = (cum + np.arange(n_hosts)[:, None]).ravel()
     z = np.searchsorted(flat, src + u, side="right") - src * n_profiles
     z = np.clip(z, 0, n_profiles - 1)
+    labels = z.astype(np.int32)
 
     port_of = np.zeros(n, dtype=np.int64)
     hour_f = np.zeros(n)
@@ -177,6 +182,7 @@ def generate_flows(n: int, seed: int = 7, n_hosts: int | None = None, n_profiles
         own = np.concatenate([orng.permutation(W) for _ in range(-(-n_sl // W))])[:n_sl]
         own = own[orng.permutation(n_sl)]
         b = own[first[h_lt] + (rng.random(lt.size) * slots[h_lt]).astype(np.int64)]
+        labels[lt] = n_profiles + b
         port_of[lt] = cb_port[b]
         hour_f[lt] = cb_hour[b]
         lbytes[lt] = cb_lbytes[b]
@@ -226,6 +232,7 @@ def generate_flows(n: int, seed: int = 7, n_hosts: int | None = None, n_profiles
     # scoring above ranks no lower than any rare flow of a small document.
     anomaly_rows = np.sort(rng.choice(n, size=min(n_anomalies, n), replace=False))
     na = anomaly_rows.size
+    labels[anomaly_rows] = -1
     if na:
         if anomaly_hosts == "quiet":
             quiet = np.argsort(w)[: max(1, n_hosts // 10)]
@@ -313,7 +320,7 @@ def generate_flows(n: int, seed: int = 7, n_hosts: int | None = None, n_profiles
                 txt[i] = t
             cols[k6] = StringColumn.from_list(txt)
             cols[k4] = np.where(v6_rows, 0, cols[k4]).astype(np.uint32)
-    return FlowDay(cols=cols, theta_true=theta, host_ips=host_ips, anomaly_rows=anomaly_rows)
+    return FlowDay(cols=cols, theta_true=theta, host_ips=host_ips, anomaly_rows=anomaly_rows, labels=labels)
 
 
 def generate_flows_sharded(per: int, parts: int, seed: int = 7, n_hosts: int | None = None, procs: int = 8,
@@ -332,16 +339,18 @@ def generate_flows_sharded(per: int, parts: int, seed: int = 7, n_hosts: int | N
     if any(not isinstance(v, np.ndarray) for v in probe.cols.values()):
         raise ValueError("sharded generation supports numeric columns only (no IPv6 text columns)")
     n = per * parts
+    shapes = dict(probe.cols, _labels=probe.labels)
     shm = {k: shared_memory.SharedMemory(create=True, size=max(1, n * v.dtype.itemsize))
-           for k, v in probe.cols.items()}
-    spec_ = {k: (s.name, probe.cols[k].dtype.str) for k, s in shm.items()}
+           for k, v in shapes.items()}
+    spec_ = {k: (s.name, shapes[k].dtype.str) for k, s in shm.items()}
     ctx = mp.get_context("fork")
 
     def work(r: int, q) -> None:
         d = generate_flows(per, seed=seed, n_hosts=n_hosts, rank=r, **kw)
+        src = dict(d.cols, _labels=d.labels)
         for k, (name, dt) in spec_.items():
             s = shared_memory.SharedMemory(name=name)
-            np.ndarray((n,), dtype=np.dtype(dt), buffer=s.buf)[r * per:(r + 1) * per] = d.cols[k]
+            np.ndarray((n,), dtype=np.dtype(dt), buffer=s.buf)[r * per:(r + 1) * per] = src[k]
             s.close()
         q.put((r, d.anomaly_rows + r * per))
 
@@ -369,5 +378,6 @@ def generate_flows_sharded(per: int, parts: int, seed: int = 7, n_hosts: int | N
         cols[k] = np.ndarray((n,), dtype=np.dtype(spec_[k][1]), buffer=s.buf).copy()
         s.close()
         s.unlink()
+    labels = cols.pop("_labels")
     return FlowDay(cols=cols, theta_true=probe.theta_true, host_ips=probe.host_ips,
-                   anomaly_rows=np.concatenate([anomalies[r] for r in range(parts)]))
+                   anomaly_rows=np.concatenate([anomalies[r] for r in range(parts)]), labels=labels)

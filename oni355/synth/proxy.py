@@ -45,6 +45,9 @@ PROXY_FIELDS = ["date", "time", "time-taken", "c-ip", "cs-username", "cs-auth-gr
 class ProxyDay:
     cols: dict
     anomaly_rows: np.ndarray
+    # generating label per row (tools/oracle_recall.py): profile p, len(profiles) + b for long-tail
+    # behaviour b, -1 for a planted anomaly
+    labels: np.ndarray | None = None
 
     @property
     def n(self) -> int:
@@ -122,6 +125,7 @@ def generate_proxy(n: int, seed: int = 9, n_clients: int | None = None, alpha_tr
         # behaviour its client never shows: the row comes from the client's least likely profile
         # (globally common words, rare for this client -- the P(word | doc) anomaly)
         z[anomaly_rows] = np.argmin(theta[cli[anomaly_rows]], axis=1)
+    labels = z.astype(np.int32)
     host, method, ua, ctype, path = [""] * n, [""] * n, [""] * n, [""] * n, [""] * n
     hour_f = np.zeros(n)
     status = np.full(n, 200, np.int64)
@@ -174,6 +178,7 @@ def generate_proxy(n: int, seed: int = 9, n_clients: int | None = None, alpha_tr
         own = own[orng.permutation(n_sl)]
         b = own[first[c_w] + (rng.random(wide.size) * slots[c_w]).astype(np.int64)]
         hour_f[wide] = cb_h[b]
+        labels[wide] = P + b
         for i, j in zip(wide.tolist(), b.tolist()):
             host[i], method[i], ua[i], ctype[i], path[i], status[i] = cb[j]
     hour = np.mod(np.floor(hour_f), 24).astype(int)
@@ -216,7 +221,8 @@ def generate_proxy(n: int, seed: int = 9, n_clients: int | None = None, alpha_tr
         "bcappname": StringColumn.from_list(["-"] * n), "bcappoperation": StringColumn.from_list(["-"] * n),
         "fulluri": StringColumn.from_list(fulluri),
     }
-    return ProxyDay(cols=cols, anomaly_rows=anomaly_rows)
+    labels[anomaly_rows] = -1
+    return ProxyDay(cols=cols, anomaly_rows=anomaly_rows, labels=labels)
 
 
 def write_log(day: ProxyDay, path: str) -> None:

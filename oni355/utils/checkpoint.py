@@ -232,10 +232,12 @@ def _same_chain(saved: dict, run: dict, sweep: int) -> bool:
     identities do; an MH run's state inside its dense burn-in is also a prefix of any MH run whose
     burn-in reaches that sweep (a 2-sweep run capped the same ONI_MH_BURN = 3 at 2)."""
     s, r = dict(saved), dict(run)
-    sc, rc = s.pop("chain", None), r.pop("chain", None)
-    if s != r or (sc is None) != (rc is None):
+    # a manifest written before identities carried the chain holds the dense sampler's chain
+    dense = {"sampler": "dense", "mh_burn": 0}
+    sc, rc = s.pop("chain", None) or dense, r.pop("chain", None) or dense
+    if s != r:
         return False
-    if sc is None or sc == rc:
+    if sc == rc:
         return True
     return sc.get("sampler") == rc.get("sampler") and sweep <= min(sc.get("mh_burn", 0), rc.get("mh_burn", 0))
 

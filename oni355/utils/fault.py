@@ -8,6 +8,9 @@ it reaches sweep S:
 * ``nan``   -- the model's counts and q table are corrupted (a negative count, a NaN q entry):
   the numerical health check after the sweep raises :class:`NumericalFault`;
 * ``raise`` -- :class:`InjectedFault` is raised.
+* ``capture`` -- the rank's next HIP-graph capture of the sweeps fails (raised between
+  capture begin and end): every rank must then fall back to eager sweeps together
+  (models/gibbs.py GibbsLDA._capture_agreed).
 
 ``attempt:A`` restricts the fault to the A-th launch of a supervised run (``ONI_RESTART_COUNT``,
 set by ``oni-ml --max-restarts``), so a restarted child does not fail again at the same sweep.
@@ -49,6 +52,8 @@ def maybe_inject(sweep: int, rank: int, corrupt=None) -> None:
     if "attempt" in f and int(os.environ.get("ONI_RESTART_COUNT", "0")) != f["attempt"]:
         return
     kind = f["kind"]
+    if kind == "capture":
+        return  # fired by capture_fails(), inside the graph capture
     if kind == "exit":
         sys.stderr.write(f"[oni355] injected fault: exit at sweep {sweep} rank {rank}\n")
         sys.stderr.flush()
@@ -61,6 +66,14 @@ def maybe_inject(sweep: int, rank: int, corrupt=None) -> None:
         corrupt()
         return
     raise InjectedFault(f"injected fault at sweep {sweep} rank {rank}")
+
+
+def capture_fails(rank: int) -> bool:
+    """Should this rank's sweep-graph capture fail (``ONI_FAULT=rank:R,kind:capture``)?"""
+    f = parse(os.environ.get("ONI_FAULT"))
+    if not f or f["kind"] != "capture" or f["rank"] != rank:
+        return False
+    return "attempt" not in f or int(os.environ.get("ONI_RESTART_COUNT", "0")) == f["attempt"]
 
 
 class Watchdog:

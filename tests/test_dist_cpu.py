@@ -77,6 +77,7 @@ def test_balanced_owner_evens_out_power_law_docs():
 
     class _Comm:
         world = 8
+        dist = live = True
 
         def allgather_var(self, t):
             return [t]
@@ -198,3 +199,109 @@ def test_dns_proxy_dp_matches_single_process(source):
     assert r1.size > 0
     assert np.array_equal(r1, r2) and np.array_equal(s1, s2) and np.array_equal(w1, w2)
     assert t1 == t2 and t1.count(b"\n") == r1.size  # the CSV rows, gathered from both ranks
+
+
+def _forced_real_worker(port, n_total, out_q, env):
+    os.environ.update(env)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    torch.set_num_threads(1)
+    from oni355.parallel import comm as pc
+    from oni355.pipeline.flow import run_flow
+    from oni355.synth.flow import generate_flows
+    comm = pc.init_from_env("cpu")
+    assert comm.dist and comm.world == 1 and comm.live == (env.get("ONI_COMM_REAL") == "1")
+    res = run_flow(dict(generate_flows(n_total, seed=11).cols), K=20, sweeps=4, maxresults=150, device="cpu",
+                   comm=comm)
+    out_q.put((res.rows, res.scores, res.src_scores, res.dst_scores, res.stats["loglik"],
+               res.lda.model._x01 is not None, res.lda.model._inplace_ok))
+    comm.barrier()
+    pc.shutdown()
+
+
+@pytest.mark.parametrize("env", [{"ONI_FORCE_DIST": "1", "ONI_COMM_REAL": "1"},
+                                 {"ONI_FORCE_DIST": "1", "ONI_COMM_REAL": "1", "ONI_X01_PACK": "1"}])
+def test_forced_real_one_rank_group_matches_single_process(env):
+    """ONI_COMM_REAL=1: a 1-rank process group runs every collective for real (X01 on the Δ
+    buffer -- packed too --, the vocabulary gather, the routing all-to-all, the result gather);
+    the run stays bitwise equal to the plain single process, and the in-place apply (which would
+    bypass the Δ buffer the all-reduce reads) is off."""
+    n = 6000
+    one = _run_world(1, n)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_forced_real_worker, args=(_free_port(), n, q, env))
+    p.start()
+    res = q.get(timeout=600)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    for a, b in zip(one[:4], res[:4]):
+        assert np.array_equal(a, b)
+    assert one[4] == pytest.approx(res[4], rel=1e-9)
+    assert res[5] == (env.get("ONI_X01_PACK") == "1")
+    assert res[6] is False
+
+
+class _FakeGraph:
+    def replay(self):
+        raise AssertionError("a graph was replayed although another rank's capture failed")
+
+
+def _vote_worker(rank, world, port, n_total, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from oni355.models.gibbs import GibbsLDA
+    from oni355.parallel import comm as pc
+    from oni355.pipeline.flow import run_flow
+    from oni355.synth.flow import generate_flows
+
+    # CPU stand-ins for HIP graph capture: rank 1's capture raises, rank 0's "succeeds"
+    def fake_capture(self, mode):
+        if rank == 1:
+            raise RuntimeError("hipErrorStreamCaptureInvalidated (simulated)")
+        entry = (_FakeGraph(), (self.a, self.b, self.cn))
+        self._graphs[(mode, self._acc)] = entry
+        return entry
+    GibbsLDA._graphable = lambda self: not getattr(self, "_graph_off", False)
+    GibbsLDA._capture = fake_capture
+    comm = pc.init_from_env("cpu")
+    day = generate_flows(n_total, seed=11)
+    per = n_total // world
+    lo = rank * per
+    hi = n_total if rank == world - 1 else lo + per
+    cols = {k: v[lo:hi] for k, v in day.cols.items()}
+    res = run_flow(cols, K=20, sweeps=4, maxresults=150, device="cpu", comm=comm, row_offset=lo)
+    fb = res.lda.model.timings.get("graph_fallback")
+    got = comm.allgather_var(torch.tensor([1 if fb else 0]))
+    if rank == 0:
+        out_q.put((res.rows, res.scores, res.src_scores, res.dst_scores, res.stats["loglik"],
+                   [int(t[0]) for t in got], res.lda.model.timings.get("graph_replays", 0)))
+    comm.barrier()
+    pc.shutdown()
+
+
+def test_capture_failure_on_one_rank_sends_every_rank_to_eager_sweeps():
+    """The sweep-graph capture vote (GibbsLDA._capture_agreed): rank 1's capture fails, rank 0's
+    succeeds; the MIN all-reduce makes BOTH ranks drop their graphs and sweep eagerly (rank 0's
+    graph is never replayed), and the day is still bitwise the single-process day."""
+    n = 6000
+    one = _run_world(1, n)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_vote_worker, args=(r, 2, port, n, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=600)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for a, b in zip(one[:4], res[:4]):
+        assert np.array_equal(a, b)
+    assert one[4] == pytest.approx(res[4], rel=1e-9)
+    assert res[5] == [1, 1] and res[6] == 0
+
+
+def test_agree_is_a_min_vote():
+    from oni355.parallel.comm import Comm
+    assert Comm().agree(True) and not Comm().agree(False)

@@ -122,6 +122,7 @@ def test_split_placement_balances_a_30pct_document():
 
     class _Comm:
         world = 8
+        dist = live = True
 
         def allgather_var(self, t):
             return [t]

@@ -159,6 +159,49 @@ def test_checkpoint_identity_names_the_chain(tmp_path):
     assert ck.restore(m3) == 2
 
 
+def test_checkpoint_from_before_chain_identities_resumes_dense(tmp_path):
+    """A manifest / shard written before identities carried the chain (no "chain" key) is the
+    dense chain: it resumes a dense run and still refuses an MH run."""
+    import glob
+    import json
+    m = _model(torch.device("cpu"), sweeps=8)
+    m.sweep(2)
+    ck = Checkpointer(str(tmp_path))
+    ck.save(m)
+    mp = tmp_path / "manifest.json"
+    man = json.loads(mp.read_text())
+    man["ident"].pop("chain")
+    mp.write_text(json.dumps(man))
+    for f in glob.glob(str(tmp_path / "ckpt_s*.pt")):
+        pl = torch.load(f, weights_only=True)
+        pl["ident"].pop("chain")
+        torch.save(pl, f)
+    m2 = _model(torch.device("cpu"), sweeps=8)
+    assert ck.restore(m2) == 2
+    assert torch.equal(m2.canonical_z(), m.canonical_z())
+    m3 = _model(torch.device("cpu"), sweeps=8)
+    m3.chain = {"sampler": "mh", "mh_burn": 20}
+    with pytest.raises(ValueError, match="sampler and MH burn-in"):
+        ck.restore(m3)
+
+
+def test_average_state_in_the_old_tiling_padded_format_loads():
+    """Averaging sums saved KS-wide (before the K-column format) load: the padding columns are
+    dropped."""
+    m = _model(torch.device("cpu"), K=100)
+    m.sweep(1)
+    m._avg["n"] = 1
+    m._accumulate()
+    a = m._avg
+    old = {"n": 1, "wk": a["wk"].to(torch.int64).clone(), "k": a["k"].to(torch.int64).clone(),
+           "dk": a["dk"].to(torch.int64).clone()}
+    assert old["wk"].shape[1] == m.KS != m.K
+    want = m.average_state()
+    a["wk"].fill_(-1)
+    m.load_average_state(old)
+    assert torch.equal(m.average_state()["wk"], want["wk"]) and torch.equal(m.average_state()["dk"], want["dk"])
+
+
 def test_average_state_is_tiling_free():
     """The saved sums hold the K real topics: a KS = 112 (dense) state loads into KS = 100 (MH)."""
     m = _model(torch.device("cpu"), K=100)
