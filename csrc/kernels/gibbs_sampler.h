@@ -58,6 +58,9 @@ struct OniGibbs {
                                 //   (written once with the corpus, 0xFFFF: read wsorted)
                                // (MODE 4 reuses chg_mask as a u32 bitmap over word-sorted positions)
   int32_t* chg_count;          // optional: += number of tokens whose topic changed (drives the auto mode)
+  uint8_t* tok_zlag;           // optional, SELL (ONI_X01_LAG): the topic each token holds in the counts
+                               //   behind q (one sweep older than the doc rows): the word-side exclusion
+                               //   is taken there; the pass writes tok_zlag := the token's sweep-start topic
   int64_t n_slices;
   int32_t K;
   int32_t KS;
@@ -332,15 +335,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 8))) 
   uint32_t w_nx = len > 0 ? a.tok_word[off + c] : oni::kPadWord;
   int z_nx = (!INIT && len > 0) ? (int)a.tok_z[off + c] : 0;
   int32_t p_nx = (WPF && len > 0) ? a.wpos[off + c] : 0;
+  // lagged word side (ONI_X01_LAG): the word-side exclusion at the topic the counts behind q hold
+  const bool lag = !INIT && a.tok_zlag != nullptr;
+  int l_nx = (lag && len > 0) ? (int)a.tok_zlag[off + c] : z_nx;
   Pend<MODE> pend;
   for (int s = 0; s < len; ++s) {
     const int64_t idx = off + (int64_t)s * S + c;
     const uint32_t w = w_nx;
     const int zo = z_nx;
+    const int zl = lag ? l_nx : zo;
     const int32_t pw = p_nx;
     if (s + 1 < len) {
       w_nx = a.tok_word[idx + S];
       if (!INIT) z_nx = (int)a.tok_z[idx + S];
+      if (lag) l_nx = (int)a.tok_zlag[idx + S];
       if (WPF) p_nx = a.wpos[idx + S];
     }
     if constexpr (!INIT) pend.flush(a, KS);
@@ -363,14 +371,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 8))) 
         load_row_f<KP>(a.q + (int64_t)w * KS + kbase, qv);
         wprev = w;
       }
-      const float qz = a.q[(int64_t)w * KS + zo];
-      const float qe = fmaf(qz, a.qfix[zo], -a.qfix[KS + zo]);
+      const float qz = a.q[(int64_t)w * KS + zl];
+      const float qe = fmaf(qz, a.qfix[zl], -a.qfix[KS + zl]);
       const float f = qe / qz;
       float loc[KP];
       float run = 0.f;
 #pragma unroll
       for (int j = 0; j < KP; ++j) {
-        const bool own = kbase + j == zo;
+        const bool own = kbase + j == zl;
         float av = (float)n[j] + a.alpha;
         float qj = qv[j];
         if (G == 1) qj = own ? qe : qj;
@@ -406,6 +414,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 8))) 
         ++nchg;
         pend.note(idx, zo, zn, pw, w);
       }
+      if (lag && g == 0 && zl != zo) a.tok_zlag[idx] = (uint8_t)zo;
       if constexpr (MODE == 2) {
         // lane 0 (c = 0) owns the slice's longest chunk, so it is active at every step
         const uint64_t m = __ballot(changed);
@@ -483,7 +492,7 @@ __device__ __forceinline__ int count_le(const float (&P)[KP], float excl, float 
 // 3-wave register budget (+0.011 ms) all lost.
 // WPD (off: measured 0.255 vs 0.248 ms/sweep): MODE 3/4 changed tokens load their word-sorted
 // slot when they change (exec-masked, ~10 % of lanes) instead of streaming it with every token.
-template <int KP, int MODE, bool AIR, bool WPD, bool ALN = false>
+template <int KP, int MODE, bool AIR, bool WPD, bool ALN = false, bool LAG = false, bool PKQ = true>
 struct X1 {
   static constexpr int KS = KP;
   static constexpr bool WPF = (MODE == 3 || MODE == 4) && !WPD;
@@ -499,6 +508,7 @@ struct X1 {
   uint32_t ws[2];
   int zs[2];
   int32_t ps[2];
+  int ls[2];  // LAG: the tokens' topics in the counts behind q (tok_zlag)
   PhiloxPair rng;
   uint32_t pinc_lo, pinc_hi;  // 2-bit field +1 at the previous token's new topic (pending)
   int znp;                    // that topic (-1: none pending)
@@ -522,6 +532,7 @@ struct X1 {
     const int64_t idx = off + (int64_t)s * 64 + lane;
     const uint32_t w = ws[PAR];
     const int zo = zs[PAR];
+    const int zl = LAG ? ls[PAR] : zo;
     const int32_t pw = ps[PAR];
     // token s+1: its q row into the other register set (copied when the word repeats)
     if (ws[NX] != oni::kPadWord) {
@@ -536,6 +547,7 @@ struct X1 {
     if constexpr (LOAD) {
       ws[PAR] = a.tok_word[idx + 128];
       zs[PAR] = (int)a.tok_z[idx + 128];
+      if constexpr (LAG) ls[PAR] = (int)a.tok_zlag[idx + 128];
       if constexpr (WPF) ps[PAR] = a.wpos[idx + 128];
     } else {
       ws[PAR] = oni::kPadWord;
@@ -553,13 +565,27 @@ struct X1 {
       if (znp == zo) mlo = mhi = 0u;
       add_fields(mlo, mhi);
     }
-    const float2 ab = qfx[zo];
+    const float2 ab = qfx[zl];
     float P[KP];
     float run = 0.f;
+    // q' = fma(q_j, A, −B) of every slot on topic pairs (v_pk_fma_f32), then the select
+    using f2 = float __attribute__((ext_vector_type(2)));
+    const f2 A2 = {ab.x, ab.x}, B2 = {-ab.y, -ab.y};
+    float qx[KP];
+    if constexpr (PKQ) {
+#pragma unroll
+      for (int j = 0; j < KP; j += 2) {
+        const f2 e = __builtin_elementwise_fma(f2{qc[j], qc[j + 1]}, A2, B2);
+        qx[j] = j == zl ? e.x : qc[j];
+        qx[j + 1] = j + 1 == zl ? e.y : qc[j + 1];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < KP; ++j) qx[j] = j == zl ? fmaf(qc[j], ab.x, -ab.y) : qc[j];
+    }
 #pragma unroll
     for (int j = 0; j < KP; ++j) {
-      const float qj = j == zo ? fmaf(qc[j], ab.x, -ab.y) : qc[j];
-      run = fmaf(AIR ? r[j] : r[j] + a.alpha, qj, run);
+      run = fmaf(AIR ? r[j] : r[j] + a.alpha, qx[j], run);
       P[j] = run;
     }
     const float thr = oni::u01(rr) * run;
@@ -584,6 +610,9 @@ struct X1 {
       pinc_hi = sh >= 32u ? (1u << (sh - 32u)) : 0u;
       znp = zn;
     }
+    if constexpr (LAG) {
+      if (zl != zo) a.tok_zlag[idx] = (uint8_t)zo;
+    }
     const bool changed = zn != zo;
     if (changed) {
       ++nchg;
@@ -603,7 +632,7 @@ struct X1 {
 
 // 4 waves per SIMD up to KP = 24 (≤ 128 VGPRs: 3 rows of KP plus the weights); wider rows take
 // what they need (a forced 4-wave budget spills at KP = 32)
-template <int KP, int MODE, bool AIR, bool WPD = false, bool ALN = false>
+template <int KP, int MODE, bool AIR, bool WPD = false, bool ALN = false, bool LAG = false, bool PKQ = true>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KP <= 24 ? 4 : 1, 8))) void k_gibbs_x1(
     const OniGibbs a) {
   static_assert(KP <= 32 && KP % 4 == 0, "one-lane units hold at most 32 topics");
@@ -612,7 +641,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KP <= 24
   if (threadIdx.x < KP) qfx[threadIdx.x] = make_float2(a.qfix[threadIdx.x], a.qfix[KP + threadIdx.x]);
   __syncthreads();
 
-  using XT = X1<KP, MODE, AIR, WPD, ALN>;
+  using XT = X1<KP, MODE, AIR, WPD, ALN, LAG, PKQ>;
   XT x(a, qfx);
   const int wave = threadIdx.x >> 6;
   x.lane = threadIdx.x & 63;
@@ -644,6 +673,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KP <= 24
   for (int t = 0; t < 2; ++t) {
     x.ws[t] = len > t ? a.tok_word[off + t * 64 + c] : oni::kPadWord;
     x.zs[t] = len > t ? (int)a.tok_z[off + t * 64 + c] : 0;
+    x.ls[t] = (LAG && len > t) ? (int)a.tok_zlag[off + t * 64 + c] : 0;
     x.ps[t] = (XT::WPF && len > t) ? a.wpos[off + t * 64 + c] : 0;
   }
   float qa[KP], qb[KP];
@@ -753,7 +783,7 @@ __device__ __forceinline__ uint32_t unit_word(const oni::U4& r, int s, int off) 
   }
 }
 
-template <int G, int KP, int MODE, bool ALN = false>
+template <int G, int KP, int MODE, bool ALN = false, bool LAG = false>
 struct LG {
   static constexpr int S = oni::kWave / G;
   static constexpr int KS = G * KP;
@@ -768,6 +798,7 @@ struct LG {
   uint32_t ws[2];  // parity slots with static roles, as in X1
   int zs[2];
   int32_t ps[2];
+  int ls[2];  // LAG: the tokens' topics in the counts behind q (tok_zlag)
   float qzs[2];
   uint32_t pos0, key, sweep, gbase;
   oni::U4 r;
@@ -784,16 +815,18 @@ struct LG {
     const int64_t idx = off + (int64_t)s * S + c;
     const uint32_t w = ws[PAR];
     const int zo = zs[PAR];
+    const int zl = LAG ? ls[PAR] : zo;
     const int32_t pw = ps[PAR];
     const float qz = qzs[PAR];
     if (ws[NX] != oni::kPadWord) {
       const float* qr = a.q + (int64_t)ws[NX] * KS;
       load_row_f<KP>(qr + kbase, qn);
-      qzs[NX] = qr[zs[NX]];
+      qzs[NX] = qr[LAG ? ls[NX] : zs[NX]];
     }
     if constexpr (LOAD) {
       ws[PAR] = a.tok_word[idx + 2 * S];
       zs[PAR] = (int)a.tok_z[idx + 2 * S];
+      if constexpr (LAG) ls[PAR] = (int)a.tok_zlag[idx + 2 * S];
       if constexpr (WPF) ps[PAR] = a.wpos[idx + 2 * S];
     } else {
       ws[PAR] = oni::kPadWord;
@@ -814,11 +847,18 @@ struct LG {
       rr = (uint32_t)__shfl((int)oni::pick4(r, pos & 3u), (int)(gi - gbase), G);
     }
     const unsigned zlo = (unsigned)(zo - kbase);
-    const float2 ab = qfx[zo];
+    const unsigned zll = LAG ? (unsigned)(zl - kbase) : zlo;
+    const float2 ab = qfx[zl];
     const float qe = fmaf(qz, ab.x, -ab.y);
     const float f = qe / qz;
     float tz = 0.f;
-    if (zlo < (unsigned)KP) {
+    if constexpr (LAG) {
+      if (zlo < (unsigned)KP) rowf[zlo] -= 1.0f;  // n^¬t + α (doc side, at the sweep-start topic)
+      if (zll < (unsigned)KP) {
+        tz = rowf[zll];
+        rowf[zll] = tz * f;    // e_zl for this step only (word-side exclusion at the lagged topic)
+      }
+    } else if (zlo < (unsigned)KP) {
       tz = rowf[zlo] - 1.0f;   // n^¬t + α
       rowf[zlo] = tz * f;      // e_zo for this step only
     }
@@ -836,7 +876,7 @@ struct LG {
       run = fmaf(av.w, qc[4 * j + 3], run);
       P[4 * j + 3] = run;
     }
-    if (zlo < (unsigned)KP) rowf[zlo] = tz;
+    if (zll < (unsigned)KP) rowf[zll] = tz;
     const float incl = group_scan_dpp<G>(run, g);
     float excl = dpp_row_shr<1>(incl);
     if (g == 0) excl = 0.f;
@@ -851,6 +891,9 @@ struct LG {
       ++nchg;
       pend.note(idx, zo, zn, pw, w);
     }
+    if constexpr (LAG) {
+      if (g == 0 && zl != zo) a.tok_zlag[idx] = (uint8_t)zo;
+    }
     if constexpr (MODE == 2) {
       const uint64_t m = __ballot(changed);
       if (lane == 0) {
@@ -861,7 +904,7 @@ struct LG {
   }
 };
 
-template <int G, int KP, int MODE, int OCC = 1, bool ALN = false>
+template <int G, int KP, int MODE, int OCC = 1, bool ALN = false, bool LAG = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void k_gibbs_ldsg(const OniGibbs a) {
   static_assert(G > 1, "G = 1 uses k_gibbs_x1");
   constexpr int S = oni::kWave / G;
@@ -871,7 +914,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OCC, 8))
   __shared__ int32_t red[kWavesPerBlock][KS];
   __shared__ float2 qfx[KS];
   for (int k = threadIdx.x; k < KS; k += kBlock) qfx[k] = make_float2(a.qfix[k], a.qfix[KS + k]);
-  LG<G, KP, MODE, ALN> x(a, qfx);
+  LG<G, KP, MODE, ALN, LAG> x(a, qfx);
   const int wave = threadIdx.x >> 6;
   x.lane = threadIdx.x & 63;
   x.c = x.lane / G;
@@ -908,14 +951,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OCC, 8))
   // kRefresh = 4G - 3 steps each unit recomputes the G blocks that cover its next kRefresh tokens.
   x.gbase = x.pos0 >> 2;
   x.r = oni::philox10(oni::U4{x.gbase + (uint32_t)g, x.key, x.sweep, 1u}, a.seed0, a.seed1);
-  x.next_refresh = LG<G, KP, MODE, ALN>::kRefresh;
+  x.next_refresh = LG<G, KP, MODE, ALN, LAG>::kRefresh;
   x.nchg = 0;
-  constexpr bool WPF = LG<G, KP, MODE, ALN>::WPF;
+  constexpr bool WPF = LG<G, KP, MODE, ALN, LAG>::WPF;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     x.ws[t] = len > t ? a.tok_word[off + t * S + c] : oni::kPadWord;
     x.zs[t] = len > t ? (int)a.tok_z[off + t * S + c] : 0;
     x.ps[t] = (WPF && len > t) ? a.wpos[off + t * S + c] : 0;
+    x.ls[t] = (LAG && len > t) ? (int)a.tok_zlag[off + t * S + c] : 0;
     x.qzs[t] = 0.f;
   }
   float qa[KP], qb[KP];
@@ -924,7 +968,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OCC, 8))
   if (x.ws[0] != oni::kPadWord) {
     const float* qr = a.q + (int64_t)x.ws[0] * KS;
     load_row_f<KP>(qr + kbase, qa);
-    x.qzs[0] = qr[x.zs[0]];
+    x.qzs[0] = qr[LAG ? x.ls[0] : x.zs[0]];
   }
   int s = 0;
   for (; s + 3 < len; s += 2) {
@@ -962,9 +1006,36 @@ int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s)
   }
   if (a.qfix == nullptr) return (int)hipErrorInvalidValue;
   const bool air = (a.flags & 1) != 0;
-  if constexpr (G == 1) {
+  if (a.tok_zlag != nullptr) {
+    // lagged word side: the specialised kernels on the default paths (aligned chunks, recount /
+    // wdelta), the generic kernel (which reads tok_zlag at run time) for anything else
+    if constexpr (G == 1) {
+      if (qpf == 3 && KP <= 32 && air && (a.flags & 16) && !(a.flags & 2) && (mode == 0 || mode == 4)) {
+        if (mode == 0) k_gibbs_x1<KP, 0, true, false, true, true><<<grid, kBlock, 0, s>>>(a);
+        else k_gibbs_x1<KP, 4, true, false, true, true><<<grid, kBlock, 0, s>>>(a);
+        return (int)hipGetLastError();
+      }
+    } else {
+      if (qpf == 2 && air && (a.flags & 16) && (G == 2 || G == 4) && (mode == 0 || mode == 4)) {
+        if (mode == 0) k_gibbs_ldsg<G, KP, 0, 1, true, true><<<grid, kBlock, 0, s>>>(a);
+        else k_gibbs_ldsg<G, KP, 4, 1, true, true><<<grid, kBlock, 0, s>>>(a);
+        return (int)hipGetLastError();
+      }
+      if (qpf == 2 && air && (mode == 0 || mode == 4)) {
+        if (mode == 0) k_gibbs_ldsg<G, KP, 0, 1, false, true><<<grid, kBlock, 0, s>>>(a);
+        else k_gibbs_ldsg<G, KP, 4, 1, false, true><<<grid, kBlock, 0, s>>>(a);
+        return (int)hipGetLastError();
+      }
+    }
+  } else if constexpr (G == 1) {
     if (qpf == 3 && KP <= 32 && air && (a.flags & 16) && !(a.flags & 2) && (mode == 0 || mode == 4)) {
-      // every chunk starts at a multiple of 4 tokens (the default day's path: recount / wdelta)
+      // every chunk starts at a multiple of 4 tokens (the default day's path: recount / wdelta);
+      // flags bit 5 (ONI_SAMPLER_AB & 4): A/B of the scalar q' fma against the packed one
+      if (a.flags & 32) {
+        if (mode == 0) k_gibbs_x1<KP, 0, true, false, true, false, false><<<grid, kBlock, 0, s>>>(a);
+        else k_gibbs_x1<KP, 4, true, false, true, false, false><<<grid, kBlock, 0, s>>>(a);
+        return (int)hipGetLastError();
+      }
       if (mode == 0) k_gibbs_x1<KP, 0, true, false, true><<<grid, kBlock, 0, s>>>(a);
       else k_gibbs_x1<KP, 4, true, false, true><<<grid, kBlock, 0, s>>>(a);
       return (int)hipGetLastError();

@@ -56,8 +56,16 @@ def sampler_for(K: int, sampler: str | None = None) -> str:
     The corpus must be built for its tiling (:func:`tiling_for`)."""
     s = sampler if sampler is not None else os.environ.get("ONI_SAMPLER", "auto")
     if s == "auto":
-        return "mh" if K >= MH_AUTO_MIN_K else "dense"
+        # the lagged X01 (ONI_X01_LAG) runs the dense samplers only
+        return "mh" if K >= MH_AUTO_MIN_K and not x01_lag_on() else "dense"
     return s
+
+
+def x01_lag_on() -> bool:
+    """ONI_X01_LAG=1: the X01 all-reduce of sweep s runs on a side stream during sweep s + 1
+    (GibbsLDA._x01_start): every sweep samples its word side against the global counts one sweep
+    older than its doc rows -- the same rule on any number of GPUs."""
+    return os.environ.get("ONI_X01_LAG", "0") == "1"
 
 
 def mh_burn_for(sweeps: int) -> int:
@@ -125,6 +133,8 @@ class GibbsConfig:
     # initial topics: "random" (Philox stream 0 per token) or "word" (every token of a word in the
     # word's hashed topic, independent of the seed: chains of different seeds start together)
     init: str = field(default_factory=lambda: os.environ.get("ONI_INIT", "random"))
+    # lagged X01 (ONI_X01_LAG, x01_lag_on): the sweep's Δ all-reduce overlaps the next sweep
+    x01_lag: bool = field(default_factory=x01_lag_on)
 
     def resolved_alpha(self) -> float:
         return float(self.alpha) if self.alpha is not None else 50.0 / self.K
@@ -152,6 +162,25 @@ def _capture_stream(device) -> "torch.cuda.Stream":
     if key not in _CAPTURE_STREAMS:
         _CAPTURE_STREAMS[key] = torch.cuda.Stream(device)
     return _CAPTURE_STREAMS[key]
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+_X01_STREAMS: dict = {}
+
+
+def _x01_stream(device) -> "torch.cuda.Stream":
+    """The side stream the lagged X01 (pack → all-reduce → unpack) runs on, one per device."""
+    key = str(device)
+    if key not in _X01_STREAMS:
+        _X01_STREAMS[key] = torch.cuda.Stream(device)
+    return _X01_STREAMS[key]
 
 
 class GibbsLDA:
@@ -258,6 +287,26 @@ class GibbsLDA:
         self.chain = {"sampler": "mh" if self.mh else "dense", "mh_burn": 0}
         if self.mh:
             self.chain["mh_word"] = self.mh_word
+        # lagged X01 (cfg.x01_lag): the word side of sweep s samples against the global counts
+        # through sweep s − 2 (one sweep behind the doc rows) while Δ_{s−1} is reduced on a side
+        # stream. tok_zlag = each token's topic in those counts (the word-side exclusion is taken
+        # there, spec.gibbs_pass); x01_red = the reduced Δ of the previous sweep that the sweep's
+        # apply adds; its count mode decides absolute / delta (_pend_abs). Every sweep() call
+        # ends in a drain (_lag_drain): the counts are current between calls.
+        self.lag = bool(cfg.x01_lag)
+        if self.lag:
+            if self.mh:
+                raise ValueError("the lagged X01 (ONI_X01_LAG) runs the dense samplers only")
+            self.chain["x01_lag"] = 1
+            self.tok_zlag = torch.empty_like(self.tok_z)
+        self._pend_abs = False
+        self._lag_base = 0
+        # the lag starts with the auto count mode's switch to delta bookkeeping (few tokens still
+        # change topic, so one sweep of staleness costs the chain little; from a random start it
+        # slows the burn-in: profiles/r6/x01_lag/) -- or at sweep ONI_X01_LAG_FROM
+        self._lag_live = False
+        lf = os.environ.get("ONI_X01_LAG_FROM", "auto")
+        self._lag_from = None if lf == "auto" else int(lf)
         self.a = 0  # ndk parity
         self.b = 0  # delta-buffer parity
         self.cn = 0  # nk parity
@@ -275,11 +324,14 @@ class GibbsLDA:
         self._x01 = None
         if comm is not None and comm.dist and self.KS % 2 == 0 and self._x01_wanted():
             self._setup_x01()
+        if self.lag:
+            self.x01_red = torch.zeros_like(self.dn[0])
         # one rank (no process group, or a 1-rank group whose all-reduce is the identity): the count
         # passes add Δn_wk straight into n_wk and k_apply refreshes q from it (2 of its 5 passes
         # over V·KS fewer); ONI_APPLY_INPLACE=0 keeps the Δ buffer
         self._inplace_ok = ((comm is None or not comm.live and self._x01 is None)
-                            and self._split is None and os.environ.get("ONI_APPLY_INPLACE", "1") != "0")
+                            and self._split is None and not self.lag
+                            and os.environ.get("ONI_APPLY_INPLACE", "1") != "0")
         # chunk starts (doc-local token positions) are multiples of the chunk length L, pieces of
         # split documents included: with L % 4 == 0 every chunk starts a Philox 4-token group
         self._pos_aligned = int(self.c.L) % 4 == 0
@@ -409,6 +461,8 @@ class GibbsLDA:
             d = self.dn[self.b]
             st.update(ndk_src=self.ndk[self.a], ndk_dst=self.ndk[1 - self.a], dnwk=d[:VK].view(self.V, self.KS),
                       dnk=d[VK:self._aux_off], chg_count=d[self._aux_off:self._aux_off + 1])
+            if self._lag_live:
+                st["tok_zlag"] = self.tok_zlag
         return st
 
     @traced("oni:lda.initialize")
@@ -495,6 +549,12 @@ class GibbsLDA:
         if not self.auto or self.cfg.auto_switch > 0 or self._delta_on or self._poll_off:
             return
         src = self.dn[1 - self.b][self._aux_off:self._aux_off + 1]
+        sw = self.sweeps_done
+        if self._lag_live:
+            # the last sweep's count is still in flight: the reduced one of the sweep before
+            src, sw = self.x01_red[self._aux_off:self._aux_off + 1], self.sweeps_done - 1
+            if sw <= self._lag_base:
+                return
         if self.device.type == "cuda":
             from ..io import staging
             buf = torch.empty(1, dtype=torch.int32, pin_memory=True)
@@ -503,7 +563,7 @@ class GibbsLDA:
             ev.record()
         else:
             buf, ev = src.clone(), None
-        self._chg_q.append((self.sweeps_done, buf, ev))
+        self._chg_q.append((sw, buf, ev))
 
     def _decide_mode(self) -> None:
         """At even sweep counts, consume counts of sweeps ≤ now-2 (deterministic on every rank)."""
@@ -561,6 +621,12 @@ class GibbsLDA:
         self.cn = 1 - self.cn
         self.sweep_ctr.fill_(self.sweeps_done + 1)
         self._last_inplace = False  # dn[0] zeroed here, dn[1] by the apply
+        if self.lag:
+            # the counts are current: the next sweep's word side counts every token at tok_z, and
+            # the Δ it reduces first (dn[1 - b], zeroed) adds nothing
+            self.tok_zlag.copy_(self.tok_z)
+            self._pend_abs = False
+            self._lag_base = self.sweeps_done
         _ = VK
 
     # ---------------------------------------------------------------------------------------------
@@ -583,6 +649,7 @@ class GibbsLDA:
         if self.mh:
             self.mh_build_tables()
             st.update(self.mh_state())
+        side = self._x01_start(self.dn[1 - self.b]) if self._lag_live else None
         ops.gibbs_pass(st, self.G, self.KP, self.K, self.alpha, self.cfg.seed, False,
                        self.sweep_ctr, c.chunk_len, host_sweep=self.sweeps_done + 1, mode=mode, sampler=self.qpf,
                        chg_mask=self.wbits if mode == 4 else getattr(self, "chg_mask", None), wpos=c.wpos,
@@ -604,7 +671,11 @@ class GibbsLDA:
                               head, self.KS, self.G)
         if self._split is not None:
             self._split_delta(self.dn[self.b], self.ndk[self.a], self.ndk[1 - self.a])
-        if self.comm is not None and self.comm.dist:
+        if self._lag_live:
+            if self._split is not None:
+                # split documents' Δn_dk rows stay synchronous (their rows are doc side)
+                self.comm.allreduce_(self.dn[self.b][self._split_off:])
+        elif self.comm is not None and self.comm.dist:
             self._allreduce_dn(self.dn[self.b])
         if self._split is not None:
             self._split_apply(self.dn[self.b], self.ndk[self.a], self.ndk[1 - self.a])
@@ -612,10 +683,20 @@ class GibbsLDA:
         # inside a contiguous averaging window the sample sums gain this sweep's counts in the
         # same launch (int64: no extra pass over n_wk, no separate adds)
         acc = ((self._avg["wk"], self._avg["k"], self._avg["dk"], self.ndk[1 - self.a]) if self._acc else None)
-        ops.gibbs_apply(self.nwk, self.dn[self.b][:so], self.dn[1 - self.b][:so], self.nk[self.cn], self.nk[1 - self.cn],
-                        self.q, self.qfix, self.V, self.K, self.KS, self.beta, self.vbeta, self.sweep_ctr, bump=True,
-                        absolute=mode in (0, 3), rows_copy=(self.ndk[1 - self.a], self.ndk[self.a], c.long_rows),
-                        acc=acc, inplace=inplace)
+        if self._lag_live:
+            # join the side stream; add the previous sweep's reduced Δ (absolute if that sweep
+            # recounted) and zero its buffer, which the next sweep writes
+            self._x01_finish(side)
+            ops.gibbs_apply(self.nwk, self.x01_red[:so], self.dn[1 - self.b][:so], self.nk[self.cn],
+                            self.nk[1 - self.cn], self.q, self.qfix, self.V, self.K, self.KS, self.beta, self.vbeta,
+                            self.sweep_ctr, bump=True, absolute=self._pend_abs,
+                            rows_copy=(self.ndk[1 - self.a], self.ndk[self.a], c.long_rows), acc=acc)
+            self._pend_abs = mode in (0, 3)
+        else:
+            ops.gibbs_apply(self.nwk, self.dn[self.b][:so], self.dn[1 - self.b][:so], self.nk[self.cn],
+                            self.nk[1 - self.cn], self.q, self.qfix, self.V, self.K, self.KS, self.beta, self.vbeta,
+                            self.sweep_ctr, bump=True, absolute=mode in (0, 3),
+                            rows_copy=(self.ndk[1 - self.a], self.ndk[self.a], c.long_rows), acc=acc, inplace=inplace)
         self.a, self.b, self.cn = 1 - self.a, 1 - self.b, 1 - self.cn
         self.sweeps_done += 1
         self._tail_cache = None
@@ -634,6 +715,84 @@ class GibbsLDA:
 
     def _pair_inplace(self, mode: int) -> bool:
         return self._inplace_ok and mode in (1, 2, 4)
+
+    def _lag_due(self, sweep: int, mode: int) -> bool:
+        """Does (1-based) sweep ``sweep`` of count mode ``mode`` run with the lagged X01? The same
+        on every rank: the auto switch is decided from all-reduced change counts."""
+        if not self.lag:
+            return False
+        if self._lag_from is not None:
+            return sweep >= self._lag_from
+        if self.auto:
+            return mode == self.mode and mode != self.early
+        return sweep >= 16
+
+    def _lag_enter(self) -> None:
+        """Start lagging (eager, between sweeps): the counts are current, so the first lagged
+        sweep's word side counts every token at tok_z and the Δ it reduces (the buffer the last
+        synchronous sweep consumed) must add nothing."""
+        self.dn[1 - self.b].zero_()
+        self.tok_zlag.copy_(self.tok_z)
+        self._pend_abs = False
+        self._lag_base = self.sweeps_done
+        self._lag_live = True
+
+    def _x01_start(self, src: torch.Tensor):
+        """Lagged X01, issued at a sweep's start: x01_red := Σ over ranks of ``src`` (the previous
+        sweep's Δ buffer, which this sweep does not touch before its apply) -- packed, reduced and
+        unpacked on a side stream while the sampler runs. Returns the stream to join."""
+        so = self._split_off
+        side = None
+        if self.device.type == "cuda":
+            side = _x01_stream(self.device)
+            side.wait_stream(torch.cuda.current_stream(self.device))
+        timed = side is not None and not self._capturing and len(self._ar_events) < 64
+        with (torch.cuda.stream(side) if side is not None else _nullctx()):
+            if timed:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+            x = self._x01
+            if x is not None:
+                ops.x01_pack(src, x["tiny"], x["light"], x["heavy"], self.KS, x["tail_off"], x["tail_len"], x["O8"],
+                             x["O"], x["buf"])
+                self.comm.allreduce_(x["buf"])
+                ops.x01_unpack(x["buf"], x["tiny"], x["light"], x["heavy"], self.KS, x["tail_off"], x["tail_len"],
+                               x["WO8"], x["WO"], self.x01_red)
+            else:
+                self.x01_red[:so].copy_(src[:so])
+                if self.comm is not None:
+                    self.comm.allreduce_(self.x01_red[:so])
+            if timed:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record()
+                self._ar_events.append((e0, e1))
+        if self.comm is not None and self.comm.dist:
+            self.timings["allreduce_calls"] += 1
+        return side
+
+    def _x01_finish(self, side) -> None:
+        if side is not None:
+            torch.cuda.current_stream(self.device).wait_stream(side)
+
+    def _lag_drain(self) -> None:
+        """End of a sweep() call with the lagged X01: reduce and add the last sweep's Δ (no sample
+        is drawn and the sweep counter stays), so n_wk, n_k and q are current again; the next
+        sweep's word side then counts every token at tok_z."""
+        pb = 1 - self.b
+        so = self._split_off
+        side = self._x01_start(self.dn[pb])
+        self._x01_finish(side)
+        ops.gibbs_apply(self.nwk, self.x01_red[:so], self.dn[pb][:so], self.nk[self.cn], self.nk[1 - self.cn], self.q,
+                        self.qfix, self.V, self.K, self.KS, self.beta, self.vbeta, self.sweep_ctr, bump=False,
+                        absolute=self._pend_abs)
+        # n_k back into the current slot: the sweep parities (a, b, cn) keep their relation, so the
+        # captured sweep pairs replay after the drain
+        self.nk[self.cn].copy_(self.nk[1 - self.cn])
+        self.tok_zlag.copy_(self.tok_z)
+        self._pend_abs = False
+        self._lag_base = self.sweeps_done  # the next sweep reduces the zeroed buffer: no count
+        self._tail_cache = None
+        self._avg_cache = None
 
     def _allreduce_dn(self, buf: torch.Tensor) -> None:
         """X01: all-reduce of the sweep's Δ buffer (Δn_wk ‖ Δn_k replicas ‖ aux words).
@@ -708,7 +867,7 @@ class GibbsLDA:
 
     def _capture(self, mode: int):
         """Capture two sweeps of count mode ``mode`` (parities return to their start) into one HIP graph."""
-        saved = (self.a, self.b, self.cn, self.sweeps_done, self._aux_synced)
+        saved = (self.a, self.b, self.cn, self.sweeps_done, self._aux_synced, self._pend_abs)
         self._force_mode = mode
         if mode == self.mode:
             self._aux_synced = True  # the eager aux sync happens before the first replay
@@ -741,10 +900,10 @@ class GibbsLDA:
             if gc_on:
                 gc.enable()
             torch.cuda.current_stream(self.device).wait_stream(s)
-            self.a, self.b, self.cn, self.sweeps_done, self._aux_synced = saved
+            self.a, self.b, self.cn, self.sweeps_done, self._aux_synced, self._pend_abs = saved
             self._force_mode = None
         entry = (g, (self.a, self.b, self.cn))
-        self._graphs[(mode, self._acc)] = entry
+        self._graphs[(mode, self._acc, self._lag_live)] = entry
         return entry
 
     def _capture_agreed(self, mode: int, also: int | None = None):
@@ -811,6 +970,8 @@ class GibbsLDA:
                 n -= seg
                 if not contiguous and self._avg is not None and self.sweeps_done in self._avg_at:
                     self._add_sample()
+            if self._lag_live:
+                self._lag_drain()
         finally:
             if self._watchdog is not None:
                 self._watchdog.disarm()
@@ -890,7 +1051,13 @@ class GibbsLDA:
             self._decide_mode()
             m1 = self._sweep_mode(self.sweeps_done + 1)
             m2 = self._sweep_mode(self.sweeps_done + 2)
-            if not (self._graphable() and n - done >= 2 and m1 == m2):
+            if not self._lag_live and self._lag_due(self.sweeps_done + 1, m1):
+                self._lag_enter()
+            # a lagged pair's first apply adds the previous sweep's Δ: same absoluteness as m1's
+            # (and a pair never straddles the start of the lag)
+            lag_off = self.lag and (self._lag_due(self.sweeps_done + 1, m1) != self._lag_due(self.sweeps_done + 2, m2)
+                                    or (self._lag_live and self._pend_abs != (m1 in (0, 3))))
+            if not (self._graphable() and n - done >= 2 and m1 == m2) or lag_off:
                 self._one_sweep()
                 self._note_changes()
                 done += 1
@@ -899,7 +1066,7 @@ class GibbsLDA:
                 self._sync_aux_z()
             if m1 == 3:
                 self._ensure_zw()
-            entry = self._graphs.get((m1, self._acc))
+            entry = self._graphs.get((m1, self._acc, self._lag_live))
             if entry is not None and entry[1] != (self.a, self.b, self.cn):
                 self._one_sweep()  # realign parities with the captured pair
                 self._note_changes()
@@ -907,8 +1074,8 @@ class GibbsLDA:
                 continue
             if entry is None:
                 # capture the delta pair now too: no capture stall at the switch
-                also = (self.mode if (self.auto and self.cfg.auto_switch == 0 and m1 == self.early
-                                      and (self.mode, self._acc) not in self._graphs) else None)
+                also = (self.mode if (self.auto and self.cfg.auto_switch == 0 and m1 == self.early and not self.lag
+                                      and (self.mode, self._acc, False) not in self._graphs) else None)
                 entry = self._capture_agreed(m1, also)
                 if entry is None:
                     continue  # fell back to eager sweeps (every rank)
@@ -917,6 +1084,8 @@ class GibbsLDA:
             self._graph = entry[0]
             entry[0].replay()
             self._last_inplace = self._pair_inplace(m1)
+            if self._lag_live:
+                self._pend_abs = m1 in (0, 3)
             self.timings["graph_replays"] = self.timings.get("graph_replays", 0) + 1
             self.sweeps_done += 2
             self._aux_synced = self._keeps_aux(m1)

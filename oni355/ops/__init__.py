@@ -409,6 +409,8 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
         if sampler == SAMPLER_MH and not init:
             if G != 1:
                 raise ValueError("the MH sampler runs one-lane units")
+            if st.get("tok_zlag") is not None:
+                raise ValueError("the lagged word side (ONI_X01_LAG) runs the dense samplers only")
             spec.gibbs_pass_mh(npst, KS, K, alpha, s0, s1, sweep_no, chunk_len.numpy(), doc_moves=mh_doc_moves)
         else:
             spec.gibbs_pass(npst, G, KP, K, alpha, s0, s1, init, sweep_no, chunk_len.numpy(), word_init=word_init)
@@ -450,6 +452,12 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
         a.wpos, a.zz_w, a.chg_mask = _lib.ptr(wpos), _lib.ptr(zz_w), _lib.ptr(chg_mask)
     if st.get("chg_count") is not None:
         a.chg_count = _lib.ptr(st["chg_count"])
+    if not init and st.get("tok_zlag") is not None:
+        if sampler == SAMPLER_MH:
+            raise ValueError("the lagged word side (ONI_X01_LAG) runs the dense samplers only")
+        if st["tok_zlag"].numel() != st["tok_z"].numel() or st["tok_zlag"].dtype != torch.uint8:
+            raise ValueError("tok_zlag must be a uint8 SELL array like tok_z")
+        a.tok_zlag = _lib.ptr(st["tok_zlag"])
     a.n_slices, a.K, a.KS, a.alpha, a.seed0, a.seed1 = n_slices, K, KS, float(alpha), s0, s1
     a.nk_rep = nk_rep
     # the caller vouches that n + α is exact in f32 for every doc-topic count of this corpus
@@ -457,8 +465,10 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
     # (k_gibbs_x1), bit 1 = 4-wave register budget (k_gibbs_ldsg)
     # pos_aligned: every chunk starts at a multiple of 4 tokens (chunk length % 4 == 0), so the
     # one-lane sampler picks its Philox word by the uniform step index (bit 4)
-    a.flags = ((1 if alpha_in_row else 0) | (int(os.environ.get("ONI_SAMPLER_AB", "0")) & 3) << 1
-               | (8 if (init and word_init) else 0) | (16 if pos_aligned else 0))
+    ab = int(os.environ.get("ONI_SAMPLER_AB", "0"))
+    # bit 2 of ONI_SAMPLER_AB (flags bit 5): k_gibbs_x1's q' by scalar fma instead of v_pk_fma_f32
+    a.flags = ((1 if alpha_in_row else 0) | (ab & 3) << 1 | (8 if (init and word_init) else 0)
+               | (16 if pos_aligned else 0) | (32 if ab & 4 else 0))
     if sampler == SAMPLER_MH:
         if G != 1:
             raise ValueError("the MH sampler runs one-lane units")

@@ -32,7 +32,7 @@ class OniGibbs(C.Structure):
         ("tok_word", vp), ("tok_z", vp), ("slice_off", vp), ("slice_len", vp),
         ("chunk_doc", vp), ("chunk_pos0", vp), ("chunk_key", vp), ("chunk_multi", vp),
         ("ndk_src", vp), ("ndk_dst", vp), ("q", vp), ("qfix", vp), ("dnwk", vp), ("dnk", vp), ("sweep_ctr", vp), ("chg_mask", vp),
-        ("wpos", vp), ("z_w", vp), ("zz_w", vp), ("chg_count", vp),
+        ("wpos", vp), ("z_w", vp), ("zz_w", vp), ("chg_count", vp), ("tok_zlag", vp),
         ("n_slices", i64), ("K", i32), ("KS", i32), ("alpha", f32), ("seed0", u32), ("seed1", u32),
         ("nk_rep", i32), ("flags", i32),
     ]

@@ -313,6 +313,12 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed0: int, seed
     The draw is the first topic whose running weight exceeds u·total (count of P_j ≤ thr, capped
     at K − 1).
 
+    Lagged word side (``st["tok_zlag"]`` present, ONI_X01_LAG, models/gibbs.py): q and qfix come
+    from the global counts one sweep older than the doc rows, which count every token at its topic
+    of that older sweep, ``zl = tok_zlag`` -- so the word-side exclusion (q' in place of q, or the
+    row scale f) is taken at zl while the doc side still removes the token at zo; the pass then
+    writes tok_zlag := zo (the topics the next sweep's word side will count).
+
     st keys: tok_word u32, tok_z u8, slice_off i64, slice_len i32, chunk_doc i32, chunk_pos0 i32,
     chunk_key u32, chunk_multi u8, ndk_src i32 [D,KS], ndk_dst i32 [D,KS], q f32 [V,KS],
     qfix f32 [2,KS] (sweeps), dnwk i32 [V,KS], dnk i32 [KS].
@@ -327,6 +333,7 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed0: int, seed
     if not init:
         n[live] = st["ndk_src"][doc[live]]
         qfix = st["qfix"]
+    lag = not init and st.get("tok_zlag") is not None
     n_start = n.copy()
     clen = np.where(live, chunk_len, 0)
     alpha32 = F32(alpha)
@@ -349,16 +356,17 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed0: int, seed
             np.add.at(st["dnwk"], (w, z), 1)
             continue
         zo = st["tok_z"][idx].astype(np.int64)
+        zl = st["tok_zlag"][idx].astype(np.int64) if lag else zo
         n[act, zo] -= 1
         qv = st["q"][w].copy()
-        qz = qv[ar, zo]
-        qe = excluded_q(qz, zo, qfix)
+        qz = qv[ar, zl]
+        qe = excluded_q(qz, zl, qfix)
         av = n[act].astype(F32) + alpha32
         if G == 1:
-            qv[ar, zo] = qe
+            qv[ar, zl] = qe
         else:
             f = (qe / qz).astype(F32)
-            av[ar, zo] = (av[ar, zo] * f).astype(F32)
+            av[ar, zl] = (av[ar, zl] * f).astype(F32)
         avg = av.reshape(-1, G, KP)
         qg = qv.reshape(-1, G, KP)
         loc = np.empty_like(avg)
@@ -385,6 +393,8 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed0: int, seed
         zn = np.minimum(cnt, K - 1).astype(np.int64)
         n[act, zn] += 1
         ch = zn != zo
+        if lag:
+            st["tok_zlag"][idx] = zo.astype(np.uint8)
         st["tok_z"][idx[ch]] = zn[ch].astype(np.uint8)
         np.add.at(st["dnwk"], (w[ch], zo[ch]), -1)
         np.add.at(st["dnwk"], (w[ch], zn[ch]), 1)

@@ -19,9 +19,13 @@ Two variants:
   (a day-unique normal word then also scores 0, as it would for any estimator that learns from
   the day) -- what label knowledge alone buys from this day's data. A document with no other
   normal token falls back to the word's day marginal.
+* ``loo_smooth`` -- ``loo`` with LDA's word smoothing, P̂(w | ℓ) = (c(ℓ, w) + β) / (c(ℓ) + Vβ):
+  an LDA whose topic assignments are the true labels, scoring every event as the model trained
+  on all the other events sees it. Day-unique words (planted or not) are then ordered by their
+  documents' label mixtures, as LDA orders them.
 
 LDA sees neither labels nor the true mixtures, so its recall is bounded by ``leave_in`` and
-comparable to ``loo``. Ties count as a random order (:func:`expected_recall`).
+comparable to ``loo_smooth``. Ties count as a random order (:func:`expected_recall`).
 """
 from __future__ import annotations
 
@@ -44,10 +48,10 @@ def _lookup(keys: torch.Tensor, vals: torch.Tensor, q: torch.Tensor) -> torch.Te
 
 
 def label_oracle(doc_keys: list, word_keys: list, labels: np.ndarray, device="cpu",
-                 chunk: int = 1 << 21) -> dict:
+                 chunk: int = 1 << 21, beta: float = 0.01) -> dict:
     """Per-event oracle scores. ``doc_keys[j]`` / ``word_keys[j]``: the document / word key of
     token slot j of every event (int64-convertible arrays or tensors of length n); ``labels``:
-    int [n], -1 for planted rows. Returns {"leave_in": float64 [n], "loo": float64 [n]}."""
+    int [n], -1 for planted rows. Returns {"leave_in", "loo", "loo_smooth": float64 [n]}."""
     dev = torch.device(device)
     S = len(doc_keys)
     n = int(len(labels))
@@ -83,6 +87,10 @@ def label_oracle(doc_keys: list, word_keys: list, labels: np.ndarray, device="cp
     hi = torch.searchsorted(dl_doc, torch.arange(D, device=dev), right=True)
     nlab = hi - lo
     Spair = torch.zeros(pkeys.numel(), dtype=torch.float64, device=dev)
+    Vb = V * beta
+    Sb = torch.zeros_like(Spair)  # Σ_ℓ c(d, ℓ) c(ℓ, w) / (c(ℓ) + Vβ)
+    # R(d) = Σ_ℓ c(d, ℓ) / (c(ℓ) + Vβ): the smoothing mass of a word none of d's labels produced
+    R = torch.zeros(D, dtype=torch.float64, device=dev).index_add_(0, dl_doc, dl_cnt / (c_l[dl_keys % NL] + Vb))
     # expand every pair over its document's labels, in chunks of pairs (bounded memory)
     cum = torch.cumsum(nlab[pd], 0)
     start = 0
@@ -102,6 +110,7 @@ def label_oracle(doc_keys: list, word_keys: list, labels: np.ndarray, device="cp
             cdl = dl_cnt[row]
             clw = _lookup(lw_keys, lw_cnt, l_of * V + pw[pid])
             Spair.index_add_(0, pid, cdl * clw / c_l[l_of])
+            Sb.index_add_(0, pid, cdl * clw / (c_l[l_of] + Vb))
         start = stop
     del pd, pw
     s_tok = Spair[pinv]
@@ -120,8 +129,16 @@ def label_oracle(doc_keys: list, word_keys: list, labels: np.ndarray, device="cp
     marg_loo = (c_w[w] - 1).clamp(min=0) / max(N - 1, 1)
     loo_norm = torch.where(cd > 1, num / (cd - 1).clamp(min=1), marg_loo)
     loo = torch.where(normal, loo_norm, leave_in)
+    # smoothed: planted tokens (not in any count) as they are, normal ones without themselves
+    sb_tok = Sb[pinv] + beta * R[d]
+    sm_in = torch.where(cd > 0, sb_tok / cd.clamp(min=1), (c_w[w] + beta) / (N + Vb))
+    own_b = cdl_own * clw_own / (cl_own + Vb) + beta * cdl_own / (cl_own + Vb)
+    own_b_loo = (cdl_own - 1) * (clw_own - 1 + beta) / (cl_own - 1 + Vb)
+    sm_loo = torch.where(cd > 1, (sb_tok - own_b + own_b_loo) / (cd - 1).clamp(min=1),
+                         (c_w[w] - 1 + beta) / (N - 1 + Vb))
+    loo_smooth = torch.where(normal, sm_loo, sm_in)
     out = {}
-    for name, t in (("leave_in", leave_in), ("loo", loo)):
+    for name, t in (("leave_in", leave_in), ("loo", loo), ("loo_smooth", loo_smooth)):
         ev = t.view(S, n).min(0).values if S > 1 else t.view(n)
         out[name] = ev.clamp(min=0).cpu().numpy()
     return out

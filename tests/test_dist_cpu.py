@@ -260,7 +260,7 @@ def _vote_worker(rank, world, port, n_total, out_q):
         if rank == 1:
             raise RuntimeError("hipErrorStreamCaptureInvalidated (simulated)")
         entry = (_FakeGraph(), (self.a, self.b, self.cn))
-        self._graphs[(mode, self._acc)] = entry
+        self._graphs[(mode, self._acc, self._lag_live)] = entry
         return entry
     GibbsLDA._graphable = lambda self: not getattr(self, "_graph_off", False)
     GibbsLDA._capture = fake_capture

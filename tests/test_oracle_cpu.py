@@ -11,6 +11,22 @@ def _brute(docs, words, labels):
     normal = [t for t in toks if t[2] >= 0]
     allw = [t[1] for t in normal]
 
+    Vall = len({t[1] for t in toks})
+    beta = 0.01
+
+    def ps(d, w, excl=None):
+        pool = [t for t in normal if not (excl is not None and t is excl)]
+        cd = sum(1 for t in pool if t[0] == d)
+        if cd == 0:
+            return (sum(1 for t in pool if t[1] == w) + beta) / (len(pool) + Vall * beta)
+        tot = 0.0
+        for lab in {t[2] for t in pool if t[0] == d}:
+            cdl = sum(1 for t in pool if t[0] == d and t[2] == lab)
+            cl = sum(1 for t in pool if t[2] == lab)
+            clw = sum(1 for t in pool if t[2] == lab and t[1] == w)
+            tot += cdl / cd * (clw + beta) / (cl + Vall * beta)
+        return tot
+
     def p(d, w, excl=None):
         pool = [t for t in normal if t[3] != excl or excl is None] if excl is not None else normal
         pool = [t for t in normal if not (excl is not None and t is excl)]
@@ -27,12 +43,14 @@ def _brute(docs, words, labels):
         return tot
     li = np.zeros(n)
     lo = np.zeros(n)
+    sm = np.zeros(n)
     for e in range(n):
         mine = [t for t in toks if t[3] == e]
         li[e] = min(p(t[0], t[1]) for t in mine)
         lo[e] = min(p(t[0], t[1], excl=t if t[2] >= 0 else None) for t in mine)
+        sm[e] = min(ps(t[0], t[1], excl=t if t[2] >= 0 else None) for t in mine)
     _ = allw
-    return li, lo
+    return li, lo, sm
 
 
 @pytest.mark.parametrize("S", [1, 2])
@@ -45,9 +63,10 @@ def test_label_oracle_matches_brute_force(S):
     labels[r.choice(n, 6, replace=False)] = -1
     docs[0][:2] = 1000  # a document holding a single event
     got = label_oracle(docs, words, labels)
-    li, lo = _brute(docs, words, labels)
+    li, lo, sm = _brute(docs, words, labels)
     np.testing.assert_allclose(got["leave_in"], li, rtol=1e-12, atol=1e-15)
     np.testing.assert_allclose(got["loo"], lo, rtol=1e-12, atol=1e-15)
+    np.testing.assert_allclose(got["loo_smooth"], sm, rtol=1e-10, atol=1e-15)
 
 
 def test_label_oracle_chunked_expansion_is_the_same():
@@ -59,6 +78,7 @@ def test_label_oracle_chunked_expansion_is_the_same():
     b = label_oracle(docs, words, labels, chunk=3)
     np.testing.assert_allclose(a["leave_in"], b["leave_in"], rtol=1e-13)
     np.testing.assert_allclose(a["loo"], b["loo"], rtol=1e-13)
+    np.testing.assert_allclose(a["loo_smooth"], b["loo_smooth"], rtol=1e-13)
 
 
 def test_expected_recall_counts_ties_fractionally():

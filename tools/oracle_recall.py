@@ -109,7 +109,7 @@ def run_case(name, device, sweeps, seed):
     out = {"case": name, "source": src, "events": n, "realistic_vocab": wide, "K": K, "sweeps": sweeps,
            "anomaly_kind": kind or "default", "planted": int(planted.size), "vocab": vocab,
            "lda_recall": lda}
-    for k in ("leave_in", "loo"):
+    for k in ("leave_in", "loo", "loo_smooth"):
         out[f"oracle_{k}_recall"] = {str(t): round(expected_recall(orc[k], planted, t), 4) for t in TOPS}
     # anatomy: planted rows whose (every) word no normal row of the day carries (oracle score 0)
     out["planted_oracle_zero"] = int((orc["leave_in"][planted] == 0).sum())
