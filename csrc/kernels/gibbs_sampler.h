@@ -492,7 +492,7 @@ __device__ __forceinline__ int count_le(const float (&P)[KP], float excl, float 
 // 3-wave register budget (+0.011 ms) all lost.
 // WPD (off: measured 0.255 vs 0.248 ms/sweep): MODE 3/4 changed tokens load their word-sorted
 // slot when they change (exec-masked, ~10 % of lanes) instead of streaming it with every token.
-template <int KP, int MODE, bool AIR, bool WPD, bool ALN = false, bool LAG = false, bool PKQ = true>
+template <int KP, int MODE, bool AIR, bool WPD, bool ALN = false, bool LAG = false, bool PKQ = false>
 struct X1 {
   static constexpr int KS = KP;
   static constexpr bool WPF = (MODE == 3 || MODE == 4) && !WPD;
@@ -568,25 +568,26 @@ struct X1 {
     const float2 ab = qfx[zl];
     float P[KP];
     float run = 0.f;
-    // q' = fma(q_j, A, −B) of every slot on topic pairs (v_pk_fma_f32), then the select
-    using f2 = float __attribute__((ext_vector_type(2)));
-    const f2 A2 = {ab.x, ab.x}, B2 = {-ab.y, -ab.y};
-    float qx[KP];
     if constexpr (PKQ) {
+      // q' = fma(q_j, A, −B) on topic pairs (v_pk_fma_f32) inside the chain, so only the pair in
+      // flight is live (materialising all KP q' values first spilled at the 4-wave budget)
+      using f2 = float __attribute__((ext_vector_type(2)));
+      const f2 A2 = {ab.x, ab.x}, B2 = {-ab.y, -ab.y};
 #pragma unroll
       for (int j = 0; j < KP; j += 2) {
         const f2 e = __builtin_elementwise_fma(f2{qc[j], qc[j + 1]}, A2, B2);
-        qx[j] = j == zl ? e.x : qc[j];
-        qx[j + 1] = j + 1 == zl ? e.y : qc[j + 1];
+        run = fmaf(AIR ? r[j] : r[j] + a.alpha, j == zl ? e.x : qc[j], run);
+        P[j] = run;
+        run = fmaf(AIR ? r[j + 1] : r[j + 1] + a.alpha, j + 1 == zl ? e.y : qc[j + 1], run);
+        P[j + 1] = run;
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < KP; ++j) qx[j] = j == zl ? fmaf(qc[j], ab.x, -ab.y) : qc[j];
-    }
-#pragma unroll
-    for (int j = 0; j < KP; ++j) {
-      run = fmaf(AIR ? r[j] : r[j] + a.alpha, qx[j], run);
-      P[j] = run;
+      for (int j = 0; j < KP; ++j) {
+        const float qj = j == zl ? fmaf(qc[j], ab.x, -ab.y) : qc[j];
+        run = fmaf(AIR ? r[j] : r[j] + a.alpha, qj, run);
+        P[j] = run;
+      }
     }
     const float thr = oni::u01(rr) * run;
     int cnt = 0;
@@ -632,8 +633,9 @@ struct X1 {
 
 // 4 waves per SIMD up to KP = 24 (≤ 128 VGPRs: 3 rows of KP plus the weights); wider rows take
 // what they need (a forced 4-wave budget spills at KP = 32)
-template <int KP, int MODE, bool AIR, bool WPD = false, bool ALN = false, bool LAG = false, bool PKQ = true>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KP <= 24 ? 4 : 1, 8))) void k_gibbs_x1(
+// LAG streams one more topic per token: 3 waves per SIMD (≤ 168 VGPRs) -- at the 4-wave budget it spilled
+template <int KP, int MODE, bool AIR, bool WPD = false, bool ALN = false, bool LAG = false, bool PKQ = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KP <= 24 ? (LAG ? 3 : 4) : 1, 8))) void k_gibbs_x1(
     const OniGibbs a) {
   static_assert(KP <= 32 && KP % 4 == 0, "one-lane units hold at most 32 topics");
   __shared__ float2 qfx[KP];
@@ -1030,10 +1032,11 @@ int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s)
   } else if constexpr (G == 1) {
     if (qpf == 3 && KP <= 32 && air && (a.flags & 16) && !(a.flags & 2) && (mode == 0 || mode == 4)) {
       // every chunk starts at a multiple of 4 tokens (the default day's path: recount / wdelta);
-      // flags bit 5 (ONI_SAMPLER_AB & 4): A/B of the scalar q' fma against the packed one
+      // flags bit 5 (ONI_SAMPLER_AB & 4): A/B of the packed q' (v_pk_fma_f32) against the scalar
+      // one -- 30 fewer VALU per two steps, 3.5 % slower per sweep (profiles/r6/packed_fp32/)
       if (a.flags & 32) {
-        if (mode == 0) k_gibbs_x1<KP, 0, true, false, true, false, false><<<grid, kBlock, 0, s>>>(a);
-        else k_gibbs_x1<KP, 4, true, false, true, false, false><<<grid, kBlock, 0, s>>>(a);
+        if (mode == 0) k_gibbs_x1<KP, 0, true, false, true, false, true><<<grid, kBlock, 0, s>>>(a);
+        else k_gibbs_x1<KP, 4, true, false, true, false, true><<<grid, kBlock, 0, s>>>(a);
         return (int)hipGetLastError();
       }
       if (mode == 0) k_gibbs_x1<KP, 0, true, false, true><<<grid, kBlock, 0, s>>>(a);

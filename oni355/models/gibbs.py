@@ -164,25 +164,6 @@ def _capture_stream(device) -> "torch.cuda.Stream":
     return _CAPTURE_STREAMS[key]
 
 
-class _nullctx:
-    def __enter__(self):
-        return self
-
-    def __exit__(self, *exc):
-        return False
-
-
-_X01_STREAMS: dict = {}
-
-
-def _x01_stream(device) -> "torch.cuda.Stream":
-    """The side stream the lagged X01 (pack → all-reduce → unpack) runs on, one per device."""
-    key = str(device)
-    if key not in _X01_STREAMS:
-        _X01_STREAMS[key] = torch.cuda.Stream(device)
-    return _X01_STREAMS[key]
-
-
 class GibbsLDA:
     """Device state + sweep loop. ``comm`` (oni355.parallel.comm.Comm) enables data parallelism."""
 
@@ -739,40 +720,33 @@ class GibbsLDA:
 
     def _x01_start(self, src: torch.Tensor):
         """Lagged X01, issued at a sweep's start: x01_red := Σ over ranks of ``src`` (the previous
-        sweep's Δ buffer, which this sweep does not touch before its apply) -- packed, reduced and
-        unpacked on a side stream while the sampler runs. Returns the stream to join."""
+        sweep's Δ buffer, untouched by this sweep before its apply). The pack (or a copy: the apply
+        cannot read and zero one buffer) runs on the compute stream; the collective is issued
+        asynchronously, so RCCL runs it on its own stream while this sweep's sampler runs, and
+        :meth:`_x01_finish` joins it before the apply -- inside the captured sweep graph too."""
         so = self._split_off
-        side = None
-        if self.device.type == "cuda":
-            side = _x01_stream(self.device)
-            side.wait_stream(torch.cuda.current_stream(self.device))
-        timed = side is not None and not self._capturing and len(self._ar_events) < 64
-        with (torch.cuda.stream(side) if side is not None else _nullctx()):
-            if timed:
-                e0 = torch.cuda.Event(enable_timing=True)
-                e0.record()
-            x = self._x01
-            if x is not None:
-                ops.x01_pack(src, x["tiny"], x["light"], x["heavy"], self.KS, x["tail_off"], x["tail_len"], x["O8"],
-                             x["O"], x["buf"])
-                self.comm.allreduce_(x["buf"])
-                ops.x01_unpack(x["buf"], x["tiny"], x["light"], x["heavy"], self.KS, x["tail_off"], x["tail_len"],
-                               x["WO8"], x["WO"], self.x01_red)
-            else:
-                self.x01_red[:so].copy_(src[:so])
-                if self.comm is not None:
-                    self.comm.allreduce_(self.x01_red[:so])
-            if timed:
-                e1 = torch.cuda.Event(enable_timing=True)
-                e1.record()
-                self._ar_events.append((e0, e1))
+        x = self._x01
+        if x is not None:
+            ops.x01_pack(src, x["tiny"], x["light"], x["heavy"], self.KS, x["tail_off"], x["tail_len"], x["O8"],
+                         x["O"], x["buf"])
+            buf = x["buf"]
+        else:
+            self.x01_red[:so].copy_(src[:so])
+            buf = self.x01_red[:so]
+        # (no timing events: issue → join spans the sampler; allreduce_ms_per_sweep probes the
+        # payload's collective on its own instead)
+        h = self.comm.allreduce_async_(buf) if self.comm is not None else None
         if self.comm is not None and self.comm.dist:
             self.timings["allreduce_calls"] += 1
-        return side
+        return h
 
-    def _x01_finish(self, side) -> None:
-        if side is not None:
-            torch.cuda.current_stream(self.device).wait_stream(side)
+    def _x01_finish(self, h) -> None:
+        if h is not None:
+            h.wait()
+        x = self._x01
+        if x is not None:
+            ops.x01_unpack(x["buf"], x["tiny"], x["light"], x["heavy"], self.KS, x["tail_off"], x["tail_len"],
+                           x["WO8"], x["WO"], self.x01_red)
 
     def _lag_drain(self) -> None:
         """End of a sweep() call with the lagged X01: reduce and add the last sweep's Δ (no sample
@@ -862,7 +836,11 @@ class GibbsLDA:
         if self.comm is None or not self.comm.dist:
             return True
         # RCCL collectives are captured into the sweep graph (the communicator exists: initialize()
-        # already all-reduced n_wk); gloo routes through host copies and cannot be captured
+        # already all-reduced n_wk); gloo routes through host copies and cannot be captured.
+        # Lagged sweeps with live collectives run eagerly: capturing the deferred join of an async
+        # RCCL collective crashed in capture_end (hipGraph, ROCm 7.0 RCCL 2.26; tools/lag_real_probe.py)
+        if self._lag_live and self.comm.live:
+            return False
         return self.comm.graph_capturable() and os.environ.get("ONI_DIST_GRAPH", "1") != "0"
 
     def _capture(self, mode: int):

@@ -23,6 +23,18 @@ import torch
 import torch.distributed as dist
 
 
+class _Pending:
+    """An issued async collective: ``wait()`` joins it to the current stream, then runs ``after``."""
+
+    def __init__(self, work, after):
+        self.work, self.after = work, after
+
+    def wait(self) -> None:
+        self.work.wait()
+        if self.after is not None:
+            self.after()
+
+
 class Comm:
     def __init__(self, rank: int = 0, world: int = 1, device: torch.device | None = None, group=None,
                  forced: bool = False, backend: str | None = None):
@@ -64,6 +76,30 @@ class Comm:
                 dist.all_reduce(t, op=rop, group=self.group)
         return t
 
+    def allreduce_async_(self, t: torch.Tensor):
+        """Start a SUM all-reduce of ``t`` in place; returns a handle whose ``wait()`` makes the
+        current stream wait for it (RCCL: the process group's own stream runs the collective after
+        the work already queued on the current stream, so kernels queued between this call and
+        ``wait()`` overlap it -- also inside a HIP graph capture; gloo: wait() blocks). None when
+        no collective runs (``wait`` on None: nothing to do)."""
+        if not self.live:
+            return None
+        if self._one_rank_rccl():
+            out = self._a2a_scratch(t)
+            work = dist.all_to_all_single(out, t.reshape(-1), group=self.group, async_op=True)
+            return _Pending(work, lambda: t.copy_(out.view(t.shape)))
+        if self._via_host and t.is_cuda:
+            self.allreduce_(t)  # through host copies: synchronous
+            return None
+        return _Pending(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True), None)
+
+    def _a2a_scratch(self, t: torch.Tensor) -> torch.Tensor:
+        key = (t.numel(), t.dtype)
+        cache = self.__dict__.setdefault("_a2a_scratch_bufs", {})
+        if key not in cache:
+            cache[key] = torch.empty(t.numel(), dtype=t.dtype, device=t.device)
+        return cache[key]
+
     def _rop(self, op: str):
         return {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
 
@@ -77,11 +113,7 @@ class Comm:
         return self.real and self.backend == "nccl" and self.device.type == "cuda" and not self._via_host
 
     def _reduce_one_rank(self, t: torch.Tensor) -> torch.Tensor:
-        key = (t.numel(), t.dtype)
-        cache = self.__dict__.setdefault("_a2a_scratch", {})
-        if key not in cache:
-            cache[key] = torch.empty(t.numel(), dtype=t.dtype, device=t.device)
-        out = cache[key]
+        out = self._a2a_scratch(t)
         dist.all_to_all_single(out, t.reshape(-1), group=self.group)
         t.copy_(out.view(t.shape))
         return t
