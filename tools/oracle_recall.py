@@ -79,14 +79,56 @@ def _tokens(src, day, device):
     return [docs], [words.to(torch.int64)]
 
 
-def run_case(name, device, sweeps, seed):
+def _anatomy(day, rows, planted, docs, words, orc, src, top=3000):
+    """What fills the LDA top-N: label kind of each row (planted / behaviour profile / long-tail
+    behaviour), how often its rarest word occurs among the day's tokens, its documents' sizes;
+    and where the missed planted rows and the top-N normal rows sit in the smoothed oracle."""
+    import torch
+    lab = np.asarray(day.labels)
+    P = 20 if src == "flow" else None
+    n = lab.size
+    wk = torch.cat([w.reshape(-1).cpu() for w in words])
+    dk = torch.cat([d.reshape(-1).cpu() for d in docs])
+    _, winv, wcnt = torch.unique(wk, return_inverse=True, return_counts=True)
+    _, dinv, dcnt = torch.unique(dk, return_inverse=True, return_counts=True)
+    S = len(words)
+    wc = wcnt[winv].view(S, n).min(0).values.numpy()   # the event's rarest word's day count
+    dc = dcnt[dinv].view(S, n).min(0).values.numpy()   # its smaller document
+    head = rows[:top]
+    normal = head[lab[head] >= 0]
+    kinds = {"planted": int((lab[head] < 0).sum())}
+    if P is not None:
+        kinds["profile"] = int(((lab[normal] >= 0) & (lab[normal] < P)).sum())
+        kinds["long_tail"] = int((lab[normal] >= P).sum())
+    sm = orc["loo_smooth"]
+    order = np.argsort(sm, kind="stable")
+    srank = np.empty(n, np.int64)
+    srank[order] = np.arange(n)
+    missed = planted[~np.isin(planted, head)]
+    q = lambda a: [int(x) for x in np.percentile(a, [10, 50, 90])] if len(a) else None  # noqa: E731
+    return {"top": top, "kinds": kinds,
+            "normal_top_word_count_p10_50_90": q(wc[normal]), "normal_top_doc_tokens_p10_50_90": q(dc[normal]),
+            "normal_top_singleton_words": int((wc[normal] == 1).sum()),
+            "normal_top_smooth_oracle_rank_p10_50_90": q(srank[normal]),
+            "missed_planted": int(missed.size), "missed_word_count_p10_50_90": q(wc[missed]),
+            "missed_doc_tokens_p10_50_90": q(dc[missed]), "missed_lda_rank_p10_50_90":
+            q(np.array([int(np.nonzero(rows == m)[0][0]) if (rows == m).any() else len(rows) for m in missed])),
+            "planted_word_count_p10_50_90": q(wc[planted]), "planted_doc_tokens_p10_50_90": q(dc[planted])}
+
+
+def run_case(name, device, sweeps, seed, K=None, beta=None, alpha=None, anatomy=False):
     import torch
     from oni355.synth.oracle import expected_recall, label_oracle
-    src, n, wide, K, kind, shards = CASES[name]
+    src, n, wide, K0, kind, shards = CASES[name]
+    K = K or K0
     t0 = time.perf_counter()
     day = _day(src, n, wide, kind, shards, seed)
     gen_s = time.perf_counter() - t0
     kw = dict(K=K, sweeps=sweeps, maxresults=max(TOPS), device=device)
+    if beta is not None:
+        kw["beta"] = beta
+    if alpha is not None:
+        kw["alpha"] = alpha
     if src == "flow":
         from oni355.pipeline.flow import run_flow
         res = run_flow(day.cols, **kw)
@@ -107,8 +149,10 @@ def run_case(name, device, sweeps, seed):
     docs, words = _tokens(src, day, device)
     orc = label_oracle(docs, words, day.labels, device=device)
     out = {"case": name, "source": src, "events": n, "realistic_vocab": wide, "K": K, "sweeps": sweeps,
-           "anomaly_kind": kind or "default", "planted": int(planted.size), "vocab": vocab,
-           "lda_recall": lda}
+           "alpha": alpha, "beta": beta, "anomaly_kind": kind or "default", "planted": int(planted.size),
+           "vocab": vocab, "lda_recall": lda}
+    if anatomy:
+        out["anatomy"] = _anatomy(day, rows, planted, docs, words, orc, src)
     for k in ("leave_in", "loo", "loo_smooth"):
         out[f"oracle_{k}_recall"] = {str(t): round(expected_recall(orc[k], planted, t), 4) for t in TOPS}
     # anatomy: planted rows whose (every) word no normal row of the day carries (oracle score 0)
@@ -126,9 +170,13 @@ def main() -> int:
     ap.add_argument("--sweeps", type=int, default=200)
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--topics", type=int, default=None, help="estimator A/B: K instead of the case's")
+    ap.add_argument("--beta", type=float, default=None, help="estimator A/B: β")
+    ap.add_argument("--alpha", type=float, default=None, help="estimator A/B: α (default 50/K)")
+    ap.add_argument("--anatomy", action="store_true", help="describe the LDA top-N rows (label kind, word counts)")
     a = ap.parse_args()
     for name in a.case:
-        r = run_case(name, a.device, a.sweeps, a.seed)
+        r = run_case(name, a.device, a.sweeps, a.seed, K=a.topics, beta=a.beta, alpha=a.alpha, anatomy=a.anatomy)
         line = json.dumps(r)
         print(line, flush=True)
         if a.out:
