@@ -139,6 +139,26 @@ __global__ __launch_bounds__(256) void k_apply(int32_t* __restrict__ nwk, const 
   }
 }
 
+// Exactness guard of the row-f32 samplers (k_gibbs_x1 / k_gibbs_ldsg keep n + α as f32 in their
+// rows): *flag := 1 iff every count of the given rows (the documents long enough to matter) is at
+// most `limit` -- the largest sweep-start count whose chunk can still move it by L without leaving
+// the exactly representable range. One block, before the sweep's sampler (inside its graph).
+__global__ __launch_bounds__(256) void k_exact_guard(const int32_t* __restrict__ ndk, const int32_t* __restrict__ rows,
+                                                     int64_t n_rows, int KS, int K, int32_t limit,
+                                                     int32_t* __restrict__ flag) {
+  __shared__ int bad;
+  if (threadIdx.x == 0) bad = 0;
+  __syncthreads();
+  int b = 0;
+  for (int64_t i = threadIdx.x; i < n_rows * K; i += blockDim.x) {
+    const int64_t r = rows[i / K];
+    b |= ndk[r * KS + (int)(i % K)] > limit;
+  }
+  if (b) atomicOr(&bad, 1);
+  __syncthreads();
+  if (threadIdx.x == 0) *flag = bad ? 0 : 1;
+}
+
 __global__ void k_copy_rows(const int32_t* __restrict__ src, int32_t* __restrict__ dst,
                             const int32_t* __restrict__ rows, int64_t n_rows, int KS) {
   const int64_t total = n_rows * KS;
@@ -473,6 +493,13 @@ ONI_API int oni_gibbs_launch(const OniGibbs* a, int G, int KP, int init, int mod
 }
 
 ONI_API int oni_gibbs_sizeof_args() { return (int)sizeof(OniGibbs); }
+
+ONI_API int oni_exact_guard(const int32_t* ndk, const int32_t* rows, int64_t n_rows, int KS, int K, int32_t limit,
+                            int32_t* flag, hipStream_t s) {
+  if (n_rows < 0 || K < 1 || K > KS || flag == nullptr) return (int)hipErrorInvalidValue;
+  k_exact_guard<<<1, 256, 0, s>>>(ndk, rows, n_rows, KS, K, limit, flag);
+  return (int)hipGetLastError();
+}
 
 // rsrc/rdst/rows/n_rows: optional fused long-row copy for the next sweep (n_rows = 0: none).
 // inplace: Δn_wk was added straight into nwk by the count pass (world 1); only q, n_k, the Δn_k

@@ -58,6 +58,9 @@ struct OniGibbs {
                                 //   (written once with the corpus, 0xFFFF: read wsorted)
                                // (MODE 4 reuses chg_mask as a u32 bitmap over word-sorted positions)
   int32_t* chg_count;          // optional: += number of tokens whose topic changed (drives the auto mode)
+  const int32_t* exact_guard;  // optional device flag (1: every count this sweep's rows can reach keeps
+                               //   n + α exact in f32): the row-f32 kernels run when it is set, the generic
+                               //   kernel (launched beside them) when it is not -- see k_exact_guard
   uint8_t* tok_zlag;           // optional, SELL (ONI_X01_LAG): the topic each token holds in the counts
                                //   behind q (one sweep older than the doc rows): the word-side exclusion
                                //   is taken there; the pass writes tok_zlag := the token's sweep-start topic
@@ -297,6 +300,8 @@ struct Pend {
 // weight of zo by f = q'/q_zo.
 template <int G, int KP, bool INIT, int MODE>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 8))) void k_gibbs(const OniGibbs a) {
+  // flags bit 6: the guarded twin of a row-f32 kernel (launch_gibbs) -- it runs only when they do not
+  if (!INIT && (a.flags & 64) && *a.exact_guard != 0) return;
   constexpr int S = oni::kWave / G;
   constexpr int KS = G * KP;
   __shared__ int32_t red[kWavesPerBlock][KS];
@@ -638,6 +643,7 @@ template <int KP, int MODE, bool AIR, bool WPD = false, bool ALN = false, bool L
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KP <= 24 ? (LAG ? 3 : 4) : 1, 8))) void k_gibbs_x1(
     const OniGibbs a) {
   static_assert(KP <= 32 && KP % 4 == 0, "one-lane units hold at most 32 topics");
+  if (a.exact_guard != nullptr && *a.exact_guard == 0) return;  // a count may leave f32 exactness: generic
   __shared__ float2 qfx[KP];
   __shared__ int32_t red[kWavesPerBlock][KP];
   if (threadIdx.x < KP) qfx[threadIdx.x] = make_float2(a.qfix[threadIdx.x], a.qfix[KP + threadIdx.x]);
@@ -909,6 +915,7 @@ struct LG {
 template <int G, int KP, int MODE, int OCC = 1, bool ALN = false, bool LAG = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void k_gibbs_ldsg(const OniGibbs a) {
   static_assert(G > 1, "G = 1 uses k_gibbs_x1");
+  if (a.exact_guard != nullptr && *a.exact_guard == 0) return;  // a count may leave f32 exactness: generic
   constexpr int S = oni::kWave / G;
   constexpr int KS = G * KP;
   constexpr int kSlots = LdsRow<KP>::kSlots;
@@ -995,7 +1002,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OCC, 8))
 //   0 = generic k_gibbs (any G; the fallback), 2 = k_gibbs_ldsg (G > 1), 3 = k_gibbs_x1 (G = 1).
 // The specialised kernels need n + α exact in f32 (flags bit 0); otherwise the generic one runs.
 template <int G, int KP>
+int launch_gibbs_one(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s);
+
+// With a device exactness guard (a.exact_guard) the row-f32 kernel and the generic kernel are both
+// launched; each reads the flag and all but one return at once -- a per-sweep choice that graph
+// replays keep making on the device (the same draws either way: every variant replays the oracle).
+template <int G, int KP>
 int launch_gibbs(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s) {
+  const int rc = launch_gibbs_one<G, KP>(a, init, mode, qpf, s);
+  if (rc != 0 || init || a.exact_guard == nullptr || !(a.flags & 1) || (qpf != 2 && qpf != 3)) return rc;
+  OniGibbs b = a;
+  b.flags = (b.flags & ~1) | 64;  // no row-f32 kernel: the generic one, guarded
+  return launch_gibbs_one<G, KP>(b, init, mode, 0, s);
+}
+
+template <int G, int KP>
+int launch_gibbs_one(const OniGibbs& a, bool init, int mode, int qpf, hipStream_t s) {
   if (a.KS != G * KP || mode < 0 || mode > 4) return (int)hipErrorInvalidValue;
   const unsigned grid = (unsigned)((a.n_slices + kWavesPerBlock - 1) / kWavesPerBlock);
   if (grid == 0) return 0;

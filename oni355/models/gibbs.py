@@ -259,8 +259,14 @@ class GibbsLDA:
         # the specialised kernels keep n + α as f32 in their count rows: exact only when every
         # n + α of this corpus is (one device read of the longest document); else generic
         self._air = False
+        self._guard = None
         if self.qpf not in (SAMPLERS["generic"], SAMPLERS["mh"]):
             self._air = _alpha_in_row_exact(self.alpha, corpus.max_doc_len())
+            if not self._air:
+                # a document longer than the exact range: the row kernels may still run on every
+                # sweep whose counts stay inside it -- decided per sweep on the device
+                self._guard = self._make_guard()
+                self._air = self._guard is not None
             if not self._air:
                 self.qpf = SAMPLERS["generic"]
         # the Markov chain this model runs (checkpoint identity): the dense kernels are bitwise
@@ -320,6 +326,36 @@ class GibbsLDA:
         self._acc = False         # sweeps add their counts to the accumulators (inside graphs too)
         self._avg_at: list = []   # sweep counts at which a sample is added
         self._avg_cache = None    # (θ, φ) of the completed average
+
+    def _make_guard(self):
+        """Device exactness guard (k_exact_guard) for a corpus with documents past the range in
+        which n + α is exact in f32: (rows to check, count limit, flag). A chunk moves its row by at
+        most its length L from the sweep-start counts, so the row kernels are exact for a sweep iff
+        every sweep-start count of a row that can pass limit = N_safe − L is ≤ limit; only rows
+        longer than that can (split documents: their global counts). None when no guard fits, or
+        ONI_EXACT_GUARD=0 (the generic kernel on every sweep, as before)."""
+        if os.environ.get("ONI_EXACT_GUARD", "1") == "0" or self.device.type != "cuda" and not os.environ.get(
+                "ONI_EXACT_GUARD_CPU"):
+            return None
+        lo, hi = 0, 1 << 25
+        while lo < hi:  # largest n with every count ≤ n exact
+            mid = (lo + hi + 1) // 2
+            lo, hi = (mid, hi) if _alpha_in_row_exact(self.alpha, mid) else (lo, mid - 1)
+        c = self.c
+        Lmax = int(c.chunk_len.max()) if c.chunk_len.numel() else int(c.L)
+        limit = lo - max(Lmax, int(c.L))
+        if os.environ.get("ONI_EXACT_GUARD_LIMIT"):  # tests: force the generic side
+            limit = min(limit, int(os.environ["ONI_EXACT_GUARD_LIMIT"]))
+        if limit < 0:
+            return None
+        lens = c.doc_lengths().to(torch.int64)
+        risky = torch.nonzero(lens > limit).flatten()
+        if c.split is not None and int(c.split["max_count"]) > limit:
+            sp = c.split
+            risky = torch.unique(torch.cat([risky.to(self.device), sp["piece_rows"].to(self.device).to(torch.int64),
+                                            sp["prim_rows"].to(self.device).to(torch.int64)]))
+        return dict(rows=risky.to(torch.int32).to(self.device), limit=int(limit),
+                    flag=torch.ones(1, dtype=torch.int32, device=self.device))
 
     def _setup_mh(self) -> None:
         """MH sampler state: per-sweep proposal tables (every word's level-1 CDF row; alias rows of
@@ -631,6 +667,10 @@ class GibbsLDA:
             self.mh_build_tables()
             st.update(self.mh_state())
         side = self._x01_start(self.dn[1 - self.b]) if self._lag_live else None
+        if self._guard is not None:
+            g = self._guard
+            ops.exact_guard(self.ndk[self.a], g["rows"], self.K, g["limit"], g["flag"])
+            st["exact_guard"] = g["flag"]
         ops.gibbs_pass(st, self.G, self.KP, self.K, self.alpha, self.cfg.seed, False,
                        self.sweep_ctr, c.chunk_len, host_sweep=self.sweeps_done + 1, mode=mode, sampler=self.qpf,
                        chg_mask=self.wbits if mode == 4 else getattr(self, "chg_mask", None), wpos=c.wpos,

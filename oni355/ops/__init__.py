@@ -452,6 +452,8 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
         a.wpos, a.zz_w, a.chg_mask = _lib.ptr(wpos), _lib.ptr(zz_w), _lib.ptr(chg_mask)
     if st.get("chg_count") is not None:
         a.chg_count = _lib.ptr(st["chg_count"])
+    if not init and st.get("exact_guard") is not None:
+        a.exact_guard = _lib.ptr(st["exact_guard"])
     if not init and st.get("tok_zlag") is not None:
         if sampler == SAMPLER_MH:
             raise ValueError("the lagged word side (ONI_X01_LAG) runs the dense samplers only")
@@ -596,6 +598,18 @@ def wdelta_recount(wbits, wsorted, zz_w, dnwk_out, KS: int) -> None:
 RECOUNT_TILE = 4096
 DN_AUX = 4  # auxiliary int32 words at the end of a Δ buffer (matches kDnAux)
 RECOUNT_CELLS = 2048  # LDS histogram cells per recount block (8 KB; matches kRecountCells)
+
+
+def exact_guard(ndk: torch.Tensor, rows: torch.Tensor, K: int, limit: int, flag: torch.Tensor) -> None:
+    """flag[0] := 1 if every count of ``rows`` (first K columns of ``ndk``) is ≤ ``limit``, else 0
+    (k_exact_guard: the row-f32 samplers run this sweep only when it is 1)."""
+    KS = ndk.shape[-1]
+    if not _is_dev(ndk):
+        ok = not bool((ndk[rows.long(), :K] > limit).any()) if rows.numel() else True
+        flag.fill_(1 if ok else 0)
+        return
+    _lib.check(_lib.lib().oni_exact_guard(_lib.ptr(ndk), _lib.ptr(rows), int(rows.numel()), KS, K, int(limit),
+                                          _lib.ptr(flag), _lib.stream()), "oni_exact_guard")
 
 
 def recount(wsorted, wslot, tok_z, nwk_out, KS: int) -> None:

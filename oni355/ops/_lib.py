@@ -32,7 +32,7 @@ class OniGibbs(C.Structure):
         ("tok_word", vp), ("tok_z", vp), ("slice_off", vp), ("slice_len", vp),
         ("chunk_doc", vp), ("chunk_pos0", vp), ("chunk_key", vp), ("chunk_multi", vp),
         ("ndk_src", vp), ("ndk_dst", vp), ("q", vp), ("qfix", vp), ("dnwk", vp), ("dnk", vp), ("sweep_ctr", vp), ("chg_mask", vp),
-        ("wpos", vp), ("z_w", vp), ("zz_w", vp), ("chg_count", vp), ("tok_zlag", vp),
+        ("wpos", vp), ("z_w", vp), ("zz_w", vp), ("chg_count", vp), ("exact_guard", vp), ("tok_zlag", vp),
         ("n_slices", i64), ("K", i32), ("KS", i32), ("alpha", f32), ("seed0", u32), ("seed1", u32),
         ("nk_rep", i32), ("flags", i32),
     ]
@@ -58,6 +58,7 @@ _SIGS = {
     "oni_sell_perm_z": [vp, vp, vp, i64, C.c_int, vp, vp, vp, vp, C.c_int, vp],
     "oni_gibbs_launch": [C.POINTER(OniGibbs), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp],
     "oni_gibbs_sizeof_args": [],
+    "oni_exact_guard": [vp, vp, i64, C.c_int, C.c_int, C.c_int32, vp, vp],
     "oni_gibbs_mh_launch": [C.POINTER(OniMH), C.c_int, C.c_int, vp],
     "oni_mh_sizeof_args": [],
     "oni_mh_tables": [vp, i64, C.c_int, C.c_int, vp, vp, i64, f32, vp, vp, vp, vp, vp, f32, vp, vp],

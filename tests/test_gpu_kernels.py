@@ -306,3 +306,39 @@ def test_wdelta_recount_far_words_matches_cpu(gpu):
         out[dev] = d.cpu()
     assert torch.equal(out["cpu"], out[gpu])
     assert int(out["cpu"].abs().sum()) > 0
+
+
+@pytest.mark.parametrize("K,force_generic", [(20, False), (20, True), (50, False), (50, True)])
+def test_exact_guard_picks_the_row_kernel_per_sweep_bitwise(gpu, monkeypatch, K, force_generic):
+    """A document longer than the range in which n + α is exact in f32 (α = 0.5 + 2^-10: counts up
+    to 16,381) no longer sends every sweep to the generic kernel: k_exact_guard checks the long rows'
+    sweep-start counts on the device and the row kernel (k_gibbs_x1 / k_gibbs_ldsg) or its generic
+    twin runs -- the oracle's draws either way. ONI_EXACT_GUARD_LIMIT forces the generic side."""
+    from oni355.models import gibbs as gm
+    if force_generic:
+        monkeypatch.setenv("ONI_EXACT_GUARD_LIMIT", "10")
+    r = np.random.default_rng(K)
+    D, V = 120, 300
+    lens = r.zipf(1.6, D).clip(1, 500)
+    lens[0] = 20_000
+    tdoc = torch.from_numpy(np.repeat(np.arange(D), lens))
+    tword = torch.from_numpy((r.zipf(1.3, int(lens.sum())) - 1) % V)
+    keys = torch.from_numpy(((np.arange(D, dtype=np.int64) * 2654435761 + 7) % (2**31 - 1)).astype(np.int32))
+    G, _ = ops.choose_tiling(K)
+    alpha = 0.5 + 2.0 ** -10
+    cc = build_corpus(tdoc, tword, D, V, keys, G, L=64)
+    cg = build_corpus(tdoc.to(gpu), tword.to(gpu), D, V, keys.to(gpu), G, L=64)
+    assert not gm._alpha_in_row_exact(alpha, cg.max_doc_len())
+    mc = GibbsLDA(cc, GibbsConfig(K=K, alpha=alpha, seed=5, use_graph=False, count_mode="atomic", sampler="dense"))
+    mg = GibbsLDA(cg, GibbsConfig(K=K, alpha=alpha, seed=5, count_mode="wdelta", sampler="dense"))
+    assert mg._guard is not None and mg.qpf == (3 if G == 1 else 2)
+    assert mg._guard["rows"].numel() == 1
+    for m in (mc, mg):
+        m.initialize()
+    for n in (1, 4, 2):
+        mc.sweep(n)
+        mg.sweep(n)
+        assert int(mg._guard["flag"].item()) == (0 if force_generic else 1)
+        for a, b in ((mc.tok_z, mg.tok_z), (mc.nwk, mg.nwk), (mc.ndk_cur, mg.ndk_cur), (mc.q, mg.q)):
+            assert torch.equal(a, b.cpu())
+    mg.close()

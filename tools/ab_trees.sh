@@ -1,6 +1,7 @@
 #!/bin/bash
-# A/B of two trees' default day on ONE box (alternating runs): the current tree and the side
-# worktree ab_old/ (another commit, built in place). Usage: bash tools/ab_trees.sh TAG REPS [bench args]
+# A/B of two trees' default day on ONE box (alternating runs): the current tree and a side
+# worktree ab_old/ of another commit (git worktree add ab_old <commit>; python tools/build.py inside it).
+# Usage: bash tools/ab_trees.sh TAG REPS [bench args]
 set -o pipefail
 TOP="$(cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && pwd)"
 [[ "${STAGE:-0}" == "1" ]] && SRC="$TOP/gpurun_stage" || SRC="$TOP"

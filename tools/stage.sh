@@ -18,5 +18,5 @@ PY
 rm -rf gpurun_stage
 mkdir -p gpurun_stage
 tar --exclude=./.git --exclude=./gpurun_out --exclude=./gpurun_stage --exclude=./profiles \
-  --exclude='__pycache__' --exclude=./build --exclude=./ab_old/build --exclude=./ab_old/profiles --exclude='*_asan*' --exclude='*.log' --exclude=./gpurun_out -cf - . | tar -xf - -C gpurun_stage
+  --exclude='__pycache__' --exclude=./build --exclude='*_asan*' --exclude='*.log' --exclude=./gpurun_out -cf - . | tar -xf - -C gpurun_stage
 echo "staged $(du -sh gpurun_stage | cut -f1)"
