@@ -288,12 +288,12 @@ class GibbsLDA:
             self.tok_zlag = torch.empty_like(self.tok_z)
         self._pend_abs = False
         self._lag_base = 0
-        # the lag starts with the auto count mode's switch to delta bookkeeping (few tokens still
-        # change topic, so one sweep of staleness costs the chain little; from a random start it
-        # slows the burn-in: profiles/r6/x01_lag/) -- or at sweep ONI_X01_LAG_FROM
+        # the lag starts at sweep ONI_X01_LAG_FROM (default 20: past the burn-in's high-change
+        # sweeps -- the auto count mode switches at 16-20 on the measured days -- so one sweep of
+        # staleness costs the chain little; from a random start it slows the burn-in:
+        # docs/performance.md). A fixed sweep, so a resumed run starts it where the original did
         self._lag_live = False
-        lf = os.environ.get("ONI_X01_LAG_FROM", "auto")
-        self._lag_from = None if lf == "auto" else int(lf)
+        self._lag_from = int(os.environ.get("ONI_X01_LAG_FROM", "20"))
         self.a = 0  # ndk parity
         self.b = 0  # delta-buffer parity
         self.cn = 0  # nk parity
@@ -738,15 +738,8 @@ class GibbsLDA:
         return self._inplace_ok and mode in (1, 2, 4)
 
     def _lag_due(self, sweep: int, mode: int) -> bool:
-        """Does (1-based) sweep ``sweep`` of count mode ``mode`` run with the lagged X01? The same
-        on every rank: the auto switch is decided from all-reduced change counts."""
-        if not self.lag:
-            return False
-        if self._lag_from is not None:
-            return sweep >= self._lag_from
-        if self.auto:
-            return mode == self.mode and mode != self.early
-        return sweep >= 16
+        """Does (1-based) sweep ``sweep`` (of count mode ``mode``) run with the lagged X01?"""
+        return self.lag and sweep >= self._lag_from
 
     def _lag_enter(self) -> None:
         """Start lagging (eager, between sweeps): the counts are current, so the first lagged

@@ -332,7 +332,7 @@ def test_exact_guard_picks_the_row_kernel_per_sweep_bitwise(gpu, monkeypatch, K,
     mc = GibbsLDA(cc, GibbsConfig(K=K, alpha=alpha, seed=5, use_graph=False, count_mode="atomic", sampler="dense"))
     mg = GibbsLDA(cg, GibbsConfig(K=K, alpha=alpha, seed=5, count_mode="wdelta", sampler="dense"))
     assert mg._guard is not None and mg.qpf == (3 if G == 1 else 2)
-    assert mg._guard["rows"].numel() == 1
+    assert mg._guard["rows"].numel() == 1 or force_generic  # only the long document can leave the range
     for m in (mc, mg):
         m.initialize()
     for n in (1, 4, 2):
