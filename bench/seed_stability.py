@@ -26,6 +26,7 @@ def main() -> int:
     ap.add_argument("--sweeps", type=int, default=200)
     ap.add_argument("--days", default="default,realistic")
     ap.add_argument("--deep", type=int, default=4, help="also rank each seed's rows this many times deeper")
+    ap.add_argument("--beta", type=float, default=0.01, help="LDA β (estimator A/B)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -33,7 +34,7 @@ def main() -> int:
     from oni355.pipeline.flow import run_flow
     from oni355.synth.flow import generate_flows
 
-    out = {"flows": a.flows, "maxresults": a.maxresults, "sweeps": a.sweeps, "post_samples":
+    out = {"flows": a.flows, "maxresults": a.maxresults, "sweeps": a.sweeps, "beta": a.beta, "post_samples":
            os.environ.get("ONI_POST_SAMPLES", "default"), "chains": int(os.environ.get("ONI_CHAINS", "1")), "days": {}}
     for kind in a.days.split(","):
         day = generate_flows(a.flows, seed=7, wide_vocab=kind == "realistic")
@@ -44,7 +45,7 @@ def main() -> int:
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             res = run_flow(day.cols, K=20, sweeps=a.sweeps, maxresults=a.maxresults * a.deep, device="cuda:0",
-                           seed=0x0D15EA5E + 7919 * i)
+                           seed=0x0D15EA5E + 7919 * i, beta=a.beta)
             torch.cuda.synchronize()
             times.append(time.perf_counter() - t0)
             deep = np.asarray(res.rows)

@@ -126,7 +126,7 @@ def doc_owner(doc_keys64: torch.Tensor, world: int) -> torch.Tensor:
     return ((h >> 16) % world).to(torch.int64)
 
 
-HEAVY_DOCS_PER_RANK = 4096
+HEAVY_DOCS_PER_RANK = int(os.environ.get("ONI_HEAVY_DOCS_PER_RANK", "4096"))
 PLACEMENT_BUCKETS_PER_RANK = 64
 # A document holding more than 1/(SPLIT_DEN · world) of the day's tokens (one NAT gateway or
 # resolver) is cut into chunk-aligned pieces that are placed like documents;
@@ -242,8 +242,16 @@ def place_docs(doc_keys64: torch.Tensor, weights: torch.Tensor | None, comm: Com
         w = weights.to(torch.int64) if weights is not None else torch.ones(inv.numel(), dtype=torch.int64)
         ucnt = torch.zeros(ukeys.numel(), dtype=torch.int64).index_add_(0, inv.long(), w)
     # local proposals: every document holding more than 1/H of this rank's tokens -- at most H of
-    # them, picked by a threshold instead of a sort; ukeys is ascending, so the proposals are too
-    prop = ukeys[ucnt * HEAVY_DOCS_PER_RANK > ucnt.sum()].contiguous()
+    # them, picked by a threshold instead of a sort; ukeys is ascending, so the proposals are too.
+    # With splitting on, also every document holding more than 1/(SPLIT_DEN · W²) of the day's
+    # tokens here (≤ SPLIT_DEN · W² of them): a document above the split threshold has at least
+    # 1/W of its tokens on some rank, so it is proposed whatever H, W and the shard sizes are
+    splitting = bool(split_L and split_L > 0 and W >= SPLIT_MIN_WORLD and SPLIT_DEN > 0)
+    heavy = ucnt * HEAVY_DOCS_PER_RANK > ucnt.sum()
+    if splitting:
+        total = comm.allreduce_scalar(float(ucnt.sum()))
+        heavy = heavy | (ucnt.to(torch.float64) * (SPLIT_DEN * W * W) > total)
+    prop = ukeys[heavy].contiguous()
     cand = prop if W == 1 else torch.unique(torch.cat([p.to(dev) for p in comm.allgather_var(prop)]))
     # all other documents are hashed into B buckets that are placed like documents, so the rank
     # that takes a huge IP takes correspondingly fewer light ones
@@ -255,7 +263,7 @@ def place_docs(doc_keys64: torch.Tensor, weights: torch.Tensor | None, comm: Com
     bc = both.cpu().numpy().astype(np.int64)
     ccg, bl = bc[:nc], bc[nc:]
     sp = np.zeros(nc, bool)
-    if split_L and split_L > 0 and W >= SPLIT_MIN_WORLD and SPLIT_DEN > 0:
+    if splitting:
         thr = float(bc.sum()) / (SPLIT_DEN * W)
         sp = ccg > max(thr, 2.0 * split_L)
     pdoc, pp0, pp1 = _split_pieces(ccg[sp], float(bc.sum()) / (SPLIT_DEN * W) if sp.any() else 1.0, max(split_L or 1, 1))

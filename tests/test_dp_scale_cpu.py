@@ -253,3 +253,16 @@ def test_realistic_vocab_world8_packed_x01_bitwise():
     x = eight["x01"]
     assert x is not None and x["tiny"] > 0
     assert x["bytes"] < 0.4 * x["dense_bytes"], x
+
+
+def test_document_above_the_split_threshold_is_proposed_whatever_H():
+    """proposals were only the documents above 1/H of a rank's tokens, which covers every
+    document above the split threshold 1/(SPLIT_DEN·W) of the day only while SPLIT_DEN·W ≤ H. With
+    H = 4 and SPLIT_DEN·W = 8 an IP with 18 % of the tokens (above 1/8, below 1/4 of each rank's) is
+    still cut into pieces, and the day stays bitwise the single-process day."""
+    env = {"ONI_HEAVY_DOCS_PER_RANK": "4", "ONI_SPLIT_DEN": "2"}
+    job = dict(source="flow", n=8000, heavy=0.18, env=env)
+    one = _run(1, job)
+    four = _run(4, job)
+    assert four["n_split"] >= 1
+    assert np.array_equal(one["rows"], four["rows"]) and np.array_equal(one["scores"], four["scores"])
