@@ -130,6 +130,9 @@ def test_split_placement_balances_a_30pct_document():
         def allreduce_(self, t):
             return t
 
+        def allreduce_scalar(self, x):
+            return x
+
     r = np.random.default_rng(0)
     keys = r.zipf(1.3, 600_000).astype(np.int64) * 7919 % (2**32)
     keys[r.random(keys.size) < 0.30] = HEAVY_IP
