@@ -63,6 +63,7 @@ def parse(argv=None):
     ap.add_argument("--chunk-len", type=int, default=0, help="0 = auto (global token count)")
     ap.add_argument("--maxresults", type=int, default=3000)
     ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--beta", type=float, default=None, help="LDA β (default: the pipeline's)")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--prefetch-at", choices=["start", "train"], default="start",
@@ -196,6 +197,8 @@ def run_pipeline_mode(a, comm) -> dict:
 
     kw = dict(K=a.topics, sweeps=a.sweeps, tol=1.0, maxresults=a.maxresults, chunk_len=a.chunk_len, device=dev,
               comm=comm, row_offset=row_off)
+    if a.beta is not None:
+        kw["beta"] = a.beta
     # flow days stream in through a double-buffered prefetcher: the loader's pinned buffers are
     # uploaded on a copy stream while the previous day computes (every step still uploads its day)
     pf, pinned, ahead = None, None, None

@@ -29,7 +29,7 @@ class OniConfig:
     SWEEPS: int = 200
     BURNIN: int = 0
     ALPHA: float = -1.0             # <= 0: 50/K
-    BETA: float = 0.01
+    BETA: float | None = None  # None: models.gibbs.default_beta(TOPIC_COUNT)
     SEED: int = 0x0D15EA5E
     CHUNK_LEN: int = 0              # tokens per sampler chunk; 0 = auto from the global token count (32..128)
     EVAL_EVERY: int = 0             # log-likelihood every N sweeps (0 = only at the end)

@@ -30,6 +30,19 @@ from .corpus import Corpus, canonical_tokens
 
 
 NK_REP = 32
+# the word-side Dirichlet prior β when none is given (default_beta): 0.1 from BETA_WIDE_MIN_K topics,
+# 0.01 below
+BETA_WIDE_MIN_K = 100
+
+
+def default_beta(K: int) -> float:
+    """β when the caller gives none: 0.1 for K ≥ BETA_WIDE_MIN_K (the config-5 models), else 0.01.
+    Round-6 A/B (docs/performance.md, profiles/r6/beta/): at K = 100 β = 0.1 lifts top-3000 recall
+    on the config-5 flow share 0.35 → 0.985 and on the 62.5M-flow day 0.405 → 0.455 at the same day
+    time; below, the A/Bs were mixed (proxy quiet-client plants 0.88 → 1.0, DNS own-client plants
+    0.66 → 0.62) and on small days with many topics (6000 DNS events, K = 50) Vβ outweighs a topic's
+    tokens and recall collapses -- so the K = 20 / 50 models keep 0.01."""
+    return 0.1 if K >= BETA_WIDE_MIN_K else 0.01
 POLL_GIVE_UP_SWEEP = 40  # auto count mode: last sweep that may still start a far-off switch
 # largest global token count a model takes: every int32 count (n_wk, n_k, n_dk, Δ) is ≤ the token
 # count, and the Δn_k replicas hold partial sums of it
@@ -87,7 +100,7 @@ def tiling_for(K: int, sampler: str | None = None) -> tuple[int, int]:
 class GibbsConfig:
     K: int = 20
     alpha: float | None = None  # default 50/K (Griffiths & Steyvers)
-    beta: float = 0.01
+    beta: float | None = None  # None: default_beta(K)
     seed: int = 0x0D15EA5E
     use_graph: bool = True
     # n_wk bookkeeping: "auto" (default: "recount" while most topics still move, then "delta"),
@@ -139,6 +152,9 @@ class GibbsConfig:
     def resolved_alpha(self) -> float:
         return float(self.alpha) if self.alpha is not None else 50.0 / self.K
 
+    def resolved_beta(self) -> float:
+        return float(self.beta) if self.beta is not None else default_beta(self.K)
+
 
 def _alpha_in_row_exact(alpha: float, max_doc_len: int) -> bool:
     """May the LDS samplers keep n + α (f32) in their rows? Only if every n + α with
@@ -177,7 +193,7 @@ class GibbsLDA:
             raise ValueError(f"corpus built for G={corpus.G}, K={cfg.K} needs G={self.G}")
         self.KS = self.G * self.KP
         self.alpha = cfg.resolved_alpha()
-        self.beta = float(cfg.beta)
+        self.beta = cfg.resolved_beta()
         self.V = int(V_global if V_global is not None else corpus.V)
         self.vbeta = float(np.float32(self.V * self.beta))
         dev = corpus.tok_word.device

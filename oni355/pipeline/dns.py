@@ -112,7 +112,7 @@ def featurize(d: dict, comm: Comm | None, topset: HashSet | None, user_domain: s
 
 @traced("oni:dns.run")
 def run_dns(cols: dict, K: int = 50, sweeps: int = 200, tol: float = 1.0, maxresults: int = 3000,
-            alpha: float | None = None, beta: float = 0.01, seed: int = 0x0D15EA5E, chunk_len: int = 0,
+            alpha: float | None = None, beta: float | None = None, seed: int = 0x0D15EA5E, chunk_len: int = 0,
             device="cpu", comm: Comm | None = None, top_domains=None, user_domain: str = "",
             feedback: dict | None = None, dupfactor: int = 1000, row_offset: int = 0, eval_every: int = 0, burnin: int = 0,
             ckpt=None, log=None, ldac_dir: str | None = None, ldac_lag: int = 0,
