@@ -593,16 +593,8 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
     chains = max(1, int(os.environ.get("ONI_CHAINS", "1")))
     if chains > 1 and (mh or ckpt is not None or not train or sweeps < 2 * chains):
         chains = 1
-    # ONI_CHAIN_BRANCH = B > 0: the chains share the first B sweeps (the burn-in's high-change
-    # sweeps) and branch from chain 1's state at sweep B with their own seeds: each runs
-    # B + (sweeps − B) // C sweeps, the total is still ``sweeps``, and the extra chains skip their
-    # initialisation and burn-in
-    branch = int(os.environ.get("ONI_CHAIN_BRANCH", "0")) if chains > 1 else 0
-    if branch <= 0 or branch >= sweeps - chains:
-        branch = 0
-    total_sweeps = sweeps
     if chains > 1:
-        sweeps = branch + (sweeps - branch) // chains if branch else sweeps // chains
+        sweeps = sweeps // chains
     with timer.stage("init"):
         model = GibbsLDA(corpus, GibbsConfig(K=K, alpha=alpha, beta=beta, seed=seed), comm=comm,
                          V_global=int(vocab.numel()))
@@ -634,7 +626,6 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
         step = eval_every if eval_every > 0 else remaining
         ck_every = ckpt.every if ckpt is not None and ckpt.every > 0 else 0
         lag = int(ldac_lag) if ldac_dir else 0
-        branch_z = None
         while remaining > 0:
             cur = burner or model
             n = min(step, remaining)
@@ -644,12 +635,8 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
                 n = min(n, ck_every - (cur.sweeps_done % ck_every))
             if lag:
                 n = min(n, lag - (cur.sweeps_done % lag))
-            if branch and cur.sweeps_done < branch:
-                n = min(n, branch - cur.sweeps_done)
             cur.sweep(n)
             remaining -= n
-            if branch and cur.sweeps_done == branch and branch_z is None:
-                branch_z = cur.canonical_z().clone()  # the extra chains start here
             mixed = cur.sweeps_done > burnin
             if eval_every > 0 and cur.sweeps_done % eval_every == 0 and mixed:
                 ll = cur.record_likelihood()
@@ -675,17 +662,11 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
                 mc = GibbsLDA(corpus, GibbsConfig(K=K, alpha=alpha, beta=beta, seed=(seed + c * 0x9E3779B1) & 0xFFFFFFFF),
                               comm=comm, V_global=int(vocab.numel()))
                 mc.plan_average(sweeps)
-                if branch:
-                    mc.load_canonical_z(branch_z, branch)
-                    mc.sweep(sweeps - branch)
-                else:
-                    mc.initialize()
-                    mc.sweep(sweeps)
+                mc.initialize()
+                mc.sweep(sweeps)
                 mc.close()
                 run.extra_models.append(mc)
-    run.timings.update({"sweeps": (branch + (sweeps - branch) * chains) if branch else sweeps * chains,
-                        "chains": chains, "chain_branch": branch})
-    _ = total_sweeps
+    run.timings.update({"sweeps": sweeps * chains, "chains": chains})
     return run
 
 

@@ -24,18 +24,3 @@ def test_two_chains_average_scores(monkeypatch):
     assert not np.array_equal(one.scores, two.scores)
     assert np.all(np.diff(two.scores) >= 0)
     assert np.isin(day.anomaly_rows, two.rows).mean() >= np.isin(day.anomaly_rows, one.rows).mean() - 0.2
-
-
-def test_branching_chains_share_the_burn_in(monkeypatch):
-    """ONI_CHAIN_BRANCH = B: both chains run the first B sweeps once (chain 1), the second starts
-    from chain 1's state at sweep B with its own seed; the total sweep count stays the budget."""
-    import torch
-    monkeypatch.setenv("ONI_CHAIN_BRANCH", "6")
-    two, day = _run(monkeypatch, 2)
-    again, _ = _run(monkeypatch, 2)
-    m1, m2 = two.lda.model, two.lda.extra_models[0]
-    assert m1.sweeps_done == m2.sweeps_done == 6 + (16 - 6) // 2
-    assert two.timings["chain_branch"] == 6 and two.timings["sweeps"] == 16
-    assert np.array_equal(two.rows, again.rows) and np.array_equal(two.scores, again.scores)
-    assert not torch.equal(m1.canonical_z(), m2.canonical_z())  # the branches diverged
-    m2.check_invariants()
