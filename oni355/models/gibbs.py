@@ -75,9 +75,10 @@ def sampler_for(K: int, sampler: str | None = None) -> str:
 
 
 def x01_lag_on() -> bool:
-    """ONI_X01_LAG=1: the X01 all-reduce of sweep s runs on a side stream during sweep s + 1
-    (GibbsLDA._x01_start): every sweep samples its word side against the global counts one sweep
-    older than its doc rows -- the same rule on any number of GPUs."""
+    """ONI_X01_LAG=1: the X01 all-reduce of sweep s is issued asynchronously and runs beside the
+    sampler of sweep s + 1 (GibbsLDA._x01_start): from sweep ONI_X01_LAG_FROM every sweep samples
+    its word side against the global counts one sweep older than its doc rows -- the same rule on
+    any number of GPUs."""
     return os.environ.get("ONI_X01_LAG", "0") == "1"
 
 
@@ -291,8 +292,8 @@ class GibbsLDA:
         if self.mh:
             self.chain["mh_word"] = self.mh_word
         # lagged X01 (cfg.x01_lag): the word side of sweep s samples against the global counts
-        # through sweep s − 2 (one sweep behind the doc rows) while Δ_{s−1} is reduced on a side
-        # stream. tok_zlag = each token's topic in those counts (the word-side exclusion is taken
+        # through sweep s − 2 (one sweep behind the doc rows) while Δ_{s−1} is reduced beside the
+        # sampler. tok_zlag = each token's topic in those counts (the word-side exclusion is taken
         # there, spec.gibbs_pass); x01_red = the reduced Δ of the previous sweep that the sweep's
         # apply adds; its count mode decides absolute / delta (_pend_abs). Every sweep() call
         # ends in a drain (_lag_drain): the counts are current between calls.
@@ -682,7 +683,7 @@ class GibbsLDA:
         if self.mh:
             self.mh_build_tables()
             st.update(self.mh_state())
-        side = self._x01_start(self.dn[1 - self.b]) if self._lag_live else None
+        pending = self._x01_start(self.dn[1 - self.b]) if self._lag_live else None
         if self._guard is not None:
             g = self._guard
             ops.exact_guard(self.ndk[self.a], g["rows"], self.K, g["limit"], g["flag"])
@@ -721,9 +722,9 @@ class GibbsLDA:
         # same launch (int64: no extra pass over n_wk, no separate adds)
         acc = ((self._avg["wk"], self._avg["k"], self._avg["dk"], self.ndk[1 - self.a]) if self._acc else None)
         if self._lag_live:
-            # join the side stream; add the previous sweep's reduced Δ (absolute if that sweep
+            # join the collective; add the previous sweep's reduced Δ (absolute if that sweep
             # recounted) and zero its buffer, which the next sweep writes
-            self._x01_finish(side)
+            self._x01_finish(pending)
             ops.gibbs_apply(self.nwk, self.x01_red[:so], self.dn[1 - self.b][:so], self.nk[self.cn],
                             self.nk[1 - self.cn], self.q, self.qfix, self.V, self.K, self.KS, self.beta, self.vbeta,
                             self.sweep_ctr, bump=True, absolute=self._pend_abs,
@@ -803,8 +804,7 @@ class GibbsLDA:
         sweep's word side then counts every token at tok_z."""
         pb = 1 - self.b
         so = self._split_off
-        side = self._x01_start(self.dn[pb])
-        self._x01_finish(side)
+        self._x01_finish(self._x01_start(self.dn[pb]))
         ops.gibbs_apply(self.nwk, self.x01_red[:so], self.dn[pb][:so], self.nk[self.cn], self.nk[1 - self.cn], self.q,
                         self.qfix, self.V, self.K, self.KS, self.beta, self.vbeta, self.sweep_ctr, bump=False,
                         absolute=self._pend_abs)
