@@ -85,7 +85,7 @@ class Comm:
         if not self.live:
             return None
         if self._one_rank_rccl():
-            out = self._a2a_scratch(t)
+            out = self._a2a_scratch(t, "async")  # its own buffer: sync reductions may run before wait()
             work = dist.all_to_all_single(out, t.reshape(-1), group=self.group, async_op=True)
             return _Pending(work, lambda: t.copy_(out.view(t.shape)))
         if self._via_host and t.is_cuda:
@@ -93,8 +93,8 @@ class Comm:
             return None
         return _Pending(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True), None)
 
-    def _a2a_scratch(self, t: torch.Tensor) -> torch.Tensor:
-        key = (t.numel(), t.dtype)
+    def _a2a_scratch(self, t: torch.Tensor, tag: str = "sync") -> torch.Tensor:
+        key = (t.numel(), t.dtype, tag)
         cache = self.__dict__.setdefault("_a2a_scratch_bufs", {})
         if key not in cache:
             cache[key] = torch.empty(t.numel(), dtype=t.dtype, device=t.device)
