@@ -485,6 +485,20 @@ def apply_split(corpus: Corpus, meta: dict) -> None:
 
 
 @dataclass
+class ChainEstimate:
+    """θ and φ of a finished extra chain (ONI_CHAINS > 1): all that scoring reads of it."""
+    theta_rows: torch.Tensor
+    phi_rows: torch.Tensor
+    sweeps_done: int
+
+    def theta(self) -> torch.Tensor:
+        return self.theta_rows
+
+    def phi(self) -> torch.Tensor:
+        return self.phi_rows
+
+
+@dataclass
 class LdaRun:
     corpus: Corpus
     model: GibbsLDA
@@ -665,7 +679,10 @@ def build_and_train(doc_keys64: torch.Tensor, word_keys64: torch.Tensor | None, 
                 mc.initialize()
                 mc.sweep(sweeps)
                 mc.close()
-                run.extra_models.append(mc)
+                # keep only the chain's estimate: its count tables, Δ buffers and posterior sums are
+                # freed here instead of living until scoring (HBM grew by (C−1)× a model)
+                run.extra_models.append(ChainEstimate(mc.theta(), mc.phi(), mc.sweeps_done))
+                del mc
     run.timings.update({"sweeps": sweeps * chains, "chains": chains})
     return run
 
