@@ -64,6 +64,8 @@ def parse(argv=None):
     ap.add_argument("--maxresults", type=int, default=3000)
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--beta", type=float, default=None, help="LDA β (default: the pipeline's)")
+    ap.add_argument("--env", action="append", default=[], metavar="KEY=VALUE",
+                    help="set an ONI_* environment knob for this run (A/B runs; repeatable)")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--prefetch-at", choices=["start", "train"], default="start",
@@ -80,6 +82,11 @@ def parse(argv=None):
                     help="after the headline, also time this many steps (1 warm-up) of the realistic-vocabulary "
                          "day of the same size and report them under 'realistic_vocab' (0: skip)")
     a = ap.parse_args(argv)
+    for kv in a.env:
+        k, _, v = kv.partition("=")
+        if not k.startswith("ONI_"):
+            raise SystemExit(f"--env takes ONI_* knobs, not {k}")
+        os.environ[k] = v
     a.topics_set = a.topics is not None
     if a.topics is None:
         a.topics = 20 if a.source != "dns" else 50

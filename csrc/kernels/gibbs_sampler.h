@@ -497,12 +497,14 @@ __device__ __forceinline__ int count_le(const float (&P)[KP], float excl, float 
 // 3-wave register budget (+0.011 ms) all lost.
 // WPD (off: measured 0.255 vs 0.248 ms/sweep): MODE 3/4 changed tokens load their word-sorted
 // slot when they change (exec-masked, ~10 % of lanes) instead of streaming it with every token.
-template <int KP, int MODE, bool AIR, bool WPD, bool ALN = false, bool LAG = false, bool PKQ = false>
+template <int KP, int MODE, bool AIR, bool WPD, bool ALN = false, bool LAG = false, bool PKQ = false,
+          bool LUT = false>
 struct X1 {
   static constexpr int KS = KP;
   static constexpr bool WPF = (MODE == 3 || MODE == 4) && !WPD;
   const OniGibbs& a;
   const float2* qfx;  // LDS: (A, B) per topic
+  const float2* dlut;  // LUT: LDS, the (Δ_2p, Δ_2p+1) pair of every 4-bit field pair of the mask
   int lane;
   int64_t off;
   int len;
@@ -523,11 +525,25 @@ struct X1 {
   __device__ __forceinline__ X1(const OniGibbs& a_, const float2* q_) : a(a_), qfx(q_) {}
 
   __device__ __forceinline__ void add_fields(uint32_t mlo, uint32_t mhi) {
+    if constexpr (LUT) {
+      // A/B: the two 2-bit fields of a topic pair index a 16-entry LDS table of float pairs (one
+      // bfe, one ds_read_b64, one v_pk_add_f32 per pair instead of two bfe + two cvt + an add)
+      using f2 = float __attribute__((ext_vector_type(2)));
 #pragma unroll
-    for (int j = 0; j < KP; ++j) {
-      const uint32_t m = j < 16 ? mlo : mhi;
-      const int sh = 30 - 2 * (j & 15);
-      r[j] += (float)((int32_t)(m << sh) >> 30);
+      for (int p = 0; p < KP / 2; ++p) {
+        const uint32_t m = 2 * p < 16 ? mlo : mhi;
+        const float2 d = dlut[__builtin_amdgcn_ubfe(m, 4u * (uint32_t)(p & 7), 4u)];
+        f2 v = f2{r[2 * p], r[2 * p + 1]} + f2{d.x, d.y};
+        r[2 * p] = v.x;
+        r[2 * p + 1] = v.y;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < KP; ++j) {
+        const uint32_t m = j < 16 ? mlo : mhi;
+        const int sh = 30 - 2 * (j & 15);
+        r[j] += (float)((int32_t)(m << sh) >> 30);
+      }
     }
   }
 
@@ -639,18 +655,25 @@ struct X1 {
 // 4 waves per SIMD up to KP = 24 (≤ 128 VGPRs: 3 rows of KP plus the weights); wider rows take
 // what they need (a forced 4-wave budget spills at KP = 32)
 // LAG streams one more topic per token: 3 waves per SIMD (≤ 168 VGPRs) -- at the 4-wave budget it spilled
-template <int KP, int MODE, bool AIR, bool WPD = false, bool ALN = false, bool LAG = false, bool PKQ = false>
+template <int KP, int MODE, bool AIR, bool WPD = false, bool ALN = false, bool LAG = false, bool PKQ = false,
+          bool LUT = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KP <= 24 ? (LAG ? 3 : 4) : 1, 8))) void k_gibbs_x1(
     const OniGibbs a) {
   static_assert(KP <= 32 && KP % 4 == 0, "one-lane units hold at most 32 topics");
   if (a.exact_guard != nullptr && *a.exact_guard == 0) return;  // a count may leave f32 exactness: generic
   __shared__ float2 qfx[KP];
+  __shared__ float2 dlut[16];
   __shared__ int32_t red[kWavesPerBlock][KP];
   if (threadIdx.x < KP) qfx[threadIdx.x] = make_float2(a.qfix[threadIdx.x], a.qfix[KP + threadIdx.x]);
+  if (LUT && threadIdx.x < 16) {
+    const int lo = (int)(threadIdx.x & 3u), hi = (int)(threadIdx.x >> 2);  // 2-bit fields: 0, +1, (−2), −1
+    dlut[threadIdx.x] = make_float2((float)((lo << 30) >> 30), (float)((hi << 30) >> 30));
+  }
   __syncthreads();
 
-  using XT = X1<KP, MODE, AIR, WPD, ALN, LAG, PKQ>;
+  using XT = X1<KP, MODE, AIR, WPD, ALN, LAG, PKQ, LUT>;
   XT x(a, qfx);
+  x.dlut = dlut;
   const int wave = threadIdx.x >> 6;
   x.lane = threadIdx.x & 63;
   const int64_t slice = (int64_t)blockIdx.x * kWavesPerBlock + wave;
@@ -1059,6 +1082,11 @@ int launch_gibbs_one(const OniGibbs& a, bool init, int mode, int qpf, hipStream_
       if (a.flags & 32) {
         if (mode == 0) k_gibbs_x1<KP, 0, true, false, true, false, true><<<grid, kBlock, 0, s>>>(a);
         else k_gibbs_x1<KP, 4, true, false, true, false, true><<<grid, kBlock, 0, s>>>(a);
+        return (int)hipGetLastError();
+      }
+      if (a.flags & 128) {  // A/B (ONI_SAMPLER_AB & 8): the ±1 count update through an LDS table
+        if (mode == 0) k_gibbs_x1<KP, 0, true, false, true, false, false, true><<<grid, kBlock, 0, s>>>(a);
+        else k_gibbs_x1<KP, 4, true, false, true, false, false, true><<<grid, kBlock, 0, s>>>(a);
         return (int)hipGetLastError();
       }
       if (mode == 0) k_gibbs_x1<KP, 0, true, false, true><<<grid, kBlock, 0, s>>>(a);
