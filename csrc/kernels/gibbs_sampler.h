@@ -526,8 +526,10 @@ struct X1 {
 
   __device__ __forceinline__ void add_fields(uint32_t mlo, uint32_t mhi) {
     if constexpr (LUT) {
-      // A/B: the two 2-bit fields of a topic pair index a 16-entry LDS table of float pairs (one
-      // bfe, one ds_read_b64, one v_pk_add_f32 per pair instead of two bfe + two cvt + an add)
+      // the two 2-bit fields of a topic pair index a 16-entry LDS table of float pairs: one field
+      // extract, one ds_read_b64 and one v_pk_add_f32 per pair instead of two bfe + two cvt + an
+      // add (ISA: 733 against 789 VALU per two-step loop; 0.2303-0.2328 against 0.2406-0.2432 ms
+      // per sweep, profiles/r6/count_lut/)
       using f2 = float __attribute__((ext_vector_type(2)));
 #pragma unroll
       for (int p = 0; p < KP / 2; ++p) {
@@ -1084,13 +1086,15 @@ int launch_gibbs_one(const OniGibbs& a, bool init, int mode, int qpf, hipStream_
         else k_gibbs_x1<KP, 4, true, false, true, false, true><<<grid, kBlock, 0, s>>>(a);
         return (int)hipGetLastError();
       }
-      if (a.flags & 128) {  // A/B (ONI_SAMPLER_AB & 8): the ±1 count update through an LDS table
-        if (mode == 0) k_gibbs_x1<KP, 0, true, false, true, false, false, true><<<grid, kBlock, 0, s>>>(a);
-        else k_gibbs_x1<KP, 4, true, false, true, false, false, true><<<grid, kBlock, 0, s>>>(a);
+      if (a.flags & 128) {  // A/B (ONI_SAMPLER_AB & 8): the ±1 count update by per-topic bfe + cvt (round 5)
+        if (mode == 0) k_gibbs_x1<KP, 0, true, false, true><<<grid, kBlock, 0, s>>>(a);
+        else k_gibbs_x1<KP, 4, true, false, true><<<grid, kBlock, 0, s>>>(a);
         return (int)hipGetLastError();
       }
-      if (mode == 0) k_gibbs_x1<KP, 0, true, false, true><<<grid, kBlock, 0, s>>>(a);
-      else k_gibbs_x1<KP, 4, true, false, true><<<grid, kBlock, 0, s>>>(a);
+      // default: the ±1 count update through the LDS table of float pairs (4 % faster per sweep,
+      // profiles/r6/count_lut/)
+      if (mode == 0) k_gibbs_x1<KP, 0, true, false, true, false, false, true><<<grid, kBlock, 0, s>>>(a);
+      else k_gibbs_x1<KP, 4, true, false, true, false, false, true><<<grid, kBlock, 0, s>>>(a);
       return (int)hipGetLastError();
     }
     if (qpf == 3 && KP <= 32) {
