@@ -616,8 +616,10 @@ __device__ __forceinline__ MHLds mh_lds(unsigned char* smem, int KS) {
   return L;
 }
 
-template <int MODE, int DM, int WP>
-__global__ __launch_bounds__(64) void k_gibbs_mh(const OniMH m) {
+// OCC > 0: a register budget for OCC waves per SIMD (A/B, ONI_SAMPLER_AB & 16)
+template <int MODE, int DM, int WP, int OCC = 0>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1, 8)))
+void k_gibbs_mh(const OniMH m) {
   extern __shared__ __align__(16) unsigned char smem_mh[];
   const OniGibbs& a = m.g;
   const int KS = a.KS;
@@ -783,6 +785,11 @@ ONI_API int oni_gibbs_mh_launch(const OniMH* m, int init, int mode, hipStream_t 
   if (mode == 2 && !a.chg_mask) return (int)hipErrorInvalidValue;
   if (mode == 3 && (!a.wpos || !a.z_w)) return (int)hipErrorInvalidValue;
   if (mode == 4 && (!a.wpos || !a.zz_w || !a.chg_mask)) return (int)hipErrorInvalidValue;
+  if ((a.flags & 256) && m->doc_moves == 2 && m->wp == 8 && (mode == 0 || mode == 4)) {
+    if (mode == 0) k_gibbs_mh<0, 2, 8, 4><<<grid, 64, lds, s>>>(*m);
+    else k_gibbs_mh<4, 2, 8, 4><<<grid, 64, lds, s>>>(*m);
+    return (int)hipGetLastError();
+  }
 #define ONI_MH(md, dm)                                                  \
   do {                                                                  \
     if (m->wp == 0) k_gibbs_mh<md, dm, 0><<<grid, 64, lds, s>>>(*m);    \

@@ -469,9 +469,11 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
     # one-lane sampler picks its Philox word by the uniform step index (bit 4)
     ab = int(os.environ.get("ONI_SAMPLER_AB", "0"))
     # bit 2 of ONI_SAMPLER_AB (flags bit 5): k_gibbs_x1's q' by v_pk_fma_f32 on topic pairs (A/B: loses);
-    # bit 3 (flags bit 7): its ±1 count update by per-topic bfe + cvt instead of the LDS table (A/B)
+    # bit 3 (flags bit 7): its ±1 count update by per-topic bfe + cvt instead of the LDS table (A/B);
+    # bit 4 (flags bit 8): k_gibbs_mh under a 4-wave register budget (A/B)
     a.flags = ((1 if alpha_in_row else 0) | (ab & 3) << 1 | (8 if (init and word_init) else 0)
-               | (16 if pos_aligned else 0) | (32 if ab & 4 else 0) | (128 if ab & 8 else 0))
+               | (16 if pos_aligned else 0) | (32 if ab & 4 else 0) | (128 if ab & 8 else 0)
+               | (256 if ab & 16 else 0))
     if sampler == SAMPLER_MH:
         if G != 1:
             raise ValueError("the MH sampler runs one-lane units")
