@@ -251,7 +251,11 @@ struct MHLds {
   float* gk;
   uint8_t* cnt;
   uint8_t* zsl;
+  float* c1s;  // CO: level-1 CDF rows of the wave's 64 tokens, [64][kC1S] (after zsl)
+  float* qbs;  // CO > 1: the proposed buckets' q values, [64][kQBS] (the c1s area)
 };
+constexpr int kC1S = 20;  // c1 staging row stride (floats): 16-B aligned, rows 20 banks apart
+constexpr int kQBS = 20;  // bucket staging row stride (floats): up to 16 values
 
 // stage-B data of one token (issued one step ahead; none of it depends on the chain state)
 template <int DM>
@@ -280,8 +284,14 @@ struct MHB {
 // on one common address for the doc tables) and every decision is a select, so no loaded value is
 // merged at a control-flow join -- a merge there makes the compiler wait for every outstanding
 // memory op (vmcnt(0)), which serialised the token pipeline.
-template <int MODE, int DM, int WP>
+template <int MODE, int DM, int WP, int CO = 0>
 struct MHLane {
+  static constexpr int NQ = (WP > 0 ? WP : 4) / 4;  // float4 loads of a bucket
+  // CO (A/B): 1 = level-1 rows gathered four lanes per row; 2 = also the buckets (NQ lanes per
+  // bucket); 3 = 2 with words read four tokens ahead and the level-1 rows issued a whole step before
+  // their use; 4 = 1 with that word pipeline
+  static constexpr bool CB = CO == 2 || CO == 3;
+  static constexpr bool WD = CO >= 3;
   static constexpr int WB = WP > 0 ? WP : 1;
   const OniMH& m;
   const OniGibbs& a;
@@ -296,9 +306,14 @@ struct MHLane {
   const int32_t* brow;  // n_src row of the doc
   const uint32_t* drow; // dalias row of the doc (row 0 for one-chunk docs)
   uint32_t wa[2];       // stage A: token words (parity slots)
+  uint32_t wb[2];       // WD: the words two tokens further ahead (parity slots)
+  int64_t last;         // WD: SELL index of this lane's slot in the slice's last step
   int32_t pa[2];        // stage A: word-sorted slots (MODE 3/4)
   MHB<DM> b[2];             // stage B (parity slots)
   float c1[16];         // level-1 word CDF row of the token after next (gathered a step ahead of its stage B)
+  float4 c1v[4];        // CO: this lane's quarter of rows 16 i + lane / 4 (i = 0..3), in flight
+  float4 qbv[NQ];       // CO > 1: this lane's share of the buckets of rows (64 / NQ) i + lane / NQ
+  uint32_t qbin;        // CO > 1: bit i: float4 i lies inside its q row
   float qb[WB];         // the proposed bucket's q values (stage B → stage C of one token)
   float ywd;            // the word draw's y = u·Z
   float base;           // C[bucket − 1] (gathered)
@@ -336,8 +351,21 @@ struct MHLane {
   }
 
   // level-1 word CDF row of word w (a stage ahead of its stage B: its bucket gather depends on it)
+  // CO: the 64 rows are gathered four lanes per row (lane l loads quarter l % 4 of row 16 i + l / 4
+  // in load i): each load touches 16 lines instead of 64, a quarter of the address-unit work of one
+  // row per lane (the TA unit was the busiest one of this kernel, profiles/r6/mh_pmc/). The rows are
+  // turned back to one per lane through LDS when they are used (land_c1).
   __device__ __forceinline__ void load_c1(uint32_t w) {
     if constexpr (WP == 0) return;
+    if constexpr (CO > 0) {
+      const int wc = (int)(w == oni::kPadWord ? 0u : w);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t wr = (uint32_t)__shfl(wc, 16 * i + (lane >> 2));
+        c1v[i] = reinterpret_cast<const float4*>(m.wcdf)[(int64_t)wr * 4 + (lane & 3)];
+      }
+      return;
+    }
     const float4* r = reinterpret_cast<const float4*>(m.wcdf) + (int64_t)(w == oni::kPadWord ? 0u : w) * 4;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -349,8 +377,62 @@ struct MHLane {
     }
   }
 
+  // CO: the quarters in flight to LDS, then this lane's own row back (one wave: its LDS accesses
+  // run in order; the fences keep the compiler from reordering them)
+  __device__ __forceinline__ void land_c1() {
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      *reinterpret_cast<float4*>(L.c1s + (16 * i + (lane >> 2)) * kC1S + 4 * (lane & 3)) = c1v[i];
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float4 v = *reinterpret_cast<const float4*>(L.c1s + lane * kC1S + 4 * i);
+      c1[4 * i] = v.x;
+      c1[4 * i + 1] = v.y;
+      c1[4 * i + 2] = v.z;
+      c1[4 * i + 3] = v.w;
+    }
+    asm volatile("" ::: "memory");
+  }
+
+  // CO > 1: load I of the cooperative bucket gather (a template so that the shuffles need no loop)
+  template <int I>
+  __device__ __forceinline__ void bucket_load(uint32_t offr) {
+    if constexpr (I < NQ) {
+      const int src = (64 / NQ) * I + lane / NQ;
+      const int h = lane % NQ;
+      const uint32_t o = (uint32_t)__shfl((int)offr, src);
+      const int b2 = __shfl(bk, src);
+      const bool in = b2 * WB + 4 * h < KS;
+      qbin |= in ? 1u << I : 0u;
+      qbv[I] = *reinterpret_cast<const float4*>(in ? a.q + o + 4 * h : a.q);
+    }
+  }
+
+  template <int I>
+  __device__ __forceinline__ void bucket_land() {
+    if constexpr (I < NQ) {
+      const bool in = ((qbin >> I) & 1u) != 0u;
+      float* d = L.qbs + ((64 / NQ) * I + lane / NQ) * kQBS + 4 * (lane % NQ);
+      *reinterpret_cast<float4*>(d) =
+          make_float4(in ? qbv[I].x : 0.f, in ? qbv[I].y : 0.f, in ? qbv[I].z : 0.f, in ? qbv[I].w : 0.f);
+    }
+  }
+  template <int I>
+  __device__ __forceinline__ void bucket_take() {
+    if constexpr (I < NQ) {
+      const float4 v = *reinterpret_cast<const float4*>(L.qbs + lane * kQBS + 4 * I);
+      qb[4 * I] = v.x;
+      qb[4 * I + 1] = v.y;
+      qb[4 * I + 2] = v.z;
+      qb[4 * I + 3] = v.w;
+    }
+  }
+
   // stage B of the token at step s (word w): Philox block, then the state-free gathers
   __device__ __forceinline__ void issue_b(int P, int s, uint32_t w) {
+    if constexpr (CO > 0 && WP > 0) land_c1();
     MHB<DM>& x = b[P];
     const uint32_t wc = w == oni::kPadWord ? 0u : w;
     x.r = oni::philox10(oni::U4{pos0 + (uint32_t)s, key, sweep, 2u}, a.seed0, a.seed1);
@@ -373,15 +455,25 @@ struct MHLane {
 #pragma unroll
       for (int i = 0; i < 15; ++i) base = i == bk - 1 ? c1[i] : base;
       // level 2: the bucket's q values (a float4 past the row's KS padding is not read)
-      const float* qr = a.q + (int64_t)wc * KS + bk * WB;
+      if constexpr (CB) {
+        // NQ lanes per bucket: load i brings float4 lane % NQ of the bucket of row (64/NQ) i + lane/NQ
+        const uint32_t offr = wc * (uint32_t)KS + (uint32_t)(bk * WB);
+        qbin = 0u;
+        bucket_load<0>(offr);
+        bucket_load<1>(offr);
+        bucket_load<2>(offr);
+        bucket_load<3>(offr);
+      } else {
+        const float* qr = a.q + (int64_t)wc * KS + bk * WB;
 #pragma unroll
-      for (int j4 = 0; j4 < WB / 4; ++j4) {
-        const bool in = bk * WB + 4 * j4 < KS;
-        const float4 v = *reinterpret_cast<const float4*>(in ? qr + 4 * j4 : a.q);
-        qb[4 * j4] = in ? v.x : 0.f;
-        qb[4 * j4 + 1] = in ? v.y : 0.f;
-        qb[4 * j4 + 2] = in ? v.z : 0.f;
-        qb[4 * j4 + 3] = in ? v.w : 0.f;
+        for (int j4 = 0; j4 < WB / 4; ++j4) {
+          const bool in = bk * WB + 4 * j4 < KS;
+          const float4 v = *reinterpret_cast<const float4*>(in ? qr + 4 * j4 : a.q);
+          qb[4 * j4] = in ? v.x : 0.f;
+          qb[4 * j4 + 1] = in ? v.y : 0.f;
+          qb[4 * j4 + 2] = in ? v.z : 0.f;
+          qb[4 * j4 + 3] = in ? v.w : 0.f;
+        }
       }
     }
     // one-chunk docs read one common address (they use neither value): no scattered lines
@@ -402,6 +494,20 @@ struct MHLane {
   __device__ __forceinline__ void issue_c(int P, int s, uint32_t w) {
     MHB<DM>& x = b[P];
     const uint32_t qo = (w == oni::kPadWord ? 0u : w) * (uint32_t)KS;
+    if constexpr (CB && WP > 0) {
+      // the buckets in flight to LDS, then this lane's own bucket back (cf. land_c1)
+      asm volatile("" ::: "memory");
+      bucket_land<0>();
+      bucket_land<1>();
+      bucket_land<2>();
+      bucket_land<3>();
+      asm volatile("" ::: "memory");
+      bucket_take<0>();
+      bucket_take<1>();
+      bucket_take<2>();
+      bucket_take<3>();
+      asm volatile("" ::: "memory");
+    }
     if constexpr (WP == 0) {
       x.tw = alias_draw(x.r.x, x.rw.x);
     } else {
@@ -460,7 +566,16 @@ struct MHLane {
     asm volatile("" ::: "memory");
     if constexpr (LOAD_B) issue_b(NX, s + 1, wa[NX]);
     asm volatile("" ::: "memory");
-    if constexpr (LOAD_A) {
+    if constexpr (WD) {
+      // the level-1 row of token s + 2 now (its word came two steps ago), used a step from now
+      if constexpr (LOAD_B) load_c1(wb[P]);
+      asm volatile("" ::: "memory");
+      wa[P] = wb[P];
+      // word of token s + 4 (clamped to the slice: past its end nothing uses it)
+      const int64_t i4 = idx + 256;
+      wb[P] = a.tok_word[i4 < last ? i4 : last];
+      if constexpr (LOAD_A && (MODE == 3 || MODE == 4)) pa[P] = a.wpos[idx + 128];
+    } else if constexpr (LOAD_A) {
       wa[P] = a.tok_word[idx + 128];
       if constexpr (MODE == 3 || MODE == 4) pa[P] = a.wpos[idx + 128];
     } else {
@@ -546,7 +661,7 @@ struct MHLane {
     }
     asm volatile("" ::: "memory");
     if constexpr (LOAD_B) {
-      load_c1(wa[P]);  // the token after next (issued before stage C: its wait must not cover C)
+      if constexpr (!WD) load_c1(wa[P]);  // the token after next (issued before stage C: its wait must not cover C)
       asm volatile("" ::: "memory");
       issue_c(NX, s + 1, wa[NX]);
     }
@@ -616,15 +731,19 @@ __device__ __forceinline__ MHLds mh_lds(unsigned char* smem, int KS) {
   return L;
 }
 
-// OCC > 0: a register budget for OCC waves per SIMD (A/B, ONI_SAMPLER_AB & 16)
-template <int MODE, int DM, int WP, int OCC = 0>
+// OCC > 0: a register budget for OCC waves per SIMD (A/B, ONI_SAMPLER_AB & 16); CO ≥ 1: the level-1
+// CDF rows gathered four lanes per row (ONI_SAMPLER_AB & 32); CO = 2: also the buckets, WB / 4 lanes
+// per bucket (& 64)
+template <int MODE, int DM, int WP, int OCC = 0, int CO = 0>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1, 8)))
 void k_gibbs_mh(const OniMH m) {
   extern __shared__ __align__(16) unsigned char smem_mh[];
   const OniGibbs& a = m.g;
   const int KS = a.KS;
-  MHLane<MODE, DM, WP> x(m);
+  MHLane<MODE, DM, WP, CO> x(m);
   x.L = mh_lds(smem_mh, KS);
+  x.L.c1s = reinterpret_cast<float*>(x.L.zsl + (size_t)m.lmax * 64);
+  x.L.qbs = x.L.c1s;  // used at other times than c1s (issue_c vs issue_b): one staging area
   int32_t* red = reinterpret_cast<int32_t*>(smem_mh + (size_t)KS * (sizeof(float2) + sizeof(float)));
   x.red = red;
   const int lane = threadIdx.x;
@@ -672,7 +791,9 @@ void k_gibbs_mh(const OniMH m) {
   for (int t = 0; t < 2; ++t) {
     x.wa[t] = len > t ? a.tok_word[x.off + t * 64 + lane] : oni::kPadWord;
     x.pa[t] = ((MODE == 3 || MODE == 4) && len > t) ? a.wpos[x.off + t * 64 + lane] : 0;
+    x.wb[t] = len > t + 2 ? a.tok_word[x.off + (t + 2) * 64 + lane] : oni::kPadWord;
   }
+  x.last = x.off + (int64_t)(len > 0 ? len - 1 : 0) * 64 + lane;
   x.load_c1(x.wa[0]);
   x.issue_b(0, 0, x.wa[0]);
   x.load_c1(x.wa[1]);
@@ -736,8 +857,9 @@ __global__ __launch_bounds__(64) void k_gibbs_mh_init(const OniMH m) {
 
 }  // namespace
 
-static size_t mh_lds_bytes(int KS, int lmax) {
-  return (size_t)KS * (sizeof(float2) + sizeof(float) + sizeof(int32_t)) + (size_t)KS * 64 + (size_t)lmax * 64;
+static size_t mh_lds_bytes(int KS, int lmax, int co = 0) {
+  return (size_t)KS * (sizeof(float2) + sizeof(float) + sizeof(int32_t)) + (size_t)KS * 64 + (size_t)lmax * 64 +
+         (co > 0 ? (size_t)64 * (kC1S > kQBS ? kC1S : kQBS) * sizeof(float) : 0);
 }
 
 // Per-sweep MH tables. Word proposal: alias records (walias + wsum, k_mh_alias over the V word rows)
@@ -785,9 +907,28 @@ ONI_API int oni_gibbs_mh_launch(const OniMH* m, int init, int mode, hipStream_t 
   if (mode == 2 && !a.chg_mask) return (int)hipErrorInvalidValue;
   if (mode == 3 && (!a.wpos || !a.z_w)) return (int)hipErrorInvalidValue;
   if (mode == 4 && (!a.wpos || !a.zz_w || !a.chg_mask)) return (int)hipErrorInvalidValue;
-  if ((a.flags & 256) && m->doc_moves == 2 && m->wp == 8 && (mode == 0 || mode == 4)) {
-    if (mode == 0) k_gibbs_mh<0, 2, 8, 4><<<grid, 64, lds, s>>>(*m);
-    else k_gibbs_mh<4, 2, 8, 4><<<grid, 64, lds, s>>>(*m);
+  // A/B variants of the default configuration (two doc moves, CDF word proposal, recount / wdelta)
+  if ((a.flags & (256 | 512 | 1024 | 2048)) && m->doc_moves == 2 && m->wp == 8 && (mode == 0 || mode == 4)) {
+    int co = (a.flags & 1024) ? 2 : (a.flags & 512) ? 1 : 0;
+    if (a.flags & 2048) co = co == 2 ? 3 : 4;
+    const bool occ = (a.flags & 256) != 0;
+    const size_t lco = mh_lds_bytes(a.KS, m->lmax, co);
+#define ONI_MH_AB(md)                                                                          \
+  do {                                                                                         \
+    if (occ) {                                                                                 \
+      if (co == 2) k_gibbs_mh<md, 2, 8, 4, 2><<<grid, 64, lco, s>>>(*m);                       \
+      else if (co == 1) k_gibbs_mh<md, 2, 8, 4, 1><<<grid, 64, lco, s>>>(*m);                  \
+      else k_gibbs_mh<md, 2, 8, 4, 0><<<grid, 64, lco, s>>>(*m);                               \
+    } else {                                                                                   \
+      if (co == 4) k_gibbs_mh<md, 2, 8, 0, 4><<<grid, 64, lco, s>>>(*m);                       \
+      else if (co == 3) k_gibbs_mh<md, 2, 8, 0, 3><<<grid, 64, lco, s>>>(*m);                  \
+      else if (co == 2) k_gibbs_mh<md, 2, 8, 0, 2><<<grid, 64, lco, s>>>(*m);                  \
+      else k_gibbs_mh<md, 2, 8, 0, 1><<<grid, 64, lco, s>>>(*m);                               \
+    }                                                                                          \
+  } while (0)
+    if (mode == 0) ONI_MH_AB(0);
+    else ONI_MH_AB(4);
+#undef ONI_MH_AB
     return (int)hipGetLastError();
   }
 #define ONI_MH(md, dm)                                                  \
