@@ -21,10 +21,17 @@
 //    ≤ 127 tokens), so 100 topics cost 6.4 KB per wave instead of 25.6 KB of f32 rows. The
 //    chunk's current topics (the one-chunk doc proposal picks a random other token) sit next to
 //    them, also u8 and interleaved.
-//  * Loads are software-pipelined by token: the token word two steps ahead; the next token's
-//    Philox block, q[w, zo], the word table's row sum, its alias entry (and a multi-chunk doc's
-//    alias entry and n_src[zo]) one step ahead -- all independent of the chain state -- so a
-//    step waits only for the gathers that depend on its proposals (q[w, t], n_src[t]).
+//  * Loads are software-pipelined by token: the token word four steps ahead (CDF proposal; two
+//    with the alias records), the level-1 CDF row two steps ahead; the next token's Philox block,
+//    q[w, zo], the bucket's q values, its alias entry (and a multi-chunk doc's alias entry and
+//    n_src[zo]) one step ahead -- all independent of the chain state -- so a step waits only for
+//    the gathers that depend on its proposals (q[w, t], n_src[t]).
+//  * The texture-address unit is this kernel's busiest (~75 % at the config-5 flow share,
+//    profiles/r6/mh_pmc/): a scattered load costs it about a cycle per distinct line, so the 64-B
+//    level-1 rows are gathered four lanes per row (16 lines per load instead of 64) and turned back
+//    to one row per lane through LDS (4.30 → 4.16 ms per config-5 sweep with the deeper word
+//    pipeline, profiles/r6/mh_coop/; the buckets gathered the same way lost: their LDS round trip
+//    sits in the step's dependency chain).
 //  * Every draw is Philox4x32-10 on (pos, doc key, sweep, 2 + move): a pure function of the data
 //    and the seed, so the chain is bitwise identical for any GPU count or chunk placement.
 #include "gibbs_sampler.h"
@@ -251,11 +258,9 @@ struct MHLds {
   float* gk;
   uint8_t* cnt;
   uint8_t* zsl;
-  float* c1s;  // CO: level-1 CDF rows of the wave's 64 tokens, [64][kC1S] (after zsl)
-  float* qbs;  // CO > 1: the proposed buckets' q values, [64][kQBS] (the c1s area)
+  float* c1s;  // level-1 CDF rows of the wave's 64 tokens, [64][kC1S] (after zsl; not with R5)
 };
 constexpr int kC1S = 20;  // c1 staging row stride (floats): 16-B aligned, rows 20 banks apart
-constexpr int kQBS = 20;  // bucket staging row stride (floats): up to 16 values
 
 // stage-B data of one token (issued one step ahead; none of it depends on the chain state)
 template <int DM>
@@ -284,14 +289,14 @@ struct MHB {
 // on one common address for the doc tables) and every decision is a select, so no loaded value is
 // merged at a control-flow join -- a merge there makes the compiler wait for every outstanding
 // memory op (vmcnt(0)), which serialised the token pipeline.
-template <int MODE, int DM, int WP, int CO = 0>
+// R5 (A/B, ONI_SAMPLER_AB & 32): round 5's level-1 rows (one lane per row, issued at the end of the
+// step before their use, words two tokens ahead)
+template <int MODE, int DM, int WP, bool R5 = false>
 struct MHLane {
-  static constexpr int NQ = (WP > 0 ? WP : 4) / 4;  // float4 loads of a bucket
-  // CO (A/B): 1 = level-1 rows gathered four lanes per row; 2 = also the buckets (NQ lanes per
-  // bucket); 3 = 2 with words read four tokens ahead and the level-1 rows issued a whole step before
-  // their use; 4 = 1 with that word pipeline
-  static constexpr bool CB = CO == 2 || CO == 3;
-  static constexpr bool WD = CO >= 3;
+  // CDF word proposal: level-1 rows gathered four lanes per row (CO) and issued a whole step before
+  // their use, from words read four tokens ahead (WD)
+  static constexpr bool CO = !R5 && WP > 0;
+  static constexpr bool WD = CO;
   static constexpr int WB = WP > 0 ? WP : 1;
   const OniMH& m;
   const OniGibbs& a;
@@ -312,8 +317,6 @@ struct MHLane {
   MHB<DM> b[2];             // stage B (parity slots)
   float c1[16];         // level-1 word CDF row of the token after next (gathered a step ahead of its stage B)
   float4 c1v[4];        // CO: this lane's quarter of rows 16 i + lane / 4 (i = 0..3), in flight
-  float4 qbv[NQ];       // CO > 1: this lane's share of the buckets of rows (64 / NQ) i + lane / NQ
-  uint32_t qbin;        // CO > 1: bit i: float4 i lies inside its q row
   float qb[WB];         // the proposed bucket's q values (stage B → stage C of one token)
   float ywd;            // the word draw's y = u·Z
   float base;           // C[bucket − 1] (gathered)
@@ -357,7 +360,7 @@ struct MHLane {
   // turned back to one per lane through LDS when they are used (land_c1).
   __device__ __forceinline__ void load_c1(uint32_t w) {
     if constexpr (WP == 0) return;
-    if constexpr (CO > 0) {
+    if constexpr (CO) {
       const int wc = (int)(w == oni::kPadWord ? 0u : w);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -396,43 +399,9 @@ struct MHLane {
     asm volatile("" ::: "memory");
   }
 
-  // CO > 1: load I of the cooperative bucket gather (a template so that the shuffles need no loop)
-  template <int I>
-  __device__ __forceinline__ void bucket_load(uint32_t offr) {
-    if constexpr (I < NQ) {
-      const int src = (64 / NQ) * I + lane / NQ;
-      const int h = lane % NQ;
-      const uint32_t o = (uint32_t)__shfl((int)offr, src);
-      const int b2 = __shfl(bk, src);
-      const bool in = b2 * WB + 4 * h < KS;
-      qbin |= in ? 1u << I : 0u;
-      qbv[I] = *reinterpret_cast<const float4*>(in ? a.q + o + 4 * h : a.q);
-    }
-  }
-
-  template <int I>
-  __device__ __forceinline__ void bucket_land() {
-    if constexpr (I < NQ) {
-      const bool in = ((qbin >> I) & 1u) != 0u;
-      float* d = L.qbs + ((64 / NQ) * I + lane / NQ) * kQBS + 4 * (lane % NQ);
-      *reinterpret_cast<float4*>(d) =
-          make_float4(in ? qbv[I].x : 0.f, in ? qbv[I].y : 0.f, in ? qbv[I].z : 0.f, in ? qbv[I].w : 0.f);
-    }
-  }
-  template <int I>
-  __device__ __forceinline__ void bucket_take() {
-    if constexpr (I < NQ) {
-      const float4 v = *reinterpret_cast<const float4*>(L.qbs + lane * kQBS + 4 * I);
-      qb[4 * I] = v.x;
-      qb[4 * I + 1] = v.y;
-      qb[4 * I + 2] = v.z;
-      qb[4 * I + 3] = v.w;
-    }
-  }
-
   // stage B of the token at step s (word w): Philox block, then the state-free gathers
   __device__ __forceinline__ void issue_b(int P, int s, uint32_t w) {
-    if constexpr (CO > 0 && WP > 0) land_c1();
+    if constexpr (CO) land_c1();
     MHB<DM>& x = b[P];
     const uint32_t wc = w == oni::kPadWord ? 0u : w;
     x.r = oni::philox10(oni::U4{pos0 + (uint32_t)s, key, sweep, 2u}, a.seed0, a.seed1);
@@ -455,25 +424,15 @@ struct MHLane {
 #pragma unroll
       for (int i = 0; i < 15; ++i) base = i == bk - 1 ? c1[i] : base;
       // level 2: the bucket's q values (a float4 past the row's KS padding is not read)
-      if constexpr (CB) {
-        // NQ lanes per bucket: load i brings float4 lane % NQ of the bucket of row (64/NQ) i + lane/NQ
-        const uint32_t offr = wc * (uint32_t)KS + (uint32_t)(bk * WB);
-        qbin = 0u;
-        bucket_load<0>(offr);
-        bucket_load<1>(offr);
-        bucket_load<2>(offr);
-        bucket_load<3>(offr);
-      } else {
-        const float* qr = a.q + (int64_t)wc * KS + bk * WB;
+      const float* qr = a.q + (int64_t)wc * KS + bk * WB;
 #pragma unroll
-        for (int j4 = 0; j4 < WB / 4; ++j4) {
-          const bool in = bk * WB + 4 * j4 < KS;
-          const float4 v = *reinterpret_cast<const float4*>(in ? qr + 4 * j4 : a.q);
-          qb[4 * j4] = in ? v.x : 0.f;
-          qb[4 * j4 + 1] = in ? v.y : 0.f;
-          qb[4 * j4 + 2] = in ? v.z : 0.f;
-          qb[4 * j4 + 3] = in ? v.w : 0.f;
-        }
+      for (int j4 = 0; j4 < WB / 4; ++j4) {
+        const bool in = bk * WB + 4 * j4 < KS;
+        const float4 v = *reinterpret_cast<const float4*>(in ? qr + 4 * j4 : a.q);
+        qb[4 * j4] = in ? v.x : 0.f;
+        qb[4 * j4 + 1] = in ? v.y : 0.f;
+        qb[4 * j4 + 2] = in ? v.z : 0.f;
+        qb[4 * j4 + 3] = in ? v.w : 0.f;
       }
     }
     // one-chunk docs read one common address (they use neither value): no scattered lines
@@ -494,20 +453,6 @@ struct MHLane {
   __device__ __forceinline__ void issue_c(int P, int s, uint32_t w) {
     MHB<DM>& x = b[P];
     const uint32_t qo = (w == oni::kPadWord ? 0u : w) * (uint32_t)KS;
-    if constexpr (CB && WP > 0) {
-      // the buckets in flight to LDS, then this lane's own bucket back (cf. land_c1)
-      asm volatile("" ::: "memory");
-      bucket_land<0>();
-      bucket_land<1>();
-      bucket_land<2>();
-      bucket_land<3>();
-      asm volatile("" ::: "memory");
-      bucket_take<0>();
-      bucket_take<1>();
-      bucket_take<2>();
-      bucket_take<3>();
-      asm volatile("" ::: "memory");
-    }
     if constexpr (WP == 0) {
       x.tw = alias_draw(x.r.x, x.rw.x);
     } else {
@@ -731,19 +676,14 @@ __device__ __forceinline__ MHLds mh_lds(unsigned char* smem, int KS) {
   return L;
 }
 
-// OCC > 0: a register budget for OCC waves per SIMD (A/B, ONI_SAMPLER_AB & 16); CO ≥ 1: the level-1
-// CDF rows gathered four lanes per row (ONI_SAMPLER_AB & 32); CO = 2: also the buckets, WB / 4 lanes
-// per bucket (& 64)
-template <int MODE, int DM, int WP, int OCC = 0, int CO = 0>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1, 8)))
-void k_gibbs_mh(const OniMH m) {
+template <int MODE, int DM, int WP, bool R5 = false>
+__global__ __launch_bounds__(64) void k_gibbs_mh(const OniMH m) {
   extern __shared__ __align__(16) unsigned char smem_mh[];
   const OniGibbs& a = m.g;
   const int KS = a.KS;
-  MHLane<MODE, DM, WP, CO> x(m);
+  MHLane<MODE, DM, WP, R5> x(m);
   x.L = mh_lds(smem_mh, KS);
   x.L.c1s = reinterpret_cast<float*>(x.L.zsl + (size_t)m.lmax * 64);
-  x.L.qbs = x.L.c1s;  // used at other times than c1s (issue_c vs issue_b): one staging area
   int32_t* red = reinterpret_cast<int32_t*>(smem_mh + (size_t)KS * (sizeof(float2) + sizeof(float)));
   x.red = red;
   const int lane = threadIdx.x;
@@ -857,9 +797,9 @@ __global__ __launch_bounds__(64) void k_gibbs_mh_init(const OniMH m) {
 
 }  // namespace
 
-static size_t mh_lds_bytes(int KS, int lmax, int co = 0) {
+static size_t mh_lds_bytes(int KS, int lmax, bool co) {
   return (size_t)KS * (sizeof(float2) + sizeof(float) + sizeof(int32_t)) + (size_t)KS * 64 + (size_t)lmax * 64 +
-         (co > 0 ? (size_t)64 * (kC1S > kQBS ? kC1S : kQBS) * sizeof(float) : 0);
+         (co ? (size_t)64 * kC1S * sizeof(float) : 0);
 }
 
 // Per-sweep MH tables. Word proposal: alias records (walias + wsum, k_mh_alias over the V word rows)
@@ -895,9 +835,8 @@ ONI_API int oni_gibbs_mh_launch(const OniMH* m, int init, int mode, hipStream_t 
   if (m->lmax < 1 || m->lmax > 127 || !m->chunk_len) return (int)hipErrorInvalidValue;
   if (a.n_slices < 1) return 0;
   const unsigned grid = (unsigned)a.n_slices;
-  const size_t lds = mh_lds_bytes(a.KS, m->lmax);
   if (init) {
-    k_gibbs_mh_init<<<grid, 64, lds, s>>>(*m);
+    k_gibbs_mh_init<<<grid, 64, mh_lds_bytes(a.KS, m->lmax, false), s>>>(*m);
     return (int)hipGetLastError();
   }
   if (!a.qfix || !m->mh_g || !m->chunk_dslot) return (int)hipErrorInvalidValue;
@@ -907,28 +846,11 @@ ONI_API int oni_gibbs_mh_launch(const OniMH* m, int init, int mode, hipStream_t 
   if (mode == 2 && !a.chg_mask) return (int)hipErrorInvalidValue;
   if (mode == 3 && (!a.wpos || !a.z_w)) return (int)hipErrorInvalidValue;
   if (mode == 4 && (!a.wpos || !a.zz_w || !a.chg_mask)) return (int)hipErrorInvalidValue;
-  // A/B variants of the default configuration (two doc moves, CDF word proposal, recount / wdelta)
-  if ((a.flags & (256 | 512 | 1024 | 2048)) && m->doc_moves == 2 && m->wp == 8 && (mode == 0 || mode == 4)) {
-    int co = (a.flags & 1024) ? 2 : (a.flags & 512) ? 1 : 0;
-    if (a.flags & 2048) co = co == 2 ? 3 : 4;
-    const bool occ = (a.flags & 256) != 0;
-    const size_t lco = mh_lds_bytes(a.KS, m->lmax, co);
-#define ONI_MH_AB(md)                                                                          \
-  do {                                                                                         \
-    if (occ) {                                                                                 \
-      if (co == 2) k_gibbs_mh<md, 2, 8, 4, 2><<<grid, 64, lco, s>>>(*m);                       \
-      else if (co == 1) k_gibbs_mh<md, 2, 8, 4, 1><<<grid, 64, lco, s>>>(*m);                  \
-      else k_gibbs_mh<md, 2, 8, 4, 0><<<grid, 64, lco, s>>>(*m);                               \
-    } else {                                                                                   \
-      if (co == 4) k_gibbs_mh<md, 2, 8, 0, 4><<<grid, 64, lco, s>>>(*m);                       \
-      else if (co == 3) k_gibbs_mh<md, 2, 8, 0, 3><<<grid, 64, lco, s>>>(*m);                  \
-      else if (co == 2) k_gibbs_mh<md, 2, 8, 0, 2><<<grid, 64, lco, s>>>(*m);                  \
-      else k_gibbs_mh<md, 2, 8, 0, 1><<<grid, 64, lco, s>>>(*m);                               \
-    }                                                                                          \
-  } while (0)
-    if (mode == 0) ONI_MH_AB(0);
-    else ONI_MH_AB(4);
-#undef ONI_MH_AB
+  const bool r5 = (a.flags & 512) != 0;  // A/B: round 5's level-1 row gathers
+  const size_t lds = mh_lds_bytes(a.KS, m->lmax, m->wp > 0 && !r5);
+  if (r5 && m->doc_moves == 2 && m->wp == 8 && (mode == 0 || mode == 4)) {
+    if (mode == 0) k_gibbs_mh<0, 2, 8, true><<<grid, 64, lds, s>>>(*m);
+    else k_gibbs_mh<4, 2, 8, true><<<grid, 64, lds, s>>>(*m);
     return (int)hipGetLastError();
   }
 #define ONI_MH(md, dm)                                                  \

@@ -470,13 +470,11 @@ def gibbs_pass(st: dict, G: int, KP: int, K: int, alpha: float, seed: int, init:
     ab = int(os.environ.get("ONI_SAMPLER_AB", "0"))
     # bit 2 of ONI_SAMPLER_AB (flags bit 5): k_gibbs_x1's q' by v_pk_fma_f32 on topic pairs (A/B: loses);
     # bit 3 (flags bit 7): its ±1 count update by per-topic bfe + cvt instead of the LDS table (A/B);
-    # bit 4 (flags bit 8): k_gibbs_mh under a 4-wave register budget (A/B); bit 5 (flags bit 9): its
-    # level-1 word CDF rows gathered four lanes per row (A/B); bit 6 (flags bit 10): also the buckets;
-    # bit 7 (flags bit 11): words four tokens ahead, level-1 rows a step before their use
+    # bit 5 (flags bit 9): k_gibbs_mh's round-5 level-1 word CDF gathers (one lane per row, words two
+    # tokens ahead) instead of four lanes per row a step ahead (A/B)
     a.flags = ((1 if alpha_in_row else 0) | (ab & 3) << 1 | (8 if (init and word_init) else 0)
                | (16 if pos_aligned else 0) | (32 if ab & 4 else 0) | (128 if ab & 8 else 0)
-               | (256 if ab & 16 else 0) | (512 if ab & 32 else 0) | (1024 if ab & 64 else 0)
-               | (2048 if ab & 128 else 0))
+               | (512 if ab & 32 else 0))
     if sampler == SAMPLER_MH:
         if G != 1:
             raise ValueError("the MH sampler runs one-lane units")
