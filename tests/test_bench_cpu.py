@@ -119,3 +119,20 @@ def test_sizing_counts_mh_burn_in_and_posterior_sums():
     assert 0.75 * 154e9 < p.peak_bytes < 1.25 * 154e9, p.as_dict()
     nb = sizing.plan("flow", 500_000_000, 100, 20_000_000, 7008, mh_burn=0)
     assert nb.peak_bytes < p.peak_bytes
+
+
+def test_day_ab_alternates_variants_on_one_day(tmp_path):
+    """bench/day_ab.py (the in-process whole-day A/B): every variant runs every round on the same
+    generated day; an env-only variant draws the same chain as the base (same log-likelihood)."""
+    out = tmp_path / "ab.json"
+    cmd = [sys.executable, "bench/day_ab.py", "--device", "cpu", "--flows", "3000", "--topics", "20",
+           "--sweeps", "6", "--rounds", "2", "--variant", "base:", "--variant", "ab:ONI_SAMPLER_AB=32",
+           "--variant", "L64:chunk=64", "--out", str(out)]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(out.read_text())
+    assert set(d["summary"]) == {"base", "ab", "L64"} and all(len(v) == 2 for v in d["days"].values())
+    assert d["variants"]["L64"]["chunk"] == 64 and d["variants"]["ab"]["env"] == {"ONI_SAMPLER_AB": "32"}
+    ll = {n: {x["loglik"] for x in v} for n, v in d["days"].items()}
+    assert ll["base"] == ll["ab"] and len(ll["base"]) == 1  # CPU oracle: the A/B bits change no draw
