@@ -97,6 +97,14 @@ def test_mh_sweep_bitwise_vs_oracle(gpu, K, mode, dm, L, word, monkeypatch):
     assert int(mg.nwk.min()) >= 0 and int(mg.ndk_cur.min()) >= 0
 
 
+@pytest.mark.parametrize("mode", ["recount", "wdelta"])
+def test_mh_round5_gathers_match_the_oracle(gpu, mode, monkeypatch):
+    """ONI_SAMPLER_AB=32 (k_gibbs_mh's round-5 level-1 CDF gathers, kept for A/B) draws the same
+    chain as the oracle, like the default cooperative gathers."""
+    monkeypatch.setenv("ONI_SAMPLER_AB", "32")
+    test_mh_sweep_bitwise_vs_oracle(gpu, 100, mode, 2, 64, "cdf", monkeypatch)
+
+
 def test_mh_graph_auto_matches_eager(gpu):
     """Graph-captured sweeps (the auto count mode's recount → wdelta switch) equal eager ones."""
     tdoc, tword, keys = _toy(2000, 700, 3)
