@@ -294,9 +294,9 @@ struct MHB {
 template <int MODE, int DM, int WP, bool R5 = false>
 struct MHLane {
   // CDF word proposal: level-1 rows gathered four lanes per row (CO) and issued a whole step before
-  // their use, from words read four tokens ahead (WD)
+  // their use; words read four tokens ahead (WD; with the alias records they only feed stage B)
   static constexpr bool CO = !R5 && WP > 0;
-  static constexpr bool WD = CO;
+  static constexpr bool WD = !R5;
   static constexpr int WB = WP > 0 ? WP : 1;
   const OniMH& m;
   const OniGibbs& a;
@@ -848,9 +848,14 @@ ONI_API int oni_gibbs_mh_launch(const OniMH* m, int init, int mode, hipStream_t 
   if (mode == 4 && (!a.wpos || !a.zz_w || !a.chg_mask)) return (int)hipErrorInvalidValue;
   const bool r5 = (a.flags & 512) != 0;  // A/B: round 5's level-1 row gathers
   const size_t lds = mh_lds_bytes(a.KS, m->lmax, m->wp > 0 && !r5);
-  if (r5 && m->doc_moves == 2 && m->wp == 8 && (mode == 0 || mode == 4)) {
-    if (mode == 0) k_gibbs_mh<0, 2, 8, true><<<grid, 64, lds, s>>>(*m);
-    else k_gibbs_mh<4, 2, 8, true><<<grid, 64, lds, s>>>(*m);
+  if (r5 && m->doc_moves == 2 && (m->wp == 8 || m->wp == 0) && (mode == 0 || mode == 4)) {
+    if (m->wp == 8) {
+      if (mode == 0) k_gibbs_mh<0, 2, 8, true><<<grid, 64, lds, s>>>(*m);
+      else k_gibbs_mh<4, 2, 8, true><<<grid, 64, lds, s>>>(*m);
+    } else {
+      if (mode == 0) k_gibbs_mh<0, 2, 0, true><<<grid, 64, lds, s>>>(*m);
+      else k_gibbs_mh<4, 2, 0, true><<<grid, 64, lds, s>>>(*m);
+    }
     return (int)hipGetLastError();
   }
 #define ONI_MH(md, dm)                                                  \
