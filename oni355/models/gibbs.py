@@ -318,6 +318,7 @@ class GibbsLDA:
         self.likelihoods: list[tuple[int, float]] = []
         self._graph = None
         self._graphs: dict = {}
+        self._eager_lead_done = False  # the eager pair that hides a model's first capture (_sweep_n)
         self._watchdog = fault.Watchdog.from_env()
         self.timings = {"allreduce_calls": 0}
         self._ar_events: list = []
@@ -1098,6 +1099,17 @@ class GibbsLDA:
                 self._one_sweep()  # realign parities with the captured pair
                 self._note_changes()
                 done += 1
+                continue
+            if entry is None and not self._graphs and not self._eager_lead_done and n - done >= 4 \
+                    and os.environ.get("ONI_GRAPH_EAGER_LEAD", "1") == "1":
+                # the first capture of a model costs ~0.26 ms of host time with nothing queued: run
+                # this pair eagerly first, so that the device works through it while the host
+                # captures (eager and replayed sweeps draw the same chain)
+                self._eager_lead_done = True
+                for _ in range(2):
+                    self._one_sweep()
+                    self._note_changes()
+                done += 2
                 continue
             if entry is None:
                 # capture the delta pair now too: no capture stall at the switch
